@@ -1,0 +1,213 @@
+"""Headline benchmark: Mpps, device-resident, 64 B IPv4 cksum + classify.
+
+Workload (BASELINE.json configs[1], C2): 1,048,576 packets of 60-B UDP/IPv4
+frames (64 B on the wire) in 64-B slots, one 5-tuple, resident in HBM. One
+step = one pass of the hot path over one batch:
+
+    CheckIPHeader(OFFSET 14, CHECKSUM true) -> AggregateHash (IPFlowID low 32)
+    -> FlowSwitch LB_MODE hash over 16 outputs -> stable per-port partition
+
+i.e. k_rx + k_scan + k_part of libfcgpu.so. Steps rotate over --nbuf distinct
+batches placed in different HBM regions (default 16 x 72 MB = 1.15 GB > the
+256 MB Infinity Cache), so every step reads its packets from HBM.
+
+Multi-GPU (torchrun, one process per GPU): each rank processes its own batch
+per step (weak scaling, no data-path collective); the per-port / per-reason
+counters are summed across ranks with one all-reduce over RCCL at the end of
+the timed region (the reference sums per-thread counters on read).
+
+rank 0 prints ONE JSON line (contract in the task statement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+PKT_BYTES_READ = 72          # 64-B header window + 8-B descriptor
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--packets", type=int, default=1 << 20)
+    ap.add_argument("--nbuf", type=int, default=16)
+    ap.add_argument("--nports", type=int, default=16)
+    ap.add_argument("--no-perm", action="store_true", help="skip the partition scatter")
+    ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds: float):
+    """Reported CPU baseline: the scalar restatement of the reference elements
+    (oracle/cpu_baseline.cc: 32-packet linked-list PacketBatch, CheckIPHeader ->
+    AggregateHash -> FlowSwitch hash -> CLASSIFY_EACH_PACKET, atomic counters),
+    one pipeline per core, on this host."""
+    exe = os.path.join(ROOT, "oracle", "_build", "fc_cpu_baseline")
+    if not os.path.exists(exe):
+        try:
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "baseline"])
+        except Exception:
+            return None
+    cores = len(os.sched_getaffinity(0))
+    cores = max(1, min(cores, 16))
+    try:
+        out = subprocess.run([exe, "--seconds", str(seconds), "--threads", str(cores)],
+                             capture_output=True, text=True, timeout=seconds * 4 + 60)
+        res = json.loads(out.stdout.strip().splitlines()[-1])
+    except Exception as e:  # reported baseline only
+        print(f"cpu baseline failed: {e}", file=sys.stderr)
+        return None
+    return dict(value=round(res["mpps"], 3), unit="Mpps", cores=res["threads"], kind="port",
+                sample=res["sample"], mpps_1core=round(res.get("mpps_1core", 0.0), 3))
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from fastclick_amd import synth, _native as N
+    from fastclick_amd.device import DeviceBatch, DeviceOutputs
+
+    n = args.packets
+    host = synth.c2(n)
+    # nbuf distinct copies at distinct HBM addresses
+    bufs = []
+    for k in range(args.nbuf):
+        bufs.append(DeviceBatch.upload(host, device=dev))
+    del host
+    cfg = N.make_cfg(offset=14, checksum=True, hash_mode=N.HASH_FLOWID, classify=N.CLS_LB_HASH,
+                     nports=args.nports)
+    ctx = N.Context(local, n, cfg)
+    outs = DeviceOutputs(n, args.nports, device=dev, verdict=True, hash=True, anno=False,
+                         perm=not args.no_perm, port_start=not args.no_perm)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    optr = outs.ptrs()
+
+    def step(k):
+        b = bufs[k % len(bufs)]
+        ctx.process(b.arena.data_ptr(), b.desc.data_ptr(), n, stream=sptr, **optr)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    # counters accumulate straight into a torch tensor so RCCL can reduce them
+    ctr_t = torch.zeros(N.NCOUNTERS, dtype=torch.int64, device=dev)
+    ctx.use_counters(ctr_t.data_ptr())
+    if not args.no_timing:
+        ctx.set_timing(True)
+        ctx.read_timing()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    if world > 1:
+        # per-port / per-reason counters summed across GPUs: one RCCL all-reduce
+        # of the device counter vector (xGMI), like PER_THREAD_SUM on read
+        glob = ctr_t.clone()
+        dist.all_reduce(glob)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        total_valid = int(glob[N.CTR_COUNT].item())
+    else:
+        total_valid = int(ctr_t[N.CTR_COUNT].item())
+
+    timing = None
+    if not args.no_timing:
+        ms, cnt = ctx.read_timing()
+        timing = dict(k_rx_ms=ms[0] / max(cnt[0], 1), k_scan_ms=ms[1] / max(cnt[1], 1),
+                      k_part_ms=ms[2] / max(cnt[2], 1), launches=cnt)
+
+    total_pkts = n * args.steps * world
+    assert total_valid == total_pkts, f"valid count {total_valid} != {total_pkts}"
+    mpps = total_pkts / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+
+    if rank == 0:
+        roof = None
+        if timing:
+            t_launch = timing["k_rx_ms"] * 1e-3
+            achieved = PKT_BYTES_READ * n / t_launch / 1e9
+            traffic = None
+            try:
+                with open(args.traffic_json) as f:
+                    tj = json.load(f)
+                if tj.get("packets") == n:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                pass
+            roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                        kernel="k_rx", kernel_ms=round(timing["k_rx_ms"], 5),
+                        scan_ms=round(timing["k_scan_ms"], 5), part_ms=round(timing["k_part_ms"], 5))
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(args.cpu_seconds)
+        line = {
+            "metric": "Mpps device-resident, 64 B IPv4 cksum+classify, 1/2/4/8 MI355X",
+            "value": round(mpps, 1),
+            "unit": "Mpps",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": ("C2: 64 B IPv4/UDP (60-B frames in 64-B slots), 1M-packet "
+                             "device-resident batch, single 5-tuple; CheckIPHeader(CHECKSUM true)"
+                             " + AggregateHash + FlowSwitch hash 16 outputs"
+                             + ("" if args.no_perm else " + stable per-port partition")),
+                "packets_per_step_per_gpu": n,
+                "hbm_batches": args.nbuf,
+                "nports": args.nports,
+                "parallelism": f"batch-sharded x{world}, counters all-reduced (RCCL)",
+            },
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

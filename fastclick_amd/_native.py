@@ -1,0 +1,270 @@
+"""ctypes binding of the C ABI in include/fastclick_gpu.h (libfcgpu.so).
+
+The shared library is built in-tree by ``fastclick_amd.build`` (hipcc, gfx950)
+into ``fastclick_amd/lib/``. Loading fails loudly when it is missing: there is
+no CPU fallback for the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIBFCGPU = os.path.join(LIB_DIR, "libfcgpu.so")
+LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
+
+# ---- constants mirrored from include/fastclick_gpu.h -----------------------
+ABI_VERSION = 1
+OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
+R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
+    R_BAD_IP6, R_VLAN_REJECT = range(9)
+NREASON_SLOTS = 8
+CHECK_IP4, MARK_IP4, CHECK_AUTO = 0, 1, 2
+HASH_NONE, HASH_FLOWID, HASH_FLOW5ID = 0, 1, 2
+CLS_NONE, CLS_LB_HASH, CLS_HASH_IP, CLS_HASHSWITCH = 0, 1, 2, 3
+MAX_PORTS = 64
+MAX_ADDRS = 16
+CTR_COUNT, CTR_DROPS, CTR_REASON, CTR_PORT = 0, 1, 2, 10
+NCOUNTERS = CTR_PORT + MAX_PORTS + 1
+
+REASON_TEXTS = ["tiny packet", "bad IPv4 version", "bad IPv4 header length",
+                "bad IPv4 length", "bad IPv4 checksum", "bad source address"]
+
+
+class fcgpu_cfg(C.Structure):
+    _fields_ = [
+        ("size", C.c_uint32),
+        ("check_mode", C.c_uint32),
+        ("offset", C.c_int32),
+        ("checksum", C.c_uint32),
+        ("hash_mode", C.c_uint32),
+        ("classify", C.c_uint32),
+        ("nports", C.c_uint32),
+        ("hs_offset", C.c_int32),
+        ("hs_length", C.c_int32),
+        ("native_vlan", C.c_int32),
+        ("nbadsrc", C.c_uint32),
+        ("ngooddst", C.c_uint32),
+        ("badsrc", C.c_uint32 * MAX_ADDRS),
+        ("gooddst", C.c_uint32 * MAX_ADDRS),
+        ("nbad6", C.c_uint32),
+        ("bad6", (C.c_uint8 * 16) * MAX_ADDRS),
+    ]
+
+
+class fcgpu_anno(C.Structure):
+    _fields_ = [
+        ("dst_ip", C.c_uint32),
+        ("length", C.c_uint16),
+        ("nh", C.c_uint8),
+        ("th", C.c_uint8),
+        ("vlan_tci", C.c_uint16),
+        ("ip6_nxt", C.c_uint8),
+        ("ipver", C.c_uint8),
+        ("reserved", C.c_uint32),
+    ]
+
+
+ANNO_DTYPE = None   # numpy structured dtype, set lazily (numpy import is optional here)
+
+
+def anno_dtype():
+    global ANNO_DTYPE
+    if ANNO_DTYPE is None:
+        import numpy as np
+        ANNO_DTYPE = np.dtype([("dst_ip", "<u4"), ("length", "<u2"), ("nh", "u1"), ("th", "u1"),
+                               ("vlan_tci", "<u2"), ("ip6_nxt", "u1"), ("ipver", "u1"),
+                               ("reserved", "<u4")])
+        assert ANNO_DTYPE.itemsize == C.sizeof(fcgpu_anno) == 16
+    return ANNO_DTYPE
+
+
+class fcgpu_out(C.Structure):
+    _fields_ = [
+        ("verdict", C.c_void_p),
+        ("hash", C.c_void_p),
+        ("anno", C.c_void_p),
+        ("perm", C.c_void_p),
+        ("port_start", C.c_void_p),
+    ]
+
+
+# Every symbol include/fastclick_gpu.h declares (checked by tests/test_abi.py).
+FCGPU_SYMBOLS = {
+    "fcgpu_abi_version": (C.c_int, []),
+    "fcgpu_device_count": (C.c_int, []),
+    "fcgpu_default_cfg": (None, [C.POINTER(fcgpu_cfg)]),
+    "fcgpu_open": (C.c_int, [C.c_int, C.c_uint32, C.POINTER(C.c_void_p)]),
+    "fcgpu_configure": (C.c_int, [C.c_void_p, C.POINTER(fcgpu_cfg)]),
+    "fcgpu_close": (None, [C.c_void_p]),
+    "fcgpu_process": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                C.POINTER(fcgpu_out), C.c_void_p]),
+    "fcgpu_process_host": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_void_p, C.c_uint32,
+                                     C.POINTER(fcgpu_out)]),
+    "fcgpu_read_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
+    "fcgpu_reset_counters": (C.c_int, [C.c_void_p]),
+    "fcgpu_counters_device": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
+    "fcgpu_use_counters": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "fcgpu_set_timing": (C.c_int, [C.c_void_p, C.c_int]),
+    "fcgpu_read_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint32),
+                                    C.c_int]),
+    "fcgpu_last_error": (C.c_char_p, [C.c_void_p]),
+}
+
+_lib = None
+
+
+class NativeMissing(RuntimeError):
+    pass
+
+
+def load(path: str = LIBFCGPU):
+    """Load libfcgpu.so (after torch, so one HIP runtime serves both)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise NativeMissing(
+            f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    try:
+        import torch  # noqa: F401  (share torch's HIP runtime: same soname)
+    except Exception:
+        pass
+    lib = C.CDLL(path)
+    for name, (res, args) in FCGPU_SYMBOLS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.fcgpu_abi_version() != ABI_VERSION:
+        raise NativeMissing("libfcgpu.so ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def default_cfg() -> fcgpu_cfg:
+    cfg = fcgpu_cfg()
+    lib = _lib
+    if lib is not None:
+        lib.fcgpu_default_cfg(C.byref(cfg))
+    else:
+        # same values as fcgpu_default_cfg (fcgpu_api.hip)
+        cfg.size = C.sizeof(fcgpu_cfg)
+        cfg.check_mode = CHECK_IP4
+        cfg.hash_mode = HASH_FLOWID
+        cfg.classify = CLS_NONE
+        cfg.nports = 1
+        cfg.hs_length = 1
+        cfg.nbad6 = 1
+        for j in range(16):
+            cfg.bad6[0][j] = 0xFF
+    return cfg
+
+
+def make_cfg(*, check_mode=CHECK_IP4, offset=0, checksum=False, hash_mode=HASH_FLOWID,
+             classify=CLS_NONE, nports=1, hs_offset=0, hs_length=1, native_vlan=0,
+             badsrc=(), gooddst=(), bad6=None) -> fcgpu_cfg:
+    """Build an fcgpu_cfg. Addresses are raw network-order words (bytes a.b.c.d
+    -> little-endian u32 of those bytes), as IPAddress stores them."""
+    cfg = default_cfg()
+    cfg.check_mode = check_mode
+    cfg.offset = offset
+    cfg.checksum = 1 if checksum else 0
+    cfg.hash_mode = hash_mode
+    cfg.classify = classify
+    cfg.nports = nports
+    cfg.hs_offset = hs_offset
+    cfg.hs_length = hs_length
+    cfg.native_vlan = native_vlan
+    cfg.nbadsrc = len(badsrc)
+    for j, a in enumerate(badsrc):
+        cfg.badsrc[j] = a
+    cfg.ngooddst = len(gooddst)
+    for j, a in enumerate(gooddst):
+        cfg.gooddst[j] = a
+    if bad6 is not None:
+        cfg.nbad6 = len(bad6)
+        for j, a in enumerate(bad6):
+            for k in range(16):
+                cfg.bad6[j][k] = a[k]
+    return cfg
+
+
+def raw_addr(dotted: str) -> int:
+    """'a.b.c.d' -> raw s_addr word as read little-endian from packet bytes."""
+    b = bytes(int(x) for x in dotted.split("."))
+    return int.from_bytes(b, "little")
+
+
+class Context:
+    """Owning wrapper over an fcgpu_ctx (one per thread x stream)."""
+
+    def __init__(self, device: int = 0, max_batch: int = 1 << 20, cfg: fcgpu_cfg | None = None):
+        self.lib = load()
+        h = C.c_void_p()
+        rc = self.lib.fcgpu_open(device, max_batch, C.byref(h))
+        if rc != OK:
+            raise RuntimeError(f"fcgpu_open failed ({rc}): {self.lib.fcgpu_last_error(None).decode()}")
+        self.h = h
+        self.max_batch = max_batch
+        self.cfg = None
+        if cfg is not None:
+            self.configure(cfg)
+
+    def _chk(self, rc, what):
+        if rc != OK:
+            raise RuntimeError(f"{what} failed ({rc}): {self.lib.fcgpu_last_error(self.h).decode()}")
+
+    def configure(self, cfg: fcgpu_cfg):
+        self._chk(self.lib.fcgpu_configure(self.h, C.byref(cfg)), "fcgpu_configure")
+        self.cfg = cfg
+
+    def process(self, arena_ptr, desc_ptr, n, *, verdict=0, hash=0, anno=0, perm=0,
+                port_start=0, stream=0):
+        out = fcgpu_out(verdict or None, hash or None, anno or None, perm or None,
+                        port_start or None)
+        self._chk(self.lib.fcgpu_process(self.h, arena_ptr, desc_ptr, n, C.byref(out),
+                                         stream or None), "fcgpu_process")
+
+    def process_host(self, frames, lens_ptr, n, *, verdict=0, hash=0, anno=0, perm=0,
+                     port_start=0):
+        out = fcgpu_out(verdict or None, hash or None, anno or None, perm or None,
+                        port_start or None)
+        self._chk(self.lib.fcgpu_process_host(self.h, frames, lens_ptr, n, C.byref(out)),
+                  "fcgpu_process_host")
+
+    def counters(self, n=NCOUNTERS):
+        buf = (C.c_uint64 * n)()
+        self._chk(self.lib.fcgpu_read_counters(self.h, buf, n), "fcgpu_read_counters")
+        return list(buf)
+
+    def reset_counters(self):
+        self._chk(self.lib.fcgpu_reset_counters(self.h), "fcgpu_reset_counters")
+
+    def counters_device_ptr(self) -> int:
+        p = C.c_void_p()
+        self._chk(self.lib.fcgpu_counters_device(self.h, C.byref(p)), "fcgpu_counters_device")
+        return p.value
+
+    def use_counters(self, dptr: int):
+        self._chk(self.lib.fcgpu_use_counters(self.h, dptr or None), "fcgpu_use_counters")
+
+    def set_timing(self, on: bool):
+        self._chk(self.lib.fcgpu_set_timing(self.h, 1 if on else 0), "fcgpu_set_timing")
+
+    def read_timing(self):
+        ms = (C.c_double * 3)()
+        cnt = (C.c_uint32 * 3)()
+        self._chk(self.lib.fcgpu_read_timing(self.h, ms, cnt, 3), "fcgpu_read_timing")
+        return list(ms), list(cnt)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.fcgpu_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

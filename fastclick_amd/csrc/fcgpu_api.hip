@@ -1,0 +1,393 @@
+// fcgpu_api.hip -- C ABI (include/fastclick_gpu.h) over the gfx950 kernels.
+//
+// A context owns: the uploaded configuration, the partition workspace (per-tile
+// histograms + bin totals), the device counter vector, pinned/device staging
+// for host-resident batches, and optional per-stage timing events. Launch
+// sequence per batch (all on one stream):
+//   k_rx   fused check/hash/classify + per-tile histograms   (grid = tiles)
+//   k_scan per-bin exclusive scan over tiles + counters       (grid = bins)
+//   k_part stable partition scatter, only if perm requested   (grid = tiles)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdio.h>
+#include <string>
+#include <vector>
+
+#include "fcgpu_device.hh"
+
+#pragma clang diagnostic ignored "-Wunused-result"
+#pragma clang diagnostic ignored "-Wunused-value"
+
+using namespace fcgpu;
+
+namespace {
+constexpr uint32_t kHostCap = 128;          // bytes gathered per frame in host mode
+constexpr uint32_t kArenaPad = 256;
+
+struct EvPair {
+    hipEvent_t a, b;
+    int stage;
+};
+}  // namespace
+
+struct fcgpu_ctx {
+    int device = -1;
+    uint32_t max_batch = 0;
+    uint32_t max_tiles = 0;
+    hipStream_t stream = nullptr;
+    fcgpu_cfg cfg{};
+    DevCfg dcfg{};
+    bool configured = false;
+    uint32_t *d_tilecnt = nullptr;
+    uint32_t *d_totals = nullptr;
+    unsigned long long *d_ctr = nullptr;      // active counter vector
+    unsigned long long *d_ctr_own = nullptr;  // context-owned vector
+    uint16_t *d_verdict = nullptr;   // scratch verdicts when the caller wants perm only
+    // host-resident staging
+    uint8_t *h_arena = nullptr, *d_arena = nullptr;
+    uint32_t *h_desc = nullptr, *d_desc = nullptr;
+    uint16_t *d_hv = nullptr;
+    uint32_t *d_hh = nullptr, *d_hperm = nullptr, *d_hstart = nullptr;
+    fcgpu_anno *d_hanno = nullptr;
+    // timing
+    bool timing = false;
+    std::vector<EvPair> pending;
+    std::vector<hipEvent_t> free_ev;
+    std::string err;
+};
+
+static std::string g_open_err;
+
+static int fail(fcgpu_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    else g_open_err = msg;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                   \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail((ctx), FCGPU_ERUNTIME,                                              \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                 \
+    } while (0)
+
+static hipEvent_t take_event(fcgpu_ctx *c) {
+    if (!c->free_ev.empty()) {
+        hipEvent_t e = c->free_ev.back();
+        c->free_ev.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+template <int CM, bool CK>
+static void launch_rx(const RxArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL((k_rx<CM, CK>), dim3(a.ntiles), dim3(kTile), 0, s, a);
+}
+
+static void launch_rx_any(uint32_t cm, bool ck, const RxArgs &a, hipStream_t s) {
+    switch (cm * 2 + (ck ? 1 : 0)) {
+    case 0: launch_rx<FCGPU_CHECK_IP4, false>(a, s); break;
+    case 1: launch_rx<FCGPU_CHECK_IP4, true>(a, s); break;
+    case 2: case 3: launch_rx<FCGPU_MARK_IP4, false>(a, s); break;
+    case 4: launch_rx<FCGPU_CHECK_AUTO, false>(a, s); break;
+    default: launch_rx<FCGPU_CHECK_AUTO, true>(a, s); break;
+    }
+}
+
+extern "C" {
+
+int fcgpu_abi_version(void) { return FCGPU_ABI_VERSION; }
+
+int fcgpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void fcgpu_default_cfg(fcgpu_cfg *c) {
+    memset(c, 0, sizeof(*c));
+    c->size = sizeof(fcgpu_cfg);
+    c->check_mode = FCGPU_CHECK_IP4;
+    c->offset = 0;
+    c->checksum = 0;                   // CheckIPHeader::configure read_or_set(..., 0)
+    c->hash_mode = FCGPU_HASH_FLOWID;
+    c->classify = FCGPU_CLS_NONE;
+    c->nports = 1;
+    c->hs_length = 1;
+    c->native_vlan = 0;                // StripEtherVLANHeader default NATIVE_VLAN 0
+    c->nbad6 = 1;                      // CheckIP6Header default bad source ff..ff
+    memset(c->bad6[0], 0xff, 16);
+}
+
+const char *fcgpu_last_error(fcgpu_ctx *ctx) { return ctx ? ctx->err.c_str() : g_open_err.c_str(); }
+
+void fcgpu_close(fcgpu_ctx *c) {
+    if (!c) return;
+    if (c->device >= 0) {
+        hipSetDevice(c->device);
+        if (c->stream) hipStreamSynchronize(c->stream);
+        for (auto &p : c->pending) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
+        for (auto e : c->free_ev) hipEventDestroy(e);
+        hipFree(c->d_tilecnt);
+        hipFree(c->d_totals);
+        hipFree(c->d_ctr_own);
+        hipFree(c->d_verdict);
+        hipFree(c->d_arena);
+        hipFree(c->d_desc);
+        hipFree(c->d_hv);
+        hipFree(c->d_hh);
+        hipFree(c->d_hperm);
+        hipFree(c->d_hstart);
+        hipFree(c->d_hanno);
+        hipHostFree(c->h_arena);
+        hipHostFree(c->h_desc);
+        if (c->stream) hipStreamDestroy(c->stream);
+    }
+    delete c;
+}
+
+int fcgpu_open(int device, uint32_t max_batch, fcgpu_ctx **out) {
+    if (!out || max_batch == 0) return fail(nullptr, FCGPU_EINVAL, "fcgpu_open: bad arguments");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(nullptr, FCGPU_ENODEV, "fcgpu_open: no HIP device");
+    if (device < 0 || device >= ndev) return fail(nullptr, FCGPU_ENODEV, "fcgpu_open: bad device index");
+    fcgpu_ctx *c = new fcgpu_ctx();
+    c->device = device;
+    c->max_batch = max_batch;
+    c->max_tiles = (max_batch + kTile - 1) / kTile;
+    int rc = FCGPU_OK;
+    auto chk = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && rc == FCGPU_OK) rc = fail(c, FCGPU_ENOMEM, std::string(what) + ": " + hipGetErrorString(e));
+    };
+    chk(hipSetDevice(device), "hipSetDevice");
+    chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+    chk(hipMalloc(&c->d_tilecnt, sizeof(uint32_t) * (size_t)kMaxBins * c->max_tiles), "hipMalloc tilecnt");
+    chk(hipMalloc(&c->d_totals, sizeof(uint32_t) * kMaxBins), "hipMalloc totals");
+    chk(hipMalloc(&c->d_ctr_own, sizeof(unsigned long long) * FCGPU_NCOUNTERS), "hipMalloc counters");
+    c->d_ctr = c->d_ctr_own;
+    if (rc == FCGPU_OK) chk(hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * FCGPU_NCOUNTERS), "hipMemset");
+    if (rc != FCGPU_OK) {
+        g_open_err = c->err;
+        fcgpu_close(c);
+        return rc;
+    }
+    fcgpu_cfg def;
+    fcgpu_default_cfg(&def);
+    fcgpu_configure(c, &def);
+    *out = c;
+    return FCGPU_OK;
+}
+
+int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
+    if (!c || !cfg) return FCGPU_EINVAL;
+    if (cfg->size != sizeof(fcgpu_cfg)) return fail(c, FCGPU_EINVAL, "fcgpu_cfg size mismatch (ABI)");
+    if (cfg->check_mode > FCGPU_CHECK_AUTO) return fail(c, FCGPU_EINVAL, "bad check_mode");
+    if (cfg->hash_mode > FCGPU_HASH_FLOW5ID) return fail(c, FCGPU_EINVAL, "bad hash_mode");
+    if (cfg->classify > FCGPU_CLS_HASHSWITCH) return fail(c, FCGPU_EINVAL, "bad classify mode");
+    if (cfg->nports < 1 || cfg->nports > FCGPU_MAX_PORTS) return fail(c, FCGPU_EINVAL, "nports out of range");
+    if (cfg->offset < 0 || cfg->offset > 255) return fail(c, FCGPU_EINVAL, "OFFSET out of range [0,255]");
+    if (cfg->nbadsrc > FCGPU_MAX_ADDRS || cfg->ngooddst > FCGPU_MAX_ADDRS || cfg->nbad6 > FCGPU_MAX_ADDRS)
+        return fail(c, FCGPU_EINVAL, "too many addresses");
+    if (cfg->classify == FCGPU_CLS_HASHSWITCH && (cfg->hs_length <= 0 || cfg->hs_offset < 0))
+        return fail(c, FCGPU_EINVAL, "length must be > 0");   // hashswitch.cc:40-41
+    if (cfg->native_vlan > 0xFFF) return fail(c, FCGPU_EINVAL, "bad NATIVE_VLAN");
+    c->cfg = *cfg;
+    DevCfg &d = c->dcfg;
+    memset(&d, 0, sizeof(d));
+    d.offset = cfg->offset;
+    d.nports = cfg->nports;
+    d.hash_mode = cfg->hash_mode;
+    d.classify = cfg->classify;
+    d.hs_offset = cfg->hs_offset;
+    d.hs_length = cfg->hs_length;
+    d.native_vlan = cfg->native_vlan;
+    d.nbadsrc = cfg->nbadsrc;
+    d.ngooddst = cfg->ngooddst;
+    d.nbad6 = cfg->nbad6;
+    memcpy(d.badsrc, cfg->badsrc, sizeof(d.badsrc));
+    memcpy(d.gooddst, cfg->gooddst, sizeof(d.gooddst));
+    memcpy(d.bad6, cfg->bad6, sizeof(d.bad6));
+    c->configured = true;
+    return FCGPU_OK;
+}
+
+int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, uint32_t n,
+                  const fcgpu_out *o, void *stream) {
+    if (!c || !o) return FCGPU_EINVAL;
+    if (!c->configured) return fail(c, FCGPU_EINVAL, "not configured");
+    if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "batch larger than max_batch");
+    if (n == 0) return FCGPU_OK;
+    if (!d_arena || !d_desc) return fail(c, FCGPU_EINVAL, "null arena/desc");
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint32_t ntiles = (n + kTile - 1) / kTile;
+    const uint32_t nports = c->cfg.nports;
+    const uint32_t nbt = nports + 1 + FCGPU_NREASON_SLOTS;
+    uint16_t *verdict = o->verdict;
+    if (!verdict && o->perm) {
+        if (!c->d_verdict) HIPCHK(c, hipMalloc(&c->d_verdict, sizeof(uint16_t) * c->max_batch));
+        verdict = c->d_verdict;
+    }
+    RxArgs a;
+    a.arena = d_arena;
+    a.desc = reinterpret_cast<const uint2 *>(d_desc);
+    a.n = n;
+    a.ntiles = ntiles;
+    a.verdict = verdict;
+    a.hash = o->hash;
+    a.anno = o->anno;
+    a.tilecnt = c->d_tilecnt;
+    a.cfg = c->dcfg;
+
+    EvPair ev[3];
+    if (c->timing)
+        for (int k = 0; k < 3; ++k) { ev[k].a = take_event(c); ev[k].b = take_event(c); ev[k].stage = k; }
+
+    if (c->timing) hipEventRecord(ev[0].a, s);
+    launch_rx_any(c->cfg.check_mode, c->cfg.checksum != 0, a, s);
+    HIPCHK(c, hipGetLastError());
+    if (c->timing) { hipEventRecord(ev[0].b, s); hipEventRecord(ev[1].a, s); }
+    hipLaunchKernelGGL(k_scan, dim3(nbt), dim3(1024), 0, s, c->d_tilecnt, ntiles, nports, c->d_totals,
+                       c->d_ctr);
+    HIPCHK(c, hipGetLastError());
+    if (c->timing) hipEventRecord(ev[1].b, s);
+    if (o->perm || o->port_start) {
+        if (c->timing) hipEventRecord(ev[2].a, s);
+        if (o->perm) {
+            hipLaunchKernelGGL(k_part, dim3(ntiles), dim3(kTile), 0, s, verdict, n, ntiles, nports,
+                               c->d_tilecnt, c->d_totals, o->perm, o->port_start);
+        } else {
+            hipLaunchKernelGGL(k_part, dim3(1), dim3(kTile), 0, s, verdict, 0u, ntiles, nports,
+                               c->d_tilecnt, c->d_totals, o->perm, o->port_start);
+        }
+        HIPCHK(c, hipGetLastError());
+        if (c->timing) hipEventRecord(ev[2].b, s);
+    }
+    if (c->timing) {
+        c->pending.push_back(ev[0]);
+        c->pending.push_back(ev[1]);
+        if (o->perm || o->port_start) c->pending.push_back(ev[2]);
+        else { c->free_ev.push_back(ev[2].a); c->free_ev.push_back(ev[2].b); }
+    }
+    return FCGPU_OK;
+}
+
+int fcgpu_process_host(fcgpu_ctx *c, const uint8_t *const *frames, const uint32_t *lens, uint32_t n,
+                       const fcgpu_out *h) {
+    if (!c || !h || (n && (!frames || !lens))) return FCGPU_EINVAL;
+    if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "batch larger than max_batch");
+    if (n == 0) return FCGPU_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t arena_cap = (size_t)c->max_batch * kHostCap + kArenaPad;
+    if (!c->h_arena) {
+        HIPCHK(c, hipHostMalloc((void **)&c->h_arena, arena_cap, hipHostMallocDefault));
+        HIPCHK(c, hipHostMalloc((void **)&c->h_desc, sizeof(uint32_t) * 2 * c->max_batch, hipHostMallocDefault));
+        HIPCHK(c, hipMalloc(&c->d_arena, arena_cap));
+        HIPCHK(c, hipMemset(c->d_arena, 0, arena_cap));
+        HIPCHK(c, hipMalloc(&c->d_desc, sizeof(uint32_t) * 2 * c->max_batch));
+        HIPCHK(c, hipMalloc(&c->d_hv, sizeof(uint16_t) * c->max_batch));
+        HIPCHK(c, hipMalloc(&c->d_hh, sizeof(uint32_t) * c->max_batch));
+        HIPCHK(c, hipMalloc(&c->d_hperm, sizeof(uint32_t) * c->max_batch));
+        HIPCHK(c, hipMalloc(&c->d_hstart, sizeof(uint32_t) * (FCGPU_MAX_PORTS + 2)));
+        HIPCHK(c, hipMalloc(&c->d_hanno, sizeof(fcgpu_anno) * c->max_batch));
+    }
+    // gather: first min(len, 128) bytes of each frame at 64-B aligned offsets.
+    // The device sees the real frame length; bytes past the capture are never
+    // needed for a verdict with headers <= 128 B.
+    size_t off = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t cap = lens[i] < kHostCap ? lens[i] : kHostCap;
+        memcpy(c->h_arena + off, frames[i], cap);
+        c->h_desc[2 * i] = (uint32_t)off;
+        c->h_desc[2 * i + 1] = lens[i];
+        off += (cap + 63) & ~(size_t)63;
+        if (cap == 0) off += 64;
+    }
+    hipStream_t s = c->stream;
+    HIPCHK(c, hipMemcpyAsync(c->d_arena, c->h_arena, off, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->d_desc, c->h_desc, sizeof(uint32_t) * 2 * n, hipMemcpyHostToDevice, s));
+    fcgpu_out d;
+    d.verdict = c->d_hv;
+    d.hash = h->hash ? c->d_hh : nullptr;
+    d.anno = h->anno ? c->d_hanno : nullptr;
+    d.perm = h->perm ? c->d_hperm : nullptr;
+    d.port_start = h->port_start ? c->d_hstart : nullptr;
+    int rc = fcgpu_process(c, c->d_arena, c->d_desc, n, &d, s);
+    if (rc != FCGPU_OK) return rc;
+    if (h->verdict) HIPCHK(c, hipMemcpyAsync(h->verdict, d.verdict, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, s));
+    if (h->hash) HIPCHK(c, hipMemcpyAsync(h->hash, d.hash, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
+    if (h->anno) HIPCHK(c, hipMemcpyAsync(h->anno, d.anno, sizeof(fcgpu_anno) * n, hipMemcpyDeviceToHost, s));
+    if (h->perm) HIPCHK(c, hipMemcpyAsync(h->perm, d.perm, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
+    if (h->port_start)
+        HIPCHK(c, hipMemcpyAsync(h->port_start, d.port_start, sizeof(uint32_t) * (c->cfg.nports + 2),
+                                 hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    return FCGPU_OK;
+}
+
+int fcgpu_read_counters(fcgpu_ctx *c, uint64_t *out, int n) {
+    if (!c || !out || n < 0) return FCGPU_EINVAL;
+    if (n > FCGPU_NCOUNTERS) n = FCGPU_NCOUNTERS;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(out, c->d_ctr, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
+    return FCGPU_OK;
+}
+
+int fcgpu_reset_counters(fcgpu_ctx *c) {
+    if (!c) return FCGPU_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * FCGPU_NCOUNTERS));
+    return FCGPU_OK;
+}
+
+int fcgpu_counters_device(fcgpu_ctx *c, uint64_t **d) {
+    if (!c || !d) return FCGPU_EINVAL;
+    *d = reinterpret_cast<uint64_t *>(c->d_ctr);
+    return FCGPU_OK;
+}
+
+int fcgpu_use_counters(fcgpu_ctx *c, uint64_t *d) {
+    if (!c) return FCGPU_EINVAL;
+    c->d_ctr = d ? reinterpret_cast<unsigned long long *>(d) : c->d_ctr_own;
+    return FCGPU_OK;
+}
+
+int fcgpu_set_timing(fcgpu_ctx *c, int enable) {
+    if (!c) return FCGPU_EINVAL;
+    c->timing = enable != 0;
+    return FCGPU_OK;
+}
+
+int fcgpu_read_timing(fcgpu_ctx *c, double *ms, uint32_t *launches, int nstages) {
+    if (!c || nstages < 0) return FCGPU_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    double acc[3] = {0, 0, 0};
+    uint32_t cnt[3] = {0, 0, 0};
+    for (auto &p : c->pending) {
+        HIPCHK(c, hipEventSynchronize(p.b));
+        float t = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&t, p.a, p.b));
+        acc[p.stage] += t;
+        cnt[p.stage]++;
+        c->free_ev.push_back(p.a);
+        c->free_ev.push_back(p.b);
+    }
+    c->pending.clear();
+    for (int k = 0; k < nstages && k < 3; ++k) {
+        if (ms) ms[k] = acc[k];
+        if (launches) launches[k] = cnt[k];
+    }
+    return FCGPU_OK;
+}
+
+}  // extern "C"

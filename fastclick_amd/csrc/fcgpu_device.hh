@@ -1,0 +1,410 @@
+// fcgpu_device.hh -- device code of the receive-path element library (gfx950).
+//
+// One lane per packet, 64 packets per wave, 256 packets per workgroup tile.
+// Each wave gathers the first 64 bytes of its 64 frames into LDS with four
+// 1-KiB LDS-DMA instructions (global_load_lds_dwordx4, per-lane source address
+// = arena + frame offset), so four consecutive lanes fetch one frame's 64 B as
+// one contiguous 64-B segment. Chunks are XOR-swizzled per row so that the
+// b128 lane groups hit distinct LDS slots. Each lane then parses its own row
+// with 4-B LDS reads at runtime offsets (IP header offset, transport offset),
+// falling back to aligned global loads for bytes past the 64-B window (IPv4
+// options, large OFFSET): correctness never depends on the window size.
+//
+// Integer/byte work only; no MFMA. The kernel is bound by HBM read bytes:
+// 8 B descriptor + 64 B window per packet.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/fastclick_gpu.h"
+
+namespace fcgpu {
+
+constexpr int kWave = 64;
+constexpr int kTile = 256;                  // packets per workgroup (4 waves)
+constexpr int kWin = 64;                    // header window bytes staged in LDS
+constexpr int kMaxBins = FCGPU_MAX_PORTS + 1 + FCGPU_NREASON_SLOTS;
+
+struct DevCfg {
+    int32_t offset;
+    uint32_t nports;
+    uint32_t hash_mode;
+    uint32_t classify;
+    int32_t hs_offset;
+    int32_t hs_length;
+    int32_t native_vlan;
+    uint32_t nbadsrc;
+    uint32_t ngooddst;
+    uint32_t nbad6;
+    uint32_t badsrc[FCGPU_MAX_ADDRS];
+    uint32_t gooddst[FCGPU_MAX_ADDRS];
+    uint32_t bad6[FCGPU_MAX_ADDRS][4];
+};
+
+struct RxArgs {
+    const uint8_t *arena;
+    const uint2 *desc;
+    uint32_t n;
+    uint32_t ntiles;
+    uint16_t *verdict;
+    uint32_t *hash;
+    fcgpu_anno *anno;
+    uint32_t *tilecnt;     // [nbins_total][ntiles]
+    DevCfg cfg;
+};
+
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xff) << 8) | ((x >> 8) & 0xff); }
+__device__ __forceinline__ uint32_t rotl32(uint32_t v, uint32_t r) {
+    // v_alignbit_b32 funnel shift; shift count is taken mod 32, so r = 0 -> v
+    return __builtin_amdgcn_alignbit(v, v, (32u - r) & 31u);
+}
+
+// One lane's view of its frame: 64-B window in LDS (swizzled 16-B chunks),
+// beyond that aligned global loads from the arena.
+struct FrameView {
+    const uint8_t *row;       // this lane's 64-B LDS row
+    const uint8_t *gwin;      // arena address of window byte 0 (16-B aligned)
+    uint32_t sw;              // chunk swizzle of this row
+    uint32_t shift;           // frame byte b lives at window byte b + shift
+
+    // aligned dword at window byte x (x % 4 == 0)
+    __device__ __forceinline__ uint32_t wdw(uint32_t x) const {
+        if (x < (uint32_t)kWin)
+            return *reinterpret_cast<const uint32_t *>(row + ((((x >> 4) ^ sw) << 4) | (x & 15)));
+        return *reinterpret_cast<const uint32_t *>(gwin + x);
+    }
+    // little-endian 32-bit value at frame byte b (any alignment)
+    __device__ __forceinline__ uint32_t rd32(uint32_t b) const {
+        const uint32_t x = b + shift;
+        const uint32_t lo = wdw(x & ~3u), hi = wdw((x & ~3u) + 4);
+        return __builtin_amdgcn_alignbyte(hi, lo, x & 3u);
+    }
+    // K consecutive little-endian dwords starting at frame byte b
+    template <int K>
+    __device__ __forceinline__ void run(uint32_t b, uint32_t (&out)[K]) const {
+        const uint32_t x = b + shift, a = x & ~3u, r = x & 3u;
+        uint32_t w[K + 1];
+#pragma unroll
+        for (int j = 0; j <= K; ++j) w[j] = wdw(a + 4 * j);
+#pragma unroll
+        for (int j = 0; j < K; ++j) out[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], r);
+    }
+    __device__ __forceinline__ uint32_t rd8(uint32_t b) const {
+        const uint32_t x = b + shift;
+        return (wdw(x & ~3u) >> (8 * (x & 3u))) & 0xff;
+    }
+};
+
+// click_in_cksum(hdr, hlen) == 0  <=>  the end-around-carry sum of the header's
+// 16-bit words folds to 0xffff (lib/in_cksum.c:20-51). Summing little-endian
+// dwords and folding is the same one's-complement sum (RFC 1071 associativity).
+__device__ __forceinline__ bool cksum_ok(const FrameView &f, uint32_t o, uint32_t hlen,
+                                         const uint32_t (&h)[5]) {
+    uint64_t s = (uint64_t)h[0] + h[1] + h[2] + h[3] + h[4];
+    for (uint32_t j = 20; j < hlen; j += 4) s += f.rd32(o + j);
+    s = (s & 0xffffffffu) + (s >> 32);
+    s = (s & 0xffffffffu) + (s >> 32);
+    uint32_t t = (uint32_t)s;
+    t = (t & 0xffff) + (t >> 16);
+    t = (t & 0xffff) + (t >> 16);
+    return t == 0xffff;
+}
+
+__device__ __forceinline__ int lb_port(uint32_t h, uint32_t n) {
+    return (int)(((h >> 16) ^ (h & 0xffff)) % n);
+}
+
+// HashSwitch::process / LoadBalancer::hash_ip byte-sum (hashswitch.cc:50-66,
+// loadbalancer.hh:227-243)
+__device__ __forceinline__ int bytesum_port(const FrameView &f, uint32_t len, int o, int l, uint32_t n) {
+    if ((int)len < o + l) return 0;
+    int d = 0;
+    for (int i = 0; i < l; ++i) d += (int)f.rd8((uint32_t)(o + i));
+    if (n == 2 || n == 4 || n == 8) return (d ^ (d >> 4)) & (int)(n - 1);
+    return d % (int)n;
+}
+
+struct PktResult {
+    uint32_t reason;
+    uint32_t port;
+    uint32_t hash;
+    fcgpu_anno an;
+};
+
+// CheckIPHeader::valid (elements/ip/checkipheader.cc:163-226); ip header at o.
+template <bool CK>
+__device__ __forceinline__ uint32_t check_ip4(const DevCfg &c, const FrameView &f, uint32_t len,
+                                              uint32_t o, uint32_t (&h)[5], fcgpu_anno &an) {
+    const uint32_t plen = len - o;
+    if ((int)plen < 20) return FCGPU_R_MINISCULE;
+    f.run<5>(o, h);
+    an.ipver = 4;
+    const uint32_t b0 = h[0] & 0xff;
+    if ((b0 >> 4) != 4) return FCGPU_R_BAD_VERSION;
+    const uint32_t hlen = (b0 & 15) << 2;
+    if (hlen < 20) return FCGPU_R_BAD_HLEN;
+    const uint32_t L = bswap16(h[0] >> 16);
+    if (L > plen || L < hlen) return FCGPU_R_BAD_IP_LEN;
+    if (CK && !cksum_ok(f, o, hlen, h)) return FCGPU_R_BAD_CKSUM;
+    if (c.nbadsrc) {
+        bool bad = false, good = false;
+        for (uint32_t j = 0; j < c.nbadsrc; ++j) bad |= (c.badsrc[j] == h[3]);
+        for (uint32_t j = 0; j < c.ngooddst; ++j) good |= (c.gooddst[j] == h[4]);
+        if (bad && !good) return FCGPU_R_BAD_SADDR;
+    }
+    an.nh = (uint8_t)o;
+    an.th = (uint8_t)(o + hlen);
+    an.length = (uint16_t)(plen > L ? len - (plen - L) : len);
+    an.dst_ip = h[4];
+    return FCGPU_R_OK;
+}
+
+// CheckIP6Header::simple_action (elements/ip6/checkip6header.cc:105-168)
+__device__ __forceinline__ uint32_t check_ip6(const DevCfg &c, const FrameView &f, uint32_t len,
+                                              uint32_t o, fcgpu_anno &an) {
+    const uint32_t plen = len - o;
+    an.ipver = 6;
+    if ((int)plen < 40) return FCGPU_R_BAD_IP6;
+    uint32_t h[2];
+    f.run<2>(o, h);
+    if (((h[0] & 0xff) >> 4) != 6) return FCGPU_R_BAD_IP6;
+    const uint32_t pl6 = bswap16(h[1] & 0xffff);
+    if (pl6 > plen - 40) return FCGPU_R_BAD_IP6;
+    if (c.nbad6) {
+        uint32_t s[4];
+        f.run<4>(o + 8, s);
+        for (uint32_t j = 0; j < c.nbad6; ++j)
+            if (s[0] == c.bad6[j][0] && s[1] == c.bad6[j][1] && s[2] == c.bad6[j][2] &&
+                s[3] == c.bad6[j][3])
+                return FCGPU_R_BAD_IP6;
+    }
+    an.nh = (uint8_t)o;
+    an.th = (uint8_t)(o + 40);
+    an.ip6_nxt = (uint8_t)((h[1] >> 16) & 0xff);
+    an.length = (uint16_t)(pl6 < plen - 40 ? len - (plen - 40 - pl6) : len);
+    return FCGPU_R_OK;
+}
+
+template <int CM, bool CK>
+__device__ __forceinline__ void process_packet(const DevCfg &c, const FrameView &f, uint32_t len,
+                                               PktResult &r) {
+    fcgpu_anno &an = r.an;
+    uint32_t o = (uint32_t)c.offset;
+    uint32_t h[5] = {0, 0, 0, 0, 0};
+    bool v6 = false;
+    r.hash = 0;
+    if (CM == FCGPU_CHECK_AUTO) {
+        // StripEtherVLANHeader::simple_action (stripethervlanheader.cc:48-61)
+        const uint32_t e = f.rd32(o + 12);        // bytes 12..15: type, tci
+        if ((e & 0xffff) == 0x0081) {             // be16 == 0x8100
+            an.vlan_tci = (uint16_t)(e >> 16);    // raw network-order tci
+            o += 18;
+        } else if (c.native_vlan >= 0) {
+            an.vlan_tci = (uint16_t)bswap16((uint32_t)c.native_vlan);
+            o += 14;
+        } else {
+            r.reason = FCGPU_R_VLAN_REJECT;
+            r.port = c.nports;
+            return;
+        }
+        v6 = ((int)(len - o) >= 1) && ((f.rd8(o) >> 4) == 6);
+        r.reason = v6 ? check_ip6(c, f, len, o, an) : check_ip4<CK>(c, f, len, o, h, an);
+    } else if (CM == FCGPU_MARK_IP4) {
+        // MarkIPHeader::simple_action (markipheader.cc:43-48)
+        f.run<5>(o, h);
+        an.nh = (uint8_t)o;
+        an.th = (uint8_t)(o + ((h[0] & 15) << 2));
+        an.length = (uint16_t)len;
+        an.ipver = 4;
+        r.reason = FCGPU_R_OK;
+    } else {
+        r.reason = check_ip4<CK>(c, f, len, o, h, an);
+    }
+    if (r.reason != FCGPU_R_OK) {
+        r.port = c.nports;
+        return;
+    }
+    uint32_t hv = 0;
+    if (c.hash_mode != FCGPU_HASH_NONE) {
+        const uint32_t pd = f.rd32(an.th);              // sport, dport (network order)
+        const uint32_t s = bswap16(pd & 0xffff), d = bswap16(pd >> 16);
+        if (v6) {
+            // IP6FlowID::hashcode (ip6flowid.hh:220-230), IP6Address::hashcode
+            const uint32_t sa = (f.rd32(an.nh + 16) << 1) + f.rd32(an.nh + 20);
+            const uint32_t da = (f.rd32(an.nh + 32) << 1) + f.rd32(an.nh + 36);
+            hv = rotl32(sa, s & 15) ^ rotl32(da, 31 - (d & 15)) ^ ((d << 16) | s);
+        } else {
+            // IPFlowID(p) (lib/ipflowid.cc:29-46): non-first fragments -> zero flow
+            const bool first = (bswap16(h[1] >> 16) & 0x1fff) == 0;
+            if (first) hv = rotl32(h[3], (s & 15) + 1) ^ rotl32(h[4], 31 - (d & 15)) ^ ((d << 16) | s);
+            if (c.hash_mode == FCGPU_HASH_FLOW5ID) hv ^= (h[2] >> 8) & 0xff;
+        }
+    }
+    r.hash = hv;
+    switch (c.classify) {
+    case FCGPU_CLS_LB_HASH: r.port = (uint32_t)lb_port(hv, c.nports); break;
+    case FCGPU_CLS_HASH_IP: r.port = (uint32_t)bytesum_port(f, an.length, 26, 8, c.nports); break;
+    case FCGPU_CLS_HASHSWITCH:
+        r.port = (uint32_t)bytesum_port(f, an.length, c.hs_offset, c.hs_length, c.nports);
+        break;
+    default: r.port = 0;
+    }
+}
+
+__device__ __forceinline__ void glds16(const uint8_t *src, uint8_t *lds) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                     (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t reason_slot(uint32_t r) { return r < 6 ? r : r - 1; }
+
+// Fused CheckIPHeader -> AggregateHash -> classify over one 256-packet tile,
+// plus the tile's per-output / per-reason histogram for the partition scan.
+template <int CM, bool CK>
+__global__ __launch_bounds__(kTile) void k_rx(RxArgs A) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[4 * kWave * kWin];
+    __shared__ uint32_t s_cnt[4][kMaxBins];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t i = blockIdx.x * kTile + threadIdx.x;
+    const bool live = i < A.n;
+    uint2 d = make_uint2(0, 0);
+    if (live) d = A.desc[i];
+
+    // gather: 4 x (16 frames x 64 B) per wave, LDS-DMA, swizzled 16-B chunks
+    uint8_t *wl = s_win + wave * (kWave * kWin);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t p = k * 16 + (lane >> 2);
+        const uint32_t poff = __shfl(d.x, (int)p);
+        const uint32_t c = (lane & 3) ^ ((p >> 2) & 3);
+        glds16(A.arena + (poff & ~15u) + c * 16, wl + k * 1024);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    FrameView f;
+    f.row = wl + lane * kWin;
+    f.sw = (lane >> 2) & 3;
+    f.shift = d.x & 15;
+    f.gwin = A.arena + (d.x & ~15u);
+
+    PktResult r;
+    r.an = fcgpu_anno{};
+    uint32_t bin = 0xffffffffu, rslot = 0xffffffffu;
+    if (live) {
+        process_packet<CM, CK>(A.cfg, f, d.y, r);
+        if (A.verdict) A.verdict[i] = (uint16_t)(r.reason | (r.port << 8));
+        if (A.hash) A.hash[i] = r.hash;
+        if (A.anno) A.anno[i] = r.an;
+        bin = r.port;
+        if (r.reason != FCGPU_R_OK) rslot = reason_slot(r.reason);
+    }
+
+    // per-wave histogram by ballot: outputs 0..nports (nports = invalid list)
+    const uint32_t nb = A.cfg.nports + 1;
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint64_t m = __ballot(bin == b);
+        if (lane == 0) s_cnt[wave][b] = (uint32_t)__popcll(m);
+    }
+    const uint64_t mbad = __ballot(rslot != 0xffffffffu);
+    for (uint32_t s = 0; s < FCGPU_NREASON_SLOTS; ++s) {
+        const uint32_t c = mbad ? (uint32_t)__popcll(__ballot(rslot == s)) : 0u;
+        if (lane == 0) s_cnt[wave][nb + s] = c;
+    }
+    __syncthreads();
+    const uint32_t nbt = nb + FCGPU_NREASON_SLOTS;
+    if (threadIdx.x < nbt) {
+        const uint32_t t = threadIdx.x;
+        A.tilecnt[t * A.ntiles + blockIdx.x] = s_cnt[0][t] + s_cnt[1][t] + s_cnt[2][t] + s_cnt[3][t];
+    }
+}
+
+// Exclusive scan of one bin's per-tile counts (in place), bin total, counters.
+// grid = nbins_total blocks of 1024 threads.
+__global__ __launch_bounds__(1024) void k_scan(uint32_t *tilecnt, uint32_t ntiles, uint32_t nports,
+                                               uint32_t *totals, unsigned long long *ctr) {
+    __shared__ uint32_t s_w[16];
+    const uint32_t b = blockIdx.x;
+    uint32_t *col = tilecnt + (size_t)b * ntiles;
+    const uint32_t per = (ntiles + 1023) / 1024;
+    const uint32_t beg = threadIdx.x * per;
+    uint32_t sum = 0;
+    for (uint32_t j = 0; j < per; ++j) {
+        const uint32_t t = beg + j;
+        if (t < ntiles) sum += col[t];
+    }
+    // block exclusive scan of per-thread sums
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t incl = sum;
+#pragma unroll
+    for (int dlt = 1; dlt < 64; dlt <<= 1) {
+        const uint32_t v = __shfl_up(incl, dlt);
+        if (lane >= (uint32_t)dlt) incl += v;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t wpre = 0, total = 0;
+    for (uint32_t w = 0; w < 16; ++w) {
+        const uint32_t v = s_w[w];
+        if (w < wave) wpre += v;
+        total += v;
+    }
+    uint32_t run = wpre + incl - sum;
+    for (uint32_t j = 0; j < per; ++j) {
+        const uint32_t t = beg + j;
+        if (t < ntiles) {
+            const uint32_t v = col[t];
+            col[t] = run;
+            run += v;
+        }
+    }
+    if (threadIdx.x == 0) {
+        totals[b] = total;
+        const unsigned long long T = total;
+        if (b < nports) {
+            atomicAdd(&ctr[FCGPU_CTR_PORT + b], T);
+            atomicAdd(&ctr[FCGPU_CTR_COUNT], T);
+        } else if (b == nports) {
+            atomicAdd(&ctr[FCGPU_CTR_PORT + b], T);
+            atomicAdd(&ctr[FCGPU_CTR_DROPS], T);
+        } else {
+            atomicAdd(&ctr[FCGPU_CTR_REASON + (b - nports - 1)], T);
+        }
+    }
+}
+
+// Stable partition (CLASSIFY_EACH_PACKET order): perm[start[bin] + rank] = i.
+__global__ __launch_bounds__(kTile) void k_part(const uint16_t *verdict, uint32_t n, uint32_t ntiles,
+                                                uint32_t nports, const uint32_t *tileoff,
+                                                const uint32_t *totals, uint32_t *perm,
+                                                uint32_t *port_start) {
+    __shared__ uint32_t s_cnt[4][FCGPU_MAX_PORTS + 1];
+    __shared__ uint32_t s_base[FCGPU_MAX_PORTS + 2];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t i = blockIdx.x * kTile + threadIdx.x;
+    const uint32_t nb = nports + 1;
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t b = 0; b < nb; ++b) { s_base[b] = acc; acc += totals[b]; }
+        s_base[nb] = acc;
+    }
+    if (blockIdx.x == 0 && port_start) {
+        __syncthreads();
+        if (threadIdx.x <= nb) port_start[threadIdx.x] = s_base[threadIdx.x];
+    }
+    const bool live = i < n;
+    const uint32_t bin = live ? (uint32_t)(verdict[i] >> 8) : 0xffffffffu;
+    uint32_t rank = 0;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint64_t m = __ballot(bin == b);
+        if (bin == b) rank = (uint32_t)__popcll(m & lt);
+        if (lane == 0) s_cnt[wave][b] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (live) {
+        uint32_t wpre = 0;
+        for (uint32_t w = 0; w < wave; ++w) wpre += s_cnt[w][bin];
+        perm[s_base[bin] + tileoff[(size_t)bin * ntiles + blockIdx.x] + wpre + rank] = i;
+    }
+}
+
+}  // namespace fcgpu

@@ -1,0 +1,95 @@
+"""Device-resident batches and one-call helpers over the C ABI.
+
+torch provides the device memory and the stream (plumbing only); every packet
+byte is processed by the HIP kernels in libfcgpu.so.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native as N
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("no HIP device visible to torch")
+    return torch
+
+
+@dataclass
+class DeviceBatch:
+    arena: "object"      # torch.uint8 cuda tensor
+    desc: "object"       # torch.int32 cuda tensor [n, 2] (uint32 bit pattern)
+    n: int
+
+    @classmethod
+    def upload(cls, batch, device="cuda"):
+        torch = _torch()
+        arena = torch.from_numpy(np.ascontiguousarray(batch.arena)).to(device)
+        desc = torch.from_numpy(np.ascontiguousarray(batch.desc).view(np.int32)).to(device)
+        return cls(arena=arena, desc=desc, n=batch.n)
+
+
+class DeviceOutputs:
+    def __init__(self, n, nports, device="cuda", *, verdict=True, hash=True, anno=False,
+                 perm=False, port_start=False):
+        torch = _torch()
+        self.n = n
+        self.nports = nports
+        mk = lambda k, dt: torch.empty(k, dtype=dt, device=device)  # noqa: E731
+        self.verdict = mk(n, torch.int16) if verdict else None
+        self.hash = mk(n, torch.int32) if hash else None
+        self.anno = mk(n * 16, torch.uint8) if anno else None
+        self.perm = mk(n, torch.int32) if perm else None
+        self.port_start = mk(nports + 2, torch.int32) if port_start else None
+
+    def ptrs(self):
+        p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+        return dict(verdict=p(self.verdict), hash=p(self.hash), anno=p(self.anno),
+                    perm=p(self.perm), port_start=p(self.port_start))
+
+    def numpy(self):
+        out = {}
+        if self.verdict is not None:
+            v = self.verdict.cpu().numpy().view(np.uint16)
+            out["verdict"] = v
+            out["reason"] = (v & 0xFF).astype(np.uint8)
+            out["port"] = (v >> 8).astype(np.uint8)
+        if self.hash is not None:
+            out["hash"] = self.hash.cpu().numpy().view(np.uint32)
+        if self.anno is not None:
+            out["anno"] = self.anno.cpu().numpy().view(N.anno_dtype())
+        if self.perm is not None:
+            out["perm"] = self.perm.cpu().numpy().view(np.uint32)
+        if self.port_start is not None:
+            out["port_start"] = self.port_start.cpu().numpy().view(np.uint32)
+        return out
+
+
+def run_device(ctx: N.Context, dbatch: DeviceBatch, outs: DeviceOutputs, stream=None):
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    ctx.process(dbatch.arena.data_ptr(), dbatch.desc.data_ptr(), dbatch.n,
+                stream=s.cuda_stream, **outs.ptrs())
+
+
+def process_batch(batch, cfg, *, anno=True, perm=True, device_index=0):
+    """Upload a host Batch, run the device path once, return numpy results and
+    the counter vector. Convenience for tests and smoke()."""
+    torch = _torch()
+    with torch.cuda.device(device_index):
+        ctx = N.Context(device_index, max(batch.n, 1), cfg)
+        try:
+            db = DeviceBatch.upload(batch, device=f"cuda:{device_index}")
+            outs = DeviceOutputs(batch.n, cfg.nports, device=f"cuda:{device_index}",
+                                 anno=anno, perm=perm, port_start=perm)
+            run_device(ctx, db, outs)
+            torch.cuda.synchronize()
+            res = outs.numpy()
+            res["counters"] = np.array(ctx.counters(), dtype=np.uint64)
+        finally:
+            ctx.close()
+    return res

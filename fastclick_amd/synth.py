@@ -1,0 +1,297 @@
+"""Deterministic synthetic packet batches for the receive-path hot path.
+
+Builds the inputs of BASELINE.json's configs (C1..C5) as an *arena + descriptor*
+batch, the layout the GPU element consumes (DESIGN.md "Data layout"):
+
+* ``arena``  uint8[...]  frames placed at 64-B aligned offsets, padded by
+  ``ARENA_PAD`` bytes so a 128-B header window never runs off the end;
+* ``desc``   uint32[n, 2] per packet ``(offset, length)``.
+
+Frames follow the packet-format conventions of the reference's own generators:
+"64 B" on the wire is a 60-B captured frame (``conf/pktgen/pktgen-l3.click:13``,
+``elements/tcpudp/fastudpflows.cc:146-175``: ip_len = L - 14, TTL 64, UDP, zero
+payload, valid IPv4 checksum).
+
+This module is data plumbing for tests, bench and golden generation; it does not
+implement any element semantics.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+ARENA_PAD = 256          # bytes of slack after the last frame (window over-read)
+SLOT_ALIGN = 64          # frame offsets are multiples of this
+ETH_IP4 = 0x0800
+ETH_IP6 = 0x86DD
+ETH_8021Q = 0x8100
+
+# error kinds injected by ``inject_errors`` (names mirror CheckIPHeader reasons,
+# elements/ip/checkipheader.hh:139-147)
+ERR_TINY, ERR_VERSION, ERR_HLEN, ERR_IPLEN, ERR_CKSUM, ERR_BADSRC = range(6)
+ERR_NAMES = ["tiny", "version", "hlen", "iplen", "cksum", "badsrc"]
+BADSRC_ADDR = bytes([192, 0, 2, 255])     # the address ``badsrc`` errors use
+
+
+@dataclass
+class Batch:
+    arena: np.ndarray                 # uint8
+    desc: np.ndarray                  # uint32 [n, 2] (offset, length)
+    meta: dict = field(default_factory=dict)
+
+    @property
+    def n(self) -> int:
+        return int(self.desc.shape[0])
+
+    def frame(self, i: int) -> bytes:
+        off, ln = (int(x) for x in self.desc[i])
+        return bytes(self.arena[off:off + ln])
+
+    def frames(self):
+        return [self.frame(i) for i in range(self.n)]
+
+
+def _ip4_cksum(h: np.ndarray) -> np.ndarray:
+    """Internet checksum of rows of 20-byte IPv4 headers (cksum field zero)."""
+    w = h[:, 0::2].astype(np.uint32) << 8 | h[:, 1::2].astype(np.uint32)
+    s = w.sum(axis=1, dtype=np.uint64)
+    s = (s & 0xFFFF) + (s >> 16)
+    s = (s & 0xFFFF) + (s >> 16)
+    return (~s & 0xFFFF).astype(np.uint16)
+
+
+def _be16(a: np.ndarray) -> np.ndarray:
+    a = np.asarray(a, dtype=np.uint32)
+    return np.stack([(a >> 8) & 0xFF, a & 0xFF], axis=-1).astype(np.uint8)
+
+
+def _be32(a: np.ndarray) -> np.ndarray:
+    a = np.asarray(a, dtype=np.uint64)
+    return np.stack([(a >> 24) & 0xFF, (a >> 16) & 0xFF, (a >> 8) & 0xFF, a & 0xFF],
+                    axis=-1).astype(np.uint8)
+
+
+def build_headers(n, *, src, dst, sport, dport, proto=17, frame_len=60,
+                  vlan_tci=None, ip6=None, ttl=64, ip_id=None, width=128):
+    """Return uint8[n, width] header rows (Ethernet [+802.1Q] + IPv4/IPv6 + L4).
+
+    src/dst: uint32 (host-order value of the dotted quad) for IPv4 rows; for IPv6
+    rows (``ip6`` mask true) src/dst are taken from ``ip6['src']/['dst']`` (n,16).
+    frame_len: per-packet captured length (scalar or array).
+    vlan_tci: None or int array (n,) with -1 = untagged.
+    """
+    frame_len = np.broadcast_to(np.asarray(frame_len, dtype=np.int64), (n,))
+    hdr = np.zeros((n, width), dtype=np.uint8)
+    hdr[:, 0:6] = [0x02, 0, 0, 0, 0, 0x02]
+    hdr[:, 6:12] = [0x02, 0, 0, 0, 0, 0x01]
+    tagged = np.zeros(n, bool) if vlan_tci is None else (np.asarray(vlan_tci) >= 0)
+    is6 = np.zeros(n, bool) if ip6 is None else np.asarray(ip6["mask"], bool)
+    o = np.where(tagged, 18, 14)
+    etype = np.where(is6, ETH_IP6, ETH_IP4)
+    # untagged: ethertype at 12
+    u = ~tagged
+    hdr[u, 12:14] = _be16(etype[u])
+    if tagged.any():
+        hdr[tagged, 12:14] = _be16(np.full(tagged.sum(), ETH_8021Q))
+        hdr[tagged, 14:16] = _be16(np.asarray(vlan_tci)[tagged])
+        hdr[tagged, 16:18] = _be16(etype[tagged])
+    sport = np.broadcast_to(np.asarray(sport, dtype=np.uint32), (n,))
+    dport = np.broadcast_to(np.asarray(dport, dtype=np.uint32), (n,))
+    src = np.broadcast_to(np.asarray(src, dtype=np.uint64), (n,))
+    dst = np.broadcast_to(np.asarray(dst, dtype=np.uint64), (n,))
+    proto = np.broadcast_to(np.asarray(proto, dtype=np.uint32), (n,))
+    if ip_id is None:
+        ip_id = np.arange(n, dtype=np.uint32) & 0xFFFF
+    for off in (14, 18):
+        sel4 = (o == off) & ~is6
+        if sel4.any():
+            k = sel4.sum()
+            ip = np.zeros((k, 20), np.uint8)
+            ip[:, 0] = 0x45
+            ip[:, 2:4] = _be16(frame_len[sel4] - off)
+            ip[:, 4:6] = _be16(np.asarray(ip_id)[sel4])
+            ip[:, 8] = ttl
+            ip[:, 9] = proto[sel4]
+            ip[:, 12:16] = _be32(src[sel4])
+            ip[:, 16:20] = _be32(dst[sel4])
+            ip[:, 10:12] = _be16(_ip4_cksum(ip))
+            hdr[sel4, off:off + 20] = ip
+            l4 = np.zeros((k, 8), np.uint8)
+            l4[:, 0:2] = _be16(sport[sel4])
+            l4[:, 2:4] = _be16(dport[sel4])
+            l4[:, 4:6] = _be16(np.maximum(frame_len[sel4] - off - 20, 0))
+            hdr[sel4, off + 20:off + 28] = l4
+        sel6 = (o == off) & is6
+        if sel6.any():
+            k = sel6.sum()
+            ip = np.zeros((k, 40), np.uint8)
+            ip[:, 0] = 0x60
+            ip[:, 4:6] = _be16(frame_len[sel6] - off - 40)
+            ip[:, 6] = proto[sel6]
+            ip[:, 7] = 64
+            ip[:, 8:24] = np.asarray(ip6["src"])[sel6]
+            ip[:, 24:40] = np.asarray(ip6["dst"])[sel6]
+            hdr[sel6, off:off + 40] = ip
+            l4 = np.zeros((k, 8), np.uint8)
+            l4[:, 0:2] = _be16(sport[sel6])
+            l4[:, 2:4] = _be16(dport[sel6])
+            l4[:, 4:6] = _be16(np.maximum(frame_len[sel6] - off - 40, 0))
+            hdr[sel6, off + 40:off + 48] = l4
+    return hdr
+
+
+def pack(hdr: np.ndarray, frame_len, *, meta=None) -> Batch:
+    """Place frames at SLOT_ALIGN-aligned offsets; only header rows are non-zero."""
+    n = hdr.shape[0]
+    frame_len = np.broadcast_to(np.asarray(frame_len, dtype=np.int64), (n,))
+    slot = np.maximum((frame_len + SLOT_ALIGN - 1) // SLOT_ALIGN * SLOT_ALIGN, SLOT_ALIGN)
+    off = np.zeros(n, np.int64)
+    if n:
+        off[1:] = np.cumsum(slot)[:-1]
+    total = int(off[-1] + slot[-1]) if n else 0
+    arena = np.zeros(total + ARENA_PAD, np.uint8)
+    w = hdr.shape[1]
+    if n and (slot == slot[0]).all() and slot[0] >= w:
+        arena[:n * slot[0]].reshape(n, slot[0])[:, :w] = hdr
+    elif n:
+        width = np.minimum(slot, w)
+        for cw in np.unique(width):
+            sel = np.nonzero(width == cw)[0]
+            idx = off[sel, None] + np.arange(cw)[None, :]
+            arena[idx] = hdr[sel, :cw]
+    desc = np.stack([off.astype(np.uint32), frame_len.astype(np.uint32)], axis=1)
+    return Batch(arena=arena, desc=np.ascontiguousarray(desc), meta=dict(meta or {}))
+
+
+def _rand_flows(rng, k):
+    return dict(src=rng.integers(0, 2**32, k, dtype=np.uint64),
+                dst=rng.integers(0, 2**32, k, dtype=np.uint64),
+                sport=rng.integers(0, 2**16, k, dtype=np.uint32),
+                dport=rng.integers(0, 2**16, k, dtype=np.uint32))
+
+
+def ip4(a, b, c, d):
+    return (a << 24) | (b << 16) | (c << 8) | d
+
+
+def c1(n=4096, seed=1):
+    """C1: 60-B UDP/IPv4 frames over 4096 uniform random 5-tuples, all valid."""
+    rng = np.random.default_rng(seed)
+    fl = _rand_flows(rng, 4096)
+    pick = rng.integers(0, 4096, n)
+    hdr = build_headers(n, **{k: v[pick] for k, v in fl.items()}, frame_len=60)
+    return pack(hdr, 60, meta=dict(config="C1", seed=seed))
+
+
+def c2(n=1 << 20, seed=2):
+    """C2: 60-B frames in 64-B slots, one 5-tuple 10.0.0.1:1234 -> 10.0.0.2:5678."""
+    hdr = build_headers(n, src=ip4(10, 0, 0, 1), dst=ip4(10, 0, 0, 2),
+                        sport=1234, dport=5678, frame_len=60, width=64)
+    return pack(hdr, 60, meta=dict(config="C2", seed=seed))
+
+
+IMIX_LEN = np.array([60, 566, 1496])      # 64/570/1500 B on the wire, 7:4:1
+IMIX_W = np.array([7, 4, 1]) / 12.0
+
+
+def c3(n=1 << 20, nflows=10000, seed=3):
+    """C3: IMIX (64/570/1500 B at 7:4:1), 10k uniform random 5-tuples."""
+    rng = np.random.default_rng(seed)
+    fl = _rand_flows(rng, nflows)
+    pick = rng.integers(0, nflows, n)
+    flen = IMIX_LEN[rng.choice(3, n, p=IMIX_W)]
+    hdr = build_headers(n, **{k: v[pick] for k, v in fl.items()}, frame_len=flen, width=64)
+    return pack(hdr, flen, meta=dict(config="C3", seed=seed, nflows=nflows))
+
+
+def c4(n=1 << 20, seed=4):
+    """C4: 60-B frames, every packet an independent uniform random 5-tuple."""
+    rng = np.random.default_rng(seed)
+    fl = _rand_flows(rng, n)
+    hdr = build_headers(n, **fl, frame_len=60, width=64)
+    return pack(hdr, 60, meta=dict(config="C4", seed=seed))
+
+
+def c5(n=1 << 16, seed=5):
+    """C5: 50% 802.1Q tagged (random VID), 30% IPv6 (80-B frame), 70% IPv4 (60-B)."""
+    rng = np.random.default_rng(seed)
+    fl = _rand_flows(rng, n)
+    tagged = rng.random(n) < 0.5
+    tci = np.where(tagged, rng.integers(0, 4096, n), -1)
+    is6 = rng.random(n) < 0.3
+    src6 = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    dst6 = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    flen = np.where(is6, 80, 60) + np.where(tagged, 4, 0)
+    hdr = build_headers(n, **fl, frame_len=flen, vlan_tci=tci,
+                        ip6=dict(mask=is6, src=src6, dst=dst6))
+    return pack(hdr, flen, meta=dict(config="C5", seed=seed))
+
+
+def inject_errors(batch: Batch, rate: float, seed: int = 7, kinds=range(6),
+                  ip_off: int = 14) -> np.ndarray:
+    """Corrupt ~``rate`` of the packets per kind, in place. Returns int8[n] kind
+    (-1 = untouched). Assumes untagged IPv4 frames with the IP header at ip_off."""
+    rng = np.random.default_rng(seed)
+    n = batch.n
+    kind = np.full(n, -1, np.int8)
+    r = rng.random(n)
+    kinds = list(kinds)
+    for j, k in enumerate(kinds):
+        sel = np.nonzero((r >= j * rate) & (r < (j + 1) * rate))[0]
+        kind[sel] = k
+    A = batch.arena
+    off = batch.desc[:, 0].astype(np.int64) + ip_off
+    for i in np.nonzero(kind >= 0)[0]:
+        o = int(off[i])
+        k = int(kind[i])
+        if k == ERR_TINY:
+            batch.desc[i, 1] = ip_off + int(rng.integers(0, 20))
+        elif k == ERR_VERSION:
+            A[o] = (int(rng.choice([0, 5, 6, 15])) << 4) | int(A[o] & 15)
+        elif k == ERR_HLEN:
+            A[o] = 0x40 | int(rng.integers(0, 5))
+        elif k == ERR_IPLEN:
+            plen = int(batch.desc[i, 1]) - ip_off
+            bad = plen + 1 + int(rng.integers(0, 100)) if rng.random() < 0.5 else int(rng.integers(0, 20))
+            A[o + 2], A[o + 3] = (bad >> 8) & 0xFF, bad & 0xFF
+        elif k == ERR_CKSUM:
+            A[o + 10] ^= 1 << int(rng.integers(0, 8))
+        elif k == ERR_BADSRC:
+            A[o + 12:o + 16] = np.frombuffer(BADSRC_ADDR, np.uint8)
+        if k in (ERR_VERSION, ERR_HLEN, ERR_IPLEN, ERR_BADSRC):
+            _refresh_cksum(A, o)
+    return kind
+
+
+def _refresh_cksum(A, o):
+    hl = max(int(A[o] & 15) * 4, 20)
+    A[o + 10] = A[o + 11] = 0
+    w = A[o:o + hl].astype(np.uint32)
+    s = int((w[0::2] << 8 | w[1::2]).sum())
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    c = ~s & 0xFFFF
+    A[o + 10], A[o + 11] = c >> 8, c & 0xFF
+
+
+def add_ip_options(batch: Batch, frac: float, seed: int = 9, ip_off: int = 14):
+    """Rewrite ~frac of IPv4 packets to carry 4..40 bytes of NOP options
+    (ihl 6..15) with a consistent ip_len/checksum, shifting the L4 header. The
+    frame must have room: the frame length is kept, payload shrinks."""
+    rng = np.random.default_rng(seed)
+    A = batch.arena
+    sel = np.nonzero(rng.random(batch.n) < frac)[0]
+    for i in sel:
+        off, ln = int(batch.desc[i, 0]), int(batch.desc[i, 1])
+        o = off + ip_off
+        ihl = int(rng.integers(6, 16))
+        extra = (ihl - 5) * 4
+        if ln - ip_off < ihl * 4 + 8:
+            continue
+        l4 = A[o + 20:o + 28].copy()
+        A[o + 20:o + 20 + extra] = 1          # NOP options
+        A[o + 20 + extra:o + 28 + extra] = l4
+        A[o] = 0x40 | ihl
+        _refresh_cksum(A, o)
+    return sel

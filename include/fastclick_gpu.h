@@ -1,0 +1,191 @@
+/*
+ * fastclick_gpu.h -- C ABI of the MI355X receive-path element library
+ * (libfcgpu.so, HIP for gfx950).
+ *
+ * One call processes one batch of packets through the fused chain
+ *
+ *     [StripEtherVLANHeader] -> CheckIPHeader | CheckIP6Header | MarkIPHeader
+ *         -> AggregateHash (IPFlowID / IPFlow5ID / IP6FlowID low-32 hash)
+ *         -> per-port classify (FlowSwitch LB hash, LB hash_ip, HashSwitch)
+ *         -> stable per-port partition (CLASSIFY_EACH_PACKET)
+ *
+ * and replaces, for a FastClick BatchElement, the per-packet loops
+ *   - CheckIPHeader::valid            elements/ip/checkipheader.cc:163-226
+ *   - click_in_cksum                  lib/in_cksum.c:20-51
+ *   - IPFlowID::hashcode              include/click/ipflowid.hh:153-164
+ *   - IPFlow5ID::hashcode             include/click/ipflowid.hh:242-251
+ *   - AggregateHash::simple_action    elements/analysis/aggregatehash.cc:49-55
+ *   - LoadBalancer::pick_server       include/click/loadbalancer.hh:553-584
+ *   - HashSwitch::process             elements/standard/hashswitch.cc:50-66
+ *   - StripEtherVLANHeader::simple_action elements/ethernet/stripethervlanheader.cc:48-61
+ *   - CheckIP6Header::simple_action   elements/ip6/checkip6header.cc:105-168
+ *   - IP6FlowID::hashcode             include/click/ip6flowid.hh:220-230
+ *   - CLASSIFY_EACH_PACKET            include/click/packetbatch.hh:259-307
+ * (SURVEY.md section 8(a) rows A1-A15). The FastClick-side caller is the
+ * GPUIPCheckClassify element (fastclick_amd/csrc/host/), which keeps the
+ * Element::push_batch API (include/click/element.hh:53-54) and calls this ABI.
+ *
+ * Batch layout ("arena + descriptor"):
+ *   arena : bytes; packet i's frame starts at arena + desc[2i] and is
+ *           desc[2i+1] bytes long. The arena must stay readable for 128 bytes
+ *           past every frame start (header-window over-read; never used for a
+ *           verdict).
+ *   desc  : uint32 pairs (offset, length), 8 bytes per packet.
+ * Results are per-packet structure-of-arrays; every output pointer may be NULL
+ * (that output is then not produced).
+ *
+ * Errors: every int-returning entry point returns FCGPU_OK (0) or a negative
+ * FCGPU_E* code; fcgpu_last_error() gives the message. There is no silent
+ * fallback: a missing device or a failed launch is an error return.
+ */
+#ifndef FASTCLICK_GPU_H
+#define FASTCLICK_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FCGPU_ABI_VERSION 1
+
+#define FCGPU_OK          0
+#define FCGPU_EINVAL     -1   /* bad argument / configuration            */
+#define FCGPU_ENODEV     -2   /* no HIP device / device not usable       */
+#define FCGPU_ENOMEM     -3   /* allocation failed / batch > max_batch   */
+#define FCGPU_ERUNTIME   -4   /* HIP runtime or kernel launch failure    */
+
+/* Verdict reason codes. 0..6 are CheckIPHeader::Reason
+ * (elements/ip/checkipheader.hh:139-147); 6 = NREASONS = valid. */
+#define FCGPU_R_MINISCULE   0
+#define FCGPU_R_BAD_VERSION 1
+#define FCGPU_R_BAD_HLEN    2
+#define FCGPU_R_BAD_IP_LEN  3
+#define FCGPU_R_BAD_CKSUM   4
+#define FCGPU_R_BAD_SADDR   5
+#define FCGPU_R_OK          6
+#define FCGPU_R_BAD_IP6     7   /* CheckIP6Header's single drop reason      */
+#define FCGPU_R_VLAN_REJECT 8   /* StripEtherVLANHeader output 1 (untagged, NATIVE_VLAN < 0) */
+#define FCGPU_NREASON_SLOTS 8   /* counters for reasons 0-5, 7, 8           */
+
+/* check_mode */
+#define FCGPU_CHECK_IP4   0   /* CheckIPHeader(OFFSET o[, CHECKSUM c, BADSRC, GOODDST]) */
+#define FCGPU_MARK_IP4    1   /* MarkIPHeader(o): no validation                         */
+#define FCGPU_CHECK_AUTO  2   /* StripEtherVLANHeader(NATIVE_VLAN) at o, then by IP version
+                                 nibble: 6 -> CheckIP6Header, else -> CheckIPHeader      */
+/* hash_mode (written to the AGGREGATE annotation output) */
+#define FCGPU_HASH_NONE     0
+#define FCGPU_HASH_FLOWID   1   /* IPFlowID(p).hashcode() low 32 (AggregateHash); v6: IP6FlowID */
+#define FCGPU_HASH_FLOW5ID  2   /* IPFlow5ID(p).hashcode() low 32 (adds ip_p)               */
+/* classify */
+#define FCGPU_CLS_NONE       0  /* every valid packet -> port 0                          */
+#define FCGPU_CLS_LB_HASH    1  /* LoadBalancer direct_hash / direct_hash_agg:
+                                   ((H>>16) ^ (H&0xffff)) % nports                       */
+#define FCGPU_CLS_HASH_IP    2  /* LoadBalancer direct_hash_ip (frame bytes 26..33)      */
+#define FCGPU_CLS_HASHSWITCH 3  /* HashSwitch(hs_offset, hs_length), nports = MAX        */
+
+#define FCGPU_MAX_PORTS   64
+#define FCGPU_MAX_ADDRS   16
+
+typedef struct fcgpu_cfg {
+    uint32_t size;            /* = sizeof(fcgpu_cfg)                                     */
+    uint32_t check_mode;      /* FCGPU_CHECK_*                                           */
+    int32_t  offset;          /* OFFSET: frame start -> IP header (CHECK_IP4/MARK_IP4),
+                                 or frame start -> Ethernet header (CHECK_AUTO)          */
+    uint32_t checksum;        /* CHECKSUM; the reference default is FALSE
+                                 (elements/ip/checkipheader.cc:110)          */
+    uint32_t hash_mode;       /* FCGPU_HASH_*                                            */
+    uint32_t classify;        /* FCGPU_CLS_*                                             */
+    uint32_t nports;          /* classify outputs N (1..FCGPU_MAX_PORTS)                 */
+    int32_t  hs_offset;       /* HashSwitch OFFSET (frame-relative)                      */
+    int32_t  hs_length;       /* HashSwitch LENGTH (> 0)                                 */
+    int32_t  native_vlan;     /* StripEtherVLANHeader NATIVE_VLAN (default 0; <0 reject) */
+    uint32_t nbadsrc;         /* BADSRC list (raw network-order s_addr words)            */
+    uint32_t ngooddst;        /* GOODDST list                                             */
+    uint32_t badsrc[FCGPU_MAX_ADDRS];
+    uint32_t gooddst[FCGPU_MAX_ADDRS];
+    uint32_t nbad6;           /* CheckIP6Header bad source list; default = {ff..ff}      */
+    uint8_t  bad6[FCGPU_MAX_ADDRS][16];
+} fcgpu_cfg;
+
+/* Optional per-packet annotations (16 B), mirroring what the reference
+ * elements leave on a valid packet. Offsets are relative to the frame start the
+ * element received (the descriptor offset). */
+typedef struct fcgpu_anno {
+    uint32_t dst_ip;          /* DST_IP_ANNO (IPv4 valid) = raw ip_dst word             */
+    uint16_t length;          /* packet length after Packet::take() trimming            */
+    uint8_t  nh;              /* network header offset (set_ip_header / set_ip6_header) */
+    uint8_t  th;              /* transport header offset                                 */
+    uint16_t vlan_tci;        /* VLAN_TCI_ANNO, raw network order (CHECK_AUTO)          */
+    uint8_t  ip6_nxt;         /* IP6_NXT_ANNO (IPv6 valid)                              */
+    uint8_t  ipver;           /* 4 or 6 for packets that reached a checker, else 0      */
+    uint32_t reserved;
+} fcgpu_anno;
+
+typedef struct fcgpu_out {
+    uint16_t   *verdict;      /* [n] reason | (output port << 8); invalid -> port nports */
+    uint32_t   *hash;         /* [n] AGGREGATE annotation (0 unless valid)               */
+    fcgpu_anno *anno;         /* [n] optional annotations                                */
+    uint32_t   *perm;         /* [n] packet indices grouped by output, input order kept  */
+    uint32_t   *port_start;   /* [nports+2] start of each output's run in perm; last=n   */
+} fcgpu_out;
+
+typedef struct fcgpu_ctx fcgpu_ctx;
+
+/* Counter vector layout returned by fcgpu_read_counters (uint64):
+ *   [0] count (valid packets)         CheckIPHeader "count"
+ *   [1] drops                         CheckIPHeader "drops"
+ *   [2 .. 2+8)  reason drops: slots for reasons 0-5, 7, 8 ("drop_details")
+ *   [10 .. 10+nports+1) per-output packet counts, last = invalid list       */
+#define FCGPU_CTR_COUNT   0
+#define FCGPU_CTR_DROPS   1
+#define FCGPU_CTR_REASON  2
+#define FCGPU_CTR_PORT    10
+#define FCGPU_NCOUNTERS   (FCGPU_CTR_PORT + FCGPU_MAX_PORTS + 1)
+
+int  fcgpu_abi_version(void);
+int  fcgpu_device_count(void);
+void fcgpu_default_cfg(fcgpu_cfg *cfg);
+
+/* Open a context on HIP device `device` for batches of up to max_batch packets.
+ * One context per (Click thread x stream); a context is not thread-safe. */
+int  fcgpu_open(int device, uint32_t max_batch, fcgpu_ctx **out);
+int  fcgpu_configure(fcgpu_ctx *ctx, const fcgpu_cfg *cfg);
+void fcgpu_close(fcgpu_ctx *ctx);
+
+/* Device-resident batch: arena, desc and every output pointer are device
+ * memory. Asynchronous on `stream` (hipStream_t, NULL = the context's stream).
+ * Completion: synchronise that stream. */
+int  fcgpu_process(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_desc,
+                   uint32_t n, const fcgpu_out *d_out, void *stream);
+
+/* Host-resident batch: frames[i] points at packet i's data (length lens[i]).
+ * The first min(len, 128) bytes of every frame are gathered into pinned
+ * staging, copied H2D, processed, and the requested outputs copied D2H into the
+ * host pointers of h_out. Synchronous. */
+int  fcgpu_process_host(fcgpu_ctx *ctx, const uint8_t *const *frames,
+                        const uint32_t *lens, uint32_t n, const fcgpu_out *h_out);
+
+int  fcgpu_read_counters(fcgpu_ctx *ctx, uint64_t *out, int n);
+int  fcgpu_reset_counters(fcgpu_ctx *ctx);
+/* Device address of the context's uint64 counter vector (FCGPU_NCOUNTERS), for
+ * a cross-GPU all-reduce on the caller's stream. */
+int  fcgpu_counters_device(fcgpu_ctx *ctx, uint64_t **d_counters);
+/* Make the context accumulate into caller-owned device memory (FCGPU_NCOUNTERS
+ * uint64, initialised by the caller), e.g. a tensor that is all-reduced in
+ * place over RCCL. NULL reverts to the context's own vector. */
+int  fcgpu_use_counters(fcgpu_ctx *ctx, uint64_t *d_counters);
+
+/* Per-kernel timing with HIP events on the launch stream (off by default).
+ * fcgpu_read_timing returns, per stage (0 = fused check/hash/classify,
+ * 1 = count scan, 2 = partition scatter), the summed milliseconds and launches
+ * since the last read, and resets them. Synchronises the context stream. */
+int  fcgpu_set_timing(fcgpu_ctx *ctx, int enable);
+int  fcgpu_read_timing(fcgpu_ctx *ctx, double *ms, uint32_t *launches, int nstages);
+
+const char *fcgpu_last_error(fcgpu_ctx *ctx);   /* ctx may be NULL (open errors) */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FASTCLICK_GPU_H */

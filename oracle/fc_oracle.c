@@ -1,0 +1,283 @@
+/*
+ * fc_oracle.c -- TEST INFRASTRUCTURE ONLY (see fc_oracle.h).
+ *
+ * Plain-C restatement of the reference's receive-path semantics. Every function
+ * names the reference lines it restates. This is the checker for the HIP path,
+ * never a fallback for it.
+ */
+#include "fc_oracle.h"
+#include <stdlib.h>
+#include <string.h>
+
+static inline uint32_t le32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+static inline uint16_t be16(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
+static inline uint16_t raw16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
+static inline uint32_t rotl32(uint32_t v, unsigned r) {
+    r &= 31;
+    return r ? (v << r) | (v >> (32 - r)) : v;
+}
+
+/* lib/in_cksum.c:20-51: 32-bit accumulator over host-order 16-bit words, odd
+ * trailing byte in the low byte, two folds, one's complement. */
+uint16_t fco_in_cksum(const uint8_t *addr, int len)
+{
+    int nleft = len;
+    uint32_t sum = 0;
+    const uint8_t *w = addr;
+    while (nleft > 1) {
+        uint16_t x;
+        memcpy(&x, w, 2);
+        sum += x;
+        w += 2;
+        nleft -= 2;
+    }
+    if (nleft == 1)
+        sum += (uint16_t)w[0];           /* *(uchar*)&answer = *w, little endian */
+    sum = (sum & 0xffff) + (sum >> 16);
+    sum += (sum >> 16);
+    return (uint16_t)~sum;
+}
+
+/* include/click/ipflowid.hh:153-164 with IPAddress::hashcode = raw s_addr
+ * (include/click/ipaddress.hh:346-350); hashcode_t is 64-bit, consumers keep
+ * the low 32 bits (elements/analysis/aggregatehash.cc:51). */
+uint32_t fco_ipflowid_hash(uint32_t sx, uint16_t sport_net, uint32_t dx, uint16_t dport_net)
+{
+    uint32_t s = (uint16_t)((sport_net >> 8) | (sport_net << 8));
+    uint32_t d = (uint16_t)((dport_net >> 8) | (dport_net << 8));
+    return rotl32(sx, (s % 16) + 1) ^ rotl32(dx, 31 - (d % 16)) ^ ((d << 16) | s);
+}
+
+/* include/click/ip6address.hh:348-352: (data32[2] << 1) + data32[3]. */
+static uint32_t ip6_addr_hash(const uint8_t a[16])
+{
+    return (le32(a + 8) << 1) + le32(a + 12);
+}
+
+/* include/click/ip6flowid.hh:220-230. ROT(v, 0) shifts a 32-bit value by 32
+ * (UB); x86 masks the count and yields v, restated here as rotl32(v, 0) = v. */
+uint32_t fco_ip6flowid_hash(const uint8_t src[16], uint16_t sport_net,
+                            const uint8_t dst[16], uint16_t dport_net)
+{
+    uint32_t s = (uint16_t)((sport_net >> 8) | (sport_net << 8));
+    uint32_t d = (uint16_t)((dport_net >> 8) | (dport_net << 8));
+    return rotl32(ip6_addr_hash(src), s % 16) ^ rotl32(ip6_addr_hash(dst), 31 - d % 16)
+        ^ ((d << 16) | s);
+}
+
+/* include/click/loadbalancer.hh:580-584 (direct_hash; direct_hash_agg at
+ * :570-574 is the same on AGGREGATE_ANNO), identity selector. */
+int fco_lb_hash_port(uint32_t h, int n)
+{
+    return (int)(((h >> 16) ^ (h & 65535)) % (uint32_t)n);
+}
+
+/* include/click/loadbalancer.hh:227-243 (hash_ip). */
+int fco_hash_ip_port(const uint8_t *data, uint32_t len, int n)
+{
+    int o = 26, l = 8;
+    if ((int)len < o + l)
+        return 0;
+    int d = 0;
+    for (int i = o; i < o + l; i++)
+        d += data[i];
+    if (n == 2 || n == 4 || n == 8)
+        return (d ^ (d >> 4)) & (n - 1);
+    return d % n;
+}
+
+/* elements/standard/hashswitch.cc:50-66. */
+int fco_hashswitch_port(const uint8_t *data, uint32_t len, int o, int l, int n)
+{
+    if ((int)len < o + l)
+        return 0;
+    int d = 0;
+    for (int i = o; i < o + l; i++)
+        d += data[i];
+    if (n == 2 || n == 4 || n == 8)
+        return (d ^ (d >> 4)) & (n - 1);
+    return d % n;
+}
+
+/* include/click/packetbatch.hh:259-307: stable partition into nbatches lists,
+ * out-of-range outputs to the last list. */
+void fco_classify_each_packet(int nbatches, const int *port, uint32_t n,
+                              uint32_t *perm, uint32_t *start)
+{
+    uint32_t cnt[FCGPU_MAX_PORTS + 2];
+    memset(cnt, 0, sizeof(cnt));
+    for (uint32_t i = 0; i < n; i++) {
+        int o = port[i];
+        if (o < 0 || o >= nbatches) o = nbatches - 1;
+        cnt[o]++;
+    }
+    uint32_t acc = 0;
+    for (int b = 0; b < nbatches; b++) { start[b] = acc; acc += cnt[b]; }
+    start[nbatches] = acc;
+    if (!perm) return;
+    uint32_t pos[FCGPU_MAX_PORTS + 2];
+    memcpy(pos, start, sizeof(uint32_t) * (nbatches + 1));
+    for (uint32_t i = 0; i < n; i++) {
+        int o = port[i];
+        if (o < 0 || o >= nbatches) o = nbatches - 1;
+        perm[pos[o]++] = i;
+    }
+}
+
+static int in_list(const uint32_t *l, uint32_t nl, uint32_t v)
+{
+    for (uint32_t i = 0; i < nl; i++)
+        if (l[i] == v) return 1;
+    return 0;
+}
+
+/* elements/ip/checkipheader.cc:163-226 (CheckIPHeader::valid) with
+ * Packet::take (include/click/packet.hh:2189-2207), set_ip_header
+ * (packet.hh:2493-2496) and set_dst_ip_anno. ip offset `o` from frame start. */
+static int check_ip4(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, uint32_t o,
+                     fcgpu_anno *a)
+{
+    unsigned plen = len - o;
+    if ((int)plen < 20)
+        return FCGPU_R_MINISCULE;
+    const uint8_t *ip = f + o;
+    a->ipver = 4;
+    if ((ip[0] >> 4) != 4)
+        return FCGPU_R_BAD_VERSION;
+    unsigned hlen = (unsigned)(ip[0] & 15) << 2;
+    if (hlen < 20)
+        return FCGPU_R_BAD_HLEN;
+    unsigned L = be16(ip + 2);
+    if (L > plen || L < hlen)
+        return FCGPU_R_BAD_IP_LEN;
+    if (c->checksum && fco_in_cksum(ip, (int)hlen) != 0)
+        return FCGPU_R_BAD_CKSUM;
+    uint32_t src = le32(ip + 12), dst = le32(ip + 16);
+    if (in_list(c->badsrc, c->nbadsrc, src) && !in_list(c->gooddst, c->ngooddst, dst))
+        return FCGPU_R_BAD_SADDR;
+    a->nh = (uint8_t)o;
+    a->th = (uint8_t)(o + hlen);
+    a->length = (uint16_t)(plen > L ? len - (plen - L) : len);
+    a->dst_ip = dst;
+    return FCGPU_R_OK;
+}
+
+/* elements/ip6/checkip6header.cc:105-168 (PROCESS_EH false). */
+static int check_ip6(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, uint32_t o,
+                     fcgpu_anno *a)
+{
+    unsigned plen = len - o;
+    a->ipver = 6;
+    if ((int)plen < 40)
+        return FCGPU_R_BAD_IP6;
+    const uint8_t *ip = f + o;
+    if ((ip[0] >> 4) != 6)
+        return FCGPU_R_BAD_IP6;
+    unsigned pl6 = be16(ip + 4);
+    if (pl6 > plen - 40)
+        return FCGPU_R_BAD_IP6;
+    for (uint32_t i = 0; i < c->nbad6; i++)
+        if (memcmp(ip + 8, c->bad6[i], 16) == 0)
+            return FCGPU_R_BAD_IP6;
+    a->nh = (uint8_t)o;
+    a->th = (uint8_t)(o + 40);
+    a->ip6_nxt = ip[6];
+    a->length = (uint16_t)(pl6 < plen - 40 ? len - (plen - 40 - pl6) : len);
+    return FCGPU_R_OK;
+}
+
+void fco_process_packet(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, fco_result *r)
+{
+    memset(r, 0, sizeof(*r));
+    fcgpu_anno *a = &r->anno;
+    uint32_t o = (uint32_t)c->offset;
+    int reason;
+    int v6 = 0;
+    if (c->check_mode == FCGPU_CHECK_AUTO) {
+        /* elements/ethernet/stripethervlanheader.cc:48-61 */
+        if (be16(f + o + 12) == 0x8100) {
+            a->vlan_tci = raw16(f + o + 14);
+            o += 18;
+        } else if (c->native_vlan >= 0) {
+            uint16_t t = (uint16_t)c->native_vlan;
+            a->vlan_tci = (uint16_t)((t >> 8) | (t << 8));
+            o += 14;
+        } else {
+            r->reason = FCGPU_R_VLAN_REJECT;
+            r->port = (uint8_t)c->nports;
+            return;
+        }
+        /* version dispatch as Classifier(0/60%f0, -): needs one byte */
+        v6 = ((int)(len - o) >= 1) && ((f[o] >> 4) == 6);
+        reason = v6 ? check_ip6(c, f, len, o, a) : check_ip4(c, f, len, o, a);
+    } else if (c->check_mode == FCGPU_MARK_IP4) {
+        /* elements/ip/markipheader.cc:43-48 */
+        a->nh = (uint8_t)o;
+        a->th = (uint8_t)(o + ((f[o] & 15) << 2));
+        a->length = (uint16_t)len;
+        a->ipver = 4;
+        reason = FCGPU_R_OK;
+    } else {
+        reason = check_ip4(c, f, len, o, a);
+    }
+    r->reason = (uint8_t)reason;
+    if (reason != FCGPU_R_OK) {
+        r->port = (uint8_t)c->nports;
+        return;
+    }
+    uint32_t h = 0;
+    if (c->hash_mode != FCGPU_HASH_NONE) {
+        const uint8_t *nh = f + a->nh, *th = f + a->th;
+        if (v6) {
+            /* lib/ip6flowid.cc:29-50 */
+            h = fco_ip6flowid_hash(nh + 8, raw16(th), nh + 24, raw16(th + 2));
+        } else {
+            /* lib/ipflowid.cc:29-46: non-first fragments leave the ID
+             * uninitialised in the reference; restated as the zero flow. */
+            int first = (be16(nh + 6) & 0x1fff) == 0;
+            if (first)
+                h = fco_ipflowid_hash(le32(nh + 12), raw16(th), le32(nh + 16), raw16(th + 2));
+            if (c->hash_mode == FCGPU_HASH_FLOW5ID)
+                h ^= nh[9];   /* include/click/ipflowid.hh:242-251 */
+        }
+    }
+    r->hash = h;
+    int port = 0;
+    switch (c->classify) {
+    case FCGPU_CLS_LB_HASH:    port = fco_lb_hash_port(h, (int)c->nports); break;
+    case FCGPU_CLS_HASH_IP:    port = fco_hash_ip_port(f, a->length, (int)c->nports); break;
+    case FCGPU_CLS_HASHSWITCH: port = fco_hashswitch_port(f, a->length, c->hs_offset,
+                                                           c->hs_length, (int)c->nports); break;
+    default: port = 0;
+    }
+    r->port = (uint8_t)port;
+}
+
+static int reason_slot(int r) { return r < 6 ? r : r - 1; }
+
+void fco_process_batch(const fcgpu_cfg *c, const uint8_t *arena, const uint32_t *desc,
+                       uint32_t n, uint16_t *verdict, uint32_t *hash, fcgpu_anno *anno,
+                       uint32_t *perm, uint32_t *port_start, uint64_t *ctr)
+{
+    int nb = (int)c->nports + 1;
+    int *port = (int *)malloc(sizeof(int) * (n ? n : 1));
+    for (uint32_t i = 0; i < n; i++) {
+        fco_result r;
+        fco_process_packet(c, arena + desc[2 * i], desc[2 * i + 1], &r);
+        if (verdict) verdict[i] = (uint16_t)(r.reason | (r.port << 8));
+        if (hash) hash[i] = r.hash;
+        if (anno) anno[i] = r.anno;
+        port[i] = r.port;
+        if (ctr) {
+            if (r.reason == FCGPU_R_OK) ctr[FCGPU_CTR_COUNT]++;
+            else { ctr[FCGPU_CTR_DROPS]++; ctr[FCGPU_CTR_REASON + reason_slot(r.reason)]++; }
+            ctr[FCGPU_CTR_PORT + r.port]++;
+        }
+    }
+    if (perm || port_start) {
+        uint32_t start[FCGPU_MAX_PORTS + 2];
+        fco_classify_each_packet(nb, port, n, perm, start);
+        if (port_start) memcpy(port_start, start, sizeof(uint32_t) * (nb + 1));
+    }
+    free(port);
+}

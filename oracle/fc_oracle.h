@@ -1,0 +1,59 @@
+/*
+ * fc_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Scalar CPU restatement of the FastClick receive-path elements, used as the
+ * parity checker for the HIP path (tests/, __graft_entry__.smoke(), and
+ * bench.py's cpu_baseline leg). Nothing in fastclick_amd/ may include, link or
+ * call this code. Each function cites the reference file:line it restates.
+ *
+ * Parity pin: the restatement is checked against golden vectors produced by the
+ * compiled reference (tests/golden/, generator tests/golden/gen_golden.py).
+ */
+#ifndef FC_ORACLE_H
+#define FC_ORACLE_H
+#include <stdint.h>
+#include "../include/fastclick_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* A1: lib/in_cksum.c:20-51 */
+uint16_t fco_in_cksum(const uint8_t *addr, int len);
+
+/* Per-packet result of the fused chain (same meaning as the GPU outputs). */
+typedef struct fco_result {
+    uint8_t    reason;   /* FCGPU_R_* */
+    uint8_t    port;     /* output index; nports for the invalid list */
+    uint32_t   hash;
+    fcgpu_anno anno;
+} fco_result;
+
+/* A2 (+A4/A13/A14): one packet through the configured check chain, then
+ * A5-A7/A15 hashing and A8/A9 classification. */
+void fco_process_packet(const fcgpu_cfg *cfg, const uint8_t *frame, uint32_t len,
+                        fco_result *r);
+
+/* Batch driver over the arena+descriptor layout, same outputs as the device
+ * path: verdict/hash/anno arrays may be NULL. perm/port_start as A10
+ * (CLASSIFY_EACH_PACKET stable partition, include/click/packetbatch.hh:259-307).
+ * counters (FCGPU_NCOUNTERS) are accumulated (not reset). */
+void fco_process_batch(const fcgpu_cfg *cfg, const uint8_t *arena, const uint32_t *desc,
+                       uint32_t n, uint16_t *verdict, uint32_t *hash, fcgpu_anno *anno,
+                       uint32_t *perm, uint32_t *port_start, uint64_t *counters);
+
+/* Individual pieces, exposed for known-answer tests. */
+uint32_t fco_ipflowid_hash(uint32_t saddr_raw, uint16_t sport_net,
+                           uint32_t daddr_raw, uint16_t dport_net);  /* A6 */
+uint32_t fco_ip6flowid_hash(const uint8_t src[16], uint16_t sport_net,
+                            const uint8_t dst[16], uint16_t dport_net); /* A15 */
+int fco_lb_hash_port(uint32_t h, int n);                         /* A8 direct_hash */
+int fco_hash_ip_port(const uint8_t *data, uint32_t len, int n);  /* A8 hash_ip */
+int fco_hashswitch_port(const uint8_t *data, uint32_t len, int off, int l, int n); /* A9 */
+void fco_classify_each_packet(int nbatches, const int *port, uint32_t n,
+                              uint32_t *perm, uint32_t *start); /* A10 */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

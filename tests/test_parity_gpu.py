@@ -1,0 +1,218 @@
+"""GPU parity: the HIP path through the C ABI vs the C oracle, bit-exact.
+
+Every case runs fastclick_amd.device.process_batch (libfcgpu.so kernels) and
+oracle.process_batch (fc_oracle.c) on the same seeded batch and compares the
+reason code, output port, 32-bit flow hash, annotations, stable per-port
+permutation and counters. The oracle itself is pinned to the compiled
+reference by tests/test_golden.py.
+"""
+import numpy as np
+import pytest
+
+from fastclick_amd import synth
+from fastclick_amd import _native as N
+from tests.helpers import compare, repack, set_fragment
+
+pytestmark = pytest.mark.gpu
+
+BADSRC = [N.raw_addr("192.0.2.255"), N.raw_addr("255.255.255.255")]
+GOODDST = [N.raw_addr("10.9.9.9")]
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    from fastclick_amd import device
+    N.load()
+    return device
+
+
+def _check(dev, oracle, batch, cfg, ctx, anno=True, perm=True):
+    got = dev.process_batch(batch, cfg, anno=anno, perm=perm)
+    exp = oracle.process_batch(cfg, batch)
+    compare(got, exp, anno=anno, perm=perm, ctx=ctx)
+    assert np.array_equal(got["counters"], exp["counters"]), \
+        f"{ctx}: counters {got['counters'][:12]} vs {exp['counters'][:12]}"
+    return got, exp
+
+
+def test_c2_cksum_hash_classify16(dev, oracle):
+    b = synth.c2(70_001)
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16)
+    got, _ = _check(dev, oracle, b, cfg, "C2")
+    assert (got["reason"] == N.R_OK).all()
+
+
+@pytest.mark.parametrize("checksum", [True, False])
+def test_c4_errors(dev, oracle, checksum):
+    b = synth.c4(200_000, seed=40)
+    kind = synth.inject_errors(b, 0.02, seed=41)
+    cfg = N.make_cfg(offset=14, checksum=checksum, classify=N.CLS_LB_HASH, nports=16,
+                     badsrc=BADSRC, gooddst=GOODDST)
+    got, exp = _check(dev, oracle, b, cfg, f"C4 errors cksum={checksum}")
+    # every injected error kind shows up as its reason (checksum only if enabled)
+    for k in range(6):
+        if k == synth.ERR_CKSUM and not checksum:
+            continue
+        assert (exp["reason"][kind == k] == k).mean() > 0.95
+
+
+def test_c3_imix_flow5id(dev, oracle):
+    b = synth.c3(150_000, nflows=10_000)
+    cfg = N.make_cfg(offset=14, checksum=True, hash_mode=N.HASH_FLOW5ID,
+                     classify=N.CLS_LB_HASH, nports=16)
+    _check(dev, oracle, b, cfg, "C3")
+
+
+def test_ip_options_and_fragments(dev, oracle):
+    b = synth.c3(60_000, seed=31)
+    synth.add_ip_options(b, 0.3)
+    set_fragment(b, 0.1)
+    synth.inject_errors(b, 0.01, seed=32)
+    for ck in (True, False):
+        cfg = N.make_cfg(offset=14, checksum=ck, classify=N.CLS_LB_HASH, nports=7)
+        _check(dev, oracle, b, cfg, f"options ck={ck}")
+
+
+def test_misaligned_offsets(dev, oracle):
+    b = synth.c3(20_000, seed=33)
+    synth.add_ip_options(b, 0.5, seed=34)
+    synth.inject_errors(b, 0.02, seed=35)
+    b = repack(b, misalign_seed=36)
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16,
+                     badsrc=BADSRC)
+    _check(dev, oracle, b, cfg, "misaligned")
+
+
+def test_offset_zero_and_large(dev, oracle):
+    # frames starting at the IP header (after Strip(14)) and a deep OFFSET
+    b = synth.c4(10_000, seed=50)
+    synth.inject_errors(b, 0.02, seed=51)
+    frames = [f[14:] for f in b.frames()]
+    lens = np.array([len(f) for f in frames])
+    hdr = np.zeros((b.n, 64), np.uint8)
+    for i, f in enumerate(frames):
+        hdr[i, :len(f)] = np.frombuffer(f, np.uint8)
+    b0 = synth.pack(hdr, lens)
+    cfg = N.make_cfg(offset=0, checksum=True, classify=N.CLS_LB_HASH, nports=16)
+    _check(dev, oracle, b0, cfg, "offset0")
+    pad = 100
+    hdr2 = np.zeros((b.n, 256), np.uint8)
+    for i, f in enumerate(b.frames()):
+        hdr2[i, pad:pad + len(f)] = np.frombuffer(f, np.uint8)
+    b2 = synth.pack(hdr2, b.desc[:, 1].astype(np.int64) + pad)
+    cfg = N.make_cfg(offset=pad + 14, checksum=True, classify=N.CLS_LB_HASH, nports=16)
+    _check(dev, oracle, b2, cfg, "offset114")
+
+
+@pytest.mark.parametrize("native", [0, 5, -1])
+def test_c5_vlan_ip6(dev, oracle, native):
+    b = synth.c5(80_000)
+    cfg = N.make_cfg(check_mode=N.CHECK_AUTO, offset=0, checksum=True, classify=N.CLS_LB_HASH,
+                     nports=16, native_vlan=native)
+    got, exp = _check(dev, oracle, b, cfg, f"C5 native={native}")
+    assert (exp["anno"]["ipver"] == 6).any()
+
+
+def test_c5_ip6_bad_and_trim(dev, oracle):
+    b = synth.c5(30_000, seed=55)
+    rng = np.random.default_rng(56)
+    A = b.arena
+    for i in range(b.n):
+        off, ln = (int(x) for x in b.desc[i])
+        o = off + (18 if A[off + 12] == 0x81 else 14)
+        if A[o] >> 4 != 6:
+            continue
+        r = rng.random()
+        if r < 0.05:
+            A[o + 8:o + 24] = 0xFF                       # bad source ff..ff
+        elif r < 0.10:
+            A[o + 4], A[o + 5] = 0x40, 0                 # payload length too large
+        elif r < 0.20:
+            A[o + 4], A[o + 5] = 0, int(rng.integers(0, 8))   # trimmed
+        elif r < 0.25:
+            b.desc[i, 1] = o - off + int(rng.integers(0, 40))  # shorter than 40 B
+    cfg = N.make_cfg(check_mode=N.CHECK_AUTO, checksum=True, classify=N.CLS_LB_HASH, nports=16)
+    _check(dev, oracle, b, cfg, "C5 bad/trim")
+
+
+def test_mark_mode(dev, oracle):
+    b = synth.c4(20_000, seed=60)
+    synth.inject_errors(b, 0.02, seed=61)
+    cfg = N.make_cfg(check_mode=N.MARK_IP4, offset=14, hash_mode=N.HASH_FLOW5ID,
+                     classify=N.CLS_LB_HASH, nports=5)
+    _check(dev, oracle, b, cfg, "mark")
+
+
+@pytest.mark.parametrize("n", [2, 4, 5, 8, 16])
+def test_hash_ip_and_hashswitch(dev, oracle, n):
+    b = synth.c3(20_000, seed=70 + n)
+    synth.inject_errors(b, 0.01, seed=80 + n)
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_HASH_IP, nports=n)
+    _check(dev, oracle, b, cfg, f"hash_ip n={n}")
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_HASHSWITCH, nports=n,
+                     hs_offset=26, hs_length=12)
+    _check(dev, oracle, b, cfg, f"hashswitch n={n}")
+    cfg = N.make_cfg(offset=14, classify=N.CLS_HASHSWITCH, nports=n, hs_offset=60, hs_length=70)
+    _check(dev, oracle, b, cfg, f"hashswitch long n={n}")
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 255, 256, 257])
+def test_ragged_sizes(dev, oracle, n):
+    b = synth.c4(n, seed=90 + n)
+    synth.inject_errors(b, 0.1, seed=91)
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=64)
+    _check(dev, oracle, b, cfg, f"n={n}")
+
+
+def test_empty_batch(dev):
+    ctx = N.Context(0, 16, N.make_cfg(offset=14))
+    ctx.process(0, 0, 0)
+    assert ctx.counters()[:2] == [0, 0]
+    ctx.close()
+
+
+def test_counters_accumulate_and_host_path(dev, oracle):
+    import ctypes as C
+    b = synth.c4(5000, seed=95)
+    synth.inject_errors(b, 0.03, seed=96)
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16, badsrc=BADSRC)
+    exp = oracle.process_batch(cfg, b)
+    ctx = N.Context(0, b.n, cfg)
+    frames = b.frames()
+    bufs = [C.create_string_buffer(f, len(f)) for f in frames]
+    ptrs = (C.c_void_p * b.n)(*[C.addressof(x) for x in bufs])
+    lens = np.ascontiguousarray(b.desc[:, 1], dtype=np.uint32)
+    verdict = np.zeros(b.n, np.uint16)
+    hsh = np.zeros(b.n, np.uint32)
+    anno = np.zeros(b.n, N.anno_dtype())
+    perm = np.zeros(b.n, np.uint32)
+    start = np.zeros(cfg.nports + 2, np.uint32)
+    for _ in range(3):
+        ctx.process_host(ptrs, lens.ctypes.data, b.n, verdict=verdict.ctypes.data,
+                         hash=hsh.ctypes.data, anno=anno.ctypes.data, perm=perm.ctypes.data,
+                         port_start=start.ctypes.data)
+        got = dict(reason=(verdict & 0xFF).astype(np.uint8), port=(verdict >> 8).astype(np.uint8),
+                   hash=hsh, anno=anno, perm=perm, port_start=start)
+        compare(got, exp, ctx="host path")
+    ctr = np.array(ctx.counters(), np.uint64)
+    assert np.array_equal(ctr, 3 * exp["counters"])
+    ctx.close()
+
+
+def test_large_batch_properties(dev, oracle):
+    """4M packets: full oracle comparison of hash/port plus partition
+    properties (sorted runs, permutation, counts)."""
+    n = 1 << 22
+    b = synth.c4(n, seed=99)
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16)
+    got = dev.process_batch(b, cfg, anno=False, perm=True)
+    exp = oracle.process_batch(cfg, b)
+    compare(got, exp, anno=False, ctx="4M")
+    perm, start = got["perm"], got["port_start"]
+    assert np.array_equal(np.sort(perm), np.arange(n, dtype=np.uint32))
+    for p in range(17):
+        run = perm[start[p]:start[p + 1]]
+        assert (np.diff(run.astype(np.int64)) > 0).all()
+        assert (got["port"][run] == p).all()
