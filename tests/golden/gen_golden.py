@@ -1,0 +1,350 @@
+#!/usr/bin/env python3
+"""Generate golden vectors from the compiled FastClick reference.
+
+Run here (not on the GPU box): needs a userlevel FastClick build of the
+reference tree (configure + make into /tmp/fcbuild, and a
+--enable-ctx --enable-flow-dynamic build in /tmp/fcbuild3 for FlowSwitch) and
+the reference harness oracle/_ref/fcref (oracle/ref/Makefile). Inputs are
+synthetic, deterministic (fastclick_amd.synth, fixed seeds) and written as
+pcaps with timestamp = 1000 + packet index, so every reference output line can
+be mapped back to its input packet.
+
+Outputs (committed): tests/golden/<set>.npz (inputs + expected outputs, only
+data) and tests/golden/PROVENANCE.json (graphs, binary hashes, tool versions).
+
+Per field, the reference mechanism that produced it:
+  reason    CheckIPHeader(CHECKSUM true, BADSRC .., GOODDST ..): valid vs port-1
+            split from one graph; per-packet reason of every dropped packet from
+            a single-packet run of the same element with DETAILS true
+            (drop_details handler, elements/ip/checkipheader.cc:241-266)
+  hash      AggregateHash -> ToIPSummaryDump(FIELDS timestamp aggregate)
+  length    ToDump(ENCAP IP) of the valid packets after Strip(14) (caplen)
+  lb16      FlowSwitch(LB_MODE hash) behind CTXManager/CTXDispatcher (fcbuild3)
+  hs4/hs7   HashSwitch(26, 8) with 4/7 outputs behind CheckIPHeader(OFFSET 14)
+  v6        StripEtherVLANHeader -> Classifier(0/60%f0, -) -> CheckIP6Header /
+            CheckIPHeader: verdicts and lengths; IP6FlowID hash from fcref
+  cksum/h6  click_in_cksum and IPFlowID/IP6FlowID::hashcode compiled from the
+            reference sources by oracle/ref/Makefile (fcref)
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import json
+import os
+import struct
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from fastclick_amd import synth  # noqa: E402
+
+CLICK = os.environ.get("FC_CLICK", "/tmp/fcbuild/userlevel/click")
+CLICK3 = os.environ.get("FC_CLICK3", "/tmp/fcbuild3/userlevel/click")
+FCREF = os.path.join(ROOT, "oracle", "_ref", "fcref")
+T0 = 1000
+BADSRC = "192.0.2.255 255.255.255.255"
+GOODDST = "10.9.9.9"
+NOT_PINNED = 255
+
+
+def write_pcap(path, frames):
+    with open(path, "wb") as f:
+        f.write(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, 65535, 1))
+        for i, fr in enumerate(frames):
+            f.write(struct.pack("<IIII", T0 + i, 0, len(fr), len(fr)))
+            f.write(fr)
+
+
+def read_pcap(path):
+    out = {}
+    with open(path, "rb") as f:
+        data = f.read()
+    pos = 24
+    while pos + 16 <= len(data):
+        ts, _, incl, orig = struct.unpack_from("<IIII", data, pos)
+        pos += 16
+        out[ts - T0] = (incl, data[pos:pos + incl])
+        pos += incl
+    return out
+
+
+def read_ipsum(path, fields):
+    rows = {}
+    if not os.path.exists(path):
+        return rows
+    for line in open(path):
+        if line.startswith("!") or not line.strip():
+            continue
+        parts = line.split()
+        idx = int(float(parts[0])) - T0
+        rows[idx] = parts[1:]
+    return rows
+
+
+def click(binary, cfg, cwd):
+    r = subprocess.run([binary, "-e", cfg], cwd=cwd, capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        raise RuntimeError(f"click failed: {r.stderr[-2000:]}")
+    return r.stdout, r.stderr
+
+
+def reason_of_single(args):
+    idx, pcap, chain_prefix, ck_args = args
+    with tempfile.TemporaryDirectory() as d:
+        frames = read_pcap_frames(pcap)
+        write_pcap(os.path.join(d, "one.pcap"), [frames[idx]])
+        out, err = click(CLICK, f"FromDump(one.pcap, STOP true, TIMING false) -> {chain_prefix}"
+                         f"ck :: CheckIPHeader({ck_args}, DETAILS true) -> Discard; ck[1] -> Discard;"
+                         " DriverManager(wait, print ck.drop_details)", d)
+    counts = [int(line.split()[0]) for line in out.strip().splitlines()]
+    assert len(counts) == 6, out
+    if sum(counts) == 0:
+        return idx, 6
+    assert sum(counts) == 1, (idx, counts)
+    return idx, counts.index(1)
+
+
+_frames_cache = {}
+
+
+def read_pcap_frames(pcap):
+    if pcap not in _frames_cache:
+        d = read_pcap(pcap)
+        _frames_cache[pcap] = [d[i][1] for i in range(len(d))]
+    return _frames_cache[pcap]
+
+
+def make_ip4_set(n=2400, seed=2024):
+    """Untagged IPv4 frames (60..252 B), ~2% of each error kind, IP options on
+    15%, non-first fragments on 5%, a few TCP/ICMP protocol numbers."""
+    rng = np.random.default_rng(seed)
+    fl = synth._rand_flows(rng, n)
+    flen = rng.choice([60, 60, 60, 74, 98, 128, 190, 252], n)
+    proto = rng.choice([17, 17, 17, 6, 1], n)
+    hdr = synth.build_headers(n, **fl, proto=proto, frame_len=flen)
+    # a few GOODDST destinations so BADSRC/GOODDST interplay is exercised
+    b = synth.pack(hdr, flen, meta=dict(set="ip4", seed=seed))
+    synth.add_ip_options(b, 0.15, seed=seed + 1)
+    A = b.arena
+    frag = rng.random(n) < 0.05
+    for i in np.nonzero(frag)[0]:
+        o = int(b.desc[i, 0]) + 14
+        fo = int(rng.integers(1, 0x1FFF))
+        A[o + 6], A[o + 7] = (fo >> 8) & 0x1F, fo & 0xFF
+        synth._refresh_cksum(A, o)
+    kind = synth.inject_errors(b, 0.02, seed=seed + 2)
+    good = rng.random(n) < 0.3
+    for i in np.nonzero((kind == synth.ERR_BADSRC) & good)[0]:
+        o = int(b.desc[i, 0]) + 14
+        A[o + 16:o + 20] = [10, 9, 9, 9]
+        synth._refresh_cksum(A, o)
+    return b, kind
+
+
+def make_mix_set(n=1600, seed=2025):
+    """C5-style: 50% 802.1Q, 30% IPv6 (some bad/trimmed), IPv4 with errors."""
+    b = synth.c5(n, seed=seed)
+    rng = np.random.default_rng(seed + 1)
+    A = b.arena
+    for i in range(b.n):
+        off = int(b.desc[i, 0])
+        o = off + (18 if A[off + 12] == 0x81 else 14)
+        r = rng.random()
+        if A[o] >> 4 == 6:
+            if r < 0.05:
+                A[o + 8:o + 24] = 0xFF
+            elif r < 0.10:
+                A[o + 4], A[o + 5] = 0x40, 0
+            elif r < 0.2:
+                A[o + 4], A[o + 5] = 0, int(rng.integers(8, 20))
+        else:
+            if r < 0.05:
+                A[o + 10] ^= 0x10
+            elif r < 0.08:
+                A[o] = 0x55
+    return b
+
+
+def run_ip4(b, tmp):
+    pcap = os.path.join(tmp, "ip4.pcap")
+    frames = b.frames()
+    write_pcap(pcap, frames)
+    n = b.n
+    ck_args = f"CHECKSUM true, BADSRC {BADSRC}, GOODDST {GOODDST}"
+    cfg = (f"FromDump(ip4.pcap, STOP true, TIMING false) -> Strip(14) -> ck :: CheckIPHeader({ck_args})"
+           " -> AggregateHash -> t :: Tee(2); t[0] -> ToIPSummaryDump(good.ipsum, FIELDS timestamp aggregate);"
+           " t[1] -> ToDump(good.pcap, ENCAP IP); ck[1] -> ToIPSummaryDump(bad.ipsum, FIELDS timestamp);")
+    click(CLICK, cfg, tmp)
+    good = read_ipsum(os.path.join(tmp, "good.ipsum"), 1)
+    bad = read_ipsum(os.path.join(tmp, "bad.ipsum"), 0)
+    dump = read_pcap(os.path.join(tmp, "good.pcap"))
+    assert len(good) + len(bad) == n, (len(good), len(bad), n)
+    reason = np.full(n, NOT_PINNED, np.uint8)
+    hsh = np.zeros(n, np.uint32)
+    length = np.zeros(n, np.uint16)
+    for i, row in good.items():
+        reason[i] = 6
+        hsh[i] = int(row[0])
+        length[i] = 14 + dump[i][0]
+    with cf.ThreadPoolExecutor(8) as ex:
+        for i, r in ex.map(reason_of_single, [(i, pcap, "Strip(14) -> ", ck_args) for i in sorted(bad)]):
+            reason[i] = r
+    # default CheckIPHeader (no CHECKSUM keyword) -> checksum NOT verified
+    cfgd = ("FromDump(ip4.pcap, STOP true, TIMING false) -> Strip(14) -> ck :: CheckIPHeader()"
+            " -> ToIPSummaryDump(gd.ipsum, FIELDS timestamp); ck[1] -> ToIPSummaryDump(bd.ipsum, FIELDS timestamp);")
+    click(CLICK, cfgd, tmp)
+    valid_default = np.zeros(n, np.uint8)
+    for i in read_ipsum(os.path.join(tmp, "gd.ipsum"), 0):
+        valid_default[i] = 1
+    # FlowSwitch LB_MODE hash, 16 outputs (fcbuild3: ctx + flow-dynamic). UDP only
+    # reaches the switch (CTXDispatcher rule 9/11); others: not pinned.
+    lb16 = np.full(n, NOT_PINNED, np.uint8)
+    lb16_order = []
+    if os.path.exists(CLICK3):
+        outs = " ".join(f"fs[{k}] -> ToIPSummaryDump(lb{k}.ipsum, FIELDS timestamp);" for k in range(16))
+        cfg3 = (f"FromDump(ip4.pcap, STOP true, TIMING false) -> Strip(14) -> CheckIPHeader({ck_args})"
+                " -> CTXManager(BUILDER 1, AGGCACHE false) -> CTXDispatcher(9/11 12/0/ffffffff:HASH-3"
+                " 16/0/ffffffff:HASH-3 20/0/ffffffff:HASH-3 0, - drop) -> fs :: FlowSwitch(LB_MODE hash); " + outs)
+        click(CLICK3, cfg3, tmp)
+        for k in range(16):
+            rows = read_ipsum(os.path.join(tmp, f"lb{k}.ipsum"), 0)
+            for i in rows:
+                lb16[i] = k
+            lb16_order.append(list(rows.keys()))
+    # HashSwitch(26, 8) on the unstripped frame behind CheckIPHeader(OFFSET 14)
+    hs = {}
+    for m in (4, 7):
+        outs = " ".join(f"hs[{k}] -> ToIPSummaryDump(hs{m}_{k}.ipsum, FIELDS timestamp);" for k in range(m))
+        cfgh = (f"FromDump(ip4.pcap, STOP true, TIMING false) -> CheckIPHeader(OFFSET 14, {ck_args})"
+                f" -> hs :: HashSwitch(26, 8); " + outs)
+        click(CLICK, cfgh, tmp)
+        arr = np.full(n, NOT_PINNED, np.uint8)
+        for k in range(m):
+            for i in read_ipsum(os.path.join(tmp, f"hs{m}_{k}.ipsum"), 0):
+                arr[i] = k
+        hs[m] = arr
+    return dict(reason=reason, hash=hsh, length=length, valid_default=valid_default, lb16=lb16,
+                hs4=hs[4], hs7=hs[7],
+                lb16_order=np.array([j for k in range(len(lb16_order)) for j in lb16_order[k]], np.uint32),
+                lb16_count=np.array([len(x) for x in lb16_order], np.uint32))
+
+
+def run_mix(b, tmp):
+    pcap = os.path.join(tmp, "mix.pcap")
+    write_pcap(pcap, b.frames())
+    n = b.n
+    cfg = ("FromDump(mix.pcap, STOP true, TIMING false) -> StripEtherVLANHeader(0) -> c :: Classifier(0/60%f0, -);"
+           " c[0] -> ck6 :: CheckIP6Header -> ToDump(good6.pcap, ENCAP IP); ck6[1] -> ToDump(bad6.pcap, ENCAP IP);"
+           " c[1] -> ck4 :: CheckIPHeader(CHECKSUM true) -> AggregateHash -> t :: Tee(2);"
+           " t[0] -> ToIPSummaryDump(good4.ipsum, FIELDS timestamp aggregate); t[1] -> ToDump(good4.pcap, ENCAP IP);"
+           " ck4[1] -> ToDump(bad4.pcap, ENCAP IP);")
+    click(CLICK, cfg, tmp)
+    good6 = read_pcap(os.path.join(tmp, "good6.pcap"))
+    bad6 = read_pcap(os.path.join(tmp, "bad6.pcap"))
+    good4 = read_ipsum(os.path.join(tmp, "good4.ipsum"), 1)
+    g4d = read_pcap(os.path.join(tmp, "good4.pcap"))
+    bad4 = read_pcap(os.path.join(tmp, "bad4.pcap"))
+    assert len(good6) + len(bad6) + len(good4) + len(bad4) == n
+    A = b.arena
+    off = b.desc[:, 0].astype(np.int64)
+    o = np.where(A[off + 12] == 0x81, 18, 14)
+    reason = np.full(n, NOT_PINNED, np.uint8)
+    length = np.zeros(n, np.uint16)
+    hsh = np.zeros(n, np.uint32)
+    ipver = np.zeros(n, np.uint8)
+    for i, (incl, _) in good6.items():
+        reason[i], ipver[i], length[i] = 6, 6, o[i] + incl
+    for i in bad6:
+        reason[i], ipver[i] = 7, 6
+    for i, row in good4.items():
+        reason[i], ipver[i], hsh[i], length[i] = 6, 4, int(row[0]), o[i] + g4d[i][0]
+    for i in bad4:
+        ipver[i] = 4       # reason: single-packet runs below
+    todo = sorted(bad4)
+    with tempfile.TemporaryDirectory() as d2:
+        # re-run each bad IPv4 packet alone for its reason (after the VLAN strip)
+        args = [(i, pcap, "StripEtherVLANHeader(0) -> ", "CHECKSUM true") for i in todo]
+        with cf.ThreadPoolExecutor(8) as ex:
+            for i, r in ex.map(reason_of_single, args):
+                reason[i] = r
+    # IP6FlowID hashes of valid IPv6 packets: reference harness (header-inline code)
+    h6idx = [i for i in good6]
+    if h6idx and os.path.exists(FCREF):
+        recs = b"".join(_h6_record(A, int(off[i]) + int(o[i])) for i in h6idx)
+        out = subprocess.run([FCREF, "flow6"], input=recs, capture_output=True, check=True).stdout
+        vals = np.frombuffer(out, np.uint32)
+        for i, v in zip(h6idx, vals):
+            hsh[i] = v
+    return dict(reason=reason, length=length, hash=hsh, ipver=ipver,
+                h6_pinned=np.array(bool(h6idx) and os.path.exists(FCREF)))
+
+
+def _h6_record(A, o):
+    th = o + 40
+    return (bytes(A[o + 8:o + 24]) + bytes(A[th:th + 2]) + bytes(A[o + 24:o + 40]) + bytes(A[th + 2:th + 4]))
+
+
+def run_kat(tmp):
+    """click_in_cksum on random buffers (odd lengths included) and IPFlowID /
+    IP6FlowID hashcodes on random tuples, from the reference harness."""
+    if not os.path.exists(FCREF):
+        return None
+    rng = np.random.default_rng(77)
+    lens = rng.integers(0, 80, 400)
+    bufs = [rng.integers(0, 256, int(k), dtype=np.uint8).tobytes() for k in lens]
+    rec = b"".join(struct.pack("<H", len(x)) + x for x in bufs)
+    ck = np.frombuffer(subprocess.run([FCREF, "cksum"], input=rec, capture_output=True, check=True).stdout,
+                       np.uint16)
+    t4 = rng.integers(0, 256, (2000, 12), dtype=np.uint8)
+    h4 = np.frombuffer(subprocess.run([FCREF, "flow4"], input=t4.tobytes(), capture_output=True,
+                                      check=True).stdout, np.uint32)
+    t6 = rng.integers(0, 256, (2000, 36), dtype=np.uint8)
+    t6[:64, 32:34] = 0   # sport % 16 == 0 cases (the ROT(v,0) corner)
+    t6[:64, 16:18] = rng.integers(0, 16, (64, 2)) * 16
+    h6 = np.frombuffer(subprocess.run([FCREF, "flow6"], input=t6.tobytes(), capture_output=True,
+                                      check=True).stdout, np.uint32)
+    blob = np.frombuffer(b"".join(bufs), np.uint8)
+    return dict(ck_lens=lens.astype(np.uint32), ck_blob=blob, ck=ck, t4=t4, h4=h4, t6=t6, h6=h6)
+
+
+def sha(path):
+    if not os.path.exists(path):
+        return None
+    return hashlib.sha256(open(path, "rb").read()).hexdigest()
+
+
+def main():
+    prov = dict(generator="tests/golden/gen_golden.py", click=CLICK, click_sha256=sha(CLICK),
+                click3=CLICK3, click3_sha256=sha(CLICK3), fcref=FCREF, fcref_sha256=sha(FCREF),
+                t0=T0, badsrc=BADSRC, gooddst=GOODDST, not_pinned=NOT_PINNED)
+    with tempfile.TemporaryDirectory() as tmp:
+        b, kind = make_ip4_set()
+        r = run_ip4(b, tmp)
+        np.savez_compressed(os.path.join(HERE, "ip4.npz"), arena=b.arena, desc=b.desc, kind=kind, **r)
+        print("ip4:", np.bincount(r["reason"], minlength=7), "lb16 pinned", int((r["lb16"] != 255).sum()))
+        m = make_mix_set()
+        rm = run_mix(m, tmp)
+        np.savez_compressed(os.path.join(HERE, "mix.npz"), arena=m.arena, desc=m.desc, **rm)
+        print("mix:", np.bincount(rm["reason"], minlength=8))
+        kat = run_kat(tmp)
+        if kat is not None:
+            np.savez_compressed(os.path.join(HERE, "kat.npz"), **kat)
+            print("kat: cksum", len(kat["ck"]), "h4", len(kat["h4"]), "h6", len(kat["h6"]))
+    prov["sets"] = {
+        "ip4": "CheckIPHeader(CHECKSUM true, BADSRC, GOODDST)/AggregateHash/FlowSwitch hash 16/HashSwitch(26,8)x{4,7}",
+        "mix": "StripEtherVLANHeader(0) -> Classifier(0/60%f0,-) -> CheckIP6Header | CheckIPHeader(CHECKSUM true) -> AggregateHash",
+        "kat": "fcref: click_in_cksum (lib/in_cksum.c), IPFlowID/IP6FlowID::hashcode (headers)",
+    }
+    with open(os.path.join(HERE, "PROVENANCE.json"), "w") as f:
+        json.dump(prov, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

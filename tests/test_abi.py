@@ -1,0 +1,62 @@
+"""The C-ABI libraries load on a CPU-only host and export every symbol that
+include/*.h declares (no compute calls: there is no GPU here)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from fastclick_amd import _native as N
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared(header):
+    src = open(os.path.join(ROOT, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(fc(?:gpu|click)_[a-z_0-9]+)\s*\(",
+                                 src, flags=re.M)))
+
+
+def test_fcgpu_exports_every_declared_symbol():
+    names = declared("fastclick_gpu.h")
+    assert len(names) >= 15
+    lib = N.load()
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(N.FCGPU_SYMBOLS), set(names) ^ set(N.FCGPU_SYMBOLS)
+    assert lib.fcgpu_abi_version() == N.ABI_VERSION
+
+
+def test_struct_layouts_match_header():
+    assert C.sizeof(N.fcgpu_anno) == 16
+    assert C.sizeof(N.fcgpu_out) == 5 * 8
+    # 12 u32 scalars + 2x16 u32 lists + nbad6 + 16x16 B
+    assert C.sizeof(N.fcgpu_cfg) == 4 * 12 + 4 * 32 + 4 + 256
+    lib = N.load()
+    cfg = N.fcgpu_cfg()
+    lib.fcgpu_default_cfg(C.byref(cfg))
+    assert cfg.size == C.sizeof(N.fcgpu_cfg)
+    assert cfg.checksum == 0          # CheckIPHeader default: CHECKSUM false
+    assert cfg.native_vlan == 0 and cfg.nbad6 == 1 and bytes(cfg.bad6[0]) == b"\xff" * 16
+
+
+def test_open_without_device_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    lib = N.load()
+    h = C.c_void_p()
+    rc = lib.fcgpu_open(0, 1024, C.byref(h))
+    assert rc == N.ENODEV
+    assert b"no HIP device" in lib.fcgpu_last_error(None)
+
+
+def test_fcclick_exports_every_declared_symbol():
+    if not os.path.exists(os.path.join(ROOT, "include", "fcclick.h")):
+        pytest.skip("no host harness header")
+    from fastclick_amd import click as K
+    names = declared("fcclick.h")
+    lib = K.load()
+    for n in names:
+        assert hasattr(lib, n), n
