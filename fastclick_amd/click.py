@@ -1,0 +1,101 @@
+"""ctypes binding of the Click-shaped host harness (include/fcclick.h).
+
+    run_element("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16)", batch,
+                burst=32, nsinks=17)
+
+pushes the batch through the element in BURST-packet PacketBatches and returns,
+per input packet, the output it left on, its departure order and its
+annotations -- the observable behaviour a Click graph sees.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _native as N
+
+_lib = None
+
+
+class fcclick_result(C.Structure):
+    _fields_ = [("out_port", C.c_void_p), ("out_seq", C.c_void_p), ("out_agg", C.c_void_p),
+                ("out_dst", C.c_void_p), ("out_len", C.c_void_p), ("out_nh", C.c_void_p),
+                ("out_batches", C.c_void_p), ("handlers", C.c_char_p), ("handlers_cap", C.c_size_t)]
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    N.load()   # libfcgpu.so first (same HIP runtime as torch), then the harness
+    if not os.path.exists(N.LIBFCCLICK):
+        raise N.NativeMissing(f"{N.LIBFCCLICK} not built (run __graft_entry__.build())")
+    lib = C.CDLL(N.LIBFCCLICK)
+    lib.fcclick_check_config.restype = C.c_int
+    lib.fcclick_check_config.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t]
+    lib.fcclick_run.restype = C.c_int
+    lib.fcclick_run.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                C.POINTER(fcclick_result), C.c_char_p, C.c_size_t]
+    lib.fcclick_bench.restype = C.c_int
+    lib.fcclick_bench.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                  C.POINTER(C.c_double), C.c_char_p, C.c_size_t]
+    _lib = lib
+    return lib
+
+
+class ConfigError(ValueError):
+    pass
+
+
+def check_config(conf: str):
+    lib = load()
+    err = C.create_string_buffer(512)
+    if lib.fcclick_check_config(conf.encode(), err, 512) != 0:
+        raise ConfigError(err.value.decode())
+
+
+def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1):
+    lib = load()
+    n = batch.n
+    arena = np.ascontiguousarray(batch.arena)
+    desc = np.ascontiguousarray(batch.desc, dtype=np.uint32)
+    out = {k: np.zeros(n, dt) for k, dt in (("port", np.uint32), ("seq", np.uint32), ("agg", np.uint32),
+                                            ("dst", np.uint32), ("len", np.uint32), ("nh", np.int32))}
+    nb = np.zeros(1, np.uint32)
+    hbuf = C.create_string_buffer(4096)
+    res = fcclick_result(out["port"].ctypes.data, out["seq"].ctypes.data, out["agg"].ctypes.data,
+                         out["dst"].ctypes.data, out["len"].ctypes.data, out["nh"].ctypes.data,
+                         nb.ctypes.data, C.cast(hbuf, C.c_char_p), 4096)
+    err = C.create_string_buffer(512)
+    rc = lib.fcclick_run(conf.encode(), arena.ctypes.data, desc.ctypes.data, n, burst, nsinks,
+                         C.byref(res), err, 512)
+    if rc == -1:
+        raise ConfigError(err.value.decode())
+    if rc != 0:
+        raise RuntimeError(f"element runtime error: {err.value.decode()}")
+    handlers = {}
+    name = None
+    for line in hbuf.value.decode().splitlines():
+        if "=" in line and line.split("=", 1)[0] in ("count", "drops", "drop_details", "port_counts", "error"):
+            name, val = line.split("=", 1)
+            handlers[name] = val
+        elif name is not None:
+            handlers[name] += "\n" + line
+    out["batches"] = int(nb[0])
+    out["handlers"] = handlers
+    return out
+
+
+def bench_element(conf: str, batch, *, burst: int = 32, reps: int = 5) -> float:
+    lib = load()
+    arena = np.ascontiguousarray(batch.arena)
+    desc = np.ascontiguousarray(batch.desc, dtype=np.uint32)
+    pps = C.c_double()
+    err = C.create_string_buffer(512)
+    rc = lib.fcclick_bench(conf.encode(), arena.ctypes.data, desc.ctypes.data, batch.n, burst, reps,
+                           C.byref(pps), err, 512)
+    if rc != 0:
+        raise RuntimeError(err.value.decode())
+    return pps.value

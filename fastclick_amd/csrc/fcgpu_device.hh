@@ -206,6 +206,7 @@ __device__ __forceinline__ void process_packet(const DevCfg &c, const FrameView 
             r.port = c.nports;
             return;
         }
+        an.nh = (uint8_t)o;                       // the pull() StripEtherVLANHeader did
         v6 = ((int)(len - o) >= 1) && ((f.rd8(o) >> 4) == 6);
         r.reason = v6 ? check_ip6(c, f, len, o, an) : check_ip4<CK>(c, f, len, o, h, an);
     } else if (CM == FCGPU_MARK_IP4) {

@@ -1,0 +1,204 @@
+// fcclick_capi.cc -- C ABI of the host harness (include/fcclick.h).
+#include <chrono>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../../include/fcclick.h"
+#include "click_model.hh"
+#include "gpu_element.hh"
+
+using namespace fcx;
+
+namespace {
+
+// Records every packet that leaves the element on one output, then frees it.
+class Sink : public Element {
+  public:
+    Sink(int port, fcclick_result *r, uint32_t *seq, uint32_t *nbatch)
+        : _port(port), _r(r), _seq(seq), _nbatch(nbatch) {}
+    const char *class_name() const override { return "Sink"; }
+    int configure(const std::vector<std::string> &, std::string &) override { return 0; }
+    void push_batch(int, PacketBatch *b) override {
+        ++*_nbatch;
+        unsigned cnt = 0;
+        for (Packet *p = b->first(); p;) {
+            Packet *nx = p->next();
+            const uint32_t i = p->id;
+            if (_r) {
+                if (_r->out_port) _r->out_port[i] = (uint32_t)_port;
+                if (_r->out_seq) _r->out_seq[i] = (*_seq);
+                if (_r->out_agg) _r->out_agg[i] = p->anno_u32(AGGREGATE_ANNO_OFFSET);
+                if (_r->out_dst) _r->out_dst[i] = p->anno_u32(DST_IP_ANNO_OFFSET);
+                if (_r->out_len) _r->out_len[i] = p->length();
+                if (_r->out_nh) _r->out_nh[i] = p->network_header_offset();
+            }
+            ++*_seq;
+            ++cnt;
+            p->kill();
+            p = nx;
+        }
+        if (cnt != b->count()) fprintf(stderr, "Sink: batch count %u != linked %u\n", b->count(), cnt);
+    }
+
+  private:
+    int _port;
+    fcclick_result *_r;
+    uint32_t *_seq, *_nbatch;
+};
+
+bool parse_element(const char *conf, std::string &cls, std::vector<std::string> &args, std::string &err) {
+    std::string s = trim(conf ? conf : "");
+    size_t lp = s.find('(');
+    if (lp == std::string::npos) {
+        cls = s;
+        return !cls.empty();
+    }
+    if (s.back() != ')') {
+        err = "syntax error: expected ')'";
+        return false;
+    }
+    cls = trim(s.substr(0, lp));
+    args = split_conf(s.substr(lp + 1, s.size() - lp - 2));
+    return true;
+}
+
+std::unique_ptr<Element> make_element(const char *conf, std::string &err) {
+    std::string cls;
+    std::vector<std::string> args;
+    if (!parse_element(conf, cls, args, err)) {
+        if (err.empty()) err = "empty configuration";
+        return nullptr;
+    }
+    std::unique_ptr<Element> e;
+    if (cls == "GPUIPCheckClassify") e.reset(new GPUIPCheckClassify());
+    else {
+        err = "unknown element class '" + cls + "'";
+        return nullptr;
+    }
+    if (e->configure(args, err) < 0) return nullptr;
+    return e;
+}
+
+void copy_err(const std::string &m, char *err, size_t cap) {
+    if (err && cap) {
+        snprintf(err, cap, "%s", m.c_str());
+    }
+}
+
+uint32_t max_len(const uint32_t *desc, uint32_t n) {
+    uint32_t m = 64;
+    for (uint32_t i = 0; i < n; ++i) m = desc[2 * i + 1] > m ? desc[2 * i + 1] : m;
+    return m;
+}
+
+}  // namespace
+
+extern "C" int fcclick_check_config(const char *conf, char *err, size_t errcap) {
+    std::string e;
+    auto el = make_element(conf, e);
+    if (!el) {
+        copy_err(e, err, errcap);
+        return -1;
+    }
+    return 0;
+}
+
+extern "C" int fcclick_run(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                           uint32_t burst, uint32_t nsinks, fcclick_result *res, char *err, size_t errcap) {
+    std::string e;
+    auto el = make_element(conf, e);
+    if (!el || el->initialize(e) < 0) {
+        copy_err(e, err, errcap);
+        return -1;
+    }
+    if (burst == 0) burst = 32;
+    uint32_t seq = 0, nbatch = 0;
+    if (res) {
+        for (uint32_t i = 0; i < n; ++i) {
+            if (res->out_port) res->out_port[i] = 0xffffffffu;
+            if (res->out_seq) res->out_seq[i] = 0xffffffffu;
+        }
+    }
+    std::vector<std::unique_ptr<Sink>> sinks;
+    for (uint32_t k = 0; k < nsinks; ++k) {
+        sinks.emplace_back(new Sink((int)k, res, &seq, &nbatch));
+        el->connect_output((int)k, sinks.back().get(), 0);
+    }
+    const uint32_t headroom = 128;
+    PacketPool pool(n ? n : 1, headroom + max_len(desc, n) + 64, headroom);
+    // FromDPDKDevice-style source: BURST packets per PacketBatch
+    for (uint32_t i = 0; i < n; i += burst) {
+        uint32_t m = n - i < burst ? n - i : burst;
+        Packet *head = nullptr, *prev = nullptr;
+        for (uint32_t j = 0; j < m; ++j) {
+            Packet *p = pool.make(arena + desc[2 * (i + j)], desc[2 * (i + j) + 1]);
+            p->id = i + j;
+            if (prev) prev->set_next(p);
+            else head = p;
+            prev = p;
+        }
+        el->push_batch(0, PacketBatch::make_from_list(head, prev, m));
+    }
+    el->flush();
+    if (res) {
+        if (res->out_batches) *res->out_batches = nbatch;
+        if (res->handlers && res->handlers_cap) {
+            std::string h;
+            for (const char *name : {"count", "drops", "drop_details", "port_counts", "error"})
+                h += std::string(name) + "=" + el->read_handler(name) + "\n";
+            snprintf(res->handlers, res->handlers_cap, "%s", h.c_str());
+        }
+    }
+    std::string er = el->read_handler("error");
+    if (!er.empty()) {
+        copy_err(er, err, errcap);
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int fcclick_bench(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                             uint32_t burst, uint32_t reps, double *pps, char *err, size_t errcap) {
+    std::string e;
+    auto el = make_element(conf, e);
+    if (!el || el->initialize(e) < 0) {
+        copy_err(e, err, errcap);
+        return -1;
+    }
+    if (burst == 0) burst = 32;
+    uint32_t seq = 0, nbatch = 0;
+    std::vector<std::unique_ptr<Sink>> sinks;
+    for (uint32_t k = 0; k < 65; ++k) {
+        sinks.emplace_back(new Sink((int)k, nullptr, &seq, &nbatch));
+        el->connect_output((int)k, sinks.back().get(), 0);
+    }
+    const uint32_t headroom = 128;
+    PacketPool pool(n, headroom + max_len(desc, n) + 64, headroom);
+    auto one = [&]() {
+        for (uint32_t i = 0; i < n; i += burst) {
+            uint32_t m = n - i < burst ? n - i : burst;
+            Packet *head = nullptr, *prev = nullptr;
+            for (uint32_t j = 0; j < m; ++j) {
+                Packet *p = pool.make(arena + desc[2 * (i + j)], desc[2 * (i + j) + 1]);
+                if (prev) prev->set_next(p);
+                else head = p;
+                prev = p;
+            }
+            el->push_batch(0, PacketBatch::make_from_list(head, prev, m));
+        }
+        el->flush();
+    };
+    one();   // warm-up (allocations, first launch)
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t r = 0; r < reps; ++r) one();
+    auto t1 = std::chrono::steady_clock::now();
+    double s = std::chrono::duration<double>(t1 - t0).count();
+    if (pps) *pps = (double)n * reps / s;
+    std::string er = el->read_handler("error");
+    if (!er.empty()) {
+        copy_err(er, err, errcap);
+        return -2;
+    }
+    return 0;
+}

@@ -1,0 +1,270 @@
+// gpu_element.hh -- GPUIPCheckClassify: the drop-in BatchElement.
+//
+// Replaces the CPU chain
+//     [Strip(14) | StripEtherVLANHeader] -> CheckIPHeader / CheckIP6Header
+//         -> AggregateHash -> FlowSwitch(LB_MODE hash) | HashSwitch   (=> N outputs)
+// with one element whose push_batch gathers the batch, runs it through the
+// MI355X kernels (C ABI, include/fastclick_gpu.h) and pushes one PacketBatch per
+// output, packets in input order within each output (CLASSIFY_EACH_PACKET,
+// include/click/packetbatch.hh:259-307). Invalid packets leave on output N
+// when it exists, else are killed (CheckIPHeader::drop, checkipheader.cc:143-161).
+//
+// Keyword arguments mirror the replaced elements:
+//   OFFSET, CHECKSUM (default FALSE: checkipheader.cc:110), BADSRC, GOODDST,
+//   VERBOSE, DETAILS                         -- CheckIPHeader
+//   NATIVE_VLAN (default 0)                  -- StripEtherVLANHeader
+//   BADADDRS                                 -- CheckIP6Header (IPv6, MODE AUTO)
+//   N / LB_MODE hash|hash_agg|hash_ip        -- FlowSwitch / LoadBalancer
+//   HASHSWITCH "OFFSET LENGTH"               -- HashSwitch
+//   MODE CHECK|MARK|AUTO, HASH NONE|FLOWID|FLOW5ID, STRIP, BATCH, DEVICE
+// Handlers: count, drops, drop_details (DETAILS true), port_counts.
+//
+// Packets are parked until BATCH packets are staged (MinBatch pattern,
+// elements/standard/minbatch.cc:57-76) or flush() is called. GPU/runtime
+// errors are reported, never papered over: the staged packets are killed and
+// the error is returned through the `error` handler.
+#pragma once
+#include <vector>
+#include <string>
+#include <sstream>
+#include <inttypes.h>
+
+#include "click_model.hh"
+#include "../../../include/fastclick_gpu.h"
+
+namespace fcx {
+
+class GPUIPCheckClassify : public Element {
+  public:
+    GPUIPCheckClassify() { fcgpu_default_cfg(&_cfg); }
+    ~GPUIPCheckClassify() override { if (_ctx) fcgpu_close(_ctx); }
+
+    const char *class_name() const override { return "GPUIPCheckClassify"; }
+
+    int configure(const std::vector<std::string> &conf, std::string &errh) override {
+        fcgpu_default_cfg(&_cfg);
+        _cfg.checksum = 0;
+        bool strip_set = false;
+        for (const auto &raw : conf) {
+            ConfArg a = parse_arg(raw);
+            const std::string &k = a.key, &v = a.value;
+            long n;
+            bool b;
+            if (k == "OFFSET") {
+                if (!parse_int(v, n) || n < 0 || n > 255) return err(errh, "OFFSET expects an integer in [0,255]");
+                _cfg.offset = (int32_t)n;
+            } else if (k == "CHECKSUM") {
+                if (!parse_bool(v, b)) return err(errh, "CHECKSUM expects true/false");
+                _cfg.checksum = b;
+            } else if (k == "VERBOSE") {
+                if (!parse_bool(v, _verbose)) return err(errh, "VERBOSE expects true/false");
+            } else if (k == "DETAILS") {
+                if (!parse_bool(v, _details)) return err(errh, "DETAILS expects true/false");
+            } else if (k == "BADSRC" || k == "GOODDST") {
+                std::istringstream ss(v);
+                std::string w;
+                uint32_t *dst = k == "BADSRC" ? _cfg.badsrc : _cfg.gooddst;
+                uint32_t &cnt = k == "BADSRC" ? _cfg.nbadsrc : _cfg.ngooddst;
+                cnt = 0;
+                while (ss >> w) {
+                    uint32_t ip;
+                    if (!parse_ip4(w, ip)) return err(errh, k + " expects IP addresses");
+                    if (cnt >= FCGPU_MAX_ADDRS) return err(errh, k + ": too many addresses");
+                    dst[cnt++] = ip;
+                }
+            } else if (k == "NATIVE_VLAN") {
+                if (!parse_int(v, n) || n > 0xFFF) return err(errh, "bad NATIVE_VLAN");
+                _cfg.native_vlan = n >= 0 ? (int32_t)n : -1;
+            } else if (k == "N" || k == "NPORTS") {
+                if (!parse_int(v, n) || n < 1 || n > FCGPU_MAX_PORTS) return err(errh, "N out of range");
+                _cfg.nports = (uint32_t)n;
+                if (_cfg.classify == FCGPU_CLS_NONE) _cfg.classify = FCGPU_CLS_LB_HASH;
+            } else if (k == "LB_MODE") {
+                if (v == "hash" || v == "hash_agg") _cfg.classify = FCGPU_CLS_LB_HASH;
+                else if (v == "hash_ip") _cfg.classify = FCGPU_CLS_HASH_IP;
+                else return err(errh, "unsupported LB_MODE " + v);
+            } else if (k == "HASHSWITCH") {
+                long o, l;
+                std::istringstream ss(v);
+                std::string a1, a2;
+                ss >> a1 >> a2;
+                if (!parse_int(a1, o) || !parse_int(a2, l) || l <= 0 || o < 0)
+                    return err(errh, "HASHSWITCH expects OFFSET LENGTH (length must be > 0)");
+                _cfg.classify = FCGPU_CLS_HASHSWITCH;
+                _cfg.hs_offset = (int32_t)o;
+                _cfg.hs_length = (int32_t)l;
+            } else if (k == "MODE") {
+                if (v == "CHECK") _cfg.check_mode = FCGPU_CHECK_IP4;
+                else if (v == "MARK") _cfg.check_mode = FCGPU_MARK_IP4;
+                else if (v == "AUTO") _cfg.check_mode = FCGPU_CHECK_AUTO;
+                else return err(errh, "MODE expects CHECK, MARK or AUTO");
+            } else if (k == "HASH") {
+                if (v == "NONE") _cfg.hash_mode = FCGPU_HASH_NONE;
+                else if (v == "FLOWID") _cfg.hash_mode = FCGPU_HASH_FLOWID;
+                else if (v == "FLOW5ID") _cfg.hash_mode = FCGPU_HASH_FLOW5ID;
+                else return err(errh, "HASH expects NONE, FLOWID or FLOW5ID");
+            } else if (k == "STRIP") {
+                if (!parse_bool(v, _strip)) return err(errh, "STRIP expects true/false");
+                strip_set = true;
+            } else if (k == "BATCH") {
+                if (!parse_int(v, n) || n < 0 || n > (1L << 26)) return err(errh, "bad BATCH");
+                _batch = (uint32_t)n;
+            } else if (k == "DEVICE") {
+                if (!parse_int(v, n) || n < 0) return err(errh, "bad DEVICE");
+                _device = (int)n;
+            } else if (k == "BADADDRS") {
+                return err(errh, "BADADDRS: only the default IPv6 bad source (ff..ff) is supported");
+            } else if (k.empty()) {
+                return err(errh, "too many arguments");        // Args::complete(): OFFSET is keyword-only
+            } else {
+                return err(errh, "unknown keyword " + k);
+            }
+        }
+        if (!strip_set) _strip = (_cfg.check_mode == FCGPU_CHECK_AUTO);
+        return 0;
+    }
+
+    int initialize(std::string &errh) override {
+        uint32_t cap = _batch ? _batch : 65536;
+        _cap = cap + 8192;   // a burst may overshoot BATCH
+        int rc = fcgpu_open(_device, _cap, &_ctx);
+        if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_open: ") + fcgpu_last_error(nullptr));
+        rc = fcgpu_configure(_ctx, &_cfg);
+        if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_configure: ") + fcgpu_last_error(_ctx));
+        _pkts.reserve(_cap);
+        _frames.reserve(_cap);
+        _lens.reserve(_cap);
+        _verdict.resize(_cap);
+        _hash.resize(_cap);
+        _anno.resize(_cap);
+        _perm.resize(_cap);
+        _start.resize(FCGPU_MAX_PORTS + 2);
+        return 0;
+    }
+
+    void push_batch(int, PacketBatch *batch) override {
+        for (Packet *p = batch->first(); p; p = p->next()) {
+            if (_pkts.size() == _cap) process_staged();
+            _pkts.push_back(p);
+        }
+        if (_pkts.size() >= (_batch ? _batch : 1)) process_staged();
+    }
+
+    void flush() override {
+        if (!_pkts.empty()) process_staged();
+    }
+
+    std::string read_handler(const std::string &h) override {
+        uint64_t c[FCGPU_NCOUNTERS] = {0};
+        if (_ctx) fcgpu_read_counters(_ctx, c, FCGPU_NCOUNTERS);
+        std::ostringstream s;
+        if (h == "count") s << c[FCGPU_CTR_COUNT];
+        else if (h == "drops") s << c[FCGPU_CTR_DROPS];
+        else if (h == "drop_details" && _details) {
+            // checkipheader.cc:247-256 format
+            static const char *texts[6] = {"tiny packet", "bad IPv4 version", "bad IPv4 header length",
+                                           "bad IPv4 length", "bad IPv4 checksum", "bad source address"};
+            char line[96];
+            for (int i = 0; i < 6; ++i) {
+                snprintf(line, sizeof line, "%15" PRIu64 " packets due to: %24s\n", c[FCGPU_CTR_REASON + i], texts[i]);
+                s << line;
+            }
+        } else if (h == "port_counts") {
+            for (uint32_t p = 0; p <= _cfg.nports; ++p) s << (p ? " " : "") << c[FCGPU_CTR_PORT + p];
+        } else if (h == "error") s << _error;
+        return s.str();
+    }
+
+  private:
+    int err(std::string &errh, const std::string &m) {
+        errh = std::string(class_name()) + ": " + m;
+        return -1;
+    }
+
+    void process_staged() {
+        const uint32_t n = (uint32_t)_pkts.size();
+        _frames.resize(n);
+        _lens.resize(n);
+        for (uint32_t i = 0; i < n; ++i) {
+            _frames[i] = _pkts[i]->data();
+            _lens[i] = _pkts[i]->length();
+        }
+        fcgpu_out o;
+        o.verdict = _verdict.data();
+        o.hash = _hash.data();
+        o.anno = _anno.data();
+        o.perm = _perm.data();
+        o.port_start = _start.data();
+        int rc = fcgpu_process_host(_ctx, _frames.data(), _lens.data(), n, &o);
+        if (rc != FCGPU_OK) {
+            // no CPU fallback: report, drop the staged packets, keep running
+            _error = fcgpu_last_error(_ctx);
+            fprintf(stderr, "%s: GPU processing failed: %s\n", class_name(), _error.c_str());
+            for (Packet *p : _pkts) p->kill();
+            _pkts.clear();
+            return;
+        }
+        const bool hashing = _cfg.hash_mode != FCGPU_HASH_NONE;
+        const bool autom = _cfg.check_mode == FCGPU_CHECK_AUTO;
+        for (uint32_t i = 0; i < n; ++i) {
+            Packet *p = _pkts[i];
+            const fcgpu_anno &a = _anno[i];
+            const uint32_t reason = _verdict[i] & 0xff;
+            if (autom && reason != FCGPU_R_VLAN_REJECT)
+                p->set_anno_u16(VLAN_TCI_ANNO_OFFSET, a.vlan_tci);    // StripEtherVLANHeader
+            if (reason == FCGPU_R_OK) {
+                p->set_network_header(a.nh, a.th);                     // set_ip_header / set_ip6_header
+                if (a.length < p->length()) p->take(p->length() - a.length);
+                if (a.ipver == 6) p->set_anno_u8(IP6_NXT_ANNO_OFFSET, a.ip6_nxt);
+                else p->set_anno_u32(DST_IP_ANNO_OFFSET, a.dst_ip);
+                if (hashing) p->set_anno_u32(AGGREGATE_ANNO_OFFSET, _hash[i]);   // AggregateHash
+                if (_strip) p->pull(a.nh);
+            } else {
+                if (!_warned || _verbose) {
+                    fprintf(stderr, "%s: IP header check failed: reason %u\n", class_name(), reason);
+                    _warned = true;
+                }
+                // the replaced Strip / StripEtherVLANHeader ran before the checker
+                if (_strip && reason != FCGPU_R_VLAN_REJECT) p->pull(autom ? a.nh : (uint32_t)_cfg.offset);
+            }
+        }
+        // one batch per output in port order, input order within a port
+        // (chunked to MAX_BATCH_SIZE, include/click/packetbatch.hh:416)
+        const uint32_t nb = _cfg.nports + 1;
+        for (uint32_t port = 0; port < nb; ++port) {
+            uint32_t s = _start[port], e = _start[port + 1];
+            while (s < e) {
+                uint32_t m = e - s < kMaxBatch ? e - s : kMaxBatch;
+                Packet *head = _pkts[_perm[s]], *prev = head;
+                for (uint32_t j = 1; j < m; ++j) {
+                    Packet *q = _pkts[_perm[s + j]];
+                    prev->set_next(q);
+                    prev = q;
+                }
+                PacketBatch *b = PacketBatch::make_from_list(head, prev, m);
+                checked_output_push_batch((int)port, b);
+                s += m;
+            }
+        }
+        _pkts.clear();
+    }
+
+    static constexpr uint32_t kMaxBatch = 8192;
+    fcgpu_cfg _cfg;
+    fcgpu_ctx *_ctx = nullptr;
+    int _device = 0;
+    uint32_t _batch = 0;      // 0: process every incoming batch immediately
+    uint32_t _cap = 0;
+    bool _verbose = false, _details = false, _strip = false, _warned = false;
+    std::string _error;
+    std::vector<Packet *> _pkts;
+    std::vector<const uint8_t *> _frames;
+    std::vector<uint32_t> _lens;
+    std::vector<uint16_t> _verdict;
+    std::vector<uint32_t> _hash;
+    std::vector<fcgpu_anno> _anno;
+    std::vector<uint32_t> _perm;
+    std::vector<uint32_t> _start;
+};
+
+}  // namespace fcx

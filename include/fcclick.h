@@ -1,0 +1,54 @@
+/*
+ * fcclick.h -- C ABI of the Click-shaped host harness (libfcclick.so).
+ *
+ * Drives the GPUIPCheckClassify BatchElement (fastclick_amd/csrc/host/
+ * gpu_element.hh) the way FastClick drives an element behind FromDPDKDevice:
+ * a source pushes PacketBatches of BURST packets (FromDPDKDevice BURST 32,
+ * elements/userlevel/fromdpdkdevice.cc:124) into Element::push_batch
+ * (include/click/element.hh:53-54); every output port feeds a sink that
+ * records what left on it, in order. This is how the element is tested and
+ * how the end-to-end host-resident rate is measured.
+ */
+#ifndef FCCLICK_H
+#define FCCLICK_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Parse/validate an element configuration such as
+ *   "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash)"
+ * without touching a GPU. Returns 0, or -1 with the message in err. */
+int fcclick_check_config(const char *conf, char *err, size_t errcap);
+
+typedef struct fcclick_result {
+    uint32_t *out_port;     /* [n] output the packet left on; 0xffffffff = killed        */
+    uint32_t *out_seq;      /* [n] global departure order (0..), 0xffffffff = killed     */
+    uint32_t *out_agg;      /* [n] AGGREGATE_ANNO (anno u32 @20) on departure            */
+    uint32_t *out_dst;      /* [n] DST_IP_ANNO (anno u32 @0)                              */
+    uint32_t *out_len;      /* [n] packet length on departure                            */
+    int32_t  *out_nh;       /* [n] network header offset from data() (-1 unset)          */
+    uint32_t *out_batches;  /* [1] number of PacketBatches the sinks received             */
+    char     *handlers;     /* "name=value\n" for count, drops, drop_details, port_counts */
+    size_t    handlers_cap;
+} fcclick_result;
+
+/* Run a graph  Source(frames, BURST) -> conf => [0 .. nsinks-1] Sink  over n
+ * frames (arena + (offset, length) descriptors, host memory), then flush.
+ * Returns 0 on success, -1 on configuration/initialisation error (message in
+ * err), -2 when the element reported a GPU runtime error. */
+int fcclick_run(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                uint32_t burst, uint32_t nsinks, fcclick_result *res, char *err, size_t errcap);
+
+/* Host-resident rate: repeat the same run `reps` times (packets recycled into
+ * the pool, sinks discard), return packets per second through the element
+ * including gather, PCIe copies, kernels and relinking. */
+int fcclick_bench(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                  uint32_t burst, uint32_t reps, double *pps, char *err, size_t errcap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

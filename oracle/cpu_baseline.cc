@@ -1,0 +1,313 @@
+// cpu_baseline.cc -- TEST INFRASTRUCTURE ONLY: the reported CPU baseline.
+//
+// Scalar restatement of the reference CPU pipeline the GPU element replaces,
+// run the way FastClick runs it:
+//   ReplayUnqueue-style source (preloaded trace, BURST 32 linked-list
+//   PacketBatches) -> Strip(14) -> CheckIPHeader(CHECKSUM true)
+//   -> AggregateHash -> FlowSwitch LB_MODE hash (16 outputs, CLASSIFY_EACH_PACKET)
+//   -> Discard (packets recycled)
+// Per-element atomic counters as CheckIPHeader's atomic_uint64_t _count
+// (checkipheader.hh:160-162); one independent pipeline per thread, like
+// `click -j N` with StaticThreadSched. Packet semantics from
+// fastclick_amd/csrc/host/click_model.hh; per-packet functions from the C
+// oracle (fc_oracle.c). Only bench.py's cpu_baseline leg and tests run this.
+//
+//   fc_cpu_baseline --seconds S --threads T [--flows K]   -> one JSON line
+//   fc_cpu_baseline --verify                              -> exit 0 if the
+//       pipeline matches fco_process_batch on a batch with injected errors
+#include <atomic>
+#include <chrono>
+#include <thread>
+#include <vector>
+#include <string>
+#include <string.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "fc_oracle.h"
+#include "../fastclick_amd/csrc/host/click_model.hh"
+
+using namespace fcx;
+
+namespace {
+
+inline uint32_t le32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+inline uint16_t raw16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
+
+struct Pipeline {
+    // CheckIPHeader state
+    std::atomic<uint64_t> count{0}, drops{0};
+    std::atomic<uint64_t> reason_drops[6];
+    uint64_t port_count[17] = {0};
+    std::vector<uint32_t> *record_port = nullptr;   // verify mode: per-packet port
+    std::vector<uint32_t> *record_hash = nullptr;
+    int stages = 3;    // 0: Strip only (harness floor), 1: Strip+CheckIPHeader, 2: +AggregateHash, 3: +FlowSwitch classify
+    Pipeline() { for (auto &r : reason_drops) r = 0; }
+
+    // Strip::simple_action_batch (elements/standard/strip.cc:38-50)
+    void strip(PacketBatch *b) {
+        for (Packet *p = b->first(); p; p = p->next()) p->pull(14);
+    }
+
+    // CheckIPHeader::valid (elements/ip/checkipheader.cc:163-226), CHECKSUM true
+    int valid(Packet *p) {
+        unsigned plen = p->length();
+        if ((int)plen < 20) return 0;
+        const uint8_t *ip = p->data();
+        if ((ip[0] >> 4) != 4) return 1;
+        unsigned hlen = (unsigned)(ip[0] & 15) << 2;
+        if (hlen < 20) return 2;
+        unsigned len = ((unsigned)ip[2] << 8) | ip[3];
+        if (len > plen || len < hlen) return 3;
+        if (fco_in_cksum(ip, (int)hlen) != 0) return 4;
+        p->set_network_header(0, (int)hlen);
+        if (plen > len) p->take(plen - len);
+        p->set_anno_u32(DST_IP_ANNO_OFFSET, le32(ip + 16));
+        count++;
+        return 6;
+    }
+
+    // EXECUTE_FOR_EACH_PACKET_DROPPABLE (include/click/packetbatch.hh:111-142)
+    PacketBatch *check(PacketBatch *b) {
+        Packet *last = nullptr, *p = b->first();
+        PacketBatch *head = b;
+        unsigned cnt = b->count();
+        while (p) {
+            Packet *nx = p->next();
+            int r = valid(p);
+            if (r != 6) {
+                drops++;
+                reason_drops[r]++;
+                if (record_port) (*record_port)[p->id] = 16;
+                p->kill();
+                if (last) last->set_next(nx);
+                else head = nx ? PacketBatch::start_head(nx) : nullptr;
+                cnt--;
+            } else {
+                last = p;
+            }
+            p = nx;
+        }
+        if (head) {
+            head->set_count(cnt);
+            head->set_tail(last);
+            last->set_next(nullptr);
+        }
+        return head;
+    }
+
+    // AggregateHash::simple_action (elements/analysis/aggregatehash.cc:49-55)
+    void aggregate(PacketBatch *b) {
+        for (Packet *p = b->first(); p; p = p->next()) {
+            const uint8_t *nh = p->network_header(), *th = p->transport_header();
+            uint32_t h = 0;
+            if (((((unsigned)nh[6] << 8) | nh[7]) & 0x1fff) == 0)
+                h = fco_ipflowid_hash(le32(nh + 12), raw16(th), le32(nh + 16), raw16(th + 2));
+            p->set_anno_u32(AGGREGATE_ANNO_OFFSET, h);
+        }
+    }
+
+    // FlowSwitch LB_MODE hash_agg port + CLASSIFY_EACH_PACKET into 17 lists
+    void classify(PacketBatch *b) {
+        PacketBatch *out[17] = {nullptr};
+        Packet *p = b->first();
+        while (p) {
+            Packet *nx = p->next();
+            int o = fco_lb_hash_port(p->anno_u32(AGGREGATE_ANNO_OFFSET), 16);
+            if (record_port) {
+                (*record_port)[p->id] = (uint32_t)o;
+                (*record_hash)[p->id] = p->anno_u32(AGGREGATE_ANNO_OFFSET);
+            }
+            if (!out[o]) {
+                out[o] = PacketBatch::start_head(p);
+                out[o]->set_count(1);
+                out[o]->set_tail(p);
+            } else {
+                out[o]->append_packet(p);
+            }
+            p = nx;
+        }
+        for (int i = 0; i < 17; ++i)
+            if (out[i]) {
+                out[i]->tail()->set_next(nullptr);
+                port_count[i] += out[i]->count();
+                out[i]->kill();          // Discard::push_batch -> fast_kill
+            }
+    }
+
+    void push_batch(PacketBatch *b) {
+        strip(b);
+        if (stages == 0) { b->kill(); return; }
+        b = check(b);
+        if (!b) return;
+        if (stages >= 2) aggregate(b);
+        if (stages >= 3) classify(b);
+        else b->kill();
+    }
+};
+
+// preloaded trace -> BURST-packet batches from a packet pool (ReplayUnqueue)
+struct Replay {
+    const uint8_t *arena;
+    const uint32_t *desc;
+    uint32_t n, pos = 0;
+    PacketPool pool;
+    Replay(const uint8_t *a, const uint32_t *d, uint32_t n_, uint32_t maxlen)
+        : arena(a), desc(d), n(n_), pool(4096, 128 + maxlen + 64, 128) {}
+    PacketBatch *next(uint32_t burst) {
+        Packet *head = nullptr, *prev = nullptr;
+        uint32_t m = 0;
+        for (; m < burst; ++m) {
+            uint32_t i = pos;
+            pos = pos + 1 == n ? 0 : pos + 1;
+            Packet *p = pool.make(arena + desc[2 * i], desc[2 * i + 1]);
+            if (!p) break;
+            p->id = i;
+            if (prev) prev->set_next(p);
+            else head = p;
+            prev = p;
+        }
+        return m ? PacketBatch::make_from_list(head, prev, m) : nullptr;
+    }
+};
+
+// C2-shaped trace: 60-B UDP/IPv4 frames, `flows` distinct 5-tuples (1 = C2)
+void make_trace(uint32_t n, uint32_t flows, std::vector<uint8_t> &arena, std::vector<uint32_t> &desc) {
+    arena.assign((size_t)n * 64 + 256, 0);
+    desc.resize(2 * n);
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    std::vector<uint8_t> tmpl(60, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        uint8_t *f = arena.data() + (size_t)i * 64;
+        uint32_t flow = flows > 1 ? (uint32_t)(i % flows) : 0;
+        uint64_t h = (flow + 1) * x;
+        uint8_t eth[14] = {2, 0, 0, 0, 0, 2, 2, 0, 0, 0, 0, 1, 8, 0};
+        memcpy(f, eth, 14);
+        uint8_t *ip = f + 14;
+        ip[0] = 0x45; ip[2] = 0; ip[3] = 46; ip[8] = 64; ip[9] = 17;
+        uint8_t src[4] = {10, 0, 0, 1}, dst[4] = {10, 0, 0, 2};
+        if (flows > 1) { memcpy(src, &h, 4); memcpy(dst, (uint8_t *)&h + 4, 4); }
+        memcpy(ip + 12, src, 4);
+        memcpy(ip + 16, dst, 4);
+        uint16_t c = fco_in_cksum(ip, 20);
+        memcpy(ip + 10, &c, 2);
+        uint16_t sp = flows > 1 ? (uint16_t)(h >> 13) : 1234, dp = flows > 1 ? (uint16_t)(h >> 29) : 5678;
+        ip[20] = sp >> 8; ip[21] = sp & 0xff; ip[22] = dp >> 8; ip[23] = dp & 0xff; ip[25] = 26;
+        desc[2 * i] = i * 64;
+        desc[2 * i + 1] = 60;
+    }
+}
+
+int verify() {
+    // a trace with every error kind and IP options, checked against the oracle
+    const uint32_t n = 20000;
+    std::vector<uint8_t> arena;
+    std::vector<uint32_t> desc;
+    make_trace(n, 4096, arena, desc);
+    uint64_t s = 12345;
+    auto rnd = [&]() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; };
+    for (uint32_t i = 0; i < n; ++i) {
+        uint8_t *ip = arena.data() + desc[2 * i] + 14;
+        switch (rnd() % 40) {
+        case 0: desc[2 * i + 1] = 14 + rnd() % 20; break;
+        case 1: ip[0] = 0x55; break;
+        case 2: ip[0] = 0x43; break;
+        case 3: ip[3] = 200; break;
+        case 4: ip[10] ^= 1; break;
+        case 5: ip[6] = 0x01; break;   // non-first fragment (hash 0 by definition)
+        default: break;
+        }
+    }
+    fcgpu_cfg cfg;
+    memset(&cfg, 0, sizeof cfg);
+    cfg.size = sizeof cfg;
+    cfg.check_mode = FCGPU_CHECK_IP4;
+    cfg.offset = 14;
+    cfg.checksum = 1;
+    cfg.hash_mode = FCGPU_HASH_FLOWID;
+    cfg.classify = FCGPU_CLS_LB_HASH;
+    cfg.nports = 16;
+    std::vector<uint16_t> verdict(n);
+    std::vector<uint32_t> hash(n);
+    fco_process_batch(&cfg, arena.data(), desc.data(), n, verdict.data(), hash.data(), nullptr, nullptr,
+                      nullptr, nullptr);
+    Pipeline pl;
+    std::vector<uint32_t> port(n, 999), h(n, 0);
+    pl.record_port = &port;
+    pl.record_hash = &h;
+    Replay src(arena.data(), desc.data(), n, 64);
+    for (uint32_t done = 0; done < n;) {
+        uint32_t m = n - done < 32 ? n - done : 32;
+        PacketBatch *b = src.next(m);
+        pl.push_batch(b);
+        done += m;
+    }
+    uint32_t bad = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t ep = verdict[i] >> 8;
+        if (port[i] != ep || ((verdict[i] & 0xff) == FCGPU_R_OK && h[i] != hash[i])) bad++;
+    }
+    printf("{\"verify\": %s, \"mismatches\": %u, \"valid\": %llu}\n", bad ? "false" : "true", bad,
+           (unsigned long long)pl.count.load());
+    return bad ? 1 : 0;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    double seconds = 10;
+    int threads = 1;
+    uint32_t flows = 1;
+    int stages = 3;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        if (a == "--verify") return verify();
+        if (a == "--seconds" && i + 1 < argc) seconds = atof(argv[++i]);
+        else if (a == "--threads" && i + 1 < argc) threads = atoi(argv[++i]);
+        else if (a == "--flows" && i + 1 < argc) flows = (uint32_t)atoi(argv[++i]);
+        else if (a == "--stages" && i + 1 < argc) stages = atoi(argv[++i]);
+    }
+    const uint32_t n = 4096;
+    std::vector<uint8_t> arena;
+    std::vector<uint32_t> desc;
+    make_trace(n, flows, arena, desc);
+
+    auto run = [&](int nth, double secs) {
+        std::vector<std::thread> th;
+        std::vector<uint64_t> pk(nth, 0);
+        std::atomic<bool> stop{false};
+        for (int t = 0; t < nth; ++t)
+            th.emplace_back([&, t]() {
+                Pipeline pl;
+                pl.stages = stages;
+                Replay src(arena.data(), desc.data(), n, 64);
+                uint64_t c = 0;
+                while (!stop.load(std::memory_order_relaxed)) {
+                    for (int k = 0; k < 64; ++k) {
+                        PacketBatch *b = src.next(32);
+                        pl.push_batch(b);
+                        c += 32;
+                    }
+                }
+                if (stages > 0 && pl.count.load() + pl.drops.load() != c) fprintf(stderr, "count mismatch\n");
+                pk[t] = c;
+            });
+        auto t0 = std::chrono::steady_clock::now();
+        std::this_thread::sleep_for(std::chrono::duration<double>(secs));
+        stop = true;
+        for (auto &x : th) x.join();
+        double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        uint64_t tot = 0;
+        for (auto v : pk) tot += v;
+        return tot / dt / 1e6;
+    };
+    double one = run(1, seconds / 2);
+    double all = threads > 1 ? run(threads, seconds / 2) : one;
+    printf("{\"mpps\": %.3f, \"mpps_1core\": %.3f, \"threads\": %d, \"sample\": \"%s\"}\n", all, one, threads,
+           ("C2-shaped 60-B UDP/IPv4 trace (4096 pkts, " + std::to_string(flows) +
+            " flow(s)) replayed in 32-packet linked-list batches: Strip(14) -> CheckIPHeader(CHECKSUM true) -> "
+            "AggregateHash -> FlowSwitch hash x16 -> Discard; " + std::to_string(seconds / 2) +
+            " s at 1 thread + " + std::to_string(seconds / 2) + " s at all threads")
+               .c_str());
+    return 0;
+}

@@ -207,6 +207,7 @@ void fco_process_packet(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, fco_
             r->port = (uint8_t)c->nports;
             return;
         }
+        a->nh = (uint8_t)o;   /* the pull() StripEtherVLANHeader did */
         /* version dispatch as Classifier(0/60%f0, -): needs one byte */
         v6 = ((int)(len - o) >= 1) && ((f[o] >> 4) == 6);
         reason = v6 ? check_ip6(c, f, len, o, a) : check_ip4(c, f, len, o, a);

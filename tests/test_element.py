@@ -1,0 +1,118 @@
+"""The drop-in BatchElement (GPUIPCheckClassify) driven like a Click graph.
+
+Source(BURST packets per PacketBatch) -> GPUIPCheckClassify(...) => Sink per
+output. Checks the element-level contract of the replaced chain:
+  - each packet leaves exactly once, on the output CLASSIFY_EACH_PACKET picks
+    (invalid ones on output N if it exists, else killed);
+  - input order is preserved within every output;
+  - AGGREGATE / DST_IP annotations, take() trimming, header marks, Strip;
+  - handlers count / drops / drop_details in CheckIPHeader's format.
+"""
+import numpy as np
+import pytest
+
+from fastclick_amd import synth
+from fastclick_amd import _native as N
+from tests.helpers import set_fragment
+
+CONF = "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, DETAILS true, BADSRC 192.0.2.255)"
+
+
+def test_config_errors():
+    from fastclick_amd import click as K
+    K.check_config(CONF)
+    for bad, msg in [("GPUIPCheckClassify(14)", "too many arguments"),
+                     ("GPUIPCheckClassify(CHECKSUM maybe)", "CHECKSUM"),
+                     ("GPUIPCheckClassify(N 65)", "N out of range"),
+                     ("GPUIPCheckClassify(HASHSWITCH 26 0)", "length must be > 0"),
+                     ("GPUIPCheckClassify(NATIVE_VLAN 5000)", "NATIVE_VLAN"),
+                     ("GPUIPCheckClassify(OFFSET x)", "OFFSET"),
+                     ("NoSuchElement", "unknown element class")]:
+        with pytest.raises(K.ConfigError, match=msg):
+            K.check_config(bad)
+
+
+def expected(batch, cfg, oracle):
+    return oracle.process_batch(cfg, batch)
+
+
+def _cfg_for_conf():
+    return N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16,
+                      badsrc=[N.raw_addr("192.0.2.255")])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nsinks,batch", [(17, 0), (16, 0), (17, 4096)])
+def test_element_outputs_order_annotations(oracle, nsinks, batch):
+    from fastclick_amd import click as K
+    b = synth.c4(20_000, seed=500)
+    synth.add_ip_options(b, 0.1, seed=501)
+    synth.inject_errors(b, 0.02, seed=502)
+    conf = CONF[:-1] + f", BATCH {batch})"
+    r = K.run_element(conf, b, burst=32, nsinks=nsinks)
+    e = expected(b, _cfg_for_conf(), oracle)
+    port = e["port"].astype(np.uint32)
+    exp_port = np.where(port < nsinks, port, 0xFFFFFFFF)
+    assert np.array_equal(r["port"], exp_port)
+    ok = e["reason"] == N.R_OK
+    assert np.array_equal(r["agg"][ok], e["hash"][ok])
+    assert np.array_equal(r["dst"][ok], e["anno"]["dst_ip"][ok])
+    assert np.array_equal(r["len"][ok], e["anno"]["length"][ok])
+    assert np.array_equal(r["nh"][ok], e["anno"]["nh"][ok].astype(np.int32))
+    # every output keeps input order
+    for p in range(nsinks):
+        idx = np.nonzero(r["port"] == p)[0]
+        assert (np.diff(r["seq"][idx].astype(np.int64)) > 0).all()
+    h = r["handlers"]
+    assert int(h["count"]) == int(ok.sum()) and int(h["drops"]) == int((~ok).sum())
+    lines = h["drop_details"].strip("\n").split("\n")
+    assert len(lines) == 6
+    for i, line in enumerate(lines):
+        assert line.endswith(N.REASON_TEXTS[i]) and " packets due to: " in line
+        assert int(line.split()[0]) == int((e["reason"] == i).sum())
+    if batch:
+        assert r["batches"] <= 2 * 17 * (b.n // batch + 1) + 40
+
+
+@pytest.mark.gpu
+def test_element_strip_and_auto(oracle):
+    from fastclick_amd import click as K
+    b = synth.c5(10_000, seed=510)
+    r = K.run_element("GPUIPCheckClassify(MODE AUTO, CHECKSUM true, N 8, LB_MODE hash)", b, nsinks=9)
+    e = oracle.process_batch(N.make_cfg(check_mode=N.CHECK_AUTO, checksum=True,
+                                        classify=N.CLS_LB_HASH, nports=8), b)
+    assert np.array_equal(r["port"], e["port"].astype(np.uint32))
+    ok = e["reason"] == N.R_OK
+    # MODE AUTO strips like StripEtherVLANHeader: data starts at the IP header
+    assert (r["nh"][ok] == 0).all()
+    assert np.array_equal(r["len"][ok], e["anno"]["length"][ok] - e["anno"]["nh"][ok])
+    assert np.array_equal(r["agg"][ok], e["hash"][ok])
+
+
+@pytest.mark.gpu
+def test_element_golden_flowswitch():
+    """Element-level parity with the reference FlowSwitch goldens."""
+    from fastclick_amd import click as K
+    from tests.test_golden import load, batch_of, first_fragment_mask
+    g = load("ip4")
+    b = batch_of(g)
+    r = K.run_element("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, "
+                      "BADSRC 192.0.2.255 255.255.255.255, GOODDST 10.9.9.9)", b, nsinks=17)
+    ff = first_fragment_mask(g)
+    pin = (g["lb16"] != 255) & ff
+    assert np.array_equal(r["port"][pin], g["lb16"][pin].astype(np.uint32))
+    ok = (g["reason"] == 6) & ff
+    assert np.array_equal(r["agg"][ok], g["hash"][ok])
+    assert np.array_equal(r["len"][g["reason"] == 6], g["length"][g["reason"] == 6])
+    assert np.array_equal(r["port"] == 16, g["reason"] != 6)
+
+
+@pytest.mark.gpu
+def test_element_fragments_and_burst_sizes(oracle):
+    from fastclick_amd import click as K
+    b = synth.c3(8_000, seed=520)
+    set_fragment(b, 0.2)
+    e = oracle.process_batch(N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=4), b)
+    for burst in (1, 32, 256, 8000):
+        r = K.run_element("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4)", b, burst=burst, nsinks=5)
+        assert np.array_equal(r["port"], e["port"].astype(np.uint32))
