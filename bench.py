@@ -45,7 +45,10 @@ def parse():
     ap.add_argument("--packets", type=int, default=1 << 20)
     ap.add_argument("--nbuf", type=int, default=16)
     ap.add_argument("--nports", type=int, default=16)
-    ap.add_argument("--no-perm", action="store_true", help="skip the partition scatter")
+    ap.add_argument("--no-perm", action="store_true", help="skip the partition")
+    ap.add_argument("--partition", choices=["tile", "global"], default="tile",
+                    help="tile: each 256-packet tile is one classified PacketBatch (1 launch); "
+                         "global: the whole batch is one (3 launches)")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -103,8 +106,9 @@ def main():
     cfg = N.make_cfg(offset=14, checksum=True, hash_mode=N.HASH_FLOWID, classify=N.CLS_LB_HASH,
                      nports=args.nports)
     ctx = N.Context(local, n, cfg)
+    part = N.PART_TILE if args.partition == "tile" else N.PART_GLOBAL
     outs = DeviceOutputs(n, args.nports, device=dev, verdict=True, hash=True, anno=False,
-                         perm=not args.no_perm, port_start=not args.no_perm)
+                         perm=not args.no_perm, port_start=not args.no_perm, partition=part)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
     optr = outs.ptrs()
@@ -117,7 +121,7 @@ def main():
         step(k)
     torch.cuda.synchronize()
     # counters accumulate straight into a torch tensor so RCCL can reduce them
-    ctr_t = torch.zeros(N.NCOUNTERS, dtype=torch.int64, device=dev)
+    ctr_t = torch.zeros(N.CTR_SHARDS, N.NCOUNTERS, dtype=torch.int64, device=dev)
     ctx.use_counters(ctr_t.data_ptr())
     if not args.no_timing:
         ctx.set_timing(True)
@@ -131,7 +135,7 @@ def main():
     if world > 1:
         # per-port / per-reason counters summed across GPUs: one RCCL all-reduce
         # of the device counter vector (xGMI), like PER_THREAD_SUM on read
-        glob = ctr_t.clone()
+        glob = ctr_t.sum(0)
         dist.all_reduce(glob)
     torch.cuda.synchronize()
     if world > 1:
@@ -144,7 +148,7 @@ def main():
         elapsed = float(t.item())
         total_valid = int(glob[N.CTR_COUNT].item())
     else:
-        total_valid = int(ctr_t[N.CTR_COUNT].item())
+        total_valid = int(ctr_t.sum(0)[N.CTR_COUNT].item())
 
     timing = None
     if not args.no_timing:
@@ -194,7 +198,11 @@ def main():
                 "workload": ("C2: 64 B IPv4/UDP (60-B frames in 64-B slots), 1M-packet "
                              "device-resident batch, single 5-tuple; CheckIPHeader(CHECKSUM true)"
                              " + AggregateHash + FlowSwitch hash 16 outputs"
-                             + ("" if args.no_perm else " + stable per-port partition")),
+                             + ("" if args.no_perm else
+                                " + stable per-port partition of every 256-packet PacketBatch"
+                                if args.partition == "tile" else
+                                " + stable per-port partition of the whole 1M-packet batch")),
+                "partition": "none" if args.no_perm else args.partition,
                 "packets_per_step_per_gpu": n,
                 "hbm_batches": args.nbuf,
                 "nports": args.nports,

@@ -14,7 +14,7 @@ LIBFCGPU = os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 1
+ABI_VERSION = 2
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
     R_BAD_IP6, R_VLAN_REJECT = range(9)
@@ -26,6 +26,9 @@ MAX_PORTS = 64
 MAX_ADDRS = 16
 CTR_COUNT, CTR_DROPS, CTR_REASON, CTR_PORT = 0, 1, 2, 10
 NCOUNTERS = CTR_PORT + MAX_PORTS + 1
+CTR_SHARDS = 64
+PART_GLOBAL, PART_TILE = 0, 1
+TILE = 256
 
 REASON_TEXTS = ["tiny packet", "bad IPv4 version", "bad IPv4 header length",
                 "bad IPv4 length", "bad IPv4 checksum", "bad source address"]
@@ -86,6 +89,9 @@ class fcgpu_out(C.Structure):
         ("anno", C.c_void_p),
         ("perm", C.c_void_p),
         ("port_start", C.c_void_p),
+        ("tile_count", C.c_void_p),
+        ("partition", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 
@@ -220,16 +226,16 @@ class Context:
         self.cfg = cfg
 
     def process(self, arena_ptr, desc_ptr, n, *, verdict=0, hash=0, anno=0, perm=0,
-                port_start=0, stream=0):
+                port_start=0, tile_count=0, partition=PART_GLOBAL, stream=0):
         out = fcgpu_out(verdict or None, hash or None, anno or None, perm or None,
-                        port_start or None)
+                        port_start or None, tile_count or None, partition, 0)
         self._chk(self.lib.fcgpu_process(self.h, arena_ptr, desc_ptr, n, C.byref(out),
                                          stream or None), "fcgpu_process")
 
     def process_host(self, frames, lens_ptr, n, *, verdict=0, hash=0, anno=0, perm=0,
-                     port_start=0):
+                     port_start=0, tile_count=0, partition=PART_GLOBAL):
         out = fcgpu_out(verdict or None, hash or None, anno or None, perm or None,
-                        port_start or None)
+                        port_start or None, tile_count or None, partition, 0)
         self._chk(self.lib.fcgpu_process_host(self.h, frames, lens_ptr, n, C.byref(out)),
                   "fcgpu_process_host")
 

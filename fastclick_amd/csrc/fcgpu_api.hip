@@ -4,10 +4,13 @@
 // histograms + bin totals), the device counter vector, pinned/device staging
 // for host-resident batches, and optional per-stage timing events. Launch
 // sequence per batch (all on one stream):
-//   k_rx   fused check/hash/classify + per-tile histograms   (grid = tiles)
-//   k_scan per-bin exclusive scan over tiles + counters       (grid = bins)
-//   k_part stable partition scatter, only if perm requested   (grid = tiles)
+//   k_rx   fused check/hash/classify, per-tile histograms, sharded counters,
+//          and (FCGPU_PART_TILE) each tile's stable partition  (grid = tiles)
+//   FCGPU_PART_GLOBAL only:
+//   k_scan per-output exclusive scan over tiles                 (grid = outputs)
+//   k_part dense stable partition scatter                       (grid = tiles)
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <string.h>
 #include <stdio.h>
@@ -20,6 +23,9 @@
 #pragma clang diagnostic ignored "-Wunused-value"
 
 using namespace fcgpu;
+
+static_assert(kTile == FCGPU_TILE, "tile size is part of the ABI");
+static constexpr size_t kCtrWords = (size_t)FCGPU_CTR_SHARDS * FCGPU_NCOUNTERS;
 
 namespace {
 constexpr uint32_t kHostCap = 128;          // bytes gathered per frame in host mode
@@ -49,6 +55,7 @@ struct fcgpu_ctx {
     uint32_t *h_desc = nullptr, *d_desc = nullptr;
     uint16_t *d_hv = nullptr;
     uint32_t *d_hh = nullptr, *d_hperm = nullptr, *d_hstart = nullptr;
+    uint16_t *d_htc = nullptr;
     fcgpu_anno *d_hanno = nullptr;
     // timing
     bool timing = false;
@@ -84,19 +91,32 @@ static hipEvent_t take_event(fcgpu_ctx *c) {
     return e;
 }
 
-template <int CM, bool CK>
-static void launch_rx(const RxArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL((k_rx<CM, CK>), dim3(a.ntiles), dim3(kTile), 0, s, a);
+// ev0/ev1 non-null: hipExtLaunchKernelGGL records them around the dispatch
+// itself (timestamps of the kernel, not of the stream around it).
+template <int CM, bool CK, int PART>
+static void launch_rx(const RxArgs &a, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    if (ev0)
+        hipExtLaunchKernelGGL((k_rx<CM, CK, PART>), dim3(a.ntiles), dim3(kTile), 0, s, ev0, ev1, 0, a);
+    else
+        hipLaunchKernelGGL((k_rx<CM, CK, PART>), dim3(a.ntiles), dim3(kTile), 0, s, a);
 }
 
-static void launch_rx_any(uint32_t cm, bool ck, const RxArgs &a, hipStream_t s) {
+template <int PART>
+static void launch_rx_part(uint32_t cm, bool ck, const RxArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     switch (cm * 2 + (ck ? 1 : 0)) {
-    case 0: launch_rx<FCGPU_CHECK_IP4, false>(a, s); break;
-    case 1: launch_rx<FCGPU_CHECK_IP4, true>(a, s); break;
-    case 2: case 3: launch_rx<FCGPU_MARK_IP4, false>(a, s); break;
-    case 4: launch_rx<FCGPU_CHECK_AUTO, false>(a, s); break;
-    default: launch_rx<FCGPU_CHECK_AUTO, true>(a, s); break;
+    case 0: launch_rx<FCGPU_CHECK_IP4, false, PART>(a, s, e0, e1); break;
+    case 1: launch_rx<FCGPU_CHECK_IP4, true, PART>(a, s, e0, e1); break;
+    case 2: case 3: launch_rx<FCGPU_MARK_IP4, false, PART>(a, s, e0, e1); break;
+    case 4: launch_rx<FCGPU_CHECK_AUTO, false, PART>(a, s, e0, e1); break;
+    default: launch_rx<FCGPU_CHECK_AUTO, true, PART>(a, s, e0, e1); break;
     }
+}
+
+static void launch_rx_any(int part, uint32_t cm, bool ck, const RxArgs &a, hipStream_t s, hipEvent_t e0,
+                          hipEvent_t e1) {
+    if (part == kPartTile) launch_rx_part<kPartTile>(cm, ck, a, s, e0, e1);
+    else if (part == kPartGlobal) launch_rx_part<kPartGlobal>(cm, ck, a, s, e0, e1);
+    else launch_rx_part<kPartNone>(cm, ck, a, s, e0, e1);
 }
 
 extern "C" {
@@ -144,6 +164,7 @@ void fcgpu_close(fcgpu_ctx *c) {
         hipFree(c->d_hperm);
         hipFree(c->d_hstart);
         hipFree(c->d_hanno);
+        hipFree(c->d_htc);
         hipHostFree(c->h_arena);
         hipHostFree(c->h_desc);
         if (c->stream) hipStreamDestroy(c->stream);
@@ -168,11 +189,11 @@ int fcgpu_open(int device, uint32_t max_batch, fcgpu_ctx **out) {
     };
     chk(hipSetDevice(device), "hipSetDevice");
     chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
-    chk(hipMalloc(&c->d_tilecnt, sizeof(uint32_t) * (size_t)kMaxBins * c->max_tiles), "hipMalloc tilecnt");
+    chk(hipMalloc(&c->d_tilecnt, sizeof(uint32_t) * (size_t)(FCGPU_MAX_PORTS + 1) * c->max_tiles), "hipMalloc tilecnt");
     chk(hipMalloc(&c->d_totals, sizeof(uint32_t) * kMaxBins), "hipMalloc totals");
-    chk(hipMalloc(&c->d_ctr_own, sizeof(unsigned long long) * FCGPU_NCOUNTERS), "hipMalloc counters");
+    chk(hipMalloc(&c->d_ctr_own, sizeof(unsigned long long) * kCtrWords), "hipMalloc counters");
     c->d_ctr = c->d_ctr_own;
-    if (rc == FCGPU_OK) chk(hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * FCGPU_NCOUNTERS), "hipMemset");
+    if (rc == FCGPU_OK) chk(hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * kCtrWords), "hipMemset");
     if (rc != FCGPU_OK) {
         g_open_err = c->err;
         fcgpu_close(c);
@@ -229,12 +250,17 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     HIPCHK(c, hipSetDevice(c->device));
     const uint32_t ntiles = (n + kTile - 1) / kTile;
     const uint32_t nports = c->cfg.nports;
-    const uint32_t nbt = nports + 1 + FCGPU_NREASON_SLOTS;
     uint16_t *verdict = o->verdict;
-    if (!verdict && o->perm) {
+    if (!verdict && o->partition == FCGPU_PART_GLOBAL && o->perm) {
         if (!c->d_verdict) HIPCHK(c, hipMalloc(&c->d_verdict, sizeof(uint16_t) * c->max_batch));
         verdict = c->d_verdict;
     }
+    const bool tile = o->partition == FCGPU_PART_TILE;
+    if (o->partition > FCGPU_PART_TILE) return fail(c, FCGPU_EINVAL, "bad partition mode");
+    if (tile && (!o->perm != !o->tile_count))
+        return fail(c, FCGPU_EINVAL, "FCGPU_PART_TILE needs both perm and tile_count");
+    const bool want_global = !tile && (o->perm || o->port_start);
+    const int part = tile && o->perm ? kPartTile : (want_global ? kPartGlobal : kPartNone);
     RxArgs a;
     a.arena = d_arena;
     a.desc = reinterpret_cast<const uint2 *>(d_desc);
@@ -244,37 +270,36 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     a.hash = o->hash;
     a.anno = o->anno;
     a.tilecnt = c->d_tilecnt;
+    a.perm = o->perm;
+    a.tile_count = o->tile_count;
+    a.ctr = c->d_ctr;
     a.cfg = c->dcfg;
 
     EvPair ev[3];
     if (c->timing)
         for (int k = 0; k < 3; ++k) { ev[k].a = take_event(c); ev[k].b = take_event(c); ev[k].stage = k; }
 
-    if (c->timing) hipEventRecord(ev[0].a, s);
-    launch_rx_any(c->cfg.check_mode, c->cfg.checksum != 0, a, s);
+    launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, a, s, c->timing ? ev[0].a : nullptr,
+                  c->timing ? ev[0].b : nullptr);
     HIPCHK(c, hipGetLastError());
-    if (c->timing) { hipEventRecord(ev[0].b, s); hipEventRecord(ev[1].a, s); }
-    hipLaunchKernelGGL(k_scan, dim3(nbt), dim3(1024), 0, s, c->d_tilecnt, ntiles, nports, c->d_totals,
-                       c->d_ctr);
-    HIPCHK(c, hipGetLastError());
-    if (c->timing) hipEventRecord(ev[1].b, s);
-    if (o->perm || o->port_start) {
-        if (c->timing) hipEventRecord(ev[2].a, s);
-        if (o->perm) {
-            hipLaunchKernelGGL(k_part, dim3(ntiles), dim3(kTile), 0, s, verdict, n, ntiles, nports,
-                               c->d_tilecnt, c->d_totals, o->perm, o->port_start);
-        } else {
-            hipLaunchKernelGGL(k_part, dim3(1), dim3(kTile), 0, s, verdict, 0u, ntiles, nports,
-                               c->d_tilecnt, c->d_totals, o->perm, o->port_start);
-        }
+    if (want_global) {
+        if (c->timing) hipEventRecord(ev[1].a, s);
+        hipLaunchKernelGGL(k_scan, dim3(nports + 1), dim3(1024), 0, s, c->d_tilecnt, ntiles, c->d_totals);
+        HIPCHK(c, hipGetLastError());
+        if (c->timing) { hipEventRecord(ev[1].b, s); hipEventRecord(ev[2].a, s); }
+        hipLaunchKernelGGL(k_part, dim3(o->perm ? ntiles : 1), dim3(kTile), 0, s, verdict, o->perm ? n : 0u,
+                           ntiles, nports, c->d_tilecnt, c->d_totals, o->perm, o->port_start);
         HIPCHK(c, hipGetLastError());
         if (c->timing) hipEventRecord(ev[2].b, s);
     }
     if (c->timing) {
         c->pending.push_back(ev[0]);
-        c->pending.push_back(ev[1]);
-        if (o->perm || o->port_start) c->pending.push_back(ev[2]);
-        else { c->free_ev.push_back(ev[2].a); c->free_ev.push_back(ev[2].b); }
+        if (want_global) {
+            c->pending.push_back(ev[1]);
+            c->pending.push_back(ev[2]);
+        } else {
+            for (int k = 1; k < 3; ++k) { c->free_ev.push_back(ev[k].a); c->free_ev.push_back(ev[k].b); }
+        }
     }
     return FCGPU_OK;
 }
@@ -297,6 +322,7 @@ int fcgpu_process_host(fcgpu_ctx *c, const uint8_t *const *frames, const uint32_
         HIPCHK(c, hipMalloc(&c->d_hperm, sizeof(uint32_t) * c->max_batch));
         HIPCHK(c, hipMalloc(&c->d_hstart, sizeof(uint32_t) * (FCGPU_MAX_PORTS + 2)));
         HIPCHK(c, hipMalloc(&c->d_hanno, sizeof(fcgpu_anno) * c->max_batch));
+        HIPCHK(c, hipMalloc(&c->d_htc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * c->max_tiles));
     }
     // gather: first min(len, 128) bytes of each frame at 64-B aligned offsets.
     // The device sees the real frame length; bytes past the capture are never
@@ -319,12 +345,19 @@ int fcgpu_process_host(fcgpu_ctx *c, const uint8_t *const *frames, const uint32_
     d.anno = h->anno ? c->d_hanno : nullptr;
     d.perm = h->perm ? c->d_hperm : nullptr;
     d.port_start = h->port_start ? c->d_hstart : nullptr;
+    d.tile_count = h->tile_count ? c->d_htc : nullptr;
+    d.partition = h->partition;
+    d.reserved = 0;
     int rc = fcgpu_process(c, c->d_arena, c->d_desc, n, &d, s);
     if (rc != FCGPU_OK) return rc;
     if (h->verdict) HIPCHK(c, hipMemcpyAsync(h->verdict, d.verdict, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, s));
     if (h->hash) HIPCHK(c, hipMemcpyAsync(h->hash, d.hash, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
     if (h->anno) HIPCHK(c, hipMemcpyAsync(h->anno, d.anno, sizeof(fcgpu_anno) * n, hipMemcpyDeviceToHost, s));
     if (h->perm) HIPCHK(c, hipMemcpyAsync(h->perm, d.perm, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
+    if (h->tile_count)
+        HIPCHK(c, hipMemcpyAsync(h->tile_count, d.tile_count,
+                                 sizeof(uint16_t) * (c->cfg.nports + 1) * ((n + kTile - 1) / kTile),
+                                 hipMemcpyDeviceToHost, s));
     if (h->port_start)
         HIPCHK(c, hipMemcpyAsync(h->port_start, d.port_start, sizeof(uint32_t) * (c->cfg.nports + 2),
                                  hipMemcpyDeviceToHost, s));
@@ -338,7 +371,13 @@ int fcgpu_read_counters(fcgpu_ctx *c, uint64_t *out, int n) {
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipDeviceSynchronize());
-    HIPCHK(c, hipMemcpy(out, c->d_ctr, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> all(kCtrWords);
+    HIPCHK(c, hipMemcpy(all.data(), c->d_ctr, sizeof(uint64_t) * kCtrWords, hipMemcpyDeviceToHost));
+    for (int k = 0; k < n; ++k) {
+        uint64_t v = 0;
+        for (int r = 0; r < FCGPU_CTR_SHARDS; ++r) v += all[(size_t)r * FCGPU_NCOUNTERS + k];
+        out[k] = v;
+    }
     return FCGPU_OK;
 }
 
@@ -346,7 +385,7 @@ int fcgpu_reset_counters(fcgpu_ctx *c) {
     if (!c) return FCGPU_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipDeviceSynchronize());
-    HIPCHK(c, hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * FCGPU_NCOUNTERS));
+    HIPCHK(c, hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * kCtrWords));
     return FCGPU_OK;
 }
 

@@ -48,7 +48,10 @@ struct RxArgs {
     uint16_t *verdict;
     uint32_t *hash;
     fcgpu_anno *anno;
-    uint32_t *tilecnt;     // [nbins_total][ntiles]
+    uint32_t *tilecnt;     // [nports+1][ntiles] (kPartGlobal)
+    uint32_t *perm;        // [n] tile-local partition (kPartTile)
+    uint16_t *tile_count;  // [ntiles][nports+1] (kPartTile)
+    unsigned long long *ctr;   // [FCGPU_CTR_SHARDS][FCGPU_NCOUNTERS]
     DevCfg cfg;
 };
 
@@ -258,14 +261,24 @@ __device__ __forceinline__ void glds16(const uint8_t *src, uint8_t *lds) {
 
 __device__ __forceinline__ uint32_t reason_slot(uint32_t r) { return r < 6 ? r : r - 1; }
 
-// Fused CheckIPHeader -> AggregateHash -> classify over one 256-packet tile,
-// plus the tile's per-output / per-reason histogram for the partition scan.
-template <int CM, bool CK>
+// Partition modes of k_rx
+constexpr int kPartNone = 0;     // counters only
+constexpr int kPartGlobal = 1;   // + per-tile port histogram for k_scan/k_part (dense perm)
+constexpr int kPartTile = 2;     // + stable partition of each 256-packet tile, in-kernel
+
+// Fused [StripEtherVLANHeader ->] CheckIPHeader/CheckIP6Header -> AggregateHash
+// -> classify over one 256-packet tile; per-tile histogram by wave ballots;
+// counters by sharded atomics; optionally the tile's stable per-output
+// partition (CLASSIFY_EACH_PACKET on a 256-packet PacketBatch).
+template <int CM, bool CK, int PART>
 __global__ __launch_bounds__(kTile) void k_rx(RxArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4 * kWave * kWin];
     __shared__ uint32_t s_cnt[4][kMaxBins];
+    __shared__ uint32_t s_base[FCGPU_MAX_PORTS + 2];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t i = blockIdx.x * kTile + threadIdx.x;
+    // grid-stride over tiles (grid == ntiles: one tile per workgroup)
+    for (uint32_t tile = blockIdx.x; tile < A.ntiles; tile += gridDim.x) {
+    const uint32_t i = tile * kTile + threadIdx.x;
     const bool live = i < A.n;
     uint2 d = make_uint2(0, 0);
     if (live) d = A.desc[i];
@@ -301,8 +314,11 @@ __global__ __launch_bounds__(kTile) void k_rx(RxArgs A) {
 
     // per-wave histogram by ballot: outputs 0..nports (nports = invalid list)
     const uint32_t nb = A.cfg.nports + 1;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t rank = 0;
     for (uint32_t b = 0; b < nb; ++b) {
         const uint64_t m = __ballot(bin == b);
+        if (PART == kPartTile && bin == b) rank = (uint32_t)__popcll(m & lt);
         if (lane == 0) s_cnt[wave][b] = (uint32_t)__popcll(m);
     }
     const uint64_t mbad = __ballot(rslot != 0xffffffffu);
@@ -312,16 +328,52 @@ __global__ __launch_bounds__(kTile) void k_rx(RxArgs A) {
     }
     __syncthreads();
     const uint32_t nbt = nb + FCGPU_NREASON_SLOTS;
-    if (threadIdx.x < nbt) {
-        const uint32_t t = threadIdx.x;
-        A.tilecnt[t * A.ntiles + blockIdx.x] = s_cnt[0][t] + s_cnt[1][t] + s_cnt[2][t] + s_cnt[3][t];
+    const uint32_t t = threadIdx.x;
+    uint32_t tot = 0;
+    if (t < nbt) tot = s_cnt[0][t] + s_cnt[1][t] + s_cnt[2][t] + s_cnt[3][t];
+    if (PART == kPartGlobal && t < nb) A.tilecnt[t * A.ntiles + tile] = tot;
+    if (PART == kPartTile) {
+        if (t < nb) A.tile_count[(size_t)tile * nb + t] = (uint16_t)tot;
+        // exclusive scan of the tile's output totals (wave 0; nb <= 65)
+        if (wave == 0) {
+            uint32_t v = lane < nb ? tot : 0u, incl = v;
+#pragma unroll
+            for (int dl = 1; dl < 64; dl <<= 1) {
+                const uint32_t u = __shfl_up(incl, dl);
+                if (lane >= (uint32_t)dl) incl += u;
+            }
+            if (lane < nb) s_base[lane] = incl - v;
+            if (lane == 63) s_base[64] = incl;   // base of output 64 (nports == 64)
+        }
+    }
+    // counters: one atomic per non-zero bin per tile, sharded by tile
+    if (t < nbt) {
+        unsigned long long *ctr = A.ctr + (size_t)(tile & (FCGPU_CTR_SHARDS - 1)) * FCGPU_NCOUNTERS;
+        if (tot) {
+            if (t < nb) atomicAdd(&ctr[FCGPU_CTR_PORT + t], (unsigned long long)tot);
+            else atomicAdd(&ctr[FCGPU_CTR_REASON + (t - nb)], (unsigned long long)tot);
+        }
+        if (t == nb - 1) {   // the invalid list: drops, and count = packets - drops
+            const uint32_t live_n = min(A.n - tile * kTile, (uint32_t)kTile);
+            if (tot) atomicAdd(&ctr[FCGPU_CTR_DROPS], (unsigned long long)tot);
+            if (live_n - tot) atomicAdd(&ctr[FCGPU_CTR_COUNT], (unsigned long long)(live_n - tot));
+        }
+    }
+    if (PART == kPartTile) {
+        __syncthreads();
+        if (live) {
+            uint32_t wpre = 0;
+            for (uint32_t w = 0; w < wave; ++w) wpre += s_cnt[w][bin];
+            A.perm[(size_t)tile * kTile + s_base[bin] + wpre + rank] = i;
+        }
+    }
+    __syncthreads();   // s_cnt / s_base / s_win reused by the next tile
     }
 }
 
-// Exclusive scan of one bin's per-tile counts (in place), bin total, counters.
-// grid = nbins_total blocks of 1024 threads.
-__global__ __launch_bounds__(1024) void k_scan(uint32_t *tilecnt, uint32_t ntiles, uint32_t nports,
-                                               uint32_t *totals, unsigned long long *ctr) {
+// Exclusive scan of one output's per-tile counts (in place) and its total.
+// grid = nports+1 blocks of 1024 threads.
+__global__ __launch_bounds__(1024) void k_scan(uint32_t *tilecnt, uint32_t ntiles, uint32_t *totals) {
     __shared__ uint32_t s_w[16];
     const uint32_t b = blockIdx.x;
     uint32_t *col = tilecnt + (size_t)b * ntiles;
@@ -332,7 +384,6 @@ __global__ __launch_bounds__(1024) void k_scan(uint32_t *tilecnt, uint32_t ntile
         const uint32_t t = beg + j;
         if (t < ntiles) sum += col[t];
     }
-    // block exclusive scan of per-thread sums
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t incl = sum;
 #pragma unroll
@@ -357,22 +408,11 @@ __global__ __launch_bounds__(1024) void k_scan(uint32_t *tilecnt, uint32_t ntile
             run += v;
         }
     }
-    if (threadIdx.x == 0) {
-        totals[b] = total;
-        const unsigned long long T = total;
-        if (b < nports) {
-            atomicAdd(&ctr[FCGPU_CTR_PORT + b], T);
-            atomicAdd(&ctr[FCGPU_CTR_COUNT], T);
-        } else if (b == nports) {
-            atomicAdd(&ctr[FCGPU_CTR_PORT + b], T);
-            atomicAdd(&ctr[FCGPU_CTR_DROPS], T);
-        } else {
-            atomicAdd(&ctr[FCGPU_CTR_REASON + (b - nports - 1)], T);
-        }
-    }
+    if (threadIdx.x == 0) totals[b] = total;
 }
 
-// Stable partition (CLASSIFY_EACH_PACKET order): perm[start[bin] + rank] = i.
+// Dense global stable partition (CLASSIFY_EACH_PACKET order over the whole
+// batch): perm[start[bin] + rank] = i.
 __global__ __launch_bounds__(kTile) void k_part(const uint16_t *verdict, uint32_t n, uint32_t ntiles,
                                                 uint32_t nports, const uint32_t *tileoff,
                                                 const uint32_t *totals, uint32_t *perm,

@@ -16,7 +16,9 @@
 //   BADADDRS                                 -- CheckIP6Header (IPv6, MODE AUTO)
 //   N / LB_MODE hash|hash_agg|hash_ip        -- FlowSwitch / LoadBalancer
 //   HASHSWITCH "OFFSET LENGTH"               -- HashSwitch
-//   MODE CHECK|MARK|AUTO, HASH NONE|FLOWID|FLOW5ID, STRIP, BATCH, DEVICE
+//   MODE CHECK|MARK|AUTO, HASH NONE|FLOWID|FLOW5ID, STRIP, BATCH, DEVICE,
+//   PARTITION TILE (default: each 256-packet tile classified as one batch, one
+//   fused launch) | GLOBAL (the whole staged batch as one, three launches)
 // Handlers: count, drops, drop_details (DETAILS true), port_counts.
 //
 // Packets are parked until BATCH packets are staged (MinBatch pattern,
@@ -112,6 +114,10 @@ class GPUIPCheckClassify : public Element {
             } else if (k == "DEVICE") {
                 if (!parse_int(v, n) || n < 0) return err(errh, "bad DEVICE");
                 _device = (int)n;
+            } else if (k == "PARTITION") {
+                if (v == "TILE") _partition = FCGPU_PART_TILE;
+                else if (v == "GLOBAL") _partition = FCGPU_PART_GLOBAL;
+                else return err(errh, "PARTITION expects TILE or GLOBAL");
             } else if (k == "BADADDRS") {
                 return err(errh, "BADADDRS: only the default IPv6 bad source (ff..ff) is supported");
             } else if (k.empty()) {
@@ -139,6 +145,7 @@ class GPUIPCheckClassify : public Element {
         _anno.resize(_cap);
         _perm.resize(_cap);
         _start.resize(FCGPU_MAX_PORTS + 2);
+        _tile_count.resize((size_t)(FCGPU_MAX_PORTS + 1) * ((_cap + FCGPU_TILE - 1) / FCGPU_TILE));
         return 0;
     }
 
@@ -194,7 +201,10 @@ class GPUIPCheckClassify : public Element {
         o.hash = _hash.data();
         o.anno = _anno.data();
         o.perm = _perm.data();
-        o.port_start = _start.data();
+        o.partition = _partition;
+        o.port_start = _partition == FCGPU_PART_GLOBAL ? _start.data() : nullptr;
+        o.tile_count = _partition == FCGPU_PART_TILE ? _tile_count.data() : nullptr;
+        o.reserved = 0;
         int rc = fcgpu_process_host(_ctx, _frames.data(), _lens.data(), n, &o);
         if (rc != FCGPU_OK) {
             // no CPU fallback: report, drop the staged packets, keep running
@@ -228,25 +238,40 @@ class GPUIPCheckClassify : public Element {
                 if (_strip && reason != FCGPU_R_VLAN_REJECT) p->pull(autom ? a.nh : (uint32_t)_cfg.offset);
             }
         }
-        // one batch per output in port order, input order within a port
-        // (chunked to MAX_BATCH_SIZE, include/click/packetbatch.hh:416)
         const uint32_t nb = _cfg.nports + 1;
-        for (uint32_t port = 0; port < nb; ++port) {
-            uint32_t s = _start[port], e = _start[port + 1];
-            while (s < e) {
-                uint32_t m = e - s < kMaxBatch ? e - s : kMaxBatch;
-                Packet *head = _pkts[_perm[s]], *prev = head;
-                for (uint32_t j = 1; j < m; ++j) {
-                    Packet *q = _pkts[_perm[s + j]];
-                    prev->set_next(q);
-                    prev = q;
+        if (_partition == FCGPU_PART_GLOBAL) {
+            // one batch per output in port order, input order within a port
+            // (chunked to MAX_BATCH_SIZE, include/click/packetbatch.hh:416)
+            for (uint32_t port = 0; port < nb; ++port)
+                emit_run(port, _start[port], _start[port + 1]);
+        } else {
+            // every FCGPU_TILE-packet tile is one classified PacketBatch: its
+            // runs leave in port order, tiles in input order
+            const uint32_t ntiles = (n + FCGPU_TILE - 1) / FCGPU_TILE;
+            for (uint32_t t = 0; t < ntiles; ++t) {
+                uint32_t s = t * FCGPU_TILE;
+                for (uint32_t port = 0; port < nb; ++port) {
+                    const uint32_t c = _tile_count[(size_t)t * nb + port];
+                    emit_run(port, s, s + c);
+                    s += c;
                 }
-                PacketBatch *b = PacketBatch::make_from_list(head, prev, m);
-                checked_output_push_batch((int)port, b);
-                s += m;
             }
         }
         _pkts.clear();
+    }
+
+    void emit_run(uint32_t port, uint32_t s, uint32_t e) {
+        while (s < e) {
+            uint32_t m = e - s < kMaxBatch ? e - s : kMaxBatch;
+            Packet *head = _pkts[_perm[s]], *prev = head;
+            for (uint32_t j = 1; j < m; ++j) {
+                Packet *q = _pkts[_perm[s + j]];
+                prev->set_next(q);
+                prev = q;
+            }
+            checked_output_push_batch((int)port, PacketBatch::make_from_list(head, prev, m));
+            s += m;
+        }
     }
 
     static constexpr uint32_t kMaxBatch = 8192;
@@ -265,6 +290,8 @@ class GPUIPCheckClassify : public Element {
     std::vector<fcgpu_anno> _anno;
     std::vector<uint32_t> _perm;
     std::vector<uint32_t> _start;
+    std::vector<uint16_t> _tile_count;
+    uint32_t _partition = FCGPU_PART_TILE;
 };
 
 }  // namespace fcx

@@ -35,21 +35,26 @@ class DeviceBatch:
 
 class DeviceOutputs:
     def __init__(self, n, nports, device="cuda", *, verdict=True, hash=True, anno=False,
-                 perm=False, port_start=False):
+                 perm=False, port_start=False, partition=N.PART_GLOBAL):
         torch = _torch()
         self.n = n
         self.nports = nports
+        self.partition = partition
         mk = lambda k, dt: torch.empty(k, dtype=dt, device=device)  # noqa: E731
         self.verdict = mk(n, torch.int16) if verdict else None
         self.hash = mk(n, torch.int32) if hash else None
         self.anno = mk(n * 16, torch.uint8) if anno else None
         self.perm = mk(n, torch.int32) if perm else None
-        self.port_start = mk(nports + 2, torch.int32) if port_start else None
+        tile = partition == N.PART_TILE
+        self.port_start = mk(nports + 2, torch.int32) if port_start and not tile else None
+        ntiles = (n + N.TILE - 1) // N.TILE
+        self.tile_count = mk(ntiles * (nports + 1), torch.int16) if perm and tile else None
 
     def ptrs(self):
         p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
         return dict(verdict=p(self.verdict), hash=p(self.hash), anno=p(self.anno),
-                    perm=p(self.perm), port_start=p(self.port_start))
+                    perm=p(self.perm), port_start=p(self.port_start),
+                    tile_count=p(self.tile_count), partition=self.partition)
 
     def numpy(self):
         out = {}
@@ -63,7 +68,10 @@ class DeviceOutputs:
         if self.anno is not None:
             out["anno"] = self.anno.cpu().numpy().view(N.anno_dtype())
         if self.perm is not None:
-            out["perm"] = self.perm.cpu().numpy().view(np.uint32)
+            key = "perm_tile" if self.partition == N.PART_TILE else "perm"
+            out[key] = self.perm.cpu().numpy().view(np.uint32)
+        if self.tile_count is not None:
+            out["tile_count"] = self.tile_count.cpu().numpy().view(np.uint16)
         if self.port_start is not None:
             out["port_start"] = self.port_start.cpu().numpy().view(np.uint32)
         return out
@@ -76,7 +84,7 @@ def run_device(ctx: N.Context, dbatch: DeviceBatch, outs: DeviceOutputs, stream=
                 stream=s.cuda_stream, **outs.ptrs())
 
 
-def process_batch(batch, cfg, *, anno=True, perm=True, device_index=0):
+def process_batch(batch, cfg, *, anno=True, perm=True, device_index=0, partition=N.PART_GLOBAL):
     """Upload a host Batch, run the device path once, return numpy results and
     the counter vector. Convenience for tests and smoke()."""
     torch = _torch()
@@ -85,7 +93,7 @@ def process_batch(batch, cfg, *, anno=True, perm=True, device_index=0):
         try:
             db = DeviceBatch.upload(batch, device=f"cuda:{device_index}")
             outs = DeviceOutputs(batch.n, cfg.nports, device=f"cuda:{device_index}",
-                                 anno=anno, perm=perm, port_start=perm)
+                                 anno=anno, perm=perm, port_start=perm, partition=partition)
             run_device(ctx, db, outs)
             torch.cuda.synchronize()
             res = outs.numpy()

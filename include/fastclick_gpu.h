@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 1
+#define FCGPU_ABI_VERSION 2
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -122,12 +122,29 @@ typedef struct fcgpu_anno {
     uint32_t reserved;
 } fcgpu_anno;
 
+/* Stable per-output partition (CLASSIFY_EACH_PACKET, packetbatch.hh:259-307),
+ * selected by fcgpu_out.partition:
+ *   FCGPU_PART_GLOBAL: the whole batch is one PacketBatch. perm[n] lists packet
+ *       indices grouped by output in input order; output b occupies
+ *       perm[port_start[b] .. port_start[b+1]). Three launches.
+ *   FCGPU_PART_TILE: the batch is a sequence of FCGPU_TILE-packet PacketBatches
+ *       (the element's input batches), each partitioned on its own, exactly as
+ *       a ClassifyElement partitions every batch it receives. Tile t's entries
+ *       are perm[t*FCGPU_TILE ...], grouped by output; tile_count[t*(nports+1)+b]
+ *       is the size of output b's run in tile t. One fused launch.           */
+#define FCGPU_PART_GLOBAL 0
+#define FCGPU_PART_TILE   1
+#define FCGPU_TILE        256
+
 typedef struct fcgpu_out {
     uint16_t   *verdict;      /* [n] reason | (output port << 8); invalid -> port nports */
     uint32_t   *hash;         /* [n] AGGREGATE annotation (0 unless valid)               */
     fcgpu_anno *anno;         /* [n] optional annotations                                */
     uint32_t   *perm;         /* [n] packet indices grouped by output, input order kept  */
-    uint32_t   *port_start;   /* [nports+2] start of each output's run in perm; last=n   */
+    uint32_t   *port_start;   /* GLOBAL: [nports+2] start of each output's run in perm   */
+    uint16_t   *tile_count;   /* TILE: [ceil(n/FCGPU_TILE)][nports+1] run sizes          */
+    uint32_t    partition;    /* FCGPU_PART_GLOBAL or FCGPU_PART_TILE                    */
+    uint32_t    reserved;
 } fcgpu_out;
 
 typedef struct fcgpu_ctx fcgpu_ctx;
@@ -142,6 +159,10 @@ typedef struct fcgpu_ctx fcgpu_ctx;
 #define FCGPU_CTR_REASON  2
 #define FCGPU_CTR_PORT    10
 #define FCGPU_NCOUNTERS   (FCGPU_CTR_PORT + FCGPU_MAX_PORTS + 1)
+/* On the device the vector is kept in FCGPU_CTR_SHARDS replicas (tiles add to
+ * replica tile % FCGPU_CTR_SHARDS) and summed on read, like per_thread<>
+ * counters summed by PER_THREAD_SUM (include/click/sync.hh:56,384). */
+#define FCGPU_CTR_SHARDS  64
 
 int  fcgpu_abi_version(void);
 int  fcgpu_device_count(void);
@@ -168,12 +189,12 @@ int  fcgpu_process_host(fcgpu_ctx *ctx, const uint8_t *const *frames,
 
 int  fcgpu_read_counters(fcgpu_ctx *ctx, uint64_t *out, int n);
 int  fcgpu_reset_counters(fcgpu_ctx *ctx);
-/* Device address of the context's uint64 counter vector (FCGPU_NCOUNTERS), for
- * a cross-GPU all-reduce on the caller's stream. */
+/* Device address of the context's uint64 counter replicas
+ * (FCGPU_CTR_SHARDS x FCGPU_NCOUNTERS), for a cross-GPU all-reduce. */
 int  fcgpu_counters_device(fcgpu_ctx *ctx, uint64_t **d_counters);
-/* Make the context accumulate into caller-owned device memory (FCGPU_NCOUNTERS
- * uint64, initialised by the caller), e.g. a tensor that is all-reduced in
- * place over RCCL. NULL reverts to the context's own vector. */
+/* Make the context accumulate into caller-owned device memory
+ * (FCGPU_CTR_SHARDS x FCGPU_NCOUNTERS uint64, initialised by the caller), e.g. a
+ * tensor that is all-reduced over RCCL. NULL reverts to the context's own. */
 int  fcgpu_use_counters(fcgpu_ctx *ctx, uint64_t *d_counters);
 
 /* Per-kernel timing with HIP events on the launch stream (off by default).

@@ -124,6 +124,18 @@ void fco_classify_each_packet(int nbatches, const int *port, uint32_t n,
     }
 }
 
+void fco_partition_tiles(int nbatches, const int *port, uint32_t n, uint32_t tile,
+                         uint32_t *perm, uint16_t *tile_count)
+{
+    uint32_t start[FCGPU_MAX_PORTS + 2];
+    for (uint32_t t0 = 0, t = 0; t0 < n; t0 += tile, ++t) {
+        uint32_t m = n - t0 < tile ? n - t0 : tile;
+        fco_classify_each_packet(nbatches, port + t0, m, perm + t0, start);
+        for (uint32_t j = 0; j < m; ++j) perm[t0 + j] += t0;
+        for (int b = 0; b < nbatches; ++b) tile_count[(size_t)t * nbatches + b] = (uint16_t)(start[b + 1] - start[b]);
+    }
+}
+
 static int in_list(const uint32_t *l, uint32_t nl, uint32_t v)
 {
     for (uint32_t i = 0; i < nl; i++)
@@ -260,6 +272,14 @@ void fco_process_batch(const fcgpu_cfg *c, const uint8_t *arena, const uint32_t 
                        uint32_t n, uint16_t *verdict, uint32_t *hash, fcgpu_anno *anno,
                        uint32_t *perm, uint32_t *port_start, uint64_t *ctr)
 {
+    fco_process_batch2(c, arena, desc, n, verdict, hash, anno, perm, port_start, NULL, NULL, ctr);
+}
+
+void fco_process_batch2(const fcgpu_cfg *c, const uint8_t *arena, const uint32_t *desc,
+                        uint32_t n, uint16_t *verdict, uint32_t *hash, fcgpu_anno *anno,
+                        uint32_t *perm, uint32_t *port_start, uint32_t *perm_tile,
+                        uint16_t *tile_count, uint64_t *ctr)
+{
     int nb = (int)c->nports + 1;
     int *port = (int *)malloc(sizeof(int) * (n ? n : 1));
     for (uint32_t i = 0; i < n; i++) {
@@ -280,5 +300,7 @@ void fco_process_batch(const fcgpu_cfg *c, const uint8_t *arena, const uint32_t 
         fco_classify_each_packet(nb, port, n, perm, start);
         if (port_start) memcpy(port_start, start, sizeof(uint32_t) * (nb + 1));
     }
+    if (perm_tile && tile_count)
+        fco_partition_tiles(nb, port, n, FCGPU_TILE, perm_tile, tile_count);
     free(port);
 }

@@ -42,6 +42,12 @@ void fco_process_batch(const fcgpu_cfg *cfg, const uint8_t *arena, const uint32_
                        uint32_t n, uint16_t *verdict, uint32_t *hash, fcgpu_anno *anno,
                        uint32_t *perm, uint32_t *port_start, uint64_t *counters);
 
+/* Same, plus the FCGPU_PART_TILE outputs (perm_tile, tile_count). */
+void fco_process_batch2(const fcgpu_cfg *cfg, const uint8_t *arena, const uint32_t *desc,
+                        uint32_t n, uint16_t *verdict, uint32_t *hash, fcgpu_anno *anno,
+                        uint32_t *perm, uint32_t *port_start, uint32_t *perm_tile,
+                        uint16_t *tile_count, uint64_t *counters);
+
 /* Individual pieces, exposed for known-answer tests. */
 uint32_t fco_ipflowid_hash(uint32_t saddr_raw, uint16_t sport_net,
                            uint32_t daddr_raw, uint16_t dport_net);  /* A6 */
@@ -52,6 +58,11 @@ int fco_hash_ip_port(const uint8_t *data, uint32_t len, int n);  /* A8 hash_ip *
 int fco_hashswitch_port(const uint8_t *data, uint32_t len, int off, int l, int n); /* A9 */
 void fco_classify_each_packet(int nbatches, const int *port, uint32_t n,
                               uint32_t *perm, uint32_t *start); /* A10 */
+/* A10 applied to consecutive `tile`-packet batches (FCGPU_PART_TILE layout):
+ * perm[t*tile ...] = tile t's packet indices grouped by output, tile_count
+ * [t*nbatches + b] = run sizes. */
+void fco_partition_tiles(int nbatches, const int *port, uint32_t n, uint32_t tile,
+                         uint32_t *perm, uint16_t *tile_count);
 
 #ifdef __cplusplus
 }

@@ -41,6 +41,10 @@ def load():
     lib.fco_ip6flowid_hash.argtypes = [C.c_void_p, C.c_uint16, C.c_void_p, C.c_uint16]
     lib.fco_lb_hash_port.restype = C.c_int
     lib.fco_lb_hash_port.argtypes = [C.c_uint32, C.c_int]
+    lib.fco_process_batch2.restype = None
+    lib.fco_process_batch2.argtypes = [C.POINTER(N.fcgpu_cfg), C.c_void_p, C.c_void_p, C.c_uint32,
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_void_p, C.c_void_p]
     lib.fco_process_batch.restype = None
     lib.fco_process_batch.argtypes = [C.POINTER(N.fcgpu_cfg), C.c_void_p, C.c_void_p, C.c_uint32,
                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -66,11 +70,14 @@ def process_batch(cfg, batch):
     perm = np.zeros(n, np.uint32)
     start = np.zeros(cfg.nports + 2, np.uint32)
     ctr = np.zeros(N.NCOUNTERS, np.uint64)
-    lib.fco_process_batch(C.byref(cfg), _p(arena), _p(desc), n, _p(verdict), _p(hsh), _p(anno),
-                          _p(perm), _p(start), _p(ctr))
+    ntiles = (n + N.TILE - 1) // N.TILE
+    perm_tile = np.zeros(n, np.uint32)
+    tile_count = np.zeros(ntiles * (cfg.nports + 1), np.uint16)
+    lib.fco_process_batch2(C.byref(cfg), _p(arena), _p(desc), n, _p(verdict), _p(hsh), _p(anno),
+                           _p(perm), _p(start), _p(perm_tile), _p(tile_count), _p(ctr))
     return dict(verdict=verdict, reason=(verdict & 0xFF).astype(np.uint8),
                 port=(verdict >> 8).astype(np.uint8), hash=hsh, anno=anno, perm=perm,
-                port_start=start, counters=ctr)
+                port_start=start, perm_tile=perm_tile, tile_count=tile_count, counters=ctr)
 
 
 def in_cksum(data: bytes) -> int:

@@ -42,13 +42,14 @@ def _cfg_for_conf():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nsinks,batch", [(17, 0), (16, 0), (17, 4096)])
-def test_element_outputs_order_annotations(oracle, nsinks, batch):
+@pytest.mark.parametrize("nsinks,batch,part", [(17, 0, "TILE"), (16, 0, "TILE"), (17, 4096, "TILE"),
+                                               (17, 4096, "GLOBAL"), (16, 100000, "GLOBAL")])
+def test_element_outputs_order_annotations(oracle, nsinks, batch, part):
     from fastclick_amd import click as K
     b = synth.c4(20_000, seed=500)
     synth.add_ip_options(b, 0.1, seed=501)
     synth.inject_errors(b, 0.02, seed=502)
-    conf = CONF[:-1] + f", BATCH {batch})"
+    conf = CONF[:-1] + f", BATCH {batch}, PARTITION {part})"
     r = K.run_element(conf, b, burst=32, nsinks=nsinks)
     e = expected(b, _cfg_for_conf(), oracle)
     port = e["port"].astype(np.uint32)
@@ -70,7 +71,7 @@ def test_element_outputs_order_annotations(oracle, nsinks, batch):
     for i, line in enumerate(lines):
         assert line.endswith(N.REASON_TEXTS[i]) and " packets due to: " in line
         assert int(line.split()[0]) == int((e["reason"] == i).sum())
-    if batch:
+    if batch and part == "GLOBAL":
         assert r["batches"] <= 2 * 17 * (b.n // batch + 1) + 40
 
 

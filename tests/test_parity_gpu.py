@@ -29,11 +29,12 @@ def dev():
 
 
 def _check(dev, oracle, batch, cfg, ctx, anno=True, perm=True):
-    got = dev.process_batch(batch, cfg, anno=anno, perm=perm)
     exp = oracle.process_batch(cfg, batch)
-    compare(got, exp, anno=anno, perm=perm, ctx=ctx)
-    assert np.array_equal(got["counters"], exp["counters"]), \
-        f"{ctx}: counters {got['counters'][:12]} vs {exp['counters'][:12]}"
+    for part in (N.PART_GLOBAL, N.PART_TILE):
+        got = dev.process_batch(batch, cfg, anno=anno, perm=perm, partition=part)
+        compare(got, exp, anno=anno, perm=perm, ctx=f"{ctx} part={part}")
+        assert np.array_equal(got["counters"], exp["counters"]), \
+            f"{ctx}: counters {got['counters'][:12]} vs {exp['counters'][:12]}"
     return got, exp
 
 
@@ -189,7 +190,12 @@ def test_counters_accumulate_and_host_path(dev, oracle):
     anno = np.zeros(b.n, N.anno_dtype())
     perm = np.zeros(b.n, np.uint32)
     start = np.zeros(cfg.nports + 2, np.uint32)
-    for _ in range(3):
+    tc = np.zeros(((b.n + 255) // 256) * 17, np.uint16)
+    ptile = np.zeros(b.n, np.uint32)
+    ctx.process_host(ptrs, lens.ctypes.data, b.n, verdict=verdict.ctypes.data, perm=ptile.ctypes.data,
+                     tile_count=tc.ctypes.data, partition=N.PART_TILE)
+    assert np.array_equal(ptile, exp["perm_tile"]) and np.array_equal(tc, exp["tile_count"])
+    for _ in range(2):
         ctx.process_host(ptrs, lens.ctypes.data, b.n, verdict=verdict.ctypes.data,
                          hash=hsh.ctypes.data, anno=anno.ctypes.data, perm=perm.ctypes.data,
                          port_start=start.ctypes.data)
@@ -216,3 +222,5 @@ def test_large_batch_properties(dev, oracle):
         run = perm[start[p]:start[p + 1]]
         assert (np.diff(run.astype(np.int64)) > 0).all()
         assert (got["port"][run] == p).all()
+    gt = dev.process_batch(b, cfg, anno=False, perm=True, partition=N.PART_TILE)
+    assert np.array_equal(gt["perm_tile"], exp["perm_tile"]) and np.array_equal(gt["tile_count"], exp["tile_count"])
