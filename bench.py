@@ -50,6 +50,10 @@ def parse():
                     help="tile: each 256-packet tile is one classified PacketBatch (1 launch); "
                          "global: the whole batch is one (3 launches)")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
+    ap.add_argument("--timing-every", type=int, default=8,
+                    help="bracket every k-th step's kernels with HIP events (ext-launch "
+                         "start/stop on the launch stream); sampling keeps the event cost "
+                         "out of most steps")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -123,15 +127,21 @@ def main():
     # counters accumulate straight into a torch tensor so RCCL can reduce them
     ctr_t = torch.zeros(N.CTR_SHARDS, N.NCOUNTERS, dtype=torch.int64, device=dev)
     ctx.use_counters(ctr_t.data_ptr())
-    if not args.no_timing:
-        ctx.set_timing(True)
+    timing_on = not args.no_timing
+    if timing_on:
         ctx.read_timing()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    every = max(1, args.timing_every)
     for k in range(args.steps):
-        step(k)
+        if timing_on and k % every == 0:
+            ctx.set_timing(True)
+            step(k)
+            ctx.set_timing(False)
+        else:
+            step(k)
     if world > 1:
         # per-port / per-reason counters summed across GPUs: one RCCL all-reduce
         # of the device counter vector (xGMI), like PER_THREAD_SUM on read

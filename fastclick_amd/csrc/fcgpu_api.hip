@@ -224,6 +224,7 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     memset(&d, 0, sizeof(d));
     d.offset = cfg->offset;
     d.nports = cfg->nports;
+    d.lb_magic = cfg->nports > 1 ? (uint32_t)((((uint64_t)1 << 32) + cfg->nports - 1) / cfg->nports) : 0u;
     d.hash_mode = cfg->hash_mode;
     d.classify = cfg->classify;
     d.hs_offset = cfg->hs_offset;

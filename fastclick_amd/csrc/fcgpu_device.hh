@@ -27,6 +27,7 @@ constexpr int kMaxBins = FCGPU_MAX_PORTS + 1 + FCGPU_NREASON_SLOTS;
 struct DevCfg {
     int32_t offset;
     uint32_t nports;
+    uint32_t lb_magic;       // ceil(2^32 / nports): x % nports for x < 2^16 (fastmod)
     uint32_t hash_mode;
     uint32_t classify;
     int32_t hs_offset;
@@ -112,8 +113,15 @@ __device__ __forceinline__ bool cksum_ok(const FrameView &f, uint32_t o, uint32_
     return t == 0xffff;
 }
 
-__device__ __forceinline__ int lb_port(uint32_t h, uint32_t n) {
-    return (int)(((h >> 16) ^ (h & 0xffff)) % n);
+// ((h >> 16) ^ (h & 0xffff)) % n (loadbalancer.hh:580-584). The folded value is
+// < 2^16, so with m = ceil(2^32 / n): q = (x * m) >> 32 is exact (x * (m*n - 2^32)
+// ceil error e = m*n - 2^32 < n, and x*e < 2^16 * 64 < 2^32 keeps the quotient
+// exact; n = 1 is special-cased (m would not fit). Checked exhaustively in
+// tests/test_abi.py::test_lb_fastmod_exhaustive).
+__device__ __forceinline__ int lb_port(uint32_t h, uint32_t n, uint32_t m) {
+    const uint32_t x = (h >> 16) ^ (h & 0xffff);
+    const uint32_t q = __umulhi(x, m);
+    return n == 1 ? 0 : (int)(x - q * n);
 }
 
 // HashSwitch::process / LoadBalancer::hash_ip byte-sum (hashswitch.cc:50-66,
@@ -245,7 +253,7 @@ __device__ __forceinline__ void process_packet(const DevCfg &c, const FrameView 
     }
     r.hash = hv;
     switch (c.classify) {
-    case FCGPU_CLS_LB_HASH: r.port = (uint32_t)lb_port(hv, c.nports); break;
+    case FCGPU_CLS_LB_HASH: r.port = (uint32_t)lb_port(hv, c.nports, c.lb_magic); break;
     case FCGPU_CLS_HASH_IP: r.port = (uint32_t)bytesum_port(f, an.length, 26, 8, c.nports); break;
     case FCGPU_CLS_HASHSWITCH:
         r.port = (uint32_t)bytesum_port(f, an.length, c.hs_offset, c.hs_length, c.nports);
@@ -254,12 +262,93 @@ __device__ __forceinline__ void process_packet(const DevCfg &c, const FrameView 
     }
 }
 
+// Straight-line IPv4 fast path (CheckIPHeader -> AggregateHash -> classify) for
+// the common shape: IP header + first L4 word inside the 64-B LDS window and
+// no IP options. Reads 7 LDS dwords, no global loads, no data-dependent
+// branches except the (wave-uniform) configuration. Returns false when this
+// lane needs the general path (options, header beyond the window, hash modes
+// or classifiers it does not cover); the caller then runs process_packet.
+template <bool CK>
+__device__ __forceinline__ bool ip4_fast(const DevCfg &c, const FrameView &f, uint32_t len, PktResult &r) {
+    const uint32_t o = (uint32_t)c.offset;
+    const uint32_t x = f.shift + o, a = x & ~3u, sh = x & 3u;
+    if (a + 28 > (uint32_t)kWin) return false;
+    uint32_t w[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j)
+        w[j] = *reinterpret_cast<const uint32_t *>(f.row + (((((a + 4 * j) >> 4) ^ f.sw) << 4) | ((a + 4 * j) & 15)));
+    uint32_t h[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) h[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+    const uint32_t plen = len - o;
+    const uint32_t b0 = h[0] & 0xff, hlen = (b0 & 15) << 2, L = bswap16(h[0] >> 16);
+    uint32_t reason;
+    if ((int)plen < 20) reason = FCGPU_R_MINISCULE;
+    else if ((b0 >> 4) != 4) reason = FCGPU_R_BAD_VERSION;
+    else if (hlen < 20) reason = FCGPU_R_BAD_HLEN;
+    else if (L > plen || L < hlen) reason = FCGPU_R_BAD_IP_LEN;
+    else if (hlen != 20) return false;                 // IP options: general path
+    else {
+        reason = FCGPU_R_OK;
+        if (CK) {
+            uint64_t sum = (uint64_t)h[0] + h[1] + h[2] + h[3] + h[4];
+            sum = (sum & 0xffffffffu) + (sum >> 32);
+            uint32_t t = (uint32_t)sum + (uint32_t)(sum >> 32);
+            t = (t & 0xffff) + (t >> 16);
+            t = (t & 0xffff) + (t >> 16);
+            if (t != 0xffff) reason = FCGPU_R_BAD_CKSUM;
+        }
+        if (reason == FCGPU_R_OK && c.nbadsrc) {
+            bool bad = false, good = false;
+            for (uint32_t j = 0; j < c.nbadsrc; ++j) bad |= (c.badsrc[j] == h[3]);
+            for (uint32_t j = 0; j < c.ngooddst; ++j) good |= (c.gooddst[j] == h[4]);
+            if (bad && !good) reason = FCGPU_R_BAD_SADDR;
+        }
+    }
+    r.reason = reason;
+    r.hash = 0;
+    if (reason != FCGPU_R_OK) {
+        r.port = c.nports;
+        return true;
+    }
+    fcgpu_anno &an = r.an;
+    an.ipver = 4;
+    an.nh = (uint8_t)o;
+    an.th = (uint8_t)(o + 20);
+    an.length = (uint16_t)(plen > L ? len - (plen - L) : len);
+    an.dst_ip = h[4];
+    uint32_t hv = 0;
+    if (c.hash_mode != FCGPU_HASH_NONE) {
+        const uint32_t s = bswap16(h[5] & 0xffff), d = bswap16(h[5] >> 16);
+        if ((bswap16(h[1] >> 16) & 0x1fff) == 0)
+            hv = rotl32(h[3], (s & 15) + 1) ^ rotl32(h[4], 31 - (d & 15)) ^ ((d << 16) | s);
+        if (c.hash_mode == FCGPU_HASH_FLOW5ID) hv ^= (h[2] >> 8) & 0xff;
+    }
+    r.hash = hv;
+    if (c.classify == FCGPU_CLS_LB_HASH) r.port = (uint32_t)lb_port(hv, c.nports, c.lb_magic);
+    else if (c.classify == FCGPU_CLS_NONE) r.port = 0;
+    else return false;                                 // byte-sum classifiers: general path
+    return true;
+}
+
 __device__ __forceinline__ void glds16(const uint8_t *src, uint8_t *lds) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                      (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
 }
 
 __device__ __forceinline__ uint32_t reason_slot(uint32_t r) { return r < 6 ? r : r - 1; }
+
+// Lanes of this wave whose `key` equals mine, among the lanes in `live`
+// (a match-any built from one ballot per key bit: the cost depends on the key
+// width, not on how many distinct keys the wave holds).
+__device__ __forceinline__ uint64_t match_any(uint32_t key, uint32_t nbits, uint64_t live) {
+    uint64_t m = live;
+    for (uint32_t k = 0; k < nbits; ++k) {
+        const uint64_t bk = __ballot((key >> k) & 1u);
+        m &= ((key >> k) & 1u) ? bk : ~bk;
+    }
+    return m;
+}
 
 // Partition modes of k_rx
 constexpr int kPartNone = 0;     // counters only
@@ -270,14 +359,14 @@ constexpr int kPartTile = 2;     // + stable partition of each 256-packet tile, 
 // -> classify over one 256-packet tile; per-tile histogram by wave ballots;
 // counters by sharded atomics; optionally the tile's stable per-output
 // partition (CLASSIFY_EACH_PACKET on a 256-packet PacketBatch).
-template <int CM, bool CK, int PART>
-__global__ __launch_bounds__(kTile) void k_rx(RxArgs A) {
+template <int CM, bool CK, int PART, bool FAST = (CM == FCGPU_CHECK_IP4)>
+__global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4 * kWave * kWin];
     __shared__ uint32_t s_cnt[4][kMaxBins];
-    __shared__ uint32_t s_base[FCGPU_MAX_PORTS + 2];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // grid-stride over tiles (grid == ntiles: one tile per workgroup)
-    for (uint32_t tile = blockIdx.x; tile < A.ntiles; tile += gridDim.x) {
+    // one 256-packet tile per workgroup (grid == ntiles). A grid-stride loop
+    // measured slower here: hoisted loop invariants spill around it.
+    const uint32_t tile = blockIdx.x;
     const uint32_t i = tile * kTile + threadIdx.x;
     const bool live = i < A.n;
     uint2 d = make_uint2(0, 0);
@@ -303,8 +392,19 @@ __global__ __launch_bounds__(kTile) void k_rx(RxArgs A) {
     PktResult r;
     r.an = fcgpu_anno{};
     uint32_t bin = 0xffffffffu, rslot = 0xffffffffu;
-    if (live) {
+    if (FAST && CM == FCGPU_CHECK_IP4) {
+        bool done = !live;
+        if (live) done = ip4_fast<CK>(A.cfg, f, d.y, r);
+        if (__ballot(!done)) {
+            if (!done) {
+                r.an = fcgpu_anno{};
+                process_packet<CM, CK>(A.cfg, f, d.y, r);
+            }
+        }
+    } else if (live) {
         process_packet<CM, CK>(A.cfg, f, d.y, r);
+    }
+    if (live) {
         if (A.verdict) A.verdict[i] = (uint16_t)(r.reason | (r.port << 8));
         if (A.hash) A.hash[i] = r.hash;
         if (A.anno) A.anno[i] = r.an;
@@ -312,19 +412,21 @@ __global__ __launch_bounds__(kTile) void k_rx(RxArgs A) {
         if (r.reason != FCGPU_R_OK) rslot = reason_slot(r.reason);
     }
 
-    // per-wave histogram by ballot: outputs 0..nports (nports = invalid list)
+    // per-wave histogram: outputs 0..nports (nports = invalid list) by
+    // match-any; each group's first lane writes its count, absent outputs 0
     const uint32_t nb = A.cfg.nports + 1;
+    const uint32_t nbits = 32 - __clz(nb - 1 | 1);
     const uint64_t lt = (1ull << lane) - 1ull;
-    uint32_t rank = 0;
-    for (uint32_t b = 0; b < nb; ++b) {
-        const uint64_t m = __ballot(bin == b);
-        if (PART == kPartTile && bin == b) rank = (uint32_t)__popcll(m & lt);
-        if (lane == 0) s_cnt[wave][b] = (uint32_t)__popcll(m);
-    }
+    const uint64_t mlive = __ballot(live);
+    const uint64_t grp = match_any(bin, nbits, mlive);
+    const uint32_t rank = (uint32_t)__popcll(grp & lt);
+    for (uint32_t b = lane; b < nb + FCGPU_NREASON_SLOTS; b += 64) s_cnt[wave][b] = 0;
+    __builtin_amdgcn_wave_barrier();
+    if (live && rank == 0) s_cnt[wave][bin] = (uint32_t)__popcll(grp);
     const uint64_t mbad = __ballot(rslot != 0xffffffffu);
-    for (uint32_t s = 0; s < FCGPU_NREASON_SLOTS; ++s) {
-        const uint32_t c = mbad ? (uint32_t)__popcll(__ballot(rslot == s)) : 0u;
-        if (lane == 0) s_cnt[wave][nb + s] = c;
+    if (mbad) {   // rare: per-reason counts
+        const uint64_t g2 = match_any(rslot, 3, mbad);
+        if (rslot != 0xffffffffu && __popcll(g2 & lt) == 0) s_cnt[wave][nb + rslot] = (uint32_t)__popcll(g2);
     }
     __syncthreads();
     const uint32_t nbt = nb + FCGPU_NREASON_SLOTS;
@@ -334,17 +436,34 @@ __global__ __launch_bounds__(kTile) void k_rx(RxArgs A) {
     if (PART == kPartGlobal && t < nb) A.tilecnt[t * A.ntiles + tile] = tot;
     if (PART == kPartTile) {
         if (t < nb) A.tile_count[(size_t)tile * nb + t] = (uint16_t)tot;
-        // exclusive scan of the tile's output totals (wave 0; nb <= 65)
-        if (wave == 0) {
-            uint32_t v = lane < nb ? tot : 0u, incl = v;
+        // every wave scans the tile's output totals in registers (lane = output,
+        // nb <= 65: output 64 rides in lane 63's inclusive sum) and adds the
+        // counts of the waves before it, then each lane fetches its output's
+        // start with one lane shuffle -- no second block barrier, no LDS base
+        uint32_t v = 0, wpre = 0;
+        if (lane < nb) {
 #pragma unroll
-            for (int dl = 1; dl < 64; dl <<= 1) {
-                const uint32_t u = __shfl_up(incl, dl);
-                if (lane >= (uint32_t)dl) incl += u;
+            for (uint32_t w = 0; w < 4; ++w) {
+                const uint32_t c = s_cnt[w][lane];
+                v += c;
+                wpre += w < wave ? c : 0u;
             }
-            if (lane < nb) s_base[lane] = incl - v;
-            if (lane == 63) s_base[64] = incl;   // base of output 64 (nports == 64)
         }
+        uint32_t incl = v;
+#pragma unroll
+        for (int dl = 1; dl < 64; dl <<= 1) {
+            const uint32_t u = __shfl_up(incl, dl);
+            if (lane >= (uint32_t)dl) incl += u;
+        }
+        const uint32_t start = incl - v + wpre;   // lane b: start of output b for this wave
+        uint32_t mine = __shfl(start, (int)(bin & 63));
+        if (nb > 64) {   // output 64 (nports == 64): base = sum of outputs 0..63
+            uint32_t w64 = 0;
+            for (uint32_t w = 0; w < wave; ++w) w64 += s_cnt[w][64];
+            const uint32_t s64 = __shfl(incl, 63) + w64;
+            if (bin == 64) mine = s64;
+        }
+        if (live) A.perm[(size_t)tile * kTile + mine + rank] = i;
     }
     // counters: one atomic per non-zero bin per tile, sharded by tile
     if (t < nbt) {
@@ -358,16 +477,6 @@ __global__ __launch_bounds__(kTile) void k_rx(RxArgs A) {
             if (tot) atomicAdd(&ctr[FCGPU_CTR_DROPS], (unsigned long long)tot);
             if (live_n - tot) atomicAdd(&ctr[FCGPU_CTR_COUNT], (unsigned long long)(live_n - tot));
         }
-    }
-    if (PART == kPartTile) {
-        __syncthreads();
-        if (live) {
-            uint32_t wpre = 0;
-            for (uint32_t w = 0; w < wave; ++w) wpre += s_cnt[w][bin];
-            A.perm[(size_t)tile * kTile + s_base[bin] + wpre + rank] = i;
-        }
-    }
-    __syncthreads();   // s_cnt / s_base / s_win reused by the next tile
     }
 }
 
@@ -433,13 +542,12 @@ __global__ __launch_bounds__(kTile) void k_part(const uint16_t *verdict, uint32_
     }
     const bool live = i < n;
     const uint32_t bin = live ? (uint32_t)(verdict[i] >> 8) : 0xffffffffu;
-    uint32_t rank = 0;
     const uint64_t lt = (1ull << lane) - 1ull;
-    for (uint32_t b = 0; b < nb; ++b) {
-        const uint64_t m = __ballot(bin == b);
-        if (bin == b) rank = (uint32_t)__popcll(m & lt);
-        if (lane == 0) s_cnt[wave][b] = (uint32_t)__popcll(m);
-    }
+    const uint64_t grp = match_any(bin, 32 - __clz(nb - 1 | 1), __ballot(live));
+    const uint32_t rank = (uint32_t)__popcll(grp & lt);
+    for (uint32_t b = lane; b < nb; b += 64) s_cnt[wave][b] = 0;
+    __builtin_amdgcn_wave_barrier();
+    if (live && rank == 0) s_cnt[wave][bin] = (uint32_t)__popcll(grp);
     __syncthreads();
     if (live) {
         uint32_t wpre = 0;

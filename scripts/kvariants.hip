@@ -127,6 +127,7 @@ int main(int argc, char **argv) {
     memset(&A.cfg, 0, sizeof(A.cfg));
     A.cfg.offset = 14;
     A.cfg.nports = nports;
+    A.cfg.lb_magic = (uint32_t)((((uint64_t)1 << 32) + nports - 1) / nports);
     A.cfg.hash_mode = FCGPU_HASH_FLOWID;
     A.cfg.classify = FCGPU_CLS_LB_HASH;
     const double bytes = 72.0 * n;
@@ -184,13 +185,11 @@ int main(int argc, char **argv) {
             else hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, X);
         };
     };
-    run("k_rx none  grid=tiles", rx(k_rx<FCGPU_CHECK_IP4, true, kPartNone>, ntiles));
-    run("k_rx tile  grid=tiles", rx(k_rx<FCGPU_CHECK_IP4, true, kPartTile>, ntiles));
-    for (uint32_t g : {256u * 2, 256u * 4, 256u * 6, 256u * 8}) {
-        char nm[64];
-        snprintf(nm, sizeof nm, "k_rx tile  grid=%u", g);
-        run(nm, rx(k_rx<FCGPU_CHECK_IP4, true, kPartTile>, g));
-    }
-    run("k_rx global grid=tiles", rx(k_rx<FCGPU_CHECK_IP4, true, kPartGlobal>, ntiles));
+    run("k_rx none", rx(k_rx<FCGPU_CHECK_IP4, true, kPartNone>, ntiles));
+    run("k_rx none fast", rx(k_rx<FCGPU_CHECK_IP4, true, kPartNone, true>, ntiles));
+    run("k_rx tile", rx(k_rx<FCGPU_CHECK_IP4, true, kPartTile>, ntiles));
+    run("k_rx tile fast", rx(k_rx<FCGPU_CHECK_IP4, true, kPartTile, true>, ntiles));
+    run("k_rx global", rx(k_rx<FCGPU_CHECK_IP4, true, kPartGlobal>, ntiles));
+    run("k_rx global fast", rx(k_rx<FCGPU_CHECK_IP4, true, kPartGlobal, true>, ntiles));
     return 0;
 }

@@ -60,3 +60,14 @@ def test_fcclick_exports_every_declared_symbol():
     lib = K.load()
     for n in names:
         assert hasattr(lib, n), n
+
+
+def test_lb_fastmod_exhaustive():
+    """The device computes ((H>>16)^(H&0xffff)) % n as x - umulhi(x, ceil(2^32/n)) * n
+    (fcgpu_device.hh lb_port); exact for every 16-bit x and every n <= 64."""
+    import numpy as np
+    x = np.arange(1 << 16, dtype=np.uint64)
+    for n in range(2, 65):
+        m = ((1 << 32) + n - 1) // n
+        q = (x * np.uint64(m)) >> np.uint64(32)
+        assert np.array_equal(x - q * np.uint64(n), x % np.uint64(n)), n
