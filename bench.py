@@ -54,6 +54,9 @@ def parse():
                     help="bracket every k-th step's kernels with HIP events (ext-launch "
                          "start/stop on the launch stream); sampling keeps the event cost "
                          "out of most steps")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse "
+                         "several ranks on one GPU)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -92,10 +95,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    gpu = local % max(ndev, 1)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    local = gpu
 
     from fastclick_amd import synth, _native as N
     from fastclick_amd.device import DeviceBatch, DeviceOutputs
@@ -145,15 +154,16 @@ def main():
     if world > 1:
         # per-port / per-reason counters summed across GPUs: one RCCL all-reduce
         # of the device counter vector (xGMI), like PER_THREAD_SUM on read
-        glob = ctr_t.sum(0)
-        dist.all_reduce(glob)
+        from fastclick_amd.dist import reduce_counters
+        glob = reduce_counters(ctr_t if args.backend == "nccl" else ctr_t.cpu())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         total_valid = int(glob[N.CTR_COUNT].item())
