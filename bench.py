@@ -122,7 +122,11 @@ def main():
     part = N.PART_TILE if args.partition == "tile" else N.PART_GLOBAL
     outs = DeviceOutputs(n, args.nports, device=dev, verdict=True, hash=True, anno=False,
                          perm=not args.no_perm, port_start=not args.no_perm, partition=part)
-    stream = torch.cuda.current_stream(dev)
+    # one explicit stream carries the kernels, the counter all-reduce and the
+    # timing events, so RCCL (which runs on the current stream) is ordered after
+    # the last kernel
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
     optr = outs.ptrs()
 

@@ -247,7 +247,7 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "batch larger than max_batch");
     if (n == 0) return FCGPU_OK;
     if (!d_arena || !d_desc) return fail(c, FCGPU_EINVAL, "null arena/desc");
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream, as in HIP
     HIPCHK(c, hipSetDevice(c->device));
     const uint32_t ntiles = (n + kTile - 1) / kTile;
     const uint32_t nports = c->cfg.nports;

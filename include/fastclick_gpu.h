@@ -175,8 +175,8 @@ int  fcgpu_configure(fcgpu_ctx *ctx, const fcgpu_cfg *cfg);
 void fcgpu_close(fcgpu_ctx *ctx);
 
 /* Device-resident batch: arena, desc and every output pointer are device
- * memory. Asynchronous on `stream` (hipStream_t, NULL = the context's stream).
- * Completion: synchronise that stream. */
+ * memory. Asynchronous on `stream` (a hipStream_t; NULL = the HIP null stream,
+ * as everywhere in HIP). Completion: synchronise that stream. */
 int  fcgpu_process(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_desc,
                    uint32_t n, const fcgpu_out *d_out, void *stream);
 
