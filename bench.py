@@ -54,6 +54,10 @@ def parse():
                     help="bracket every k-th step's kernels with HIP events (ext-launch "
                          "start/stop on the launch stream); sampling keeps the event cost "
                          "out of most steps")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="HIP streams the consecutive steps alternate over (each with its own "
+                         "context and output buffers), so one batch's tail overlaps the next "
+                         "batch's head, as back-to-back NIC batches would")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse "
                          "several ranks on one GPU)")
@@ -118,31 +122,42 @@ def main():
     del host
     cfg = N.make_cfg(offset=14, checksum=True, hash_mode=N.HASH_FLOWID, classify=N.CLS_LB_HASH,
                      nports=args.nports)
-    ctx = N.Context(local, n, cfg)
     part = N.PART_TILE if args.partition == "tile" else N.PART_GLOBAL
-    outs = DeviceOutputs(n, args.nports, device=dev, verdict=True, hash=True, anno=False,
-                         perm=not args.no_perm, port_start=not args.no_perm, partition=part)
-    # one explicit stream carries the kernels, the counter all-reduce and the
-    # timing events, so RCCL (which runs on the current stream) is ordered after
-    # the last kernel
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(stream)
-    sptr = stream.cuda_stream
-    optr = outs.ptrs()
+    tile = part == N.PART_TILE
+    nstreams = max(1, args.streams)
+    # per stream: its own context (workspace) and output buffers
+    ctxs, streams, optrs, outs_keep = [], [], [], []
+    for _ in range(nstreams):
+        ctxs.append(N.Context(local, n, cfg))
+        streams.append(torch.cuda.Stream(dev))
+        o = DeviceOutputs(n, args.nports, device=dev, verdict=True, hash=True, anno=False,
+                          perm=(not args.no_perm) and not tile, tile_perm=(not args.no_perm) and tile,
+                          port_start=not args.no_perm, partition=part)
+        outs_keep.append(o)
+        optrs.append(o.ptrs())
+    ctx = ctxs[0]
+    # the first stream also carries the counter all-reduce; it waits for the others
+    main_stream = streams[0]
+    torch.cuda.set_stream(main_stream)
 
     def step(k):
+        j = k % nstreams
         b = bufs[k % len(bufs)]
-        ctx.process(b.arena.data_ptr(), b.desc.data_ptr(), n, stream=sptr, **optr)
+        ctxs[j].process(b.arena.data_ptr(), b.desc.data_ptr(), n, stream=streams[j].cuda_stream,
+                        **optrs[j])
 
     for k in range(args.warmup):
         step(k)
     torch.cuda.synchronize()
     # counters accumulate straight into a torch tensor so RCCL can reduce them
     ctr_t = torch.zeros(N.CTR_SHARDS, N.NCOUNTERS, dtype=torch.int64, device=dev)
-    ctx.use_counters(ctr_t.data_ptr())
+    torch.cuda.synchronize()
+    for c in ctxs:
+        c.use_counters(ctr_t.data_ptr())
     timing_on = not args.no_timing
     if timing_on:
-        ctx.read_timing()
+        for c in ctxs:
+            c.read_timing()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -150,11 +165,14 @@ def main():
     every = max(1, args.timing_every)
     for k in range(args.steps):
         if timing_on and k % every == 0:
-            ctx.set_timing(True)
+            c = ctxs[k % nstreams]
+            c.set_timing(True)
             step(k)
-            ctx.set_timing(False)
+            c.set_timing(False)
         else:
             step(k)
+    for s_ in streams[1:]:
+        main_stream.wait_stream(s_)
     if world > 1:
         # per-port / per-reason counters summed across GPUs: one RCCL all-reduce
         # of the device counter vector (xGMI), like PER_THREAD_SUM on read
@@ -176,7 +194,11 @@ def main():
 
     timing = None
     if not args.no_timing:
-        ms, cnt = ctx.read_timing()
+        ms, cnt = [0.0] * 3, [0] * 3
+        for c in ctxs:
+            m_, c_ = c.read_timing()
+            ms = [a + b for a, b in zip(ms, m_)]
+            cnt = [a + b for a, b in zip(cnt, c_)]
         timing = dict(k_rx_ms=ms[0] / max(cnt[0], 1), k_scan_ms=ms[1] / max(cnt[1], 1),
                       k_part_ms=ms[2] / max(cnt[2], 1), launches=cnt)
 
@@ -227,6 +249,7 @@ def main():
                                 if args.partition == "tile" else
                                 " + stable per-port partition of the whole 1M-packet batch")),
                 "partition": "none" if args.no_perm else args.partition,
+                "streams": nstreams,
                 "packets_per_step_per_gpu": n,
                 "hbm_batches": args.nbuf,
                 "nports": args.nports,
@@ -236,7 +259,8 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -14,7 +14,7 @@ LIBFCGPU = os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 2
+ABI_VERSION = 3
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
     R_BAD_IP6, R_VLAN_REJECT = range(9)
@@ -92,6 +92,7 @@ class fcgpu_out(C.Structure):
         ("tile_count", C.c_void_p),
         ("partition", C.c_uint32),
         ("reserved", C.c_uint32),
+        ("tile_perm", C.c_void_p),
     ]
 
 
@@ -226,16 +227,16 @@ class Context:
         self.cfg = cfg
 
     def process(self, arena_ptr, desc_ptr, n, *, verdict=0, hash=0, anno=0, perm=0,
-                port_start=0, tile_count=0, partition=PART_GLOBAL, stream=0):
+                port_start=0, tile_count=0, partition=PART_GLOBAL, tile_perm=0, stream=0):
         out = fcgpu_out(verdict or None, hash or None, anno or None, perm or None,
-                        port_start or None, tile_count or None, partition, 0)
+                        port_start or None, tile_count or None, partition, 0, tile_perm or None)
         self._chk(self.lib.fcgpu_process(self.h, arena_ptr, desc_ptr, n, C.byref(out),
                                          stream or None), "fcgpu_process")
 
     def process_host(self, frames, lens_ptr, n, *, verdict=0, hash=0, anno=0, perm=0,
-                     port_start=0, tile_count=0, partition=PART_GLOBAL):
+                     port_start=0, tile_count=0, partition=PART_GLOBAL, tile_perm=0):
         out = fcgpu_out(verdict or None, hash or None, anno or None, perm or None,
-                        port_start or None, tile_count or None, partition, 0)
+                        port_start or None, tile_count or None, partition, 0, tile_perm or None)
         self._chk(self.lib.fcgpu_process_host(self.h, frames, lens_ptr, n, C.byref(out)),
                   "fcgpu_process_host")
 

@@ -56,6 +56,7 @@ struct fcgpu_ctx {
     uint16_t *d_hv = nullptr;
     uint32_t *d_hh = nullptr, *d_hperm = nullptr, *d_hstart = nullptr;
     uint16_t *d_htc = nullptr;
+    uint8_t *d_htp = nullptr;
     fcgpu_anno *d_hanno = nullptr;
     // timing
     bool timing = false;
@@ -165,6 +166,7 @@ void fcgpu_close(fcgpu_ctx *c) {
         hipFree(c->d_hstart);
         hipFree(c->d_hanno);
         hipFree(c->d_htc);
+        hipFree(c->d_htp);
         hipHostFree(c->h_arena);
         hipHostFree(c->h_desc);
         if (c->stream) hipStreamDestroy(c->stream);
@@ -188,7 +190,6 @@ int fcgpu_open(int device, uint32_t max_batch, fcgpu_ctx **out) {
         if (e != hipSuccess && rc == FCGPU_OK) rc = fail(c, FCGPU_ENOMEM, std::string(what) + ": " + hipGetErrorString(e));
     };
     chk(hipSetDevice(device), "hipSetDevice");
-    chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
     chk(hipMalloc(&c->d_tilecnt, sizeof(uint32_t) * (size_t)(FCGPU_MAX_PORTS + 1) * c->max_tiles), "hipMalloc tilecnt");
     chk(hipMalloc(&c->d_totals, sizeof(uint32_t) * kMaxBins), "hipMalloc totals");
     chk(hipMalloc(&c->d_ctr_own, sizeof(unsigned long long) * kCtrWords), "hipMalloc counters");
@@ -258,10 +259,11 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     }
     const bool tile = o->partition == FCGPU_PART_TILE;
     if (o->partition > FCGPU_PART_TILE) return fail(c, FCGPU_EINVAL, "bad partition mode");
-    if (tile && (!o->perm != !o->tile_count))
-        return fail(c, FCGPU_EINVAL, "FCGPU_PART_TILE needs both perm and tile_count");
+    const bool tperm = o->perm || o->tile_perm;
+    if (tile && (tperm != (o->tile_count != nullptr)))
+        return fail(c, FCGPU_EINVAL, "FCGPU_PART_TILE needs tile_count and perm and/or tile_perm");
     const bool want_global = !tile && (o->perm || o->port_start);
-    const int part = tile && o->perm ? kPartTile : (want_global ? kPartGlobal : kPartNone);
+    const int part = tile && tperm ? kPartTile : (want_global ? kPartGlobal : kPartNone);
     RxArgs a;
     a.arena = d_arena;
     a.desc = reinterpret_cast<const uint2 *>(d_desc);
@@ -273,6 +275,8 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     a.tilecnt = c->d_tilecnt;
     a.perm = o->perm;
     a.tile_count = o->tile_count;
+    a.tile_perm = tile ? o->tile_perm : nullptr;
+    if (tile) a.perm = o->perm;
     a.ctr = c->d_ctr;
     a.cfg = c->dcfg;
 
@@ -313,6 +317,9 @@ int fcgpu_process_host(fcgpu_ctx *c, const uint8_t *const *frames, const uint32_
     HIPCHK(c, hipSetDevice(c->device));
     const size_t arena_cap = (size_t)c->max_batch * kHostCap + kArenaPad;
     if (!c->h_arena) {
+        // the context's own stream exists only for the host-resident path (a
+        // stream per context maps onto one of the few hardware queues)
+        HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         HIPCHK(c, hipHostMalloc((void **)&c->h_arena, arena_cap, hipHostMallocDefault));
         HIPCHK(c, hipHostMalloc((void **)&c->h_desc, sizeof(uint32_t) * 2 * c->max_batch, hipHostMallocDefault));
         HIPCHK(c, hipMalloc(&c->d_arena, arena_cap));
@@ -324,6 +331,7 @@ int fcgpu_process_host(fcgpu_ctx *c, const uint8_t *const *frames, const uint32_
         HIPCHK(c, hipMalloc(&c->d_hstart, sizeof(uint32_t) * (FCGPU_MAX_PORTS + 2)));
         HIPCHK(c, hipMalloc(&c->d_hanno, sizeof(fcgpu_anno) * c->max_batch));
         HIPCHK(c, hipMalloc(&c->d_htc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * c->max_tiles));
+        HIPCHK(c, hipMalloc(&c->d_htp, (size_t)c->max_batch + kTile));
     }
     // gather: first min(len, 128) bytes of each frame at 64-B aligned offsets.
     // The device sees the real frame length; bytes past the capture are never
@@ -349,12 +357,14 @@ int fcgpu_process_host(fcgpu_ctx *c, const uint8_t *const *frames, const uint32_
     d.tile_count = h->tile_count ? c->d_htc : nullptr;
     d.partition = h->partition;
     d.reserved = 0;
+    d.tile_perm = h->tile_perm ? c->d_htp : nullptr;
     int rc = fcgpu_process(c, c->d_arena, c->d_desc, n, &d, s);
     if (rc != FCGPU_OK) return rc;
     if (h->verdict) HIPCHK(c, hipMemcpyAsync(h->verdict, d.verdict, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, s));
     if (h->hash) HIPCHK(c, hipMemcpyAsync(h->hash, d.hash, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
     if (h->anno) HIPCHK(c, hipMemcpyAsync(h->anno, d.anno, sizeof(fcgpu_anno) * n, hipMemcpyDeviceToHost, s));
     if (h->perm) HIPCHK(c, hipMemcpyAsync(h->perm, d.perm, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
+    if (h->tile_perm) HIPCHK(c, hipMemcpyAsync(h->tile_perm, d.tile_perm, n, hipMemcpyDeviceToHost, s));
     if (h->tile_count)
         HIPCHK(c, hipMemcpyAsync(h->tile_count, d.tile_count,
                                  sizeof(uint16_t) * (c->cfg.nports + 1) * ((n + kTile - 1) / kTile),
@@ -370,7 +380,6 @@ int fcgpu_read_counters(fcgpu_ctx *c, uint64_t *out, int n) {
     if (!c || !out || n < 0) return FCGPU_EINVAL;
     if (n > FCGPU_NCOUNTERS) n = FCGPU_NCOUNTERS;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipDeviceSynchronize());
     std::vector<uint64_t> all(kCtrWords);
     HIPCHK(c, hipMemcpy(all.data(), c->d_ctr, sizeof(uint64_t) * kCtrWords, hipMemcpyDeviceToHost));

@@ -52,6 +52,7 @@ struct RxArgs {
     uint32_t *tilecnt;     // [nports+1][ntiles] (kPartGlobal)
     uint32_t *perm;        // [n] tile-local partition (kPartTile)
     uint16_t *tile_count;  // [ntiles][nports+1] (kPartTile)
+    uint8_t *tile_perm;    // [n] tile-local partition (kPartTile)
     unsigned long long *ctr;   // [FCGPU_CTR_SHARDS][FCGPU_NCOUNTERS]
     DevCfg cfg;
 };
@@ -272,62 +273,64 @@ template <bool CK>
 __device__ __forceinline__ bool ip4_fast(const DevCfg &c, const FrameView &f, uint32_t len, PktResult &r) {
     const uint32_t o = (uint32_t)c.offset;
     const uint32_t x = f.shift + o, a = x & ~3u, sh = x & 3u;
-    if (a + 28 > (uint32_t)kWin) return false;
+    const bool inwin = a + 28 <= (uint32_t)kWin;
+    const uint32_t ab = inwin ? a : 0u;   // keep the LDS reads in the row either way
     uint32_t w[7];
 #pragma unroll
     for (int j = 0; j < 7; ++j)
-        w[j] = *reinterpret_cast<const uint32_t *>(f.row + (((((a + 4 * j) >> 4) ^ f.sw) << 4) | ((a + 4 * j) & 15)));
+        w[j] = *reinterpret_cast<const uint32_t *>(f.row + (((((ab + 4 * j) >> 4) ^ f.sw) << 4) | ((ab + 4 * j) & 15)));
     uint32_t h[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) h[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+    // CheckIPHeader::valid reason chain, computed as predicates (no divergent
+    // branches); the first failing check wins, as in the reference
     const uint32_t plen = len - o;
     const uint32_t b0 = h[0] & 0xff, hlen = (b0 & 15) << 2, L = bswap16(h[0] >> 16);
-    uint32_t reason;
-    if ((int)plen < 20) reason = FCGPU_R_MINISCULE;
-    else if ((b0 >> 4) != 4) reason = FCGPU_R_BAD_VERSION;
-    else if (hlen < 20) reason = FCGPU_R_BAD_HLEN;
-    else if (L > plen || L < hlen) reason = FCGPU_R_BAD_IP_LEN;
-    else if (hlen != 20) return false;                 // IP options: general path
-    else {
-        reason = FCGPU_R_OK;
-        if (CK) {
-            uint64_t sum = (uint64_t)h[0] + h[1] + h[2] + h[3] + h[4];
-            sum = (sum & 0xffffffffu) + (sum >> 32);
-            uint32_t t = (uint32_t)sum + (uint32_t)(sum >> 32);
-            t = (t & 0xffff) + (t >> 16);
-            t = (t & 0xffff) + (t >> 16);
-            if (t != 0xffff) reason = FCGPU_R_BAD_CKSUM;
-        }
-        if (reason == FCGPU_R_OK && c.nbadsrc) {
-            bool bad = false, good = false;
-            for (uint32_t j = 0; j < c.nbadsrc; ++j) bad |= (c.badsrc[j] == h[3]);
-            for (uint32_t j = 0; j < c.ngooddst; ++j) good |= (c.gooddst[j] == h[4]);
-            if (bad && !good) reason = FCGPU_R_BAD_SADDR;
-        }
+    const bool tiny = (int)plen < 20, badv = (b0 >> 4) != 4, badhl = hlen < 20;
+    const bool badlen = L > plen || L < hlen;
+    bool ckbad = false;
+    if (CK) {
+        uint64_t sum = (uint64_t)h[0] + h[1] + h[2] + h[3] + h[4];
+        uint32_t t = (uint32_t)sum + (uint32_t)(sum >> 32);      // fold the carries
+        t = (t < (uint32_t)sum) ? t + 1 : t;                       // end-around carry
+        t = (t & 0xffff) + (t >> 16);
+        t = (t & 0xffff) + (t >> 16);
+        ckbad = t != 0xffff;
     }
-    r.reason = reason;
-    r.hash = 0;
-    if (reason != FCGPU_R_OK) {
-        r.port = c.nports;
-        return true;
+    bool srcbad = false;
+    if (c.nbadsrc) {   // wave-uniform
+        bool bad = false, good = false;
+        for (uint32_t j = 0; j < c.nbadsrc; ++j) bad |= (c.badsrc[j] == h[3]);
+        for (uint32_t j = 0; j < c.ngooddst; ++j) good |= (c.gooddst[j] == h[4]);
+        srcbad = bad && !good;
     }
-    fcgpu_anno &an = r.an;
-    an.ipver = 4;
-    an.nh = (uint8_t)o;
-    an.th = (uint8_t)(o + 20);
-    an.length = (uint16_t)(plen > L ? len - (plen - L) : len);
-    an.dst_ip = h[4];
+    const uint32_t early = tiny ? FCGPU_R_MINISCULE : badv ? FCGPU_R_BAD_VERSION
+                         : badhl ? FCGPU_R_BAD_HLEN : badlen ? FCGPU_R_BAD_IP_LEN : FCGPU_R_OK;
+    // decline: header not in the window, or IP options deciding checksum/ports
+    if (!inwin || (early == FCGPU_R_OK && hlen != 20)) return false;
+    const uint32_t reason = early != FCGPU_R_OK ? early
+                          : ckbad ? FCGPU_R_BAD_CKSUM : srcbad ? FCGPU_R_BAD_SADDR : FCGPU_R_OK;
+    const bool ok = reason == FCGPU_R_OK;
     uint32_t hv = 0;
-    if (c.hash_mode != FCGPU_HASH_NONE) {
-        const uint32_t s = bswap16(h[5] & 0xffff), d = bswap16(h[5] >> 16);
-        if ((bswap16(h[1] >> 16) & 0x1fff) == 0)
-            hv = rotl32(h[3], (s & 15) + 1) ^ rotl32(h[4], 31 - (d & 15)) ^ ((d << 16) | s);
+    if (c.hash_mode != FCGPU_HASH_NONE) {   // wave-uniform
+        const uint32_t sp = bswap16(h[5] & 0xffff), dp = bswap16(h[5] >> 16);
+        const bool first = (bswap16(h[1] >> 16) & 0x1fff) == 0;
+        hv = first ? rotl32(h[3], (sp & 15) + 1) ^ rotl32(h[4], 31 - (dp & 15)) ^ ((dp << 16) | sp) : 0u;
         if (c.hash_mode == FCGPU_HASH_FLOW5ID) hv ^= (h[2] >> 8) & 0xff;
     }
-    r.hash = hv;
-    if (c.classify == FCGPU_CLS_LB_HASH) r.port = (uint32_t)lb_port(hv, c.nports, c.lb_magic);
-    else if (c.classify == FCGPU_CLS_NONE) r.port = 0;
+    uint32_t port;
+    if (c.classify == FCGPU_CLS_LB_HASH) port = (uint32_t)lb_port(hv, c.nports, c.lb_magic);
+    else if (c.classify == FCGPU_CLS_NONE) port = 0;
     else return false;                                 // byte-sum classifiers: general path
+    r.reason = reason;
+    r.hash = ok ? hv : 0u;
+    r.port = ok ? port : c.nports;
+    fcgpu_anno &an = r.an;
+    an.ipver = early == FCGPU_R_MINISCULE ? 0 : 4;
+    an.nh = (uint8_t)(ok ? o : 0u);
+    an.th = (uint8_t)(ok ? o + 20 : 0u);
+    an.length = (uint16_t)(ok ? (plen > L ? len - (plen - L) : len) : 0u);
+    an.dst_ip = ok ? h[4] : 0u;
     return true;
 }
 
@@ -463,7 +466,11 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
             const uint32_t s64 = __shfl(incl, 63) + w64;
             if (bin == 64) mine = s64;
         }
-        if (live) A.perm[(size_t)tile * kTile + mine + rank] = i;
+        if (live) {
+            const size_t pos = (size_t)tile * kTile + mine + rank;
+            if (A.perm) A.perm[pos] = i;
+            if (A.tile_perm) A.tile_perm[pos] = (uint8_t)threadIdx.x;
+        }
     }
     // counters: one atomic per non-zero bin per tile, sharded by tile
     if (t < nbt) {

@@ -144,6 +144,7 @@ class GPUIPCheckClassify : public Element {
         _hash.resize(_cap);
         _anno.resize(_cap);
         _perm.resize(_cap);
+        _tperm.resize(_cap + FCGPU_TILE);
         _start.resize(FCGPU_MAX_PORTS + 2);
         _tile_count.resize((size_t)(FCGPU_MAX_PORTS + 1) * ((_cap + FCGPU_TILE - 1) / FCGPU_TILE));
         return 0;
@@ -200,7 +201,8 @@ class GPUIPCheckClassify : public Element {
         o.verdict = _verdict.data();
         o.hash = _hash.data();
         o.anno = _anno.data();
-        o.perm = _perm.data();
+        o.perm = _partition == FCGPU_PART_GLOBAL ? _perm.data() : nullptr;
+        o.tile_perm = _partition == FCGPU_PART_TILE ? _tperm.data() : nullptr;
         o.partition = _partition;
         o.port_start = _partition == FCGPU_PART_GLOBAL ? _start.data() : nullptr;
         o.tile_count = _partition == FCGPU_PART_TILE ? _tile_count.data() : nullptr;
@@ -243,16 +245,18 @@ class GPUIPCheckClassify : public Element {
             // one batch per output in port order, input order within a port
             // (chunked to MAX_BATCH_SIZE, include/click/packetbatch.hh:416)
             for (uint32_t port = 0; port < nb; ++port)
-                emit_run(port, _start[port], _start[port + 1]);
+                emit_run(port, _start[port], _start[port + 1], [this](uint32_t j) { return _perm[j]; });
         } else {
             // every FCGPU_TILE-packet tile is one classified PacketBatch: its
             // runs leave in port order, tiles in input order
             const uint32_t ntiles = (n + FCGPU_TILE - 1) / FCGPU_TILE;
             for (uint32_t t = 0; t < ntiles; ++t) {
-                uint32_t s = t * FCGPU_TILE;
+                const uint32_t base = t * FCGPU_TILE;
+                uint32_t s = base;
+                auto idx = [this, base](uint32_t j) { return base + _tperm[j]; };
                 for (uint32_t port = 0; port < nb; ++port) {
                     const uint32_t c = _tile_count[(size_t)t * nb + port];
-                    emit_run(port, s, s + c);
+                    emit_run(port, s, s + c, idx);
                     s += c;
                 }
             }
@@ -260,12 +264,14 @@ class GPUIPCheckClassify : public Element {
         _pkts.clear();
     }
 
-    void emit_run(uint32_t port, uint32_t s, uint32_t e) {
+    // link packets idx(s) .. idx(e-1) into PacketBatches of <= MAX_BATCH_SIZE
+    template <class Idx>
+    void emit_run(uint32_t port, uint32_t s, uint32_t e, Idx idx) {
         while (s < e) {
             uint32_t m = e - s < kMaxBatch ? e - s : kMaxBatch;
-            Packet *head = _pkts[_perm[s]], *prev = head;
+            Packet *head = _pkts[idx(s)], *prev = head;
             for (uint32_t j = 1; j < m; ++j) {
-                Packet *q = _pkts[_perm[s + j]];
+                Packet *q = _pkts[idx(s + j)];
                 prev->set_next(q);
                 prev = q;
             }
@@ -289,6 +295,7 @@ class GPUIPCheckClassify : public Element {
     std::vector<uint32_t> _hash;
     std::vector<fcgpu_anno> _anno;
     std::vector<uint32_t> _perm;
+    std::vector<uint8_t> _tperm;
     std::vector<uint32_t> _start;
     std::vector<uint16_t> _tile_count;
     uint32_t _partition = FCGPU_PART_TILE;

@@ -35,7 +35,7 @@ class DeviceBatch:
 
 class DeviceOutputs:
     def __init__(self, n, nports, device="cuda", *, verdict=True, hash=True, anno=False,
-                 perm=False, port_start=False, partition=N.PART_GLOBAL):
+                 perm=False, port_start=False, partition=N.PART_GLOBAL, tile_perm=False):
         torch = _torch()
         self.n = n
         self.nports = nports
@@ -44,17 +44,19 @@ class DeviceOutputs:
         self.verdict = mk(n, torch.int16) if verdict else None
         self.hash = mk(n, torch.int32) if hash else None
         self.anno = mk(n * 16, torch.uint8) if anno else None
-        self.perm = mk(n, torch.int32) if perm else None
         tile = partition == N.PART_TILE
+        self.perm = mk(n, torch.int32) if perm else None
+        self.tile_perm = mk(n, torch.uint8) if (tile and (tile_perm or perm)) else None
         self.port_start = mk(nports + 2, torch.int32) if port_start and not tile else None
         ntiles = (n + N.TILE - 1) // N.TILE
-        self.tile_count = mk(ntiles * (nports + 1), torch.int16) if perm and tile else None
+        self.tile_count = mk(ntiles * (nports + 1), torch.int16) if (perm or tile_perm) and tile else None
 
     def ptrs(self):
         p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
         return dict(verdict=p(self.verdict), hash=p(self.hash), anno=p(self.anno),
                     perm=p(self.perm), port_start=p(self.port_start),
-                    tile_count=p(self.tile_count), partition=self.partition)
+                    tile_count=p(self.tile_count), partition=self.partition,
+                    tile_perm=p(self.tile_perm))
 
     def numpy(self):
         out = {}
@@ -72,6 +74,8 @@ class DeviceOutputs:
             out[key] = self.perm.cpu().numpy().view(np.uint32)
         if self.tile_count is not None:
             out["tile_count"] = self.tile_count.cpu().numpy().view(np.uint16)
+        if self.tile_perm is not None:
+            out["tile_perm"] = self.tile_perm.cpu().numpy()
         if self.port_start is not None:
             out["port_start"] = self.port_start.cpu().numpy().view(np.uint32)
         return out

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 2
+#define FCGPU_ABI_VERSION 3
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -130,8 +130,10 @@ typedef struct fcgpu_anno {
  *   FCGPU_PART_TILE: the batch is a sequence of FCGPU_TILE-packet PacketBatches
  *       (the element's input batches), each partitioned on its own, exactly as
  *       a ClassifyElement partitions every batch it receives. Tile t's entries
- *       are perm[t*FCGPU_TILE ...], grouped by output; tile_count[t*(nports+1)+b]
- *       is the size of output b's run in tile t. One fused launch.           */
+ *       are perm[t*FCGPU_TILE ...] (packet index) and/or tile_perm[t*FCGPU_TILE
+ *       ...] (index within the tile, 1 byte), grouped by output;
+ *       tile_count[t*(nports+1)+b] is the size of output b's run in tile t.
+ *       One fused launch.                                                   */
 #define FCGPU_PART_GLOBAL 0
 #define FCGPU_PART_TILE   1
 #define FCGPU_TILE        256
@@ -145,6 +147,7 @@ typedef struct fcgpu_out {
     uint16_t   *tile_count;   /* TILE: [ceil(n/FCGPU_TILE)][nports+1] run sizes          */
     uint32_t    partition;    /* FCGPU_PART_GLOBAL or FCGPU_PART_TILE                    */
     uint32_t    reserved;
+    uint8_t    *tile_perm;    /* TILE: [n] index within the tile, grouped by output      */
 } fcgpu_out;
 
 typedef struct fcgpu_ctx fcgpu_ctx;

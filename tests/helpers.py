@@ -58,6 +58,9 @@ def compare(got: dict, exp: dict, *, keys=("reason", "port", "hash"), anno=True,
     if perm and "perm" in got:
         assert np.array_equal(got["port_start"], exp["port_start"]), f"{ctx}: port_start"
         assert np.array_equal(got["perm"], exp["perm"]), f"{ctx}: perm"
+    if perm and "tile_perm" in got:
+        local = (exp["perm_tile"] % 256).astype(np.uint8)
+        assert np.array_equal(got["tile_perm"], local), f"{ctx}: tile_perm"
     if perm and "perm_tile" in got:
         assert np.array_equal(got["tile_count"], exp["tile_count"]), f"{ctx}: tile_count"
         assert np.array_equal(got["perm_tile"], exp["perm_tile"]), f"{ctx}: perm_tile"
