@@ -14,17 +14,20 @@ LIBFCGPU = os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 3
+ABI_VERSION = 4
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
-    R_BAD_IP6, R_VLAN_REJECT = range(9)
-NREASON_SLOTS = 8
+    R_BAD_IP6, R_VLAN_REJECT, R_NO_MATCH = range(10)
+NREASON_SLOTS = 9
 CHECK_IP4, MARK_IP4, CHECK_AUTO = 0, 1, 2
 HASH_NONE, HASH_FLOWID, HASH_FLOW5ID = 0, 1, 2
-CLS_NONE, CLS_LB_HASH, CLS_HASH_IP, CLS_HASHSWITCH = 0, 1, 2, 3
+CLS_NONE, CLS_LB_HASH, CLS_HASH_IP, CLS_HASHSWITCH, CLS_PROGRAM = 0, 1, 2, 3, 4
+PROG_IPFILTER, PROG_CLASSIFIER = 0, 1
+STEP_SHORT_YES = 1
+MAX_STEPS = 8192
 MAX_PORTS = 64
 MAX_ADDRS = 16
-CTR_COUNT, CTR_DROPS, CTR_REASON, CTR_PORT = 0, 1, 2, 10
+CTR_COUNT, CTR_DROPS, CTR_REASON, CTR_PORT = 0, 1, 2, 11
 NCOUNTERS = CTR_PORT + MAX_PORTS + 1
 CTR_SHARDS = 64
 PART_GLOBAL, PART_TILE = 0, 1
@@ -96,6 +99,17 @@ class fcgpu_out(C.Structure):
     ]
 
 
+class fcgpu_step(C.Structure):
+    _fields_ = [
+        ("offset", C.c_int32),
+        ("value", C.c_uint32),
+        ("mask", C.c_uint32),
+        ("yes", C.c_int32),
+        ("no", C.c_int32),
+        ("flags", C.c_uint32),
+    ]
+
+
 # Every symbol include/fastclick_gpu.h declares (checked by tests/test_abi.py).
 FCGPU_SYMBOLS = {
     "fcgpu_abi_version": (C.c_int, []),
@@ -108,6 +122,8 @@ FCGPU_SYMBOLS = {
                                 C.POINTER(fcgpu_out), C.c_void_p]),
     "fcgpu_process_host": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_void_p, C.c_uint32,
                                      C.POINTER(fcgpu_out)]),
+    "fcgpu_set_program": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(fcgpu_step), C.c_uint32,
+                                    C.c_int32]),
     "fcgpu_read_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "fcgpu_reset_counters": (C.c_int, [C.c_void_p]),
     "fcgpu_counters_device": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
@@ -239,6 +255,14 @@ class Context:
                         port_start or None, tile_count or None, partition, 0, tile_perm or None)
         self._chk(self.lib.fcgpu_process_host(self.h, frames, lens_ptr, n, C.byref(out)),
                   "fcgpu_process_host")
+
+    def set_program(self, kind, steps, output_everything=-1):
+        """steps: sequence of (offset, value, mask, yes, no, flags) or fcgpu_step."""
+        arr = (fcgpu_step * max(len(steps), 1))()
+        for i, st in enumerate(steps):
+            arr[i] = st if isinstance(st, fcgpu_step) else fcgpu_step(*[int(x) for x in st])
+        self._chk(self.lib.fcgpu_set_program(self.h, kind, arr, len(steps), output_everything),
+                  "fcgpu_set_program")
 
     def counters(self, n=NCOUNTERS):
         buf = (C.c_uint64 * n)()

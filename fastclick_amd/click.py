@@ -35,6 +35,10 @@ def load():
     lib = C.CDLL(N.LIBFCCLICK)
     lib.fcclick_check_config.restype = C.c_int
     lib.fcclick_check_config.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t]
+    lib.fcclick_parse_program.restype = C.c_int
+    lib.fcclick_parse_program.argtypes = [C.c_char_p, C.POINTER(N.fcgpu_step), C.c_uint32,
+                                          C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.c_char_p,
+                                          C.c_size_t]
     lib.fcclick_run.restype = C.c_int
     lib.fcclick_run.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                 C.POINTER(fcclick_result), C.c_char_p, C.c_size_t]
@@ -54,6 +58,19 @@ def check_config(conf: str):
     err = C.create_string_buffer(512)
     if lib.fcclick_check_config(conf.encode(), err, 512) != 0:
         raise ConfigError(err.value.decode())
+
+
+def parse_program(text: str):
+    """Reference `program` handler text -> (steps: list[fcgpu_step], output_everything)."""
+    lib = load()
+    cap = N.MAX_STEPS
+    steps = (N.fcgpu_step * cap)()
+    n = C.c_uint32()
+    oe = C.c_int32()
+    err = C.create_string_buffer(512)
+    if lib.fcclick_parse_program(text.encode(), steps, cap, C.byref(n), C.byref(oe), err, 512) != 0:
+        raise ConfigError(err.value.decode())
+    return [steps[i] for i in range(n.value)], oe.value
 
 
 def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1):

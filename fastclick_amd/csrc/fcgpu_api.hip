@@ -49,6 +49,9 @@ struct fcgpu_ctx {
     uint32_t *d_totals = nullptr;
     unsigned long long *d_ctr = nullptr;      // active counter vector
     unsigned long long *d_ctr_own = nullptr;  // context-owned vector
+    uint4 *d_prog = nullptr;                  // decision program (FCGPU_CLS_PROGRAM)
+    uint32_t prog_n = 0, prog_kind = 0;
+    int32_t prog_all = -1;
     uint16_t *d_verdict = nullptr;   // scratch verdicts when the caller wants perm only
     // host-resident staging
     uint8_t *h_arena = nullptr, *d_arena = nullptr;
@@ -157,6 +160,7 @@ void fcgpu_close(fcgpu_ctx *c) {
         hipFree(c->d_tilecnt);
         hipFree(c->d_totals);
         hipFree(c->d_ctr_own);
+        hipFree(c->d_prog);
         hipFree(c->d_verdict);
         hipFree(c->d_arena);
         hipFree(c->d_desc);
@@ -212,7 +216,7 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     if (cfg->size != sizeof(fcgpu_cfg)) return fail(c, FCGPU_EINVAL, "fcgpu_cfg size mismatch (ABI)");
     if (cfg->check_mode > FCGPU_CHECK_AUTO) return fail(c, FCGPU_EINVAL, "bad check_mode");
     if (cfg->hash_mode > FCGPU_HASH_FLOW5ID) return fail(c, FCGPU_EINVAL, "bad hash_mode");
-    if (cfg->classify > FCGPU_CLS_HASHSWITCH) return fail(c, FCGPU_EINVAL, "bad classify mode");
+    if (cfg->classify > FCGPU_CLS_PROGRAM) return fail(c, FCGPU_EINVAL, "bad classify mode");
     if (cfg->nports < 1 || cfg->nports > FCGPU_MAX_PORTS) return fail(c, FCGPU_EINVAL, "nports out of range");
     if (cfg->offset < 0 || cfg->offset > 255) return fail(c, FCGPU_EINVAL, "OFFSET out of range [0,255]");
     if (cfg->nbadsrc > FCGPU_MAX_ADDRS || cfg->ngooddst > FCGPU_MAX_ADDRS || cfg->nbad6 > FCGPU_MAX_ADDRS)
@@ -237,6 +241,10 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     memcpy(d.badsrc, cfg->badsrc, sizeof(d.badsrc));
     memcpy(d.gooddst, cfg->gooddst, sizeof(d.gooddst));
     memcpy(d.bad6, cfg->bad6, sizeof(d.bad6));
+    d.prog = c->d_prog;
+    d.prog_n = c->prog_n;
+    d.prog_kind = c->prog_kind;
+    d.prog_all = c->prog_all;
     c->configured = true;
     return FCGPU_OK;
 }
@@ -245,6 +253,8 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
                   const fcgpu_out *o, void *stream) {
     if (!c || !o) return FCGPU_EINVAL;
     if (!c->configured) return fail(c, FCGPU_EINVAL, "not configured");
+    if (c->cfg.classify == FCGPU_CLS_PROGRAM && !c->d_prog && c->prog_all < 0)
+        return fail(c, FCGPU_EINVAL, "FCGPU_CLS_PROGRAM without fcgpu_set_program");
     if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "batch larger than max_batch");
     if (n == 0) return FCGPU_OK;
     if (!d_arena || !d_desc) return fail(c, FCGPU_EINVAL, "null arena/desc");
@@ -402,6 +412,43 @@ int fcgpu_reset_counters(fcgpu_ctx *c) {
 int fcgpu_counters_device(fcgpu_ctx *c, uint64_t **d) {
     if (!c || !d) return FCGPU_EINVAL;
     *d = reinterpret_cast<uint64_t *>(c->d_ctr);
+    return FCGPU_OK;
+}
+
+int fcgpu_set_program(fcgpu_ctx *c, uint32_t kind, const fcgpu_step *steps, uint32_t nsteps,
+                      int32_t output_everything) {
+    if (!c) return FCGPU_EINVAL;
+    if (kind > FCGPU_PROG_CLASSIFIER) return fail(c, FCGPU_EINVAL, "bad program kind");
+    if (nsteps > FCGPU_MAX_STEPS || (nsteps && !steps)) return fail(c, FCGPU_EINVAL, "bad program size");
+    if (nsteps == 0 && output_everything < 0) return fail(c, FCGPU_EINVAL, "empty program without output");
+    std::vector<uint4> dev(nsteps ? nsteps : 1);
+    auto jump = [](int32_t j) -> int32_t {       // [X] (drop) and out-of-range -> unmatched
+        if (j <= -32767 || j > 32767) return -kProgUnmatched;
+        return j;
+    };
+    for (uint32_t k = 0; k < nsteps; ++k) {
+        const fcgpu_step &st = steps[k];
+        if (st.offset < -32768 || st.offset > 32767) return fail(c, FCGPU_EINVAL, "step offset out of range");
+        const int32_t y = jump(st.yes), n = jump(st.no);
+        if (y > (int32_t)nsteps - 1 || n > (int32_t)nsteps - 1) return fail(c, FCGPU_EINVAL, "jump past the program");
+        dev[k].x = (uint32_t)(uint16_t)st.offset | ((st.flags & FCGPU_STEP_SHORT_YES) << 16);
+        dev[k].y = st.value & st.mask;
+        dev[k].z = st.mask;
+        dev[k].w = (uint32_t)(uint16_t)y | ((uint32_t)(uint16_t)n << 16);
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());
+    hipFree(c->d_prog);
+    c->d_prog = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_prog, sizeof(uint4) * dev.size()));
+    HIPCHK(c, hipMemcpy(c->d_prog, dev.data(), sizeof(uint4) * dev.size(), hipMemcpyHostToDevice));
+    c->prog_n = nsteps;
+    c->prog_kind = kind;
+    c->prog_all = nsteps == 0 ? output_everything : -1;
+    c->dcfg.prog = c->d_prog;
+    c->dcfg.prog_n = c->prog_n;
+    c->dcfg.prog_kind = c->prog_kind;
+    c->dcfg.prog_all = c->prog_all;
     return FCGPU_OK;
 }
 

@@ -39,7 +39,15 @@ struct DevCfg {
     uint32_t badsrc[FCGPU_MAX_ADDRS];
     uint32_t gooddst[FCGPU_MAX_ADDRS];
     uint32_t bad6[FCGPU_MAX_ADDRS][4];
+    const uint4 *prog;        // decision program (FCGPU_CLS_PROGRAM), 16 B per step
+    uint32_t prog_n;
+    uint32_t prog_kind;
+    int32_t prog_all;         // >= 0: empty program, every packet -> this output
 };
+
+// Device step: x = (u16)offset | flags << 16, y = value, z = mask,
+// w = (u16)yes | (u16)no << 16 (signed 16-bit jumps).
+constexpr int32_t kProgUnmatched = 0x7fff;
 
 struct RxArgs {
     const uint8_t *arena;
@@ -133,6 +141,52 @@ __device__ __forceinline__ int bytesum_port(const FrameView &f, uint32_t len, in
     for (int i = 0; i < l; ++i) d += (int)f.rd8((uint32_t)(o + i));
     if (n == 2 || n == 4 || n == 8) return (d ^ (d >> 4)) & (int)(n - 1);
     return d % (int)n;
+}
+
+// A decision program over one valid packet (IPFilter::match, ipfilter.hh:393-481
+// with length_checked_match, ipfilter.cc:1415-1474; Classifier: Program::match,
+// classification.hh:372-392 / classification.cc:1146-1176). Every step is
+// length-checked, which is what the reference's unchecked fast loop computes
+// whenever the packet is at least the program's safe length. Bytes before the
+// frame start (MAC header - 2) read as zero.
+__device__ __forceinline__ uint32_t prog_word(const FrameView &f, int b) {
+    if (b >= 0) return f.rd32((uint32_t)b);
+    if (b <= -4) return 0u;
+    return f.rd32(0) << (8 * (-b));
+}
+
+__device__ __forceinline__ uint32_t run_program(const DevCfg &c, const FrameView &f, const fcgpu_anno &an) {
+    if (c.prog_all >= 0) return (uint32_t)c.prog_all;
+    const bool ipf = c.prog_kind == FCGPU_PROG_IPFILTER;
+    int plen;
+    if (ipf) {
+        const int nl = (int)an.length - (int)an.nh, nhl = (int)an.th - (int)an.nh;
+        plen = nl > nhl ? nl + 512 - nhl : nl + 256;
+    } else {
+        plen = (int)an.length;
+    }
+    int pos = 0;
+    for (uint32_t it = 0; it <= c.prog_n; ++it) {
+        const uint4 st = c.prog[pos];
+        const int off = (int16_t)(st.x & 0xffff);
+        const uint32_t m = st.z;
+        bool avail = off + 4 <= plen;
+        if (!avail && off < plen) {
+            const int a = plen - off;
+            avail = !((m >> 24) || (((m >> 16) & 0xff) && a <= 2) || (((m >> 8) & 0xff) && a == 1));
+        }
+        int j;
+        if (avail) {
+            const int b = !ipf ? off : off >= 512 ? (int)an.th + off - 512 : off >= 256 ? (int)an.nh + off - 256 : off - 2;
+            const uint32_t data = prog_word(f, b) & m;
+            j = data == st.y ? (int16_t)(st.w & 0xffff) : (int16_t)(st.w >> 16);
+        } else {
+            j = ((st.x >> 16) & FCGPU_STEP_SHORT_YES) ? (int16_t)(st.w & 0xffff) : (int16_t)(st.w >> 16);
+        }
+        if (j <= 0) return (uint32_t)(-j);
+        pos = j;
+    }
+    return (uint32_t)kProgUnmatched;   // malformed (cyclic) program
 }
 
 struct PktResult {
@@ -259,6 +313,16 @@ __device__ __forceinline__ void process_packet(const DevCfg &c, const FrameView 
     case FCGPU_CLS_HASHSWITCH:
         r.port = (uint32_t)bytesum_port(f, an.length, c.hs_offset, c.hs_length, c.nports);
         break;
+    case FCGPU_CLS_PROGRAM: {
+        const uint32_t out = run_program(c, f, an);
+        if (out >= c.nports) {            // no output: CLASSIFY_EACH_PACKET kills it
+            r.reason = FCGPU_R_NO_MATCH;
+            r.port = c.nports;
+        } else {
+            r.port = out;
+        }
+        break;
+    }
     default: r.port = 0;
     }
 }
@@ -428,7 +492,7 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
     if (live && rank == 0) s_cnt[wave][bin] = (uint32_t)__popcll(grp);
     const uint64_t mbad = __ballot(rslot != 0xffffffffu);
     if (mbad) {   // rare: per-reason counts
-        const uint64_t g2 = match_any(rslot, 3, mbad);
+        const uint64_t g2 = match_any(rslot, 4, mbad);
         if (rslot != 0xffffffffu && __popcll(g2 & lt) == 0) s_cnt[wave][nb + rslot] = (uint32_t)__popcll(g2);
     }
     __syncthreads();
@@ -479,10 +543,13 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
             if (t < nb) atomicAdd(&ctr[FCGPU_CTR_PORT + t], (unsigned long long)tot);
             else atomicAdd(&ctr[FCGPU_CTR_REASON + (t - nb)], (unsigned long long)tot);
         }
-        if (t == nb - 1) {   // the invalid list: drops, and count = packets - drops
+        if (t == nb - 1) {   // the invalid list: drops (minus no-match), count = packets - drops
             const uint32_t live_n = min(A.n - tile * kTile, (uint32_t)kTile);
-            if (tot) atomicAdd(&ctr[FCGPU_CTR_DROPS], (unsigned long long)tot);
-            if (live_n - tot) atomicAdd(&ctr[FCGPU_CTR_COUNT], (unsigned long long)(live_n - tot));
+            const uint32_t sm = nb + FCGPU_NREASON_SLOTS - 1;   // reason 9's slot
+            const uint32_t nomatch = s_cnt[0][sm] + s_cnt[1][sm] + s_cnt[2][sm] + s_cnt[3][sm];
+            const uint32_t drops = tot - nomatch;
+            if (drops) atomicAdd(&ctr[FCGPU_CTR_DROPS], (unsigned long long)drops);
+            if (live_n - drops) atomicAdd(&ctr[FCGPU_CTR_COUNT], (unsigned long long)(live_n - drops));
         }
     }
 }

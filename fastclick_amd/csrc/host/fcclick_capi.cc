@@ -104,6 +104,25 @@ extern "C" int fcclick_check_config(const char *conf, char *err, size_t errcap) 
     return 0;
 }
 
+extern "C" int fcclick_parse_program(const char *text, fcgpu_step *steps, uint32_t cap, uint32_t *nsteps,
+                                     int32_t *output_everything, char *err, size_t errcap) {
+    if (!text || !nsteps || !output_everything) {
+        copy_err("null argument", err, errcap);
+        return -1;
+    }
+    fcx::ParsedProgram pr;
+    std::string e = fcx::parse_program(text, pr);
+    if (e.empty() && pr.steps.size() > cap) e = "program longer than cap";
+    if (!e.empty()) {
+        copy_err(e, err, errcap);
+        return -1;
+    }
+    for (size_t i = 0; i < pr.steps.size(); ++i) steps[i] = pr.steps[i];
+    *nsteps = (uint32_t)pr.steps.size();
+    *output_everything = pr.output_everything;
+    return 0;
+}
+
 extern "C" int fcclick_run(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
                            uint32_t burst, uint32_t nsinks, fcclick_result *res, char *err, size_t errcap) {
     std::string e;

@@ -16,6 +16,12 @@
 //   BADADDRS                                 -- CheckIP6Header (IPv6, MODE AUTO)
 //   N / LB_MODE hash|hash_agg|hash_ip        -- FlowSwitch / LoadBalancer
 //   HASHSWITCH "OFFSET LENGTH"               -- HashSwitch
+//   PROGRAM "<program text>", PROGRAM_KIND IPFILTER|CLASSIFIER
+//                                            -- IPFilter / IPClassifier / Classifier:
+//     the compiled program as the reference's `program` handler prints it
+//     (lines separated by newlines or '|', program_text.hh); N is the
+//     classifier's output count. Packets no rule matches are killed, as
+//     CLASSIFY_EACH_PACKET kills a packet whose port is out of range.
 //   MODE CHECK|MARK|AUTO, HASH NONE|FLOWID|FLOW5ID, STRIP, BATCH, DEVICE,
 //   PARTITION TILE (default: each 256-packet tile classified as one batch, one
 //   fused launch) | GLOBAL (the whole staged batch as one, three launches)
@@ -32,6 +38,7 @@
 #include <inttypes.h>
 
 #include "click_model.hh"
+#include "program_text.hh"
 #include "../../../include/fastclick_gpu.h"
 
 namespace fcx {
@@ -95,6 +102,16 @@ class GPUIPCheckClassify : public Element {
                 _cfg.classify = FCGPU_CLS_HASHSWITCH;
                 _cfg.hs_offset = (int32_t)o;
                 _cfg.hs_length = (int32_t)l;
+            } else if (k == "PROGRAM") {
+                std::string text = v;
+                if (text.size() >= 2 && text.front() == '"' && text.back() == '"') text = text.substr(1, text.size() - 2);
+                std::string e = parse_program(text, _prog);
+                if (!e.empty()) return err(errh, "PROGRAM: " + e);
+                _cfg.classify = FCGPU_CLS_PROGRAM;
+            } else if (k == "PROGRAM_KIND") {
+                if (v == "IPFILTER") _prog_kind = FCGPU_PROG_IPFILTER;
+                else if (v == "CLASSIFIER") _prog_kind = FCGPU_PROG_CLASSIFIER;
+                else return err(errh, "PROGRAM_KIND expects IPFILTER or CLASSIFIER");
             } else if (k == "MODE") {
                 if (v == "CHECK") _cfg.check_mode = FCGPU_CHECK_IP4;
                 else if (v == "MARK") _cfg.check_mode = FCGPU_MARK_IP4;
@@ -127,6 +144,14 @@ class GPUIPCheckClassify : public Element {
             }
         }
         if (!strip_set) _strip = (_cfg.check_mode == FCGPU_CHECK_AUTO);
+        if (_cfg.classify == FCGPU_CLS_PROGRAM) {
+            if (_prog.output_everything >= (int32_t)_cfg.nports && _prog.output_everything != 0x7fff)
+                return err(errh, "PROGRAM sends everything to a missing output");
+            for (const auto &st : _prog.steps)
+                if ((st.yes <= 0 && -st.yes >= (int32_t)_cfg.nports && st.yes != -2147483647) ||
+                    (st.no <= 0 && -st.no >= (int32_t)_cfg.nports && st.no != -2147483647))
+                    return err(errh, "PROGRAM jumps to an output >= N");
+        }
         return 0;
     }
 
@@ -137,6 +162,11 @@ class GPUIPCheckClassify : public Element {
         if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_open: ") + fcgpu_last_error(nullptr));
         rc = fcgpu_configure(_ctx, &_cfg);
         if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_configure: ") + fcgpu_last_error(_ctx));
+        if (_cfg.classify == FCGPU_CLS_PROGRAM) {
+            rc = fcgpu_set_program(_ctx, _prog_kind, _prog.steps.data(), (uint32_t)_prog.steps.size(),
+                                   _prog.output_everything);
+            if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_set_program: ") + fcgpu_last_error(_ctx));
+        }
         _pkts.reserve(_cap);
         _frames.reserve(_cap);
         _lens.reserve(_cap);
@@ -144,6 +174,7 @@ class GPUIPCheckClassify : public Element {
         _hash.resize(_cap);
         _anno.resize(_cap);
         _perm.resize(_cap);
+        _keep.resize(_cap);
         _tperm.resize(_cap + FCGPU_TILE);
         _start.resize(FCGPU_MAX_PORTS + 2);
         _tile_count.resize((size_t)(FCGPU_MAX_PORTS + 1) * ((_cap + FCGPU_TILE - 1) / FCGPU_TILE));
@@ -224,7 +255,7 @@ class GPUIPCheckClassify : public Element {
             const uint32_t reason = _verdict[i] & 0xff;
             if (autom && reason != FCGPU_R_VLAN_REJECT)
                 p->set_anno_u16(VLAN_TCI_ANNO_OFFSET, a.vlan_tci);    // StripEtherVLANHeader
-            if (reason == FCGPU_R_OK) {
+            if (reason == FCGPU_R_OK || reason == FCGPU_R_NO_MATCH) {
                 p->set_network_header(a.nh, a.th);                     // set_ip_header / set_ip6_header
                 if (a.length < p->length()) p->take(p->length() - a.length);
                 if (a.ipver == 6) p->set_anno_u8(IP6_NXT_ANNO_OFFSET, a.ip6_nxt);
@@ -267,6 +298,18 @@ class GPUIPCheckClassify : public Element {
     // link packets idx(s) .. idx(e-1) into PacketBatches of <= MAX_BATCH_SIZE
     template <class Idx>
     void emit_run(uint32_t port, uint32_t s, uint32_t e, Idx idx) {
+        if (port == _cfg.nports && _cfg.classify == FCGPU_CLS_PROGRAM) {
+            // the last slot mixes invalid packets (output N) and packets no
+            // rule matched (killed); keep input order for the former
+            uint32_t w = s;
+            for (uint32_t j = s; j < e; ++j) {
+                const uint32_t i = idx(j);
+                if ((_verdict[i] & 0xff) == FCGPU_R_NO_MATCH) _pkts[i]->kill();
+                else _keep[w++ - s] = i;
+            }
+            emit_list(port, w - s);
+            return;
+        }
         while (s < e) {
             uint32_t m = e - s < kMaxBatch ? e - s : kMaxBatch;
             Packet *head = _pkts[idx(s)], *prev = head;
@@ -280,7 +323,24 @@ class GPUIPCheckClassify : public Element {
         }
     }
 
+    void emit_list(uint32_t port, uint32_t m) {
+        for (uint32_t s = 0; s < m;) {
+            uint32_t k = m - s < kMaxBatch ? m - s : kMaxBatch;
+            Packet *head = _pkts[_keep[s]], *prev = head;
+            for (uint32_t j = 1; j < k; ++j) {
+                Packet *q = _pkts[_keep[s + j]];
+                prev->set_next(q);
+                prev = q;
+            }
+            checked_output_push_batch((int)port, PacketBatch::make_from_list(head, prev, k));
+            s += k;
+        }
+    }
+
     static constexpr uint32_t kMaxBatch = 8192;
+    ParsedProgram _prog;
+    uint32_t _prog_kind = FCGPU_PROG_IPFILTER;
+    std::vector<uint32_t> _keep;
     fcgpu_cfg _cfg;
     fcgpu_ctx *_ctx = nullptr;
     int _device = 0;

@@ -88,13 +88,17 @@ def run_device(ctx: N.Context, dbatch: DeviceBatch, outs: DeviceOutputs, stream=
                 stream=s.cuda_stream, **outs.ptrs())
 
 
-def process_batch(batch, cfg, *, anno=True, perm=True, device_index=0, partition=N.PART_GLOBAL):
+def process_batch(batch, cfg, *, anno=True, perm=True, device_index=0, partition=N.PART_GLOBAL,
+                  program=None):
     """Upload a host Batch, run the device path once, return numpy results and
-    the counter vector. Convenience for tests and smoke()."""
+    the counter vector. Convenience for tests and smoke(). program: optional
+    (kind, steps, output_everything) for CLS_PROGRAM (fcgpu_set_program)."""
     torch = _torch()
     with torch.cuda.device(device_index):
         ctx = N.Context(device_index, max(batch.n, 1), cfg)
         try:
+            if program is not None:
+                ctx.set_program(*program)
             db = DeviceBatch.upload(batch, device=f"cuda:{device_index}")
             outs = DeviceOutputs(batch.n, cfg.nports, device=f"cuda:{device_index}",
                                  anno=anno, perm=perm, port_start=perm, partition=partition)

@@ -28,7 +28,8 @@
  * Batch layout ("arena + descriptor"):
  *   arena : bytes; packet i's frame starts at arena + desc[2i] and is
  *           desc[2i+1] bytes long. The arena must stay readable for 128 bytes
- *           past every frame start (header-window over-read; never used for a
+ *           past every frame start and 8 bytes past every frame end
+ *           (header-window over-read; bytes outside the frame never decide a
  *           verdict).
  *   desc  : uint32 pairs (offset, length), 8 bytes per packet.
  * Results are per-packet structure-of-arrays; every output pointer may be NULL
@@ -47,7 +48,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 3
+#define FCGPU_ABI_VERSION 4
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -66,7 +67,9 @@ extern "C" {
 #define FCGPU_R_OK          6
 #define FCGPU_R_BAD_IP6     7   /* CheckIP6Header's single drop reason      */
 #define FCGPU_R_VLAN_REJECT 8   /* StripEtherVLANHeader output 1 (untagged, NATIVE_VLAN < 0) */
-#define FCGPU_NREASON_SLOTS 8   /* counters for reasons 0-5, 7, 8           */
+#define FCGPU_R_NO_MATCH    9   /* valid, but the classifier program matched no output:
+                                   CLASSIFY_EACH_PACKET kills it (packetbatch.hh:268)  */
+#define FCGPU_NREASON_SLOTS 9   /* counters for reasons 0-5, 7, 8, 9        */
 
 /* check_mode */
 #define FCGPU_CHECK_IP4   0   /* CheckIPHeader(OFFSET o[, CHECKSUM c, BADSRC, GOODDST]) */
@@ -83,6 +86,8 @@ extern "C" {
                                    ((H>>16) ^ (H&0xffff)) % nports                       */
 #define FCGPU_CLS_HASH_IP    2  /* LoadBalancer direct_hash_ip (frame bytes 26..33)      */
 #define FCGPU_CLS_HASHSWITCH 3  /* HashSwitch(hs_offset, hs_length), nports = MAX        */
+#define FCGPU_CLS_PROGRAM    4  /* decision program set by fcgpu_set_program: IPFilter /
+                                   IPClassifier or Classifier                          */
 
 #define FCGPU_MAX_PORTS   64
 #define FCGPU_MAX_ADDRS   16
@@ -155,12 +160,13 @@ typedef struct fcgpu_ctx fcgpu_ctx;
 /* Counter vector layout returned by fcgpu_read_counters (uint64):
  *   [0] count (valid packets)         CheckIPHeader "count"
  *   [1] drops                         CheckIPHeader "drops"
- *   [2 .. 2+8)  reason drops: slots for reasons 0-5, 7, 8 ("drop_details")
- *   [10 .. 10+nports+1) per-output packet counts, last = invalid list       */
+ *   [2 .. 2+9)  reason slots for reasons 0-5, 7, 8 ("drop_details") and 9
+ *               (no classifier match; not a drop of the checker)
+ *   [11 .. 11+nports+1) per-output packet counts, last = invalid list       */
 #define FCGPU_CTR_COUNT   0
 #define FCGPU_CTR_DROPS   1
 #define FCGPU_CTR_REASON  2
-#define FCGPU_CTR_PORT    10
+#define FCGPU_CTR_PORT    11
 #define FCGPU_NCOUNTERS   (FCGPU_CTR_PORT + FCGPU_MAX_PORTS + 1)
 /* On the device the vector is kept in FCGPU_CTR_SHARDS replicas (tiles add to
  * replica tile % FCGPU_CTR_SHARDS) and summed on read, like per_thread<>
@@ -189,6 +195,38 @@ int  fcgpu_process(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_des
  * host pointers of h_out. Synchronous. */
 int  fcgpu_process_host(fcgpu_ctx *ctx, const uint8_t *const *frames,
                         const uint32_t *lens, uint32_t n, const fcgpu_out *h_out);
+
+/* Decision programs. A program is the step list the
+ * reference's own compiler produces and prints through the `program` handler
+ * (IPFilter/IPClassifier: elements/ip/ipfilter.cc; Classifier:
+ * elements/standard/classification.cc:978-991 and :1104-1140): each step loads
+ * the 32-bit word at `offset`, masks it, compares with `value` and jumps to
+ * `yes`/`no`; a jump > 0 is a step index, <= 0 is output -jump. A step whose
+ * word is not entirely inside the packet takes `yes` if FCGPU_STEP_SHORT_YES
+ * else `no` (length_checked_match, ipfilter.cc:1415-1474,
+ * classification.cc:1146-1176).
+ *   FCGPU_PROG_IPFILTER: offsets >= 512 address the transport header,
+ *     >= 256 the network header, else the MAC header - 2 (ipfilter.hh:393-481).
+ *   FCGPU_PROG_CLASSIFIER: offsets address the frame start
+ *     (Classification::Wordwise::Program::match, classification.hh:372-392). */
+#define FCGPU_PROG_IPFILTER   0
+#define FCGPU_PROG_CLASSIFIER 1
+#define FCGPU_STEP_SHORT_YES  1u
+#define FCGPU_MAX_STEPS       8192
+
+typedef struct fcgpu_step {
+    int32_t  offset;
+    uint32_t value;           /* bytes in packet order, read as a little-endian word */
+    uint32_t mask;
+    int32_t  yes;
+    int32_t  no;
+    uint32_t flags;           /* FCGPU_STEP_SHORT_YES */
+} fcgpu_step;
+
+/* Install a program for FCGPU_CLS_PROGRAM. output_everything >= 0 means the
+ * program is empty and every packet goes to that output ("all->[N]"). */
+int  fcgpu_set_program(fcgpu_ctx *ctx, uint32_t kind, const fcgpu_step *steps, uint32_t nsteps,
+                       int32_t output_everything);
 
 int  fcgpu_read_counters(fcgpu_ctx *ctx, uint64_t *out, int n);
 int  fcgpu_reset_counters(fcgpu_ctx *ctx);

@@ -23,6 +23,16 @@ extern "C" {
  * without touching a GPU. Returns 0, or -1 with the message in err. */
 int fcclick_check_config(const char *conf, char *err, size_t errcap);
 
+/* Parse a decision program in the text form the reference's IPFilter /
+ * IPClassifier / Classifier `program` read handler prints
+ * (elements/standard/classification.cc:978-991, :1104-1140) into fcgpu_step
+ * entries for fcgpu_set_program. Lines may be separated by '\n' or '|'.
+ * *nsteps receives the step count (<= cap), *output_everything the "all->[N]"
+ * output or -1. Returns 0, or -1 with the message in err. */
+struct fcgpu_step;
+int fcclick_parse_program(const char *text, struct fcgpu_step *steps, uint32_t cap, uint32_t *nsteps,
+                          int32_t *output_everything, char *err, size_t errcap);
+
 typedef struct fcclick_result {
     uint32_t *out_port;     /* [n] output the packet left on; 0xffffffff = killed        */
     uint32_t *out_seq;      /* [n] global departure order (0..), 0xffffffff = killed     */

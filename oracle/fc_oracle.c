@@ -198,6 +198,73 @@ static int check_ip6(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, uint32_
     return FCGPU_R_OK;
 }
 
+/* ---- decision programs (A11) ------------------------------------------- */
+static struct {
+    uint32_t kind, n;
+    int32_t all;
+    fcgpu_step *steps;
+} g_prog = {0, 0, -1, NULL};
+
+void fco_set_program(uint32_t kind, const fcgpu_step *steps, uint32_t nsteps, int32_t all)
+{
+    free(g_prog.steps);
+    g_prog.steps = NULL;
+    g_prog.kind = kind;
+    g_prog.n = nsteps;
+    g_prog.all = nsteps ? -1 : all;
+    if (nsteps) {
+        g_prog.steps = (fcgpu_step *)malloc(sizeof(fcgpu_step) * nsteps);
+        memcpy(g_prog.steps, steps, sizeof(fcgpu_step) * nsteps);
+    }
+}
+
+/* word at frame byte b; bytes before the frame start (MAC header - 2) are 0 */
+static uint32_t prog_word(const uint8_t *f, int b)
+{
+    uint8_t w[4];
+    for (int k = 0; k < 4; k++) w[k] = (b + k >= 0) ? f[b + k] : 0;
+    return le32(w);
+}
+
+/* elements/ip/ipfilter.hh:393-481 + ipfilter.cc:1415-1474 (IPFilter), and
+ * classification.hh:372-392 + classification.cc:1146-1176 (Classifier). The
+ * reference skips length checks when the packet is at least the safe length,
+ * where they always pass; here every step is checked. */
+uint32_t fco_run_program(const uint8_t *f, const fcgpu_anno *a)
+{
+    if (g_prog.all >= 0) return (uint32_t)g_prog.all;
+    int ipf = g_prog.kind == FCGPU_PROG_IPFILTER;
+    int plen;
+    if (ipf) {
+        int nl = (int)a->length - (int)a->nh, nhl = (int)a->th - (int)a->nh;
+        plen = nl > nhl ? nl + 512 - nhl : nl + 256;   /* ipfilter.hh:396-400 */
+    } else {
+        plen = (int)a->length;
+    }
+    int pos = 0;
+    for (uint32_t it = 0; it <= g_prog.n; it++) {
+        const fcgpu_step *st = &g_prog.steps[pos];
+        int off = st->offset;
+        int j;
+        int ok = off + 4 <= plen;
+        if (!ok && off < plen) {
+            unsigned avail = (unsigned)(plen - off);
+            const uint8_t *c = (const uint8_t *)&st->mask;
+            ok = !(c[3] || (c[2] && avail <= 2) || (c[1] && avail == 1));
+        }
+        if (ok) {
+            int b = !ipf ? off : off >= 512 ? (int)a->th + off - 512 : off >= 256 ? (int)a->nh + off - 256 : off - 2;
+            uint32_t data = prog_word(f, b) & st->mask;
+            j = data == (st->value & st->mask) ? st->yes : st->no;
+        } else {
+            j = (st->flags & FCGPU_STEP_SHORT_YES) ? st->yes : st->no;
+        }
+        if (j <= 0) return (j <= -32767) ? 0x7fff : (uint32_t)(-j);
+        pos = j;
+    }
+    return 0x7fff;
+}
+
 void fco_process_packet(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, fco_result *r)
 {
     memset(r, 0, sizeof(*r));
@@ -261,6 +328,12 @@ void fco_process_packet(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, fco_
     case FCGPU_CLS_HASH_IP:    port = fco_hash_ip_port(f, a->length, (int)c->nports); break;
     case FCGPU_CLS_HASHSWITCH: port = fco_hashswitch_port(f, a->length, c->hs_offset,
                                                            c->hs_length, (int)c->nports); break;
+    case FCGPU_CLS_PROGRAM: {
+        uint32_t out = fco_run_program(f, a);
+        if (out >= c->nports) { r->reason = FCGPU_R_NO_MATCH; port = (int)c->nports; }
+        else port = (int)out;
+        break;
+    }
     default: port = 0;
     }
     r->port = (uint8_t)port;
@@ -291,6 +364,7 @@ void fco_process_batch2(const fcgpu_cfg *c, const uint8_t *arena, const uint32_t
         port[i] = r.port;
         if (ctr) {
             if (r.reason == FCGPU_R_OK) ctr[FCGPU_CTR_COUNT]++;
+            else if (r.reason == FCGPU_R_NO_MATCH) { ctr[FCGPU_CTR_COUNT]++; ctr[FCGPU_CTR_REASON + reason_slot(r.reason)]++; }
             else { ctr[FCGPU_CTR_DROPS]++; ctr[FCGPU_CTR_REASON + reason_slot(r.reason)]++; }
             ctr[FCGPU_CTR_PORT + r.port]++;
         }

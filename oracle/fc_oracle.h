@@ -48,6 +48,13 @@ void fco_process_batch2(const fcgpu_cfg *cfg, const uint8_t *arena, const uint32
                         uint32_t *perm, uint32_t *port_start, uint32_t *perm_tile,
                         uint16_t *tile_count, uint64_t *counters);
 
+/* Decision program for FCGPU_CLS_PROGRAM (A11): the oracle keeps one
+ * (process-global; test use is single-threaded). Same step format as the ABI. */
+void fco_set_program(uint32_t kind, const fcgpu_step *steps, uint32_t nsteps, int32_t all);
+/* IPFilter::match / Classifier Program::match on one packet whose anno holds
+ * nh/th/length (after the check): returns the output, or 0x7fff if none. */
+uint32_t fco_run_program(const uint8_t *frame, const fcgpu_anno *a);
+
 /* Individual pieces, exposed for known-answer tests. */
 uint32_t fco_ipflowid_hash(uint32_t saddr_raw, uint16_t sport_net,
                            uint32_t daddr_raw, uint16_t dport_net);  /* A6 */

@@ -45,6 +45,8 @@ def load():
     lib.fco_process_batch2.argtypes = [C.POINTER(N.fcgpu_cfg), C.c_void_p, C.c_void_p, C.c_uint32,
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.fco_set_program.restype = None
+    lib.fco_set_program.argtypes = [C.c_uint32, C.POINTER(N.fcgpu_step), C.c_uint32, C.c_int32]
     lib.fco_process_batch.restype = None
     lib.fco_process_batch.argtypes = [C.POINTER(N.fcgpu_cfg), C.c_void_p, C.c_void_p, C.c_uint32,
                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -57,10 +59,23 @@ def _p(a):
     return a.ctypes.data if a is not None else None
 
 
-def process_batch(cfg, batch):
-    """Run the oracle over a synth.Batch; returns the same dict as the device path."""
+def set_program(kind, steps, output_everything=-1):
+    """Install the decision program the oracle uses for CLS_PROGRAM (global)."""
     from fastclick_amd import _native as N
     lib = load()
+    arr = (N.fcgpu_step * max(len(steps), 1))()
+    for i, st in enumerate(steps):
+        arr[i] = st if isinstance(st, N.fcgpu_step) else N.fcgpu_step(*[int(x) for x in st])
+    lib.fco_set_program(kind, arr, len(steps), output_everything)
+
+
+def process_batch(cfg, batch, program=None):
+    """Run the oracle over a synth.Batch; returns the same dict as the device path.
+    program: optional (kind, steps, output_everything) for CLS_PROGRAM."""
+    from fastclick_amd import _native as N
+    lib = load()
+    if program is not None:
+        set_program(*program)
     n = batch.n
     arena = np.ascontiguousarray(batch.arena)
     desc = np.ascontiguousarray(batch.desc, dtype=np.uint32)

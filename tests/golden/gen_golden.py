@@ -23,6 +23,10 @@ Per field, the reference mechanism that produced it:
   hs4/hs7   HashSwitch(26, 8) with 4/7 outputs behind CheckIPHeader(OFFSET 14)
   v6        StripEtherVLANHeader -> Classifier(0/60%f0, -) -> CheckIP6Header /
             CheckIPHeader: verdicts and lengths; IP6FlowID hash from fcref
+  prog      IPClassifier (IPFILTER kind) and Classifier (CLASSIFIER kind)
+            behind CheckIPHeader: each element's compiled program as its
+            `program` handler prints it, and the output every packet left on
+            (none = no rule matched -> NOMATCH)
   cksum/h6  click_in_cksum and IPFlowID/IP6FlowID::hashcode compiled from the
             reference sources by oracle/ref/Makefile (fcref)
 """
@@ -291,6 +295,87 @@ def _h6_record(A, o):
     return (bytes(A[o + 8:o + 24]) + bytes(A[th:th + 2]) + bytes(A[o + 24:o + 40]) + bytes(A[th + 2:th + 4]))
 
 
+IPC_RULES = ["udp && dst port 53", "tcp && (dst port 80 or dst port 443)", "src net 128.0.0.0/1 && udp",
+             "dst port >= 1024 && dst port < 4096", "icmp", "ip frag", "src port > 60000",
+             "ip ttl < 10", "ip tos 4"]
+CLS_RULES = ["23/11 36/0035", "23/06 !36/0050", "12/0800 23/01", "26/80%c0", "14/46%4f", "30/0a"]
+NOMATCH = 254
+
+
+def make_prog_set(n=3000, seed=2026):
+    """IPv4 frames shaped for the classifier rules: popular ports, TCP/UDP/ICMP,
+    fragments (first and later), low TTLs, TOS 4, IP options, L4-truncated
+    datagrams (short->yes paths) and ~2% invalid headers."""
+    rng = np.random.default_rng(seed)
+    fl = synth._rand_flows(rng, n)
+    fl["dport"] = np.where(rng.random(n) < 0.6, rng.choice([53, 80, 443, 1500, 3000, 4095, 4096, 8080], n),
+                           fl["dport"]).astype(np.uint32)
+    fl["sport"] = np.where(rng.random(n) < 0.2, rng.integers(59990, 65536, n), fl["sport"]).astype(np.uint32)
+    flen = rng.choice([60, 60, 74, 98, 128, 190], n)
+    proto = rng.choice([17, 17, 6, 6, 1, 47], n)
+    hdr = synth.build_headers(n, **fl, proto=proto, frame_len=flen)
+    b = synth.pack(hdr, flen, meta=dict(set="prog", seed=seed))
+    synth.add_ip_options(b, 0.1, seed=seed + 1)
+    A = b.arena
+    for i in range(n):
+        o = int(b.desc[i, 0]) + 14
+        r = rng.random()
+        if r < 0.05:                       # non-first fragment
+            fo = int(rng.integers(1, 0x1FFF))
+            A[o + 6], A[o + 7] = (fo >> 8) & 0x1F, fo & 0xFF
+        elif r < 0.08:                     # first fragment (MF)
+            A[o + 6] |= 0x20
+        if rng.random() < 0.1:
+            A[o + 8] = int(rng.integers(1, 12))
+        if rng.random() < 0.1:
+            A[o + 1] = 4
+        if rng.random() < 0.04:            # truncate the datagram inside the L4 header
+            hl = (A[o] & 15) * 4
+            L = hl + int(rng.integers(0, 4))
+            A[o + 2], A[o + 3] = L >> 8, L & 0xFF
+        synth._refresh_cksum(A, o)
+    kind = synth.inject_errors(b, 0.02, seed=seed + 2)
+    return b, kind
+
+
+def _program_of(out):
+    lines = out.splitlines()
+    k = max(i for i, l in enumerate(lines) if l.startswith("alignment offset"))
+    j = k
+    while j > 0 and (lines[j - 1].startswith(" ") or lines[j - 1][:1].isdigit()
+                     or lines[j - 1].startswith("safe length") or lines[j - 1].startswith("all->")):
+        j -= 1
+    return "\n".join(lines[j:k + 1]) + "\n"
+
+
+def run_prog(b, tmp):
+    pcap = os.path.join(tmp, "prog.pcap")
+    write_pcap(pcap, b.frames())
+    n = b.n
+    res = {}
+    for name, elem, rules, pre in (("ipc", "IPClassifier", IPC_RULES, "Strip(14) -> CheckIPHeader(CHECKSUM true)"),
+                                   ("cls", "Classifier", CLS_RULES, "CheckIPHeader(OFFSET 14, CHECKSUM true)")):
+        m = len(rules)
+        outs = " ".join(f"c[{k}] -> ToIPSummaryDump({name}{k}.ipsum, FIELDS timestamp);" for k in range(m))
+        cfg = (f"FromDump(prog.pcap, STOP true, TIMING false) -> {pre} -> c :: {elem}({', '.join(rules)}); "
+               f"{outs} DriverManager(wait, print c.program)")
+        # invalid headers leave the checker on its port 1
+        cfg = cfg.replace("CheckIPHeader(", "chk :: CheckIPHeader(", 1) + "; chk[1] -> ToIPSummaryDump(" \
+            + f"{name}bad.ipsum, FIELDS timestamp);"
+        out, _ = click(CLICK, cfg, tmp)
+        prog = _program_of(out)
+        got = np.full(n, NOMATCH, np.uint8)
+        for k in range(m):
+            for i in read_ipsum(os.path.join(tmp, f"{name}{k}.ipsum"), 0):
+                got[i] = k
+        for i in read_ipsum(os.path.join(tmp, f"{name}bad.ipsum"), 0):
+            got[i] = 255
+        res[f"{name}_out"] = got
+        res[f"{name}_prog"] = np.frombuffer(prog.encode(), np.uint8)
+        res[f"{name}_nout"] = np.array(m)
+    return res
+
+
 def run_kat(tmp):
     """click_in_cksum on random buffers (odd lengths included) and IPFlowID /
     IP6FlowID hashcodes on random tuples, from the reference harness."""
@@ -320,31 +405,45 @@ def sha(path):
     return hashlib.sha256(open(path, "rb").read()).hexdigest()
 
 
-def main():
-    prov = dict(generator="tests/golden/gen_golden.py", click=CLICK, click_sha256=sha(CLICK),
+def main(sets=("ip4", "mix", "prog", "kat")):
+    prov_path = os.path.join(HERE, "PROVENANCE.json")
+    prov = json.load(open(prov_path)) if os.path.exists(prov_path) else {}
+    prov.update(generator="tests/golden/gen_golden.py", click=CLICK, click_sha256=sha(CLICK),
                 click3=CLICK3, click3_sha256=sha(CLICK3), fcref=FCREF, fcref_sha256=sha(FCREF),
-                t0=T0, badsrc=BADSRC, gooddst=GOODDST, not_pinned=NOT_PINNED)
+                t0=T0, badsrc=BADSRC, gooddst=GOODDST, not_pinned=NOT_PINNED, nomatch=NOMATCH)
     with tempfile.TemporaryDirectory() as tmp:
-        b, kind = make_ip4_set()
-        r = run_ip4(b, tmp)
-        np.savez_compressed(os.path.join(HERE, "ip4.npz"), arena=b.arena, desc=b.desc, kind=kind, **r)
-        print("ip4:", np.bincount(r["reason"], minlength=7), "lb16 pinned", int((r["lb16"] != 255).sum()))
-        m = make_mix_set()
-        rm = run_mix(m, tmp)
-        np.savez_compressed(os.path.join(HERE, "mix.npz"), arena=m.arena, desc=m.desc, **rm)
-        print("mix:", np.bincount(rm["reason"], minlength=8))
-        kat = run_kat(tmp)
-        if kat is not None:
-            np.savez_compressed(os.path.join(HERE, "kat.npz"), **kat)
-            print("kat: cksum", len(kat["ck"]), "h4", len(kat["h4"]), "h6", len(kat["h6"]))
-    prov["sets"] = {
+        if "ip4" in sets:
+            b, kind = make_ip4_set()
+            r = run_ip4(b, tmp)
+            np.savez_compressed(os.path.join(HERE, "ip4.npz"), arena=b.arena, desc=b.desc, kind=kind, **r)
+            print("ip4:", np.bincount(r["reason"], minlength=7), "lb16 pinned", int((r["lb16"] != 255).sum()))
+        if "mix" in sets:
+            m = make_mix_set()
+            rm = run_mix(m, tmp)
+            np.savez_compressed(os.path.join(HERE, "mix.npz"), arena=m.arena, desc=m.desc, **rm)
+            print("mix:", np.bincount(rm["reason"], minlength=8))
+        if "prog" in sets:
+            pb, pkind = make_prog_set()
+            rp = run_prog(pb, tmp)
+            np.savez_compressed(os.path.join(HERE, "prog.npz"), arena=pb.arena, desc=pb.desc, kind=pkind, **rp)
+            print("prog: ipc", np.bincount(rp["ipc_out"], minlength=256)[[*range(9), 254, 255]],
+                  "cls", np.bincount(rp["cls_out"], minlength=256)[[*range(6), 254, 255]])
+        if "kat" in sets:
+            kat = run_kat(tmp)
+            if kat is not None:
+                np.savez_compressed(os.path.join(HERE, "kat.npz"), **kat)
+                print("kat: cksum", len(kat["ck"]), "h4", len(kat["h4"]), "h6", len(kat["h6"]))
+    prov.setdefault("sets", {}).update({
         "ip4": "CheckIPHeader(CHECKSUM true, BADSRC, GOODDST)/AggregateHash/FlowSwitch hash 16/HashSwitch(26,8)x{4,7}",
         "mix": "StripEtherVLANHeader(0) -> Classifier(0/60%f0,-) -> CheckIP6Header | CheckIPHeader(CHECKSUM true) -> AggregateHash",
+        "prog": "Strip(14) -> CheckIPHeader(CHECKSUM true) -> IPClassifier(IPC_RULES) | CheckIPHeader(OFFSET 14, CHECKSUM true) -> Classifier(CLS_RULES): program text + per-packet output",
         "kat": "fcref: click_in_cksum (lib/in_cksum.c), IPFlowID/IP6FlowID::hashcode (headers)",
-    }
-    with open(os.path.join(HERE, "PROVENANCE.json"), "w") as f:
+    })
+    prov["ipc_rules"] = IPC_RULES
+    prov["cls_rules"] = CLS_RULES
+    with open(prov_path, "w") as f:
         json.dump(prov, f, indent=1)
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]) or ("ip4", "mix", "prog", "kat"))

@@ -1,0 +1,233 @@
+"""Decision programs: IPFilter / IPClassifier / Classifier.
+
+The reference compiles its rule language into a step program and prints it
+through the element's `program` handler (elements/ip/ipfilter.cc:1402,
+elements/standard/classification.cc:978-991, :1104-1140). tests/golden/prog.npz
+holds, from the compiled reference (gen_golden.py, set "prog"):
+  * the program text of an IPClassifier with nine rules and of a Classifier
+    with six, exactly as `print c.program` printed them;
+  * the output every packet of a 3000-frame set left on (254 = no rule
+    matched -> killed; 255 = CheckIPHeader rejected it first).
+The C oracle's interpreter is pinned to those outputs; the HIP interpreter is
+checked against the goldens and against the oracle on random programs.
+"""
+import numpy as np
+import pytest
+
+from fastclick_amd import synth
+from fastclick_amd import _native as N
+from tests.helpers import compare, repack
+from tests.test_golden import load, batch_of
+
+NOMATCH, INVALID = 254, 255
+KINDS = {"ipc": N.PROG_IPFILTER, "cls": N.PROG_CLASSIFIER}
+
+
+def _program(g, name):
+    from fastclick_amd import click
+    text = bytes(g[f"{name}_prog"]).decode()
+    steps, oe = click.parse_program(text)
+    return text, (KINDS[name], steps, oe), int(g[f"{name}_nout"])
+
+
+def _outputs(r):
+    return np.where(r["reason"] == N.R_OK, r["port"],
+                    np.where(r["reason"] == N.R_NO_MATCH, NOMATCH, INVALID)).astype(np.uint8)
+
+
+def _cfg(nout, **kw):
+    return N.make_cfg(offset=14, checksum=True, classify=N.CLS_PROGRAM, nports=nout, **kw)
+
+
+# ---------------------------------------------------------------- parser (CPU)
+
+def test_parse_reference_program_text():
+    g = load("prog")
+    text, (kind, steps, oe), nout = _program(g, "ipc")
+    assert oe == -1 and len(steps) == text.count("yes->")
+    # step 0 of the IPClassifier: "264/00110000%00ff0000" = IP protocol == UDP
+    assert (steps[0].offset, steps[0].value, steps[0].mask) == (264, 0x1100, 0xFF00)
+    assert any(s.flags & N.STEP_SHORT_YES for s in steps)
+    # [X] (no output) is kept distinct from every real output
+    assert any(s.no == -2147483647 for s in steps)
+    _, (_, csteps, coe), cnout = _program(g, "cls")
+    assert coe == -1 and cnout == 6 and len(csteps) > 0
+
+
+def test_parse_errors_and_all():
+    from fastclick_amd import click
+    assert click.parse_program("all->[3]\nsafe length 0\nalignment offset 0\n") == ([], 3)
+    bad = [" 0 264/0011000%00ff0000  yes->[0]  no->[1]",          # short hex
+           " 1 264/00110000%00ff0000  yes->[0]  no->[1]",          # index != 0
+           " 0 264/00110000%00ff0000  yes->step 3  no->[1]",       # jump past the end
+           " 0 264/00110000%00ff0000  yes->[0]",                   # no "no->"
+           ""]
+    for t in bad:
+        with pytest.raises(click.ConfigError):
+            click.parse_program(t)
+    # '|' separates lines too (configuration strings)
+    steps, oe = click.parse_program(" 0 256/45000000%ff000000  yes->[0]  no->[1]|safe length 260")
+    assert len(steps) == 1 and steps[0].value == 0x45 and steps[0].mask == 0xFF
+
+
+def test_element_program_keyword_errors():
+    from fastclick_amd import click
+    ok = "GPUIPCheckClassify(OFFSET 14, N 2, PROGRAM \" 0 265/11000000%ff000000  yes->[0]  no->[1]\")"
+    click.check_config(ok)
+    for conf in ["GPUIPCheckClassify(OFFSET 14, N 1, PROGRAM \" 0 265/11000000%ff000000  yes->[0]  no->[1]\")",
+                 "GPUIPCheckClassify(OFFSET 14, N 2, PROGRAM \"garbage\")",
+                 "GPUIPCheckClassify(OFFSET 14, N 2, PROGRAM_KIND ETHER)",
+                 "GPUIPCheckClassify(OFFSET 14, N 2, PROGRAM \"all->[5]\")"]:
+        with pytest.raises(click.ConfigError):
+            click.check_config(conf)
+
+
+# ------------------------------------------------------- oracle vs reference
+
+@pytest.mark.parametrize("name", ["ipc", "cls"])
+def test_oracle_program_golden(oracle, name):
+    g = load("prog")
+    _, prog, nout = _program(g, name)
+    r = oracle.process_batch(_cfg(nout), batch_of(g), program=prog)
+    exp = g[f"{name}_out"]
+    got = _outputs(r)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, f"{name}: {len(bad)} packets differ, first {bad[:8]}: {got[bad[:8]]} vs {exp[bad[:8]]}"
+    # every rule and the no-match path are exercised
+    assert len(np.unique(exp)) == nout + 2
+    # counters: unmatched packets are counted (CheckIPHeader passed them) but
+    # are not CheckIPHeader drops
+    c = r["counters"]
+    assert c[N.CTR_COUNT] == (exp != INVALID).sum()
+    assert c[N.CTR_DROPS] == (exp == INVALID).sum()
+    assert c[N.CTR_REASON + N.NREASON_SLOTS - 1] == (exp == NOMATCH).sum()
+    assert c[N.CTR_PORT + nout] == (exp >= NOMATCH).sum()
+
+
+# ------------------------------------------------------------------- GPU
+
+def random_program(rng, batch, kind, nout, nsteps):
+    """Random forward-jumping program whose comparison values are taken from
+    real packets (so both branches are taken), with out-of-range outputs, [X]
+    and short->yes steps mixed in."""
+    A = batch.arena
+    off = batch.desc[:, 0].astype(np.int64)
+    steps = []
+    for k in range(nsteps):
+        if kind == N.PROG_IPFILTER:
+            base = int(rng.choice([0, 256, 512]))
+            o = base + int(rng.integers(0, 44 if base else 16)) + (int(rng.integers(0, 200)) if rng.random() < 0.05 else 0)
+            frame_off = 14 + (o - 256) if base == 256 else 34 + (o - 512) if base == 512 else o - 2
+        else:
+            o = int(rng.integers(0, 80)) + (int(rng.integers(0, 200)) if rng.random() < 0.05 else 0)
+            frame_off = o
+        p = int(rng.integers(0, batch.n))
+        fo = int(off[p]) + max(frame_off, 0)
+        word = int.from_bytes(A[fo:fo + 4].tobytes(), "little")
+        mb = [int(rng.choice([0, 0xFF, 0xF0, 0x0F, 0x80, 0x1F])) for _ in range(4)]
+        mask = int.from_bytes(bytes(mb), "little")
+        value = word & mask if rng.random() < 0.7 else int(rng.integers(0, 1 << 32)) & mask
+
+        def jump():
+            r = rng.random()
+            if r < 0.55 and k + 1 < nsteps:
+                return int(rng.integers(k + 1, nsteps))
+            if r < 0.85:
+                return -int(rng.integers(0, nout))
+            return -2147483647 if r < 0.92 else -nout - int(rng.integers(0, 3))   # [X] / missing output
+        steps.append((o, value, mask, jump(), jump(), int(rng.random() < 0.3)))
+    return steps
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    from fastclick_amd import device
+    N.load()
+    return device
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ipc", "cls"])
+def test_gpu_program_golden(dev, name):
+    g = load("prog")
+    _, prog, nout = _program(g, name)
+    for part in (N.PART_GLOBAL, N.PART_TILE):
+        r = dev.process_batch(batch_of(g), _cfg(nout), partition=part, program=prog)
+        got = _outputs(r)
+        exp = g[f"{name}_out"]
+        bad = np.nonzero(got != exp)[0]
+        assert len(bad) == 0, f"{name} part={part}: {len(bad)} differ, first {bad[:8]}: {got[bad[:8]]} vs {exp[bad[:8]]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", [N.PROG_IPFILTER, N.PROG_CLASSIFIER])
+@pytest.mark.parametrize("mode", ["c4", "mix", "misaligned"])
+def test_gpu_random_programs_vs_oracle(dev, oracle, kind, mode):
+    rng = np.random.default_rng(100 + kind * 10 + len(mode))
+    if mode == "mix":
+        b = synth.c5(20_000, seed=5)
+        base = dict(check_mode=N.CHECK_AUTO, checksum=True)
+    else:
+        b = synth.c4(20_000, seed=4)
+        synth.add_ip_options(b, 0.1, seed=6)
+        synth.inject_errors(b, 0.02, seed=7)
+        if mode == "misaligned":
+            b = repack(b, misalign_seed=8)
+        base = dict(offset=14, checksum=True)
+    outcomes = set()
+    for trial in range(6):
+        nout = int(rng.integers(1, 65))
+        nsteps = int(rng.integers(1, 120 if trial < 5 else 2000))
+        prog = (kind, random_program(rng, b, kind, nout, nsteps), -1)
+        cfg = N.make_cfg(classify=N.CLS_PROGRAM, nports=nout, **base)
+        exp = oracle.process_batch(cfg, b, program=prog)
+        for part in (N.PART_GLOBAL, N.PART_TILE):
+            got = dev.process_batch(b, cfg, partition=part, program=prog)
+            compare(got, exp, ctx=f"kind={kind} {mode} trial={trial} part={part}")
+            assert np.array_equal(got["counters"], exp["counters"])
+        outcomes |= set(np.unique(exp["reason"]).tolist())
+    assert N.R_NO_MATCH in outcomes and N.R_OK in outcomes
+
+
+@pytest.mark.gpu
+def test_gpu_program_output_everything(dev, oracle):
+    b = synth.c4(5000, seed=9)
+    synth.inject_errors(b, 0.05, seed=10)
+    for oe in (0, 3):
+        cfg = _cfg(4)
+        prog = (N.PROG_IPFILTER, [], oe)
+        exp = oracle.process_batch(cfg, b, program=prog)
+        got = dev.process_batch(b, cfg, partition=N.PART_TILE, program=prog)
+        compare(got, exp, ctx=f"all->[{oe}]")
+        assert (got["port"][got["reason"] == N.R_OK] == oe).all()
+
+
+@pytest.mark.gpu
+def test_gpu_program_required(dev):
+    b = synth.c1(100)
+    with pytest.raises(RuntimeError, match="fcgpu_set_program"):
+        dev.process_batch(b, _cfg(2))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ipc", "cls"])
+def test_element_program_golden(name):
+    """IPClassifier/Classifier through the element: packets leave on the rule's
+    output in input order, unmatched packets are killed, invalid ones leave on N."""
+    from fastclick_amd import click
+    g = load("prog")
+    text, _, nout = _program(g, name)
+    kind = "IPFILTER" if name == "ipc" else "CLASSIFIER"
+    conf = (f"GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N {nout}, PROGRAM_KIND {kind}, "
+            f"PROGRAM \"{text.replace(chr(10), '|')}\")")
+    res = click.run_element(conf, batch_of(g), nsinks=nout + 1)
+    exp = g[f"{name}_out"].astype(np.int64)
+    port = res["port"].astype(np.int64)
+    want = np.where(exp == NOMATCH, 0xFFFFFFFF, np.where(exp == INVALID, nout, exp))
+    assert np.array_equal(port, want)
+    seq = res["seq"].astype(np.int64)
+    for k in range(nout + 1):
+        sel = np.nonzero(port == k)[0]
+        assert np.all(np.diff(seq[sel]) > 0), f"output {k} order"
