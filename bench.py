@@ -61,13 +61,27 @@ def parse():
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse "
                          "several ranks on one GPU)")
+    ap.add_argument("--workload", choices=["c2", "c4"], default="c2",
+                    help="c2: one 5-tuple (BASELINE configs[1], the headline); c4: independent "
+                         "uniform random 5-tuples")
+    ap.add_argument("--classify", choices=["lb", "ipclass16"], default="lb",
+                    help="lb: FlowSwitch LB_MODE hash x16 (headline); ipclass16: the survey's "
+                         "IPClassifier with 15 UDP dst-port ranges + '-' (program printed by the "
+                         "reference compiler, tests/golden/reftests.json)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
 
-def cpu_baseline(seconds: float):
+def ipclass16_program():
+    """The survey's 16-output IPClassifier as compiled by the reference (text)."""
+    with open(os.path.join(ROOT, "tests", "golden", "reftests.json")) as f:
+        progs = {p["case"]: p for p in json.load(f)["programs"]}
+    return progs["ipclass16"]["program"]
+
+
+def cpu_baseline(seconds: float, flows: int = 1, program: str | None = None):
     """Reported CPU baseline: the scalar restatement of the reference elements
     (oracle/cpu_baseline.cc: 32-packet linked-list PacketBatch, CheckIPHeader ->
     AggregateHash -> FlowSwitch hash -> CLASSIFY_EACH_PACKET, atomic counters),
@@ -80,13 +94,23 @@ def cpu_baseline(seconds: float):
             return None
     cores = len(os.sched_getaffinity(0))
     cores = max(1, min(cores, 16))
+    cmd = [exe, "--seconds", str(seconds), "--threads", str(cores), "--flows", str(flows)]
+    tmp = None
+    if program is not None:
+        import tempfile
+        tmp = tempfile.NamedTemporaryFile("w", suffix=".prog", delete=False)
+        tmp.write(program)
+        tmp.close()
+        cmd += ["--program", tmp.name]
     try:
-        out = subprocess.run([exe, "--seconds", str(seconds), "--threads", str(cores)],
-                             capture_output=True, text=True, timeout=seconds * 4 + 60)
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=seconds * 4 + 60)
         res = json.loads(out.stdout.strip().splitlines()[-1])
     except Exception as e:  # reported baseline only
         print(f"cpu baseline failed: {e}", file=sys.stderr)
         return None
+    finally:
+        if tmp is not None:
+            os.unlink(tmp.name)
     return dict(value=round(res["mpps"], 3), unit="Mpps", cores=res["threads"], kind="port",
                 sample=res["sample"], mpps_1core=round(res.get("mpps_1core", 0.0), 3))
 
@@ -114,14 +138,21 @@ def main():
     from fastclick_amd.device import DeviceBatch, DeviceOutputs
 
     n = args.packets
-    host = synth.c2(n)
+    host = synth.c2(n) if args.workload == "c2" else synth.c4(n)
     # nbuf distinct copies at distinct HBM addresses
     bufs = []
     for k in range(args.nbuf):
         bufs.append(DeviceBatch.upload(host, device=dev))
     del host
-    cfg = N.make_cfg(offset=14, checksum=True, hash_mode=N.HASH_FLOWID, classify=N.CLS_LB_HASH,
-                     nports=args.nports)
+    program = None
+    if args.classify == "ipclass16":
+        from fastclick_amd import click
+        text = ipclass16_program()
+        steps, oe = click.parse_program(text)
+        program = (N.PROG_IPFILTER, steps, oe)
+        args.nports = 16
+    cfg = N.make_cfg(offset=14, checksum=True, hash_mode=N.HASH_FLOWID,
+                     classify=N.CLS_LB_HASH if program is None else N.CLS_PROGRAM, nports=args.nports)
     part = N.PART_TILE if args.partition == "tile" else N.PART_GLOBAL
     tile = part == N.PART_TILE
     nstreams = max(1, args.streams)
@@ -129,6 +160,8 @@ def main():
     ctxs, streams, optrs, outs_keep = [], [], [], []
     for _ in range(nstreams):
         ctxs.append(N.Context(local, n, cfg))
+        if program is not None:
+            ctxs[-1].set_program(*program)
         streams.append(torch.cuda.Stream(dev))
         o = DeviceOutputs(n, args.nports, device=dev, verdict=True, hash=True, anno=False,
                           perm=(not args.no_perm) and not tile, tile_perm=(not args.no_perm) and tile,
@@ -226,7 +259,8 @@ def main():
                         scan_ms=round(timing["k_scan_ms"], 5), part_ms=round(timing["k_part_ms"], 5))
         cpu = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(args.cpu_seconds)
+            cpu = cpu_baseline(args.cpu_seconds, flows=1 if args.workload == "c2" else 4096,
+                               program=ipclass16_program() if program is not None else None)
         line = {
             "metric": "Mpps device-resident, 64 B IPv4 cksum+classify, 1/2/4/8 MI355X",
             "value": round(mpps, 1),
@@ -241,13 +275,18 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": ("C2: 64 B IPv4/UDP (60-B frames in 64-B slots), 1M-packet "
-                             "device-resident batch, single 5-tuple; CheckIPHeader(CHECKSUM true)"
-                             " + AggregateHash + FlowSwitch hash 16 outputs"
+                "workload": (("C2: 64 B IPv4/UDP (60-B frames in 64-B slots), 1M-packet "
+                              "device-resident batch, single 5-tuple" if args.workload == "c2" else
+                              "C4: 64 B IPv4/UDP (60-B frames in 64-B slots), 1M-packet "
+                              "device-resident batch, independent uniform 5-tuples")
+                             + "; CheckIPHeader(CHECKSUM true) + AggregateHash + "
+                             + ("FlowSwitch hash 16 outputs" if program is None else
+                                "IPClassifier(15 UDP dst-port ranges, -) 16 outputs")
                              + ("" if args.no_perm else
                                 " + stable per-port partition of every 256-packet PacketBatch"
                                 if args.partition == "tile" else
                                 " + stable per-port partition of the whole 1M-packet batch")),
+                "classify": args.classify,
                 "partition": "none" if args.no_perm else args.partition,
                 "streams": nstreams,
                 "packets_per_step_per_gpu": n,

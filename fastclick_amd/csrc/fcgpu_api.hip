@@ -97,30 +97,40 @@ static hipEvent_t take_event(fcgpu_ctx *c) {
 
 // ev0/ev1 non-null: hipExtLaunchKernelGGL records them around the dispatch
 // itself (timestamps of the kernel, not of the stream around it).
-template <int CM, bool CK, int PART>
+template <int CM, bool CK, int PART, bool PROG>
 static void launch_rx(const RxArgs &a, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    const size_t lds = PROG ? prog_lds_bytes(a.cfg) : 0;
     if (ev0)
-        hipExtLaunchKernelGGL((k_rx<CM, CK, PART>), dim3(a.ntiles), dim3(kTile), 0, s, ev0, ev1, 0, a);
+        hipExtLaunchKernelGGL((k_rx<CM, CK, PART, PROG>), dim3(a.ntiles), dim3(kTile), lds, s, ev0, ev1, 0, a);
     else
-        hipLaunchKernelGGL((k_rx<CM, CK, PART>), dim3(a.ntiles), dim3(kTile), 0, s, a);
+        hipLaunchKernelGGL((k_rx<CM, CK, PART, PROG>), dim3(a.ntiles), dim3(kTile), lds, s, a);
 }
 
-template <int PART>
+template <int PART, bool PROG>
 static void launch_rx_part(uint32_t cm, bool ck, const RxArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     switch (cm * 2 + (ck ? 1 : 0)) {
-    case 0: launch_rx<FCGPU_CHECK_IP4, false, PART>(a, s, e0, e1); break;
-    case 1: launch_rx<FCGPU_CHECK_IP4, true, PART>(a, s, e0, e1); break;
-    case 2: case 3: launch_rx<FCGPU_MARK_IP4, false, PART>(a, s, e0, e1); break;
-    case 4: launch_rx<FCGPU_CHECK_AUTO, false, PART>(a, s, e0, e1); break;
-    default: launch_rx<FCGPU_CHECK_AUTO, true, PART>(a, s, e0, e1); break;
+    case 0: launch_rx<FCGPU_CHECK_IP4, false, PART, PROG>(a, s, e0, e1); break;
+    case 1: launch_rx<FCGPU_CHECK_IP4, true, PART, PROG>(a, s, e0, e1); break;
+    case 2: case 3: launch_rx<FCGPU_MARK_IP4, false, PART, PROG>(a, s, e0, e1); break;
+    case 4: launch_rx<FCGPU_CHECK_AUTO, false, PART, PROG>(a, s, e0, e1); break;
+    default: launch_rx<FCGPU_CHECK_AUTO, true, PART, PROG>(a, s, e0, e1); break;
     }
+}
+
+// PROG: the decision-program classifier is compiled only into the kernels
+// launched for FCGPU_CLS_PROGRAM, so the other modes keep their lean code.
+template <bool PROG>
+static void launch_rx_prog(int part, uint32_t cm, bool ck, const RxArgs &a, hipStream_t s, hipEvent_t e0,
+                           hipEvent_t e1) {
+    if (part == kPartTile) launch_rx_part<kPartTile, PROG>(cm, ck, a, s, e0, e1);
+    else if (part == kPartGlobal) launch_rx_part<kPartGlobal, PROG>(cm, ck, a, s, e0, e1);
+    else launch_rx_part<kPartNone, PROG>(cm, ck, a, s, e0, e1);
 }
 
 static void launch_rx_any(int part, uint32_t cm, bool ck, const RxArgs &a, hipStream_t s, hipEvent_t e0,
                           hipEvent_t e1) {
-    if (part == kPartTile) launch_rx_part<kPartTile>(cm, ck, a, s, e0, e1);
-    else if (part == kPartGlobal) launch_rx_part<kPartGlobal>(cm, ck, a, s, e0, e1);
-    else launch_rx_part<kPartNone>(cm, ck, a, s, e0, e1);
+    if (a.cfg.classify == FCGPU_CLS_PROGRAM) launch_rx_prog<true>(part, cm, ck, a, s, e0, e1);
+    else launch_rx_prog<false>(part, cm, ck, a, s, e0, e1);
 }
 
 extern "C" {

@@ -155,7 +155,9 @@ __device__ __forceinline__ uint32_t prog_word(const FrameView &f, int b) {
     return f.rd32(0) << (8 * (-b));
 }
 
-__device__ __forceinline__ uint32_t run_program(const DevCfg &c, const FrameView &f, const fcgpu_anno &an) {
+template <class Steps>
+__device__ __forceinline__ uint32_t run_program_on(const DevCfg &c, const FrameView &f, const fcgpu_anno &an,
+                                                   const Steps &prog) {
     if (c.prog_all >= 0) return (uint32_t)c.prog_all;
     const bool ipf = c.prog_kind == FCGPU_PROG_IPFILTER;
     int plen;
@@ -167,7 +169,7 @@ __device__ __forceinline__ uint32_t run_program(const DevCfg &c, const FrameView
     }
     int pos = 0;
     for (uint32_t it = 0; it <= c.prog_n; ++it) {
-        const uint4 st = c.prog[pos];
+        const uint4 st = prog[pos];
         const int off = (int16_t)(st.x & 0xffff);
         const uint32_t m = st.z;
         bool avail = off + 4 <= plen;
@@ -187,6 +189,20 @@ __device__ __forceinline__ uint32_t run_program(const DevCfg &c, const FrameView
         pos = j;
     }
     return (uint32_t)kProgUnmatched;   // malformed (cyclic) program
+}
+
+// Steps come from the workgroup's LDS copy when the program fits (sprog !=
+// nullptr, block-uniform), else from global memory.
+constexpr uint32_t kProgLds = 128;          // steps cached in LDS (<= 2 KiB)
+__host__ __device__ inline bool prog_in_lds(const DevCfg &c) {
+    return c.classify == FCGPU_CLS_PROGRAM && c.prog_all < 0 && c.prog_n <= kProgLds;
+}
+// dynamic LDS of a k_rx launch: only program mode pays for the step cache
+inline size_t prog_lds_bytes(const DevCfg &c) { return prog_in_lds(c) ? sizeof(uint4) * c.prog_n : 0; }
+__device__ __forceinline__ uint32_t run_program(const DevCfg &c, const FrameView &f, const fcgpu_anno &an,
+                                                const uint4 *sprog) {
+    if (sprog) return run_program_on(c, f, an, sprog);
+    return run_program_on(c, f, an, c.prog);
 }
 
 struct PktResult {
@@ -250,9 +266,9 @@ __device__ __forceinline__ uint32_t check_ip6(const DevCfg &c, const FrameView &
     return FCGPU_R_OK;
 }
 
-template <int CM, bool CK>
+template <int CM, bool CK, bool PROG>
 __device__ __forceinline__ void process_packet(const DevCfg &c, const FrameView &f, uint32_t len,
-                                               PktResult &r) {
+                                               PktResult &r, const uint4 *sprog) {
     fcgpu_anno &an = r.an;
     uint32_t o = (uint32_t)c.offset;
     uint32_t h[5] = {0, 0, 0, 0, 0};
@@ -314,7 +330,8 @@ __device__ __forceinline__ void process_packet(const DevCfg &c, const FrameView 
         r.port = (uint32_t)bytesum_port(f, an.length, c.hs_offset, c.hs_length, c.nports);
         break;
     case FCGPU_CLS_PROGRAM: {
-        const uint32_t out = run_program(c, f, an);
+        if (!PROG) { r.port = 0; break; }    // not launched this way (launch_rx_any)
+        const uint32_t out = run_program(c, f, an, sprog);
         if (out >= c.nports) {            // no output: CLASSIFY_EACH_PACKET kills it
             r.reason = FCGPU_R_NO_MATCH;
             r.port = c.nports;
@@ -333,8 +350,9 @@ __device__ __forceinline__ void process_packet(const DevCfg &c, const FrameView 
 // branches except the (wave-uniform) configuration. Returns false when this
 // lane needs the general path (options, header beyond the window, hash modes
 // or classifiers it does not cover); the caller then runs process_packet.
-template <bool CK>
-__device__ __forceinline__ bool ip4_fast(const DevCfg &c, const FrameView &f, uint32_t len, PktResult &r) {
+template <bool CK, bool PROG>
+__device__ __forceinline__ bool ip4_fast(const DevCfg &c, const FrameView &f, uint32_t len, PktResult &r,
+                                         const uint4 *sprog) {
     const uint32_t o = (uint32_t)c.offset;
     const uint32_t x = f.shift + o, a = x & ~3u, sh = x & 3u;
     const bool inwin = a + 28 <= (uint32_t)kWin;
@@ -382,19 +400,23 @@ __device__ __forceinline__ bool ip4_fast(const DevCfg &c, const FrameView &f, ui
         hv = first ? rotl32(h[3], (sp & 15) + 1) ^ rotl32(h[4], 31 - (dp & 15)) ^ ((dp << 16) | sp) : 0u;
         if (c.hash_mode == FCGPU_HASH_FLOW5ID) hv ^= (h[2] >> 8) & 0xff;
     }
-    uint32_t port;
+    uint32_t port = 0;
     if (c.classify == FCGPU_CLS_LB_HASH) port = (uint32_t)lb_port(hv, c.nports, c.lb_magic);
-    else if (c.classify == FCGPU_CLS_NONE) port = 0;
-    else return false;                                 // byte-sum classifiers: general path
+    else if (c.classify != FCGPU_CLS_NONE && (!PROG || c.classify != FCGPU_CLS_PROGRAM))
+        return false;                                  // byte-sum classifiers: general path
     r.reason = reason;
     r.hash = ok ? hv : 0u;
-    r.port = ok ? port : c.nports;
     fcgpu_anno &an = r.an;
     an.ipver = early == FCGPU_R_MINISCULE ? 0 : 4;
     an.nh = (uint8_t)(ok ? o : 0u);
     an.th = (uint8_t)(ok ? o + 20 : 0u);
     an.length = (uint16_t)(ok ? (plen > L ? len - (plen - L) : len) : 0u);
     an.dst_ip = ok ? h[4] : 0u;
+    if (PROG && ok) {                                  // FCGPU_CLS_PROGRAM
+        port = run_program(c, f, an, sprog);
+        if (port >= c.nports) r.reason = FCGPU_R_NO_MATCH;
+    }
+    r.port = ok && port < c.nports ? port : c.nports;
     return true;
 }
 
@@ -426,10 +448,11 @@ constexpr int kPartTile = 2;     // + stable partition of each 256-packet tile, 
 // -> classify over one 256-packet tile; per-tile histogram by wave ballots;
 // counters by sharded atomics; optionally the tile's stable per-output
 // partition (CLASSIFY_EACH_PACKET on a 256-packet PacketBatch).
-template <int CM, bool CK, int PART, bool FAST = (CM == FCGPU_CHECK_IP4)>
+template <int CM, bool CK, int PART, bool PROG, bool FAST = (CM == FCGPU_CHECK_IP4)>
 __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4 * kWave * kWin];
     __shared__ uint32_t s_cnt[4][kMaxBins];
+    extern __shared__ uint4 s_prog[];           // prog_lds_bytes(cfg) at launch
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // one 256-packet tile per workgroup (grid == ntiles). A grid-stride loop
     // measured slower here: hoisted loop invariants spill around it.
@@ -448,7 +471,12 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
         const uint32_t c = (lane & 3) ^ ((p >> 2) & 3);
         glds16(A.arena + (poff & ~15u) + c * 16, wl + k * 1024);
     }
+    // decision program: the block's LDS copy when it fits (block-uniform)
+    const bool prog_lds = PROG && prog_in_lds(A.cfg);
+    if (prog_lds && threadIdx.x < A.cfg.prog_n) s_prog[threadIdx.x] = A.cfg.prog[threadIdx.x];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (prog_lds) __syncthreads();
+    const uint4 *sprog = prog_lds ? s_prog : nullptr;
 
     FrameView f;
     f.row = wl + lane * kWin;
@@ -461,15 +489,15 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
     uint32_t bin = 0xffffffffu, rslot = 0xffffffffu;
     if (FAST && CM == FCGPU_CHECK_IP4) {
         bool done = !live;
-        if (live) done = ip4_fast<CK>(A.cfg, f, d.y, r);
+        if (live) done = ip4_fast<CK, PROG>(A.cfg, f, d.y, r, sprog);
         if (__ballot(!done)) {
             if (!done) {
                 r.an = fcgpu_anno{};
-                process_packet<CM, CK>(A.cfg, f, d.y, r);
+                process_packet<CM, CK, PROG>(A.cfg, f, d.y, r, sprog);
             }
         }
     } else if (live) {
-        process_packet<CM, CK>(A.cfg, f, d.y, r);
+        process_packet<CM, CK, PROG>(A.cfg, f, d.y, r, sprog);
     }
     if (live) {
         if (A.verdict) A.verdict[i] = (uint16_t)(r.reason | (r.port << 8));

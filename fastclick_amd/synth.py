@@ -164,6 +164,20 @@ def pack(hdr: np.ndarray, frame_len, *, meta=None) -> Batch:
     return Batch(arena=arena, desc=np.ascontiguousarray(desc), meta=dict(meta or {}))
 
 
+def from_frames(frames, meta=None) -> Batch:
+    """Batch holding the given frames (bytes) at 64-B aligned arena offsets."""
+    offs, pos = [], 0
+    for f in frames:
+        offs.append(pos)
+        pos += (max(len(f), 1) + 63) & ~63
+    arena = np.zeros(pos + ARENA_PAD, np.uint8)
+    for o, f in zip(offs, frames):
+        arena[o:o + len(f)] = np.frombuffer(bytes(f), np.uint8)
+    desc = np.stack([np.array(offs, np.uint32).reshape(-1),
+                     np.array([len(f) for f in frames], np.uint32).reshape(-1)], axis=1)
+    return Batch(arena=arena, desc=np.ascontiguousarray(desc.reshape(-1, 2)), meta=dict(meta or {}))
+
+
 def _rand_flows(rng, k):
     return dict(src=rng.integers(0, 2**32, k, dtype=np.uint64),
                 dst=rng.integers(0, 2**32, k, dtype=np.uint64),

@@ -12,7 +12,11 @@
 // fastclick_amd/csrc/host/click_model.hh; per-packet functions from the C
 // oracle (fc_oracle.c). Only bench.py's cpu_baseline leg and tests run this.
 //
-//   fc_cpu_baseline --seconds S --threads T [--flows K]   -> one JSON line
+//   fc_cpu_baseline --seconds S --threads T [--flows K] [--program FILE]
+//       -> one JSON line. With --program, the classify stage is an IPClassifier
+//       running the given program (reference `program` handler text) instead
+//       of FlowSwitch: IPFilter::match (elements/ip/ipfilter.hh:393-481) per
+//       packet, then CLASSIFY_EACH_PACKET.
 //   fc_cpu_baseline --verify                              -> exit 0 if the
 //       pipeline matches fco_process_batch on a batch with injected errors
 #include <atomic>
@@ -26,6 +30,7 @@
 
 #include "fc_oracle.h"
 #include "../fastclick_amd/csrc/host/click_model.hh"
+#include "../fastclick_amd/csrc/host/program_text.hh"
 
 using namespace fcx;
 
@@ -42,6 +47,7 @@ struct Pipeline {
     std::vector<uint32_t> *record_port = nullptr;   // verify mode: per-packet port
     std::vector<uint32_t> *record_hash = nullptr;
     int stages = 3;    // 0: Strip only (harness floor), 1: Strip+CheckIPHeader, 2: +AggregateHash, 3: +FlowSwitch classify
+    bool program = false;   // stage 3 = IPClassifier program (fco_set_program) instead of FlowSwitch
     Pipeline() { for (auto &r : reason_drops) r = 0; }
 
     // Strip::simple_action_batch (elements/standard/strip.cc:38-50)
@@ -113,7 +119,19 @@ struct Pipeline {
         Packet *p = b->first();
         while (p) {
             Packet *nx = p->next();
-            int o = fco_lb_hash_port(p->anno_u32(AGGREGATE_ANNO_OFFSET), 16);
+            int o;
+            if (program) {
+                // IPClassifier: offsets relative to the network/transport headers
+                fcgpu_anno a;
+                memset(&a, 0, sizeof a);
+                a.nh = 14;
+                a.th = (uint8_t)(14 + (p->transport_header() - p->network_header()));
+                a.length = (uint16_t)(p->length() + 14);
+                uint32_t out = fco_run_program(p->data() - 14, &a);
+                o = out < 16 ? (int)out : 16;
+            } else {
+                o = fco_lb_hash_port(p->anno_u32(AGGREGATE_ANNO_OFFSET), 16);
+            }
             if (record_port) {
                 (*record_port)[p->id] = (uint32_t)o;
                 (*record_hash)[p->id] = p->anno_u32(AGGREGATE_ANNO_OFFSET);
@@ -259,6 +277,7 @@ int main(int argc, char **argv) {
     int threads = 1;
     uint32_t flows = 1;
     int stages = 3;
+    std::string progfile;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         if (a == "--verify") return verify();
@@ -266,6 +285,20 @@ int main(int argc, char **argv) {
         else if (a == "--threads" && i + 1 < argc) threads = atoi(argv[++i]);
         else if (a == "--flows" && i + 1 < argc) flows = (uint32_t)atoi(argv[++i]);
         else if (a == "--stages" && i + 1 < argc) stages = atoi(argv[++i]);
+        else if (a == "--program" && i + 1 < argc) progfile = argv[++i];
+    }
+    if (!progfile.empty()) {
+        FILE *f = fopen(progfile.c_str(), "rb");
+        if (!f) { fprintf(stderr, "cannot open %s\n", progfile.c_str()); return 2; }
+        std::string text;
+        char buf[4096];
+        size_t k;
+        while ((k = fread(buf, 1, sizeof buf, f)) > 0) text.append(buf, k);
+        fclose(f);
+        ParsedProgram pr;
+        std::string e = parse_program(text, pr);
+        if (!e.empty()) { fprintf(stderr, "program: %s\n", e.c_str()); return 2; }
+        fco_set_program(FCGPU_PROG_IPFILTER, pr.steps.data(), (uint32_t)pr.steps.size(), pr.output_everything);
     }
     const uint32_t n = 4096;
     std::vector<uint8_t> arena;
@@ -280,6 +313,7 @@ int main(int argc, char **argv) {
             th.emplace_back([&, t]() {
                 Pipeline pl;
                 pl.stages = stages;
+                pl.program = !progfile.empty();
                 Replay src(arena.data(), desc.data(), n, 64);
                 uint64_t c = 0;
                 while (!stop.load(std::memory_order_relaxed)) {
@@ -306,7 +340,8 @@ int main(int argc, char **argv) {
     printf("{\"mpps\": %.3f, \"mpps_1core\": %.3f, \"threads\": %d, \"sample\": \"%s\"}\n", all, one, threads,
            ("C2-shaped 60-B UDP/IPv4 trace (4096 pkts, " + std::to_string(flows) +
             " flow(s)) replayed in 32-packet linked-list batches: Strip(14) -> CheckIPHeader(CHECKSUM true) -> "
-            "AggregateHash -> FlowSwitch hash x16 -> Discard; " + std::to_string(seconds / 2) +
+            "AggregateHash -> " + (progfile.empty() ? std::string("FlowSwitch hash x16") : std::string("IPClassifier program x16")) +
+            " -> Discard; " + std::to_string(seconds / 2) +
             " s at 1 thread + " + std::to_string(seconds / 2) + " s at all threads")
                .c_str());
     return 0;

@@ -23,6 +23,10 @@ Per field, the reference mechanism that produced it:
   hs4/hs7   HashSwitch(26, 8) with 4/7 outputs behind CheckIPHeader(OFFSET 14)
   v6        StripEtherVLANHeader -> Classifier(0/60%f0, -) -> CheckIP6Header /
             CheckIPHeader: verdicts and lengths; IP6FlowID hash from fcref
+  reftests  the reference's own classifier tests (test/ip/IPFilter-0[1-7],
+            test/standard/Classifier-01): printed programs (asserted equal to
+            the text those tests expect), outputs on the prog set, and the
+            short-packet cases with their transcribed expectations
   prog      IPClassifier (IPFILTER kind) and Classifier (CLASSIFIER kind)
             behind CheckIPHeader: each element's compiled program as its
             `program` handler prints it, and the output every packet left on
@@ -50,6 +54,7 @@ sys.path.insert(0, ROOT)
 from fastclick_amd import synth  # noqa: E402
 
 CLICK = os.environ.get("FC_CLICK", "/tmp/fcbuild/userlevel/click")
+REFERENCE = os.environ.get("FC_REFERENCE", "/root/reference")
 CLICK3 = os.environ.get("FC_CLICK3", "/tmp/fcbuild3/userlevel/click")
 FCREF = os.path.join(ROOT, "oracle", "_ref", "fcref")
 T0 = 1000
@@ -308,17 +313,33 @@ def make_prog_set(n=3000, seed=2026):
     datagrams (short->yes paths) and ~2% invalid headers."""
     rng = np.random.default_rng(seed)
     fl = synth._rand_flows(rng, n)
-    fl["dport"] = np.where(rng.random(n) < 0.6, rng.choice([53, 80, 443, 1500, 3000, 4095, 4096, 8080], n),
+    fl["dport"] = np.where(rng.random(n) < 0.6,
+                           rng.choice([53, 80, 443, 1500, 3000, 4095, 4096, 8080, 7777, 8888, 7000, 137, 5353], n),
                            fl["dport"]).astype(np.uint32)
-    fl["sport"] = np.where(rng.random(n) < 0.2, rng.integers(59990, 65536, n), fl["sport"]).astype(np.uint32)
+    r = rng.random(n)
+    fl["sport"] = np.where(r < 0.2, rng.integers(59990, 65536, n),
+                           np.where(r < 0.25, 68, np.where(r < 0.35, 0x0800, fl["sport"]))).astype(np.uint32)
+    r = rng.random(n)
+    fl["src"] = np.where(r < 0.05, (128 << 24) | (230 << 16) | (206 << 8) | rng.integers(0, 256, n),
+                         np.where(r < 0.08, (2 << 24), fl["src"])).astype(np.uint64)
+    fl["dst"] = np.where(rng.random(n) < 0.05, (128 << 24) | (230 << 16) | (206 << 8) | 7,
+                         np.where(rng.random(n) < 0.05, 10 << 24, fl["dst"])).astype(np.uint64)
     flen = rng.choice([60, 60, 74, 98, 128, 190], n)
     proto = rng.choice([17, 17, 6, 6, 1, 47], n)
     hdr = synth.build_headers(n, **fl, proto=proto, frame_len=flen)
     b = synth.pack(hdr, flen, meta=dict(set="prog", seed=seed))
     synth.add_ip_options(b, 0.1, seed=seed + 1)
     A = b.arena
+    macs = [bytes([0, 1, 2, 3, 4, 5]), bytes([0x10, 0x20, 0x30, 0x40, 0x50, 0x60]), bytes([9, 10, 11, 12, 13, 14]),
+            bytes([0, 1, 0, 0, 0, 0])]
     for i in range(n):
-        o = int(b.desc[i, 0]) + 14
+        f0 = int(b.desc[i, 0])
+        if rng.random() < 0.2:                 # Ethernet addresses for the MAC-offset rules
+            A[f0 + 6 * int(rng.integers(0, 2)):][:6] = list(macs[int(rng.integers(0, len(macs)))])
+        o = f0 + 14
+        hl = int(A[o] & 15) * 4
+        if A[o + 9] == 6:                      # TCP flags byte (SYN/ACK rules)
+            A[o + hl + 13] = int(rng.choice([0x02, 0x12, 0x10, 0x18, 0x00]))
         r = rng.random()
         if r < 0.05:                       # non-first fragment
             fo = int(rng.integers(1, 0x1FFF))
@@ -330,7 +351,7 @@ def make_prog_set(n=3000, seed=2026):
         if rng.random() < 0.1:
             A[o + 1] = 4
         if rng.random() < 0.04:            # truncate the datagram inside the L4 header
-            hl = (A[o] & 15) * 4
+            hl = int(A[o] & 15) * 4
             L = hl + int(rng.integers(0, 4))
             A[o + 2], A[o + 3] = L >> 8, L & 0xFF
         synth._refresh_cksum(A, o)
@@ -376,6 +397,146 @@ def run_prog(b, tmp):
     return res
 
 
+# Programs the reference's own tests pin (test/ip/IPFilter-0[4-7].clicktest,
+# test/standard/Classifier-01.clicktest): (case, test file, element config,
+# kind, number of outputs, path in front of the element). The printed program
+# must equal the text the test expects; the outputs on the prog set come from
+# the same compiled reference.
+REFTEST_PROGRAMS = [
+    ("IPFilter-04.c", "test/ip/IPFilter-04.clicktest",
+     "IPClassifier(dst port 7777, dst port 8888, dst port 7000, icmp type echo, icmp, -)", "ipf", 6),
+    ("IPFilter-04.d", "test/ip/IPFilter-04.clicktest",
+     "IPFilter(0 udp dst port netbios-ns, 1 udp dst port 5353, 2 udp src port bootpc, 3 128.230.206.0/24, 4 -)",
+     "ipf", 5),
+    ("IPFilter-04.e", "test/ip/IPFilter-04.clicktest",
+     "IPClassifier(proto icmp, dst port 53, (proto tcp and !(syn and !ack)) or (tcpudp port >= 1024), -)", "ipf", 4),
+    ("IPFilter-05", "test/ip/IPFilter-05.clicktest",
+     "IPFilter(allow tcp && dst 10.0.0.0/32 && src 2.0.0.0/32, allow tcp && dst 10.0.0.0/32 && dst port 80 "
+     "&& src 2.0.0.0/32, allow all)", "ipf", 1),
+    ("IPFilter-06", "test/ip/IPFilter-06.clicktest",
+     "IPFilter(allow src 0:1:2:3:4:5, allow src 10.0.0.0 & 8.0.0.0 = 8.0.0.0, allow dst 10:20:30:40:50:60, "
+     "allow host 9:A:B:C:D:E, deny all)", "ipf", 1),
+    ("IPFilter-07.1", "test/ip/IPFilter-07.clicktest", "IPFilter(allow false)", "ipf", 1),
+    ("IPFilter-07.2", "test/ip/IPFilter-07.clicktest", "IPFilter(allow false, allow false, allow false, allow true)",
+     "ipf", 1),
+    ("IPFilter-07.3", "test/ip/IPFilter-07.clicktest", "IPFilter(allow false, allow false, allow src 10.0.0.1)",
+     "ipf", 1),
+    ("IPFilter-07.5", "test/ip/IPFilter-07.clicktest", "IPFilter()", "ipf", 1),
+    ("Classifier-01", "test/standard/Classifier-01.clicktest", "Classifier(1/01, -)", "cls", 2),
+]
+# The survey's CPU classifier benchmark ("+ IPClassifier with 16
+# dst-port-range rules -> 16 ports"): 15 UDP dst-port ranges of 4096 + "-".
+IPCLASS16 = ("IPClassifier(" + ", ".join(f"dst udp port >= {i * 4096} and dst udp port < {(i + 1) * 4096}"
+                                         for i in range(15)) + ", -)")
+BENCH_PROGRAMS = [("ipclass16", None, IPCLASS16, "ipf", 16)]
+
+# Short-packet behaviour the reference's tests pin (IPFilter-01/02/03/08):
+# FromIPSummaryDump(IN) -> PaintSwitch; branch k goes through `chain` into
+# filter `f`. Expected outputs transcribed from each test's %expect section
+# (X = dropped). Every packet is captured from the reference as it enters the
+# filter (ToDump), with its network-header offset.
+SHORT_IN_1 = "!data link timestamp sport\n" + "".join(f"{k} {2 * k + 1} 0\n" for k in range(8))
+SHORT_IN_2 = "!data link timestamp sport\n" + "".join(f"{k // 2} {k + 1} {128 * (k % 2)}\n" for k in range(8))
+SHORT_IN_3 = "!data link timestamp sport\n" + "".join(f"{k // 2} {k + 1} {128 * (k % 2)}\n" for k in range(4))
+ETH = "EtherEncap(0x0800, 1:1:1:1:1:1, 2:2:2:2:2:2)"
+SHORT_CASES = [
+    ("IPFilter-01", "test/ip/IPFilter-01.clicktest:9-35", SHORT_IN_1,
+     {"f0": "IPFilter(0 ip[19]&128==0)", "f1": "IPFilter(0 transp[1]&128==0)"},
+     [("", "f0"), ("", "f1"), (ETH, "f0"), (ETH, "f1"), ("Truncate(19)", "f0"), ("Truncate(21)", "f1"),
+      (f"Truncate(19) -> {ETH}", "f0"), (f"Truncate(21) -> {ETH}", "f1")],
+     # A: 1, B: 3, A: 5, B: 7 pass; the truncated 9..15 are dropped
+     {"f0": {1: 0, 5: 0, 9: "X", 13: "X"}, "f1": {3: 0, 7: 0, 11: "X", 15: "X"}}),
+    ("IPFilter-02", "test/ip/IPFilter-02.clicktest:9-39", SHORT_IN_2,
+     {"f0": "IPFilter(0 transp[1]&128==0, 1 -)", "f1": "IPFilter(0 transp[1]&128!=0, 1 -)",
+      "fx": "IPFilter(0 transp[1]&128==0 || transp[1]&128==128)"},
+     [("", "f0"), ("", "f1"), ("Truncate(21)", "f0"), ("Truncate(21)", "f1")],
+     # A: 1 / B: 4 / C: 1 2 3 4; f0[1], f1[1] feed fx, which drops 5..8
+     {"f0": {1: 0, 2: 1, 5: 1, 6: 1}, "f1": {3: 1, 4: 0, 7: 1, 8: 1},
+      "fx": {1: 0, 2: 0, 3: 0, 4: 0, 5: "X", 6: "X", 7: "X", 8: "X"}}),
+    ("IPFilter-03", "test/ip/IPFilter-03.clicktest:9-30", SHORT_IN_3,
+     {"f0": "IPFilter(0 transp[1]&128!=0, 1 -)", "f1": "IPFilter(0 not (transp[1]&128==0))"},
+     [("", "f0"), ("Truncate(21)", "f0")],
+     # A: 2 / B: 2 3 4 (f0's output 1 feeds f1)
+     {"f0": {1: 1, 2: 0, 3: 1, 4: 1}, "f1": {1: "X", 2: 0, 3: 0, 4: 0}}),
+]
+
+
+def _clicktest_text(rel):
+    path = os.path.join(REFERENCE, rel)
+    return open(path).read() if os.path.exists(path) else None
+
+
+def _print_program(conf, nout):
+    outs = " ".join(f"c[{k}] -> Idle;" for k in range(nout))
+    r = subprocess.run([CLICK, "-e", f"Idle -> c :: {conf}; {outs}", "-qh", "c.program"],
+                       capture_output=True, text=True, timeout=60)
+    if r.returncode != 0:
+        raise RuntimeError(r.stderr)
+    return r.stdout
+
+
+def run_reftests(b, tmp):
+    """Reference-test programs on the prog set + the short-packet cases."""
+    pcap = os.path.join(tmp, "prog.pcap")
+    write_pcap(pcap, b.frames())
+    n = b.n
+    out = {"programs": [], "short": []}
+    for case, rel, conf, kind, nout in REFTEST_PROGRAMS + BENCH_PROGRAMS:
+        prog = _print_program(conf, nout)
+        text = _clicktest_text(rel) if rel else None
+        if text is not None:
+            want = prog.replace("[2147483647]", "[{{2147483647|X}}]")
+            assert want in text, f"{case}: printed program differs from {rel}:\n{prog}"
+        pre = ("Strip(14) -> chk :: CheckIPHeader(CHECKSUM true)" if kind == "ipf" and case != "IPFilter-06"
+               else "chk :: CheckIPHeader(OFFSET 14, CHECKSUM true)")
+        outs = " ".join(f"c[{k}] -> ToIPSummaryDump(rt{k}.ipsum, FIELDS timestamp);" for k in range(nout))
+        for k in [*range(nout), "bad"]:
+            if os.path.exists(os.path.join(tmp, f"rt{k}.ipsum")):
+                os.remove(os.path.join(tmp, f"rt{k}.ipsum"))
+        click(CLICK, f"FromDump(prog.pcap, STOP true, TIMING false) -> {pre} -> c :: {conf}; {outs} "
+                     "chk[1] -> ToIPSummaryDump(rtbad.ipsum, FIELDS timestamp);", tmp)
+        got = np.full(n, NOMATCH, np.int64)
+        for k in range(nout):
+            for i in read_ipsum(os.path.join(tmp, f"rt{k}.ipsum"), 0):
+                got[i] = k
+        for i in read_ipsum(os.path.join(tmp, "rtbad.ipsum"), 0):
+            got[i] = 255
+        out["programs"].append(dict(case=case, test=rel, config=conf, kind=kind, nout=nout,
+                                    program=prog, outputs=got.tolist()))
+    for case, rel, infile, filters, routes, expect in SHORT_CASES:
+        d = os.path.join(tmp, case)
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "IN"), "w") as f:
+            f.write(infile)
+        graph = ["FromIPSummaryDump(IN, STOP true) -> ps :: PaintSwitch;"]
+        for k, (chain, _) in enumerate(routes):
+            enc = "ETHER" if "EtherEncap" in chain else "IP"
+            graph.append(f"ps[{k}] -> {chain + ' -> ' if chain else ''}ToDump(p{k}.pcap, ENCAP {enc});")
+        click(CLICK, " ".join(graph), d)
+        pkts = []
+        for k, (chain, fname) in enumerate(routes):
+            for ts_idx, (incl, data) in sorted(read_pcap(os.path.join(d, f"p{k}.pcap")).items()):
+                ts = ts_idx + T0
+                pkts.append(dict(ts=ts, filter=fname, nh=14 if "EtherEncap" in chain else 0,
+                                 bytes=data.hex()))
+        # fx in IPFilter-02 and f1 in IPFilter-03 also see the other filters' outputs
+        feeds = {"IPFilter-02": {"fx": ["f0", "f1"]}, "IPFilter-03": {"f1": ["f0"]}}.get(case, {})
+        for tgt, srcs in feeds.items():
+            for p in list(pkts):
+                if p["filter"] in srcs:
+                    pkts.append(dict(p, filter=tgt))
+        progs = {fn: _print_program(conf, 2 if ", 1 -" in conf else 1) for fn, conf in filters.items()}
+        # the reference itself on each captured packet (must equal the test's expectation)
+        for p in pkts:
+            exp = expect[p["filter"]].get(p["ts"])
+            if exp is None:
+                continue
+            p["expect"] = exp
+        out["short"].append(dict(case=case, test=rel, filters=filters, programs=progs,
+                                 packets=[p for p in pkts if "expect" in p]))
+    return out
+
+
 def run_kat(tmp):
     """click_in_cksum on random buffers (odd lengths included) and IPFlowID /
     IP6FlowID hashcodes on random tuples, from the reference harness."""
@@ -405,7 +566,7 @@ def sha(path):
     return hashlib.sha256(open(path, "rb").read()).hexdigest()
 
 
-def main(sets=("ip4", "mix", "prog", "kat")):
+def main(sets=("ip4", "mix", "prog", "reftests", "kat")):
     prov_path = os.path.join(HERE, "PROVENANCE.json")
     prov = json.load(open(prov_path)) if os.path.exists(prov_path) else {}
     prov.update(generator="tests/golden/gen_golden.py", click=CLICK, click_sha256=sha(CLICK),
@@ -428,6 +589,15 @@ def main(sets=("ip4", "mix", "prog", "kat")):
             np.savez_compressed(os.path.join(HERE, "prog.npz"), arena=pb.arena, desc=pb.desc, kind=pkind, **rp)
             print("prog: ipc", np.bincount(rp["ipc_out"], minlength=256)[[*range(9), 254, 255]],
                   "cls", np.bincount(rp["cls_out"], minlength=256)[[*range(6), 254, 255]])
+        if "reftests" in sets:
+            pb, _ = make_prog_set()
+            rt = run_reftests(pb, tmp)
+            with open(os.path.join(HERE, "reftests.json"), "w") as f:
+                json.dump(rt, f, indent=0)
+            for p in rt["programs"]:
+                o = np.array(p["outputs"])
+                print("reftests:", p["case"], np.bincount(o[o < 254]).tolist(), "nomatch", int((o == 254).sum()),
+                      "invalid", int((o == 255).sum()))
         if "kat" in sets:
             kat = run_kat(tmp)
             if kat is not None:
@@ -437,6 +607,10 @@ def main(sets=("ip4", "mix", "prog", "kat")):
         "ip4": "CheckIPHeader(CHECKSUM true, BADSRC, GOODDST)/AggregateHash/FlowSwitch hash 16/HashSwitch(26,8)x{4,7}",
         "mix": "StripEtherVLANHeader(0) -> Classifier(0/60%f0,-) -> CheckIP6Header | CheckIPHeader(CHECKSUM true) -> AggregateHash",
         "prog": "Strip(14) -> CheckIPHeader(CHECKSUM true) -> IPClassifier(IPC_RULES) | CheckIPHeader(OFFSET 14, CHECKSUM true) -> Classifier(CLS_RULES): program text + per-packet output",
+        "reftests": "programs printed by the reference for the configs of test/ip/IPFilter-0[4-7] and "
+                    "test/standard/Classifier-01 (checked equal to those tests' expected text) + their outputs on "
+                    "the prog set; IPFilter-01/02/03 short-packet cases (packets captured from the reference, "
+                    "expected outputs from the tests' %expect sections)",
         "kat": "fcref: click_in_cksum (lib/in_cksum.c), IPFlowID/IP6FlowID::hashcode (headers)",
     })
     prov["ipc_rules"] = IPC_RULES
@@ -446,4 +620,4 @@ def main(sets=("ip4", "mix", "prog", "kat")):
 
 
 if __name__ == "__main__":
-    main(tuple(sys.argv[1:]) or ("ip4", "mix", "prog", "kat"))
+    main(tuple(sys.argv[1:]) or ("ip4", "mix", "prog", "reftests", "kat"))

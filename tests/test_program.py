@@ -231,3 +231,71 @@ def test_element_program_golden(name):
     for k in range(nout + 1):
         sel = np.nonzero(port == k)[0]
         assert np.all(np.diff(seq[sel]) > 0), f"output {k} order"
+
+
+# ---------------------------------- programs and cases the reference's tests pin
+
+def _reftests():
+    import json
+    import os
+    from tests.test_golden import HERE
+    with open(os.path.join(HERE, "reftests.json")) as f:
+        return json.load(f)
+
+
+def _run_reftest_programs(run):
+    from fastclick_amd import click
+    g = load("prog")
+    b = batch_of(g)
+    for case in _reftests()["programs"]:
+        steps, oe = click.parse_program(case["program"])
+        kind = KINDS["cls" if case["kind"] == "cls" else "ipc"]
+        r = run(_cfg(case["nout"]), b, (kind, steps, oe))
+        exp = np.array(case["outputs"], np.int64)
+        assert len(exp) == b.n
+        got = _outputs(r).astype(np.int64)
+        bad = np.nonzero(got != exp)[0]
+        assert len(bad) == 0, f"{case['case']} ({case['test']}): {len(bad)} differ, first {bad[:8]}"
+
+
+def _run_short_cases(run):
+    """IPFilter-01/02/03/08: truncated IP packets behind a header-marking
+    source (FromIPSummaryDump sets the IP header like MarkIPHeader), raw IP
+    (nh 0) or Ethernet-encapsulated (nh 14)."""
+    from fastclick_amd import click
+    for case in _reftests()["short"]:
+        for fname, text in case["programs"].items():
+            steps, oe = click.parse_program(text)
+            nout = 2 if ", 1 -" in case["filters"][fname] else 1
+            for nh in (0, 14):
+                pk = [p for p in case["packets"] if p["filter"] == fname and p["nh"] == nh]
+                if not pk:
+                    continue
+                b = synth.from_frames([bytes.fromhex(p["bytes"]) for p in pk])
+                cfg = N.make_cfg(check_mode=N.MARK_IP4, offset=nh, hash_mode=N.HASH_NONE,
+                                 classify=N.CLS_PROGRAM, nports=nout)
+                r = run(cfg, b, (N.PROG_IPFILTER, steps, oe))
+                for j, p in enumerate(pk):
+                    want = (N.R_NO_MATCH, nout) if p["expect"] == "X" else (N.R_OK, p["expect"])
+                    got = (int(r["reason"][j]), int(r["port"][j]))
+                    assert got == want, f"{case['case']} {fname} ts={p['ts']} len={len(p['bytes']) // 2}: {got} vs {want}"
+
+
+def test_oracle_reference_test_programs(oracle):
+    _run_reftest_programs(lambda cfg, b, prog: oracle.process_batch(cfg, b, program=prog))
+
+
+def test_oracle_reference_short_packet_cases(oracle):
+    _run_short_cases(lambda cfg, b, prog: oracle.process_batch(cfg, b, program=prog))
+
+
+@pytest.mark.gpu
+def test_gpu_reference_test_programs(dev):
+    for part in (N.PART_GLOBAL, N.PART_TILE):
+        _run_reftest_programs(lambda cfg, b, prog: dev.process_batch(b, cfg, partition=part, program=prog))
+
+
+@pytest.mark.gpu
+def test_gpu_reference_short_packet_cases(dev):
+    for part in (N.PART_GLOBAL, N.PART_TILE):
+        _run_short_cases(lambda cfg, b, prog: dev.process_batch(b, cfg, partition=part, program=prog))
