@@ -14,7 +14,7 @@ LIBFCGPU = os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 4
+ABI_VERSION = 5
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
     R_BAD_IP6, R_VLAN_REJECT, R_NO_MATCH = range(10)
@@ -124,6 +124,9 @@ FCGPU_SYMBOLS = {
                                      C.POINTER(fcgpu_out)]),
     "fcgpu_set_program": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(fcgpu_step), C.c_uint32,
                                     C.c_int32]),
+    "fcgpu_set_host_threads": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "fcgpu_host_alloc": (C.c_void_p, [C.c_size_t]),
+    "fcgpu_host_free": (None, [C.c_void_p]),
     "fcgpu_read_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "fcgpu_reset_counters": (C.c_int, [C.c_void_p]),
     "fcgpu_counters_device": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
@@ -263,6 +266,9 @@ class Context:
             arr[i] = st if isinstance(st, fcgpu_step) else fcgpu_step(*[int(x) for x in st])
         self._chk(self.lib.fcgpu_set_program(self.h, kind, arr, len(steps), output_everything),
                   "fcgpu_set_program")
+
+    def set_host_threads(self, n: int):
+        self._chk(self.lib.fcgpu_set_host_threads(self.h, n), "fcgpu_set_host_threads")
 
     def counters(self, n=NCOUNTERS):
         buf = (C.c_uint64 * n)()

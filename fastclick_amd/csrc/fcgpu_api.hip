@@ -14,7 +14,12 @@
 #include <stdint.h>
 #include <string.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fcgpu_device.hh"
@@ -35,6 +40,101 @@ struct EvPair {
     hipEvent_t a, b;
     int stage;
 };
+
+constexpr uint32_t kChunk = 65536;          // packets per host-pipeline chunk (whole tiles)
+constexpr int kSlots = 3;                   // chunks in flight: gather / copy+kernel / drain
+
+// Host worker pool for the gather and copy-out loops (fcgpu_set_host_threads).
+// The calling thread always takes part; n - 1 workers are started.
+class Pool {
+  public:
+    ~Pool() { resize(1); }
+    void resize(uint32_t n) {
+        {
+            std::unique_lock<std::mutex> lk(m_);
+            quit_ = true;
+            cv_.notify_all();
+        }
+        for (auto &t : th_) t.join();
+        th_.clear();
+        quit_ = false;
+        for (uint32_t k = 1; k < n; ++k) th_.emplace_back([this, k] { loop(k); });
+    }
+    uint32_t size() const { return (uint32_t)th_.size() + 1; }
+    // fn(part, nparts) on every member, the caller included; returns when all are done
+    void run(const std::function<void(uint32_t, uint32_t)> &fn) {
+        const uint32_t np = size();
+        if (np == 1) { fn(0, 1); return; }
+        {
+            std::unique_lock<std::mutex> lk(m_);
+            job_ = &fn;
+            left_ = np - 1;
+            ++gen_;
+            cv_.notify_all();
+        }
+        fn(0, np);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [this] { return left_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void loop(uint32_t k) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(uint32_t, uint32_t)> *job;
+            uint32_t np;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+                job = job_;
+                np = (uint32_t)th_.size() + 1;
+            }
+            (*job)(k, np);
+            std::unique_lock<std::mutex> lk(m_);
+            if (--left_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(uint32_t, uint32_t)> *job_ = nullptr;
+    uint32_t left_ = 0;
+    uint64_t gen_ = 0;
+    bool quit_ = false;
+};
+
+// One in-flight chunk of the host-resident pipeline: pinned staging in, device
+// copies, device outputs, pinned outputs (used when the caller's arrays are
+// pageable), its own stream and completion event.
+struct HostSlot {
+    hipStream_t s = nullptr;
+    hipEvent_t done = nullptr;
+    uint8_t *h_arena = nullptr, *d_arena = nullptr;
+    uint32_t *h_desc = nullptr, *d_desc = nullptr;
+    uint16_t *d_v = nullptr, *h_v = nullptr;
+    uint32_t *d_h = nullptr, *h_h = nullptr;
+    fcgpu_anno *d_an = nullptr, *h_an = nullptr;
+    uint32_t *d_perm = nullptr, *h_perm = nullptr;
+    uint8_t *d_tp = nullptr, *h_tp = nullptr;
+    uint16_t *d_tc = nullptr, *h_tc = nullptr;
+    bool busy = false;
+    uint32_t base = 0, n = 0;
+};
+
+inline uint32_t span(uint32_t n, uint32_t part, uint32_t np) { return (uint32_t)((uint64_t)n * part / np); }
+
+bool host_pinned(const void *p) {
+    if (!p) return false;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
 }  // namespace
 
 struct fcgpu_ctx {
@@ -61,6 +161,10 @@ struct fcgpu_ctx {
     uint16_t *d_htc = nullptr;
     uint8_t *d_htp = nullptr;
     fcgpu_anno *d_hanno = nullptr;
+    // pipelined host path (FCGPU_PART_TILE / no whole-batch partition)
+    HostSlot slot[kSlots];
+    uint32_t slot_cap = 0;
+    Pool pool;
     // timing
     bool timing = false;
     std::vector<EvPair> pending;
@@ -133,6 +237,71 @@ static void launch_rx_any(int part, uint32_t cm, bool ck, const RxArgs &a, hipSt
     else launch_rx_prog<false>(part, cm, ck, a, s, e0, e1);
 }
 
+// Whole batch in one shot (FCGPU_PART_GLOBAL: the partition spans the batch).
+static int process_host_whole(fcgpu_ctx *c, const uint8_t *const *frames, const uint32_t *lens, uint32_t n,
+                              const fcgpu_out *h) {
+    const size_t arena_cap = (size_t)c->max_batch * kHostCap + kArenaPad;
+    if (!c->h_arena) {
+        // the context's own stream exists only for the host-resident path (a
+        // stream per context maps onto one of the few hardware queues)
+        HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        HIPCHK(c, hipHostMalloc((void **)&c->h_arena, arena_cap, hipHostMallocDefault));
+        HIPCHK(c, hipHostMalloc((void **)&c->h_desc, sizeof(uint32_t) * 2 * c->max_batch, hipHostMallocDefault));
+        HIPCHK(c, hipMalloc(&c->d_arena, arena_cap));
+        HIPCHK(c, hipMemset(c->d_arena, 0, arena_cap));
+        HIPCHK(c, hipMalloc(&c->d_desc, sizeof(uint32_t) * 2 * c->max_batch));
+        HIPCHK(c, hipMalloc(&c->d_hv, sizeof(uint16_t) * c->max_batch));
+        HIPCHK(c, hipMalloc(&c->d_hh, sizeof(uint32_t) * c->max_batch));
+        HIPCHK(c, hipMalloc(&c->d_hperm, sizeof(uint32_t) * c->max_batch));
+        HIPCHK(c, hipMalloc(&c->d_hstart, sizeof(uint32_t) * (FCGPU_MAX_PORTS + 2)));
+        HIPCHK(c, hipMalloc(&c->d_hanno, sizeof(fcgpu_anno) * c->max_batch));
+        HIPCHK(c, hipMalloc(&c->d_htc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * c->max_tiles));
+        HIPCHK(c, hipMalloc(&c->d_htp, (size_t)c->max_batch + kTile));
+    }
+    // gather: first min(len, 128) bytes of each frame at 64-B aligned offsets.
+    // The device sees the real frame length; bytes past the capture are never
+    // needed for a verdict with headers <= 128 B.
+    size_t off = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t cap = lens[i] < kHostCap ? lens[i] : kHostCap;
+        memcpy(c->h_arena + off, frames[i], cap);
+        c->h_desc[2 * i] = (uint32_t)off;
+        c->h_desc[2 * i + 1] = lens[i];
+        off += (cap + 63) & ~(size_t)63;
+        if (cap == 0) off += 64;
+    }
+    hipStream_t s = c->stream;
+    HIPCHK(c, hipMemcpyAsync(c->d_arena, c->h_arena, off, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->d_desc, c->h_desc, sizeof(uint32_t) * 2 * n, hipMemcpyHostToDevice, s));
+    fcgpu_out d;
+    d.verdict = c->d_hv;
+    d.hash = h->hash ? c->d_hh : nullptr;
+    d.anno = h->anno ? c->d_hanno : nullptr;
+    d.perm = h->perm ? c->d_hperm : nullptr;
+    d.port_start = h->port_start ? c->d_hstart : nullptr;
+    d.tile_count = h->tile_count ? c->d_htc : nullptr;
+    d.partition = h->partition;
+    d.reserved = 0;
+    d.tile_perm = h->tile_perm ? c->d_htp : nullptr;
+    int rc = fcgpu_process(c, c->d_arena, c->d_desc, n, &d, s);
+    if (rc != FCGPU_OK) return rc;
+    if (h->verdict) HIPCHK(c, hipMemcpyAsync(h->verdict, d.verdict, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, s));
+    if (h->hash) HIPCHK(c, hipMemcpyAsync(h->hash, d.hash, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
+    if (h->anno) HIPCHK(c, hipMemcpyAsync(h->anno, d.anno, sizeof(fcgpu_anno) * n, hipMemcpyDeviceToHost, s));
+    if (h->perm) HIPCHK(c, hipMemcpyAsync(h->perm, d.perm, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
+    if (h->tile_perm) HIPCHK(c, hipMemcpyAsync(h->tile_perm, d.tile_perm, n, hipMemcpyDeviceToHost, s));
+    if (h->tile_count)
+        HIPCHK(c, hipMemcpyAsync(h->tile_count, d.tile_count,
+                                 sizeof(uint16_t) * (c->cfg.nports + 1) * ((n + kTile - 1) / kTile),
+                                 hipMemcpyDeviceToHost, s));
+    if (h->port_start)
+        HIPCHK(c, hipMemcpyAsync(h->port_start, d.port_start, sizeof(uint32_t) * (c->cfg.nports + 2),
+                                 hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    return FCGPU_OK;
+}
+
+
 extern "C" {
 
 int fcgpu_abi_version(void) { return FCGPU_ABI_VERSION; }
@@ -184,6 +353,17 @@ void fcgpu_close(fcgpu_ctx *c) {
         hipHostFree(c->h_arena);
         hipHostFree(c->h_desc);
         if (c->stream) hipStreamDestroy(c->stream);
+        for (auto &sl : c->slot) {
+            if (sl.s) hipStreamSynchronize(sl.s);
+            for (void *p : {(void *)sl.d_arena, (void *)sl.d_desc, (void *)sl.d_v, (void *)sl.d_h, (void *)sl.d_an,
+                            (void *)sl.d_perm, (void *)sl.d_tp, (void *)sl.d_tc})
+                hipFree(p);
+            for (void *p : {(void *)sl.h_arena, (void *)sl.h_desc, (void *)sl.h_v, (void *)sl.h_h, (void *)sl.h_an,
+                            (void *)sl.h_perm, (void *)sl.h_tp, (void *)sl.h_tc})
+                hipHostFree(p);
+            if (sl.done) hipEventDestroy(sl.done);
+            if (sl.s) hipStreamDestroy(sl.s);
+        }
     }
     delete c;
 }
@@ -329,71 +509,191 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     return FCGPU_OK;
 }
 
+static int slot_alloc(fcgpu_ctx *c, HostSlot &sl, uint32_t cap) {
+    const size_t tiles = (cap + kTile - 1) / kTile;
+    HIPCHK(c, hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
+    HIPCHK(c, hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    const size_t arena = (size_t)cap * kHostCap + kArenaPad;
+    HIPCHK(c, hipHostMalloc((void **)&sl.h_arena, arena, hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc((void **)&sl.h_desc, sizeof(uint32_t) * 2 * cap, hipHostMallocDefault));
+    HIPCHK(c, hipMalloc(&sl.d_arena, arena));
+    HIPCHK(c, hipMemset(sl.d_arena, 0, arena));
+    HIPCHK(c, hipMalloc(&sl.d_desc, sizeof(uint32_t) * 2 * cap));
+    HIPCHK(c, hipMalloc(&sl.d_v, sizeof(uint16_t) * cap));
+    HIPCHK(c, hipMalloc(&sl.d_h, sizeof(uint32_t) * cap));
+    HIPCHK(c, hipMalloc(&sl.d_an, sizeof(fcgpu_anno) * cap));
+    HIPCHK(c, hipMalloc(&sl.d_perm, sizeof(uint32_t) * cap));
+    HIPCHK(c, hipMalloc(&sl.d_tp, (size_t)cap + kTile));
+    HIPCHK(c, hipMalloc(&sl.d_tc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * tiles));
+    HIPCHK(c, hipHostMalloc((void **)&sl.h_v, sizeof(uint16_t) * cap, hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc((void **)&sl.h_h, sizeof(uint32_t) * cap, hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc((void **)&sl.h_an, sizeof(fcgpu_anno) * cap, hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc((void **)&sl.h_perm, sizeof(uint32_t) * cap, hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc((void **)&sl.h_tp, (size_t)cap + kTile, hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc((void **)&sl.h_tc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * tiles,
+                            hipHostMallocDefault));
+    return FCGPU_OK;
+}
+
+namespace {
+struct PinnedOut {           // which caller arrays the DMA engine can write directly
+    bool v, h, an, perm, tp, tc;
+};
+}
+
+// Copy a finished chunk's outputs from pinned staging into the caller's
+// (pageable) arrays; `perm` entries become batch indices.
+static void slot_drain(fcgpu_ctx *c, HostSlot &sl, const fcgpu_out *h, const PinnedOut &pin) {
+    const uint32_t nb = c->cfg.nports + 1, n = sl.n, base = sl.base;
+    const uint32_t ntile = (n + kTile - 1) / kTile, tbase = base / kTile;
+    c->pool.run([&](uint32_t part, uint32_t np) {
+        const uint32_t lo = span(n, part, np), hi = span(n, part + 1, np);
+        if (hi <= lo) return;
+        if (h->verdict && !pin.v) memcpy(h->verdict + base + lo, sl.h_v + lo, sizeof(uint16_t) * (hi - lo));
+        if (h->hash && !pin.h) memcpy(h->hash + base + lo, sl.h_h + lo, sizeof(uint32_t) * (hi - lo));
+        if (h->anno && !pin.an) memcpy(h->anno + base + lo, sl.h_an + lo, sizeof(fcgpu_anno) * (hi - lo));
+        if (h->tile_perm && !pin.tp) memcpy(h->tile_perm + base + lo, sl.h_tp + lo, hi - lo);
+        if (h->perm) {
+            uint32_t *dst = h->perm + base;
+            const uint32_t *src = pin.perm ? dst : sl.h_perm;
+            for (uint32_t k = lo; k < hi; ++k) dst[k] = src[k] + base;
+        }
+        if (h->tile_count && !pin.tc && part == 0)
+            memcpy(h->tile_count + (size_t)tbase * nb, sl.h_tc, sizeof(uint16_t) * nb * ntile);
+    });
+    sl.busy = false;
+}
+
+// Host-resident batches, pipelined in chunks of kChunk packets over kSlots
+// streams: while chunk k is copied in, classified and copied out on its own
+// stream, the host gathers chunk k+1 (and drains chunk k-2). Every chunk is a
+// whole number of 256-packet tiles, so per-tile outputs are those of the
+// whole batch.
+static int process_host_pipelined(fcgpu_ctx *c, const uint8_t *const *frames, const uint32_t *lens, uint32_t n,
+                                  const fcgpu_out *h) {
+    if (!c->slot_cap) {
+        uint32_t chunk = kChunk;
+        if (const char *e = getenv("FCGPU_HOST_CHUNK")) {      // tuning knob (packets, whole tiles)
+            const long v = atol(e);
+            if (v >= kTile && v <= (1L << 24)) chunk = (uint32_t)v;
+        }
+        uint32_t cap = c->max_batch < chunk ? c->max_batch : chunk;
+        cap = (cap + kTile - 1) / kTile * kTile;
+        for (auto &sl : c->slot) {
+            int rc = slot_alloc(c, sl, cap);
+            if (rc != FCGPU_OK) return rc;
+        }
+        c->slot_cap = cap;
+    }
+    const uint32_t cap = c->slot_cap, nb = c->cfg.nports + 1;
+    PinnedOut pin{host_pinned(h->verdict), host_pinned(h->hash), host_pinned(h->anno), host_pinned(h->perm),
+                  host_pinned(h->tile_perm), host_pinned(h->tile_count)};
+    const uint32_t nchunks = (n + cap - 1) / cap;
+    for (uint32_t k = 0; k < nchunks; ++k) {
+        HostSlot &sl = c->slot[k % kSlots];
+        if (sl.busy) {
+            HIPCHK(c, hipEventSynchronize(sl.done));
+            slot_drain(c, sl, h, pin);
+        }
+        const uint32_t base = k * cap, cn = n - base < cap ? n - base : cap;
+        // gather the first min(len, 128) B of every frame at 64-B aligned
+        // offsets: sizes per part, then parts copy in parallel
+        const uint32_t np = c->pool.size();
+        std::vector<size_t> part_off(np + 1, 0);
+        c->pool.run([&](uint32_t part, uint32_t nparts) {
+            size_t sz = 0;
+            for (uint32_t i = span(cn, part, nparts); i < span(cn, part + 1, nparts); ++i) {
+                const uint32_t L = lens[base + i], cp = L < kHostCap ? L : kHostCap;
+                sz += cp ? (cp + 63) & ~63u : 64;
+            }
+            part_off[part + 1] = sz;
+        });
+        for (uint32_t p = 0; p < np; ++p) part_off[p + 1] += part_off[p];
+        c->pool.run([&](uint32_t part, uint32_t nparts) {
+            size_t off = part_off[part];
+            for (uint32_t i = span(cn, part, nparts); i < span(cn, part + 1, nparts); ++i) {
+                const uint32_t L = lens[base + i], cp = L < kHostCap ? L : kHostCap;
+                const uint8_t *src = frames[base + i];
+                uint8_t *dst = sl.h_arena + off;
+                if (cp >= 64) {
+                    memcpy(dst, src, 64);
+                    if (cp > 64) memcpy(dst + 64, src + 64, cp - 64);
+                } else {
+                    memcpy(dst, src, cp);
+                }
+                sl.h_desc[2 * i] = (uint32_t)off;
+                sl.h_desc[2 * i + 1] = L;
+                off += cp ? (cp + 63) & ~63u : 64;
+            }
+        });
+        hipStream_t s = sl.s;
+        HIPCHK(c, hipMemcpyAsync(sl.d_arena, sl.h_arena, part_off[np], hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(sl.d_desc, sl.h_desc, sizeof(uint32_t) * 2 * cn, hipMemcpyHostToDevice, s));
+        fcgpu_out d;
+        d.verdict = sl.d_v;
+        d.hash = h->hash ? sl.d_h : nullptr;
+        d.anno = h->anno ? sl.d_an : nullptr;
+        d.perm = h->perm ? sl.d_perm : nullptr;
+        d.port_start = nullptr;
+        d.tile_count = h->tile_count ? sl.d_tc : nullptr;
+        d.partition = h->partition;
+        d.reserved = 0;
+        d.tile_perm = h->tile_perm ? sl.d_tp : nullptr;
+        int rc = fcgpu_process(c, sl.d_arena, sl.d_desc, cn, &d, s);
+        if (rc != FCGPU_OK) return rc;
+        const uint32_t tb = base / kTile, nt = (cn + kTile - 1) / kTile;
+        auto d2h = [&](void *user, bool pinned, void *stage, const void *dev, size_t bytes, size_t uoff) {
+            return hipMemcpyAsync(pinned ? (uint8_t *)user + uoff : stage, dev, bytes, hipMemcpyDeviceToHost, s);
+        };
+        if (h->verdict) HIPCHK(c, d2h(h->verdict, pin.v, sl.h_v, sl.d_v, 2ull * cn, 2ull * base));
+        if (h->hash) HIPCHK(c, d2h(h->hash, pin.h, sl.h_h, sl.d_h, 4ull * cn, 4ull * base));
+        if (h->anno) HIPCHK(c, d2h(h->anno, pin.an, sl.h_an, sl.d_an, sizeof(fcgpu_anno) * cn, sizeof(fcgpu_anno) * base));
+        if (h->perm) HIPCHK(c, d2h(h->perm, pin.perm, sl.h_perm, sl.d_perm, 4ull * cn, 4ull * base));
+        if (h->tile_perm) HIPCHK(c, d2h(h->tile_perm, pin.tp, sl.h_tp, sl.d_tp, cn, base));
+        if (h->tile_count)
+            HIPCHK(c, d2h(h->tile_count, pin.tc, sl.h_tc, sl.d_tc, 2ull * nb * nt, 2ull * nb * tb));
+        HIPCHK(c, hipEventRecord(sl.done, s));
+        sl.busy = true;
+        sl.base = base;
+        sl.n = cn;
+    }
+    for (uint32_t k = nchunks > kSlots ? nchunks - kSlots : 0; k < nchunks; ++k) {
+        HostSlot &sl = c->slot[k % kSlots];
+        if (!sl.busy) continue;
+        HIPCHK(c, hipEventSynchronize(sl.done));
+        slot_drain(c, sl, h, pin);
+    }
+    return FCGPU_OK;
+}
+
 int fcgpu_process_host(fcgpu_ctx *c, const uint8_t *const *frames, const uint32_t *lens, uint32_t n,
                        const fcgpu_out *h) {
     if (!c || !h || (n && (!frames || !lens))) return FCGPU_EINVAL;
     if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "batch larger than max_batch");
     if (n == 0) return FCGPU_OK;
+    if (h->partition > FCGPU_PART_TILE) return fail(c, FCGPU_EINVAL, "bad partition mode");
     HIPCHK(c, hipSetDevice(c->device));
-    const size_t arena_cap = (size_t)c->max_batch * kHostCap + kArenaPad;
-    if (!c->h_arena) {
-        // the context's own stream exists only for the host-resident path (a
-        // stream per context maps onto one of the few hardware queues)
-        HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        HIPCHK(c, hipHostMalloc((void **)&c->h_arena, arena_cap, hipHostMallocDefault));
-        HIPCHK(c, hipHostMalloc((void **)&c->h_desc, sizeof(uint32_t) * 2 * c->max_batch, hipHostMallocDefault));
-        HIPCHK(c, hipMalloc(&c->d_arena, arena_cap));
-        HIPCHK(c, hipMemset(c->d_arena, 0, arena_cap));
-        HIPCHK(c, hipMalloc(&c->d_desc, sizeof(uint32_t) * 2 * c->max_batch));
-        HIPCHK(c, hipMalloc(&c->d_hv, sizeof(uint16_t) * c->max_batch));
-        HIPCHK(c, hipMalloc(&c->d_hh, sizeof(uint32_t) * c->max_batch));
-        HIPCHK(c, hipMalloc(&c->d_hperm, sizeof(uint32_t) * c->max_batch));
-        HIPCHK(c, hipMalloc(&c->d_hstart, sizeof(uint32_t) * (FCGPU_MAX_PORTS + 2)));
-        HIPCHK(c, hipMalloc(&c->d_hanno, sizeof(fcgpu_anno) * c->max_batch));
-        HIPCHK(c, hipMalloc(&c->d_htc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * c->max_tiles));
-        HIPCHK(c, hipMalloc(&c->d_htp, (size_t)c->max_batch + kTile));
-    }
-    // gather: first min(len, 128) bytes of each frame at 64-B aligned offsets.
-    // The device sees the real frame length; bytes past the capture are never
-    // needed for a verdict with headers <= 128 B.
-    size_t off = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t cap = lens[i] < kHostCap ? lens[i] : kHostCap;
-        memcpy(c->h_arena + off, frames[i], cap);
-        c->h_desc[2 * i] = (uint32_t)off;
-        c->h_desc[2 * i + 1] = lens[i];
-        off += (cap + 63) & ~(size_t)63;
-        if (cap == 0) off += 64;
-    }
-    hipStream_t s = c->stream;
-    HIPCHK(c, hipMemcpyAsync(c->d_arena, c->h_arena, off, hipMemcpyHostToDevice, s));
-    HIPCHK(c, hipMemcpyAsync(c->d_desc, c->h_desc, sizeof(uint32_t) * 2 * n, hipMemcpyHostToDevice, s));
-    fcgpu_out d;
-    d.verdict = c->d_hv;
-    d.hash = h->hash ? c->d_hh : nullptr;
-    d.anno = h->anno ? c->d_hanno : nullptr;
-    d.perm = h->perm ? c->d_hperm : nullptr;
-    d.port_start = h->port_start ? c->d_hstart : nullptr;
-    d.tile_count = h->tile_count ? c->d_htc : nullptr;
-    d.partition = h->partition;
-    d.reserved = 0;
-    d.tile_perm = h->tile_perm ? c->d_htp : nullptr;
-    int rc = fcgpu_process(c, c->d_arena, c->d_desc, n, &d, s);
-    if (rc != FCGPU_OK) return rc;
-    if (h->verdict) HIPCHK(c, hipMemcpyAsync(h->verdict, d.verdict, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, s));
-    if (h->hash) HIPCHK(c, hipMemcpyAsync(h->hash, d.hash, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
-    if (h->anno) HIPCHK(c, hipMemcpyAsync(h->anno, d.anno, sizeof(fcgpu_anno) * n, hipMemcpyDeviceToHost, s));
-    if (h->perm) HIPCHK(c, hipMemcpyAsync(h->perm, d.perm, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
-    if (h->tile_perm) HIPCHK(c, hipMemcpyAsync(h->tile_perm, d.tile_perm, n, hipMemcpyDeviceToHost, s));
-    if (h->tile_count)
-        HIPCHK(c, hipMemcpyAsync(h->tile_count, d.tile_count,
-                                 sizeof(uint16_t) * (c->cfg.nports + 1) * ((n + kTile - 1) / kTile),
-                                 hipMemcpyDeviceToHost, s));
-    if (h->port_start)
-        HIPCHK(c, hipMemcpyAsync(h->port_start, d.port_start, sizeof(uint32_t) * (c->cfg.nports + 2),
-                                 hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
+    if (h->partition == FCGPU_PART_GLOBAL && (h->perm || h->port_start))
+        return process_host_whole(c, frames, lens, n, h);
+    if (h->partition == FCGPU_PART_TILE && ((h->perm || h->tile_perm) != (h->tile_count != nullptr)))
+        return fail(c, FCGPU_EINVAL, "FCGPU_PART_TILE needs tile_count and perm and/or tile_perm");
+    return process_host_pipelined(c, frames, lens, n, h);
+}
+
+int fcgpu_set_host_threads(fcgpu_ctx *c, uint32_t nthreads) {
+    if (!c || nthreads == 0 || nthreads > 64) return FCGPU_EINVAL;
+    c->pool.resize(nthreads);
     return FCGPU_OK;
+}
+
+void *fcgpu_host_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void fcgpu_host_free(void *p) {
+    if (p) hipHostFree(p);
 }
 
 int fcgpu_read_counters(fcgpu_ctx *c, uint64_t *out, int n) {

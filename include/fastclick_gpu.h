@@ -42,13 +42,14 @@
 #ifndef FASTCLICK_GPU_H
 #define FASTCLICK_GPU_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 4
+#define FCGPU_ABI_VERSION 5
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -192,7 +193,13 @@ int  fcgpu_process(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_des
 /* Host-resident batch: frames[i] points at packet i's data (length lens[i]).
  * The first min(len, 128) bytes of every frame are gathered into pinned
  * staging, copied H2D, processed, and the requested outputs copied D2H into the
- * host pointers of h_out. Synchronous. */
+ * host pointers of h_out. Synchronous. Unless a whole-batch partition is asked
+ * for (FCGPU_PART_GLOBAL with perm/port_start), the batch is pipelined in
+ * chunks of 65,536 packets over three streams, so the gather of one chunk
+ * overlaps the copies and kernel of the previous ones; results are identical
+ * to one launch over the batch (chunks are whole 256-packet tiles). Outputs
+ * are DMA'd straight into h_out arrays that are pinned (fcgpu_host_alloc),
+ * otherwise through pinned staging. */
 int  fcgpu_process_host(fcgpu_ctx *ctx, const uint8_t *const *frames,
                         const uint32_t *lens, uint32_t n, const fcgpu_out *h_out);
 
@@ -227,6 +234,13 @@ typedef struct fcgpu_step {
  * program is empty and every packet goes to that output ("all->[N]"). */
 int  fcgpu_set_program(fcgpu_ctx *ctx, uint32_t kind, const fcgpu_step *steps, uint32_t nsteps,
                        int32_t output_everything);
+
+/* Host threads the context may use for the gather / copy-out loops of
+ * fcgpu_process_host (the caller's thread included; default 1). */
+int  fcgpu_set_host_threads(fcgpu_ctx *ctx, uint32_t nthreads);
+/* Pinned host memory for fcgpu_process_host outputs (NULL on failure). */
+void *fcgpu_host_alloc(size_t bytes);
+void fcgpu_host_free(void *p);
 
 int  fcgpu_read_counters(fcgpu_ctx *ctx, uint64_t *out, int n);
 int  fcgpu_reset_counters(fcgpu_ctx *ctx);

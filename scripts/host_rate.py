@@ -21,16 +21,30 @@ import torch  # noqa: E402,F401
 from fastclick_amd import synth, click as K, _native as N  # noqa: E402
 
 
-def raw_host(n):
+def raw_host(n, threads=1, tile=False, pinned=False):
     b = synth.c2(n)
     cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16)
     ctx = N.Context(0, n, cfg)
+    ctx.set_host_threads(threads)
     base = b.arena.ctypes.data
     ptrs = (C.c_void_p * n)(*[base + int(o) for o in b.desc[:, 0]])
     lens = np.ascontiguousarray(b.desc[:, 1], dtype=np.uint32)
-    v = np.zeros(n, np.uint16); h = np.zeros(n, np.uint32); p = np.zeros(n, np.uint32)
-    st = np.zeros(18, np.uint32)
-    kw = dict(verdict=v.ctypes.data, hash=h.ctypes.data, perm=p.ctypes.data, port_start=st.ctypes.data)
+    lib = N.load()
+
+    def arr(count, dtype):
+        dtype = np.dtype(dtype)
+        if not pinned:
+            return np.zeros(count, dtype)
+        p = lib.fcgpu_host_alloc(count * dtype.itemsize)
+        return np.ctypeslib.as_array((C.c_uint8 * (count * dtype.itemsize)).from_address(p)).view(dtype)
+    v = arr(n, np.uint16); h = arr(n, np.uint32)
+    if tile:
+        tp = arr(n, np.uint8); tc = arr(((n + 255) // 256) * 17, np.uint16)
+        kw = dict(verdict=v.ctypes.data, hash=h.ctypes.data, tile_perm=tp.ctypes.data,
+                  tile_count=tc.ctypes.data, partition=N.PART_TILE)
+    else:
+        p = np.zeros(n, np.uint32); st = np.zeros(18, np.uint32)
+        kw = dict(verdict=v.ctypes.data, hash=h.ctypes.data, perm=p.ctypes.data, port_start=st.ctypes.data)
     ctx.process_host(ptrs, lens.ctypes.data, n, **kw)
     reps = 10
     t0 = time.perf_counter()
@@ -41,8 +55,39 @@ def raw_host(n):
     return n * reps / dt / 1e6
 
 
+def h2d_gbs(nbytes=72 << 20, reps=20):
+    """Pinned host -> device copy rate on this box (the PCIe bound of the path)."""
+    src = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    dst = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    return nbytes * reps / (time.perf_counter() - t0) / 1e9
+
+
+def gather_only_mpps(n=1 << 20, reps=10):
+    """The host gather alone (numpy fancy-index copy of 64-B windows), for scale."""
+    b = synth.c2(n)
+    idx = (b.desc[:, 0].astype(np.int64)[:, None] + np.arange(64)[None, :])
+    out = np.empty((n, 64), np.uint8)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        np.take(b.arena, idx, out=out)
+    return n * reps / (time.perf_counter() - t0) / 1e6
+
+
 def main():
-    out = {"process_host_mpps_1M": round(raw_host(1 << 20), 2)}
+    out = {"h2d_pinned_gbs": round(h2d_gbs(), 2)}
+    out["process_host_mpps_1M_global"] = round(raw_host(1 << 20), 2)
+    chunk = os.environ.get("FCGPU_HOST_CHUNK", "65536")
+    out["chunk"] = int(chunk)
+    for threads in (1, 4, 8):
+        out[f"process_host_mpps_1M_tile_t{threads}"] = round(raw_host(1 << 20, threads, tile=True), 2)
+        out[f"process_host_mpps_1M_tile_t{threads}_pinned"] = round(
+            raw_host(1 << 20, threads, tile=True, pinned=True), 2)
     b = synth.c2(1 << 20)
     for batch in (4096, 65536, 262144):
         conf = f"GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BATCH {batch})"

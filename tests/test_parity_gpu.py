@@ -207,6 +207,52 @@ def test_counters_accumulate_and_host_path(dev, oracle):
     ctx.close()
 
 
+@pytest.mark.parametrize("threads,pinned", [(1, False), (4, False), (3, True)])
+def test_host_pipeline_chunks(dev, oracle, threads, pinned):
+    """fcgpu_process_host over > 3 pipeline chunks (65,536 packets each, three
+    streams): tile outputs, global-index perm, annotations and counters equal
+    one oracle pass over the whole batch, for pageable and pinned outputs."""
+    import ctypes as C
+    n = 3 * 65536 + 4 * 65536 // 3 + 77      # 5 chunks, ragged last chunk and tile
+    b = synth.c3(n, seed=97)
+    synth.inject_errors(b, 0.02, seed=98)
+    synth.add_ip_options(b, 0.05, seed=99)
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16, badsrc=BADSRC)
+    exp = oracle.process_batch(cfg, b)
+    ctx = N.Context(0, n, cfg)
+    ctx.set_host_threads(threads)
+    base = b.arena.ctypes.data
+    ptrs = (C.c_void_p * n)(*[base + int(o) for o in b.desc[:, 0]])
+    lens = np.ascontiguousarray(b.desc[:, 1], dtype=np.uint32)
+    ntiles = (n + 255) // 256
+    keep = []
+
+    def arr(count, dtype):
+        dtype = np.dtype(dtype)
+        if not pinned:
+            return np.zeros(count, dtype)
+        p = ctx.lib.fcgpu_host_alloc(count * dtype.itemsize)
+        assert p
+        keep.append(p)
+        a = np.ctypeslib.as_array((C.c_uint8 * (count * dtype.itemsize)).from_address(p)).view(dtype)
+        a[:] = 0
+        return a
+    verdict, hsh, anno = arr(n, np.uint16), arr(n, np.uint32), arr(n, N.anno_dtype())
+    perm, tperm, tc = arr(n, np.uint32), arr(n, np.uint8), arr(ntiles * 17, np.uint16)
+    for rep in range(2):
+        ctx.process_host(ptrs, lens.ctypes.data, n, verdict=verdict.ctypes.data, hash=hsh.ctypes.data,
+                         anno=anno.ctypes.data, perm=perm.ctypes.data, tile_perm=tperm.ctypes.data,
+                         tile_count=tc.ctypes.data, partition=N.PART_TILE)
+        got = dict(reason=(verdict & 0xFF).astype(np.uint8), port=(verdict >> 8).astype(np.uint8),
+                   hash=hsh.copy(), anno=anno.copy(), perm_tile=perm.copy(), tile_count=tc.copy(),
+                   tile_perm=tperm.copy())
+        compare(got, exp, ctx=f"host pipeline threads={threads} pinned={pinned} rep={rep}")
+    assert np.array_equal(np.array(ctx.counters(), np.uint64), 2 * exp["counters"])
+    ctx.close()
+    for p in keep:
+        N.load().fcgpu_host_free(p)
+
+
 def test_large_batch_properties(dev, oracle):
     """4M packets: full oracle comparison of hash/port plus partition
     properties (sorted runs, permutation, counts)."""
