@@ -55,6 +55,7 @@ class fcgpu_cfg(C.Structure):
         ("gooddst", C.c_uint32 * MAX_ADDRS),
         ("nbad6", C.c_uint32),
         ("bad6", (C.c_uint8 * 16) * MAX_ADDRS),
+        ("process_eh", C.c_uint32),
     ]
 
 
@@ -62,12 +63,12 @@ class fcgpu_anno(C.Structure):
     _fields_ = [
         ("dst_ip", C.c_uint32),
         ("length", C.c_uint16),
-        ("nh", C.c_uint8),
-        ("th", C.c_uint8),
         ("vlan_tci", C.c_uint16),
+        ("nh", C.c_uint16),
+        ("th", C.c_uint16),
         ("ip6_nxt", C.c_uint8),
         ("ipver", C.c_uint8),
-        ("reserved", C.c_uint32),
+        ("reserved", C.c_uint16),
     ]
 
 
@@ -78,9 +79,9 @@ def anno_dtype():
     global ANNO_DTYPE
     if ANNO_DTYPE is None:
         import numpy as np
-        ANNO_DTYPE = np.dtype([("dst_ip", "<u4"), ("length", "<u2"), ("nh", "u1"), ("th", "u1"),
-                               ("vlan_tci", "<u2"), ("ip6_nxt", "u1"), ("ipver", "u1"),
-                               ("reserved", "<u4")])
+        ANNO_DTYPE = np.dtype([("dst_ip", "<u4"), ("length", "<u2"), ("vlan_tci", "<u2"),
+                               ("nh", "<u2"), ("th", "<u2"), ("ip6_nxt", "u1"), ("ipver", "u1"),
+                               ("reserved", "<u2")])
         assert ANNO_DTYPE.itemsize == C.sizeof(fcgpu_anno) == 16
     return ANNO_DTYPE
 
@@ -189,7 +190,7 @@ def default_cfg() -> fcgpu_cfg:
 
 def make_cfg(*, check_mode=CHECK_IP4, offset=0, checksum=False, hash_mode=HASH_FLOWID,
              classify=CLS_NONE, nports=1, hs_offset=0, hs_length=1, native_vlan=0,
-             badsrc=(), gooddst=(), bad6=None) -> fcgpu_cfg:
+             badsrc=(), gooddst=(), bad6=None, process_eh=False) -> fcgpu_cfg:
     """Build an fcgpu_cfg. Addresses are raw network-order words (bytes a.b.c.d
     -> little-endian u32 of those bytes), as IPAddress stores them."""
     cfg = default_cfg()
@@ -208,6 +209,7 @@ def make_cfg(*, check_mode=CHECK_IP4, offset=0, checksum=False, hash_mode=HASH_F
     cfg.ngooddst = len(gooddst)
     for j, a in enumerate(gooddst):
         cfg.gooddst[j] = a
+    cfg.process_eh = 1 if process_eh else 0
     if bad6 is not None:
         cfg.nbad6 = len(bad6)
         for j, a in enumerate(bad6):

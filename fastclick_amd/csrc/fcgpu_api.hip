@@ -41,7 +41,7 @@ struct EvPair {
     int stage;
 };
 
-constexpr uint32_t kChunk = 65536;          // packets per host-pipeline chunk (whole tiles)
+constexpr uint32_t kChunk = 131072;         // packets per host-pipeline chunk (whole tiles)
 constexpr int kSlots = 3;                   // chunks in flight: gather / copy+kernel / drain
 
 // Host worker pool for the gather and copy-out loops (fcgpu_set_host_threads).
@@ -428,6 +428,7 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     d.nbadsrc = cfg->nbadsrc;
     d.ngooddst = cfg->ngooddst;
     d.nbad6 = cfg->nbad6;
+    d.process_eh = cfg->process_eh ? 1u : 0u;
     memcpy(d.badsrc, cfg->badsrc, sizeof(d.badsrc));
     memcpy(d.gooddst, cfg->gooddst, sizeof(d.gooddst));
     memcpy(d.bad6, cfg->bad6, sizeof(d.bad6));

@@ -39,6 +39,7 @@ struct DevCfg {
     uint32_t badsrc[FCGPU_MAX_ADDRS];
     uint32_t gooddst[FCGPU_MAX_ADDRS];
     uint32_t bad6[FCGPU_MAX_ADDRS][4];
+    uint32_t process_eh;
     const uint4 *prog;        // decision program (FCGPU_CLS_PROGRAM), 16 B per step
     uint32_t prog_n;
     uint32_t prog_kind;
@@ -233,8 +234,8 @@ __device__ __forceinline__ uint32_t check_ip4(const DevCfg &c, const FrameView &
         for (uint32_t j = 0; j < c.ngooddst; ++j) good |= (c.gooddst[j] == h[4]);
         if (bad && !good) return FCGPU_R_BAD_SADDR;
     }
-    an.nh = (uint8_t)o;
-    an.th = (uint8_t)(o + hlen);
+    an.nh = (uint16_t)o;
+    an.th = (uint16_t)(o + hlen);
     an.length = (uint16_t)(plen > L ? len - (plen - L) : len);
     an.dst_ip = h[4];
     return FCGPU_R_OK;
@@ -259,10 +260,28 @@ __device__ __forceinline__ uint32_t check_ip6(const DevCfg &c, const FrameView &
                 s[3] == c.bad6[j][3])
                 return FCGPU_R_BAD_IP6;
     }
-    an.nh = (uint8_t)o;
-    an.th = (uint8_t)(o + 40);
-    an.ip6_nxt = (uint8_t)((h[1] >> 16) & 0xff);
-    an.length = (uint16_t)(pl6 < plen - 40 ? len - (plen - 40 - pl6) : len);
+    uint32_t nxt = (h[1] >> 16) & 0xff, tot = 40;
+    if (c.process_eh) {
+        // ip6_follow_eh (include/click/ip6address.hh:417-448) from the first
+        // extension header to the end of the (untrimmed) packet: the last
+        // header visited gives IP6_NXT and the transport header offset
+        uint32_t eh = 40, t = nxt;
+        while (eh < plen) {
+            nxt = t;
+            tot = eh;
+            const uint32_t w = f.rd32(o + eh);          // eh->nxt, eh->len
+            const uint32_t en = w & 0xff, el = (w >> 8) & 0xff;
+            if (t == 0 || t == 43) eh += el * 8 + 8;            // hop-by-hop, routing
+            else if (t == 51) eh += ((el + 2) * 4 + 7) & ~7u;   // AH: round_up((len+2)*4, 8)
+            else if (t == 44) eh += 8;                          // fragment
+            else break;                                         // no next header / upper layer
+            t = en;
+        }
+    }
+    an.nh = (uint16_t)o;
+    an.th = (uint16_t)(o + tot);
+    an.ip6_nxt = (uint8_t)nxt;
+    an.length = (uint16_t)(pl6 < plen - tot ? len - (plen - tot - pl6) : len);
     return FCGPU_R_OK;
 }
 
@@ -288,14 +307,14 @@ __device__ __forceinline__ void process_packet(const DevCfg &c, const FrameView 
             r.port = c.nports;
             return;
         }
-        an.nh = (uint8_t)o;                       // the pull() StripEtherVLANHeader did
+        an.nh = (uint16_t)o;                       // the pull() StripEtherVLANHeader did
         v6 = ((int)(len - o) >= 1) && ((f.rd8(o) >> 4) == 6);
         r.reason = v6 ? check_ip6(c, f, len, o, an) : check_ip4<CK>(c, f, len, o, h, an);
     } else if (CM == FCGPU_MARK_IP4) {
         // MarkIPHeader::simple_action (markipheader.cc:43-48)
         f.run<5>(o, h);
-        an.nh = (uint8_t)o;
-        an.th = (uint8_t)(o + ((h[0] & 15) << 2));
+        an.nh = (uint16_t)o;
+        an.th = (uint16_t)(o + ((h[0] & 15) << 2));
         an.length = (uint16_t)len;
         an.ipver = 4;
         r.reason = FCGPU_R_OK;
@@ -408,8 +427,8 @@ __device__ __forceinline__ bool ip4_fast(const DevCfg &c, const FrameView &f, ui
     r.hash = ok ? hv : 0u;
     fcgpu_anno &an = r.an;
     an.ipver = early == FCGPU_R_MINISCULE ? 0 : 4;
-    an.nh = (uint8_t)(ok ? o : 0u);
-    an.th = (uint8_t)(ok ? o + 20 : 0u);
+    an.nh = (uint16_t)(ok ? o : 0u);
+    an.th = (uint16_t)(ok ? o + 20 : 0u);
     an.length = (uint16_t)(ok ? (plen > L ? len - (plen - L) : len) : 0u);
     an.dst_ip = ok ? h[4] : 0u;
     if (PROG && ok) {                                  // FCGPU_CLS_PROGRAM

@@ -32,6 +32,7 @@ class Sink : public Element {
                 if (_r->out_dst) _r->out_dst[i] = p->anno_u32(DST_IP_ANNO_OFFSET);
                 if (_r->out_len) _r->out_len[i] = p->length();
                 if (_r->out_nh) _r->out_nh[i] = p->network_header_offset();
+                if (_r->out_paint) _r->out_paint[i] = p->anno_u8(PAINT_ANNO_OFFSET);
             }
             ++*_seq;
             ++cnt;

@@ -13,7 +13,7 @@
 //   OFFSET, CHECKSUM (default FALSE: checkipheader.cc:110), BADSRC, GOODDST,
 //   VERBOSE, DETAILS                         -- CheckIPHeader
 //   NATIVE_VLAN (default 0)                  -- StripEtherVLANHeader
-//   BADADDRS                                 -- CheckIP6Header (IPv6, MODE AUTO)
+//   BADADDRS, PROCESS_EH                     -- CheckIP6Header (IPv6, MODE AUTO)
 //   N / LB_MODE hash|hash_agg|hash_ip        -- FlowSwitch / LoadBalancer
 //   HASHSWITCH "OFFSET LENGTH"               -- HashSwitch
 //   PROGRAM "<program text>", PROGRAM_KIND IPFILTER|CLASSIFIER
@@ -22,6 +22,8 @@
 //     (lines separated by newlines or '|', program_text.hh); N is the
 //     classifier's output count. Packets no rule matches are killed, as
 //     CLASSIFY_EACH_PACKET kills a packet whose port is out of range.
+//   COLOR (PAINT annotation on every packet)  -- IPInputCombo (with OFFSET 14,
+//     CHECKSUM true, STRIP true and no invalid output: ipinputcombo.cc:65-141)
 //   MODE CHECK|MARK|AUTO, HASH NONE|FLOWID|FLOW5ID, STRIP, BATCH, DEVICE,
 //   PARTITION TILE (default: each 256-packet tile classified as one batch, one
 //   fused launch) | GLOBAL (the whole staged batch as one, three launches)
@@ -36,6 +38,8 @@
 #include <string>
 #include <sstream>
 #include <inttypes.h>
+#include <arpa/inet.h>
+#include <string.h>
 
 #include "click_model.hh"
 #include "program_text.hh"
@@ -102,6 +106,9 @@ class GPUIPCheckClassify : public Element {
                 _cfg.classify = FCGPU_CLS_HASHSWITCH;
                 _cfg.hs_offset = (int32_t)o;
                 _cfg.hs_length = (int32_t)l;
+            } else if (k == "COLOR") {
+                if (!parse_int(v, n) || n < 0 || n > 255) return err(errh, "COLOR expects an integer in [0,255]");
+                _color = (int)n;
             } else if (k == "PROGRAM") {
                 std::string text = v;
                 if (text.size() >= 2 && text.front() == '"' && text.back() == '"') text = text.substr(1, text.size() - 2);
@@ -136,7 +143,22 @@ class GPUIPCheckClassify : public Element {
                 else if (v == "GLOBAL") _partition = FCGPU_PART_GLOBAL;
                 else return err(errh, "PARTITION expects TILE or GLOBAL");
             } else if (k == "BADADDRS") {
-                return err(errh, "BADADDRS: only the default IPv6 bad source (ff..ff) is supported");
+                // CheckIP6Header::configure (checkip6header.cc:47-87): the list
+                // adds to the default ff..ff, duplicates dropped
+                std::istringstream ss(v);
+                std::string w;
+                while (ss >> w) {
+                    uint8_t a[16];
+                    if (inet_pton(AF_INET6, w.c_str(), a) != 1) return err(errh, "BADADDRS expects IPv6 addresses");
+                    bool dup = false;
+                    for (uint32_t j = 0; j < _cfg.nbad6; ++j) dup |= memcmp(_cfg.bad6[j], a, 16) == 0;
+                    if (dup) continue;
+                    if (_cfg.nbad6 >= FCGPU_MAX_ADDRS) return err(errh, "BADADDRS: too many addresses");
+                    memcpy(_cfg.bad6[_cfg.nbad6++], a, 16);
+                }
+            } else if (k == "PROCESS_EH") {
+                if (!parse_bool(v, b)) return err(errh, "PROCESS_EH expects true/false");
+                _cfg.process_eh = b;
             } else if (k.empty()) {
                 return err(errh, "too many arguments");        // Args::complete(): OFFSET is keyword-only
             } else {
@@ -253,6 +275,7 @@ class GPUIPCheckClassify : public Element {
             Packet *p = _pkts[i];
             const fcgpu_anno &a = _anno[i];
             const uint32_t reason = _verdict[i] & 0xff;
+            if (_color >= 0) p->set_anno_u8(PAINT_ANNO_OFFSET, (uint8_t)_color);   // SET_PAINT_ANNO
             if (autom && reason != FCGPU_R_VLAN_REJECT)
                 p->set_anno_u16(VLAN_TCI_ANNO_OFFSET, a.vlan_tci);    // StripEtherVLANHeader
             if (reason == FCGPU_R_OK || reason == FCGPU_R_NO_MATCH) {
@@ -340,6 +363,7 @@ class GPUIPCheckClassify : public Element {
     static constexpr uint32_t kMaxBatch = 8192;
     ParsedProgram _prog;
     uint32_t _prog_kind = FCGPU_PROG_IPFILTER;
+    int _color = -1;
     std::vector<uint32_t> _keep;
     fcgpu_cfg _cfg;
     fcgpu_ctx *_ctx = nullptr;

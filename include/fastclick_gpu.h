@@ -112,6 +112,9 @@ typedef struct fcgpu_cfg {
     uint32_t gooddst[FCGPU_MAX_ADDRS];
     uint32_t nbad6;           /* CheckIP6Header bad source list; default = {ff..ff}      */
     uint8_t  bad6[FCGPU_MAX_ADDRS][16];
+    uint32_t process_eh;      /* CheckIP6Header PROCESS_EH: follow hop-by-hop, routing,
+                                 fragment and AH extension headers (ip6_follow_eh,
+                                 include/click/ip6address.hh:417-448)                    */
 } fcgpu_cfg;
 
 /* Optional per-packet annotations (16 B), mirroring what the reference
@@ -120,12 +123,13 @@ typedef struct fcgpu_cfg {
 typedef struct fcgpu_anno {
     uint32_t dst_ip;          /* DST_IP_ANNO (IPv4 valid) = raw ip_dst word             */
     uint16_t length;          /* packet length after Packet::take() trimming            */
-    uint8_t  nh;              /* network header offset (set_ip_header / set_ip6_header) */
-    uint8_t  th;              /* transport header offset                                 */
     uint16_t vlan_tci;        /* VLAN_TCI_ANNO, raw network order (CHECK_AUTO)          */
+    uint16_t nh;              /* network header offset (set_ip_header / set_ip6_header) */
+    uint16_t th;              /* transport header offset (IPv6: after the extension
+                                 headers when process_eh)                              */
     uint8_t  ip6_nxt;         /* IP6_NXT_ANNO (IPv6 valid)                              */
     uint8_t  ipver;           /* 4 or 6 for packets that reached a checker, else 0      */
-    uint32_t reserved;
+    uint16_t reserved;
 } fcgpu_anno;
 
 /* Stable per-output partition (CLASSIFY_EACH_PACKET, packetbatch.hh:259-307),
@@ -195,7 +199,7 @@ int  fcgpu_process(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_des
  * staging, copied H2D, processed, and the requested outputs copied D2H into the
  * host pointers of h_out. Synchronous. Unless a whole-batch partition is asked
  * for (FCGPU_PART_GLOBAL with perm/port_start), the batch is pipelined in
- * chunks of 65,536 packets over three streams, so the gather of one chunk
+ * chunks of 131,072 packets over three streams, so the gather of one chunk
  * overlaps the copies and kernel of the previous ones; results are identical
  * to one launch over the batch (chunks are whole 256-packet tiles). Outputs
  * are DMA'd straight into h_out arrays that are pinned (fcgpu_host_alloc),

@@ -43,6 +43,7 @@ typedef struct fcclick_result {
     uint32_t *out_batches;  /* [1] number of PacketBatches the sinks received             */
     char     *handlers;     /* "name=value\n" for count, drops, drop_details, port_counts */
     size_t    handlers_cap;
+    uint8_t  *out_paint;    /* [n] PAINT_ANNO (anno u8 @17) on departure (may be NULL)     */
 } fcclick_result;
 
 /* Run a graph  Source(frames, BURST) -> conf => [0 .. nsinks-1] Sink  over n

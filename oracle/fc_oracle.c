@@ -167,14 +167,17 @@ static int check_ip4(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, uint32_
     uint32_t src = le32(ip + 12), dst = le32(ip + 16);
     if (in_list(c->badsrc, c->nbadsrc, src) && !in_list(c->gooddst, c->ngooddst, dst))
         return FCGPU_R_BAD_SADDR;
-    a->nh = (uint8_t)o;
-    a->th = (uint8_t)(o + hlen);
+    a->nh = (uint16_t)o;
+    a->th = (uint16_t)(o + hlen);
     a->length = (uint16_t)(plen > L ? len - (plen - L) : len);
     a->dst_ip = dst;
     return FCGPU_R_OK;
 }
 
-/* elements/ip6/checkip6header.cc:105-168 (PROCESS_EH false). */
+/* elements/ip6/checkip6header.cc:105-168; PROCESS_EH walks the extension
+ * headers like ip6_follow_eh (include/click/ip6address.hh:417-448) up to the
+ * untrimmed packet end: the last header visited gives IP6_NXT and the
+ * transport header. */
 static int check_ip6(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, uint32_t o,
                      fcgpu_anno *a)
 {
@@ -191,10 +194,28 @@ static int check_ip6(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, uint32_
     for (uint32_t i = 0; i < c->nbad6; i++)
         if (memcmp(ip + 8, c->bad6[i], 16) == 0)
             return FCGPU_R_BAD_IP6;
-    a->nh = (uint8_t)o;
-    a->th = (uint8_t)(o + 40);
-    a->ip6_nxt = ip[6];
-    a->length = (uint16_t)(pl6 < plen - 40 ? len - (plen - 40 - pl6) : len);
+    unsigned nxt = ip[6], tot = 40;
+    if (c->process_eh) {
+        unsigned eh = 40, t = nxt;
+        while (eh < plen) {
+            nxt = t;
+            tot = eh;
+            const unsigned en = ip[eh], el = ip[eh + 1];   /* eh->nxt, eh->len */
+            if (t == 0 || t == 43)
+                eh += el * 8 + 8;                  /* IP6_EH_HOPBYHOP, IP6_EH_ROUTING */
+            else if (t == 51)
+                eh += ((el + 2) * 4 + 7) / 8 * 8;  /* IP6_EH_AH: round_up((len+2)*4, 8) */
+            else if (t == 44)
+                eh += 8;                           /* IP6_EH_FRAGMENT */
+            else
+                break;
+            t = en;
+        }
+    }
+    a->nh = (uint16_t)o;
+    a->th = (uint16_t)(o + tot);
+    a->ip6_nxt = (uint8_t)nxt;
+    a->length = (uint16_t)(pl6 < plen - tot ? len - (plen - tot - pl6) : len);
     return FCGPU_R_OK;
 }
 
@@ -286,14 +307,14 @@ void fco_process_packet(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, fco_
             r->port = (uint8_t)c->nports;
             return;
         }
-        a->nh = (uint8_t)o;   /* the pull() StripEtherVLANHeader did */
+        a->nh = (uint16_t)o;   /* the pull() StripEtherVLANHeader did */
         /* version dispatch as Classifier(0/60%f0, -): needs one byte */
         v6 = ((int)(len - o) >= 1) && ((f[o] >> 4) == 6);
         reason = v6 ? check_ip6(c, f, len, o, a) : check_ip4(c, f, len, o, a);
     } else if (c->check_mode == FCGPU_MARK_IP4) {
         /* elements/ip/markipheader.cc:43-48 */
-        a->nh = (uint8_t)o;
-        a->th = (uint8_t)(o + ((f[o] & 15) << 2));
+        a->nh = (uint16_t)o;
+        a->th = (uint16_t)(o + ((f[o] & 15) << 2));
         a->length = (uint16_t)len;
         a->ipver = 4;
         reason = FCGPU_R_OK;

@@ -537,6 +537,119 @@ def run_reftests(b, tmp):
     return out
 
 
+def run_combo(tmp):
+    """IPInputCombo(COLOR 7, BADSRC .., GOODDST ..) on the ip4 set: which
+    packets survive (it kills the rest) with their length, paint and dst anno
+    (ipinputcombo.cc:65-141)."""
+    g = np.load(os.path.join(HERE, "ip4.npz"))
+    b = synth.Batch(arena=g["arena"], desc=g["desc"])
+    pcap = os.path.join(tmp, "combo.pcap")
+    write_pcap(pcap, b.frames())
+    click(CLICK, f"FromDump(combo.pcap, STOP true, TIMING false) -> IPInputCombo(7, BADSRC {BADSRC}, "
+                 f"GOODDST {GOODDST}) -> ToIPSummaryDump(combo.ipsum, FIELDS timestamp ip_len ip_dst)"
+                 " -> Discard;", tmp)
+    rows = read_ipsum(os.path.join(tmp, "combo.ipsum"), 2)
+    n = b.n
+    valid = np.zeros(n, np.uint8)
+    iplen = np.zeros(n, np.uint16)
+    for i, r in rows.items():
+        valid[i] = 1
+        iplen[i] = int(r[0])
+    return dict(valid=valid, ip_len=iplen)
+
+
+BAD6_EXTRA = "2001:db8::bad"
+
+
+def make_eh_set(n=1200, seed=2027):
+    """Untagged IPv6 frames with chains of 0-3 extension headers (hop-by-hop,
+    routing, fragment, AH, destination options, no-next-header), UDP/TCP after
+    them; payload lengths exact, short (take) or too long (bad); frames cut
+    inside the chain; bad sources (ff..ff and BADSRC6)."""
+    import ipaddress
+    rng = np.random.default_rng(seed)
+    frames = []
+    bad_extra = ipaddress.IPv6Address(BAD6_EXTRA).packed
+    for i in range(n):
+        chain = b""
+        k = int(rng.integers(0, 4))
+        types = [int(rng.choice([0, 43, 44, 51, 60, 59])) for _ in range(k)]
+        last = int(rng.choice([17, 6]))
+        nxts = types + [last]
+        for j, t in enumerate(types):
+            nx = nxts[j + 1]
+            if t in (0, 43, 60):
+                ln = int(rng.integers(0, 3))
+                body = bytes([nx, ln]) + bytes(rng.integers(0, 256, ln * 8 + 6, dtype=np.uint8))
+            elif t == 51:
+                ln = int(rng.integers(1, 7))
+                size = ((ln + 2) * 4 + 7) // 8 * 8
+                body = bytes([nx, ln]) + bytes(rng.integers(0, 256, size - 2, dtype=np.uint8))
+            elif t == 44:
+                body = bytes([nx, 0]) + bytes(rng.integers(0, 256, 6, dtype=np.uint8))
+            else:   # 59: no next header; whatever follows is payload
+                body = bytes(rng.integers(0, 256, 8, dtype=np.uint8))
+            chain += body
+        l4 = bytes(rng.integers(0, 256, 8 + int(rng.integers(0, 24)), dtype=np.uint8))
+        payload = chain + l4
+        pl6 = len(payload)
+        r = rng.random()
+        if r < 0.1:
+            pl6 -= int(rng.integers(1, min(pl6, 16) + 1))      # take() trims
+        elif r < 0.15:
+            pl6 += int(rng.integers(1, 9))                      # longer than the packet: bad
+        src = bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+        r = rng.random()
+        if r < 0.03:
+            src = b"\xff" * 16
+        elif r < 0.06:
+            src = bad_extra
+        hdr = bytes([0x60, 0, 0, 0]) + pl6.to_bytes(2, "big") + bytes([nxts[0], 64]) + src + \
+            bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+        eth = bytes([2, 0, 0, 0, 0, 2, 2, 0, 0, 0, 0, 1, 0x86, 0xDD])
+        fr = eth + hdr + payload
+        if rng.random() < 0.12:                                  # cut inside the chain
+            fr = bytearray(fr[:14 + 40 + int(rng.integers(0, max(len(chain), 1) + 1))])
+            if rng.random() < 0.8:                               # ... with a payload length that fits
+                rem = len(fr) - 54
+                fr[18:20] = int(rng.integers(0, rem + 1)).to_bytes(2, "big")
+            fr = bytes(fr)
+        frames.append(fr)
+    return synth.from_frames(frames, meta=dict(set="eh", seed=seed))
+
+
+def run_eh(b, tmp):
+    pcap = os.path.join(tmp, "eh.pcap")
+    write_pcap(pcap, b.frames())
+    n = b.n
+    res = {}
+    for eh in (True, False):
+        tag = "eh" if eh else "noeh"
+        outs = " ".join(f"ps[{k}] -> ToIPSummaryDump({tag}_nxt{k}.ipsum, FIELDS timestamp);" for k in range(61))
+        cfg = (f"FromDump(eh.pcap, STOP true, TIMING false) -> Strip(14) -> c6 :: CheckIP6Header("
+               f"BADADDRS {BAD6_EXTRA}, PROCESS_EH {str(eh).lower()}) -> t :: Tee(3); "
+               f"t[0] -> ToDump({tag}_full.pcap, ENCAP IP); t[1] -> StripIPHeader -> ToDump({tag}_tp.pcap, ENCAP IP); "
+               f"t[2] -> ps :: PaintSwitch(ANNO 16); {outs} c6[1] -> ToIPSummaryDump({tag}_bad.ipsum, FIELDS timestamp);")
+        click(CLICK, cfg, tmp)
+        full = read_pcap(os.path.join(tmp, f"{tag}_full.pcap"))
+        tp = read_pcap(os.path.join(tmp, f"{tag}_tp.pcap"))
+        bad = read_ipsum(os.path.join(tmp, f"{tag}_bad.ipsum"), 0)
+        valid = np.zeros(n, np.uint8)
+        length = np.zeros(n, np.uint16)
+        thoff = np.zeros(n, np.uint16)
+        nxt = np.full(n, 255, np.uint8)
+        for i, (incl, _) in full.items():
+            valid[i] = 1
+            length[i] = 14 + incl
+            thoff[i] = incl - tp[i][0]
+        for k in range(61):
+            for i in read_ipsum(os.path.join(tmp, f"{tag}_nxt{k}.ipsum"), 0):
+                nxt[i] = k
+        assert len(full) + len(bad) == n
+        res.update({f"{tag}_valid": valid, f"{tag}_length": length, f"{tag}_th": thoff, f"{tag}_nxt": nxt})
+    return res
+
+
 def run_kat(tmp):
     """click_in_cksum on random buffers (odd lengths included) and IPFlowID /
     IP6FlowID hashcodes on random tuples, from the reference harness."""
@@ -566,7 +679,7 @@ def sha(path):
     return hashlib.sha256(open(path, "rb").read()).hexdigest()
 
 
-def main(sets=("ip4", "mix", "prog", "reftests", "kat")):
+def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "kat")):
     prov_path = os.path.join(HERE, "PROVENANCE.json")
     prov = json.load(open(prov_path)) if os.path.exists(prov_path) else {}
     prov.update(generator="tests/golden/gen_golden.py", click=CLICK, click_sha256=sha(CLICK),
@@ -598,6 +711,16 @@ def main(sets=("ip4", "mix", "prog", "reftests", "kat")):
                 o = np.array(p["outputs"])
                 print("reftests:", p["case"], np.bincount(o[o < 254]).tolist(), "nomatch", int((o == 254).sum()),
                       "invalid", int((o == 255).sum()))
+        if "eh" in sets:
+            eb = make_eh_set()
+            re_ = run_eh(eb, tmp)
+            np.savez_compressed(os.path.join(HERE, "eh.npz"), arena=eb.arena, desc=eb.desc, **re_)
+            print("eh: valid", int(re_["eh_valid"].sum()), "th>40", int((re_["eh_th"] > 40).sum()),
+                  "nxt", np.unique(re_["eh_nxt"]).tolist())
+        if "combo" in sets:
+            rc = run_combo(tmp)
+            np.savez_compressed(os.path.join(HERE, "combo.npz"), **rc)
+            print("combo: survivors", int(rc["valid"].sum()))
         if "kat" in sets:
             kat = run_kat(tmp)
             if kat is not None:
@@ -611,6 +734,9 @@ def main(sets=("ip4", "mix", "prog", "reftests", "kat")):
                     "test/standard/Classifier-01 (checked equal to those tests' expected text) + their outputs on "
                     "the prog set; IPFilter-01/02/03 short-packet cases (packets captured from the reference, "
                     "expected outputs from the tests' %expect sections)",
+        "eh": "Strip(14) -> CheckIP6Header(BADADDRS 2001:db8::bad, PROCESS_EH true|false) -> Tee: ToDump (length), "
+              "StripIPHeader -> ToDump (transport offset), PaintSwitch(ANNO 16) (IP6_NXT)",
+        "combo": "IPInputCombo(7, BADSRC, GOODDST) on the ip4 set: survivors and their ip_len",
         "kat": "fcref: click_in_cksum (lib/in_cksum.c), IPFlowID/IP6FlowID::hashcode (headers)",
     })
     prov["ipc_rules"] = IPC_RULES
@@ -620,4 +746,4 @@ def main(sets=("ip4", "mix", "prog", "reftests", "kat")):
 
 
 if __name__ == "__main__":
-    main(tuple(sys.argv[1:]) or ("ip4", "mix", "prog", "reftests", "kat"))
+    main(tuple(sys.argv[1:]) or ("ip4", "mix", "prog", "reftests", "combo", "eh", "kat"))

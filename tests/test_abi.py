@@ -31,14 +31,40 @@ def test_fcgpu_exports_every_declared_symbol():
 def test_struct_layouts_match_header():
     assert C.sizeof(N.fcgpu_anno) == 16
     assert C.sizeof(N.fcgpu_out) == 7 * 8 + 8
-    # 12 u32 scalars + 2x16 u32 lists + nbad6 + 16x16 B
-    assert C.sizeof(N.fcgpu_cfg) == 4 * 12 + 4 * 32 + 4 + 256
+    # 12 u32 scalars + 2x16 u32 lists + nbad6 + 16x16 B + process_eh
+    assert C.sizeof(N.fcgpu_cfg) == 4 * 12 + 4 * 32 + 4 + 256 + 4
     lib = N.load()
     cfg = N.fcgpu_cfg()
     lib.fcgpu_default_cfg(C.byref(cfg))
     assert cfg.size == C.sizeof(N.fcgpu_cfg)
     assert cfg.checksum == 0          # CheckIPHeader default: CHECKSUM false
     assert cfg.native_vlan == 0 and cfg.nbad6 == 1 and bytes(cfg.bad6[0]) == b"\xff" * 16
+
+
+def test_field_offsets_match_c_compiler(tmp_path):
+    """Every ctypes field offset equals offsetof() from the C header (gcc)."""
+    import subprocess
+    structs = {"fcgpu_cfg": N.fcgpu_cfg, "fcgpu_anno": N.fcgpu_anno, "fcgpu_out": N.fcgpu_out,
+               "fcgpu_step": N.fcgpu_step}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "fastclick_gpu.h"', "int main(void) {"]
+    for sname, st in structs.items():
+        lines.append(f'printf("{sname} sizeof %zu\\n", sizeof({sname}));')
+        for fname, _ in st._fields_:
+            lines.append(f'printf("{sname} {fname} %zu\\n", offsetof({sname}, {fname}));')
+    lines.append("return 0; }")
+    src = tmp_path / "off.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "off"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    out = subprocess.check_output([str(exe)], text=True).split("\n")
+    seen = 0
+    for line in filter(None, out):
+        sname, fname, val = line.split()
+        st = structs[sname]
+        want = C.sizeof(st) if fname == "sizeof" else getattr(st, fname).offset
+        assert int(val) == want, (sname, fname, val, want)
+        seen += 1
+    assert seen == sum(len(st._fields_) + 1 for st in structs.values())
 
 
 def test_open_without_device_fails_loudly():

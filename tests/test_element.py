@@ -117,3 +117,58 @@ def test_element_fragments_and_burst_sizes(oracle):
     for burst in (1, 32, 256, 8000):
         r = K.run_element("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4)", b, burst=burst, nsinks=5)
         assert np.array_equal(r["port"], e["port"].astype(np.uint32))
+
+
+def test_config_color_keyword():
+    from fastclick_amd import click as K
+    K.check_config("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, STRIP true, COLOR 7)")
+    with pytest.raises(K.ConfigError, match="COLOR"):
+        K.check_config("GPUIPCheckClassify(COLOR 300)")
+
+
+@pytest.mark.gpu
+def test_element_ipinputcombo_golden():
+    """IPInputCombo(7, BADSRC .., GOODDST ..) (ipinputcombo.cc:65-141) as the
+    element in COLOR/STRIP mode with one output: the reference's survivors
+    (tests/golden/combo.npz) leave in order with PAINT 7, the IP header at
+    data(), length = ip_len; every other packet is killed."""
+    from fastclick_amd import click as K
+    from tests.test_golden import load, batch_of
+    g = load("ip4")
+    c = load("combo")
+    r = K.run_element("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, STRIP true, COLOR 7, "
+                      "BADSRC 192.0.2.255 255.255.255.255, GOODDST 10.9.9.9)", batch_of(g), nsinks=1)
+    ok = c["valid"] == 1
+    assert np.array_equal(r["port"] == 0, ok)
+    assert (r["port"][~ok] == 0xFFFFFFFF).all()
+    assert (r["paint"][ok] == 7).all()
+    assert np.array_equal(r["len"][ok], c["ip_len"][ok].astype(np.uint32))
+    assert (r["nh"][ok] == 0).all()
+    assert np.all(np.diff(r["seq"][ok].astype(np.int64)) > 0)
+
+
+def test_config_ip6_keywords():
+    from fastclick_amd import click as K
+    K.check_config("GPUIPCheckClassify(MODE AUTO, BADADDRS 2001:db8::bad ffff:ffff:ffff:ffff:ffff:ffff:ffff:ffff, "
+                   "PROCESS_EH true)")
+    for bad, msg in [("GPUIPCheckClassify(MODE AUTO, BADADDRS 10.0.0.1)", "BADADDRS"),
+                     ("GPUIPCheckClassify(MODE AUTO, PROCESS_EH sometimes)", "PROCESS_EH")]:
+        with pytest.raises(K.ConfigError, match=msg):
+            K.check_config(bad)
+
+
+@pytest.mark.gpu
+def test_element_ip6_extension_headers():
+    """CheckIP6Header(BADADDRS .., PROCESS_EH true) through the element (MODE
+    AUTO, STRIP): reference verdicts; valid packets leave with the transport
+    header where the reference put it and the reference's trimmed length."""
+    from fastclick_amd import click as K
+    from tests.test_golden import load, batch_of
+    g = load("eh")
+    r = K.run_element("GPUIPCheckClassify(MODE AUTO, BADADDRS 2001:db8::bad, PROCESS_EH true, N 1, "
+                      "LB_MODE hash)", batch_of(g), nsinks=2)
+    ok = g["eh_valid"] == 1
+    assert np.array_equal(r["port"] == 0, ok) and (r["port"][~ok] == 1).all()
+    # STRIP (MODE AUTO default): data() at the IPv6 header, length trimmed
+    assert np.array_equal(r["len"][ok], g["eh_length"][ok].astype(np.uint32) - 14)
+    assert (r["nh"][ok] == 0).all()

@@ -97,6 +97,30 @@ def check_mix(run, g):
         assert np.array_equal(r["hash"][v6], g["hash"][v6]), "IP6FlowID::hashcode"
 
 
+def check_eh(run, g):
+    """CheckIP6Header(BADADDRS 2001:db8::bad, PROCESS_EH true|false): verdict,
+    IP6_NXT annotation, transport-header offset and trimmed length."""
+    import ipaddress
+    b = batch_of(g)
+    bad6 = [b"\xff" * 16, ipaddress.IPv6Address("2001:db8::bad").packed]
+    for tag, eh in (("eh", True), ("noeh", False)):
+        cfg = N.make_cfg(check_mode=N.CHECK_AUTO, classify=N.CLS_LB_HASH, nports=4, bad6=bad6, process_eh=eh)
+        r = run(cfg, b)
+        ok = g[f"{tag}_valid"] == 1
+        assert np.array_equal(r["reason"] == N.R_OK, ok), f"{tag}: verdicts"
+        assert (r["reason"][~ok] == N.R_BAD_IP6).all()
+        if "anno" in r:
+            a = r["anno"]
+            assert np.array_equal(a["ip6_nxt"][ok], g[f"{tag}_nxt"][ok]), f"{tag}: IP6_NXT"
+            assert np.array_equal((a["th"] - a["nh"])[ok], g[f"{tag}_th"][ok]), f"{tag}: transport offset"
+            assert np.array_equal(a["length"][ok], g[f"{tag}_length"][ok]), f"{tag}: take() length"
+    assert (g["eh_th"][g["eh_valid"] == 1] > 40).sum() > 200
+
+
+def test_oracle_eh_golden(oracle):
+    check_eh(oracle.process_batch, load("eh"))
+
+
 def test_oracle_ip4_golden(oracle):
     check_ip4(oracle.process_batch, load("ip4"))
 
@@ -141,6 +165,13 @@ def test_survey_aggregates(oracle):
 def test_gpu_ip4_golden():
     from fastclick_amd import device
     check_ip4(lambda cfg, b: device.process_batch(b, cfg), load("ip4"))
+
+
+@pytest.mark.gpu
+def test_gpu_eh_golden():
+    from fastclick_amd import device
+    for part in (N.PART_GLOBAL, N.PART_TILE):
+        check_eh(lambda cfg, b: device.process_batch(b, cfg, partition=part), load("eh"))
 
 
 @pytest.mark.gpu
