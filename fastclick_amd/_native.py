@@ -17,8 +17,14 @@ LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 ABI_VERSION = 5
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
-    R_BAD_IP6, R_VLAN_REJECT, R_NO_MATCH = range(10)
-NREASON_SLOTS = 9
+    R_BAD_IP6, R_VLAN_REJECT, R_NO_MATCH, R_L4_PROTO, R_L4_LENGTH, R_L4_CKSUM = range(13)
+NREASON_SLOTS = 12
+L4_NONE, L4_UDP, L4_TCP = 0, 1, 2
+
+
+def reason_slot(r: int) -> int:
+    """Counter slot of reason r (reasons 0-5, 7-12; 6 = valid has none)."""
+    return r if r < 6 else r - 1
 CHECK_IP4, MARK_IP4, CHECK_AUTO = 0, 1, 2
 HASH_NONE, HASH_FLOWID, HASH_FLOW5ID = 0, 1, 2
 CLS_NONE, CLS_LB_HASH, CLS_HASH_IP, CLS_HASHSWITCH, CLS_PROGRAM = 0, 1, 2, 3, 4
@@ -27,7 +33,7 @@ STEP_SHORT_YES = 1
 MAX_STEPS = 8192
 MAX_PORTS = 64
 MAX_ADDRS = 16
-CTR_COUNT, CTR_DROPS, CTR_REASON, CTR_PORT = 0, 1, 2, 11
+CTR_COUNT, CTR_DROPS, CTR_REASON, CTR_PORT = 0, 1, 2, 14
 NCOUNTERS = CTR_PORT + MAX_PORTS + 1
 CTR_SHARDS = 64
 PART_GLOBAL, PART_TILE = 0, 1
@@ -56,6 +62,8 @@ class fcgpu_cfg(C.Structure):
         ("nbad6", C.c_uint32),
         ("bad6", (C.c_uint8 * 16) * MAX_ADDRS),
         ("process_eh", C.c_uint32),
+        ("l4_mode", C.c_uint32),
+        ("l4_checksum", C.c_uint32),
     ]
 
 
@@ -183,6 +191,7 @@ def default_cfg() -> fcgpu_cfg:
         cfg.nports = 1
         cfg.hs_length = 1
         cfg.nbad6 = 1
+        cfg.l4_checksum = 1
         for j in range(16):
             cfg.bad6[0][j] = 0xFF
     return cfg
@@ -190,7 +199,8 @@ def default_cfg() -> fcgpu_cfg:
 
 def make_cfg(*, check_mode=CHECK_IP4, offset=0, checksum=False, hash_mode=HASH_FLOWID,
              classify=CLS_NONE, nports=1, hs_offset=0, hs_length=1, native_vlan=0,
-             badsrc=(), gooddst=(), bad6=None, process_eh=False) -> fcgpu_cfg:
+             badsrc=(), gooddst=(), bad6=None, process_eh=False, l4_mode=L4_NONE,
+             l4_checksum=True) -> fcgpu_cfg:
     """Build an fcgpu_cfg. Addresses are raw network-order words (bytes a.b.c.d
     -> little-endian u32 of those bytes), as IPAddress stores them."""
     cfg = default_cfg()
@@ -210,6 +220,8 @@ def make_cfg(*, check_mode=CHECK_IP4, offset=0, checksum=False, hash_mode=HASH_F
     for j, a in enumerate(gooddst):
         cfg.gooddst[j] = a
     cfg.process_eh = 1 if process_eh else 0
+    cfg.l4_mode = l4_mode
+    cfg.l4_checksum = 1 if l4_checksum else 0
     if bad6 is not None:
         cfg.nbad6 = len(bad6)
         for j, a in enumerate(bad6):

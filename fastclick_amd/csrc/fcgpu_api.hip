@@ -110,6 +110,7 @@ class Pool {
 // copies, device outputs, pinned outputs (used when the caller's arrays are
 // pageable), its own stream and completion event.
 struct HostSlot {
+    size_t arena_cap = 0;     // bytes of h_arena / d_arena
     hipStream_t s = nullptr;
     hipEvent_t done = nullptr;
     uint8_t *h_arena = nullptr, *d_arena = nullptr;
@@ -155,6 +156,7 @@ struct fcgpu_ctx {
     uint16_t *d_verdict = nullptr;   // scratch verdicts when the caller wants perm only
     // host-resident staging
     uint8_t *h_arena = nullptr, *d_arena = nullptr;
+    size_t h_arena_cap = 0;
     uint32_t *h_desc = nullptr, *d_desc = nullptr;
     uint16_t *d_hv = nullptr;
     uint32_t *d_hh = nullptr, *d_hperm = nullptr, *d_hstart = nullptr;
@@ -171,6 +173,12 @@ struct fcgpu_ctx {
     std::vector<hipEvent_t> free_ev;
     std::string err;
 };
+
+// Bytes of each frame the host paths stage: the 128-B header window, or the
+// whole frame when the L4 checksum covers the segment.
+static uint32_t host_capture(const fcgpu_ctx *c) {
+    return (c->cfg.l4_mode != FCGPU_L4_NONE && c->cfg.l4_checksum) ? 0xffffffffu : kHostCap;
+}
 
 static std::string g_open_err;
 
@@ -201,23 +209,35 @@ static hipEvent_t take_event(fcgpu_ctx *c) {
 
 // ev0/ev1 non-null: hipExtLaunchKernelGGL records them around the dispatch
 // itself (timestamps of the kernel, not of the stream around it).
-template <int CM, bool CK, int PART, bool PROG>
+template <int CM, bool CK, int PART, bool PROG, bool L4>
 static void launch_rx(const RxArgs &a, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     const size_t lds = PROG ? prog_lds_bytes(a.cfg) : 0;
     if (ev0)
-        hipExtLaunchKernelGGL((k_rx<CM, CK, PART, PROG>), dim3(a.ntiles), dim3(kTile), lds, s, ev0, ev1, 0, a);
+        hipExtLaunchKernelGGL((k_rx<CM, CK, PART, PROG, L4>), dim3(a.ntiles), dim3(kTile), lds, s, ev0, ev1, 0, a);
     else
-        hipLaunchKernelGGL((k_rx<CM, CK, PART, PROG>), dim3(a.ntiles), dim3(kTile), lds, s, a);
+        hipLaunchKernelGGL((k_rx<CM, CK, PART, PROG, L4>), dim3(a.ntiles), dim3(kTile), lds, s, a);
 }
 
+// L4 (CheckUDPHeader/CheckTCPHeader) exists only for the IPv4 check modes
+// (fcgpu_configure rejects it with CHECK_AUTO).
 template <int PART, bool PROG>
 static void launch_rx_part(uint32_t cm, bool ck, const RxArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    const bool l4 = a.cfg.l4_mode != FCGPU_L4_NONE;
     switch (cm * 2 + (ck ? 1 : 0)) {
-    case 0: launch_rx<FCGPU_CHECK_IP4, false, PART, PROG>(a, s, e0, e1); break;
-    case 1: launch_rx<FCGPU_CHECK_IP4, true, PART, PROG>(a, s, e0, e1); break;
-    case 2: case 3: launch_rx<FCGPU_MARK_IP4, false, PART, PROG>(a, s, e0, e1); break;
-    case 4: launch_rx<FCGPU_CHECK_AUTO, false, PART, PROG>(a, s, e0, e1); break;
-    default: launch_rx<FCGPU_CHECK_AUTO, true, PART, PROG>(a, s, e0, e1); break;
+    case 0:
+        if (l4) launch_rx<FCGPU_CHECK_IP4, false, PART, PROG, true>(a, s, e0, e1);
+        else launch_rx<FCGPU_CHECK_IP4, false, PART, PROG, false>(a, s, e0, e1);
+        break;
+    case 1:
+        if (l4) launch_rx<FCGPU_CHECK_IP4, true, PART, PROG, true>(a, s, e0, e1);
+        else launch_rx<FCGPU_CHECK_IP4, true, PART, PROG, false>(a, s, e0, e1);
+        break;
+    case 2: case 3:
+        if (l4) launch_rx<FCGPU_MARK_IP4, false, PART, PROG, true>(a, s, e0, e1);
+        else launch_rx<FCGPU_MARK_IP4, false, PART, PROG, false>(a, s, e0, e1);
+        break;
+    case 4: launch_rx<FCGPU_CHECK_AUTO, false, PART, PROG, false>(a, s, e0, e1); break;
+    default: launch_rx<FCGPU_CHECK_AUTO, true, PART, PROG, false>(a, s, e0, e1); break;
     }
 }
 
@@ -249,6 +269,7 @@ static int process_host_whole(fcgpu_ctx *c, const uint8_t *const *frames, const 
         HIPCHK(c, hipHostMalloc((void **)&c->h_desc, sizeof(uint32_t) * 2 * c->max_batch, hipHostMallocDefault));
         HIPCHK(c, hipMalloc(&c->d_arena, arena_cap));
         HIPCHK(c, hipMemset(c->d_arena, 0, arena_cap));
+        c->h_arena_cap = arena_cap;
         HIPCHK(c, hipMalloc(&c->d_desc, sizeof(uint32_t) * 2 * c->max_batch));
         HIPCHK(c, hipMalloc(&c->d_hv, sizeof(uint16_t) * c->max_batch));
         HIPCHK(c, hipMalloc(&c->d_hh, sizeof(uint32_t) * c->max_batch));
@@ -258,12 +279,29 @@ static int process_host_whole(fcgpu_ctx *c, const uint8_t *const *frames, const 
         HIPCHK(c, hipMalloc(&c->d_htc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * c->max_tiles));
         HIPCHK(c, hipMalloc(&c->d_htp, (size_t)c->max_batch + kTile));
     }
-    // gather: first min(len, 128) bytes of each frame at 64-B aligned offsets.
-    // The device sees the real frame length; bytes past the capture are never
-    // needed for a verdict with headers <= 128 B.
+    // gather: first min(len, 128) bytes of each frame (whole frames for the L4
+    // checksum) at 64-B aligned offsets. The device sees the real frame
+    // length; bytes past the capture are never needed for a verdict.
+    const uint32_t hcap = host_capture(c);
+    size_t need = kArenaPad;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t cap = lens[i] < hcap ? lens[i] : hcap;
+        need += cap ? (cap + 63) & ~(size_t)63 : 64;
+    }
+    if (need > c->h_arena_cap) {
+        hipHostFree(c->h_arena);
+        hipFree(c->d_arena);
+        c->h_arena = nullptr;
+        c->d_arena = nullptr;
+        c->h_arena_cap = 0;
+        HIPCHK(c, hipHostMalloc((void **)&c->h_arena, need, hipHostMallocDefault));
+        HIPCHK(c, hipMalloc(&c->d_arena, need));
+        HIPCHK(c, hipMemset(c->d_arena, 0, need));
+        c->h_arena_cap = need;
+    }
     size_t off = 0;
     for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t cap = lens[i] < kHostCap ? lens[i] : kHostCap;
+        const uint32_t cap = lens[i] < hcap ? lens[i] : hcap;
         memcpy(c->h_arena + off, frames[i], cap);
         c->h_desc[2 * i] = (uint32_t)off;
         c->h_desc[2 * i + 1] = lens[i];
@@ -324,6 +362,7 @@ void fcgpu_default_cfg(fcgpu_cfg *c) {
     c->hs_length = 1;
     c->native_vlan = 0;                // StripEtherVLANHeader default NATIVE_VLAN 0
     c->nbad6 = 1;                      // CheckIP6Header default bad source ff..ff
+    c->l4_checksum = 1;                // CheckUDPHeader/CheckTCPHeader default CHECKSUM true
     memset(c->bad6[0], 0xff, 16);
 }
 
@@ -407,6 +446,9 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     if (cfg->check_mode > FCGPU_CHECK_AUTO) return fail(c, FCGPU_EINVAL, "bad check_mode");
     if (cfg->hash_mode > FCGPU_HASH_FLOW5ID) return fail(c, FCGPU_EINVAL, "bad hash_mode");
     if (cfg->classify > FCGPU_CLS_PROGRAM) return fail(c, FCGPU_EINVAL, "bad classify mode");
+    if (cfg->l4_mode > FCGPU_L4_TCP) return fail(c, FCGPU_EINVAL, "bad l4_mode");
+    if (cfg->l4_mode != FCGPU_L4_NONE && cfg->check_mode == FCGPU_CHECK_AUTO)
+        return fail(c, FCGPU_EINVAL, "l4_mode needs an IPv4 check mode (CHECK_IP4 or MARK_IP4)");
     if (cfg->nports < 1 || cfg->nports > FCGPU_MAX_PORTS) return fail(c, FCGPU_EINVAL, "nports out of range");
     if (cfg->offset < 0 || cfg->offset > 255) return fail(c, FCGPU_EINVAL, "OFFSET out of range [0,255]");
     if (cfg->nbadsrc > FCGPU_MAX_ADDRS || cfg->ngooddst > FCGPU_MAX_ADDRS || cfg->nbad6 > FCGPU_MAX_ADDRS)
@@ -429,6 +471,8 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     d.ngooddst = cfg->ngooddst;
     d.nbad6 = cfg->nbad6;
     d.process_eh = cfg->process_eh ? 1u : 0u;
+    d.l4_mode = cfg->l4_mode;
+    d.l4_checksum = cfg->l4_checksum ? 1u : 0u;
     memcpy(d.badsrc, cfg->badsrc, sizeof(d.badsrc));
     memcpy(d.gooddst, cfg->gooddst, sizeof(d.gooddst));
     memcpy(d.bad6, cfg->bad6, sizeof(d.bad6));
@@ -515,6 +559,7 @@ static int slot_alloc(fcgpu_ctx *c, HostSlot &sl, uint32_t cap) {
     HIPCHK(c, hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
     HIPCHK(c, hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
     const size_t arena = (size_t)cap * kHostCap + kArenaPad;
+    sl.arena_cap = arena;
     HIPCHK(c, hipHostMalloc((void **)&sl.h_arena, arena, hipHostMallocDefault));
     HIPCHK(c, hipHostMalloc((void **)&sl.h_desc, sizeof(uint32_t) * 2 * cap, hipHostMallocDefault));
     HIPCHK(c, hipMalloc(&sl.d_arena, arena));
@@ -597,23 +642,37 @@ static int process_host_pipelined(fcgpu_ctx *c, const uint8_t *const *frames, co
             slot_drain(c, sl, h, pin);
         }
         const uint32_t base = k * cap, cn = n - base < cap ? n - base : cap;
-        // gather the first min(len, 128) B of every frame at 64-B aligned
-        // offsets: sizes per part, then parts copy in parallel
+        // gather the first min(len, 128) B of every frame (whole frames when
+        // the L4 checksum needs them) at 64-B aligned offsets: sizes per
+        // part, then parts copy in parallel
         const uint32_t np = c->pool.size();
+        const uint32_t hcap = host_capture(c);
         std::vector<size_t> part_off(np + 1, 0);
         c->pool.run([&](uint32_t part, uint32_t nparts) {
             size_t sz = 0;
             for (uint32_t i = span(cn, part, nparts); i < span(cn, part + 1, nparts); ++i) {
-                const uint32_t L = lens[base + i], cp = L < kHostCap ? L : kHostCap;
+                const uint32_t L = lens[base + i], cp = L < hcap ? L : hcap;
                 sz += cp ? (cp + 63) & ~63u : 64;
             }
             part_off[part + 1] = sz;
         });
         for (uint32_t p = 0; p < np; ++p) part_off[p + 1] += part_off[p];
+        if (part_off[np] + kArenaPad > sl.arena_cap) {      // whole frames: grow the slot's arena
+            const size_t want = (part_off[np] + kArenaPad) * 5 / 4;
+            hipHostFree(sl.h_arena);
+            hipFree(sl.d_arena);
+            sl.h_arena = nullptr;
+            sl.d_arena = nullptr;
+            sl.arena_cap = 0;
+            HIPCHK(c, hipHostMalloc((void **)&sl.h_arena, want, hipHostMallocDefault));
+            HIPCHK(c, hipMalloc(&sl.d_arena, want));
+            HIPCHK(c, hipMemset(sl.d_arena, 0, want));
+            sl.arena_cap = want;
+        }
         c->pool.run([&](uint32_t part, uint32_t nparts) {
             size_t off = part_off[part];
             for (uint32_t i = span(cn, part, nparts); i < span(cn, part + 1, nparts); ++i) {
-                const uint32_t L = lens[base + i], cp = L < kHostCap ? L : kHostCap;
+                const uint32_t L = lens[base + i], cp = L < hcap ? L : hcap;
                 const uint8_t *src = frames[base + i];
                 uint8_t *dst = sl.h_arena + off;
                 if (cp >= 64) {

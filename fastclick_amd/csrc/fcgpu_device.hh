@@ -40,6 +40,8 @@ struct DevCfg {
     uint32_t gooddst[FCGPU_MAX_ADDRS];
     uint32_t bad6[FCGPU_MAX_ADDRS][4];
     uint32_t process_eh;
+    uint32_t l4_mode;
+    uint32_t l4_checksum;
     const uint4 *prog;        // decision program (FCGPU_CLS_PROGRAM), 16 B per step
     uint32_t prog_n;
     uint32_t prog_kind;
@@ -439,6 +441,153 @@ __device__ __forceinline__ bool ip4_fast(const DevCfg &c, const FrameView &f, ui
     return true;
 }
 
+// ---- CheckUDPHeader / CheckTCPHeader ----------------------
+
+// Lengths and protocol (checkudpheader.cc:96-111, checktcpheader.cc:96-111).
+// Returns the verdict; l4len = segment length, want_sum = checksum to verify.
+__device__ __forceinline__ uint32_t l4_check(const DevCfg &c, const FrameView &f, const fcgpu_anno &an,
+                                             uint32_t &l4len, bool &want_sum) {
+    const uint32_t w0 = f.rd32(an.nh), w2 = f.rd32(an.nh + 8);
+    const uint32_t hl = (w0 & 15) << 2, proto = (w2 >> 8) & 0xff;
+    want_sum = false;
+    if (c.l4_mode == FCGPU_L4_UDP) {
+        if (proto != 17) return FCGPU_R_L4_PROTO;
+        const uint32_t u = f.rd32(an.th + 4);                 // uh_ulen, uh_sum
+        const uint32_t len = bswap16(u & 0xffff);
+        if (len < 8 || (uint32_t)an.length < len + hl + an.nh) return FCGPU_R_L4_LENGTH;
+        l4len = len;
+        want_sum = c.l4_checksum && (u >> 16) != 0;            // uh_sum == 0: not checked
+    } else {
+        if (proto != 6) return FCGPU_R_L4_PROTO;
+        const uint32_t len = bswap16(w0 >> 16) - hl;          // unsigned, as the reference
+        const uint32_t toff = ((f.rd32(an.th + 12) >> 4) & 15) << 2;   // th_off
+        if (toff < 20 || len < toff || (uint32_t)an.length < len + hl + an.nh) return FCGPU_R_L4_LENGTH;
+        l4len = len;
+        want_sum = c.l4_checksum != 0;
+    }
+    return FCGPU_R_OK;
+}
+
+// bytes [lo, hi) of the dword at byte offset off
+__device__ __forceinline__ uint32_t dw_masked(uint32_t w, uint32_t off, uint32_t lo, uint32_t hi) {
+    if (off >= lo && off + 4 <= hi) return w;
+    if (off + 4 <= lo || off >= hi) return 0u;
+    uint32_t m = 0xffffffffu;
+    if (lo > off) m &= 0xffffffffu << (8 * (lo - off));
+    if (hi < off + 4) m &= 0xffffffffu >> (8 * (off + 4 - hi));
+    return w & m;
+}
+
+// One's-complement sums of the L4 segments of the lanes in `need`: 16 lanes
+// per segment read 256 contiguous bytes per step (coalesced, each byte once),
+// four segments per wave step. Each owner lane gets the 16-bit sum of its
+// segment as ~click_in_cksum(seg, len) & 0xffff (lib/in_cksum.c:20-51): the sum
+// of little-endian 16-bit words from the 16-B aligned base, byte-swapped when
+// the segment starts at an odd address (RFC 1071 byte-order independence).
+__device__ __forceinline__ uint32_t wave_l4_sum(const uint8_t *seg, uint32_t len, uint64_t need) {
+    const uint32_t lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+    const uint64_t sa = (uint64_t)seg;
+    uint32_t mine = 0;
+    uint64_t m = need;
+    while (m) {
+        uint32_t own[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            own[k] = m ? (uint32_t)__builtin_ctzll(m) : 64u;
+            m = m ? m & (m - 1) : 0ull;
+        }
+        const uint32_t src = g == 0 ? own[0] : g == 1 ? own[1] : g == 2 ? own[2] : own[3];
+        const int sl = (int)(src & 63);
+        const uint32_t alo = __shfl((uint32_t)sa, sl), ahi = __shfl((uint32_t)(sa >> 32), sl);
+        const uint32_t L = __shfl(len, sl);
+        const uint64_t a = ((uint64_t)ahi << 32) | alo;
+        uint64_t acc = 0;
+        if (src < 64) {
+            const uint32_t lo = (uint32_t)(a & 15), hi = lo + L;
+            const uint8_t *base = reinterpret_cast<const uint8_t *>(a & ~15ull);
+            for (uint32_t o = 16 * j; o < hi; o += 256) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(base + o);
+                acc += (uint64_t)dw_masked(v.x, o, lo, hi) + dw_masked(v.y, o + 4, lo, hi) +
+                       dw_masked(v.z, o + 8, lo, hi) + dw_masked(v.w, o + 12, lo, hi);
+            }
+        }
+        uint32_t alo2 = (uint32_t)acc, ahi2 = (uint32_t)(acc >> 32);
+#pragma unroll
+        for (int o = 8; o >= 1; o >>= 1) {
+            const uint32_t xl = __shfl_xor(alo2, o), xh = __shfl_xor(ahi2, o);
+            const uint64_t t = ((uint64_t)ahi2 << 32 | alo2) + ((uint64_t)xh << 32 | xl);
+            alo2 = (uint32_t)t;
+            ahi2 = (uint32_t)(t >> 32);
+        }
+        uint32_t t = alo2 + ahi2;
+        t += (t < alo2) ? 1u : 0u;
+        t = (t & 0xffff) + (t >> 16);
+        t = (t & 0xffff) + (t >> 16);
+        if (a & 1) t = bswap16(t);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t v = __shfl(t, 16 * k);
+            if (lane == own[k]) mine = v;
+        }
+    }
+    return mine;
+}
+
+// click_in_cksum_pseudohdr (include/clicknet/ip.h:156-163, lib/in_cksum.c:53-111):
+// the final destination of an SSRR/LSRR option replaces ip_dst. True = bad.
+__device__ __forceinline__ bool l4_cksum_bad(const FrameView &f, const fcgpu_anno &an, uint32_t dsum,
+                                             uint32_t len) {
+    const uint32_t w0 = f.rd32(an.nh), hl = (w0 & 15) << 2;
+    const uint32_t proto = (f.rd32(an.nh + 8) >> 8) & 0xff;
+    const uint32_t src = f.rd32(an.nh + 12);
+    uint32_t dst = f.rd32(an.nh + 16);
+    if (hl != 20) {
+        uint32_t opt = an.nh + 20;
+        const uint32_t end = an.nh + hl;
+        while (opt < end) {
+            const uint32_t b = f.rd8(opt);
+            if (b == 1) { ++opt; continue; }                // IPOPT_NOP
+            if (b == 0) break;                              // IPOPT_EOL
+            if (opt + 1 >= end) break;
+            const uint32_t l = f.rd8(opt + 1);
+            if (l < 2 || opt + l > end) break;
+            if ((b == 137 || b == 131) && l >= 7) {         // IPOPT_SSRR, IPOPT_LSRR
+                dst = f.rd32(opt + l - 4);
+                break;
+            }
+            opt += l;
+        }
+    }
+    uint32_t c = dsum + (src & 0xffff) + (src >> 16) + (dst & 0xffff) + (dst >> 16) + bswap16(len) + (proto << 8);
+    c = (c & 0xffff) + (c >> 16);
+    return ((~(c + (c >> 16))) & 0xffffu) != 0;
+}
+
+// The L4 stage of k_rx for IPv4-accepted lanes (valid or no program match):
+// length/protocol per lane, then the wave-cooperative checksum.
+__device__ __forceinline__ void l4_stage(const DevCfg &c, const FrameView &f, const uint8_t *frame, bool live,
+                                         PktResult &r) {
+    uint32_t l4len = 0;
+    bool want = false;
+    if (live && (r.reason == FCGPU_R_OK || r.reason == FCGPU_R_NO_MATCH)) {
+        const uint32_t lr = l4_check(c, f, r.an, l4len, want);
+        if (lr != FCGPU_R_OK) {
+            r.reason = lr;
+            r.port = c.nports;
+            r.hash = 0;
+        }
+    }
+    const uint64_t need = __ballot(want);
+    if (need) {
+        const uint32_t dsum = wave_l4_sum(frame + r.an.th, l4len, need);
+        if (want && l4_cksum_bad(f, r.an, dsum, l4len)) {
+            r.reason = FCGPU_R_L4_CKSUM;
+            r.port = c.nports;
+            r.hash = 0;
+        }
+    }
+}
+
 __device__ __forceinline__ void glds16(const uint8_t *src, uint8_t *lds) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                      (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
@@ -467,7 +616,7 @@ constexpr int kPartTile = 2;     // + stable partition of each 256-packet tile, 
 // -> classify over one 256-packet tile; per-tile histogram by wave ballots;
 // counters by sharded atomics; optionally the tile's stable per-output
 // partition (CLASSIFY_EACH_PACKET on a 256-packet PacketBatch).
-template <int CM, bool CK, int PART, bool PROG, bool FAST = (CM == FCGPU_CHECK_IP4)>
+template <int CM, bool CK, int PART, bool PROG, bool L4, bool FAST = (CM == FCGPU_CHECK_IP4)>
 __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4 * kWave * kWin];
     __shared__ uint32_t s_cnt[4][kMaxBins];
@@ -518,6 +667,7 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
     } else if (live) {
         process_packet<CM, CK, PROG>(A.cfg, f, d.y, r, sprog);
     }
+    if (L4) l4_stage(A.cfg, f, A.arena + d.x, live, r);
     if (live) {
         if (A.verdict) A.verdict[i] = (uint16_t)(r.reason | (r.port << 8));
         if (A.hash) A.hash[i] = r.hash;
@@ -590,11 +740,12 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
             if (t < nb) atomicAdd(&ctr[FCGPU_CTR_PORT + t], (unsigned long long)tot);
             else atomicAdd(&ctr[FCGPU_CTR_REASON + (t - nb)], (unsigned long long)tot);
         }
-        if (t == nb - 1) {   // the invalid list: drops (minus no-match), count = packets - drops
+        if (t == nb - 1) {   // the invalid list: drops (minus post-check verdicts), count = packets - drops
             const uint32_t live_n = min(A.n - tile * kTile, (uint32_t)kTile);
-            const uint32_t sm = nb + FCGPU_NREASON_SLOTS - 1;   // reason 9's slot
-            const uint32_t nomatch = s_cnt[0][sm] + s_cnt[1][sm] + s_cnt[2][sm] + s_cnt[3][sm];
-            const uint32_t drops = tot - nomatch;
+            uint32_t post = 0;   // reasons >= FCGPU_R_NO_MATCH: slots 8 .. NREASON_SLOTS-1
+            for (uint32_t sm = nb + reason_slot(FCGPU_R_NO_MATCH); sm < nb + FCGPU_NREASON_SLOTS; ++sm)
+                post += s_cnt[0][sm] + s_cnt[1][sm] + s_cnt[2][sm] + s_cnt[3][sm];
+            const uint32_t drops = tot - post;
             if (drops) atomicAdd(&ctr[FCGPU_CTR_DROPS], (unsigned long long)drops);
             if (live_n - drops) atomicAdd(&ctr[FCGPU_CTR_COUNT], (unsigned long long)(live_n - drops));
         }

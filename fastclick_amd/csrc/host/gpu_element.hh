@@ -22,6 +22,8 @@
 //     (lines separated by newlines or '|', program_text.hh); N is the
 //     classifier's output count. Packets no rule matches are killed, as
 //     CLASSIFY_EACH_PACKET kills a packet whose port is out of range.
+//   L4 UDP|TCP, L4_CHECKSUM (default true)   -- CheckUDPHeader / CheckTCPHeader
+//     behind the IPv4 check (MODE CHECK or MARK); their drops join output N
 //   COLOR (PAINT annotation on every packet)  -- IPInputCombo (with OFFSET 14,
 //     CHECKSUM true, STRIP true and no invalid output: ipinputcombo.cc:65-141)
 //   MODE CHECK|MARK|AUTO, HASH NONE|FLOWID|FLOW5ID, STRIP, BATCH, DEVICE,
@@ -106,6 +108,14 @@ class GPUIPCheckClassify : public Element {
                 _cfg.classify = FCGPU_CLS_HASHSWITCH;
                 _cfg.hs_offset = (int32_t)o;
                 _cfg.hs_length = (int32_t)l;
+            } else if (k == "L4") {
+                if (v == "UDP") _cfg.l4_mode = FCGPU_L4_UDP;
+                else if (v == "TCP") _cfg.l4_mode = FCGPU_L4_TCP;
+                else if (v == "NONE") _cfg.l4_mode = FCGPU_L4_NONE;
+                else return err(errh, "L4 expects UDP, TCP or NONE");
+            } else if (k == "L4_CHECKSUM") {
+                if (!parse_bool(v, b)) return err(errh, "L4_CHECKSUM expects true/false");
+                _cfg.l4_checksum = b;
             } else if (k == "COLOR") {
                 if (!parse_int(v, n) || n < 0 || n > 255) return err(errh, "COLOR expects an integer in [0,255]");
                 _color = (int)n;
@@ -166,6 +176,8 @@ class GPUIPCheckClassify : public Element {
             }
         }
         if (!strip_set) _strip = (_cfg.check_mode == FCGPU_CHECK_AUTO);
+        if (_cfg.l4_mode != FCGPU_L4_NONE && _cfg.check_mode == FCGPU_CHECK_AUTO)
+            return err(errh, "L4 needs MODE CHECK or MARK");
         if (_cfg.classify == FCGPU_CLS_PROGRAM) {
             if (_prog.output_everything >= (int32_t)_cfg.nports && _prog.output_everything != 0x7fff)
                 return err(errh, "PROGRAM sends everything to a missing output");
@@ -278,12 +290,13 @@ class GPUIPCheckClassify : public Element {
             if (_color >= 0) p->set_anno_u8(PAINT_ANNO_OFFSET, (uint8_t)_color);   // SET_PAINT_ANNO
             if (autom && reason != FCGPU_R_VLAN_REJECT)
                 p->set_anno_u16(VLAN_TCI_ANNO_OFFSET, a.vlan_tci);    // StripEtherVLANHeader
-            if (reason == FCGPU_R_OK || reason == FCGPU_R_NO_MATCH) {
+            if (reason == FCGPU_R_OK || reason >= FCGPU_R_NO_MATCH) {
                 p->set_network_header(a.nh, a.th);                     // set_ip_header / set_ip6_header
                 if (a.length < p->length()) p->take(p->length() - a.length);
                 if (a.ipver == 6) p->set_anno_u8(IP6_NXT_ANNO_OFFSET, a.ip6_nxt);
                 else p->set_anno_u32(DST_IP_ANNO_OFFSET, a.dst_ip);
-                if (hashing) p->set_anno_u32(AGGREGATE_ANNO_OFFSET, _hash[i]);   // AggregateHash
+                if (hashing && reason <= FCGPU_R_NO_MATCH)   // AggregateHash (not after an L4 drop)
+                    p->set_anno_u32(AGGREGATE_ANNO_OFFSET, _hash[i]);
                 if (_strip) p->pull(a.nh);
             } else {
                 if (!_warned || _verbose) {

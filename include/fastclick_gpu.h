@@ -28,7 +28,7 @@
  * Batch layout ("arena + descriptor"):
  *   arena : bytes; packet i's frame starts at arena + desc[2i] and is
  *           desc[2i+1] bytes long. The arena must stay readable for 128 bytes
- *           past every frame start and 8 bytes past every frame end
+ *           past every frame start and 16 bytes past every frame end
  *           (header-window over-read; bytes outside the frame never decide a
  *           verdict).
  *   desc  : uint32 pairs (offset, length), 8 bytes per packet.
@@ -70,7 +70,14 @@ extern "C" {
 #define FCGPU_R_VLAN_REJECT 8   /* StripEtherVLANHeader output 1 (untagged, NATIVE_VLAN < 0) */
 #define FCGPU_R_NO_MATCH    9   /* valid, but the classifier program matched no output:
                                    CLASSIFY_EACH_PACKET kills it (packetbatch.hh:268)  */
-#define FCGPU_NREASON_SLOTS 9   /* counters for reasons 0-5, 7, 8, 9        */
+/* CheckUDPHeader / CheckTCPHeader::Reason (elements/tcpudp/checkudpheader.hh:83-87,
+ * checktcpheader.hh:83-87) for IPv4-valid packets, when l4_mode is set: */
+#define FCGPU_R_L4_PROTO    10  /* NOT_UDP / NOT_TCP                         */
+#define FCGPU_R_L4_LENGTH   11  /* BAD_LENGTH                                */
+#define FCGPU_R_L4_CKSUM    12  /* BAD_CHECKSUM (pseudo-header checksum)     */
+#define FCGPU_NREASON_SLOTS 12  /* counters for reasons 0-5, 7-12            */
+/* Reasons >= FCGPU_R_NO_MATCH are decided after CheckIPHeader accepted the
+ * packet: they count in "count", not in "drops". */
 
 /* check_mode */
 #define FCGPU_CHECK_IP4   0   /* CheckIPHeader(OFFSET o[, CHECKSUM c, BADSRC, GOODDST]) */
@@ -89,6 +96,14 @@ extern "C" {
 #define FCGPU_CLS_HASHSWITCH 3  /* HashSwitch(hs_offset, hs_length), nports = MAX        */
 #define FCGPU_CLS_PROGRAM    4  /* decision program set by fcgpu_set_program: IPFilter /
                                    IPClassifier or Classifier                          */
+
+/* l4_mode: a CheckUDPHeader / CheckTCPHeader after the IPv4 check (CHECK_IP4 or
+ * MARK_IP4 only). The checksum covers the whole L4 segment, so with
+ * l4_checksum the device reads every byte of the packet, not only the header
+ * window. */
+#define FCGPU_L4_NONE 0
+#define FCGPU_L4_UDP  1
+#define FCGPU_L4_TCP  2
 
 #define FCGPU_MAX_PORTS   64
 #define FCGPU_MAX_ADDRS   16
@@ -115,6 +130,9 @@ typedef struct fcgpu_cfg {
     uint32_t process_eh;      /* CheckIP6Header PROCESS_EH: follow hop-by-hop, routing,
                                  fragment and AH extension headers (ip6_follow_eh,
                                  include/click/ip6address.hh:417-448)                    */
+    uint32_t l4_mode;         /* FCGPU_L4_*                                               */
+    uint32_t l4_checksum;     /* CheckUDPHeader/CheckTCPHeader CHECKSUM (reference default
+                                 TRUE: checkudpheader.cc:54, checktcpheader.cc)          */
 } fcgpu_cfg;
 
 /* Optional per-packet annotations (16 B), mirroring what the reference
@@ -165,13 +183,13 @@ typedef struct fcgpu_ctx fcgpu_ctx;
 /* Counter vector layout returned by fcgpu_read_counters (uint64):
  *   [0] count (valid packets)         CheckIPHeader "count"
  *   [1] drops                         CheckIPHeader "drops"
- *   [2 .. 2+9)  reason slots for reasons 0-5, 7, 8 ("drop_details") and 9
- *               (no classifier match; not a drop of the checker)
- *   [11 .. 11+nports+1) per-output packet counts, last = invalid list       */
+ *   [2 .. 2+12) reason slots for reasons 0-5, 7, 8 ("drop_details") and
+ *               9-12 (no classifier match, L4 checks; not drops of the checker)
+ *   [14 .. 14+nports+1) per-output packet counts, last = invalid list       */
 #define FCGPU_CTR_COUNT   0
 #define FCGPU_CTR_DROPS   1
 #define FCGPU_CTR_REASON  2
-#define FCGPU_CTR_PORT    11
+#define FCGPU_CTR_PORT    14
 #define FCGPU_NCOUNTERS   (FCGPU_CTR_PORT + FCGPU_MAX_PORTS + 1)
 /* On the device the vector is kept in FCGPU_CTR_SHARDS replicas (tiles add to
  * replica tile % FCGPU_CTR_SHARDS) and summed on read, like per_thread<>

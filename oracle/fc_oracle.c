@@ -38,6 +38,41 @@ uint16_t fco_in_cksum(const uint8_t *addr, int len)
     return (uint16_t)~sum;
 }
 
+/* click_in_cksum_pseudohdr_raw / _hard (lib/in_cksum.c:53-111) and the
+ * dispatch of click_in_cksum_pseudohdr (include/clicknet/ip.h:156-163): with
+ * IP options, the final destination of an SSRR/LSRR option replaces ip_dst. */
+static uint16_t pseudohdr_raw(uint32_t csum, uint32_t src, uint32_t dst, int proto, int packet_len)
+{
+    csum = ~csum & 0xFFFF;
+    csum += (src & 0xffff) + (src >> 16);
+    csum += (dst & 0xffff) + (dst >> 16);
+    csum += (uint32_t)(uint16_t)(((packet_len & 0xff) << 8) | ((packet_len >> 8) & 0xff)) + ((uint32_t)proto << 8);
+    csum = (csum & 0xffff) + (csum >> 16);
+    return (uint16_t)(~(csum + (csum >> 16)) & 0xFFFF);
+}
+
+uint16_t fco_in_cksum_pseudohdr(uint16_t data_csum, const uint8_t *iph, int packet_len)
+{
+    uint32_t src, dst;
+    memcpy(&src, iph + 12, 4);
+    memcpy(&dst, iph + 16, 4);
+    const int hl = (iph[0] & 15) << 2;
+    if (hl != 20) {
+        const uint8_t *opt = iph + 20, *end = iph + hl;
+        while (opt < end) {
+            if (*opt == 1) { opt++; continue; }             /* IPOPT_NOP */
+            if (*opt == 0) break;                           /* IPOPT_EOL */
+            if (opt + 1 >= end || opt[1] < 2 || opt + opt[1] > end) break;
+            if ((*opt == 137 || *opt == 131) && opt[1] >= 7) { /* IPOPT_SSRR, IPOPT_LSRR */
+                memcpy(&dst, opt + opt[1] - 4, 4);
+                break;
+            }
+            opt += opt[1];
+        }
+    }
+    return pseudohdr_raw(data_csum, src, dst, iph[9], packet_len);
+}
+
 /* include/click/ipflowid.hh:153-164 with IPAddress::hashcode = raw s_addr
  * (include/click/ipaddress.hh:346-350); hashcode_t is 64-bit, consumers keep
  * the low 32 bits (elements/analysis/aggregatehash.cc:51). */
@@ -286,6 +321,36 @@ uint32_t fco_run_program(const uint8_t *f, const fcgpu_anno *a)
     return 0x7fff;
 }
 
+/* CheckUDPHeader::simple_action (elements/tcpudp/checkudpheader.cc:96-121) /
+ * CheckTCPHeader::simple_action (elements/tcpudp/checktcpheader.cc:96-123)
+ * behind the IPv4 check. */
+static int check_l4(const fcgpu_cfg *c, const uint8_t *f, const fcgpu_anno *a)
+{
+    const uint8_t *ip = f + a->nh, *th = f + a->th;
+    const unsigned hl = (unsigned)(ip[0] & 15) << 2, proto = ip[9];
+    unsigned len;
+    int want;
+    if (c->l4_mode == FCGPU_L4_UDP) {
+        if (proto != 17)
+            return FCGPU_R_L4_PROTO;
+        len = be16(th + 4);
+        if (len < 8 || a->length < len + hl + a->nh)
+            return FCGPU_R_L4_LENGTH;
+        want = c->l4_checksum && raw16(th + 6) != 0;
+    } else {
+        if (proto != 6)
+            return FCGPU_R_L4_PROTO;
+        len = be16(ip + 2) - hl;
+        const unsigned toff = (unsigned)(th[12] >> 4) << 2;
+        if (toff < 20 || len < toff || a->length < len + hl + a->nh)
+            return FCGPU_R_L4_LENGTH;
+        want = c->l4_checksum != 0;
+    }
+    if (want && fco_in_cksum_pseudohdr(fco_in_cksum(th, (int)len), ip, (int)len) != 0)
+        return FCGPU_R_L4_CKSUM;
+    return FCGPU_R_OK;
+}
+
 void fco_process_packet(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, fco_result *r)
 {
     memset(r, 0, sizeof(*r));
@@ -321,6 +386,8 @@ void fco_process_packet(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, fco_
     } else {
         reason = check_ip4(c, f, len, o, a);
     }
+    if (reason == FCGPU_R_OK && c->l4_mode != FCGPU_L4_NONE && !v6)
+        reason = check_l4(c, f, a);
     r->reason = (uint8_t)reason;
     if (reason != FCGPU_R_OK) {
         r->port = (uint8_t)c->nports;
@@ -385,7 +452,7 @@ void fco_process_batch2(const fcgpu_cfg *c, const uint8_t *arena, const uint32_t
         port[i] = r.port;
         if (ctr) {
             if (r.reason == FCGPU_R_OK) ctr[FCGPU_CTR_COUNT]++;
-            else if (r.reason == FCGPU_R_NO_MATCH) { ctr[FCGPU_CTR_COUNT]++; ctr[FCGPU_CTR_REASON + reason_slot(r.reason)]++; }
+            else if (r.reason >= FCGPU_R_NO_MATCH) { ctr[FCGPU_CTR_COUNT]++; ctr[FCGPU_CTR_REASON + reason_slot(r.reason)]++; }
             else { ctr[FCGPU_CTR_DROPS]++; ctr[FCGPU_CTR_REASON + reason_slot(r.reason)]++; }
             ctr[FCGPU_CTR_PORT + r.port]++;
         }

@@ -19,6 +19,7 @@ extern "C" {
 #endif
 
 /* A1: lib/in_cksum.c:20-51 */
+uint16_t fco_in_cksum_pseudohdr(uint16_t data_csum, const uint8_t *iph, int packet_len);
 uint16_t fco_in_cksum(const uint8_t *addr, int len);
 
 /* Per-packet result of the fused chain (same meaning as the GPU outputs). */

@@ -650,6 +650,137 @@ def run_eh(b, tmp):
     return res
 
 
+def _csum16(data: bytes) -> int:
+    if len(data) % 2:
+        data += b"\0"
+    s = int(np.frombuffer(data, ">u2").astype(np.uint64).sum()) if data else 0
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return s
+
+
+def make_l4_set(n=3000, seed=2028):
+    """IPv4 frames for CheckUDPHeader / CheckTCPHeader: UDP/TCP/ICMP/GRE,
+    payloads 0..1460 B (odd lengths included), IP options incl. LSRR/SSRR (the
+    pseudo-header then uses the route's final destination), correct L4
+    checksums, then: corrupted payload bytes, UDP checksum 0, bad uh_ulen,
+    UDP shorter than the IP payload, bad TCP data offsets, trailing padding,
+    and frames cut short (IP check fails first)."""
+    rng = np.random.default_rng(seed)
+    frames = []
+    for i in range(n):
+        proto = int(rng.choice([17, 17, 17, 6, 6, 6, 1, 47]))
+        plen = int(rng.choice([0, 1, 7, 18, 33, 100, 257, 512, 999, 1400, 1460]))
+        payload = bytes(rng.integers(0, 256, plen, dtype=np.uint8))
+        src = bytes(rng.integers(0, 256, 4, dtype=np.uint8))
+        dst = bytes(rng.integers(0, 256, 4, dtype=np.uint8))
+        opts = b""
+        final = dst
+        r = rng.random()
+        if r < 0.06:                         # LSRR / SSRR with 1-2 hops
+            hops = int(rng.integers(1, 3))
+            route = bytes(rng.integers(0, 256, 4 * hops, dtype=np.uint8))
+            kind = int(rng.choice([131, 137]))
+            opts = bytes([1, kind, 3 + 4 * hops, 4]) + route
+            final = route[-4:]
+        elif r < 0.12:                       # record route / NOPs (dst unchanged)
+            opts = bytes([1, 1, 7, 7, 4]) + bytes(4) + bytes([0])
+        elif r < 0.14:                       # malformed option length: scan stops
+            opts = bytes([131, 1, 0, 0])
+        while len(opts) % 4:
+            opts += b"\0"
+        hl = 20 + len(opts)
+        if proto == 17:
+            ulen = 8 + plen
+            l4 = bytearray(rng.integers(0, 256, 2, dtype=np.uint8).tobytes() +
+                           rng.integers(0, 256, 2, dtype=np.uint8).tobytes() + ulen.to_bytes(2, "big") + b"\0\0") + payload
+        elif proto == 6:
+            l4 = bytearray(rng.integers(0, 256, 12, dtype=np.uint8).tobytes()) + bytearray(8) + payload
+            l4[12] = 5 << 4
+            l4[13] = int(rng.choice([0x02, 0x10, 0x18]))
+        else:
+            l4 = bytearray(8) + payload
+        L = hl + len(l4)
+        ph = src + final + bytes([0, proto]) + len(l4).to_bytes(2, "big")
+        if proto in (17, 6):
+            ck = (~_csum16(ph + bytes(l4))) & 0xFFFF
+            if proto == 17 and ck == 0:
+                ck = 0xFFFF
+            pos = 6 if proto == 17 else 16
+            l4[pos:pos + 2] = ck.to_bytes(2, "big")
+        ip = bytearray([0x40 | (hl // 4), 0]) + L.to_bytes(2, "big") + bytes(rng.integers(0, 256, 2, dtype=np.uint8)) + \
+            bytes([0, 0, 64, proto, 0, 0]) + src + dst + opts
+        r = rng.random()
+        tail = b""
+        if r < 0.08 and len(l4) > 8:         # corrupt one L4 byte (checksum now bad)
+            j = int(rng.integers(0, len(l4)))
+            l4[j] ^= 1 << int(rng.integers(0, 8))
+        elif r < 0.13 and proto == 17:       # checksum 0: not verified
+            l4[6:8] = b"\0\0"
+            if len(l4) > 8:
+                l4[int(rng.integers(8, len(l4)))] ^= 0xFF
+        elif r < 0.16 and proto == 17:       # bad uh_ulen
+            l4[4:6] = int(rng.choice([0, 7, len(l4) + 1, len(l4) + 100])).to_bytes(2, "big")
+        elif r < 0.19 and proto == 17 and plen > 4:   # UDP shorter than the IP payload (valid checksum)
+            short = 8 + plen - int(rng.integers(1, 5))
+            l4[4:6] = short.to_bytes(2, "big")
+            l4[6:8] = b"\0\0"
+            ph2 = src + final + bytes([0, 17]) + short.to_bytes(2, "big")
+            ck = (~_csum16(ph2 + bytes(l4[:short]))) & 0xFFFF
+            l4[6:8] = (ck or 0xFFFF).to_bytes(2, "big")
+        elif r < 0.22 and proto == 6:        # bad TCP data offset
+            l4[12] = int(rng.choice([0, 4, 15])) << 4
+        elif r < 0.26:                       # trailing padding (trimmed by CheckIPHeader)
+            tail = bytes(rng.integers(0, 256, int(rng.integers(1, 20)), dtype=np.uint8))
+        ip[10:12] = b"\0\0"
+        ip[10:12] = ((~_csum16(bytes(ip))) & 0xFFFF).to_bytes(2, "big")
+        eth = bytes([2, 0, 0, 0, 0, 2, 2, 0, 0, 0, 0, 1, 8, 0])
+        fr = eth + bytes(ip) + bytes(l4) + tail
+        if rng.random() < 0.02:              # cut: the IP check drops it
+            fr = fr[:len(fr) - int(rng.integers(1, 8))]
+        frames.append(fr)
+    return synth.from_frames(frames, meta=dict(set="l4", seed=seed))
+
+
+def run_l4(b, tmp):
+    """Per packet and element (UDP, TCP): 255 = CheckIPHeader dropped it, 6 =
+    passed, 10 NOT_UDP/NOT_TCP, 11 BAD_LENGTH, 12 BAD_CHECKSUM (a second run
+    with CHECKSUM false separates length from checksum failures)."""
+    pcap = os.path.join(tmp, "l4.pcap")
+    write_pcap(pcap, b.frames())
+    n = b.n
+    A = b.arena
+    proto = np.array([A[int(o) + 14 + 9] for o in b.desc[:, 0]])
+    res = {}
+    for el, want in (("CheckUDPHeader", 17), ("CheckTCPHeader", 6)):
+        verdict = {}
+        for ck in (True, False):
+            tag = f"{el}_{int(ck)}"
+            click(CLICK, f"FromDump(l4.pcap, STOP true, TIMING false) -> Strip(14) -> ip :: CheckIPHeader(CHECKSUM true) "
+                         f"-> c :: {el}(CHECKSUM {str(ck).lower()}) -> ToIPSummaryDump({tag}_ok.ipsum, FIELDS timestamp); "
+                         f"c[1] -> ToIPSummaryDump({tag}_bad.ipsum, FIELDS timestamp); "
+                         f"ip[1] -> ToIPSummaryDump({tag}_ipbad.ipsum, FIELDS timestamp);", tmp)
+            v = np.zeros(n, np.uint8)
+            for i in read_ipsum(os.path.join(tmp, f"{tag}_ok.ipsum"), 0):
+                v[i] = 1
+            for i in read_ipsum(os.path.join(tmp, f"{tag}_bad.ipsum"), 0):
+                v[i] = 2
+            for i in read_ipsum(os.path.join(tmp, f"{tag}_ipbad.ipsum"), 0):
+                v[i] = 3
+            assert (v > 0).all()
+            verdict[ck] = v
+        out = np.full(n, 255, np.uint8)
+        v1, v0 = verdict[True], verdict[False]
+        out[v1 == 1] = 6
+        bad = v1 == 2
+        out[bad & (proto != want)] = 10
+        out[bad & (proto == want) & (v0 == 2)] = 11
+        out[bad & (proto == want) & (v0 == 1)] = 12
+        assert (out[v1 == 3] == 255).all()
+        res["udp" if want == 17 else "tcp"] = out
+    return res
+
+
 def run_kat(tmp):
     """click_in_cksum on random buffers (odd lengths included) and IPFlowID /
     IP6FlowID hashcodes on random tuples, from the reference harness."""
@@ -679,7 +810,7 @@ def sha(path):
     return hashlib.sha256(open(path, "rb").read()).hexdigest()
 
 
-def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "kat")):
+def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "kat")):
     prov_path = os.path.join(HERE, "PROVENANCE.json")
     prov = json.load(open(prov_path)) if os.path.exists(prov_path) else {}
     prov.update(generator="tests/golden/gen_golden.py", click=CLICK, click_sha256=sha(CLICK),
@@ -717,6 +848,12 @@ def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "kat")):
             np.savez_compressed(os.path.join(HERE, "eh.npz"), arena=eb.arena, desc=eb.desc, **re_)
             print("eh: valid", int(re_["eh_valid"].sum()), "th>40", int((re_["eh_th"] > 40).sum()),
                   "nxt", np.unique(re_["eh_nxt"]).tolist())
+        if "l4" in sets:
+            lb = make_l4_set()
+            rl = run_l4(lb, tmp)
+            np.savez_compressed(os.path.join(HERE, "l4.npz"), arena=lb.arena, desc=lb.desc, **rl)
+            for k in ("udp", "tcp"):
+                print("l4", k, {int(v): int(c) for v, c in zip(*np.unique(rl[k], return_counts=True))})
         if "combo" in sets:
             rc = run_combo(tmp)
             np.savez_compressed(os.path.join(HERE, "combo.npz"), **rc)
@@ -736,6 +873,8 @@ def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "kat")):
                     "expected outputs from the tests' %expect sections)",
         "eh": "Strip(14) -> CheckIP6Header(BADADDRS 2001:db8::bad, PROCESS_EH true|false) -> Tee: ToDump (length), "
               "StripIPHeader -> ToDump (transport offset), PaintSwitch(ANNO 16) (IP6_NXT)",
+        "l4": "Strip(14) -> CheckIPHeader(CHECKSUM true) -> CheckUDPHeader|CheckTCPHeader(CHECKSUM true|false): "
+              "per-packet verdicts (reason split by the CHECKSUM false run)",
         "combo": "IPInputCombo(7, BADSRC, GOODDST) on the ip4 set: survivors and their ip_len",
         "kat": "fcref: click_in_cksum (lib/in_cksum.c), IPFlowID/IP6FlowID::hashcode (headers)",
     })
@@ -746,4 +885,4 @@ def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "kat")):
 
 
 if __name__ == "__main__":
-    main(tuple(sys.argv[1:]) or ("ip4", "mix", "prog", "reftests", "combo", "eh", "kat"))
+    main(tuple(sys.argv[1:]) or ("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "kat"))

@@ -31,14 +31,15 @@ def test_fcgpu_exports_every_declared_symbol():
 def test_struct_layouts_match_header():
     assert C.sizeof(N.fcgpu_anno) == 16
     assert C.sizeof(N.fcgpu_out) == 7 * 8 + 8
-    # 12 u32 scalars + 2x16 u32 lists + nbad6 + 16x16 B + process_eh
-    assert C.sizeof(N.fcgpu_cfg) == 4 * 12 + 4 * 32 + 4 + 256 + 4
+    # 12 u32 scalars + 2x16 u32 lists + nbad6 + 16x16 B + process_eh, l4_mode, l4_checksum
+    assert C.sizeof(N.fcgpu_cfg) == 4 * 12 + 4 * 32 + 4 + 256 + 3 * 4
     lib = N.load()
     cfg = N.fcgpu_cfg()
     lib.fcgpu_default_cfg(C.byref(cfg))
     assert cfg.size == C.sizeof(N.fcgpu_cfg)
     assert cfg.checksum == 0          # CheckIPHeader default: CHECKSUM false
     assert cfg.native_vlan == 0 and cfg.nbad6 == 1 and bytes(cfg.bad6[0]) == b"\xff" * 16
+    assert cfg.l4_mode == N.L4_NONE and cfg.l4_checksum == 1   # CheckUDPHeader default CHECKSUM true
 
 
 def test_field_offsets_match_c_compiler(tmp_path):

@@ -178,3 +178,34 @@ def test_gpu_eh_golden():
 def test_gpu_mix_golden():
     from fastclick_amd import device
     check_mix(lambda cfg, b: device.process_batch(b, cfg), load("mix"))
+
+
+def check_l4(run, g, partitions=(None,)):
+    """CheckIPHeader(CHECKSUM true) -> CheckUDPHeader / CheckTCPHeader
+    (CHECKSUM true and false): per-packet verdicts of the reference."""
+    b = batch_of(g)
+    for key, mode in (("udp", N.L4_UDP), ("tcp", N.L4_TCP)):
+        for ck in (True, False):
+            cfg = N.make_cfg(offset=14, checksum=True, l4_mode=mode, l4_checksum=ck,
+                             classify=N.CLS_LB_HASH, nports=4)
+            r = run(cfg, b)
+            got = np.where(r["reason"] < 6, 255, r["reason"]).astype(np.uint8)
+            exp = g[key].copy()
+            if not ck:
+                exp[exp == N.R_L4_CKSUM] = N.R_OK
+            bad = np.nonzero(got != exp)[0]
+            assert len(bad) == 0, f"{key} cksum={ck}: {len(bad)} differ, first {bad[:8]} {got[bad[:8]]} {exp[bad[:8]]}"
+            ok = exp == N.R_OK
+            assert (r["port"][~ok] == 4).all()
+    assert (g["udp"] == N.R_L4_CKSUM).sum() > 50 and (g["tcp"] == N.R_L4_CKSUM).sum() > 50
+
+
+def test_oracle_l4_golden(oracle):
+    check_l4(oracle.process_batch, load("l4"))
+
+
+@pytest.mark.gpu
+def test_gpu_l4_golden():
+    from fastclick_amd import device
+    for part in (N.PART_GLOBAL, N.PART_TILE):
+        check_l4(lambda cfg, b: device.process_batch(b, cfg, partition=part), load("l4"))

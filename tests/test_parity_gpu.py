@@ -270,3 +270,30 @@ def test_large_batch_properties(dev, oracle):
         assert (got["port"][run] == p).all()
     gt = dev.process_batch(b, cfg, anno=False, perm=True, partition=N.PART_TILE)
     assert np.array_equal(gt["perm_tile"], exp["perm_tile"]) and np.array_equal(gt["tile_count"], exp["tile_count"])
+
+
+@pytest.mark.parametrize("mode", [N.L4_UDP, N.L4_TCP])
+def test_l4_checks_misaligned_and_host(dev, oracle, mode):
+    """L4 checks on the reference-pinned L4 set replicated 40x at misaligned
+    frame offsets (odd segment starts, partial 16-B chunks), device-resident
+    and through the host path (whole frames staged), vs the oracle."""
+    import ctypes as C
+    from tests.test_golden import load, batch_of
+    g = load("l4")
+    base = batch_of(g)
+    frames = base.frames() * 40
+    b = repack(synth.from_frames(frames), misalign_seed=31)
+    cfg = N.make_cfg(offset=14, checksum=True, l4_mode=mode, classify=N.CLS_LB_HASH, nports=16,
+                     hash_mode=N.HASH_FLOWID)
+    got, exp = _check(dev, oracle, b, cfg, f"l4 mode={mode}")
+    assert (exp["reason"] == N.R_L4_CKSUM).sum() > 1000
+    ctx = N.Context(0, b.n, cfg)
+    ctx.set_host_threads(4)
+    ptrs = (C.c_void_p * b.n)(*[b.arena.ctypes.data + int(o) for o in b.desc[:, 0]])
+    lens = np.ascontiguousarray(b.desc[:, 1], dtype=np.uint32)
+    verdict = np.zeros(b.n, np.uint16)
+    hsh = np.zeros(b.n, np.uint32)
+    ctx.process_host(ptrs, lens.ctypes.data, b.n, verdict=verdict.ctypes.data, hash=hsh.ctypes.data)
+    assert np.array_equal(verdict & 0xFF, exp["reason"]) and np.array_equal(verdict >> 8, exp["port"])
+    assert np.array_equal(hsh, exp["hash"])
+    ctx.close()

@@ -100,7 +100,7 @@ def test_oracle_program_golden(oracle, name):
     c = r["counters"]
     assert c[N.CTR_COUNT] == (exp != INVALID).sum()
     assert c[N.CTR_DROPS] == (exp == INVALID).sum()
-    assert c[N.CTR_REASON + N.NREASON_SLOTS - 1] == (exp == NOMATCH).sum()
+    assert c[N.CTR_REASON + N.reason_slot(N.R_NO_MATCH)] == (exp == NOMATCH).sum()
     assert c[N.CTR_PORT + nout] == (exp >= NOMATCH).sum()
 
 
