@@ -13,7 +13,7 @@ step() {  # name timeout cmd...
 }
 S=${STEPS:-tests,bench,ktrace,pmc,host}
 B="--steps 200 --warmup 20"
-[[ $S == *tests* ]] && step pytest_gpu 900 python -m pytest tests -m gpu -q
+[[ $S == *tests* ]] && step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 [[ $S == *smoke* ]] && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $S == *bench* ]] && step bench 600 python bench.py $B
 [[ $S == *ktrace* ]] && step ktrace 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_ktrace -o run -- python3 bench.py $B --no-cpu

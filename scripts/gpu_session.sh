@@ -12,7 +12,7 @@ run() {  # name timeout cmd...
   return 0
 }
 STEPS=${STEPS:-all}
-[[ $STEPS == *pytest* || $STEPS == all ]] && run pytest_gpu 900 python -m pytest tests -m gpu -x -q
+[[ $STEPS == *pytest* || $STEPS == all ]] && run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 [[ $STEPS == *smoke* || $STEPS == all ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *bench* || $STEPS == all ]] && run bench 600 python bench.py ${BENCH_ARGS:---steps 200 --warmup 20}
 exit 0

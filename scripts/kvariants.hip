@@ -69,7 +69,8 @@ __global__ __launch_bounds__(256) void k_glds(const uint8_t *arena, const uint2 
 }
 
 int main(int argc, char **argv) {
-    const uint32_t n = 1u << 20, NB = 16, nports = 16;
+    const uint32_t n = 1u << 20, nports = 16;
+    const uint32_t NB = argc > 2 ? (uint32_t)atoi(argv[2]) : 16;
     const int iters = argc > 1 ? atoi(argv[1]) : 200;
     // C2 frames: 60-B UDP/IPv4 in 64-B slots
     std::vector<uint8_t> host((size_t)n * 64 + 256, 0);
