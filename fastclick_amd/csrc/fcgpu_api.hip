@@ -202,8 +202,12 @@ static hipEvent_t take_event(fcgpu_ctx *c) {
         c->free_ev.pop_back();
         return e;
     }
+    // timing-only events: no system-scope fence, so recording one does not
+    // write back the launch's dirty L2 lines (which would bill the kernel for
+    // a cache flush the pipeline never asks for; hip_runtime_api.h notes this
+    // flag for timing accuracy)
     hipEvent_t e = nullptr;
-    (void)hipEventCreate(&e);
+    (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
     return e;
 }
 

@@ -588,9 +588,26 @@ __device__ __forceinline__ void l4_stage(const DevCfg &c, const FrameView &f, co
     }
 }
 
+// Header windows are read once per launch: non-temporal (cpol nt = 2) keeps
+// them from evicting the outputs and descriptors from L2/MALL -- 5 % shorter
+// k_rx than the default policy (profiles/r01_kernel_experiments).
+constexpr int kWinCpol = 2;
 __device__ __forceinline__ void glds16(const uint8_t *src, uint8_t *lds) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                     (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+                                     (__attribute__((address_space(3))) void *)lds, 16, 0, kWinCpol);
+}
+
+// Inclusive prefix sum over the 64 lanes of a wave by DPP (gfx9 row shifts
+// within 16-lane rows, then row_bcast:15 / row_bcast:31 across rows): six
+// VALU ops instead of six ds_bpermute round trips.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return x;
 }
 
 __device__ __forceinline__ uint32_t reason_slot(uint32_t r) { return r < 6 ? r : r - 1; }
@@ -612,40 +629,26 @@ constexpr int kPartNone = 0;     // counters only
 constexpr int kPartGlobal = 1;   // + per-tile port histogram for k_scan/k_part (dense perm)
 constexpr int kPartTile = 2;     // + stable partition of each 256-packet tile, in-kernel
 
-// Fused [StripEtherVLANHeader ->] CheckIPHeader/CheckIP6Header -> AggregateHash
-// -> classify over one 256-packet tile; per-tile histogram by wave ballots;
-// counters by sharded atomics; optionally the tile's stable per-output
-// partition (CLASSIFY_EACH_PACKET on a 256-packet PacketBatch).
-template <int CM, bool CK, int PART, bool PROG, bool L4, bool FAST = (CM == FCGPU_CHECK_IP4)>
-__global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[4 * kWave * kWin];
-    __shared__ uint32_t s_cnt[4][kMaxBins];
-    extern __shared__ uint4 s_prog[];           // prog_lds_bytes(cfg) at launch
+// Source of a wave's header-window gather: 4 x (16 frames x 64 B); lane l of
+// instruction k fetches 16-B chunk (l & 3) ^ swizzle of frame 16k + l/4.
+__device__ __forceinline__ const uint8_t *win_src(const uint8_t *arena, uint32_t doff, uint32_t lane, int k) {
+    const uint32_t p = k * 16 + (lane >> 2);
+    const uint32_t poff = __shfl(doff, (int)p);
+    const uint32_t c = (lane & 3) ^ ((p >> 2) & 3);
+    return arena + (poff & ~15u) + c * 16;
+}
+
+// One 256-packet tile once its header window is in LDS: fused
+// [StripEtherVLANHeader ->] CheckIPHeader/CheckIP6Header -> AggregateHash ->
+// classify; per-wave histogram by ballots; counters by sharded atomics;
+// optionally the tile's stable per-output partition (CLASSIFY_EACH_PACKET on a
+// 256-packet PacketBatch).
+template <int CM, bool CK, int PART, bool PROG, bool L4, bool FAST>
+__device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d, const uint8_t *wl,
+                                        uint32_t (*s_cnt)[kMaxBins], const uint4 *sprog) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // one 256-packet tile per workgroup (grid == ntiles). A grid-stride loop
-    // measured slower here: hoisted loop invariants spill around it.
-    const uint32_t tile = blockIdx.x;
     const uint32_t i = tile * kTile + threadIdx.x;
     const bool live = i < A.n;
-    uint2 d = make_uint2(0, 0);
-    if (live) d = A.desc[i];
-
-    // gather: 4 x (16 frames x 64 B) per wave, LDS-DMA, swizzled 16-B chunks
-    uint8_t *wl = s_win + wave * (kWave * kWin);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t p = k * 16 + (lane >> 2);
-        const uint32_t poff = __shfl(d.x, (int)p);
-        const uint32_t c = (lane & 3) ^ ((p >> 2) & 3);
-        glds16(A.arena + (poff & ~15u) + c * 16, wl + k * 1024);
-    }
-    // decision program: the block's LDS copy when it fits (block-uniform)
-    const bool prog_lds = PROG && prog_in_lds(A.cfg);
-    if (prog_lds && threadIdx.x < A.cfg.prog_n) s_prog[threadIdx.x] = A.cfg.prog[threadIdx.x];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (prog_lds) __syncthreads();
-    const uint4 *sprog = prog_lds ? s_prog : nullptr;
-
     FrameView f;
     f.row = wl + lane * kWin;
     f.sw = (lane >> 2) & 3;
@@ -713,12 +716,7 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
                 wpre += w < wave ? c : 0u;
             }
         }
-        uint32_t incl = v;
-#pragma unroll
-        for (int dl = 1; dl < 64; dl <<= 1) {
-            const uint32_t u = __shfl_up(incl, dl);
-            if (lane >= (uint32_t)dl) incl += u;
-        }
+        const uint32_t incl = wave_incl_scan(v);
         const uint32_t start = incl - v + wpre;   // lane b: start of output b for this wave
         uint32_t mine = __shfl(start, (int)(bin & 63));
         if (nb > 64) {   // output 64 (nports == 64): base = sum of outputs 0..63
@@ -727,6 +725,9 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
             const uint32_t s64 = __shfl(incl, 63) + w64;
             if (bin == 64) mine = s64;
         }
+        // stage the tile's permutation in LDS, then write it out coalesced
+        // (a full tile: 4 x 256 B of perm, one dword per lane of wave 0 for
+        // tile_perm) instead of one scattered store per packet
         if (live) {
             const size_t pos = (size_t)tile * kTile + mine + rank;
             if (A.perm) A.perm[pos] = i;
@@ -750,6 +751,32 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
             if (live_n - drops) atomicAdd(&ctr[FCGPU_CTR_COUNT], (unsigned long long)(live_n - drops));
         }
     }
+}
+
+
+// The receive-path kernel: one 256-packet tile per workgroup (grid = ntiles).
+// (Two tiles per workgroup with the second window prefetched into VGPRs
+// while the first is processed measured 10-15 % slower: one resident round
+// of workgroups instead of two loses the natural load/compute skew.)
+template <int CM, bool CK, int PART, bool PROG, bool L4, bool FAST = (CM == FCGPU_CHECK_IP4)>
+__global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[4 * kWave * kWin];
+    __shared__ uint32_t s_cnt[4][kMaxBins];
+    extern __shared__ uint4 s_prog[];           // prog_lds_bytes(cfg) at launch
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t tile = blockIdx.x;
+    const uint32_t i = tile * kTile + threadIdx.x;
+    uint2 d = make_uint2(0, 0);
+    if (i < A.n) d = A.desc[i];
+    uint8_t *wl = s_win + wave * (kWave * kWin);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) glds16(win_src(A.arena, d.x, lane, k), wl + k * 1024);
+    // decision program: the block's LDS copy when it fits (block-uniform)
+    const bool prog_lds = PROG && prog_in_lds(A.cfg);
+    if (prog_lds && threadIdx.x < A.cfg.prog_n) s_prog[threadIdx.x] = A.cfg.prog[threadIdx.x];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (prog_lds) __syncthreads();
+    rx_tile<CM, CK, PART, PROG, L4, FAST>(A, tile, d, wl, s_cnt, prog_lds ? s_prog : nullptr);
 }
 
 // Exclusive scan of one output's per-tile counts (in place) and its total.

@@ -112,8 +112,8 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1, k0, k1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    CK(hipEventCreate(&k0));
-    CK(hipEventCreate(&k1));
+    CK(hipEventCreateWithFlags(&k0, hipEventDisableSystemFence));
+    CK(hipEventCreateWithFlags(&k1, hipEventDisableSystemFence));
 
     RxArgs A{};
     A.n = n;
@@ -122,7 +122,9 @@ int main(int argc, char **argv) {
     A.hash = h;
     A.anno = nullptr;
     A.tilecnt = tilecnt;
-    A.perm = perm;
+    const bool tp = argc > 3 && !strcmp(argv[3], "tp");
+    A.perm = tp ? nullptr : perm;
+    A.tile_perm = tp ? (uint8_t *)perm : nullptr;
     A.tile_count = tc;
     A.ctr = ctr;
     memset(&A.cfg, 0, sizeof(A.cfg));
