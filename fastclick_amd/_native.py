@@ -14,7 +14,7 @@ LIBFCGPU = os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 5
+ABI_VERSION = 6
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
     R_BAD_IP6, R_VLAN_REJECT, R_NO_MATCH, R_L4_PROTO, R_L4_LENGTH, R_L4_CKSUM = range(13)
@@ -94,6 +94,10 @@ def anno_dtype():
     return ANNO_DTYPE
 
 
+FLOW_NONE = 0xFFFFFFFF
+FLOW_FULL = 0xFFFFFFFE
+
+
 class fcgpu_out(C.Structure):
     _fields_ = [
         ("verdict", C.c_void_p),
@@ -105,6 +109,7 @@ class fcgpu_out(C.Structure):
         ("partition", C.c_uint32),
         ("reserved", C.c_uint32),
         ("tile_perm", C.c_void_p),
+        ("flowid", C.c_void_p),
     ]
 
 
@@ -134,6 +139,9 @@ FCGPU_SYMBOLS = {
     "fcgpu_set_program": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(fcgpu_step), C.c_uint32,
                                     C.c_int32]),
     "fcgpu_set_host_threads": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "fcgpu_flow_enable": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "fcgpu_flow_reset": (C.c_int, [C.c_void_p]),
+    "fcgpu_flow_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "fcgpu_host_alloc": (C.c_void_p, [C.c_size_t]),
     "fcgpu_host_free": (None, [C.c_void_p]),
     "fcgpu_read_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
@@ -260,16 +268,18 @@ class Context:
         self.cfg = cfg
 
     def process(self, arena_ptr, desc_ptr, n, *, verdict=0, hash=0, anno=0, perm=0,
-                port_start=0, tile_count=0, partition=PART_GLOBAL, tile_perm=0, stream=0):
+                port_start=0, tile_count=0, partition=PART_GLOBAL, tile_perm=0, flowid=0, stream=0):
         out = fcgpu_out(verdict or None, hash or None, anno or None, perm or None,
-                        port_start or None, tile_count or None, partition, 0, tile_perm or None)
+                        port_start or None, tile_count or None, partition, 0, tile_perm or None,
+                        flowid or None)
         self._chk(self.lib.fcgpu_process(self.h, arena_ptr, desc_ptr, n, C.byref(out),
                                          stream or None), "fcgpu_process")
 
     def process_host(self, frames, lens_ptr, n, *, verdict=0, hash=0, anno=0, perm=0,
-                     port_start=0, tile_count=0, partition=PART_GLOBAL, tile_perm=0):
+                     port_start=0, tile_count=0, partition=PART_GLOBAL, tile_perm=0, flowid=0):
         out = fcgpu_out(verdict or None, hash or None, anno or None, perm or None,
-                        port_start or None, tile_count or None, partition, 0, tile_perm or None)
+                        port_start or None, tile_count or None, partition, 0, tile_perm or None,
+                        flowid or None)
         self._chk(self.lib.fcgpu_process_host(self.h, frames, lens_ptr, n, C.byref(out)),
                   "fcgpu_process_host")
 
@@ -280,6 +290,18 @@ class Context:
             arr[i] = st if isinstance(st, fcgpu_step) else fcgpu_step(*[int(x) for x in st])
         self._chk(self.lib.fcgpu_set_program(self.h, kind, arr, len(steps), output_everything),
                   "fcgpu_set_program")
+
+    def flow_enable(self, max_flows: int):
+        """Device flow table (FlowIPManagerHMP semantics); 0 disables it."""
+        self._chk(self.lib.fcgpu_flow_enable(self.h, max_flows), "fcgpu_flow_enable")
+
+    def flow_reset(self):
+        self._chk(self.lib.fcgpu_flow_reset(self.h), "fcgpu_flow_reset")
+
+    def flow_count(self) -> int:
+        v = C.c_uint32()
+        self._chk(self.lib.fcgpu_flow_count(self.h, C.byref(v)), "fcgpu_flow_count")
+        return v.value
 
     def set_host_threads(self, n: int):
         self._chk(self.lib.fcgpu_set_host_threads(self.h, n), "fcgpu_set_host_threads")

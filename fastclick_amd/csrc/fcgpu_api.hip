@@ -15,6 +15,7 @@
 #include <string.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <algorithm>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -23,6 +24,7 @@
 #include <vector>
 
 #include "fcgpu_device.hh"
+#include "fcgpu_flow.hh"
 
 #pragma clang diagnostic ignored "-Wunused-result"
 #pragma clang diagnostic ignored "-Wunused-value"
@@ -163,10 +165,14 @@ struct fcgpu_ctx {
     uint16_t *d_htc = nullptr;
     uint8_t *d_htp = nullptr;
     fcgpu_anno *d_hanno = nullptr;
+    uint32_t *d_hflow = nullptr;
     // pipelined host path (FCGPU_PART_TILE / no whole-batch partition)
     HostSlot slot[kSlots];
     uint32_t slot_cap = 0;
     Pool pool;
+    // flow table (fcgpu_flow_enable)
+    uint32_t max_flows = 0, flow_slots = 0, flow_words = 0;
+    FlowArgs fl{};            // device pointers; fl.slots == nullptr: disabled
     // timing
     bool timing = false;
     std::vector<EvPair> pending;
@@ -213,33 +219,36 @@ static hipEvent_t take_event(fcgpu_ctx *c) {
 
 // ev0/ev1 non-null: hipExtLaunchKernelGGL records them around the dispatch
 // itself (timestamps of the kernel, not of the stream around it).
-template <int CM, bool CK, int PART, bool PROG, bool L4>
+template <int CM, bool CK, int PART, bool PROG, bool L4, bool FLOW = false>
 static void launch_rx(const RxArgs &a, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     const size_t lds = PROG ? prog_lds_bytes(a.cfg) : 0;
     if (ev0)
-        hipExtLaunchKernelGGL((k_rx<CM, CK, PART, PROG, L4>), dim3(a.ntiles), dim3(kTile), lds, s, ev0, ev1, 0, a);
+        hipExtLaunchKernelGGL((k_rx<CM, CK, PART, PROG, L4, FLOW>), dim3(a.ntiles), dim3(kTile), lds, s, ev0, ev1,
+                              0, a);
     else
-        hipLaunchKernelGGL((k_rx<CM, CK, PART, PROG, L4>), dim3(a.ntiles), dim3(kTile), lds, s, a);
+        hipLaunchKernelGGL((k_rx<CM, CK, PART, PROG, L4, FLOW>), dim3(a.ntiles), dim3(kTile), lds, s, a);
 }
 
-// L4 (CheckUDPHeader/CheckTCPHeader) exists only for the IPv4 check modes
-// (fcgpu_configure rejects it with CHECK_AUTO).
+// IPv4 check modes: L4 (CheckUDPHeader/CheckTCPHeader) and the flow table
+// exist only there (fcgpu_configure / fcgpu_process reject them with CHECK_AUTO).
+template <int CM, bool CK, int PART, bool PROG>
+static void launch_rx_ip4(const RxArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    const bool l4 = a.cfg.l4_mode != FCGPU_L4_NONE, flow = a.fl.slots != nullptr;
+    if (flow) {
+        if (l4) launch_rx<CM, CK, PART, PROG, true, true>(a, s, e0, e1);
+        else launch_rx<CM, CK, PART, PROG, false, true>(a, s, e0, e1);
+    } else {
+        if (l4) launch_rx<CM, CK, PART, PROG, true>(a, s, e0, e1);
+        else launch_rx<CM, CK, PART, PROG, false>(a, s, e0, e1);
+    }
+}
+
 template <int PART, bool PROG>
 static void launch_rx_part(uint32_t cm, bool ck, const RxArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    const bool l4 = a.cfg.l4_mode != FCGPU_L4_NONE;
     switch (cm * 2 + (ck ? 1 : 0)) {
-    case 0:
-        if (l4) launch_rx<FCGPU_CHECK_IP4, false, PART, PROG, true>(a, s, e0, e1);
-        else launch_rx<FCGPU_CHECK_IP4, false, PART, PROG, false>(a, s, e0, e1);
-        break;
-    case 1:
-        if (l4) launch_rx<FCGPU_CHECK_IP4, true, PART, PROG, true>(a, s, e0, e1);
-        else launch_rx<FCGPU_CHECK_IP4, true, PART, PROG, false>(a, s, e0, e1);
-        break;
-    case 2: case 3:
-        if (l4) launch_rx<FCGPU_MARK_IP4, false, PART, PROG, true>(a, s, e0, e1);
-        else launch_rx<FCGPU_MARK_IP4, false, PART, PROG, false>(a, s, e0, e1);
-        break;
+    case 0: launch_rx_ip4<FCGPU_CHECK_IP4, false, PART, PROG>(a, s, e0, e1); break;
+    case 1: launch_rx_ip4<FCGPU_CHECK_IP4, true, PART, PROG>(a, s, e0, e1); break;
+    case 2: case 3: launch_rx_ip4<FCGPU_MARK_IP4, false, PART, PROG>(a, s, e0, e1); break;
     case 4: launch_rx<FCGPU_CHECK_AUTO, false, PART, PROG, false>(a, s, e0, e1); break;
     default: launch_rx<FCGPU_CHECK_AUTO, true, PART, PROG, false>(a, s, e0, e1); break;
     }
@@ -325,10 +334,13 @@ static int process_host_whole(fcgpu_ctx *c, const uint8_t *const *frames, const 
     d.partition = h->partition;
     d.reserved = 0;
     d.tile_perm = h->tile_perm ? c->d_htp : nullptr;
+    if (h->flowid && !c->d_hflow) HIPCHK(c, hipMalloc(&c->d_hflow, sizeof(uint32_t) * c->max_batch));
+    d.flowid = h->flowid ? c->d_hflow : nullptr;
     int rc = fcgpu_process(c, c->d_arena, c->d_desc, n, &d, s);
     if (rc != FCGPU_OK) return rc;
     if (h->verdict) HIPCHK(c, hipMemcpyAsync(h->verdict, d.verdict, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, s));
     if (h->hash) HIPCHK(c, hipMemcpyAsync(h->hash, d.hash, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
+    if (h->flowid) HIPCHK(c, hipMemcpyAsync(h->flowid, d.flowid, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
     if (h->anno) HIPCHK(c, hipMemcpyAsync(h->anno, d.anno, sizeof(fcgpu_anno) * n, hipMemcpyDeviceToHost, s));
     if (h->perm) HIPCHK(c, hipMemcpyAsync(h->perm, d.perm, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
     if (h->tile_perm) HIPCHK(c, hipMemcpyAsync(h->tile_perm, d.tile_perm, n, hipMemcpyDeviceToHost, s));
@@ -372,6 +384,77 @@ void fcgpu_default_cfg(fcgpu_cfg *c) {
 
 const char *fcgpu_last_error(fcgpu_ctx *ctx) { return ctx ? ctx->err.c_str() : g_open_err.c_str(); }
 
+static void flow_free(fcgpu_ctx *c) {
+    FlowArgs &F = c->fl;
+    for (void *p : {(void *)F.slots, (void *)F.claim, (void *)F.first, (void *)F.miss_pkt, (void *)F.miss_key,
+                    (void *)F.miss_slot, (void *)F.miss_first, (void *)F.bitmap, (void *)F.wordpre, (void *)F.state})
+        if (p) hipFree(p);
+    F = FlowArgs{};
+    c->max_flows = c->flow_slots = c->flow_words = 0;
+}
+
+// Empty table, IDs from 0 (synchronous).
+static int flow_clear(fcgpu_ctx *c) {
+    FlowArgs &F = c->fl;
+    HIPCHK(c, hipMemset(F.slots, 0, sizeof(uint4) * c->flow_slots));
+    HIPCHK(c, hipMemset(F.claim, 0, sizeof(uint32_t) * c->flow_slots));
+    HIPCHK(c, hipMemset(F.first, 0xff, sizeof(uint32_t) * c->flow_slots));
+    HIPCHK(c, hipMemset(F.bitmap, 0, sizeof(uint32_t) * 2 * c->flow_words));
+    uint32_t st[16] = {};
+    st[kFsWords] = c->flow_words;
+    HIPCHK(c, hipMemcpy(F.state, st, sizeof(st), hipMemcpyHostToDevice));
+    return FCGPU_OK;
+}
+
+int fcgpu_flow_enable(fcgpu_ctx *c, uint32_t max_flows) {
+    if (!c) return FCGPU_EINVAL;
+    if (max_flows > FCGPU_MAX_FLOWS) return fail(c, FCGPU_EINVAL, "max_flows above FCGPU_MAX_FLOWS");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());
+    flow_free(c);
+    if (max_flows == 0) return FCGPU_OK;
+    // at most max_flows IDs plus one batch of FULL markers (the batch that
+    // fills the table): keep the load at or under 1/2
+    uint32_t slots = 1024;
+    while (slots < 2 * (max_flows + c->max_batch)) slots <<= 1;
+    const uint32_t words = (c->max_batch + 31) / 32 + 1;
+    FlowArgs &F = c->fl;
+    HIPCHK(c, hipMalloc(&F.slots, sizeof(uint4) * slots));
+    HIPCHK(c, hipMalloc(&F.claim, sizeof(uint32_t) * slots));
+    HIPCHK(c, hipMalloc(&F.first, sizeof(uint32_t) * slots));
+    HIPCHK(c, hipMalloc(&F.miss_pkt, sizeof(uint32_t) * c->max_batch));
+    HIPCHK(c, hipMalloc(&F.miss_key, sizeof(uint4) * c->max_batch));
+    HIPCHK(c, hipMalloc(&F.miss_slot, sizeof(uint32_t) * c->max_batch));
+    HIPCHK(c, hipMalloc(&F.miss_first, sizeof(uint32_t) * c->max_batch));
+    HIPCHK(c, hipMalloc(&F.bitmap, sizeof(uint32_t) * 2 * words));
+    HIPCHK(c, hipMalloc(&F.wordpre, sizeof(uint32_t) * words));
+    HIPCHK(c, hipMalloc(&F.state, sizeof(uint32_t) * 16));
+    F.mask = slots - 1;
+    F.max_flows = max_flows;
+    c->max_flows = max_flows;
+    c->flow_slots = slots;
+    c->flow_words = words;
+    return flow_clear(c);
+}
+
+int fcgpu_flow_reset(fcgpu_ctx *c) {
+    if (!c) return FCGPU_EINVAL;
+    if (!c->fl.slots) return FCGPU_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());
+    return flow_clear(c);
+}
+
+int fcgpu_flow_count(fcgpu_ctx *c, uint32_t *count) {
+    if (!c || !count) return FCGPU_EINVAL;
+    *count = 0;
+    if (!c->fl.slots) return FCGPU_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(count, c->fl.state + kFsNext, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return FCGPU_OK;
+}
+
 void fcgpu_close(fcgpu_ctx *c) {
     if (!c) return;
     if (c->device >= 0) {
@@ -393,6 +476,8 @@ void fcgpu_close(fcgpu_ctx *c) {
         hipFree(c->d_hanno);
         hipFree(c->d_htc);
         hipFree(c->d_htp);
+        hipFree(c->d_hflow);
+        flow_free(c);
         hipHostFree(c->h_arena);
         hipHostFree(c->h_desc);
         if (c->stream) hipStreamDestroy(c->stream);
@@ -528,6 +613,10 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     if (tile) a.perm = o->perm;
     a.ctr = c->d_ctr;
     a.cfg = c->dcfg;
+    a.fl = c->fl;
+    a.fl.flowid = o->flowid;
+    if (a.fl.slots && c->cfg.check_mode == FCGPU_CHECK_AUTO)
+        return fail(c, FCGPU_EINVAL, "the flow table needs an IPv4 check mode (CHECK_IP4 or MARK_IP4)");
 
     EvPair ev[3];
     if (c->timing)
@@ -536,6 +625,14 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, a, s, c->timing ? ev[0].a : nullptr,
                   c->timing ? ev[0].b : nullptr);
     HIPCHK(c, hipGetLastError());
+    if (a.fl.slots) {   // the batch's new flows (fcgpu_flow.hh)
+        const uint32_t g = std::min<uint32_t>((n + kFlowBlock - 1) / kFlowBlock, 1024);
+        hipLaunchKernelGGL(k_flow_claim, dim3(g), dim3(kFlowBlock), 0, s, a.fl);
+        hipLaunchKernelGGL(k_flow_mark, dim3(g), dim3(kFlowBlock), 0, s, a.fl);
+        hipLaunchKernelGGL(k_flow_scan, dim3(1), dim3(1024), 0, s, a.fl, (n + 31) / 32);
+        hipLaunchKernelGGL(k_flow_assign, dim3(g), dim3(kFlowBlock), 0, s, a.fl);
+        HIPCHK(c, hipGetLastError());
+    }
     if (want_global) {
         if (c->timing) hipEventRecord(ev[1].a, s);
         hipLaunchKernelGGL(k_scan, dim3(nports + 1), dim3(1024), 0, s, c->d_tilecnt, ntiles, c->d_totals);
@@ -703,6 +800,7 @@ static int process_host_pipelined(fcgpu_ctx *c, const uint8_t *const *frames, co
         d.partition = h->partition;
         d.reserved = 0;
         d.tile_perm = h->tile_perm ? sl.d_tp : nullptr;
+        d.flowid = nullptr;   // flow tables run the whole batch in order (process_host_whole)
         int rc = fcgpu_process(c, sl.d_arena, sl.d_desc, cn, &d, s);
         if (rc != FCGPU_OK) return rc;
         const uint32_t tb = base / kTile, nt = (cn + kTile - 1) / kTile;
@@ -737,7 +835,8 @@ int fcgpu_process_host(fcgpu_ctx *c, const uint8_t *const *frames, const uint32_
     if (n == 0) return FCGPU_OK;
     if (h->partition > FCGPU_PART_TILE) return fail(c, FCGPU_EINVAL, "bad partition mode");
     HIPCHK(c, hipSetDevice(c->device));
-    if (h->partition == FCGPU_PART_GLOBAL && (h->perm || h->port_start))
+    // a flow table assigns IDs in packet order: one pass on one stream
+    if ((h->partition == FCGPU_PART_GLOBAL && (h->perm || h->port_start)) || c->fl.slots)
         return process_host_whole(c, frames, lens, n, h);
     if (h->partition == FCGPU_PART_TILE && ((h->perm || h->tile_perm) != (h->tile_count != nullptr)))
         return fail(c, FCGPU_EINVAL, "FCGPU_PART_TILE needs tile_count and perm and/or tile_perm");

@@ -52,6 +52,30 @@ struct DevCfg {
 // w = (u16)yes | (u16)no << 16 (signed 16-bit jumps).
 constexpr int32_t kProgUnmatched = 0x7fff;
 
+// Flow table state (fcgpu_flow_enable). Slot = {saddr, daddr, ports, tag} with
+// tag = proto | (flow id + 1) << 8; tag 0 = empty. Linear probing, never more
+// than half full (max_flows <= slots / 2), no deletions.
+struct FlowArgs {
+    uint4 *slots;
+    uint32_t mask;           // slots - 1
+    uint32_t max_flows;
+    uint32_t *claim;         // [slots] miss entry + 1 claiming a slot this batch
+    uint32_t *first;         // [slots] min packet index of the claiming flow
+    uint32_t *miss_n;        // misses appended by k_rx this batch
+    uint32_t *miss_pkt;      // [max_batch]
+    uint4 *miss_key;         // [max_batch]
+    uint32_t *miss_slot;     // [max_batch]
+    uint32_t *miss_first;    // [max_batch]
+    uint32_t *bitmap;        // [2][words] first-appearance bits, by batch parity
+    uint32_t *wordpre;       // [words] exclusive popcount prefix
+    uint32_t *state;         // kFs* words below
+    uint32_t *flowid;        // [n] output (may be null)
+};
+constexpr uint32_t kFsNext = 0, kFsBase = 1, kFsMiss = 2, kFsPar = 3, kFsPrevWords = 4, kFsSnap = 5,
+                   kFsWords = 8;
+constexpr uint32_t kFlowMiss = 0xfffffffdu;
+constexpr uint32_t kSlotNone = 0xffffffffu;
+
 struct RxArgs {
     const uint8_t *arena;
     const uint2 *desc;
@@ -65,6 +89,7 @@ struct RxArgs {
     uint16_t *tile_count;  // [ntiles][nports+1] (kPartTile)
     uint8_t *tile_perm;    // [n] tile-local partition (kPartTile)
     unsigned long long *ctr;   // [FCGPU_CTR_SHARDS][FCGPU_NCOUNTERS]
+    FlowArgs fl;               // FLOW instances only
     DevCfg cfg;
 };
 
@@ -638,12 +663,75 @@ __device__ __forceinline__ const uint8_t *win_src(const uint8_t *arena, uint32_t
     return arena + (poff & ~15u) + c * 16;
 }
 
+// ---- flow table lookup (FlowIPManagerHMP::process, flowipmanagerhmp.cc:96-126) ----
+__device__ __forceinline__ uint32_t flow_slot_hash(const uint4 &k) {
+    // placement only (any mix works; IDs do not depend on it): murmur3 fmix32
+    uint32_t h = k.x * 0x9E3779B1u ^ rotl32(k.y, 13) * 0x85EBCA77u ^ rotl32(k.z, 7) * 0xC2B2AE3Du ^ k.w;
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+    return h;
+}
+__device__ __forceinline__ bool flow_key_eq(const uint4 &s, const uint4 &k) {
+    return s.x == k.x && s.y == k.y && s.z == k.z && (s.w & 0xffu) == k.w;
+}
+// tag = proto | (id + 1) << 8; kTagFull marks a flow that arrived when the
+// table was full (it stays FCGPU_FLOW_FULL: no timeouts, as in HMP)
+constexpr uint32_t kTagFull = 0xffffffu;
+__device__ __forceinline__ uint32_t flow_tag_id(uint32_t tag) {
+    return (tag >> 8) == kTagFull ? FCGPU_FLOW_FULL : (tag >> 8) - 1u;
+}
+// IPFlow5ID(p) (lib/ipflowid.cc:29-46,91-94): saddr, daddr, the first L4 word
+// (sport, dport; 0 for non-first fragments), ip_p.
+__device__ __forceinline__ uint4 flow_key(const FrameView &f, const fcgpu_anno &an) {
+    uint4 k;
+    k.x = f.rd32(an.nh + 12);
+    k.y = f.rd32(an.nh + 16);
+    const uint32_t w1 = f.rd32(an.nh + 4);          // id, frag offset
+    const uint32_t w2 = f.rd32(an.nh + 8);          // ttl, proto, sum
+    k.z = (bswap16(w1 >> 16) & 0x1fff) == 0 ? f.rd32(an.th) : 0u;
+    k.w = (w2 >> 8) & 0xffu;
+    return k;
+}
+
+// Packets past the checks get the ID of their flow, or a miss entry for the
+// batch's new-flow pass (k_flow_*) -- one wave-aggregated atomic per wave.
+__device__ __forceinline__ void flow_stage(const FlowArgs &F, const FrameView &f, bool live, uint32_t i,
+                                           const PktResult &r) {
+    const bool want = live && r.an.ipver == 4 && (r.reason == FCGPU_R_OK || r.reason == FCGPU_R_NO_MATCH);
+    uint32_t id = FCGPU_FLOW_NONE;
+    uint4 k = make_uint4(0, 0, 0, 0);
+    if (want) {
+        k = flow_key(f, r.an);
+        uint32_t pos = flow_slot_hash(k) & F.mask;
+        id = kFlowMiss;
+        for (uint32_t p = 0; p <= F.mask; ++p) {
+            const uint4 sl = F.slots[pos];
+            if (sl.w == 0) break;
+            if (flow_key_eq(sl, k)) { id = flow_tag_id(sl.w); break; }
+            pos = (pos + 1) & F.mask;
+        }
+    }
+    const uint64_t mm = __ballot(id == kFlowMiss);
+    if (mm) {
+        const uint32_t lane = threadIdx.x & 63;
+        const uint32_t lead = (uint32_t)__builtin_ctzll(mm);
+        uint32_t base = 0;
+        if (lane == lead) base = atomicAdd(&F.state[kFsMiss], (uint32_t)__popcll(mm));
+        base = __shfl(base, (int)lead);
+        if (id == kFlowMiss) {
+            const uint32_t e = base + (uint32_t)__popcll(mm & ((1ull << lane) - 1ull));
+            F.miss_pkt[e] = i;
+            F.miss_key[e] = k;
+        }
+    }
+    if (live && F.flowid) F.flowid[i] = id;
+}
+
 // One 256-packet tile once its header window is in LDS: fused
 // [StripEtherVLANHeader ->] CheckIPHeader/CheckIP6Header -> AggregateHash ->
 // classify; per-wave histogram by ballots; counters by sharded atomics;
 // optionally the tile's stable per-output partition (CLASSIFY_EACH_PACKET on a
 // 256-packet PacketBatch).
-template <int CM, bool CK, int PART, bool PROG, bool L4, bool FAST>
+template <int CM, bool CK, int PART, bool PROG, bool L4, bool FAST, bool FLOW>
 __device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d, const uint8_t *wl,
                                         uint32_t (*s_cnt)[kMaxBins], const uint4 *sprog) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -671,6 +759,7 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d,
         process_packet<CM, CK, PROG>(A.cfg, f, d.y, r, sprog);
     }
     if (L4) l4_stage(A.cfg, f, A.arena + d.x, live, r);
+    if (FLOW) flow_stage(A.fl, f, live, i, r);
     if (live) {
         if (A.verdict) A.verdict[i] = (uint16_t)(r.reason | (r.port << 8));
         if (A.hash) A.hash[i] = r.hash;
@@ -758,7 +847,7 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d,
 // (Two tiles per workgroup with the second window prefetched into VGPRs
 // while the first is processed measured 10-15 % slower: one resident round
 // of workgroups instead of two loses the natural load/compute skew.)
-template <int CM, bool CK, int PART, bool PROG, bool L4, bool FAST = (CM == FCGPU_CHECK_IP4)>
+template <int CM, bool CK, int PART, bool PROG, bool L4, bool FLOW = false, bool FAST = (CM == FCGPU_CHECK_IP4)>
 __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4 * kWave * kWin];
     __shared__ uint32_t s_cnt[4][kMaxBins];
@@ -776,7 +865,7 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
     if (prog_lds && threadIdx.x < A.cfg.prog_n) s_prog[threadIdx.x] = A.cfg.prog[threadIdx.x];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (prog_lds) __syncthreads();
-    rx_tile<CM, CK, PART, PROG, L4, FAST>(A, tile, d, wl, s_cnt, prog_lds ? s_prog : nullptr);
+    rx_tile<CM, CK, PART, PROG, L4, FAST, FLOW>(A, tile, d, wl, s_cnt, prog_lds ? s_prog : nullptr);
 }
 
 // Exclusive scan of one output's per-tile counts (in place) and its total.

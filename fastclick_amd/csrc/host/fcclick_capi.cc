@@ -33,6 +33,7 @@ class Sink : public Element {
                 if (_r->out_len) _r->out_len[i] = p->length();
                 if (_r->out_nh) _r->out_nh[i] = p->network_header_offset();
                 if (_r->out_paint) _r->out_paint[i] = p->anno_u8(PAINT_ANNO_OFFSET);
+                if (_r->out_flow) _r->out_flow[i] = p->anno_u32(28);
             }
             ++*_seq;
             ++cnt;
@@ -165,7 +166,8 @@ extern "C" int fcclick_run(const char *conf, const uint8_t *arena, const uint32_
         if (res->out_batches) *res->out_batches = nbatch;
         if (res->handlers && res->handlers_cap) {
             std::string h;
-            for (const char *name : {"count", "drops", "drop_details", "port_counts", "error"})
+            for (const char *name : {"count", "drops", "drop_details", "port_counts", "flow_count", "flow_drops",
+                                     "error"})
                 h += std::string(name) + "=" + el->read_handler(name) + "\n";
             snprintf(res->handlers, res->handlers_cap, "%s", h.c_str());
         }

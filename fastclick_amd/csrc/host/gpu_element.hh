@@ -26,10 +26,18 @@
 //     behind the IPv4 check (MODE CHECK or MARK); their drops join output N
 //   COLOR (PAINT annotation on every packet)  -- IPInputCombo (with OFFSET 14,
 //     CHECKSUM true, STRIP true and no invalid output: ipinputcombo.cc:65-141)
+//   FLOW_CAPACITY n, FLOWID_ANNO o (default 28)
+//                                            -- FlowIPManagerHMP (CAPACITY) behind the
+//     checks: each checked IPv4 packet gets its flow's ID (IPFlow5ID, IDs in
+//     order of first appearance, elements/research/flowipmanagerhmp.cc:96-126)
+//     in the 4-byte annotation at FLOWID_ANNO; a new flow beyond the capacity
+//     is killed (as the IMP managers do when their flow stack is empty). Output
+//     batches are the classifier's, not split at flow changes.
 //   MODE CHECK|MARK|AUTO, HASH NONE|FLOWID|FLOW5ID, STRIP, BATCH, DEVICE,
 //   PARTITION TILE (default: each 256-packet tile classified as one batch, one
 //   fused launch) | GLOBAL (the whole staged batch as one, three launches)
-// Handlers: count, drops, drop_details (DETAILS true), port_counts.
+// Handlers: count, drops, drop_details (DETAILS true), port_counts,
+// flow_count, flow_drops.
 //
 // Packets are parked until BATCH packets are staged (MinBatch pattern,
 // elements/standard/minbatch.cc:57-76) or flush() is called. GPU/runtime
@@ -166,6 +174,12 @@ class GPUIPCheckClassify : public Element {
                     if (_cfg.nbad6 >= FCGPU_MAX_ADDRS) return err(errh, "BADADDRS: too many addresses");
                     memcpy(_cfg.bad6[_cfg.nbad6++], a, 16);
                 }
+            } else if (k == "FLOW_CAPACITY") {
+                if (!parse_int(v, n) || n < 0 || n > (long)FCGPU_MAX_FLOWS) return err(errh, "bad FLOW_CAPACITY");
+                _flow_cap = (uint32_t)n;
+            } else if (k == "FLOWID_ANNO") {
+                if (!parse_int(v, n) || n < 0 || n > ANNO_SIZE - 4) return err(errh, "bad FLOWID_ANNO");
+                _flow_anno = (int)n;
             } else if (k == "PROCESS_EH") {
                 if (!parse_bool(v, b)) return err(errh, "PROCESS_EH expects true/false");
                 _cfg.process_eh = b;
@@ -178,6 +192,8 @@ class GPUIPCheckClassify : public Element {
         if (!strip_set) _strip = (_cfg.check_mode == FCGPU_CHECK_AUTO);
         if (_cfg.l4_mode != FCGPU_L4_NONE && _cfg.check_mode == FCGPU_CHECK_AUTO)
             return err(errh, "L4 needs MODE CHECK or MARK");
+        if (_flow_cap && _cfg.check_mode == FCGPU_CHECK_AUTO)
+            return err(errh, "FLOW_CAPACITY needs MODE CHECK or MARK");
         if (_cfg.classify == FCGPU_CLS_PROGRAM) {
             if (_prog.output_everything >= (int32_t)_cfg.nports && _prog.output_everything != 0x7fff)
                 return err(errh, "PROGRAM sends everything to a missing output");
@@ -200,6 +216,11 @@ class GPUIPCheckClassify : public Element {
             rc = fcgpu_set_program(_ctx, _prog_kind, _prog.steps.data(), (uint32_t)_prog.steps.size(),
                                    _prog.output_everything);
             if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_set_program: ") + fcgpu_last_error(_ctx));
+        }
+        if (_flow_cap) {
+            rc = fcgpu_flow_enable(_ctx, _flow_cap);
+            if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_flow_enable: ") + fcgpu_last_error(_ctx));
+            _flowid.resize(_cap);
         }
         _pkts.reserve(_cap);
         _frames.reserve(_cap);
@@ -244,7 +265,12 @@ class GPUIPCheckClassify : public Element {
             }
         } else if (h == "port_counts") {
             for (uint32_t p = 0; p <= _cfg.nports; ++p) s << (p ? " " : "") << c[FCGPU_CTR_PORT + p];
-        } else if (h == "error") s << _error;
+        } else if (h == "flow_count") {
+            uint32_t f = 0;
+            if (_ctx) fcgpu_flow_count(_ctx, &f);
+            s << f;
+        } else if (h == "flow_drops") s << _flow_drops;
+        else if (h == "error") s << _error;
         return s.str();
     }
 
@@ -262,7 +288,8 @@ class GPUIPCheckClassify : public Element {
             _frames[i] = _pkts[i]->data();
             _lens[i] = _pkts[i]->length();
         }
-        fcgpu_out o;
+        fcgpu_out o{};
+        o.flowid = _flow_cap ? _flowid.data() : nullptr;
         o.verdict = _verdict.data();
         o.hash = _hash.data();
         o.anno = _anno.data();
@@ -297,6 +324,8 @@ class GPUIPCheckClassify : public Element {
                 else p->set_anno_u32(DST_IP_ANNO_OFFSET, a.dst_ip);
                 if (hashing && reason <= FCGPU_R_NO_MATCH)   // AggregateHash (not after an L4 drop)
                     p->set_anno_u32(AGGREGATE_ANNO_OFFSET, _hash[i]);
+                if (_flow_cap && _flowid[i] != FCGPU_FLOW_NONE && _flowid[i] != FCGPU_FLOW_FULL)
+                    p->set_anno_u32(_flow_anno, _flowid[i]);
                 if (_strip) p->pull(a.nh);
             } else {
                 if (!_warned || _verbose) {
@@ -334,14 +363,22 @@ class GPUIPCheckClassify : public Element {
     // link packets idx(s) .. idx(e-1) into PacketBatches of <= MAX_BATCH_SIZE
     template <class Idx>
     void emit_run(uint32_t port, uint32_t s, uint32_t e, Idx idx) {
-        if (port == _cfg.nports && _cfg.classify == FCGPU_CLS_PROGRAM) {
+        const bool nomatch = port == _cfg.nports && _cfg.classify == FCGPU_CLS_PROGRAM;
+        if (nomatch || _flow_cap) {
             // the last slot mixes invalid packets (output N) and packets no
-            // rule matched (killed); keep input order for the former
+            // rule matched (killed); a full flow table kills new flows. Keep
+            // input order for the rest.
             uint32_t w = s;
             for (uint32_t j = s; j < e; ++j) {
                 const uint32_t i = idx(j);
-                if ((_verdict[i] & 0xff) == FCGPU_R_NO_MATCH) _pkts[i]->kill();
-                else _keep[w++ - s] = i;
+                if (nomatch && (_verdict[i] & 0xff) == FCGPU_R_NO_MATCH) {
+                    _pkts[i]->kill();
+                } else if (_flow_cap && _flowid[i] == FCGPU_FLOW_FULL) {
+                    ++_flow_drops;
+                    _pkts[i]->kill();
+                } else {
+                    _keep[w++ - s] = i;
+                }
             }
             emit_list(port, w - s);
             return;
@@ -377,6 +414,10 @@ class GPUIPCheckClassify : public Element {
     ParsedProgram _prog;
     uint32_t _prog_kind = FCGPU_PROG_IPFILTER;
     int _color = -1;
+    uint32_t _flow_cap = 0;
+    int _flow_anno = 28;
+    uint64_t _flow_drops = 0;
+    std::vector<uint32_t> _flowid;
     std::vector<uint32_t> _keep;
     fcgpu_cfg _cfg;
     fcgpu_ctx *_ctx = nullptr;

@@ -35,7 +35,7 @@ class DeviceBatch:
 
 class DeviceOutputs:
     def __init__(self, n, nports, device="cuda", *, verdict=True, hash=True, anno=False,
-                 perm=False, port_start=False, partition=N.PART_GLOBAL, tile_perm=False):
+                 perm=False, port_start=False, partition=N.PART_GLOBAL, tile_perm=False, flowid=False):
         torch = _torch()
         self.n = n
         self.nports = nports
@@ -43,6 +43,7 @@ class DeviceOutputs:
         mk = lambda k, dt: torch.empty(k, dtype=dt, device=device)  # noqa: E731
         self.verdict = mk(n, torch.int16) if verdict else None
         self.hash = mk(n, torch.int32) if hash else None
+        self.flowid = mk(n, torch.int32) if flowid else None
         self.anno = mk(n * 16, torch.uint8) if anno else None
         tile = partition == N.PART_TILE
         self.perm = mk(n, torch.int32) if perm else None
@@ -56,7 +57,7 @@ class DeviceOutputs:
         return dict(verdict=p(self.verdict), hash=p(self.hash), anno=p(self.anno),
                     perm=p(self.perm), port_start=p(self.port_start),
                     tile_count=p(self.tile_count), partition=self.partition,
-                    tile_perm=p(self.tile_perm))
+                    tile_perm=p(self.tile_perm), flowid=p(self.flowid))
 
     def numpy(self):
         out = {}
@@ -67,6 +68,8 @@ class DeviceOutputs:
             out["port"] = (v >> 8).astype(np.uint8)
         if self.hash is not None:
             out["hash"] = self.hash.cpu().numpy().view(np.uint32)
+        if self.flowid is not None:
+            out["flowid"] = self.flowid.cpu().numpy().view(np.uint32)
         if self.anno is not None:
             out["anno"] = self.anno.cpu().numpy().view(N.anno_dtype())
         if self.perm is not None:
@@ -90,22 +93,39 @@ def run_device(ctx: N.Context, dbatch: DeviceBatch, outs: DeviceOutputs, stream=
 
 def process_batch(batch, cfg, *, anno=True, perm=True, device_index=0, partition=N.PART_GLOBAL,
                   program=None):
-    """Upload a host Batch, run the device path once, return numpy results and
-    the counter vector. Convenience for tests and smoke(). program: optional
-    (kind, steps, output_everything) for CLS_PROGRAM (fcgpu_set_program)."""
+    """One batch on a fresh context (see process_batches)."""
+    return process_batches([batch], cfg, anno=anno, perm=perm, device_index=device_index,
+                           partition=partition, program=program)[0]
+
+
+def process_batches(batches, cfg, *, anno=True, perm=True, device_index=0, partition=N.PART_GLOBAL,
+                    program=None, max_flows=0):
+    """Upload host Batches, run the device path over them in order on one
+    context, return per-batch numpy results and the running counter vector.
+    Convenience for tests and smoke(). program: optional (kind, steps,
+    output_everything) for CLS_PROGRAM (fcgpu_set_program); max_flows > 0
+    enables the flow table (its state carries across the batches)."""
     torch = _torch()
+    res = []
     with torch.cuda.device(device_index):
-        ctx = N.Context(device_index, max(batch.n, 1), cfg)
+        ctx = N.Context(device_index, max(max(b.n for b in batches), 1), cfg)
         try:
             if program is not None:
                 ctx.set_program(*program)
-            db = DeviceBatch.upload(batch, device=f"cuda:{device_index}")
-            outs = DeviceOutputs(batch.n, cfg.nports, device=f"cuda:{device_index}",
-                                 anno=anno, perm=perm, port_start=perm, partition=partition)
-            run_device(ctx, db, outs)
-            torch.cuda.synchronize()
-            res = outs.numpy()
-            res["counters"] = np.array(ctx.counters(), dtype=np.uint64)
+            if max_flows:
+                ctx.flow_enable(max_flows)
+            for batch in batches:
+                db = DeviceBatch.upload(batch, device=f"cuda:{device_index}")
+                outs = DeviceOutputs(batch.n, cfg.nports, device=f"cuda:{device_index}",
+                                     anno=anno, perm=perm, port_start=perm, partition=partition,
+                                     flowid=max_flows > 0)
+                run_device(ctx, db, outs)
+                torch.cuda.synchronize()
+                r = outs.numpy()
+                r["counters"] = np.array(ctx.counters(), dtype=np.uint64)
+                if max_flows:
+                    r["flow_count"] = ctx.flow_count()
+                res.append(r)
         finally:
             ctx.close()
     return res

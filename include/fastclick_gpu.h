@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 5
+#define FCGPU_ABI_VERSION 6
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -176,6 +176,8 @@ typedef struct fcgpu_out {
     uint32_t    partition;    /* FCGPU_PART_GLOBAL or FCGPU_PART_TILE                    */
     uint32_t    reserved;
     uint8_t    *tile_perm;    /* TILE: [n] index within the tile, grouped by output      */
+    uint32_t   *flowid;       /* [n] flow ID from the context's flow table (fcgpu_flow_enable);
+                                 FCGPU_FLOW_NONE for packets that reach no flow manager */
 } fcgpu_out;
 
 typedef struct fcgpu_ctx fcgpu_ctx;
@@ -256,6 +258,31 @@ typedef struct fcgpu_step {
  * program is empty and every packet goes to that output ("all->[N]"). */
 int  fcgpu_set_program(fcgpu_ctx *ctx, uint32_t kind, const fcgpu_step *steps, uint32_t nsteps,
                        int32_t output_everything);
+
+/* Flow table: the IPFlow5ID flow classification of
+ * FlowIPManagerHMP (elements/research/flowipmanagerhmp.cc:96-126; the
+ * VirtualFlowManager family, include/click/flow/virtualflowmanager.hh) placed
+ * after the IPv4 check (and the L4 check, if configured) and before the
+ * classifier: every packet that passed the checks gets the ID of its
+ * (saddr, daddr, sport, dport, proto) flow; a flow seen for the first time gets
+ * the next ID (0, 1, 2, ... in packet order, persistent across batches: the
+ * `_current.fetch_and_add(1)` of flowipmanagerhmp.cc:99-102 on one thread).
+ * Non-first fragments use ports 0 (the reference leaves them uninitialised,
+ * lib/ipflowid.cc:34-38). IPv4 check modes only.
+ *   max_flows: IDs 0 .. max_flows-1 (the table holds 2x that many slots, up to
+ *     2^23 flows); a packet of a new flow beyond that gets FCGPU_FLOW_FULL (the
+ *     manager kills it, virtualflowmanager.hh:262-266). 0 disables the table.
+ * Each fcgpu_process with flow enabled runs one extra pass over the batch's
+ * new flows (four small launches); fcgpu_process_host processes the batch in
+ * order on one stream. */
+#define FCGPU_FLOW_NONE 0xffffffffu
+#define FCGPU_FLOW_FULL 0xfffffffeu
+#define FCGPU_MAX_FLOWS (1u << 23)
+int  fcgpu_flow_enable(fcgpu_ctx *ctx, uint32_t max_flows);
+/* Forget every flow (IDs restart at 0). */
+int  fcgpu_flow_reset(fcgpu_ctx *ctx);
+/* Flows assigned so far. Synchronises the context's device work. */
+int  fcgpu_flow_count(fcgpu_ctx *ctx, uint32_t *count);
 
 /* Host threads the context may use for the gather / copy-out loops of
  * fcgpu_process_host (the caller's thread included; default 1). */

@@ -41,9 +41,11 @@ typedef struct fcclick_result {
     uint32_t *out_len;      /* [n] packet length on departure                            */
     int32_t  *out_nh;       /* [n] network header offset from data() (-1 unset)          */
     uint32_t *out_batches;  /* [1] number of PacketBatches the sinks received             */
-    char     *handlers;     /* "name=value\n" for count, drops, drop_details, port_counts */
+    char     *handlers;     /* "name=value\n" for count, drops, drop_details, port_counts,
+                               flow_count, flow_drops, error                              */
     size_t    handlers_cap;
     uint8_t  *out_paint;    /* [n] PAINT_ANNO (anno u8 @17) on departure (may be NULL)     */
+    uint32_t *out_flow;     /* [n] anno u32 @28 (FLOWID_ANNO default) on departure (may be NULL) */
 } fcclick_result;
 
 /* Run a graph  Source(frames, BURST) -> conf => [0 .. nsinks-1] Sink  over n

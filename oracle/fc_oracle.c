@@ -466,3 +466,88 @@ void fco_process_batch2(const fcgpu_cfg *c, const uint8_t *arena, const uint32_t
         fco_partition_tiles(nb, port, n, FCGPU_TILE, perm_tile, tile_count);
     free(port);
 }
+
+/* ---- Flow table: FlowIPManagerHMP::process (elements/research/flowipmanagerhmp.cc:96-126) ----
+ * `_hash.find_create(IPFlow5ID(p), [] { return _current.fetch_and_add(1); })`
+ * walked over the batch on one thread: a flow's ID is the number of distinct
+ * flows seen before its first packet, kept across batches (no timeouts).
+ * Keys: IPFlow5ID(p) (lib/ipflowid.cc:29-46,91-94) = saddr, sport, daddr,
+ * dport, ip_p; equality on all five (include/click/ipflowid.hh:236-240). The
+ * reference leaves the ports of a non-first fragment uninitialised; we use 0.
+ * Beyond max_flows IDs a new flow gets FCGPU_FLOW_FULL (the IMP managers kill
+ * such a packet, include/click/flow/virtualflowmanager.hh:262-266). */
+typedef struct { uint32_t saddr, daddr, ports, proto, id, used; } fco_flow_ent;
+struct fco_flowtab {
+    fco_flow_ent *e;
+    uint32_t cap, n, next, max_flows;
+};
+
+fco_flowtab *fco_flow_new(uint32_t max_flows)
+{
+    fco_flowtab *t = (fco_flowtab *)calloc(1, sizeof(*t));
+    t->cap = 1024;
+    t->e = (fco_flow_ent *)calloc(t->cap, sizeof(fco_flow_ent));
+    t->max_flows = max_flows;
+    return t;
+}
+
+void fco_flow_free(fco_flowtab *t)
+{
+    if (t) { free(t->e); free(t); }
+}
+
+uint32_t fco_flow_count(const fco_flowtab *t) { return t->next; }
+
+static uint32_t fco_flow_h(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+    uint32_t h = a * 0x9E3779B1u ^ (b * 0x85EBCA77u) ^ (c * 0xC2B2AE3Du) ^ d;
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13;
+    return h;
+}
+
+static fco_flow_ent *fco_flow_slot(fco_flowtab *t, uint32_t s, uint32_t d, uint32_t p, uint32_t pr)
+{
+    uint32_t i = fco_flow_h(s, d, p, pr) & (t->cap - 1);
+    while (t->e[i].used && !(t->e[i].saddr == s && t->e[i].daddr == d && t->e[i].ports == p && t->e[i].proto == pr))
+        i = (i + 1) & (t->cap - 1);
+    return &t->e[i];
+}
+
+static void fco_flow_grow(fco_flowtab *t)
+{
+    fco_flow_ent *old = t->e;
+    uint32_t oc = t->cap;
+    t->cap *= 2;
+    t->e = (fco_flow_ent *)calloc(t->cap, sizeof(fco_flow_ent));
+    for (uint32_t i = 0; i < oc; i++)
+        if (old[i].used) *fco_flow_slot(t, old[i].saddr, old[i].daddr, old[i].ports, old[i].proto) = old[i];
+    free(old);
+}
+
+void fco_flow_batch(fco_flowtab *t, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                    const uint16_t *verdict, const fcgpu_anno *anno, uint32_t *flowid)
+{
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t reason = verdict[i] & 0xff;
+        flowid[i] = FCGPU_FLOW_NONE;
+        if (anno[i].ipver != 4 || (reason != FCGPU_R_OK && reason != FCGPU_R_NO_MATCH))
+            continue;
+        const uint8_t *nh = arena + desc[2 * i] + anno[i].nh;
+        const uint8_t *th = arena + desc[2 * i] + anno[i].th;
+        uint32_t s, d, p = 0, pr = nh[9];
+        memcpy(&s, nh + 12, 4);
+        memcpy(&d, nh + 16, 4);
+        if (((((uint32_t)nh[6] << 8) | nh[7]) & 0x1fff) == 0)   /* IP_FIRSTFRAG */
+            memcpy(&p, th, 4);
+        if (2 * (t->n + 1) > t->cap) fco_flow_grow(t);
+        fco_flow_ent *e = fco_flow_slot(t, s, d, p, pr);
+        if (!e->used) {
+            if (t->next >= t->max_flows) { flowid[i] = FCGPU_FLOW_FULL; continue; }
+            e->saddr = s; e->daddr = d; e->ports = p; e->proto = pr;
+            e->id = t->next++;
+            e->used = 1;
+            t->n++;
+        }
+        flowid[i] = e->id;
+    }
+}

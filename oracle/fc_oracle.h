@@ -56,6 +56,16 @@ void fco_set_program(uint32_t kind, const fcgpu_step *steps, uint32_t nsteps, in
  * nh/th/length (after the check): returns the output, or 0x7fff if none. */
 uint32_t fco_run_program(const uint8_t *frame, const fcgpu_anno *a);
 
+/* Flow table (FlowIPManagerHMP, elements/research/flowipmanagerhmp.cc:96-126):
+ * IDs in order of first appearance, persistent across fco_flow_batch calls.
+ * verdict/anno are this batch's fco_process_batch outputs. */
+typedef struct fco_flowtab fco_flowtab;
+fco_flowtab *fco_flow_new(uint32_t max_flows);
+void fco_flow_free(fco_flowtab *t);
+uint32_t fco_flow_count(const fco_flowtab *t);
+void fco_flow_batch(fco_flowtab *t, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                    const uint16_t *verdict, const fcgpu_anno *anno, uint32_t *flowid);
+
 /* Individual pieces, exposed for known-answer tests. */
 uint32_t fco_ipflowid_hash(uint32_t saddr_raw, uint16_t sport_net,
                            uint32_t daddr_raw, uint16_t dport_net);  /* A6 */

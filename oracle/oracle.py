@@ -51,6 +51,15 @@ def load():
     lib.fco_process_batch.argtypes = [C.POINTER(N.fcgpu_cfg), C.c_void_p, C.c_void_p, C.c_uint32,
                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_void_p]
+    lib.fco_flow_new.restype = C.c_void_p
+    lib.fco_flow_new.argtypes = [C.c_uint32]
+    lib.fco_flow_free.restype = None
+    lib.fco_flow_free.argtypes = [C.c_void_p]
+    lib.fco_flow_count.restype = C.c_uint32
+    lib.fco_flow_count.argtypes = [C.c_void_p]
+    lib.fco_flow_batch.restype = None
+    lib.fco_flow_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                   C.c_void_p, C.c_void_p]
     _lib = lib
     return lib
 
@@ -93,6 +102,32 @@ def process_batch(cfg, batch, program=None):
     return dict(verdict=verdict, reason=(verdict & 0xFF).astype(np.uint8),
                 port=(verdict >> 8).astype(np.uint8), hash=hsh, anno=anno, perm=perm,
                 port_start=start, perm_tile=perm_tile, tile_count=tile_count, counters=ctr)
+
+
+class FlowTable:
+    """FlowIPManagerHMP restatement (fc_oracle.c fco_flow_*): IDs in order of
+    first appearance, kept across batches."""
+
+    def __init__(self, max_flows):
+        self.lib = load()
+        self.t = self.lib.fco_flow_new(max_flows)
+
+    def batch(self, batch, res):
+        """res: this batch's process_batch() result (verdict, anno)."""
+        flowid = np.zeros(batch.n, np.uint32)
+        arena = np.ascontiguousarray(batch.arena)
+        desc = np.ascontiguousarray(batch.desc, dtype=np.uint32)
+        self.lib.fco_flow_batch(self.t, _p(arena), _p(desc), batch.n, _p(res["verdict"]),
+                                _p(np.ascontiguousarray(res["anno"])), _p(flowid))
+        return flowid
+
+    def count(self):
+        return self.lib.fco_flow_count(self.t)
+
+    def __del__(self):
+        if getattr(self, "t", None):
+            self.lib.fco_flow_free(self.t)
+            self.t = None
 
 
 def in_cksum(data: bytes) -> int:

@@ -189,10 +189,10 @@ int main(int argc, char **argv) {
         };
     };
     run("k_rx none", rx(k_rx<FCGPU_CHECK_IP4, true, kPartNone, false, false>, ntiles));
-    run("k_rx none fast", rx(k_rx<FCGPU_CHECK_IP4, true, kPartNone, false, false, true>, ntiles));
+    run("k_rx none fast", rx(k_rx<FCGPU_CHECK_IP4, true, kPartNone, false, false, false, true>, ntiles));
     run("k_rx tile", rx(k_rx<FCGPU_CHECK_IP4, true, kPartTile, false, false>, ntiles));
-    run("k_rx tile fast", rx(k_rx<FCGPU_CHECK_IP4, true, kPartTile, false, false, true>, ntiles));
+    run("k_rx tile fast", rx(k_rx<FCGPU_CHECK_IP4, true, kPartTile, false, false, false, true>, ntiles));
     run("k_rx global", rx(k_rx<FCGPU_CHECK_IP4, true, kPartGlobal, false, false>, ntiles));
-    run("k_rx global fast", rx(k_rx<FCGPU_CHECK_IP4, true, kPartGlobal, false, false, true>, ntiles));
+    run("k_rx global fast", rx(k_rx<FCGPU_CHECK_IP4, true, kPartGlobal, false, false, false, true>, ntiles));
     return 0;
 }

@@ -56,6 +56,9 @@ from fastclick_amd import synth  # noqa: E402
 CLICK = os.environ.get("FC_CLICK", "/tmp/fcbuild/userlevel/click")
 REFERENCE = os.environ.get("FC_REFERENCE", "/root/reference")
 CLICK3 = os.environ.get("FC_CLICK3", "/tmp/fcbuild3/userlevel/click")
+# --enable-research --enable-flow --enable-flow-dynamic --enable-ctx build
+# (FlowIPManagerHMP lives in elements/research)
+CLICK4 = os.environ.get("FC_CLICK4", "/tmp/fcbuild4/userlevel/click")
 FCREF = os.path.join(ROOT, "oracle", "_ref", "fcref")
 T0 = 1000
 BADSRC = "192.0.2.255 255.255.255.255"
@@ -781,6 +784,62 @@ def run_l4(b, tmp):
     return res
 
 
+def make_flow_set(n=4000, nflows=300, seed=2029):
+    """IPv4 frames drawn from a pool of 5-tuples with a skewed popularity, so
+    flows repeat within and across batches: UDP/TCP/ICMP, the same address and
+    port pair under different protocols (distinct IPFlow5IDs), swapped
+    directions (distinct too), IP options (ports after the options), first
+    fragments (MF set, offset 0), and ~1.5% of each CheckIPHeader error kind
+    (those never reach the flow manager). Non-first fragments are left out:
+    the reference hashes their uninitialised ports (lib/ipflowid.cc:34-38)."""
+    rng = np.random.default_rng(seed)
+    pool = synth._rand_flows(rng, nflows)
+    proto_pool = rng.choice([17, 17, 6, 6, 1], nflows)
+    # tuples that differ only by protocol or by direction
+    for j in range(0, nflows // 10):
+        a, b = 2 * j, 2 * j + 1
+        for k in ("src", "dst", "sport", "dport"):
+            pool[k][b] = pool[k][a]
+        proto_pool[b] = 6 if proto_pool[a] == 17 else 17
+    for j in range(nflows // 10, nflows // 5):
+        a, b = 2 * j, 2 * j + 1
+        pool["src"][b], pool["dst"][b] = pool["dst"][a], pool["src"][a]
+        pool["sport"][b], pool["dport"][b] = pool["dport"][a], pool["sport"][a]
+        proto_pool[b] = proto_pool[a]
+    w = 1.0 / (1 + np.arange(nflows)) ** 0.8
+    pick = rng.choice(nflows, n, p=w / w.sum())
+    fl = {k: v[pick] for k, v in pool.items()}
+    flen = rng.choice([60, 60, 60, 74, 98, 128], n)
+    hdr = synth.build_headers(n, **fl, proto=proto_pool[pick], frame_len=flen)
+    b = synth.pack(hdr, flen, meta=dict(set="flow", seed=seed))
+    synth.add_ip_options(b, 0.1, seed=seed + 1)
+    A = b.arena
+    for i in np.nonzero(rng.random(n) < 0.05)[0]:          # first fragments (MF, offset 0)
+        o = int(b.desc[i, 0]) + 14
+        A[o + 6] |= 0x20
+        synth._refresh_cksum(A, o)
+    kind = synth.inject_errors(b, 0.015, seed=seed + 2, kinds=range(5))
+    return b, kind, pick
+
+
+def run_flow(b, tmp):
+    """FlowIPManagerHMP -> StoreFlowID(OFFSET 0) on the checked stream: the
+    8-byte ID StoreFlowID writes is 1 + the HMP flow ID (both count new flows in
+    arrival order on one thread, storeflowid.cc:60-67); packets CheckIPHeader
+    drops get FCGPU_FLOW_NONE."""
+    if not os.path.exists(CLICK4):
+        return None
+    pcap = os.path.join(tmp, "flow.pcap")
+    write_pcap(pcap, b.frames())
+    click(CLICK4, "FromDump(flow.pcap, STOP true, TIMING false) -> Strip(14) -> CheckIPHeader(CHECKSUM true) "
+                  "-> FlowIPManagerHMP(CAPACITY 65536) -> StoreFlowID(OFFSET 0) -> ToDump(flow_out.pcap);", tmp)
+    got = read_pcap(os.path.join(tmp, "flow_out.pcap"))
+    fid = np.full(b.n, 0xFFFFFFFF, np.uint32)
+    for i, (_, data) in got.items():
+        fid[i] = int.from_bytes(data[0:8], "little") - 1
+    return dict(flowid=fid)
+
+
 def run_kat(tmp):
     """click_in_cksum on random buffers (odd lengths included) and IPFlowID /
     IP6FlowID hashcodes on random tuples, from the reference harness."""
@@ -810,11 +869,11 @@ def sha(path):
     return hashlib.sha256(open(path, "rb").read()).hexdigest()
 
 
-def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "kat")):
+def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "kat")):
     prov_path = os.path.join(HERE, "PROVENANCE.json")
     prov = json.load(open(prov_path)) if os.path.exists(prov_path) else {}
     prov.update(generator="tests/golden/gen_golden.py", click=CLICK, click_sha256=sha(CLICK),
-                click3=CLICK3, click3_sha256=sha(CLICK3), fcref=FCREF, fcref_sha256=sha(FCREF),
+                click3=CLICK3, click3_sha256=sha(CLICK3), click4=CLICK4, click4_sha256=sha(CLICK4), fcref=FCREF, fcref_sha256=sha(FCREF),
                 t0=T0, badsrc=BADSRC, gooddst=GOODDST, not_pinned=NOT_PINNED, nomatch=NOMATCH)
     with tempfile.TemporaryDirectory() as tmp:
         if "ip4" in sets:
@@ -854,6 +913,15 @@ def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "kat")):
             np.savez_compressed(os.path.join(HERE, "l4.npz"), arena=lb.arena, desc=lb.desc, **rl)
             for k in ("udp", "tcp"):
                 print("l4", k, {int(v): int(c) for v, c in zip(*np.unique(rl[k], return_counts=True))})
+        if "flow" in sets:
+            fb, fkind, fpick = make_flow_set()
+            rf = run_flow(fb, tmp)
+            if rf is not None:
+                np.savez_compressed(os.path.join(HERE, "flow.npz"), arena=fb.arena, desc=fb.desc, kind=fkind,
+                                    pick=fpick, **rf)
+                v = rf["flowid"][rf["flowid"] != 0xFFFFFFFF]
+                print("flow: classified", len(v), "flows", int(v.max()) + 1, "dropped",
+                      int((rf["flowid"] == 0xFFFFFFFF).sum()))
         if "combo" in sets:
             rc = run_combo(tmp)
             np.savez_compressed(os.path.join(HERE, "combo.npz"), **rc)
@@ -876,6 +944,8 @@ def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "kat")):
         "l4": "Strip(14) -> CheckIPHeader(CHECKSUM true) -> CheckUDPHeader|CheckTCPHeader(CHECKSUM true|false): "
               "per-packet verdicts (reason split by the CHECKSUM false run)",
         "combo": "IPInputCombo(7, BADSRC, GOODDST) on the ip4 set: survivors and their ip_len",
+        "flow": "Strip(14) -> CheckIPHeader(CHECKSUM true) -> FlowIPManagerHMP -> StoreFlowID(OFFSET 0) (click4: "
+                "--enable-research --enable-flow-dynamic --enable-ctx): per-packet flow ID = stored ID - 1",
         "kat": "fcref: click_in_cksum (lib/in_cksum.c), IPFlowID/IP6FlowID::hashcode (headers)",
     })
     prov["ipc_rules"] = IPC_RULES
@@ -885,4 +955,4 @@ def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "kat")):
 
 
 if __name__ == "__main__":
-    main(tuple(sys.argv[1:]) or ("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "kat"))
+    main(tuple(sys.argv[1:]) or ("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "kat"))

@@ -172,3 +172,36 @@ def test_element_ip6_extension_headers():
     # STRIP (MODE AUTO default): data() at the IPv6 header, length trimmed
     assert np.array_equal(r["len"][ok], g["eh_length"][ok].astype(np.uint32) - 14)
     assert (r["nh"][ok] == 0).all()
+
+
+@pytest.mark.gpu
+def test_element_flow_golden():
+    """GPUIPCheckClassify(FLOW_CAPACITY ..): the flow ID annotation of every
+    surviving packet equals FlowIPManagerHMP's (tests/golden/flow.npz); with a
+    small capacity the new flows beyond it are killed and counted."""
+    from fastclick_amd import click as K
+    from tests.test_golden import load, batch_of
+    g = load("flow")
+    b = batch_of(g)
+    ref = g["flowid"]
+    for burst, batch in ((32, 1024), (256, 0)):
+        r = K.run_element(f"GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4, FLOW_CAPACITY 100000, BATCH {batch})",
+                          b, burst=burst, nsinks=5)
+        ok = ref != 0xFFFFFFFF
+        assert np.array_equal(r["flow"][ok], ref[ok])
+        assert r["handlers"]["flow_count"] == str(int(ref[ok].max()) + 1)
+    r = K.run_element("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4, FLOW_CAPACITY 40, BATCH 512)", b,
+                      nsinks=5)
+    full = (ref >= 40) & (ref != 0xFFFFFFFF)
+    assert (r["port"][full] == 0xFFFFFFFF).all()
+    assert np.array_equal(r["flow"][ref < 40], ref[ref < 40])
+    assert r["handlers"]["flow_drops"] == str(int(full.sum()))
+
+
+def test_config_flow_keywords():
+    from fastclick_amd import click as K
+    K.check_config("GPUIPCheckClassify(OFFSET 14, FLOW_CAPACITY 65536, FLOWID_ANNO 32)")
+    with pytest.raises(K.ConfigError, match="FLOW_CAPACITY needs"):
+        K.check_config("GPUIPCheckClassify(MODE AUTO, FLOW_CAPACITY 10)")
+    with pytest.raises(K.ConfigError, match="FLOWID_ANNO"):
+        K.check_config("GPUIPCheckClassify(FLOWID_ANNO 46)")

@@ -1,0 +1,157 @@
+"""Flow table: FlowIPManagerHMP flow IDs on the device.
+
+Pin: tests/golden/flow.npz was produced by the reference itself
+(`CheckIPHeader(CHECKSUM true) -> FlowIPManagerHMP -> StoreFlowID(OFFSET 0)`,
+tests/golden/gen_golden.py run_flow): StoreFlowID writes 1 + the flow's
+arrival rank, the ID FlowIPManagerHMP gives it
+(elements/research/flowipmanagerhmp.cc:96-126, storeflowid.cc:60-67). The C
+oracle (fco_flow_*) is checked against it on CPU; the device path is checked
+against both, with the stream cut into batches of several sizes (the table
+persists across batches), and against the oracle on seeded workloads: every
+packet a new flow (C4), a 10k-flow pool (C3), one flow (C2), repeated batches,
+a table that fills up (FCGPU_FLOW_FULL), IP options, fragments and invalid
+packets in the mix.
+"""
+import numpy as np
+import pytest
+
+from fastclick_amd import synth
+from fastclick_amd import _native as N
+from tests.test_golden import load, batch_of
+from tests.helpers import set_fragment
+
+NONE = N.FLOW_NONE
+FULL = N.FLOW_FULL
+
+
+def flow_cfg(**kw):
+    base = dict(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16)
+    base.update(kw)
+    return N.make_cfg(**base)
+
+
+def split(b, sizes):
+    out, pos = [], 0
+    for s in sizes:
+        desc = b.desc[pos:pos + s]
+        out.append(synth.Batch(arena=b.arena, desc=np.ascontiguousarray(desc)))
+        pos += s
+    assert pos == b.n
+    return out
+
+
+def oracle_flows(O, cfg, batches, max_flows):
+    t = O.FlowTable(max_flows)
+    ids = []
+    for b in batches:
+        r = O.process_batch(cfg, b)
+        ids.append(t.batch(b, r))
+    return np.concatenate(ids), t.count()
+
+
+def test_oracle_flow_golden(oracle):
+    g = load("flow")
+    b = batch_of(g)
+    for sizes in ([b.n], [1000, 1500, b.n - 2500], [1] * 7 + [b.n - 7]):
+        ids, cnt = oracle_flows(oracle, flow_cfg(), split(b, sizes), 1 << 20)
+        assert np.array_equal(ids, g["flowid"]), f"flow IDs vs reference, batches {sizes[:3]}"
+        assert cnt == int(g["flowid"][g["flowid"] != NONE].max()) + 1
+
+
+def test_oracle_flow_full(oracle):
+    g = load("flow")
+    b = batch_of(g)
+    ids, cnt = oracle_flows(oracle, flow_cfg(), [b], 50)
+    ref = g["flowid"]
+    assert cnt == 50
+    assert np.array_equal(ids[ref < 50], ref[ref < 50])
+    assert (ids[(ref >= 50) & (ref != NONE)] == FULL).all()
+
+
+def _dev_flows(cfg, batches, max_flows, **kw):
+    from fastclick_amd import device
+    res = device.process_batches(batches, cfg, max_flows=max_flows, anno=True, perm=False, **kw)
+    return np.concatenate([r["flowid"] for r in res]), res[-1]["flow_count"], res
+
+
+@pytest.mark.gpu
+def test_gpu_flow_golden():
+    g = load("flow")
+    b = batch_of(g)
+    for sizes in ([b.n], [1000, 1500, b.n - 2500], [1, 255, 257, b.n - 513]):
+        ids, cnt, _ = _dev_flows(flow_cfg(), split(b, sizes), 1 << 20)
+        assert np.array_equal(ids, g["flowid"]), f"flow IDs vs reference, batches {sizes}"
+        assert cnt == int(g["flowid"][g["flowid"] != NONE].max()) + 1
+
+
+@pytest.mark.gpu
+def test_gpu_flow_golden_full():
+    g = load("flow")
+    b = batch_of(g)
+    ids, cnt, _ = _dev_flows(flow_cfg(), split(b, [700, b.n - 700]), 50)
+    ref = g["flowid"]
+    assert cnt == 50
+    assert np.array_equal(ids[ref < 50], ref[ref < 50])
+    assert (ids[(ref >= 50) & (ref != NONE)] == FULL).all()
+
+
+def _mixed(n, nflows, seed):
+    b = synth.c3(n, nflows=nflows, seed=seed)
+    synth.add_ip_options(b, 0.05, seed=seed + 1)
+    set_fragment(b, 0.02, seed=seed + 2)
+    synth.inject_errors(b, 0.01, seed=seed + 3)
+    return b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,batches,max_flows", [
+    ("c4-all-new", lambda: [synth.c4(1 << 18, seed=41), synth.c4(1 << 18, seed=41)], 1 << 20),
+    ("c3-10k", lambda: [_mixed(100_000, 10_000, 42), _mixed(70_001, 10_000, 43)], 1 << 20),
+    ("c2-one", lambda: [synth.c2(65_536, seed=44)] * 3, 1 << 10),
+    ("fills-up", lambda: [_mixed(30_000, 5_000, 45), _mixed(30_000, 5_000, 46)], 3_000),
+    ("udp-tcp-check", lambda: [_mixed(20_000, 2_000, 47)], 1 << 16),
+])
+def test_gpu_flow_vs_oracle(oracle, name, batches, max_flows):
+    bs = batches()
+    kw = {}
+    cfg = flow_cfg()
+    if name == "udp-tcp-check":
+        cfg = flow_cfg(l4_mode=N.L4_UDP)
+    got, cnt, _ = _dev_flows(cfg, bs, max_flows, **kw)
+    exp, ecnt = oracle_flows(oracle, cfg, bs, max_flows)
+    if not np.array_equal(got, exp):
+        bad = np.nonzero(got != exp)[0]
+        raise AssertionError(f"{name}: {len(bad)} flow IDs differ, first {bad[:6]}: got {got[bad[:6]]} "
+                             f"expected {exp[bad[:6]]}")
+    assert cnt == ecnt, name
+
+
+@pytest.mark.gpu
+def test_gpu_flow_mark_and_program_modes(oracle):
+    """The flow stage sits between the checks and the classifier: MarkIPHeader
+    mode, and packets a classifier program does not match still get IDs."""
+    bs = [_mixed(20_000, 1_500, 50)]
+    cfg = flow_cfg(check_mode=N.MARK_IP4, checksum=False)
+    got, cnt, _ = _dev_flows(cfg, bs, 1 << 16)
+    exp, ecnt = oracle_flows(oracle, cfg, bs, 1 << 16)
+    assert np.array_equal(got, exp) and cnt == ecnt
+    # IPClassifier(udp && dst port even, -> [X]): odd destination ports match no
+    # rule (jump -2^31+1 = [X]); they still have flow IDs
+    nomatch = -2147483647
+    steps = [(256 + 8, 17 << 8, 0xff00, 1, nomatch, 0), (512, 0, 0x01000000, -1, nomatch, 0)]
+    prog = (N.PROG_IPFILTER, steps, -1)
+    cfg = flow_cfg(classify=N.CLS_PROGRAM, nports=2)
+    got, cnt, res = _dev_flows(cfg, bs, 1 << 16, program=prog)
+    oracle.set_program(*prog)
+    exp, ecnt = oracle_flows(oracle, cfg, bs, 1 << 16)
+    assert (res[0]["reason"] == N.R_NO_MATCH).any()
+    assert np.array_equal(got, exp) and cnt == ecnt
+
+
+@pytest.mark.gpu
+def test_gpu_flow_rejects_auto_mode():
+    from fastclick_amd import device
+    b = synth.c5(1024, seed=3)
+    cfg = N.make_cfg(check_mode=N.CHECK_AUTO, offset=0, checksum=True, nports=4)
+    with pytest.raises(RuntimeError, match="IPv4 check mode"):
+        device.process_batches([b], cfg, max_flows=1024)
