@@ -61,9 +61,14 @@ def parse():
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse "
                          "several ranks on one GPU)")
-    ap.add_argument("--workload", choices=["c2", "c4"], default="c2",
-                    help="c2: one 5-tuple (BASELINE configs[1], the headline); c4: independent "
-                         "uniform random 5-tuples")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
+                    help="c2: one 5-tuple (BASELINE configs[1], the headline); c3: IMIX "
+                         "64/570/1500 B 7:4:1 over 10k 5-tuples (configs[2]); c4: independent "
+                         "uniform random 5-tuples (configs[3]); c5: 50%% 802.1Q + 30%% IPv6 mix "
+                         "through StripEtherVLANHeader + CheckIP6Header/CheckIPHeader (configs[4])")
+    ap.add_argument("--flow-capacity", type=int, default=0,
+                    help="> 0: the device flow table (FlowIPManagerHMP flow IDs, fcgpu_flow_enable) "
+                         "behind the check, with this many IDs; its new-flow pass runs every step")
     ap.add_argument("--classify", choices=["lb", "ipclass16"], default="lb",
                     help="lb: FlowSwitch LB_MODE hash x16 (headline); ipclass16: the survey's "
                          "IPClassifier with 15 UDP dst-port ranges + '-' (program printed by the "
@@ -72,6 +77,16 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
+
+
+WORKLOADS = {
+    "c2": "C2: 64 B IPv4/UDP (60-B frames in 64-B slots), 1M-packet device-resident batch, single 5-tuple",
+    "c3": "C3: IMIX 64/570/1500 B (7:4:1) IPv4/UDP, 10k uniform 5-tuples, 1M-packet device-resident batch "
+          "(first 64 B of each frame read)",
+    "c4": "C4: 64 B IPv4/UDP (60-B frames in 64-B slots), 1M-packet device-resident batch, independent "
+          "uniform 5-tuples",
+    "c5": "C5: 50% 802.1Q-tagged, 30% IPv6 (80-B frames) / 70% IPv4 (60-B), 1M-packet device-resident batch",
+}
 
 
 def ipclass16_program():
@@ -138,7 +153,7 @@ def main():
     from fastclick_amd.device import DeviceBatch, DeviceOutputs
 
     n = args.packets
-    host = synth.c2(n) if args.workload == "c2" else synth.c4(n)
+    host = dict(c2=synth.c2, c3=synth.c3, c4=synth.c4, c5=synth.c5)[args.workload](n)
     # nbuf distinct copies at distinct HBM addresses
     bufs = []
     for k in range(args.nbuf):
@@ -151,7 +166,9 @@ def main():
         steps, oe = click.parse_program(text)
         program = (N.PROG_IPFILTER, steps, oe)
         args.nports = 16
-    cfg = N.make_cfg(offset=14, checksum=True, hash_mode=N.HASH_FLOWID,
+    auto = args.workload == "c5"
+    cfg = N.make_cfg(check_mode=N.CHECK_AUTO if auto else N.CHECK_IP4, offset=0 if auto else 14,
+                     checksum=True, hash_mode=N.HASH_FLOWID,
                      classify=N.CLS_LB_HASH if program is None else N.CLS_PROGRAM, nports=args.nports)
     part = N.PART_TILE if args.partition == "tile" else N.PART_GLOBAL
     tile = part == N.PART_TILE
@@ -162,10 +179,12 @@ def main():
         ctxs.append(N.Context(local, n, cfg))
         if program is not None:
             ctxs[-1].set_program(*program)
+        if args.flow_capacity:
+            ctxs[-1].flow_enable(args.flow_capacity)
         streams.append(torch.cuda.Stream(dev))
         o = DeviceOutputs(n, args.nports, device=dev, verdict=True, hash=True, anno=False,
                           perm=(not args.no_perm) and not tile, tile_perm=(not args.no_perm) and tile,
-                          port_start=not args.no_perm, partition=part)
+                          port_start=not args.no_perm, partition=part, flowid=args.flow_capacity > 0)
         outs_keep.append(o)
         optrs.append(o.ptrs())
     ctx = ctxs[0]
@@ -258,8 +277,8 @@ def main():
                         kernel="k_rx", kernel_ms=round(timing["k_rx_ms"], 5),
                         scan_ms=round(timing["k_scan_ms"], 5), part_ms=round(timing["k_part_ms"], 5))
         cpu = None
-        if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(args.cpu_seconds, flows=1 if args.workload == "c2" else 4096,
+        if world == 1 and not args.no_cpu and not auto and not args.flow_capacity:
+            cpu = cpu_baseline(args.cpu_seconds, flows=dict(c2=1, c3=10000).get(args.workload, 4096),
                                program=ipclass16_program() if program is not None else None)
         line = {
             "metric": "Mpps device-resident, 64 B IPv4 cksum+classify, 1/2/4/8 MI355X",
@@ -275,11 +294,12 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": (("C2: 64 B IPv4/UDP (60-B frames in 64-B slots), 1M-packet "
-                              "device-resident batch, single 5-tuple" if args.workload == "c2" else
-                              "C4: 64 B IPv4/UDP (60-B frames in 64-B slots), 1M-packet "
-                              "device-resident batch, independent uniform 5-tuples")
-                             + "; CheckIPHeader(CHECKSUM true) + AggregateHash + "
+                "workload": (WORKLOADS[args.workload]
+                             + ("; StripEtherVLANHeader + CheckIP6Header/CheckIPHeader(CHECKSUM true)"
+                                if auto else "; CheckIPHeader(CHECKSUM true)")
+                             + (f" + FlowIPManagerHMP flow table ({args.flow_capacity} IDs)"
+                                if args.flow_capacity else "")
+                             + " + AggregateHash + "
                              + ("FlowSwitch hash 16 outputs" if program is None else
                                 "IPClassifier(15 UDP dst-port ranges, -) 16 outputs")
                              + ("" if args.no_perm else

@@ -387,7 +387,8 @@ const char *fcgpu_last_error(fcgpu_ctx *ctx) { return ctx ? ctx->err.c_str() : g
 static void flow_free(fcgpu_ctx *c) {
     FlowArgs &F = c->fl;
     for (void *p : {(void *)F.slots, (void *)F.claim, (void *)F.first, (void *)F.miss_pkt, (void *)F.miss_key,
-                    (void *)F.miss_slot, (void *)F.miss_first, (void *)F.bitmap, (void *)F.wordpre, (void *)F.state})
+                    (void *)F.miss_slot, (void *)F.miss_first, (void *)F.bitmap, (void *)F.wordpre,
+                    (void *)F.state})
         if (p) hipFree(p);
     F = FlowArgs{};
     c->max_flows = c->flow_slots = c->flow_words = 0;
@@ -399,10 +400,8 @@ static int flow_clear(fcgpu_ctx *c) {
     HIPCHK(c, hipMemset(F.slots, 0, sizeof(uint4) * c->flow_slots));
     HIPCHK(c, hipMemset(F.claim, 0, sizeof(uint32_t) * c->flow_slots));
     HIPCHK(c, hipMemset(F.first, 0xff, sizeof(uint32_t) * c->flow_slots));
-    HIPCHK(c, hipMemset(F.bitmap, 0, sizeof(uint32_t) * 2 * c->flow_words));
-    uint32_t st[16] = {};
-    st[kFsWords] = c->flow_words;
-    HIPCHK(c, hipMemcpy(F.state, st, sizeof(st), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemset(F.bitmap, 0, sizeof(uint32_t) * c->flow_words));
+    HIPCHK(c, hipMemset(F.state, 0, sizeof(uint32_t) * 16));
     return FCGPU_OK;
 }
 
@@ -426,7 +425,7 @@ int fcgpu_flow_enable(fcgpu_ctx *c, uint32_t max_flows) {
     HIPCHK(c, hipMalloc(&F.miss_key, sizeof(uint4) * c->max_batch));
     HIPCHK(c, hipMalloc(&F.miss_slot, sizeof(uint32_t) * c->max_batch));
     HIPCHK(c, hipMalloc(&F.miss_first, sizeof(uint32_t) * c->max_batch));
-    HIPCHK(c, hipMalloc(&F.bitmap, sizeof(uint32_t) * 2 * words));
+    HIPCHK(c, hipMalloc(&F.bitmap, sizeof(uint32_t) * words));
     HIPCHK(c, hipMalloc(&F.wordpre, sizeof(uint32_t) * words));
     HIPCHK(c, hipMalloc(&F.state, sizeof(uint32_t) * 16));
     F.mask = slots - 1;
@@ -625,12 +624,8 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, a, s, c->timing ? ev[0].a : nullptr,
                   c->timing ? ev[0].b : nullptr);
     HIPCHK(c, hipGetLastError());
-    if (a.fl.slots) {   // the batch's new flows (fcgpu_flow.hh)
-        const uint32_t g = std::min<uint32_t>((n + kFlowBlock - 1) / kFlowBlock, 1024);
-        hipLaunchKernelGGL(k_flow_claim, dim3(g), dim3(kFlowBlock), 0, s, a.fl);
-        hipLaunchKernelGGL(k_flow_mark, dim3(g), dim3(kFlowBlock), 0, s, a.fl);
-        hipLaunchKernelGGL(k_flow_scan, dim3(1), dim3(1024), 0, s, a.fl, (n + 31) / 32);
-        hipLaunchKernelGGL(k_flow_assign, dim3(g), dim3(kFlowBlock), 0, s, a.fl);
+    if (a.fl.slots) {   // the batch's new flows get their IDs (fcgpu_flow.hh)
+        hipLaunchKernelGGL(k_flow_finish, dim3(1), dim3(kFinishBlock), 0, s, a.fl, (n + 31) / 32);
         HIPCHK(c, hipGetLastError());
     }
     if (want_global) {

@@ -66,13 +66,12 @@ struct FlowArgs {
     uint4 *miss_key;         // [max_batch]
     uint32_t *miss_slot;     // [max_batch]
     uint32_t *miss_first;    // [max_batch]
-    uint32_t *bitmap;        // [2][words] first-appearance bits, by batch parity
+    uint32_t *bitmap;        // [words] first-appearance bits of this batch's new flows
     uint32_t *wordpre;       // [words] exclusive popcount prefix
     uint32_t *state;         // kFs* words below
     uint32_t *flowid;        // [n] output (may be null)
 };
-constexpr uint32_t kFsNext = 0, kFsBase = 1, kFsMiss = 2, kFsPar = 3, kFsPrevWords = 4, kFsSnap = 5,
-                   kFsWords = 8;
+constexpr uint32_t kFsNext = 0, kFsMiss = 1;   // next flow ID; misses appended this batch
 constexpr uint32_t kFlowMiss = 0xfffffffdu;
 constexpr uint32_t kSlotNone = 0xffffffffu;
 
@@ -693,21 +692,62 @@ __device__ __forceinline__ uint4 flow_key(const FrameView &f, const fcgpu_anno &
 }
 
 // Packets past the checks get the ID of their flow, or a miss entry for the
-// batch's new-flow pass (k_flow_*) -- one wave-aggregated atomic per wave.
-__device__ __forceinline__ void flow_stage(const FlowArgs &F, const FrameView &f, bool live, uint32_t i,
-                                           const PktResult &r) {
-    const bool want = live && r.an.ipver == 4 && (r.reason == FCGPU_R_OK || r.reason == FCGPU_R_NO_MATCH);
+// batch's new-flow pass (k_flow_finish). The first slot is loaded early
+// (flow_issue, right after the checks) and examined late (flow_resolve, after
+// the histogram and partition), so its latency hides behind that work.
+struct FlowProbe {
+    uint4 key;
+    uint4 sl;        // first probed slot
+    uint32_t pos;
+    bool want;
+};
+__device__ __forceinline__ FlowProbe flow_issue(const FlowArgs &F, const FrameView &f, bool live,
+                                                const PktResult &r) {
+    FlowProbe q;
+    q.want = live && r.an.ipver == 4 && (r.reason == FCGPU_R_OK || r.reason == FCGPU_R_NO_MATCH);
+    q.key = make_uint4(0, 0, 0, 0);
+    q.sl = make_uint4(0, 0, 0, 0);
+    q.pos = 0;
+    if (q.want) {
+        q.key = flow_key(f, r.an);
+        q.pos = flow_slot_hash(q.key) & F.mask;
+        q.sl = F.slots[q.pos];
+    }
+    return q;
+}
+// A miss claims its key's slot right away (see fcgpu_flow.hh): its key is
+// published in the miss list before the CAS (release fence), and a lane that
+// finds another miss's claim reads that key with agent-scope loads.
+__device__ __forceinline__ uint32_t flow_claim(const FlowArgs &F, uint4 k, uint32_t pos, uint32_t e) {
+    if (__hip_atomic_load(&F.state[kFsNext], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= F.max_flows)
+        return kSlotNone;                        // no IDs left: FCGPU_FLOW_FULL
+    for (uint32_t p = 0; p <= F.mask; ++p) {
+        const uint4 sl = F.slots[pos];
+        if (sl.w == 0) {
+            const uint32_t old = atomicCAS(&F.claim[pos], 0u, e + 1);
+            if (old == 0) return pos;
+            const uint32_t *ok = reinterpret_cast<const uint32_t *>(&F.miss_key[old - 1]);
+            uint4 o;
+            o.x = __hip_atomic_load(ok + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            o.y = __hip_atomic_load(ok + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            o.z = __hip_atomic_load(ok + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            o.w = __hip_atomic_load(ok + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (o.x == k.x && o.y == k.y && o.z == k.z && o.w == k.w) return pos;
+        }
+        pos = (pos + 1) & F.mask;
+    }
+    return kSlotNone;
+}
+
+__device__ __forceinline__ void flow_resolve(const FlowArgs &F, FlowProbe &q, bool live, uint32_t i) {
     uint32_t id = FCGPU_FLOW_NONE;
-    uint4 k = make_uint4(0, 0, 0, 0);
-    if (want) {
-        k = flow_key(f, r.an);
-        uint32_t pos = flow_slot_hash(k) & F.mask;
+    if (q.want) {
         id = kFlowMiss;
         for (uint32_t p = 0; p <= F.mask; ++p) {
-            const uint4 sl = F.slots[pos];
-            if (sl.w == 0) break;
-            if (flow_key_eq(sl, k)) { id = flow_tag_id(sl.w); break; }
-            pos = (pos + 1) & F.mask;
+            if (q.sl.w == 0) break;
+            if (flow_key_eq(q.sl, q.key)) { id = flow_tag_id(q.sl.w); break; }
+            q.pos = (q.pos + 1) & F.mask;
+            q.sl = F.slots[q.pos];
         }
     }
     const uint64_t mm = __ballot(id == kFlowMiss);
@@ -720,7 +760,11 @@ __device__ __forceinline__ void flow_stage(const FlowArgs &F, const FrameView &f
         if (id == kFlowMiss) {
             const uint32_t e = base + (uint32_t)__popcll(mm & ((1ull << lane) - 1ull));
             F.miss_pkt[e] = i;
-            F.miss_key[e] = k;
+            F.miss_key[e] = q.key;
+            __threadfence();
+            const uint32_t slot = flow_claim(F, q.key, q.pos, e);   // q.pos: first empty slot
+            F.miss_slot[e] = slot;
+            if (slot != kSlotNone) atomicMin(&F.first[slot], i);
         }
     }
     if (live && F.flowid) F.flowid[i] = id;
@@ -759,7 +803,8 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d,
         process_packet<CM, CK, PROG>(A.cfg, f, d.y, r, sprog);
     }
     if (L4) l4_stage(A.cfg, f, A.arena + d.x, live, r);
-    if (FLOW) flow_stage(A.fl, f, live, i, r);
+    FlowProbe fq;
+    if (FLOW) fq = flow_issue(A.fl, f, live, r);
     if (live) {
         if (A.verdict) A.verdict[i] = (uint16_t)(r.reason | (r.port << 8));
         if (A.hash) A.hash[i] = r.hash;
@@ -823,6 +868,7 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d,
             if (A.tile_perm) A.tile_perm[pos] = (uint8_t)threadIdx.x;
         }
     }
+    if (FLOW) flow_resolve(A.fl, fq, live, i);
     // counters: one atomic per non-zero bin per tile, sharded by tile
     if (t < nbt) {
         unsigned long long *ctr = A.ctr + (size_t)(tile & (FCGPU_CTR_SHARDS - 1)) * FCGPU_NCOUNTERS;
