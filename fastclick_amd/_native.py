@@ -14,16 +14,18 @@ LIBFCGPU = os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 6
+ABI_VERSION = 7
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
-    R_BAD_IP6, R_VLAN_REJECT, R_NO_MATCH, R_L4_PROTO, R_L4_LENGTH, R_L4_CKSUM = range(13)
-NREASON_SLOTS = 12
+    R_BAD_IP6, R_VLAN_REJECT, R_NO_MATCH, R_L4_PROTO, R_L4_LENGTH, R_L4_CKSUM, \
+    R_TTL_EXPIRED, R_SETCKSUM_BAD = range(15)
+NREASON_SLOTS = 14
+RW_DECTTL, RW_SETCKSUM, RW_INPLACE = 1, 2, 4
 L4_NONE, L4_UDP, L4_TCP = 0, 1, 2
 
 
 def reason_slot(r: int) -> int:
-    """Counter slot of reason r (reasons 0-5, 7-12; 6 = valid has none)."""
+    """Counter slot of reason r (reasons 0-5, 7-14; 6 = valid has none)."""
     return r if r < 6 else r - 1
 CHECK_IP4, MARK_IP4, CHECK_AUTO = 0, 1, 2
 HASH_NONE, HASH_FLOWID, HASH_FLOW5ID = 0, 1, 2
@@ -33,7 +35,7 @@ STEP_SHORT_YES = 1
 MAX_STEPS = 8192
 MAX_PORTS = 64
 MAX_ADDRS = 16
-CTR_COUNT, CTR_DROPS, CTR_REASON, CTR_PORT = 0, 1, 2, 14
+CTR_COUNT, CTR_DROPS, CTR_REASON, CTR_PORT = 0, 1, 2, 16
 NCOUNTERS = CTR_PORT + MAX_PORTS + 1
 CTR_SHARDS = 64
 PART_GLOBAL, PART_TILE = 0, 1
@@ -64,6 +66,8 @@ class fcgpu_cfg(C.Structure):
         ("process_eh", C.c_uint32),
         ("l4_mode", C.c_uint32),
         ("l4_checksum", C.c_uint32),
+        ("rewrite", C.c_uint32),
+        ("ttl_multicast", C.c_uint32),
     ]
 
 
@@ -110,6 +114,7 @@ class fcgpu_out(C.Structure):
         ("reserved", C.c_uint32),
         ("tile_perm", C.c_void_p),
         ("flowid", C.c_void_p),
+        ("ip_rw", C.c_void_p),
     ]
 
 
@@ -208,7 +213,7 @@ def default_cfg() -> fcgpu_cfg:
 def make_cfg(*, check_mode=CHECK_IP4, offset=0, checksum=False, hash_mode=HASH_FLOWID,
              classify=CLS_NONE, nports=1, hs_offset=0, hs_length=1, native_vlan=0,
              badsrc=(), gooddst=(), bad6=None, process_eh=False, l4_mode=L4_NONE,
-             l4_checksum=True) -> fcgpu_cfg:
+             l4_checksum=True, rewrite=0, ttl_multicast=True) -> fcgpu_cfg:
     """Build an fcgpu_cfg. Addresses are raw network-order words (bytes a.b.c.d
     -> little-endian u32 of those bytes), as IPAddress stores them."""
     cfg = default_cfg()
@@ -230,6 +235,8 @@ def make_cfg(*, check_mode=CHECK_IP4, offset=0, checksum=False, hash_mode=HASH_F
     cfg.process_eh = 1 if process_eh else 0
     cfg.l4_mode = l4_mode
     cfg.l4_checksum = 1 if l4_checksum else 0
+    cfg.rewrite = rewrite
+    cfg.ttl_multicast = 1 if ttl_multicast else 0
     if bad6 is not None:
         cfg.nbad6 = len(bad6)
         for j, a in enumerate(bad6):
@@ -268,18 +275,19 @@ class Context:
         self.cfg = cfg
 
     def process(self, arena_ptr, desc_ptr, n, *, verdict=0, hash=0, anno=0, perm=0,
-                port_start=0, tile_count=0, partition=PART_GLOBAL, tile_perm=0, flowid=0, stream=0):
+                port_start=0, tile_count=0, partition=PART_GLOBAL, tile_perm=0, flowid=0, ip_rw=0,
+                stream=0):
         out = fcgpu_out(verdict or None, hash or None, anno or None, perm or None,
                         port_start or None, tile_count or None, partition, 0, tile_perm or None,
-                        flowid or None)
+                        flowid or None, ip_rw or None)
         self._chk(self.lib.fcgpu_process(self.h, arena_ptr, desc_ptr, n, C.byref(out),
                                          stream or None), "fcgpu_process")
 
     def process_host(self, frames, lens_ptr, n, *, verdict=0, hash=0, anno=0, perm=0,
-                     port_start=0, tile_count=0, partition=PART_GLOBAL, tile_perm=0, flowid=0):
+                     port_start=0, tile_count=0, partition=PART_GLOBAL, tile_perm=0, flowid=0, ip_rw=0):
         out = fcgpu_out(verdict or None, hash or None, anno or None, perm or None,
                         port_start or None, tile_count or None, partition, 0, tile_perm or None,
-                        flowid or None)
+                        flowid or None, ip_rw or None)
         self._chk(self.lib.fcgpu_process_host(self.h, frames, lens_ptr, n, C.byref(out)),
                   "fcgpu_process_host")
 

@@ -166,6 +166,7 @@ struct fcgpu_ctx {
     uint8_t *d_htp = nullptr;
     fcgpu_anno *d_hanno = nullptr;
     uint32_t *d_hflow = nullptr;
+    uint32_t *d_hrw = nullptr;
     // pipelined host path (FCGPU_PART_TILE / no whole-batch partition)
     HostSlot slot[kSlots];
     uint32_t slot_cap = 0;
@@ -336,11 +337,14 @@ static int process_host_whole(fcgpu_ctx *c, const uint8_t *const *frames, const 
     d.tile_perm = h->tile_perm ? c->d_htp : nullptr;
     if (h->flowid && !c->d_hflow) HIPCHK(c, hipMalloc(&c->d_hflow, sizeof(uint32_t) * c->max_batch));
     d.flowid = h->flowid ? c->d_hflow : nullptr;
+    if (h->ip_rw && !c->d_hrw) HIPCHK(c, hipMalloc(&c->d_hrw, sizeof(uint32_t) * c->max_batch));
+    d.ip_rw = h->ip_rw ? c->d_hrw : nullptr;
     int rc = fcgpu_process(c, c->d_arena, c->d_desc, n, &d, s);
     if (rc != FCGPU_OK) return rc;
     if (h->verdict) HIPCHK(c, hipMemcpyAsync(h->verdict, d.verdict, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, s));
     if (h->hash) HIPCHK(c, hipMemcpyAsync(h->hash, d.hash, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
     if (h->flowid) HIPCHK(c, hipMemcpyAsync(h->flowid, d.flowid, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
+    if (h->ip_rw) HIPCHK(c, hipMemcpyAsync(h->ip_rw, d.ip_rw, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
     if (h->anno) HIPCHK(c, hipMemcpyAsync(h->anno, d.anno, sizeof(fcgpu_anno) * n, hipMemcpyDeviceToHost, s));
     if (h->perm) HIPCHK(c, hipMemcpyAsync(h->perm, d.perm, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
     if (h->tile_perm) HIPCHK(c, hipMemcpyAsync(h->tile_perm, d.tile_perm, n, hipMemcpyDeviceToHost, s));
@@ -379,6 +383,7 @@ void fcgpu_default_cfg(fcgpu_cfg *c) {
     c->native_vlan = 0;                // StripEtherVLANHeader default NATIVE_VLAN 0
     c->nbad6 = 1;                      // CheckIP6Header default bad source ff..ff
     c->l4_checksum = 1;                // CheckUDPHeader/CheckTCPHeader default CHECKSUM true
+    c->ttl_multicast = 1;              // DecIPTTL default MULTICAST true (decipttl.cc:31)
     memset(c->bad6[0], 0xff, 16);
 }
 
@@ -476,6 +481,7 @@ void fcgpu_close(fcgpu_ctx *c) {
         hipFree(c->d_htc);
         hipFree(c->d_htp);
         hipFree(c->d_hflow);
+        hipFree(c->d_hrw);
         flow_free(c);
         hipHostFree(c->h_arena);
         hipHostFree(c->h_desc);
@@ -544,6 +550,10 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     if (cfg->classify == FCGPU_CLS_HASHSWITCH && (cfg->hs_length <= 0 || cfg->hs_offset < 0))
         return fail(c, FCGPU_EINVAL, "length must be > 0");   // hashswitch.cc:40-41
     if (cfg->native_vlan > 0xFFF) return fail(c, FCGPU_EINVAL, "bad NATIVE_VLAN");
+    if (cfg->rewrite & ~(FCGPU_RW_DECTTL | FCGPU_RW_SETCKSUM | FCGPU_RW_INPLACE))
+        return fail(c, FCGPU_EINVAL, "bad rewrite flags");
+    if ((cfg->rewrite & (FCGPU_RW_DECTTL | FCGPU_RW_SETCKSUM)) && cfg->check_mode == FCGPU_CHECK_AUTO)
+        return fail(c, FCGPU_EINVAL, "rewrite needs an IPv4 check mode (CHECK_IP4 or MARK_IP4)");
     c->cfg = *cfg;
     DevCfg &d = c->dcfg;
     memset(&d, 0, sizeof(d));
@@ -561,6 +571,8 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     d.process_eh = cfg->process_eh ? 1u : 0u;
     d.l4_mode = cfg->l4_mode;
     d.l4_checksum = cfg->l4_checksum ? 1u : 0u;
+    d.rewrite = (cfg->rewrite & (FCGPU_RW_DECTTL | FCGPU_RW_SETCKSUM)) ? cfg->rewrite : 0u;
+    d.ttl_multicast = cfg->ttl_multicast ? 1u : 0u;
     memcpy(d.badsrc, cfg->badsrc, sizeof(d.badsrc));
     memcpy(d.gooddst, cfg->gooddst, sizeof(d.gooddst));
     memcpy(d.bad6, cfg->bad6, sizeof(d.bad6));
@@ -614,6 +626,7 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     a.cfg = c->dcfg;
     a.fl = c->fl;
     a.fl.flowid = o->flowid;
+    a.ip_rw = o->ip_rw;
     if (a.fl.slots && c->cfg.check_mode == FCGPU_CHECK_AUTO)
         return fail(c, FCGPU_EINVAL, "the flow table needs an IPv4 check mode (CHECK_IP4 or MARK_IP4)");
 
@@ -796,6 +809,7 @@ static int process_host_pipelined(fcgpu_ctx *c, const uint8_t *const *frames, co
         d.reserved = 0;
         d.tile_perm = h->tile_perm ? sl.d_tp : nullptr;
         d.flowid = nullptr;   // flow tables run the whole batch in order (process_host_whole)
+        d.ip_rw = nullptr;    // so do header rewrites the caller wants back
         int rc = fcgpu_process(c, sl.d_arena, sl.d_desc, cn, &d, s);
         if (rc != FCGPU_OK) return rc;
         const uint32_t tb = base / kTile, nt = (cn + kTile - 1) / kTile;
@@ -831,7 +845,7 @@ int fcgpu_process_host(fcgpu_ctx *c, const uint8_t *const *frames, const uint32_
     if (h->partition > FCGPU_PART_TILE) return fail(c, FCGPU_EINVAL, "bad partition mode");
     HIPCHK(c, hipSetDevice(c->device));
     // a flow table assigns IDs in packet order: one pass on one stream
-    if ((h->partition == FCGPU_PART_GLOBAL && (h->perm || h->port_start)) || c->fl.slots)
+    if ((h->partition == FCGPU_PART_GLOBAL && (h->perm || h->port_start)) || c->fl.slots || h->ip_rw)
         return process_host_whole(c, frames, lens, n, h);
     if (h->partition == FCGPU_PART_TILE && ((h->perm || h->tile_perm) != (h->tile_count != nullptr)))
         return fail(c, FCGPU_EINVAL, "FCGPU_PART_TILE needs tile_count and perm and/or tile_perm");

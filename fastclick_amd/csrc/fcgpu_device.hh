@@ -42,6 +42,8 @@ struct DevCfg {
     uint32_t process_eh;
     uint32_t l4_mode;
     uint32_t l4_checksum;
+    uint32_t rewrite;         // FCGPU_RW_*
+    uint32_t ttl_multicast;
     const uint4 *prog;        // decision program (FCGPU_CLS_PROGRAM), 16 B per step
     uint32_t prog_n;
     uint32_t prog_kind;
@@ -89,6 +91,7 @@ struct RxArgs {
     uint8_t *tile_perm;    // [n] tile-local partition (kPartTile)
     unsigned long long *ctr;   // [FCGPU_CTR_SHARDS][FCGPU_NCOUNTERS]
     FlowArgs fl;               // FLOW instances only
+    uint32_t *ip_rw;           // [n] rewritten IP header bytes 8..11 (cfg.rewrite)
     DevCfg cfg;
 };
 
@@ -770,6 +773,65 @@ __device__ __forceinline__ void flow_resolve(const FlowArgs &F, FlowProbe &q, bo
     if (live && F.flowid) F.flowid[i] = id;
 }
 
+// ---- header rewrites after the classifier ----------------
+// DecIPTTL::simple_action (elements/ip/decipttl.cc:52-78): ttl <= 1 leaves on
+// output 1; else --ttl and the RFC 1624 update of the checksum,
+//   sum = (~ntohs(ip_sum) & 0xFFFF) + 0xFEFF; ip_sum = ~htons(sum + (sum >> 16)).
+// SetIPChecksum::simple_action (elements/ip/setipchecksum.cc:38-58): the full
+// click_in_cksum of the header with ip_sum = 0; kills a packet whose header
+// does not fit (only reachable in MARK mode). The packet's IP header bytes
+// 8..11 after the rewrites go to ip_rw (and the arena with FCGPU_RW_INPLACE).
+__device__ __forceinline__ void rw_stage(const DevCfg &c, const FrameView &f, uint8_t *frame, bool live,
+                                         PktResult &r, uint32_t *ip_rw, uint32_t i) {
+    uint32_t w = 0;
+    bool changed = false;
+    if (live && r.reason == FCGPU_R_OK && r.an.ipver == 4) {
+        const uint32_t nh = r.an.nh;
+        w = f.rd32(nh + 8);                         // ttl, proto, sum (network order)
+        if (c.rewrite & FCGPU_RW_DECTTL) {
+            const bool mcast = (f.rd8(nh + 16) & 0xf0u) == 0xe0u;   // IPAddress::is_multicast
+            if (c.ttl_multicast || !mcast) {
+                const uint32_t ttl = w & 0xffu;
+                if (ttl <= 1) {
+                    r.reason = FCGPU_R_TTL_EXPIRED;
+                    r.port = c.nports;
+                } else {
+                    const uint32_t old = bswap16(w >> 16);
+                    const uint32_t sum = (~old & 0xffffu) + 0xfeffu;
+                    const uint32_t nsum = ~(sum + (sum >> 16)) & 0xffffu;
+                    w = (w & 0xff00u) | (ttl - 1) | (bswap16(nsum) << 16);
+                    changed = true;
+                }
+            }
+        }
+        if ((c.rewrite & FCGPU_RW_SETCKSUM) && r.reason == FCGPU_R_OK) {
+            const uint32_t plen = (uint32_t)r.an.length - nh, hl = (f.rd8(nh) & 15u) << 2;
+            if (plen < 20 || hl < 20 || hl > plen) {
+                r.reason = FCGPU_R_SETCKSUM_BAD;
+                r.port = c.nports;
+            } else {
+                uint64_t s = (uint64_t)f.rd32(nh) + f.rd32(nh + 4) + (w & 0xffffu);
+                for (uint32_t j = 12; j < hl; j += 4) s += f.rd32(nh + j);
+                s = (s & 0xffffffffu) + (s >> 32);
+                s = (s & 0xffffffffu) + (s >> 32);
+                uint32_t t = (uint32_t)s;
+                t = (t & 0xffff) + (t >> 16);
+                t = (t & 0xffff) + (t >> 16);
+                w = (w & 0xffffu) | ((~t & 0xffffu) << 16);
+                changed = true;
+            }
+        }
+        changed = changed && r.reason == FCGPU_R_OK;   // a killed packet keeps nothing
+        if (changed && (c.rewrite & FCGPU_RW_INPLACE)) {
+            uint8_t *p = frame + nh + 8;
+            p[0] = (uint8_t)w;
+            p[2] = (uint8_t)(w >> 16);
+            p[3] = (uint8_t)(w >> 24);
+        }
+    }
+    if (live && ip_rw) ip_rw[i] = changed ? w : 0u;
+}
+
 // One 256-packet tile once its header window is in LDS: fused
 // [StripEtherVLANHeader ->] CheckIPHeader/CheckIP6Header -> AggregateHash ->
 // classify; per-wave histogram by ballots; counters by sharded atomics;
@@ -805,6 +867,8 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d,
     if (L4) l4_stage(A.cfg, f, A.arena + d.x, live, r);
     FlowProbe fq;
     if (FLOW) fq = flow_issue(A.fl, f, live, r);
+    if (A.cfg.rewrite)   // launch-uniform
+        rw_stage(A.cfg, f, const_cast<uint8_t *>(A.arena) + d.x, live, r, A.ip_rw, i);
     if (live) {
         if (A.verdict) A.verdict[i] = (uint16_t)(r.reason | (r.port << 8));
         if (A.hash) A.hash[i] = r.hash;

@@ -34,6 +34,12 @@ class Sink : public Element {
                 if (_r->out_nh) _r->out_nh[i] = p->network_header_offset();
                 if (_r->out_paint) _r->out_paint[i] = p->anno_u8(PAINT_ANNO_OFFSET);
                 if (_r->out_flow) _r->out_flow[i] = p->anno_u32(28);
+                if (_r->out_ip8 && p->network_header_offset() >= 0 &&
+                    p->network_header_offset() + 12 <= (int)p->length()) {
+                    uint32_t w;
+                    memcpy(&w, p->data() + p->network_header_offset() + 8, 4);
+                    _r->out_ip8[i] = w;
+                }
             }
             ++*_seq;
             ++cnt;

@@ -33,6 +33,11 @@
 //     in the 4-byte annotation at FLOWID_ANNO; a new flow beyond the capacity
 //     is killed (as the IMP managers do when their flow stack is empty). Output
 //     batches are the classifier's, not split at flow changes.
+//   DEC_TTL, TTL_MULTICAST (default true), SET_CHECKSUM
+//                                            -- DecIPTTL / SetIPChecksum after the
+//     classifier (IPv4): TTL-expired packets (DecIPTTL output 1) join output N,
+//     headers SetIPChecksum rejects are killed; the rewritten ttl/checksum
+//     bytes are written back into each packet.
 //   MODE CHECK|MARK|AUTO, HASH NONE|FLOWID|FLOW5ID, STRIP, BATCH, DEVICE,
 //   PARTITION TILE (default: each 256-packet tile classified as one batch, one
 //   fused launch) | GLOBAL (the whole staged batch as one, three launches)
@@ -174,6 +179,13 @@ class GPUIPCheckClassify : public Element {
                     if (_cfg.nbad6 >= FCGPU_MAX_ADDRS) return err(errh, "BADADDRS: too many addresses");
                     memcpy(_cfg.bad6[_cfg.nbad6++], a, 16);
                 }
+            } else if (k == "DEC_TTL" || k == "SET_CHECKSUM" || k == "TTL_MULTICAST") {
+                if (!parse_bool(v, b)) return err(errh, k + " expects true/false");
+                if (k == "TTL_MULTICAST") _cfg.ttl_multicast = b;
+                else {
+                    const uint32_t f = k == "DEC_TTL" ? FCGPU_RW_DECTTL : FCGPU_RW_SETCKSUM;
+                    _cfg.rewrite = b ? (_cfg.rewrite | f) : (_cfg.rewrite & ~f);
+                }
             } else if (k == "FLOW_CAPACITY") {
                 if (!parse_int(v, n) || n < 0 || n > (long)FCGPU_MAX_FLOWS) return err(errh, "bad FLOW_CAPACITY");
                 _flow_cap = (uint32_t)n;
@@ -194,6 +206,8 @@ class GPUIPCheckClassify : public Element {
             return err(errh, "L4 needs MODE CHECK or MARK");
         if (_flow_cap && _cfg.check_mode == FCGPU_CHECK_AUTO)
             return err(errh, "FLOW_CAPACITY needs MODE CHECK or MARK");
+        if (_cfg.rewrite && _cfg.check_mode == FCGPU_CHECK_AUTO)
+            return err(errh, "DEC_TTL / SET_CHECKSUM need MODE CHECK or MARK");
         if (_cfg.classify == FCGPU_CLS_PROGRAM) {
             if (_prog.output_everything >= (int32_t)_cfg.nports && _prog.output_everything != 0x7fff)
                 return err(errh, "PROGRAM sends everything to a missing output");
@@ -222,6 +236,7 @@ class GPUIPCheckClassify : public Element {
             if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_flow_enable: ") + fcgpu_last_error(_ctx));
             _flowid.resize(_cap);
         }
+        if (_cfg.rewrite) _iprw.resize(_cap);
         _pkts.reserve(_cap);
         _frames.reserve(_cap);
         _lens.reserve(_cap);
@@ -290,6 +305,7 @@ class GPUIPCheckClassify : public Element {
         }
         fcgpu_out o{};
         o.flowid = _flow_cap ? _flowid.data() : nullptr;
+        o.ip_rw = _cfg.rewrite ? _iprw.data() : nullptr;
         o.verdict = _verdict.data();
         o.hash = _hash.data();
         o.anno = _anno.data();
@@ -318,6 +334,8 @@ class GPUIPCheckClassify : public Element {
             if (autom && reason != FCGPU_R_VLAN_REJECT)
                 p->set_anno_u16(VLAN_TCI_ANNO_OFFSET, a.vlan_tci);    // StripEtherVLANHeader
             if (reason == FCGPU_R_OK || reason >= FCGPU_R_NO_MATCH) {
+                if (_cfg.rewrite && _iprw[i])                          // DecIPTTL / SetIPChecksum
+                    memcpy(p->data() + a.nh + 8, &_iprw[i], 4);
                 p->set_network_header(a.nh, a.th);                     // set_ip_header / set_ip6_header
                 if (a.length < p->length()) p->take(p->length() - a.length);
                 if (a.ipver == 6) p->set_anno_u8(IP6_NXT_ANNO_OFFSET, a.ip6_nxt);
@@ -364,14 +382,16 @@ class GPUIPCheckClassify : public Element {
     template <class Idx>
     void emit_run(uint32_t port, uint32_t s, uint32_t e, Idx idx) {
         const bool nomatch = port == _cfg.nports && _cfg.classify == FCGPU_CLS_PROGRAM;
-        if (nomatch || _flow_cap) {
+        const bool setck = port == _cfg.nports && (_cfg.rewrite & FCGPU_RW_SETCKSUM);
+        if (nomatch || setck || _flow_cap) {
             // the last slot mixes invalid packets (output N) and packets no
             // rule matched (killed); a full flow table kills new flows. Keep
             // input order for the rest.
             uint32_t w = s;
             for (uint32_t j = s; j < e; ++j) {
                 const uint32_t i = idx(j);
-                if (nomatch && (_verdict[i] & 0xff) == FCGPU_R_NO_MATCH) {
+                if ((nomatch && (_verdict[i] & 0xff) == FCGPU_R_NO_MATCH) ||
+                    (setck && (_verdict[i] & 0xff) == FCGPU_R_SETCKSUM_BAD)) {
                     _pkts[i]->kill();
                 } else if (_flow_cap && _flowid[i] == FCGPU_FLOW_FULL) {
                     ++_flow_drops;
@@ -418,6 +438,7 @@ class GPUIPCheckClassify : public Element {
     int _flow_anno = 28;
     uint64_t _flow_drops = 0;
     std::vector<uint32_t> _flowid;
+    std::vector<uint32_t> _iprw;
     std::vector<uint32_t> _keep;
     fcgpu_cfg _cfg;
     fcgpu_ctx *_ctx = nullptr;

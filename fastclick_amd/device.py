@@ -35,7 +35,8 @@ class DeviceBatch:
 
 class DeviceOutputs:
     def __init__(self, n, nports, device="cuda", *, verdict=True, hash=True, anno=False,
-                 perm=False, port_start=False, partition=N.PART_GLOBAL, tile_perm=False, flowid=False):
+                 perm=False, port_start=False, partition=N.PART_GLOBAL, tile_perm=False, flowid=False,
+                 ip_rw=False):
         torch = _torch()
         self.n = n
         self.nports = nports
@@ -44,6 +45,7 @@ class DeviceOutputs:
         self.verdict = mk(n, torch.int16) if verdict else None
         self.hash = mk(n, torch.int32) if hash else None
         self.flowid = mk(n, torch.int32) if flowid else None
+        self.ip_rw = mk(n, torch.int32) if ip_rw else None
         self.anno = mk(n * 16, torch.uint8) if anno else None
         tile = partition == N.PART_TILE
         self.perm = mk(n, torch.int32) if perm else None
@@ -57,7 +59,7 @@ class DeviceOutputs:
         return dict(verdict=p(self.verdict), hash=p(self.hash), anno=p(self.anno),
                     perm=p(self.perm), port_start=p(self.port_start),
                     tile_count=p(self.tile_count), partition=self.partition,
-                    tile_perm=p(self.tile_perm), flowid=p(self.flowid))
+                    tile_perm=p(self.tile_perm), flowid=p(self.flowid), ip_rw=p(self.ip_rw))
 
     def numpy(self):
         out = {}
@@ -68,6 +70,8 @@ class DeviceOutputs:
             out["port"] = (v >> 8).astype(np.uint8)
         if self.hash is not None:
             out["hash"] = self.hash.cpu().numpy().view(np.uint32)
+        if self.ip_rw is not None:
+            out["ip_rw"] = self.ip_rw.cpu().numpy().view(np.uint32)
         if self.flowid is not None:
             out["flowid"] = self.flowid.cpu().numpy().view(np.uint32)
         if self.anno is not None:
@@ -118,7 +122,7 @@ def process_batches(batches, cfg, *, anno=True, perm=True, device_index=0, parti
                 db = DeviceBatch.upload(batch, device=f"cuda:{device_index}")
                 outs = DeviceOutputs(batch.n, cfg.nports, device=f"cuda:{device_index}",
                                      anno=anno, perm=perm, port_start=perm, partition=partition,
-                                     flowid=max_flows > 0)
+                                     flowid=max_flows > 0, ip_rw=cfg.rewrite != 0)
                 run_device(ctx, db, outs)
                 torch.cuda.synchronize()
                 r = outs.numpy()

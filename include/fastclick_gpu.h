@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 6
+#define FCGPU_ABI_VERSION 7
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -75,7 +75,10 @@ extern "C" {
 #define FCGPU_R_L4_PROTO    10  /* NOT_UDP / NOT_TCP                         */
 #define FCGPU_R_L4_LENGTH   11  /* BAD_LENGTH                                */
 #define FCGPU_R_L4_CKSUM    12  /* BAD_CHECKSUM (pseudo-header checksum)     */
-#define FCGPU_NREASON_SLOTS 12  /* counters for reasons 0-5, 7-12            */
+/* Header rewrite stage (cfg.rewrite), after the classifier, on packets it let through: */
+#define FCGPU_R_TTL_EXPIRED 13  /* DecIPTTL output 1: ip_ttl <= 1 (decipttl.cc:62-65)          */
+#define FCGPU_R_SETCKSUM_BAD 14 /* SetIPChecksum "bad input packet": kill (setipchecksum.cc:44-56) */
+#define FCGPU_NREASON_SLOTS 14  /* counters for reasons 0-5, 7-14            */
 /* Reasons >= FCGPU_R_NO_MATCH are decided after CheckIPHeader accepted the
  * packet: they count in "count", not in "drops". */
 
@@ -105,6 +108,16 @@ extern "C" {
 #define FCGPU_L4_UDP  1
 #define FCGPU_L4_TCP  2
 
+/* rewrite flags: header rewrites after the classifier on IPv4 packets it sent
+ * to an output. The rewritten bytes 8..11 of the IP header
+ * (ttl, protocol, checksum) come back in fcgpu_out.ip_rw; with
+ * FCGPU_RW_INPLACE they are also stored into the arena (device path). */
+#define FCGPU_RW_DECTTL   1u  /* DecIPTTL: ttl <= 1 -> FCGPU_R_TTL_EXPIRED, else ttl-1 and the
+                                 RFC 1624 incremental checksum (elements/ip/decipttl.cc:52-78) */
+#define FCGPU_RW_SETCKSUM 2u  /* SetIPChecksum: full header checksum (elements/ip/setipchecksum.cc:38-58),
+                                 after DecIPTTL when both are set                          */
+#define FCGPU_RW_INPLACE  4u
+
 #define FCGPU_MAX_PORTS   64
 #define FCGPU_MAX_ADDRS   16
 
@@ -133,6 +146,8 @@ typedef struct fcgpu_cfg {
     uint32_t l4_mode;         /* FCGPU_L4_*                                               */
     uint32_t l4_checksum;     /* CheckUDPHeader/CheckTCPHeader CHECKSUM (reference default
                                  TRUE: checkudpheader.cc:54, checktcpheader.cc)          */
+    uint32_t rewrite;         /* FCGPU_RW_* (IPv4 check modes)                            */
+    uint32_t ttl_multicast;   /* DecIPTTL MULTICAST (default true: decrement multicast too) */
 } fcgpu_cfg;
 
 /* Optional per-packet annotations (16 B), mirroring what the reference
@@ -178,6 +193,9 @@ typedef struct fcgpu_out {
     uint8_t    *tile_perm;    /* TILE: [n] index within the tile, grouped by output      */
     uint32_t   *flowid;       /* [n] flow ID from the context's flow table (fcgpu_flow_enable);
                                  FCGPU_FLOW_NONE for packets that reach no flow manager */
+    uint32_t   *ip_rw;        /* [n] with cfg.rewrite: IP header bytes 8..11 after the rewrite
+                                 (little-endian load: ttl | proto << 8 | checksum bytes << 16);
+                                 written for packets the rewrite stage changed, else 0  */
 } fcgpu_out;
 
 typedef struct fcgpu_ctx fcgpu_ctx;
@@ -185,13 +203,14 @@ typedef struct fcgpu_ctx fcgpu_ctx;
 /* Counter vector layout returned by fcgpu_read_counters (uint64):
  *   [0] count (valid packets)         CheckIPHeader "count"
  *   [1] drops                         CheckIPHeader "drops"
- *   [2 .. 2+12) reason slots for reasons 0-5, 7, 8 ("drop_details") and
- *               9-12 (no classifier match, L4 checks; not drops of the checker)
- *   [14 .. 14+nports+1) per-output packet counts, last = invalid list       */
+ *   [2 .. 2+14) reason slots for reasons 0-5, 7, 8 ("drop_details") and
+ *               9-14 (no classifier match, L4 checks, DecIPTTL / SetIPChecksum;
+ *               not drops of the checker)
+ *   [16 .. 16+nports+1) per-output packet counts, last = invalid list       */
 #define FCGPU_CTR_COUNT   0
 #define FCGPU_CTR_DROPS   1
 #define FCGPU_CTR_REASON  2
-#define FCGPU_CTR_PORT    14
+#define FCGPU_CTR_PORT    16
 #define FCGPU_NCOUNTERS   (FCGPU_CTR_PORT + FCGPU_MAX_PORTS + 1)
 /* On the device the vector is kept in FCGPU_CTR_SHARDS replicas (tiles add to
  * replica tile % FCGPU_CTR_SHARDS) and summed on read, like per_thread<>

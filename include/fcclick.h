@@ -46,6 +46,8 @@ typedef struct fcclick_result {
     size_t    handlers_cap;
     uint8_t  *out_paint;    /* [n] PAINT_ANNO (anno u8 @17) on departure (may be NULL)     */
     uint32_t *out_flow;     /* [n] anno u32 @28 (FLOWID_ANNO default) on departure (may be NULL) */
+    uint32_t *out_ip8;      /* [n] network header bytes 8..11 (ttl, proto, checksum) on
+                               departure, little-endian (may be NULL)                  */
 } fcclick_result;
 
 /* Run a graph  Source(frames, BURST) -> conf => [0 .. nsinks-1] Sink  over n

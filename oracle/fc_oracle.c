@@ -351,6 +351,50 @@ static int check_l4(const fcgpu_cfg *c, const uint8_t *f, const fcgpu_anno *a)
     return FCGPU_R_OK;
 }
 
+/* Header rewrites after the classifier, on a copy of IP header bytes 8..11.
+ * DecIPTTL::simple_action (elements/ip/decipttl.cc:52-78) and
+ * SetIPChecksum::simple_action (elements/ip/setipchecksum.cc:38-58). */
+static void rewrite_ip4(const fcgpu_cfg *c, const uint8_t *f, fco_result *r)
+{
+    fcgpu_anno *a = &r->anno;
+    const uint8_t *ip = f + a->nh;
+    uint8_t b[4] = {ip[8], ip[9], ip[10], ip[11]};
+    int changed = 0;
+    if (c->rewrite & FCGPU_RW_DECTTL) {
+        int mcast = (ip[16] & 0xf0) == 0xe0;          /* IPAddress::is_multicast */
+        if (c->ttl_multicast || !mcast) {
+            if (b[0] <= 1) {
+                r->reason = FCGPU_R_TTL_EXPIRED;
+                r->port = (uint8_t)c->nports;
+                return;
+            }
+            b[0]--;
+            unsigned long sum = (~(unsigned long)((b[2] << 8) | b[3]) & 0xFFFF) + 0xFEFF;
+            uint16_t v = (uint16_t)(sum + (sum >> 16));   /* htons() takes a uint16_t */
+            uint16_t ns = (uint16_t)~v;
+            b[2] = (uint8_t)(ns >> 8);
+            b[3] = (uint8_t)ns;
+            changed = 1;
+        }
+    }
+    if (c->rewrite & FCGPU_RW_SETCKSUM) {
+        uint32_t plen = (uint32_t)a->length - a->nh, hl = (uint32_t)(ip[0] & 15) << 2;
+        if (plen < 20 || hl < 20 || hl > plen) {
+            r->reason = FCGPU_R_SETCKSUM_BAD;
+            r->port = (uint8_t)c->nports;
+            return;
+        }
+        uint8_t hdr[60];
+        memcpy(hdr, ip, hl);
+        memcpy(hdr + 8, b, 4);
+        hdr[10] = hdr[11] = 0;
+        uint16_t ck = fco_in_cksum(hdr, (int)hl);     /* stored as a host-order u16 */
+        memcpy(b + 2, &ck, 2);
+        changed = 1;
+    }
+    if (changed) r->ip_rw = (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 | (uint32_t)b[3] << 24;
+}
+
 void fco_process_packet(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, fco_result *r)
 {
     memset(r, 0, sizeof(*r));
@@ -425,6 +469,8 @@ void fco_process_packet(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, fco_
     default: port = 0;
     }
     r->port = (uint8_t)port;
+    if (r->reason == FCGPU_R_OK && !v6 && (c->rewrite & (FCGPU_RW_DECTTL | FCGPU_RW_SETCKSUM)))
+        rewrite_ip4(c, f, r);
 }
 
 static int reason_slot(int r) { return r < 6 ? r : r - 1; }
@@ -433,13 +479,13 @@ void fco_process_batch(const fcgpu_cfg *c, const uint8_t *arena, const uint32_t 
                        uint32_t n, uint16_t *verdict, uint32_t *hash, fcgpu_anno *anno,
                        uint32_t *perm, uint32_t *port_start, uint64_t *ctr)
 {
-    fco_process_batch2(c, arena, desc, n, verdict, hash, anno, perm, port_start, NULL, NULL, ctr);
+    fco_process_batch2(c, arena, desc, n, verdict, hash, anno, perm, port_start, NULL, NULL, ctr, NULL);
 }
 
 void fco_process_batch2(const fcgpu_cfg *c, const uint8_t *arena, const uint32_t *desc,
                         uint32_t n, uint16_t *verdict, uint32_t *hash, fcgpu_anno *anno,
                         uint32_t *perm, uint32_t *port_start, uint32_t *perm_tile,
-                        uint16_t *tile_count, uint64_t *ctr)
+                        uint16_t *tile_count, uint64_t *ctr, uint32_t *ip_rw)
 {
     int nb = (int)c->nports + 1;
     int *port = (int *)malloc(sizeof(int) * (n ? n : 1));
@@ -449,6 +495,7 @@ void fco_process_batch2(const fcgpu_cfg *c, const uint8_t *arena, const uint32_t
         if (verdict) verdict[i] = (uint16_t)(r.reason | (r.port << 8));
         if (hash) hash[i] = r.hash;
         if (anno) anno[i] = r.anno;
+        if (ip_rw) ip_rw[i] = r.ip_rw;
         port[i] = r.port;
         if (ctr) {
             if (r.reason == FCGPU_R_OK) ctr[FCGPU_CTR_COUNT]++;
@@ -530,7 +577,10 @@ void fco_flow_batch(fco_flowtab *t, const uint8_t *arena, const uint32_t *desc, 
     for (uint32_t i = 0; i < n; i++) {
         uint32_t reason = verdict[i] & 0xff;
         flowid[i] = FCGPU_FLOW_NONE;
-        if (anno[i].ipver != 4 || (reason != FCGPU_R_OK && reason != FCGPU_R_NO_MATCH))
+        /* the manager sits after the checks, before the classifier and the
+         * header rewrites: packets those drop still have a flow */
+        if (anno[i].ipver != 4 || (reason != FCGPU_R_OK && reason != FCGPU_R_NO_MATCH &&
+                                   reason != FCGPU_R_TTL_EXPIRED && reason != FCGPU_R_SETCKSUM_BAD))
             continue;
         const uint8_t *nh = arena + desc[2 * i] + anno[i].nh;
         const uint8_t *th = arena + desc[2 * i] + anno[i].th;

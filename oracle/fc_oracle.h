@@ -28,6 +28,7 @@ typedef struct fco_result {
     uint8_t    port;     /* output index; nports for the invalid list */
     uint32_t   hash;
     fcgpu_anno anno;
+    uint32_t   ip_rw;    /* IP header bytes 8..11 after cfg.rewrite (0 if unchanged) */
 } fco_result;
 
 /* A2 (+A4/A13/A14): one packet through the configured check chain, then
@@ -43,11 +44,12 @@ void fco_process_batch(const fcgpu_cfg *cfg, const uint8_t *arena, const uint32_
                        uint32_t n, uint16_t *verdict, uint32_t *hash, fcgpu_anno *anno,
                        uint32_t *perm, uint32_t *port_start, uint64_t *counters);
 
-/* Same, plus the FCGPU_PART_TILE outputs (perm_tile, tile_count). */
+/* Same, plus the FCGPU_PART_TILE outputs (perm_tile, tile_count) and the
+ * header rewrites (ip_rw, may be NULL). */
 void fco_process_batch2(const fcgpu_cfg *cfg, const uint8_t *arena, const uint32_t *desc,
                         uint32_t n, uint16_t *verdict, uint32_t *hash, fcgpu_anno *anno,
                         uint32_t *perm, uint32_t *port_start, uint32_t *perm_tile,
-                        uint16_t *tile_count, uint64_t *counters);
+                        uint16_t *tile_count, uint64_t *counters, uint32_t *ip_rw);
 
 /* Decision program for FCGPU_CLS_PROGRAM (A11): the oracle keeps one
  * (process-global; test use is single-threaded). Same step format as the ABI. */

@@ -44,7 +44,7 @@ def load():
     lib.fco_process_batch2.restype = None
     lib.fco_process_batch2.argtypes = [C.POINTER(N.fcgpu_cfg), C.c_void_p, C.c_void_p, C.c_uint32,
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                       C.c_void_p, C.c_void_p, C.c_void_p]
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.fco_set_program.restype = None
     lib.fco_set_program.argtypes = [C.c_uint32, C.POINTER(N.fcgpu_step), C.c_uint32, C.c_int32]
     lib.fco_process_batch.restype = None
@@ -97,11 +97,12 @@ def process_batch(cfg, batch, program=None):
     ntiles = (n + N.TILE - 1) // N.TILE
     perm_tile = np.zeros(n, np.uint32)
     tile_count = np.zeros(ntiles * (cfg.nports + 1), np.uint16)
+    ip_rw = np.zeros(n, np.uint32)
     lib.fco_process_batch2(C.byref(cfg), _p(arena), _p(desc), n, _p(verdict), _p(hsh), _p(anno),
-                           _p(perm), _p(start), _p(perm_tile), _p(tile_count), _p(ctr))
+                           _p(perm), _p(start), _p(perm_tile), _p(tile_count), _p(ctr), _p(ip_rw))
     return dict(verdict=verdict, reason=(verdict & 0xFF).astype(np.uint8),
                 port=(verdict >> 8).astype(np.uint8), hash=hsh, anno=anno, perm=perm,
-                port_start=start, perm_tile=perm_tile, tile_count=tile_count, counters=ctr)
+                port_start=start, perm_tile=perm_tile, tile_count=tile_count, counters=ctr, ip_rw=ip_rw)
 
 
 class FlowTable:

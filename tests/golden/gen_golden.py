@@ -840,6 +840,88 @@ def run_flow(b, tmp):
     return dict(flowid=fid)
 
 
+def make_rw_set(n=3000, seed=2030):
+    """IPv4 frames for DecIPTTL / SetIPChecksum: TTL 0, 1, 2, random, 255;
+    multicast destinations (224.0.0.0/4) on ~10%; IP options on 10%; ~2% bad
+    checksums (CheckIPHeader drops them); and, for the MarkIPHeader ->
+    SetIPChecksum run, ~3% of headers that do not fit (hl < 5 words, hl past
+    the frame, frames cut inside the header)."""
+    rng = np.random.default_rng(seed)
+    fl = synth._rand_flows(rng, n)
+    mc = rng.random(n) < 0.1
+    mdst = ((0xE0 + rng.integers(0, 16, n, dtype=np.uint64)) << np.uint64(24)) | (fl["dst"] & np.uint64(0xFFFFFF))
+    fl["dst"] = np.where(mc, mdst, fl["dst"])
+    flen = rng.choice([60, 60, 74, 98, 128], n)
+    hdr = synth.build_headers(n, **fl, frame_len=flen)
+    b = synth.pack(hdr, flen, meta=dict(set="rw", seed=seed))
+    synth.add_ip_options(b, 0.1, seed=seed + 1)
+    A = b.arena
+    ttl = rng.choice([0, 1, 2, 3, 64, 128, 255], n, p=[0.05, 0.05, 0.05, 0.05, 0.4, 0.2, 0.2])
+    ttl = np.where(rng.random(n) < 0.3, rng.integers(0, 256, n), ttl)
+    for i in range(n):
+        o = int(b.desc[i, 0]) + 14
+        A[o + 8] = ttl[i]
+        synth._refresh_cksum(A, o)
+    kind = synth.inject_errors(b, 0.02, seed=seed + 2, kinds=[synth.ERR_CKSUM])
+    bad = np.full(n, -1, np.int8)
+    r = rng.random(n)
+    frames = b.frames()
+    for i in range(n):
+        if r[i] < 0.01:                      # hl < 5 words
+            fr = bytearray(frames[i]); fr[14] = 0x40 | int(rng.integers(0, 5)); frames[i] = bytes(fr); bad[i] = 0
+        elif r[i] < 0.02:                    # hl past the frame
+            fr = bytearray(frames[i]); fr[14] = 0x4F; frames[i] = bytes(fr[:14 + 40]); bad[i] = 1
+        elif r[i] < 0.03:                    # frame cut inside the header
+            frames[i] = frames[i][:14 + int(rng.integers(0, 20))]; bad[i] = 2
+    return synth.from_frames(frames, meta=dict(set="rw", seed=seed)), kind, bad
+
+
+def run_rw(b, tmp, bad):
+    """Per packet: IP header bytes 8..11 after the rewrite as the reference
+    dumps them (little-endian u32), 0xFFFFFFFF when the element sent the packet
+    elsewhere: DecIPTTL output 1 (ttl <= 1) or CheckIPHeader / SetIPChecksum
+    drops (a separate mask says which)."""
+    pcap = os.path.join(tmp, "rw.pcap")
+    write_pcap(pcap, b.frames())
+    res = {}
+
+    def grab(name, off):
+        out = np.full(b.n, 0xFFFFFFFF, np.uint32)
+        for i, (_, data) in read_pcap(os.path.join(tmp, name)).items():
+            out[i] = int.from_bytes(data[off + 8:off + 12], "little")
+        return out
+
+    def present(name):
+        m = np.zeros(b.n, bool)
+        for i in read_pcap(os.path.join(tmp, name)):
+            m[i] = True
+        return m
+
+    for tag, dec in (("dec", "DecIPTTL"), ("decnm", "DecIPTTL(MULTICAST false)")):
+        click(CLICK, f"FromDump(rw.pcap, STOP true, TIMING false) -> Strip(14) -> CheckIPHeader(CHECKSUM true) "
+                     f"-> d :: {dec} -> ToDump({tag}_ok.pcap); d[1] -> ToDump({tag}_exp.pcap);", tmp)
+        res[tag] = grab(f"{tag}_ok.pcap", 0)
+        res[tag + "_expired"] = present(f"{tag}_exp.pcap")
+    click(CLICK, "FromDump(rw.pcap, STOP true, TIMING false) -> Strip(14) -> CheckIPHeader(CHECKSUM true) "
+                 "-> d :: DecIPTTL -> SetIPChecksum -> ToDump(decset_ok.pcap); d[1] -> Discard;", tmp)
+    res["decset"] = grab("decset_ok.pcap", 0)
+    # MarkIPHeader asserts that the header fits the buffer (packet.hh:2450):
+    # frames whose header runs past their end are left out of this run
+    # (0xFFFFFFFE: not pinned); hl < 20 is SetIPChecksum's own drop
+    fr = b.frames()
+    keep = [i for i in range(b.n) if bad[i] not in (1, 2)]
+    with open(os.path.join(tmp, "rw_mark.pcap"), "wb") as f:
+        f.write(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, 65535, 1))
+        for i in keep:
+            f.write(struct.pack("<IIII", T0 + i, 0, len(fr[i]), len(fr[i])))
+            f.write(fr[i])
+    click(CLICK, "FromDump(rw_mark.pcap, STOP true, TIMING false) -> MarkIPHeader(14) -> SetIPChecksum "
+                 "-> ToDump(set_ok.pcap);", tmp)
+    res["set"] = grab("set_ok.pcap", 14)
+    res["set"][(bad == 1) | (bad == 2)] = 0xFFFFFFFE
+    return res
+
+
 def run_kat(tmp):
     """click_in_cksum on random buffers (odd lengths included) and IPFlowID /
     IP6FlowID hashcodes on random tuples, from the reference harness."""
@@ -869,7 +951,7 @@ def sha(path):
     return hashlib.sha256(open(path, "rb").read()).hexdigest()
 
 
-def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "kat")):
+def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "rw", "kat")):
     prov_path = os.path.join(HERE, "PROVENANCE.json")
     prov = json.load(open(prov_path)) if os.path.exists(prov_path) else {}
     prov.update(generator="tests/golden/gen_golden.py", click=CLICK, click_sha256=sha(CLICK),
@@ -922,6 +1004,13 @@ def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "k
                 v = rf["flowid"][rf["flowid"] != 0xFFFFFFFF]
                 print("flow: classified", len(v), "flows", int(v.max()) + 1, "dropped",
                       int((rf["flowid"] == 0xFFFFFFFF).sum()))
+        if "rw" in sets:
+            rb, rkind, rbad = make_rw_set()
+            rr = run_rw(rb, tmp, rbad)
+            np.savez_compressed(os.path.join(HERE, "rw.npz"), arena=rb.arena, desc=rb.desc, kind=rkind, bad=rbad,
+                                **rr)
+            print("rw: dec ok", int((rr["dec"] != 0xFFFFFFFF).sum()), "expired", int(rr["dec_expired"].sum()),
+                  "nm expired", int(rr["decnm_expired"].sum()), "set ok", int((rr["set"] != 0xFFFFFFFF).sum()))
         if "combo" in sets:
             rc = run_combo(tmp)
             np.savez_compressed(os.path.join(HERE, "combo.npz"), **rc)
@@ -946,6 +1035,8 @@ def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "k
         "combo": "IPInputCombo(7, BADSRC, GOODDST) on the ip4 set: survivors and their ip_len",
         "flow": "Strip(14) -> CheckIPHeader(CHECKSUM true) -> FlowIPManagerHMP -> StoreFlowID(OFFSET 0) (click4: "
                 "--enable-research --enable-flow-dynamic --enable-ctx): per-packet flow ID = stored ID - 1",
+        "rw": "Strip(14) -> CheckIPHeader(CHECKSUM true) -> DecIPTTL[(MULTICAST false)] [-> SetIPChecksum] -> ToDump, "
+              "DecIPTTL[1] -> ToDump; MarkIPHeader(14) -> SetIPChecksum -> ToDump: IP header bytes 8..11 per packet",
         "kat": "fcref: click_in_cksum (lib/in_cksum.c), IPFlowID/IP6FlowID::hashcode (headers)",
     })
     prov["ipc_rules"] = IPC_RULES
@@ -955,4 +1046,4 @@ def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "k
 
 
 if __name__ == "__main__":
-    main(tuple(sys.argv[1:]) or ("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "kat"))
+    main(tuple(sys.argv[1:]) or ("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "rw", "kat"))

@@ -205,3 +205,22 @@ def test_config_flow_keywords():
         K.check_config("GPUIPCheckClassify(MODE AUTO, FLOW_CAPACITY 10)")
     with pytest.raises(K.ConfigError, match="FLOWID_ANNO"):
         K.check_config("GPUIPCheckClassify(FLOWID_ANNO 46)")
+
+
+@pytest.mark.gpu
+def test_element_dec_ttl_golden():
+    """GPUIPCheckClassify(DEC_TTL true[, SET_CHECKSUM true]): survivors carry
+    the reference's rewritten ttl/checksum bytes; TTL-expired packets leave on
+    output N (DecIPTTL output 1) -- tests/golden/rw.npz."""
+    from fastclick_amd import click as K
+    from tests.test_golden import load, batch_of
+    g = load("rw")
+    b = batch_of(g)
+    for conf, key in (("DEC_TTL true", "dec"), ("DEC_TTL true, TTL_MULTICAST false", "decnm"),
+                      ("DEC_TTL true, SET_CHECKSUM true", "decset")):
+        r = K.run_element(f"GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 2, {conf})", b, nsinks=3)
+        ok = g[key] != 0xFFFFFFFF
+        assert (r["port"][ok] < 2).all(), key
+        assert np.array_equal(r["ip8"][ok], g[key][ok]), key
+        if key != "decset":
+            assert (r["port"][g[key + "_expired"]] == 2).all(), key
