@@ -14,7 +14,8 @@ LIBFCGPU = os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 7
+ABI_VERSION = 8
+SPAN_SLOTS = 3
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
     R_BAD_IP6, R_VLAN_REJECT, R_NO_MATCH, R_L4_PROTO, R_L4_LENGTH, R_L4_CKSUM, \
@@ -144,6 +145,9 @@ FCGPU_SYMBOLS = {
     "fcgpu_set_program": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(fcgpu_step), C.c_uint32,
                                     C.c_int32]),
     "fcgpu_set_host_threads": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "fcgpu_span_submit": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32,
+                                    C.POINTER(fcgpu_out)]),
+    "fcgpu_span_wait": (C.c_int, [C.c_void_p, C.c_uint32]),
     "fcgpu_flow_enable": (C.c_int, [C.c_void_p, C.c_uint32]),
     "fcgpu_flow_reset": (C.c_int, [C.c_void_p]),
     "fcgpu_flow_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
@@ -290,6 +294,18 @@ class Context:
                         flowid or None, ip_rw or None)
         self._chk(self.lib.fcgpu_process_host(self.h, frames, lens_ptr, n, C.byref(out)),
                   "fcgpu_process_host")
+
+    def span_submit(self, slot, span_ptr, span_bytes, desc_ptr, n, *, verdict=0, hash=0, anno=0, perm=0,
+                    port_start=0, tile_count=0, partition=PART_GLOBAL, tile_perm=0, flowid=0, ip_rw=0):
+        """Asynchronous: frames already contiguous in host memory (pinned for DMA)."""
+        out = fcgpu_out(verdict or None, hash or None, anno or None, perm or None,
+                        port_start or None, tile_count or None, partition, 0, tile_perm or None,
+                        flowid or None, ip_rw or None)
+        self._chk(self.lib.fcgpu_span_submit(self.h, slot, span_ptr, span_bytes, desc_ptr, n, C.byref(out)),
+                  "fcgpu_span_submit")
+
+    def span_wait(self, slot):
+        self._chk(self.lib.fcgpu_span_wait(self.h, slot), "fcgpu_span_wait")
 
     def set_program(self, kind, steps, output_everything=-1):
         """steps: sequence of (offset, value, mask, yes, no, flags) or fcgpu_step."""

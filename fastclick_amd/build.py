@@ -22,10 +22,12 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 FCGPU_SRC = [os.path.join(CSRC, "fcgpu_api.hip")]
-FCGPU_DEPS = FCGPU_SRC + [os.path.join(CSRC, "fcgpu_device.hh"), os.path.join(INC, "fastclick_gpu.h")]
-FCCLICK_SRC = [os.path.join(CSRC, "host", f) for f in ("fcclick_capi.cc",)]
+FCGPU_DEPS = FCGPU_SRC + [os.path.join(CSRC, "fcgpu_device.hh"), os.path.join(CSRC, "fcgpu_flow.hh"),
+                          os.path.join(INC, "fastclick_gpu.h")]
+FCCLICK_SRC = [os.path.join(CSRC, "host", f) for f in ("fcclick_capi.cc", "pcap_reader.cc")]
 FCCLICK_DEPS = FCCLICK_SRC + [os.path.join(CSRC, "host", f) for f in
-                              ("click_model.hh", "gpu_element.hh")] + [os.path.join(INC, "fcclick.h")]
+                              ("click_model.hh", "gpu_element.hh", "program_text.hh")] + \
+    [os.path.join(INC, f) for f in ("fcclick.h", "fcpcap.h", "fastclick_gpu.h")]
 
 
 def _stale(out, deps):

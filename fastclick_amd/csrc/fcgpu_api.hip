@@ -127,6 +127,20 @@ struct HostSlot {
     uint32_t base = 0, n = 0;
 };
 
+// One in-flight fcgpu_span_submit: device copy of the span and descriptors,
+// device outputs, the stream it runs on.
+struct SpanSlot {
+    hipStream_t own = nullptr, s = nullptr;
+    uint8_t *d_span = nullptr;
+    size_t span_cap = 0;
+    uint32_t *d_desc = nullptr;
+    uint16_t *d_v = nullptr, *d_tc = nullptr;
+    uint32_t *d_h = nullptr, *d_perm = nullptr, *d_start = nullptr, *d_fl = nullptr, *d_rw = nullptr;
+    fcgpu_anno *d_an = nullptr;
+    uint8_t *d_tp = nullptr;
+    bool busy = false;
+};
+
 inline uint32_t span(uint32_t n, uint32_t part, uint32_t np) { return (uint32_t)((uint64_t)n * part / np); }
 
 bool host_pinned(const void *p) {
@@ -171,6 +185,8 @@ struct fcgpu_ctx {
     HostSlot slot[kSlots];
     uint32_t slot_cap = 0;
     Pool pool;
+    // fcgpu_span_submit slots
+    SpanSlot span[FCGPU_SPAN_SLOTS];
     // flow table (fcgpu_flow_enable)
     uint32_t max_flows = 0, flow_slots = 0, flow_words = 0;
     FlowArgs fl{};            // device pointers; fl.slots == nullptr: disabled
@@ -185,6 +201,15 @@ struct fcgpu_ctx {
 // whole frame when the L4 checksum covers the segment.
 static uint32_t host_capture(const fcgpu_ctx *c) {
     return (c->cfg.l4_mode != FCGPU_L4_NONE && c->cfg.l4_checksum) ? 0xffffffffu : kHostCap;
+}
+
+// hipMemset can complete after work already queued on non-blocking streams
+// (it is ordered on the null stream only): every setup-time fill waits for
+// itself before the buffer is handed to a stream.
+static hipError_t memset_sync(void *p, int v, size_t bytes) {
+    hipError_t e = hipMemsetAsync(p, v, bytes, nullptr);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(nullptr);
 }
 
 static std::string g_open_err;
@@ -282,7 +307,7 @@ static int process_host_whole(fcgpu_ctx *c, const uint8_t *const *frames, const 
         HIPCHK(c, hipHostMalloc((void **)&c->h_arena, arena_cap, hipHostMallocDefault));
         HIPCHK(c, hipHostMalloc((void **)&c->h_desc, sizeof(uint32_t) * 2 * c->max_batch, hipHostMallocDefault));
         HIPCHK(c, hipMalloc(&c->d_arena, arena_cap));
-        HIPCHK(c, hipMemset(c->d_arena, 0, arena_cap));
+        HIPCHK(c, memset_sync(c->d_arena, 0, arena_cap));
         c->h_arena_cap = arena_cap;
         HIPCHK(c, hipMalloc(&c->d_desc, sizeof(uint32_t) * 2 * c->max_batch));
         HIPCHK(c, hipMalloc(&c->d_hv, sizeof(uint16_t) * c->max_batch));
@@ -310,7 +335,7 @@ static int process_host_whole(fcgpu_ctx *c, const uint8_t *const *frames, const 
         c->h_arena_cap = 0;
         HIPCHK(c, hipHostMalloc((void **)&c->h_arena, need, hipHostMallocDefault));
         HIPCHK(c, hipMalloc(&c->d_arena, need));
-        HIPCHK(c, hipMemset(c->d_arena, 0, need));
+        HIPCHK(c, memset_sync(c->d_arena, 0, need));
         c->h_arena_cap = need;
     }
     size_t off = 0;
@@ -402,11 +427,11 @@ static void flow_free(fcgpu_ctx *c) {
 // Empty table, IDs from 0 (synchronous).
 static int flow_clear(fcgpu_ctx *c) {
     FlowArgs &F = c->fl;
-    HIPCHK(c, hipMemset(F.slots, 0, sizeof(uint4) * c->flow_slots));
-    HIPCHK(c, hipMemset(F.claim, 0, sizeof(uint32_t) * c->flow_slots));
-    HIPCHK(c, hipMemset(F.first, 0xff, sizeof(uint32_t) * c->flow_slots));
-    HIPCHK(c, hipMemset(F.bitmap, 0, sizeof(uint32_t) * c->flow_words));
-    HIPCHK(c, hipMemset(F.state, 0, sizeof(uint32_t) * 16));
+    HIPCHK(c, memset_sync(F.slots, 0, sizeof(uint4) * c->flow_slots));
+    HIPCHK(c, memset_sync(F.claim, 0, sizeof(uint32_t) * c->flow_slots));
+    HIPCHK(c, memset_sync(F.first, 0xff, sizeof(uint32_t) * c->flow_slots));
+    HIPCHK(c, memset_sync(F.bitmap, 0, sizeof(uint32_t) * c->flow_words));
+    HIPCHK(c, memset_sync(F.state, 0, sizeof(uint32_t) * 16));
     return FCGPU_OK;
 }
 
@@ -482,6 +507,14 @@ void fcgpu_close(fcgpu_ctx *c) {
         hipFree(c->d_htp);
         hipFree(c->d_hflow);
         hipFree(c->d_hrw);
+        for (auto &sp : c->span) {
+            if (sp.s) hipStreamSynchronize(sp.s);
+            for (void *p : {(void *)sp.d_span, (void *)sp.d_desc, (void *)sp.d_v, (void *)sp.d_tc, (void *)sp.d_h,
+                            (void *)sp.d_perm, (void *)sp.d_start, (void *)sp.d_fl, (void *)sp.d_rw, (void *)sp.d_an,
+                            (void *)sp.d_tp})
+                hipFree(p);
+            if (sp.own) hipStreamDestroy(sp.own);
+        }
         flow_free(c);
         hipHostFree(c->h_arena);
         hipHostFree(c->h_desc);
@@ -521,7 +554,7 @@ int fcgpu_open(int device, uint32_t max_batch, fcgpu_ctx **out) {
     chk(hipMalloc(&c->d_totals, sizeof(uint32_t) * kMaxBins), "hipMalloc totals");
     chk(hipMalloc(&c->d_ctr_own, sizeof(unsigned long long) * kCtrWords), "hipMalloc counters");
     c->d_ctr = c->d_ctr_own;
-    if (rc == FCGPU_OK) chk(hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * kCtrWords), "hipMemset");
+    if (rc == FCGPU_OK) chk(memset_sync(c->d_ctr, 0, sizeof(unsigned long long) * kCtrWords), "hipMemset");
     if (rc != FCGPU_OK) {
         g_open_err = c->err;
         fcgpu_close(c);
@@ -672,7 +705,7 @@ static int slot_alloc(fcgpu_ctx *c, HostSlot &sl, uint32_t cap) {
     HIPCHK(c, hipHostMalloc((void **)&sl.h_arena, arena, hipHostMallocDefault));
     HIPCHK(c, hipHostMalloc((void **)&sl.h_desc, sizeof(uint32_t) * 2 * cap, hipHostMallocDefault));
     HIPCHK(c, hipMalloc(&sl.d_arena, arena));
-    HIPCHK(c, hipMemset(sl.d_arena, 0, arena));
+    HIPCHK(c, memset_sync(sl.d_arena, 0, arena));
     HIPCHK(c, hipMalloc(&sl.d_desc, sizeof(uint32_t) * 2 * cap));
     HIPCHK(c, hipMalloc(&sl.d_v, sizeof(uint16_t) * cap));
     HIPCHK(c, hipMalloc(&sl.d_h, sizeof(uint32_t) * cap));
@@ -775,7 +808,7 @@ static int process_host_pipelined(fcgpu_ctx *c, const uint8_t *const *frames, co
             sl.arena_cap = 0;
             HIPCHK(c, hipHostMalloc((void **)&sl.h_arena, want, hipHostMallocDefault));
             HIPCHK(c, hipMalloc(&sl.d_arena, want));
-            HIPCHK(c, hipMemset(sl.d_arena, 0, want));
+            HIPCHK(c, memset_sync(sl.d_arena, 0, want));
             sl.arena_cap = want;
         }
         c->pool.run([&](uint32_t part, uint32_t nparts) {
@@ -852,6 +885,85 @@ int fcgpu_process_host(fcgpu_ctx *c, const uint8_t *const *frames, const uint32_
     return process_host_pipelined(c, frames, lens, n, h);
 }
 
+int fcgpu_span_submit(fcgpu_ctx *c, uint32_t slot, const uint8_t *h_span, size_t bytes, const uint32_t *h_desc,
+                      uint32_t n, const fcgpu_out *h) {
+    if (!c || !h || slot >= FCGPU_SPAN_SLOTS || (n && (!h_span || !h_desc))) return FCGPU_EINVAL;
+    if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "batch larger than max_batch");
+    if (bytes > 0xffffffffull - kArenaPad) return fail(c, FCGPU_EINVAL, "span larger than 4 GiB");
+    SpanSlot &sp = c->span[slot];
+    if (sp.busy) return fail(c, FCGPU_EINVAL, "span slot busy: fcgpu_span_wait it first");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!sp.own) {
+        const size_t m = c->max_batch, tiles = (m + kTile - 1) / kTile;
+        HIPCHK(c, hipStreamCreateWithFlags(&sp.own, hipStreamNonBlocking));
+        HIPCHK(c, hipMalloc(&sp.d_desc, sizeof(uint32_t) * 2 * m));
+        HIPCHK(c, hipMalloc(&sp.d_v, sizeof(uint16_t) * m));
+        HIPCHK(c, hipMalloc(&sp.d_h, sizeof(uint32_t) * m));
+        HIPCHK(c, hipMalloc(&sp.d_an, sizeof(fcgpu_anno) * m));
+        HIPCHK(c, hipMalloc(&sp.d_perm, sizeof(uint32_t) * m));
+        HIPCHK(c, hipMalloc(&sp.d_start, sizeof(uint32_t) * (FCGPU_MAX_PORTS + 2)));
+        HIPCHK(c, hipMalloc(&sp.d_tp, m + kTile));
+        HIPCHK(c, hipMalloc(&sp.d_tc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * tiles));
+        HIPCHK(c, hipMalloc(&sp.d_fl, sizeof(uint32_t) * m));
+        HIPCHK(c, hipMalloc(&sp.d_rw, sizeof(uint32_t) * m));
+    }
+    if (bytes + kArenaPad > sp.span_cap) {
+        HIPCHK(c, hipStreamSynchronize(sp.own));
+        hipFree(sp.d_span);
+        sp.d_span = nullptr;
+        sp.span_cap = 0;
+        const size_t cap = (bytes + kArenaPad + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+        HIPCHK(c, hipMalloc(&sp.d_span, cap));
+        HIPCHK(c, memset_sync(sp.d_span, 0, cap));
+        sp.span_cap = cap;
+    }
+    // a flow table assigns IDs in batch order: every slot then runs on the
+    // context's stream
+    if (c->fl.slots && !c->stream) HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    sp.s = c->fl.slots ? c->stream : sp.own;
+    hipStream_t s = sp.s;
+    if (n == 0) return FCGPU_OK;
+    HIPCHK(c, hipMemcpyAsync(sp.d_span, h_span, bytes, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(sp.d_desc, h_desc, sizeof(uint32_t) * 2 * n, hipMemcpyHostToDevice, s));
+    fcgpu_out d{};
+    d.verdict = h->verdict ? sp.d_v : nullptr;
+    d.hash = h->hash ? sp.d_h : nullptr;
+    d.anno = h->anno ? sp.d_an : nullptr;
+    d.perm = h->perm ? sp.d_perm : nullptr;
+    d.port_start = h->port_start ? sp.d_start : nullptr;
+    d.tile_count = h->tile_count ? sp.d_tc : nullptr;
+    d.partition = h->partition;
+    d.tile_perm = h->tile_perm ? sp.d_tp : nullptr;
+    d.flowid = h->flowid ? sp.d_fl : nullptr;
+    d.ip_rw = h->ip_rw ? sp.d_rw : nullptr;
+    int rc = fcgpu_process(c, sp.d_span, sp.d_desc, n, &d, s);
+    if (rc != FCGPU_OK) return rc;
+    auto back = [&](void *dst, const void *src, size_t b) -> int {
+        if (dst) HIPCHK(c, hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToHost, s));
+        return FCGPU_OK;
+    };
+    const size_t tiles = (n + kTile - 1) / kTile;
+    if ((rc = back(h->verdict, sp.d_v, sizeof(uint16_t) * n)) || (rc = back(h->hash, sp.d_h, sizeof(uint32_t) * n)) ||
+        (rc = back(h->anno, sp.d_an, sizeof(fcgpu_anno) * n)) || (rc = back(h->perm, sp.d_perm, sizeof(uint32_t) * n)) ||
+        (rc = back(h->port_start, sp.d_start, sizeof(uint32_t) * (c->cfg.nports + 2))) ||
+        (rc = back(h->tile_count, sp.d_tc, sizeof(uint16_t) * (c->cfg.nports + 1) * tiles)) ||
+        (rc = back(h->tile_perm, sp.d_tp, n)) || (rc = back(h->flowid, sp.d_fl, sizeof(uint32_t) * n)) ||
+        (rc = back(h->ip_rw, sp.d_rw, sizeof(uint32_t) * n)))
+        return rc;
+    sp.busy = true;
+    return FCGPU_OK;
+}
+
+int fcgpu_span_wait(fcgpu_ctx *c, uint32_t slot) {
+    if (!c || slot >= FCGPU_SPAN_SLOTS) return FCGPU_EINVAL;
+    SpanSlot &sp = c->span[slot];
+    if (!sp.busy) return FCGPU_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    sp.busy = false;
+    HIPCHK(c, hipStreamSynchronize(sp.s));
+    return FCGPU_OK;
+}
+
 int fcgpu_set_host_threads(fcgpu_ctx *c, uint32_t nthreads) {
     if (!c || nthreads == 0 || nthreads > 64) return FCGPU_EINVAL;
     c->pool.resize(nthreads);
@@ -887,7 +999,7 @@ int fcgpu_reset_counters(fcgpu_ctx *c) {
     if (!c) return FCGPU_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipDeviceSynchronize());
-    HIPCHK(c, hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * kCtrWords));
+    HIPCHK(c, memset_sync(c->d_ctr, 0, sizeof(unsigned long long) * kCtrWords));
     return FCGPU_OK;
 }
 

@@ -1,0 +1,202 @@
+// pcap_reader.cc -- pcap ingress (include/fcpcap.h): FromDump's record parsing
+// (elements/userlevel/fromdump.cc:278-316, 418-500) over read() straight into
+// the caller's buffer; descriptors point at the packet bytes in place.
+#include <algorithm>
+#include <errno.h>
+#include <fcntl.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../../include/fcpcap.h"
+
+namespace {
+constexpr uint32_t kMagic = 0xA1B2C3D4u, kMagicNano = 0xA1B23C4Du, kMagicModified = 0xA1B2CD34u;
+inline uint32_t sw32(uint32_t x) { return __builtin_bswap32(x); }
+}  // namespace
+
+struct fcpcap {
+    int fd = -1;
+    bool swapped = false, nano = false;
+    uint32_t extra = 0;          // modified pcap: 8 header bytes after the regular 16
+    int minor = 0, linktype = 0;
+    uint32_t snaplen = 0;
+    std::vector<uint8_t> carry;  // bytes read but not yet handed out (a partial record)
+    bool eof = false;
+    off_t fpos = 24;             // file offset of the next unread byte
+    unsigned threads = 1;        // parallel pread() pieces per fill
+    std::string err;
+};
+
+extern "C" {
+
+int fcpcap_open(const char *path, fcpcap **out, char *err, size_t errcap) {
+    auto fail = [&](const std::string &m) {
+        if (err && errcap) snprintf(err, errcap, "%s", m.c_str());
+        return -1;
+    };
+    if (!path || !out) return fail("null argument");
+    int fd = open(path, O_RDONLY);
+    if (fd < 0) return fail(std::string(path) + ": " + strerror(errno));
+    uint32_t fh[6];
+    ssize_t k = read(fd, fh, sizeof fh);
+    if (k != (ssize_t)sizeof fh) {
+        close(fd);
+        return fail("not a tcpdump file (too short)");
+    }
+    fcpcap *r = new fcpcap;
+    r->fd = fd;
+    uint32_t magic = fh[0];
+    if (magic != kMagic && magic != kMagicNano && magic != kMagicModified) {
+        r->swapped = true;
+        magic = sw32(magic);
+    }
+    if (magic != kMagic && magic != kMagicNano && magic != kMagicModified) {
+        fcpcap_close(r);
+        return fail("not a tcpdump file (bad magic number)");
+    }
+    r->extra = magic == kMagicModified ? 8 : 0;
+    r->nano = magic == kMagicNano;
+    uint32_t ver = r->swapped ? sw32(fh[1]) : fh[1];
+    // version_major / version_minor are 16-bit fields in file order
+    uint16_t vmaj, vmin;
+    memcpy(&vmaj, reinterpret_cast<uint8_t *>(fh) + 4, 2);
+    memcpy(&vmin, reinterpret_cast<uint8_t *>(fh) + 6, 2);
+    if (r->swapped) {
+        vmaj = __builtin_bswap16(vmaj);
+        vmin = __builtin_bswap16(vmin);
+    }
+    (void)ver;
+    if (vmaj != 2) {
+        fcpcap_close(r);
+        return fail("unknown major version " + std::to_string(vmaj));
+    }
+    r->minor = vmin;
+    r->snaplen = r->swapped ? sw32(fh[4]) : fh[4];
+    r->linktype = (int)(r->swapped ? sw32(fh[5]) : fh[5]);
+    *out = r;
+    return 0;
+}
+
+int fcpcap_linktype(const fcpcap *r) { return r ? r->linktype : -1; }
+int fcpcap_set_threads(fcpcap *r, unsigned threads) {
+    if (!r || threads < 1 || threads > 64) return -1;
+    r->threads = threads;
+    return 0;
+}
+uint32_t fcpcap_snaplen(const fcpcap *r) { return r ? r->snaplen : 0; }
+const char *fcpcap_error(const fcpcap *r) { return r ? r->err.c_str() : "null reader"; }
+
+void fcpcap_close(fcpcap *r) {
+    if (!r) return;
+    if (r->fd >= 0) close(r->fd);
+    delete r;
+}
+
+int fcpcap_read(fcpcap *r, uint8_t *buf, size_t cap, uint32_t *desc, uint32_t *wire, uint64_t *ts_ns,
+                uint32_t max, size_t *used) {
+    if (!r || !buf || !desc || !used) return -1;
+    *used = 0;
+    // the carried partial record first, then as much of the file as fits
+    size_t have = r->carry.size() < cap ? r->carry.size() : cap;
+    memcpy(buf, r->carry.data(), have);
+    r->carry.erase(r->carry.begin(), r->carry.begin() + have);
+    if (!r->eof && have < cap && r->carry.empty()) {
+        // the rest of the buffer from the file, as `threads` pread() pieces of
+        // at least 1 MiB (the copy out of the page cache is the host-side cost
+        // of this ingress); a short piece is the end of the file
+        const size_t want = cap - have;
+        const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>(r->threads, want >> 20));
+        std::vector<ssize_t> got(T, 0);
+        std::vector<int> errs(T, 0);
+        const size_t per = (want + T - 1) / T;
+        auto piece = [&](unsigned t) {
+            const size_t b = t * per, e = std::min(want, b + per);
+            size_t done = 0;
+            while (b + done < e) {
+                ssize_t k = pread(r->fd, buf + have + b + done, e - b - done, r->fpos + (off_t)(b + done));
+                if (k < 0) {
+                    if (errno == EINTR) continue;
+                    errs[t] = errno;
+                    break;
+                }
+                if (k == 0) break;
+                done += (size_t)k;
+            }
+            got[t] = (ssize_t)done;
+        };
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < T; ++t) th.emplace_back(piece, t);
+        piece(0);
+        for (auto &x : th) x.join();
+        size_t total = 0;
+        for (unsigned t = 0; t < T; ++t) {
+            if (errs[t]) {
+                r->err = std::string("read: ") + strerror(errs[t]);
+                return -1;
+            }
+            const size_t b = t * per, e = std::min(want, b + per);
+            total += (size_t)got[t];
+            if ((size_t)got[t] < e - b) {   // end of file inside this piece
+                r->eof = true;
+                break;
+            }
+        }
+        r->fpos += (off_t)total;
+        have += total;
+    }
+    const uint32_t hdr = 16 + r->extra;
+    size_t pos = 0;
+    uint32_t n = 0;
+    while (n < max && pos + 16 <= have) {
+        uint32_t h[4];
+        memcpy(h, buf + pos, 16);
+        if (r->swapped)
+            for (auto &x : h) x = sw32(x);
+        // FromDump::read_packet: caplen/len swapped before 2.3 (fromdump.cc:446-453)
+        uint32_t len, caplen, skip = 0;
+        if (r->minor > 3 || (r->minor == 3 && h[2] <= h[3])) {
+            len = h[3];
+            caplen = h[2];
+        } else {
+            len = h[2];
+            caplen = h[3];
+        }
+        if (caplen > 65535) {   // fromdump.cc:460-462
+            r->err = "bad packet header; giving up";
+            return -1;
+        }
+        if (caplen > len) {     // fromdump.cc:463-466
+            skip = caplen - len;
+            caplen = len;
+        }
+        const size_t rec = (size_t)hdr + caplen + skip;
+        if (pos + rec > have) break;
+        desc[2 * n] = (uint32_t)(pos + hdr);
+        desc[2 * n + 1] = caplen;
+        if (wire) wire[n] = len;
+        if (ts_ns) ts_ns[n] = (uint64_t)h[0] * 1000000000ull + (uint64_t)h[1] * (r->nano ? 1ull : 1000ull);
+        ++n;
+        pos += rec;
+    }
+    if (n == 0 && pos + 16 <= have && r->eof && have < cap) {
+        // a record cut short by the end of the file: FromDump stops there
+        have = pos;
+    }
+    // keep what was not handed out for the next call
+    if (pos < have) r->carry.insert(r->carry.begin(), buf + pos, buf + have);
+    if (n == 0 && !r->carry.empty() && (r->eof || have == cap)) {
+        if (have == cap && pos == 0) {
+            r->err = "record larger than the buffer";
+            return -1;
+        }
+        if (r->eof) r->carry.clear();   // truncated final record
+    }
+    *used = pos;
+    return (int)n;
+}
+
+}  // extern "C"

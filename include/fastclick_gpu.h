@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 7
+#define FCGPU_ABI_VERSION 8
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -245,6 +245,22 @@ int  fcgpu_process(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_des
  * otherwise through pinned staging. */
 int  fcgpu_process_host(fcgpu_ctx *ctx, const uint8_t *const *frames,
                         const uint32_t *lens, uint32_t n, const fcgpu_out *h_out);
+
+/* Host-resident batch whose frames already lie in one contiguous buffer
+ * (e.g. pcap records read straight into pinned memory, include/fcpcap.h):
+ * the span and the descriptors go to the device as two H2D copies -- no
+ * per-packet gather -- then the kernels run and the requested outputs are
+ * copied into the host pointers of h_out. Asynchronous: up to
+ * FCGPU_SPAN_SLOTS submissions are in flight, each on its own stream (one
+ * stream for all when a flow table is enabled, which needs batch order);
+ * h_span, h_desc and h_out must stay valid until fcgpu_span_wait(slot).
+ * Pinned buffers (fcgpu_host_alloc) make the copies true DMA. The span must be
+ * readable 128 bytes past every frame start (the context pads its device
+ * copy; bytes past the span are never part of a verdict). */
+#define FCGPU_SPAN_SLOTS 3
+int  fcgpu_span_submit(fcgpu_ctx *ctx, uint32_t slot, const uint8_t *h_span, size_t span_bytes,
+                       const uint32_t *h_desc, uint32_t n, const fcgpu_out *h_out);
+int  fcgpu_span_wait(fcgpu_ctx *ctx, uint32_t slot);
 
 /* Decision programs. A program is the step list the
  * reference's own compiler produces and prints through the `program` handler
