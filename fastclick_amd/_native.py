@@ -153,6 +153,8 @@ FCGPU_SYMBOLS = {
     "fcgpu_flow_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "fcgpu_host_alloc": (C.c_void_p, [C.c_size_t]),
     "fcgpu_host_free": (None, [C.c_void_p]),
+    "fcgpu_host_register": (C.c_int, [C.c_void_p, C.c_size_t, C.c_int]),
+    "fcgpu_host_unregister": (C.c_int, [C.c_void_p]),
     "fcgpu_read_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "fcgpu_reset_counters": (C.c_int, [C.c_void_p]),
     "fcgpu_counters_device": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),

@@ -964,6 +964,22 @@ int fcgpu_span_wait(fcgpu_ctx *c, uint32_t slot) {
     return FCGPU_OK;
 }
 
+int fcgpu_host_register(void *p, size_t bytes, int read_only) {
+    if (!p || !bytes) return FCGPU_EINVAL;
+    hipError_t e = hipHostRegister(p, bytes, read_only ? hipHostRegisterReadOnly : hipHostRegisterDefault);
+    if (e != hipSuccess) {
+        g_open_err = std::string("hipHostRegister: ") + hipGetErrorString(e);
+        (void)hipGetLastError();
+        return FCGPU_ERUNTIME;
+    }
+    return FCGPU_OK;
+}
+
+int fcgpu_host_unregister(void *p) {
+    if (!p) return FCGPU_EINVAL;
+    return hipHostUnregister(p) == hipSuccess ? FCGPU_OK : FCGPU_ERUNTIME;
+}
+
 int fcgpu_set_host_threads(fcgpu_ctx *c, uint32_t nthreads) {
     if (!c || nthreads == 0 || nthreads > 64) return FCGPU_EINVAL;
     c->pool.resize(nthreads);

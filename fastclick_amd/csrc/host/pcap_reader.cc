@@ -4,6 +4,8 @@
 #include <algorithm>
 #include <errno.h>
 #include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <string.h>
 #include <unistd.h>
 
@@ -28,6 +30,8 @@ struct fcpcap {
     bool eof = false;
     off_t fpos = 24;             // file offset of the next unread byte
     unsigned threads = 1;        // parallel pread() pieces per fill
+    const uint8_t *map = nullptr;  // fcpcap_map: the whole file, read-only
+    size_t map_bytes = 0;
     std::string err;
 };
 
@@ -92,8 +96,74 @@ const char *fcpcap_error(const fcpcap *r) { return r ? r->err.c_str() : "null re
 
 void fcpcap_close(fcpcap *r) {
     if (!r) return;
+    if (r->map) munmap(const_cast<uint8_t *>(r->map), r->map_bytes);
     if (r->fd >= 0) close(r->fd);
     delete r;
+}
+
+int fcpcap_map(fcpcap *r, const uint8_t **base, size_t *bytes) {
+    if (!r || !base || !bytes) return -1;
+    if (!r->map) {
+        struct stat st;
+        if (fstat(r->fd, &st) != 0) {
+            r->err = std::string("fstat: ") + strerror(errno);
+            return -1;
+        }
+        void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED | MAP_POPULATE, r->fd, 0);
+        if (m == MAP_FAILED) {
+            r->err = std::string("mmap: ") + strerror(errno);
+            return -1;
+        }
+        r->map = static_cast<const uint8_t *>(m);
+        r->map_bytes = (size_t)st.st_size;
+    }
+    *base = r->map;
+    *bytes = r->map_bytes;
+    return 0;
+}
+
+int fcpcap_index(fcpcap *r, uint32_t max, size_t max_bytes, size_t *chunk_off, size_t *chunk_bytes, uint32_t *desc,
+                 uint32_t *wire, uint64_t *ts_ns) {
+    if (!r || !r->map || !chunk_off || !chunk_bytes || !desc) return -1;
+    const uint32_t hdr = 16 + r->extra;
+    size_t pos = (size_t)r->fpos;
+    const size_t start = pos;
+    uint32_t n = 0;
+    while (n < max && pos + 16 <= r->map_bytes) {
+        uint32_t h[4];
+        memcpy(h, r->map + pos, 16);
+        if (r->swapped)
+            for (auto &x : h) x = sw32(x);
+        uint32_t len, caplen, skip = 0;     // as in fcpcap_read (fromdump.cc:446-466)
+        if (r->minor > 3 || (r->minor == 3 && h[2] <= h[3])) {
+            len = h[3];
+            caplen = h[2];
+        } else {
+            len = h[2];
+            caplen = h[3];
+        }
+        if (caplen > 65535) {
+            r->err = "bad packet header; giving up";
+            return -1;
+        }
+        if (caplen > len) {
+            skip = caplen - len;
+            caplen = len;
+        }
+        const size_t rec = (size_t)hdr + caplen + skip;
+        if (pos + rec > r->map_bytes) break;          // truncated final record
+        if (pos + rec - start > max_bytes && n) break;
+        desc[2 * n] = (uint32_t)(pos + hdr - start);
+        desc[2 * n + 1] = caplen;
+        if (wire) wire[n] = len;
+        if (ts_ns) ts_ns[n] = (uint64_t)h[0] * 1000000000ull + (uint64_t)h[1] * (r->nano ? 1ull : 1000ull);
+        ++n;
+        pos += rec;
+    }
+    *chunk_off = start;
+    *chunk_bytes = pos - start;
+    r->fpos = (off_t)pos;
+    return (int)n;
 }
 
 int fcpcap_read(fcpcap *r, uint8_t *buf, size_t cap, uint32_t *desc, uint32_t *wire, uint64_t *ts_ns,

@@ -325,6 +325,10 @@ int  fcgpu_set_host_threads(fcgpu_ctx *ctx, uint32_t nthreads);
 /* Pinned host memory for fcgpu_process_host outputs (NULL on failure). */
 void *fcgpu_host_alloc(size_t bytes);
 void fcgpu_host_free(void *p);
+/* Page-lock existing host memory for DMA (hipHostRegister; read-only mappings
+ * such as an mmapped pcap are registered read-only). */
+int  fcgpu_host_register(void *p, size_t bytes, int read_only);
+int  fcgpu_host_unregister(void *p);
 
 int  fcgpu_read_counters(fcgpu_ctx *ctx, uint64_t *out, int n);
 int  fcgpu_reset_counters(fcgpu_ctx *ctx);

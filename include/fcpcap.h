@@ -39,6 +39,15 @@ uint32_t fcpcap_snaplen(const fcpcap *r);
  * via fcpcap_error). *used = bytes of buf written. */
 int  fcpcap_read(fcpcap *r, uint8_t *buf, size_t cap, uint32_t *desc, uint32_t *wire, uint64_t *ts_ns,
                  uint32_t max, size_t *used);
+/* Zero-copy mode: map the whole file read-only (page cache pages; register
+ * them with fcgpu_host_register so the H2D copies DMA straight from them). */
+int  fcpcap_map(fcpcap *r, const uint8_t **base, size_t *bytes);
+/* Index the next records of the mapped file (up to max packets / max_bytes):
+ * the chunk is [base + *chunk_off, + *chunk_bytes); desc offsets are relative
+ * to its start. Returns the count (0 at the end), -1 on a bad record. Do not
+ * mix with fcpcap_read on one reader. */
+int  fcpcap_index(fcpcap *r, uint32_t max, size_t max_bytes, size_t *chunk_off, size_t *chunk_bytes,
+                  uint32_t *desc, uint32_t *wire, uint64_t *ts_ns);
 const char *fcpcap_error(const fcpcap *r);
 /* Threads fcpcap_read may use to copy file data into the buffer (parallel
  * pread() of >= 1 MiB pieces; default 1). */

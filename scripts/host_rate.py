@@ -80,7 +80,7 @@ def gather_only_mpps(n=1 << 20, reps=10):
     return n * reps / (time.perf_counter() - t0) / 1e6
 
 
-def pcap_mpps(n=1 << 22, chunk_pkts=1 << 18, threads=1):
+def pcap_mpps(n=1 << 22, chunk_pkts=1 << 18, threads=1, mapped=False):
     """pcap ingress (fcpcap + fcgpu_span_submit): a C2 trace written as a pcap
     (16-B record header + 60-B frame per packet), read from the page cache
     into pinned chunks and copied as-is; verdict + hash come back. The file is
@@ -100,16 +100,20 @@ def pcap_mpps(n=1 << 22, chunk_pkts=1 << 18, threads=1):
         best = 0.0
         for _ in range(3):
             out, cnt, secs = process_pcap(f.name, cfg, chunk_pkts=chunk_pkts, chunk_bytes=chunk_pkts * 80 + 4096,
-                                          collect=False, threads=threads)
+                                          collect=False, threads=threads, mapped=mapped)
+            reg = out["registered"]
             assert cnt == n and int(out["counters"][N.CTR_COUNT]) == n
             best = max(best, cnt / secs / 1e6)
-    return best
+    return best if not mapped else (best, reg)
 
 
 def main():
     out = {"h2d_pinned_gbs": round(h2d_gbs(), 2)}
-    for t in (1, 4, 8):
+    for t in (1, 4):
         out[f"pcap_ingress_mpps_4M_t{t}"] = round(pcap_mpps(threads=t), 2)
+    m, reg = pcap_mpps(mapped=True)
+    out["pcap_ingress_mpps_4M_mapped"] = round(m, 2)
+    out["pcap_mapped_registered"] = bool(reg)
     out["process_host_mpps_1M_global"] = round(raw_host(1 << 20), 2)
     chunk = os.environ.get("FCGPU_HOST_CHUNK", "65536")
     out["chunk"] = int(chunk)

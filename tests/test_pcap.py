@@ -107,6 +107,30 @@ def test_reader_chunk_boundaries_and_truncation(tmp_path):
         assert got == big[:-1], (cap, th)
 
 
+def test_reader_mapped_index_matches_read(tmp_path):
+    """Zero-copy mode (fcpcap_map + fcpcap_index) yields the same records."""
+    from fastclick_amd.pcap import PcapReader
+    fr = _frames(3000, seed=9)
+    p = str(tmp_path / "x.pcap")
+    for kw in (dict(), dict(swapped=True, magic=0xA1B2CD34), dict(minor=2, swap_lens=True)):
+        write_pcap(p, fr, cut_last=4, **kw)
+        rd = PcapReader(p)
+        base, size = rd.map()
+        mem = (np.ctypeslib.as_array((__import__("ctypes").c_uint8 * size).from_address(base)))
+        desc = np.zeros(2 * 700, np.uint32)
+        got = []
+        while True:
+            n, off, nb = rd.index(700, 100_000, desc.ctypes.data)
+            if n == 0:
+                break
+            assert nb <= 100_000 or n == 1
+            for i in range(n):
+                o, ln = off + int(desc[2 * i]), int(desc[2 * i + 1])
+                got.append(bytes(mem[o:o + ln]))
+        rd.close()
+        assert got == fr[:-1], kw
+
+
 def test_reader_rejects_bad_files(tmp_path):
     from fastclick_amd.pcap import PcapReader
     p = tmp_path / "bad.pcap"
@@ -132,9 +156,10 @@ def test_gpu_pcap_ingress_golden(tmp_path):
     b = batch_of(g)
     p = str(tmp_path / "ip4.pcap")
     write_pcap(p, b.frames())
-    for chunk_pkts, chunk_bytes in ((1 << 16, 1 << 24), (256, 1 << 14), (1000, 1 << 16)):
+    for chunk_pkts, chunk_bytes, mapped in ((1 << 16, 1 << 24, False), (256, 1 << 14, False),
+                                            (1000, 1 << 16, False), (1 << 16, 1 << 24, True), (700, 1 << 16, True)):
         out, n, _ = process_pcap(p, ip4_cfg(classify=N.CLS_LB_HASH, nports=16), chunk_pkts=chunk_pkts,
-                                 chunk_bytes=chunk_bytes)
+                                 chunk_bytes=chunk_bytes, mapped=mapped)
         assert n == b.n
         reason = (out["verdict"] & 0xFF).astype(np.uint8)
         assert np.array_equal(reason, g["reason"])
