@@ -14,7 +14,7 @@ LIBFCGPU = os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 8
+ABI_VERSION = 9
 SPAN_SLOTS = 3
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
@@ -28,7 +28,7 @@ L4_NONE, L4_UDP, L4_TCP = 0, 1, 2
 def reason_slot(r: int) -> int:
     """Counter slot of reason r (reasons 0-5, 7-14; 6 = valid has none)."""
     return r if r < 6 else r - 1
-CHECK_IP4, MARK_IP4, CHECK_AUTO = 0, 1, 2
+CHECK_IP4, MARK_IP4, CHECK_AUTO, MARK_IP6 = 0, 1, 2, 3
 HASH_NONE, HASH_FLOWID, HASH_FLOW5ID = 0, 1, 2
 CLS_NONE, CLS_LB_HASH, CLS_HASH_IP, CLS_HASHSWITCH, CLS_PROGRAM = 0, 1, 2, 3, 4
 PROG_IPFILTER, PROG_CLASSIFIER = 0, 1
@@ -69,6 +69,7 @@ class fcgpu_cfg(C.Structure):
         ("l4_checksum", C.c_uint32),
         ("rewrite", C.c_uint32),
         ("ttl_multicast", C.c_uint32),
+        ("vlan_ethertype", C.c_uint32),
     ]
 
 
@@ -219,7 +220,7 @@ def default_cfg() -> fcgpu_cfg:
 def make_cfg(*, check_mode=CHECK_IP4, offset=0, checksum=False, hash_mode=HASH_FLOWID,
              classify=CLS_NONE, nports=1, hs_offset=0, hs_length=1, native_vlan=0,
              badsrc=(), gooddst=(), bad6=None, process_eh=False, l4_mode=L4_NONE,
-             l4_checksum=True, rewrite=0, ttl_multicast=True) -> fcgpu_cfg:
+             l4_checksum=True, rewrite=0, ttl_multicast=True, vlan_ethertype=0) -> fcgpu_cfg:
     """Build an fcgpu_cfg. Addresses are raw network-order words (bytes a.b.c.d
     -> little-endian u32 of those bytes), as IPAddress stores them."""
     cfg = default_cfg()
@@ -243,6 +244,7 @@ def make_cfg(*, check_mode=CHECK_IP4, offset=0, checksum=False, hash_mode=HASH_F
     cfg.l4_checksum = 1 if l4_checksum else 0
     cfg.rewrite = rewrite
     cfg.ttl_multicast = 1 if ttl_multicast else 0
+    cfg.vlan_ethertype = vlan_ethertype
     if bad6 is not None:
         cfg.nbad6 = len(bad6)
         for j, a in enumerate(bad6):

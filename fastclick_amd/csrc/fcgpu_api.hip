@@ -276,6 +276,7 @@ static void launch_rx_part(uint32_t cm, bool ck, const RxArgs &a, hipStream_t s,
     case 1: launch_rx_ip4<FCGPU_CHECK_IP4, true, PART, PROG>(a, s, e0, e1); break;
     case 2: case 3: launch_rx_ip4<FCGPU_MARK_IP4, false, PART, PROG>(a, s, e0, e1); break;
     case 4: launch_rx<FCGPU_CHECK_AUTO, false, PART, PROG, false>(a, s, e0, e1); break;
+    case 6: case 7: launch_rx<FCGPU_MARK_IP6, false, PART, PROG, false>(a, s, e0, e1); break;
     default: launch_rx<FCGPU_CHECK_AUTO, true, PART, PROG, false>(a, s, e0, e1); break;
     }
 }
@@ -570,11 +571,13 @@ int fcgpu_open(int device, uint32_t max_batch, fcgpu_ctx **out) {
 int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     if (!c || !cfg) return FCGPU_EINVAL;
     if (cfg->size != sizeof(fcgpu_cfg)) return fail(c, FCGPU_EINVAL, "fcgpu_cfg size mismatch (ABI)");
-    if (cfg->check_mode > FCGPU_CHECK_AUTO) return fail(c, FCGPU_EINVAL, "bad check_mode");
+    if (cfg->check_mode > FCGPU_MARK_IP6) return fail(c, FCGPU_EINVAL, "bad check_mode");
+    const bool ip4mode = cfg->check_mode == FCGPU_CHECK_IP4 || cfg->check_mode == FCGPU_MARK_IP4;
+    if (cfg->vlan_ethertype > 0xffff) return fail(c, FCGPU_EINVAL, "bad vlan_ethertype");
     if (cfg->hash_mode > FCGPU_HASH_FLOW5ID) return fail(c, FCGPU_EINVAL, "bad hash_mode");
     if (cfg->classify > FCGPU_CLS_PROGRAM) return fail(c, FCGPU_EINVAL, "bad classify mode");
     if (cfg->l4_mode > FCGPU_L4_TCP) return fail(c, FCGPU_EINVAL, "bad l4_mode");
-    if (cfg->l4_mode != FCGPU_L4_NONE && cfg->check_mode == FCGPU_CHECK_AUTO)
+    if (cfg->l4_mode != FCGPU_L4_NONE && !ip4mode)
         return fail(c, FCGPU_EINVAL, "l4_mode needs an IPv4 check mode (CHECK_IP4 or MARK_IP4)");
     if (cfg->nports < 1 || cfg->nports > FCGPU_MAX_PORTS) return fail(c, FCGPU_EINVAL, "nports out of range");
     if (cfg->offset < 0 || cfg->offset > 255) return fail(c, FCGPU_EINVAL, "OFFSET out of range [0,255]");
@@ -585,7 +588,7 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     if (cfg->native_vlan > 0xFFF) return fail(c, FCGPU_EINVAL, "bad NATIVE_VLAN");
     if (cfg->rewrite & ~(FCGPU_RW_DECTTL | FCGPU_RW_SETCKSUM | FCGPU_RW_INPLACE))
         return fail(c, FCGPU_EINVAL, "bad rewrite flags");
-    if ((cfg->rewrite & (FCGPU_RW_DECTTL | FCGPU_RW_SETCKSUM)) && cfg->check_mode == FCGPU_CHECK_AUTO)
+    if ((cfg->rewrite & (FCGPU_RW_DECTTL | FCGPU_RW_SETCKSUM)) && !ip4mode)
         return fail(c, FCGPU_EINVAL, "rewrite needs an IPv4 check mode (CHECK_IP4 or MARK_IP4)");
     c->cfg = *cfg;
     DevCfg &d = c->dcfg;
@@ -598,6 +601,10 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     d.hs_offset = cfg->hs_offset;
     d.hs_length = cfg->hs_length;
     d.native_vlan = cfg->native_vlan;
+    {
+        const uint32_t tpid = cfg->vlan_ethertype ? cfg->vlan_ethertype : 0x8100u;
+        d.vlan_tpid = ((tpid & 0xff) << 8) | (tpid >> 8);
+    }
     d.nbadsrc = cfg->nbadsrc;
     d.ngooddst = cfg->ngooddst;
     d.nbad6 = cfg->nbad6;
@@ -660,7 +667,7 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     a.fl = c->fl;
     a.fl.flowid = o->flowid;
     a.ip_rw = o->ip_rw;
-    if (a.fl.slots && c->cfg.check_mode == FCGPU_CHECK_AUTO)
+    if (a.fl.slots && c->cfg.check_mode != FCGPU_CHECK_IP4 && c->cfg.check_mode != FCGPU_MARK_IP4)
         return fail(c, FCGPU_EINVAL, "the flow table needs an IPv4 check mode (CHECK_IP4 or MARK_IP4)");
 
     EvPair ev[3];

@@ -33,6 +33,7 @@ struct DevCfg {
     int32_t hs_offset;
     int32_t hs_length;
     int32_t native_vlan;
+    uint32_t vlan_tpid;       // tag protocol as the 16-bit little-endian load of its bytes
     uint32_t nbadsrc;
     uint32_t ngooddst;
     uint32_t nbad6;
@@ -325,7 +326,7 @@ __device__ __forceinline__ void process_packet(const DevCfg &c, const FrameView 
     if (CM == FCGPU_CHECK_AUTO) {
         // StripEtherVLANHeader::simple_action (stripethervlanheader.cc:48-61)
         const uint32_t e = f.rd32(o + 12);        // bytes 12..15: type, tci
-        if ((e & 0xffff) == 0x0081) {             // be16 == 0x8100
+        if ((e & 0xffff) == c.vlan_tpid) {        // be16 == 0x8100 (or VLANDecap ETHERTYPE)
             an.vlan_tci = (uint16_t)(e >> 16);    // raw network-order tci
             o += 18;
         } else if (c.native_vlan >= 0) {
@@ -339,6 +340,14 @@ __device__ __forceinline__ void process_packet(const DevCfg &c, const FrameView 
         an.nh = (uint16_t)o;                       // the pull() StripEtherVLANHeader did
         v6 = ((int)(len - o) >= 1) && ((f.rd8(o) >> 4) == 6);
         r.reason = v6 ? check_ip6(c, f, len, o, an) : check_ip4<CK>(c, f, len, o, h, an);
+    } else if (CM == FCGPU_MARK_IP6) {
+        // MarkIP6Header::simple_action (markip6header.cc:43-48): set_ip6_header(o, 40)
+        an.nh = (uint16_t)o;
+        an.th = (uint16_t)(o + 40);
+        an.length = (uint16_t)len;
+        an.ipver = 6;
+        v6 = true;
+        r.reason = FCGPU_R_OK;
     } else if (CM == FCGPU_MARK_IP4) {
         // MarkIPHeader::simple_action (markipheader.cc:43-48)
         f.run<5>(o, h);

@@ -13,6 +13,8 @@
 //   OFFSET, CHECKSUM (default FALSE: checkipheader.cc:110), BADSRC, GOODDST,
 //   VERBOSE, DETAILS                         -- CheckIPHeader
 //   NATIVE_VLAN (default 0)                  -- StripEtherVLANHeader
+//   VLAN_ETHERTYPE (default 0x8100)          -- VLANDecap(ETHERTYPE) + Strip(14) (MODE AUTO)
+//   MODE MARK6                               -- MarkIP6Header(OFFSET)
 //   BADADDRS, PROCESS_EH                     -- CheckIP6Header (IPv6, MODE AUTO)
 //   N / LB_MODE hash|hash_agg|hash_ip        -- FlowSwitch / LoadBalancer
 //   HASHSWITCH "OFFSET LENGTH"               -- HashSwitch
@@ -100,6 +102,10 @@ class GPUIPCheckClassify : public Element {
                     if (cnt >= FCGPU_MAX_ADDRS) return err(errh, k + ": too many addresses");
                     dst[cnt++] = ip;
                 }
+            } else if (k == "VLAN_ETHERTYPE") {
+                // VLANDecap ETHERTYPE (vlandecap.cc:35-45): the tag protocol removed
+                if (!parse_int(v, n) || n < 0 || n > 0xFFFF) return err(errh, "bad VLAN_ETHERTYPE");
+                _cfg.vlan_ethertype = (uint32_t)n;
             } else if (k == "NATIVE_VLAN") {
                 if (!parse_int(v, n) || n > 0xFFF) return err(errh, "bad NATIVE_VLAN");
                 _cfg.native_vlan = n >= 0 ? (int32_t)n : -1;
@@ -146,7 +152,8 @@ class GPUIPCheckClassify : public Element {
                 if (v == "CHECK") _cfg.check_mode = FCGPU_CHECK_IP4;
                 else if (v == "MARK") _cfg.check_mode = FCGPU_MARK_IP4;
                 else if (v == "AUTO") _cfg.check_mode = FCGPU_CHECK_AUTO;
-                else return err(errh, "MODE expects CHECK, MARK or AUTO");
+                else if (v == "MARK6") _cfg.check_mode = FCGPU_MARK_IP6;
+                else return err(errh, "MODE expects CHECK, MARK, AUTO or MARK6");
             } else if (k == "HASH") {
                 if (v == "NONE") _cfg.hash_mode = FCGPU_HASH_NONE;
                 else if (v == "FLOWID") _cfg.hash_mode = FCGPU_HASH_FLOWID;
@@ -202,11 +209,12 @@ class GPUIPCheckClassify : public Element {
             }
         }
         if (!strip_set) _strip = (_cfg.check_mode == FCGPU_CHECK_AUTO);
-        if (_cfg.l4_mode != FCGPU_L4_NONE && _cfg.check_mode == FCGPU_CHECK_AUTO)
+        const bool ip4 = _cfg.check_mode == FCGPU_CHECK_IP4 || _cfg.check_mode == FCGPU_MARK_IP4;
+        if (_cfg.l4_mode != FCGPU_L4_NONE && !ip4)
             return err(errh, "L4 needs MODE CHECK or MARK");
-        if (_flow_cap && _cfg.check_mode == FCGPU_CHECK_AUTO)
+        if (_flow_cap && !ip4)
             return err(errh, "FLOW_CAPACITY needs MODE CHECK or MARK");
-        if (_cfg.rewrite && _cfg.check_mode == FCGPU_CHECK_AUTO)
+        if (_cfg.rewrite && !ip4)
             return err(errh, "DEC_TTL / SET_CHECKSUM need MODE CHECK or MARK");
         if (_cfg.classify == FCGPU_CLS_PROGRAM) {
             if (_prog.output_everything >= (int32_t)_cfg.nports && _prog.output_everything != 0x7fff)

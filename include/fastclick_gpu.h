@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 8
+#define FCGPU_ABI_VERSION 9
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -86,7 +86,12 @@ extern "C" {
 #define FCGPU_CHECK_IP4   0   /* CheckIPHeader(OFFSET o[, CHECKSUM c, BADSRC, GOODDST]) */
 #define FCGPU_MARK_IP4    1   /* MarkIPHeader(o): no validation                         */
 #define FCGPU_CHECK_AUTO  2   /* StripEtherVLANHeader(NATIVE_VLAN) at o, then by IP version
-                                 nibble: 6 -> CheckIP6Header, else -> CheckIPHeader      */
+                                 nibble: 6 -> CheckIP6Header, else -> CheckIPHeader.
+                                 With vlan_ethertype: VLANDecap(ETHERTYPE) + Strip(14)
+                                 (elements/ethernet/vlandecap.cc:49-70): same offsets,
+                                 untagged -> tci 0 (native_vlan 0)                     */
+#define FCGPU_MARK_IP6    3   /* MarkIP6Header(o) (elements/ip6/markip6header.cc:43-48): no
+                                 validation, nh = o, th = o + 40; IP6FlowID hash        */
 /* hash_mode (written to the AGGREGATE annotation output) */
 #define FCGPU_HASH_NONE     0
 #define FCGPU_HASH_FLOWID   1   /* IPFlowID(p).hashcode() low 32 (AggregateHash); v6: IP6FlowID */
@@ -148,6 +153,8 @@ typedef struct fcgpu_cfg {
                                  TRUE: checkudpheader.cc:54, checktcpheader.cc)          */
     uint32_t rewrite;         /* FCGPU_RW_* (IPv4 check modes)                            */
     uint32_t ttl_multicast;   /* DecIPTTL MULTICAST (default true: decrement multicast too) */
+    uint32_t vlan_ethertype;  /* CHECK_AUTO tag protocol: 0x8100 (StripEtherVLANHeader, and
+                                 VLANDecap's default) or VLANDecap ETHERTYPE (e.g. 0x88a8) */
 } fcgpu_cfg;
 
 /* Optional per-packet annotations (16 B), mirroring what the reference

@@ -403,8 +403,9 @@ void fco_process_packet(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, fco_
     int reason;
     int v6 = 0;
     if (c->check_mode == FCGPU_CHECK_AUTO) {
-        /* elements/ethernet/stripethervlanheader.cc:48-61 */
-        if (be16(f + o + 12) == 0x8100) {
+        /* elements/ethernet/stripethervlanheader.cc:48-61; with vlan_ethertype,
+         * VLANDecap(ETHERTYPE) + Strip(14) (elements/ethernet/vlandecap.cc:49-70) */
+        if (be16(f + o + 12) == (c->vlan_ethertype ? c->vlan_ethertype : 0x8100)) {
             a->vlan_tci = raw16(f + o + 14);
             o += 18;
         } else if (c->native_vlan >= 0) {
@@ -420,6 +421,14 @@ void fco_process_packet(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, fco_
         /* version dispatch as Classifier(0/60%f0, -): needs one byte */
         v6 = ((int)(len - o) >= 1) && ((f[o] >> 4) == 6);
         reason = v6 ? check_ip6(c, f, len, o, a) : check_ip4(c, f, len, o, a);
+    } else if (c->check_mode == FCGPU_MARK_IP6) {
+        /* elements/ip6/markip6header.cc:43-48: set_ip6_header(data + o, 40) */
+        a->nh = (uint16_t)o;
+        a->th = (uint16_t)(o + 40);
+        a->length = (uint16_t)len;
+        a->ipver = 6;
+        v6 = 1;
+        reason = FCGPU_R_OK;
     } else if (c->check_mode == FCGPU_MARK_IP4) {
         /* elements/ip/markipheader.cc:43-48 */
         a->nh = (uint16_t)o;

@@ -922,6 +922,46 @@ def run_rw(b, tmp, bad):
     return res
 
 
+def make_qinq_set(n=1600, seed=2031):
+    """The mix set with a third of its 802.1Q tags turned into 802.1ad
+    (0x88a8) tags: under VLANDecap(ETHERTYPE 0x88a8) only those are decapped;
+    0x8100-tagged frames keep their tag and fail the IP checks."""
+    b = make_mix_set(n, seed)
+    rng = np.random.default_rng(seed + 7)
+    A = b.arena
+    for i in range(b.n):
+        off = int(b.desc[i, 0])
+        if A[off + 12] == 0x81 and rng.random() < 0.34:
+            A[off + 12], A[off + 13] = 0x88, 0xA8
+    return b
+
+
+def run_qinq(b, tmp):
+    """VLANDecap(ETHERTYPE 0x88a8) -> Strip(14) -> Classifier(0/60%f0, -) =>
+    CheckIP6Header | CheckIPHeader(CHECKSUM true) -> AggregateHash: per packet
+    valid (1) / invalid (0), IP version of valid ones, v4 AGGREGATE, and the
+    length after the check."""
+    pcap = os.path.join(tmp, "qinq.pcap")
+    write_pcap(pcap, b.frames())
+    click(CLICK, "FromDump(qinq.pcap, STOP true, TIMING false) -> VLANDecap(ETHERTYPE 0x88a8) -> Strip(14) "
+                 "-> c :: Classifier(0/60%f0, -);"
+                 " c[0] -> ck6 :: CheckIP6Header -> ToDump(q_good6.pcap, ENCAP IP); ck6[1] -> Discard;"
+                 " c[1] -> ck4 :: CheckIPHeader(CHECKSUM true) -> AggregateHash -> t :: Tee(2);"
+                 " t[0] -> ToIPSummaryDump(q_good4.ipsum, FIELDS timestamp aggregate);"
+                 " t[1] -> ToDump(q_good4.pcap, ENCAP IP); ck4[1] -> Discard;", tmp)
+    n = b.n
+    valid = np.zeros(n, np.uint8)
+    ipver = np.zeros(n, np.uint8)
+    hsh = np.zeros(n, np.uint32)
+    iplen = np.zeros(n, np.uint16)
+    for i, (incl, _) in read_pcap(os.path.join(tmp, "q_good6.pcap")).items():
+        valid[i], ipver[i], iplen[i] = 1, 6, incl
+    g4 = read_pcap(os.path.join(tmp, "q_good4.pcap"))
+    for i, row in read_ipsum(os.path.join(tmp, "q_good4.ipsum"), 1).items():
+        valid[i], ipver[i], hsh[i], iplen[i] = 1, 4, int(row[0]), g4[i][0]
+    return dict(qinq_valid=valid, qinq_ipver=ipver, qinq_hash=hsh, qinq_iplen=iplen)
+
+
 def run_kat(tmp):
     """click_in_cksum on random buffers (odd lengths included) and IPFlowID /
     IP6FlowID hashcodes on random tuples, from the reference harness."""
@@ -951,7 +991,7 @@ def sha(path):
     return hashlib.sha256(open(path, "rb").read()).hexdigest()
 
 
-def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "rw", "kat")):
+def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "rw", "qinq", "kat")):
     prov_path = os.path.join(HERE, "PROVENANCE.json")
     prov = json.load(open(prov_path)) if os.path.exists(prov_path) else {}
     prov.update(generator="tests/golden/gen_golden.py", click=CLICK, click_sha256=sha(CLICK),
@@ -1011,6 +1051,11 @@ def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "r
                                 **rr)
             print("rw: dec ok", int((rr["dec"] != 0xFFFFFFFF).sum()), "expired", int(rr["dec_expired"].sum()),
                   "nm expired", int(rr["decnm_expired"].sum()), "set ok", int((rr["set"] != 0xFFFFFFFF).sum()))
+        if "qinq" in sets:
+            qb = make_qinq_set()
+            rq = run_qinq(qb, tmp)
+            np.savez_compressed(os.path.join(HERE, "qinq.npz"), arena=qb.arena, desc=qb.desc, **rq)
+            print("qinq: valid", int(rq["qinq_valid"].sum()), "v6", int((rq["qinq_ipver"] == 6).sum()))
         if "combo" in sets:
             rc = run_combo(tmp)
             np.savez_compressed(os.path.join(HERE, "combo.npz"), **rc)
@@ -1037,6 +1082,8 @@ def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "r
                 "--enable-research --enable-flow-dynamic --enable-ctx): per-packet flow ID = stored ID - 1",
         "rw": "Strip(14) -> CheckIPHeader(CHECKSUM true) -> DecIPTTL[(MULTICAST false)] [-> SetIPChecksum] -> ToDump, "
               "DecIPTTL[1] -> ToDump; MarkIPHeader(14) -> SetIPChecksum -> ToDump: IP header bytes 8..11 per packet",
+        "qinq": "VLANDecap(ETHERTYPE 0x88a8) -> Strip(14) -> Classifier(0/60%f0,-) -> CheckIP6Header | "
+                "CheckIPHeader(CHECKSUM true) -> AggregateHash: validity, version, v4 hash, ip length",
         "kat": "fcref: click_in_cksum (lib/in_cksum.c), IPFlowID/IP6FlowID::hashcode (headers)",
     })
     prov["ipc_rules"] = IPC_RULES
@@ -1046,4 +1093,5 @@ def main(sets=("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "r
 
 
 if __name__ == "__main__":
-    main(tuple(sys.argv[1:]) or ("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "rw", "kat"))
+    main(tuple(sys.argv[1:]) or ("ip4", "mix", "prog", "reftests", "combo", "eh", "l4", "flow", "rw", "qinq",
+                                 "kat"))

@@ -32,7 +32,7 @@ def test_struct_layouts_match_header():
     assert C.sizeof(N.fcgpu_anno) == 16
     assert C.sizeof(N.fcgpu_out) == 9 * 8 + 8
     # 12 u32 scalars + 2x16 u32 lists + nbad6 + 16x16 B + process_eh, l4_mode, l4_checksum
-    assert C.sizeof(N.fcgpu_cfg) == 4 * 12 + 4 * 32 + 4 + 256 + 5 * 4
+    assert C.sizeof(N.fcgpu_cfg) == 4 * 12 + 4 * 32 + 4 + 256 + 6 * 4
     lib = N.load()
     cfg = N.fcgpu_cfg()
     lib.fcgpu_default_cfg(C.byref(cfg))

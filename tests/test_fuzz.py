@@ -75,6 +75,9 @@ CONFIGS = {
                           rewrite=N.RW_DECTTL | N.RW_SETCKSUM),
     "mark-setcksum": dict(check_mode=N.MARK_IP4, offset=14, classify=N.CLS_LB_HASH, nports=4,
                           rewrite=N.RW_SETCKSUM),
+    "auto-qinq": dict(check_mode=N.CHECK_AUTO, offset=0, checksum=True, classify=N.CLS_LB_HASH, nports=5,
+                      vlan_ethertype=0x88A8),
+    "mark6": dict(check_mode=N.MARK_IP6, offset=14, classify=N.CLS_LB_HASH, nports=8),
 }
 
 

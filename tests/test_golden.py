@@ -97,6 +97,39 @@ def check_mix(run, g):
         assert np.array_equal(r["hash"][v6], g["hash"][v6]), "IP6FlowID::hashcode"
 
 
+def check_qinq(run, g):
+    """VLANDecap(ETHERTYPE 0x88a8) + Strip(14) ahead of the version dispatch:
+    only 802.1ad tags are removed (0x8100-tagged frames fail the checks),
+    untagged frames get TCI 0 (NATIVE_VLAN 0 equivalent)."""
+    b = batch_of(g)
+    r = run(N.make_cfg(check_mode=N.CHECK_AUTO, checksum=True, classify=N.CLS_LB_HASH, nports=16,
+                       native_vlan=0, vlan_ethertype=0x88A8), b)
+    ok = g["qinq_valid"] == 1
+    assert np.array_equal(r["reason"] == N.R_OK, ok), "VLANDecap(ETHERTYPE 0x88a8) verdicts"
+    if "anno" in r:
+        a = r["anno"]
+        assert np.array_equal(a["ipver"][ok], g["qinq_ipver"][ok])
+        assert np.array_equal((a["length"].astype(np.int64) - a["nh"])[ok], g["qinq_iplen"][ok])
+    v4 = ok & (g["qinq_ipver"] == 4)
+    assert np.array_equal(r["hash"][v4], g["qinq_hash"][v4])
+
+
+def check_mark6(run, g):
+    """MarkIP6Header(18 or 14): no validation, th = nh + 40; the IP6FlowID hash
+    of the mix set's valid IPv6 packets equals the reference harness's."""
+    b = batch_of(g)
+    v6 = (g["reason"] == 6) & (g["ipver"] == 6)
+    off = b.desc[:, 0].astype(np.int64)
+    tagged = b.arena[off + 12] == 0x81
+    for o, sel in ((18, v6 & tagged), (14, v6 & ~tagged)):
+        r = run(N.make_cfg(check_mode=N.MARK_IP6, offset=o, classify=N.CLS_LB_HASH, nports=16), b)
+        assert (r["reason"] == N.R_OK).all()
+        if "anno" in r:
+            assert (r["anno"]["th"].astype(np.int64) == o + 40).all() and (r["anno"]["ipver"] == 6).all()
+        if bool(g["h6_pinned"]):
+            assert np.array_equal(r["hash"][sel], g["hash"][sel])
+
+
 def check_eh(run, g):
     """CheckIP6Header(BADADDRS 2001:db8::bad, PROCESS_EH true|false): verdict,
     IP6_NXT annotation, transport-header offset and trimmed length."""
@@ -123,6 +156,14 @@ def test_oracle_eh_golden(oracle):
 
 def test_oracle_ip4_golden(oracle):
     check_ip4(oracle.process_batch, load("ip4"))
+
+
+def test_oracle_qinq_golden(oracle):
+    check_qinq(oracle.process_batch, load("qinq"))
+
+
+def test_oracle_mark6_mix(oracle):
+    check_mark6(oracle.process_batch, load("mix"))
 
 
 def test_oracle_mix_golden(oracle):
@@ -172,6 +213,18 @@ def test_gpu_eh_golden():
     from fastclick_amd import device
     for part in (N.PART_GLOBAL, N.PART_TILE):
         check_eh(lambda cfg, b: device.process_batch(b, cfg, partition=part), load("eh"))
+
+
+@pytest.mark.gpu
+def test_gpu_qinq_golden():
+    from fastclick_amd import device
+    check_qinq(lambda cfg, b: device.process_batch(b, cfg), load("qinq"))
+
+
+@pytest.mark.gpu
+def test_gpu_mark6_mix():
+    from fastclick_amd import device
+    check_mark6(lambda cfg, b: device.process_batch(b, cfg), load("mix"))
 
 
 @pytest.mark.gpu
