@@ -240,9 +240,9 @@ def main():
                          device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        total_valid = int(glob[N.CTR_COUNT].item())
+        total_valid = int(N.derive_counters(glob.cpu().numpy())[N.CTR_COUNT])
     else:
-        total_valid = int(ctr_t.sum(0)[N.CTR_COUNT].item())
+        total_valid = int(N.derive_counters(ctr_t.sum(0).cpu().numpy())[N.CTR_COUNT])
 
     timing = None
     if not args.no_timing:

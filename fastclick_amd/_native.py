@@ -157,6 +157,7 @@ FCGPU_SYMBOLS = {
     "fcgpu_host_register": (C.c_int, [C.c_void_p, C.c_size_t, C.c_int]),
     "fcgpu_host_unregister": (C.c_int, [C.c_void_p]),
     "fcgpu_read_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
+    "fcgpu_counters_derive": (None, [C.c_void_p]),
     "fcgpu_reset_counters": (C.c_int, [C.c_void_p]),
     "fcgpu_counters_device": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
     "fcgpu_use_counters": (C.c_int, [C.c_void_p, C.c_void_p]),
@@ -251,6 +252,18 @@ def make_cfg(*, check_mode=CHECK_IP4, offset=0, checksum=False, hash_mode=HASH_F
             for k in range(16):
                 cfg.bad6[j][k] = a[k]
     return cfg
+
+
+def derive_counters(vec):
+    """fcgpu_counters_derive on a summed counter vector (numpy / list of
+    NCOUNTERS): drops = checker reason slots, count = all packets - drops."""
+    import numpy as np
+    v = np.array(vec, dtype=np.uint64).copy()
+    drops = int(v[CTR_REASON:CTR_REASON + reason_slot(R_NO_MATCH)].sum())
+    total = int(v[CTR_PORT:CTR_PORT + MAX_PORTS + 1].sum())
+    v[CTR_DROPS] = drops
+    v[CTR_COUNT] = total - drops
+    return v
 
 
 def raw_addr(dotted: str) -> int:

@@ -1003,18 +1003,26 @@ void fcgpu_host_free(void *p) {
     if (p) hipHostFree(p);
 }
 
+void fcgpu_counters_derive(uint64_t *v) {
+    if (!v) return;
+    uint64_t drops = 0, total = 0;
+    for (uint32_t s = 0; s < reason_slot(FCGPU_R_NO_MATCH); ++s) drops += v[FCGPU_CTR_REASON + s];
+    for (uint32_t b = 0; b <= FCGPU_MAX_PORTS; ++b) total += v[FCGPU_CTR_PORT + b];
+    v[FCGPU_CTR_DROPS] = drops;
+    v[FCGPU_CTR_COUNT] = total - drops;
+}
+
 int fcgpu_read_counters(fcgpu_ctx *c, uint64_t *out, int n) {
     if (!c || !out || n < 0) return FCGPU_EINVAL;
     if (n > FCGPU_NCOUNTERS) n = FCGPU_NCOUNTERS;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipDeviceSynchronize());
-    std::vector<uint64_t> all(kCtrWords);
+    std::vector<uint64_t> all(kCtrWords), sum(FCGPU_NCOUNTERS, 0);
     HIPCHK(c, hipMemcpy(all.data(), c->d_ctr, sizeof(uint64_t) * kCtrWords, hipMemcpyDeviceToHost));
-    for (int k = 0; k < n; ++k) {
-        uint64_t v = 0;
-        for (int r = 0; r < FCGPU_CTR_SHARDS; ++r) v += all[(size_t)r * FCGPU_NCOUNTERS + k];
-        out[k] = v;
-    }
+    for (int k = 0; k < FCGPU_NCOUNTERS; ++k)
+        for (int r = 0; r < FCGPU_CTR_SHARDS; ++r) sum[k] += all[(size_t)r * FCGPU_NCOUNTERS + k];
+    fcgpu_counters_derive(sum.data());
+    for (int k = 0; k < n; ++k) out[k] = sum[k];
     return FCGPU_OK;
 }
 

@@ -646,7 +646,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     return x;
 }
 
-__device__ __forceinline__ uint32_t reason_slot(uint32_t r) { return r < 6 ? r : r - 1; }
+__host__ __device__ __forceinline__ uint32_t reason_slot(uint32_t r) { return r < 6 ? r : r - 1; }
 
 // Lanes of this wave whose `key` equals mine, among the lanes in `live`
 // (a match-any built from one ballot per key bit: the cost depends on the key
@@ -942,21 +942,14 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d,
         }
     }
     if (FLOW) flow_resolve(A.fl, fq, live, i);
-    // counters: one atomic per non-zero bin per tile, sharded by tile
+    // counters: one atomic per non-zero bin per tile, sharded by tile. "count"
+    // and "drops" are not kept here: both follow from these bins on read
+    // (fcgpu_counters_derive), which saves an atomic per tile (-0.4 us / 1M).
     if (t < nbt) {
         unsigned long long *ctr = A.ctr + (size_t)(tile & (FCGPU_CTR_SHARDS - 1)) * FCGPU_NCOUNTERS;
         if (tot) {
             if (t < nb) atomicAdd(&ctr[FCGPU_CTR_PORT + t], (unsigned long long)tot);
             else atomicAdd(&ctr[FCGPU_CTR_REASON + (t - nb)], (unsigned long long)tot);
-        }
-        if (t == nb - 1) {   // the invalid list: drops (minus post-check verdicts), count = packets - drops
-            const uint32_t live_n = min(A.n - tile * kTile, (uint32_t)kTile);
-            uint32_t post = 0;   // reasons >= FCGPU_R_NO_MATCH: slots 8 .. NREASON_SLOTS-1
-            for (uint32_t sm = nb + reason_slot(FCGPU_R_NO_MATCH); sm < nb + FCGPU_NREASON_SLOTS; ++sm)
-                post += s_cnt[0][sm] + s_cnt[1][sm] + s_cnt[2][sm] + s_cnt[3][sm];
-            const uint32_t drops = tot - post;
-            if (drops) atomicAdd(&ctr[FCGPU_CTR_DROPS], (unsigned long long)drops);
-            if (live_n - drops) atomicAdd(&ctr[FCGPU_CTR_COUNT], (unsigned long long)(live_n - drops));
         }
     }
 }

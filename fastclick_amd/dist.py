@@ -2,7 +2,8 @@
 
 The path is stateless per packet, so a batch splits into contiguous index
 ranges, one per GPU, with no data-path collective. The only exchange is the
-counter vector (per-output counts, count/drops, per-reason drops): each GPU
+counter vector (per-output counts and per-reason counts; "count" and "drops"
+follow from them, _native.derive_counters / fcgpu_counters_derive): each GPU
 keeps FCGPU_CTR_SHARDS replicas that are summed locally and then all-reduced
 across ranks -- the MI355X analogue of FastClick's per_thread<> counters summed
 by PER_THREAD_SUM on read (include/click/sync.hh:56,384). When a globally

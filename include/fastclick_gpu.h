@@ -338,6 +338,13 @@ int  fcgpu_host_register(void *p, size_t bytes, int read_only);
 int  fcgpu_host_unregister(void *p);
 
 int  fcgpu_read_counters(fcgpu_ctx *ctx, uint64_t *out, int n);
+/* The device keeps the per-reason and per-output bins only; "count" and
+ * "drops" are derived: drops = the reason slots of reasons 0-5, 7, 8 (the
+ * checker's drops), count = all packets (sum of the output bins, invalid list
+ * included) - drops. fcgpu_read_counters applies this; callers summing the
+ * raw device replicas themselves (e.g. after an all-reduce) call this on the
+ * summed FCGPU_NCOUNTERS vector. */
+void fcgpu_counters_derive(uint64_t *vec);
 int  fcgpu_reset_counters(fcgpu_ctx *ctx);
 /* Device address of the context's uint64 counter replicas
  * (FCGPU_CTR_SHARDS x FCGPU_NCOUNTERS), for a cross-GPU all-reduce. */
