@@ -408,9 +408,8 @@ __device__ __forceinline__ void process_packet(const DevCfg &c, const FrameView 
 // lane needs the general path (options, header beyond the window, hash modes
 // or classifiers it does not cover); the caller then runs process_packet.
 template <bool CK, bool PROG>
-__device__ __forceinline__ bool ip4_fast(const DevCfg &c, const FrameView &f, uint32_t len, PktResult &r,
+__device__ __forceinline__ bool ip4_fast(const DevCfg &c, const FrameView &f, uint32_t len, uint32_t o, PktResult &r,
                                          const uint4 *sprog) {
-    const uint32_t o = (uint32_t)c.offset;
     const uint32_t x = f.shift + o, a = x & ~3u, sh = x & 3u;
     const bool inwin = a + 28 <= (uint32_t)kWin;
     const uint32_t ab = inwin ? a : 0u;   // keep the LDS reads in the row either way
@@ -475,6 +474,87 @@ __device__ __forceinline__ bool ip4_fast(const DevCfg &c, const FrameView &f, ui
     }
     r.port = ok && port < c.nports ? port : c.nports;
     return true;
+}
+
+// One LDS dword of the lane's window at frame byte b (any alignment); the
+// caller guarantees shift + b + 8 <= kWin (two aligned dwords in the row).
+__device__ __forceinline__ uint32_t win32(const FrameView &f, uint32_t b) {
+    const uint32_t x = f.shift + b, a = x & ~3u;
+    const uint32_t lo = *reinterpret_cast<const uint32_t *>(f.row + ((((a >> 4) ^ f.sw) << 4) | (a & 15)));
+    const uint32_t hi = *reinterpret_cast<const uint32_t *>(f.row + (((((a + 4) >> 4) ^ f.sw) << 4) | ((a + 4) & 15)));
+    return __builtin_amdgcn_alignbyte(hi, lo, x & 3u);
+}
+
+// Straight-line CheckIP6Header -> IP6FlowID hash -> classify for an IPv6
+// header at o whose 40 bytes + first L4 word lie in the window (no PROCESS_EH:
+// the caller declines that). Same outputs as check_ip6 + process_packet's v6
+// branch (checkip6header.cc:105-150, ip6flowid.hh:220-230).
+template <bool PROG>
+__device__ __forceinline__ bool ip6_fast(const DevCfg &c, const FrameView &f, uint32_t len, uint32_t o, PktResult &r,
+                                         const uint4 *sprog) {
+    const uint32_t x = f.shift + o, a = x & ~3u, sh = x & 3u;
+    if (a + 48 > (uint32_t)kWin) return false;
+    uint32_t w[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j)
+        w[j] = *reinterpret_cast<const uint32_t *>(f.row + (((((a + 4 * j) >> 4) ^ f.sw) << 4) | ((a + 4 * j) & 15)));
+    uint32_t h[11];
+#pragma unroll
+    for (int j = 0; j < 11; ++j) h[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+    if (c.classify != FCGPU_CLS_LB_HASH && (!PROG || c.classify != FCGPU_CLS_PROGRAM)) return false;
+    const uint32_t plen = len - o, pl6 = bswap16(h[1] & 0xffff);
+    bool bad = (int)plen < 40 || ((h[0] & 0xff) >> 4) != 6 || pl6 > plen - 40;
+    for (uint32_t j = 0; j < c.nbad6; ++j)   // wave-uniform
+        bad |= h[2] == c.bad6[j][0] && h[3] == c.bad6[j][1] && h[4] == c.bad6[j][2] && h[5] == c.bad6[j][3];
+    fcgpu_anno &an = r.an;
+    an.ipver = 6;
+    uint32_t hv = 0;
+    if (c.hash_mode != FCGPU_HASH_NONE) {
+        const uint32_t s = bswap16(h[10] & 0xffff), d = bswap16(h[10] >> 16);
+        const uint32_t sa = (h[4] << 1) + h[5], da = (h[8] << 1) + h[9];
+        hv = rotl32(sa, s & 15) ^ rotl32(da, 31 - (d & 15)) ^ ((d << 16) | s);
+    }
+    r.reason = bad ? FCGPU_R_BAD_IP6 : FCGPU_R_OK;
+    r.hash = bad ? 0u : hv;
+    an.th = (uint16_t)(bad ? 0u : o + 40);
+    an.ip6_nxt = (uint8_t)(bad ? 0u : (h[1] >> 16) & 0xff);
+    an.length = (uint16_t)(bad ? 0u : (pl6 < plen - 40 ? len - (plen - 40 - pl6) : len));
+    uint32_t port = c.nports;
+    if (!bad) {
+        an.nh = (uint16_t)o;
+        if (c.classify == FCGPU_CLS_LB_HASH) {
+            port = (uint32_t)lb_port(hv, c.nports, c.lb_magic);
+        } else if (PROG) {
+            const uint32_t out = run_program(c, f, an, sprog);
+            if (out >= c.nports) r.reason = FCGPU_R_NO_MATCH;
+            else port = out;
+        }
+    }
+    r.port = port;
+    return true;
+}
+
+// StripEtherVLANHeader / VLANDecap at OFFSET, then the version dispatch of
+// CHECK_AUTO, straight-line for frames whose headers sit in the window;
+// rejected untagged frames (NATIVE_VLAN < 0) and PROCESS_EH take the general
+// path.
+template <bool CK, bool PROG>
+__device__ __forceinline__ bool auto_fast(const DevCfg &c, const FrameView &f, uint32_t len, PktResult &r,
+                                          const uint4 *sprog) {
+    const uint32_t o = (uint32_t)c.offset;
+    // the tag word at o+12 and the version byte at o+18 as two aligned dwords each
+    if (c.process_eh || f.shift + o + 26 > (uint32_t)kWin) return false;
+    const uint32_t e = win32(f, o + 12);                     // type, tci
+    const bool tagged = (e & 0xffff) == c.vlan_tpid;
+    if (!tagged && c.native_vlan < 0) return false;
+    const uint32_t x = o + (tagged ? 18u : 14u);
+    const bool v6 = ((int)(len - x) >= 1) && ((win32(f, x) & 0xf0) == 0x60);
+    const bool done = v6 ? ip6_fast<PROG>(c, f, len, x, r, sprog) : ip4_fast<CK, PROG>(c, f, len, x, r, sprog);
+    if (done) {
+        r.an.vlan_tci = tagged ? (uint16_t)(e >> 16) : (uint16_t)bswap16((uint32_t)c.native_vlan);
+        r.an.nh = (uint16_t)x;                               // the pull() the strip did
+    }
+    return done;
 }
 
 // ---- CheckUDPHeader / CheckTCPHeader ----------------------
@@ -863,7 +943,16 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d,
     uint32_t bin = 0xffffffffu, rslot = 0xffffffffu;
     if (FAST && CM == FCGPU_CHECK_IP4) {
         bool done = !live;
-        if (live) done = ip4_fast<CK, PROG>(A.cfg, f, d.y, r, sprog);
+        if (live) done = ip4_fast<CK, PROG>(A.cfg, f, d.y, (uint32_t)A.cfg.offset, r, sprog);
+        if (__ballot(!done)) {
+            if (!done) {
+                r.an = fcgpu_anno{};
+                process_packet<CM, CK, PROG>(A.cfg, f, d.y, r, sprog);
+            }
+        }
+    } else if (FAST && CM == FCGPU_CHECK_AUTO) {
+        bool done = !live;
+        if (live) done = auto_fast<CK, PROG>(A.cfg, f, d.y, r, sprog);
         if (__ballot(!done)) {
             if (!done) {
                 r.an = fcgpu_anno{};
@@ -959,7 +1048,8 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d,
 // (Two tiles per workgroup with the second window prefetched into VGPRs
 // while the first is processed measured 10-15 % slower: one resident round
 // of workgroups instead of two loses the natural load/compute skew.)
-template <int CM, bool CK, int PART, bool PROG, bool L4, bool FLOW = false, bool FAST = (CM == FCGPU_CHECK_IP4)>
+template <int CM, bool CK, int PART, bool PROG, bool L4, bool FLOW = false,
+          bool FAST = (CM == FCGPU_CHECK_IP4 || CM == FCGPU_CHECK_AUTO)>
 __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4 * kWave * kWin];
     __shared__ uint32_t s_cnt[4][kMaxBins];
