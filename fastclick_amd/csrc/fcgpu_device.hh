@@ -199,6 +199,10 @@ __device__ __forceinline__ uint32_t run_program_on(const DevCfg &c, const FrameV
         plen = (int)an.length;
     }
     int pos = 0;
+    // consecutive steps mostly test the same word (a rule's fields, a range
+    // split into mask tests): keep the last one instead of re-reading it
+    int lastb = INT32_MIN;
+    uint32_t lastw = 0;
     for (uint32_t it = 0; it <= c.prog_n; ++it) {
         const uint4 st = prog[pos];
         const int off = (int16_t)(st.x & 0xffff);
@@ -211,7 +215,11 @@ __device__ __forceinline__ uint32_t run_program_on(const DevCfg &c, const FrameV
         int j;
         if (avail) {
             const int b = !ipf ? off : off >= 512 ? (int)an.th + off - 512 : off >= 256 ? (int)an.nh + off - 256 : off - 2;
-            const uint32_t data = prog_word(f, b) & m;
+            if (b != lastb) {
+                lastw = prog_word(f, b);
+                lastb = b;
+            }
+            const uint32_t data = lastw & m;
             j = data == st.y ? (int16_t)(st.w & 0xffff) : (int16_t)(st.w >> 16);
         } else {
             j = ((st.x >> 16) & FCGPU_STEP_SHORT_YES) ? (int16_t)(st.w & 0xffff) : (int16_t)(st.w >> 16);
