@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared(header):
     src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(fc(?:gpu|click)_[a-z_0-9]+)\s*\(",
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(fc(?:gpu|click|pcap)_[a-z_0-9]+)\s*\(",
                                  src, flags=re.M)))
 
 
@@ -87,6 +87,21 @@ def test_fcclick_exports_every_declared_symbol():
     lib = K.load()
     for n in names:
         assert hasattr(lib, n), n
+
+
+def test_fcpcap_exports_every_declared_symbol():
+    from fastclick_amd import click as K
+    names = declared("fcpcap.h")
+    assert len(names) >= 8
+    lib = K.load()
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+def test_every_header_is_checked():
+    """include/ holds exactly the three C-ABI headers the tests above cover."""
+    assert sorted(f for f in os.listdir(os.path.join(ROOT, "include")) if f.endswith(".h")) == \
+        ["fastclick_gpu.h", "fcclick.h", "fcpcap.h"]
 
 
 def test_lb_fastmod_exhaustive():
