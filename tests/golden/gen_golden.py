@@ -426,6 +426,9 @@ REFTEST_PROGRAMS = [
      "ipf", 1),
     ("IPFilter-07.5", "test/ip/IPFilter-07.clicktest", "IPFilter()", "ipf", 1),
     ("Classifier-01", "test/standard/Classifier-01.clicktest", "Classifier(1/01, -)", "cls", 2),
+    # test/standard/Classifier-02.clicktest: the empty program (every packet to
+    # output 0); that test holds no program text to compare with
+    ("Classifier-02", None, "Classifier(-)", "cls", 1),
 ]
 # The survey's CPU classifier benchmark ("+ IPClassifier with 16
 # dst-port-range rules -> 16 ports"): 15 UDP dst-port ranges of 4096 + "-".
