@@ -74,6 +74,9 @@ def parse_program(text: str):
     return [steps[i] for i in range(n.value)], oe.value
 
 
+PER_PACKET = 0xFFFFFFFF   # burst value: the source calls push(0, p) per packet (fcclick.h)
+
+
 def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1):
     lib = load()
     n = batch.n

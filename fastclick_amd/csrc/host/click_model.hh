@@ -172,6 +172,12 @@ class Element {
     virtual int configure(const std::vector<std::string> &conf, std::string &errh) = 0;
     virtual int initialize(std::string &) { return 0; }
     virtual void push_batch(int port, PacketBatch *batch) = 0;
+    // Per-packet entry for non-batch upstreams (Element::push, lib/element.cc:3141-3147;
+    // with batching on, Port::push hands a lone packet to a batch element the same way,
+    // include/click/element.hh:765-790). Default: a one-packet batch.
+    virtual void push(int port, Packet *p) {
+        push_batch(port, PacketBatch::make_from_list(p, p, 1));
+    }
     virtual std::string read_handler(const std::string &) { return std::string(); }
     virtual void flush() {}
 

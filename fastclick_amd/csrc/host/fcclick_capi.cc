@@ -139,7 +139,9 @@ extern "C" int fcclick_run(const char *conf, const uint8_t *arena, const uint32_
         copy_err(e, err, errcap);
         return -1;
     }
+    const bool per_packet = burst == FCCLICK_PER_PACKET;
     if (burst == 0) burst = 32;
+    if (per_packet) burst = 32;
     uint32_t seq = 0, nbatch = 0;
     if (res) {
         for (uint32_t i = 0; i < n; ++i) {
@@ -165,7 +167,14 @@ extern "C" int fcclick_run(const char *conf, const uint8_t *arena, const uint32_
             else head = p;
             prev = p;
         }
-        el->push_batch(0, PacketBatch::make_from_list(head, prev, m));
+        if (per_packet)
+            for (Packet *p = head, *nx; p; p = nx) {
+                nx = p->next();
+                p->set_next(nullptr);
+                el->push(0, p);
+            }
+        else
+            el->push_batch(0, PacketBatch::make_from_list(head, prev, m));
     }
     el->flush();
     if (res) {
@@ -194,7 +203,9 @@ extern "C" int fcclick_bench(const char *conf, const uint8_t *arena, const uint3
         copy_err(e, err, errcap);
         return -1;
     }
+    const bool per_packet = burst == FCCLICK_PER_PACKET;
     if (burst == 0) burst = 32;
+    if (per_packet) burst = 32;
     uint32_t seq = 0, nbatch = 0;
     std::vector<std::unique_ptr<Sink>> sinks;
     for (uint32_t k = 0; k < 65; ++k) {
@@ -213,7 +224,14 @@ extern "C" int fcclick_bench(const char *conf, const uint8_t *arena, const uint3
                 else head = p;
                 prev = p;
             }
-            el->push_batch(0, PacketBatch::make_from_list(head, prev, m));
+            if (per_packet)
+                for (Packet *p = head, *nx; p; p = nx) {
+                    nx = p->next();
+                    p->set_next(nullptr);
+                    el->push(0, p);
+                }
+            else
+                el->push_batch(0, PacketBatch::make_from_list(head, prev, m));
         }
         el->flush();
     };

@@ -267,6 +267,15 @@ class GPUIPCheckClassify : public Element {
         if (_pkts.size() >= (_batch ? _batch : 1)) process_staged();
     }
 
+    // A non-batch upstream: the packet is parked in the same staging ring, so a
+    // stream of single pushes still reaches the device BATCH packets at a time
+    // (without BATCH every push is its own one-packet launch).
+    void push(int, Packet *p) override {
+        if (_pkts.size() == _cap) process_staged();
+        _pkts.push_back(p);
+        if (_pkts.size() >= (_batch ? _batch : 1)) process_staged();
+    }
+
     void flush() override {
         if (!_pkts.empty()) process_staged();
     }

@@ -50,8 +50,14 @@ typedef struct fcclick_result {
                                departure, little-endian (may be NULL)                  */
 } fcclick_result;
 
+/* burst value for a non-batch upstream: the source calls the element's
+ * per-packet push(0, p) (Element::push, lib/element.cc:3141-3147) instead of
+ * push_batch. */
+#define FCCLICK_PER_PACKET 0xffffffffu
+
 /* Run a graph  Source(frames, BURST) -> conf => [0 .. nsinks-1] Sink  over n
  * frames (arena + (offset, length) descriptors, host memory), then flush.
+ * burst 0 means 32; FCCLICK_PER_PACKET pushes the frames one at a time.
  * Returns 0 on success, -1 on configuration/initialisation error (message in
  * err), -2 when the element reported a GPU runtime error. */
 int fcclick_run(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,

@@ -125,6 +125,9 @@ def main():
     for batch in (4096, 65536, 262144):
         conf = f"GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BATCH {batch})"
         out[f"element_mpps_batch{batch}"] = round(K.bench_element(conf, b, burst=32, reps=3) / 1e6, 2)
+    conf = "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BATCH 65536)"
+    out["element_mpps_batch65536_per_packet_push"] = round(
+        K.bench_element(conf, b, burst=K.PER_PACKET, reps=3) / 1e6, 2)
     print(json.dumps(out))
 
 

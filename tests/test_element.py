@@ -119,6 +119,31 @@ def test_element_fragments_and_burst_sizes(oracle):
         assert np.array_equal(r["port"], e["port"].astype(np.uint32))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [0, 1024])
+def test_element_per_packet_push(oracle, batch):
+    """A non-batch upstream (Element::push per packet, lib/element.cc:3141-3147):
+    packets are staged like a batch's, so outputs, order and annotations equal
+    the BURST-32 run's and the oracle's."""
+    from fastclick_amd import click as K
+    b = synth.c3(3_000, seed=521)
+    set_fragment(b, 0.1)
+    conf = f"GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4, BATCH {batch})"
+    e = oracle.process_batch(N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=4), b)
+    r1 = K.run_element(conf, b, burst=K.PER_PACKET, nsinks=5)
+    r32 = K.run_element(conf, b, burst=32, nsinks=5)
+    assert np.array_equal(r1["port"], e["port"].astype(np.uint32))
+    # without BATCH every single push is its own launch, so arrival order at the
+    # sinks is input order rather than per-burst port order
+    for k in ("port", "agg", "len", "dst") + (("seq",) if batch else ()):
+        assert np.array_equal(r1[k], r32[k]), k
+    if not batch:
+        reached = r1["seq"] != 0xFFFFFFFF
+        assert reached.sum() > 0.9 * b.n
+        assert np.all(np.diff(r1["seq"][reached].astype(np.int64)) > 0)
+    assert r1["handlers"] == r32["handlers"]
+
+
 def test_config_color_keyword():
     from fastclick_amd import click as K
     K.check_config("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, STRIP true, COLOR 7)")
