@@ -190,6 +190,7 @@ struct fcgpu_ctx {
     // flow table (fcgpu_flow_enable)
     uint32_t max_flows = 0, flow_slots = 0, flow_words = 0;
     FlowArgs fl{};            // device pointers; fl.slots == nullptr: disabled
+    uint32_t *flow_hmiss = nullptr;   // mapped: the last batch's miss count (~0: unknown)
     // timing
     bool timing = false;
     std::vector<EvPair> pending;
@@ -419,8 +420,10 @@ static void flow_free(fcgpu_ctx *c) {
     FlowArgs &F = c->fl;
     for (void *p : {(void *)F.slots, (void *)F.claim, (void *)F.first, (void *)F.miss_pkt, (void *)F.miss_key,
                     (void *)F.miss_slot, (void *)F.miss_first, (void *)F.bitmap, (void *)F.wordpre,
-                    (void *)F.state})
+                    (void *)F.state, (void *)F.tickets})
         if (p) hipFree(p);
+    if (c->flow_hmiss) hipHostFree(c->flow_hmiss);
+    c->flow_hmiss = nullptr;
     F = FlowArgs{};
     c->max_flows = c->flow_slots = c->flow_words = 0;
 }
@@ -433,6 +436,10 @@ static int flow_clear(fcgpu_ctx *c) {
     HIPCHK(c, memset_sync(F.first, 0xff, sizeof(uint32_t) * c->flow_slots));
     HIPCHK(c, memset_sync(F.bitmap, 0, sizeof(uint32_t) * c->flow_words));
     HIPCHK(c, memset_sync(F.state, 0, sizeof(uint32_t) * 16));
+    const uint32_t big = 1;   // matches the host hint below
+    HIPCHK(c, hipMemcpy(F.state + kFsBig, &big, sizeof big, hipMemcpyHostToDevice));
+    HIPCHK(c, memset_sync(F.tickets, 0, sizeof(uint32_t) * 32 * kTicketShards));
+    *(volatile uint32_t *)c->flow_hmiss = 0xffffffffu;   // an empty table expects new flows
     return FCGPU_OK;
 }
 
@@ -459,6 +466,14 @@ int fcgpu_flow_enable(fcgpu_ctx *c, uint32_t max_flows) {
     HIPCHK(c, hipMalloc(&F.bitmap, sizeof(uint32_t) * words));
     HIPCHK(c, hipMalloc(&F.wordpre, sizeof(uint32_t) * words));
     HIPCHK(c, hipMalloc(&F.state, sizeof(uint32_t) * 16));
+    HIPCHK(c, hipMalloc(&F.tickets, sizeof(uint32_t) * 32 * kTicketShards));
+    HIPCHK(c, hipHostMalloc((void **)&c->flow_hmiss, sizeof(uint32_t), hipHostMallocMapped));
+    HIPCHK(c, hipHostGetDevicePointer((void **)&F.host_miss, c->flow_hmiss, 0));
+    {   // experiment knob: the new-flow pass in k_rx's last workgroup instead of
+        // a dependent launch -- slower per batch at steady state
+        const char *e = getenv("FCGPU_FLOW_INLINE");
+        F.inline_finish = e && atoi(e) != 0;
+    }
     F.mask = slots - 1;
     F.max_flows = max_flows;
     c->max_flows = max_flows;
@@ -481,7 +496,10 @@ int fcgpu_flow_count(fcgpu_ctx *c, uint32_t *count) {
     if (!c->fl.slots) return FCGPU_OK;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipDeviceSynchronize());
-    HIPCHK(c, hipMemcpy(count, c->fl.state + kFsNext, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    uint32_t st[3] = {0, 0, 0};
+    HIPCHK(c, hipMemcpy(st, c->fl.state, sizeof st, hipMemcpyDeviceToHost));
+    if (st[kFsStuck]) return fail(c, FCGPU_ERUNTIME, "flow table: a k_rx completion wait timed out");
+    *count = st[kFsNext];
     return FCGPU_OK;
 }
 
@@ -666,6 +684,9 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     a.cfg = c->dcfg;
     a.fl = c->fl;
     a.fl.flowid = o->flowid;
+    // a large batch of new flows goes to k_flow_finish's 1024 threads; the
+    // previous batch's count (maybe older: no sync) predicts this one's
+    a.fl.defer = a.fl.slots && (!a.fl.inline_finish || *(volatile uint32_t *)c->flow_hmiss > kInlineFinish);
     a.ip_rw = o->ip_rw;
     if (a.fl.slots && c->cfg.check_mode != FCGPU_CHECK_IP4 && c->cfg.check_mode != FCGPU_MARK_IP4)
         return fail(c, FCGPU_EINVAL, "the flow table needs an IPv4 check mode (CHECK_IP4 or MARK_IP4)");
@@ -677,7 +698,7 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, a, s, c->timing ? ev[0].a : nullptr,
                   c->timing ? ev[0].b : nullptr);
     HIPCHK(c, hipGetLastError());
-    if (a.fl.slots) {   // the batch's new flows get their IDs (fcgpu_flow.hh)
+    if (a.fl.defer) {   // the batch's new flows get their IDs (fcgpu_flow.hh)
         hipLaunchKernelGGL(k_flow_finish, dim3(1), dim3(kFinishBlock), 0, s, a.fl, (n + 31) / 32);
         HIPCHK(c, hipGetLastError());
     }

@@ -155,3 +155,46 @@ def test_gpu_flow_rejects_auto_mode():
     cfg = N.make_cfg(check_mode=N.CHECK_AUTO, offset=0, checksum=True, nports=4)
     with pytest.raises(RuntimeError, match="IPv4 check mode"):
         device.process_batches([b], cfg, max_flows=1024)
+
+
+def _with_new(base, k, seed):
+    """base's packets with k packets of fresh flows (about 4 packets each)
+    inserted at random positions: a batch with about k misses."""
+    rng = np.random.default_rng(seed)
+    frames = [base.frame(i) for i in range(base.n)]
+    if k:
+        new = synth.c3(k, nflows=max(k // 4, 1), seed=seed + 1000)
+        pos = np.sort(rng.integers(0, len(frames) + 1, k))
+        for j, p in enumerate(pos[::-1]):
+            frames.insert(int(p), new.frame(k - 1 - j))
+    return synth.from_frames(frames)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inline", [False, True])
+@pytest.mark.parametrize("max_flows", [1 << 16, 2_600])
+def test_gpu_flow_finish_paths(oracle, monkeypatch, max_flows, inline):
+    """Every path of the new-flow pass (fcgpu_flow.hh). Default: k_flow_finish
+    after every k_rx. With FCGPU_FLOW_INLINE=1: a cold table goes to
+    k_flow_finish; after a large batch a small one (<= 256 misses) is finished
+    by the last k_rx workgroup's LDS ranks while the queued k_flow_finish finds
+    nothing left; after a small batch a large one is finished by that
+    workgroup's bitmap pass (no k_flow_finish queued). Batches with no misses
+    and with one new flow on the last packet; with max_flows 2,600 the table
+    fills inside these paths (FCGPU_FLOW_FULL)."""
+    if inline:
+        monkeypatch.setenv("FCGPU_FLOW_INLINE", "1")
+    else:
+        monkeypatch.delenv("FCGPU_FLOW_INLINE", raising=False)
+    base = synth.c3(20_000, nflows=2_000, seed=60)
+    plan = [(0, 0), (100, 1), (200, 2), (3_000, 3), (5_000, 4), (0, 5), (150, 6)]
+    bs = [base if k == 0 and s == 0 else _with_new(base, k, 61 + s) for k, s in plan]
+    last = [base.frame(i) for i in range(base.n)] + [synth.c4(1, seed=99).frame(0)]
+    bs.append(synth.from_frames(last))
+    cfg = flow_cfg()
+    got, cnt, res = _dev_flows(cfg, bs, max_flows)
+    exp, ecnt = oracle_flows(oracle, cfg, bs, max_flows)
+    for j, (r, b) in enumerate(zip(res, bs)):
+        o = exp[sum(x.n for x in bs[:j]):][:b.n]
+        assert np.array_equal(r["flowid"], o), f"batch {j}: {np.count_nonzero(r['flowid'] != o)} IDs differ"
+    assert cnt == ecnt
