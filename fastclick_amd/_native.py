@@ -102,6 +102,8 @@ def anno_dtype():
 
 FLOW_NONE = 0xFFFFFFFF
 FLOW_FULL = 0xFFFFFFFE
+FLOW_MAX_BATCH = 64 * ((1 << 14) + 64)   # FCGPU_FLOW_MAX_BATCH
+MAX_FLOWS = 1 << 23
 
 
 class fcgpu_out(C.Structure):

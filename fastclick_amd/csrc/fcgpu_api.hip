@@ -190,7 +190,8 @@ struct fcgpu_ctx {
     // flow table (fcgpu_flow_enable)
     uint32_t max_flows = 0, flow_slots = 0, flow_words = 0;
     FlowArgs fl{};            // device pointers; fl.slots == nullptr: disabled
-    uint32_t *flow_hmiss = nullptr;   // mapped: the last batch's miss count (~0: unknown)
+    uint32_t *flow_hint = nullptr;    // mapped: size class of the last finish's misses (kHint*)
+    uint32_t flow_epoch = 0;          // batches through the table (FlowArgs::epoch)
     // timing
     bool timing = false;
     std::vector<EvPair> pending;
@@ -418,12 +419,12 @@ const char *fcgpu_last_error(fcgpu_ctx *ctx) { return ctx ? ctx->err.c_str() : g
 
 static void flow_free(fcgpu_ctx *c) {
     FlowArgs &F = c->fl;
-    for (void *p : {(void *)F.slots, (void *)F.claim, (void *)F.first, (void *)F.miss_pkt, (void *)F.miss_key,
-                    (void *)F.miss_slot, (void *)F.miss_first, (void *)F.bitmap, (void *)F.wordpre,
-                    (void *)F.state, (void *)F.tickets})
+    for (void *p : {(void *)F.slots, (void *)F.claim, (void *)F.first, (void *)F.miss_key, (void *)F.miss_slot,
+                    (void *)F.miss_first, (void *)F.missmask, (void *)F.firstmask, (void *)F.wordpre,
+                    (void *)F.state})
         if (p) hipFree(p);
-    if (c->flow_hmiss) hipHostFree(c->flow_hmiss);
-    c->flow_hmiss = nullptr;
+    if (c->flow_hint) hipHostFree(c->flow_hint);
+    c->flow_hint = nullptr;
     F = FlowArgs{};
     c->max_flows = c->flow_slots = c->flow_words = 0;
 }
@@ -434,18 +435,23 @@ static int flow_clear(fcgpu_ctx *c) {
     HIPCHK(c, memset_sync(F.slots, 0, sizeof(uint4) * c->flow_slots));
     HIPCHK(c, memset_sync(F.claim, 0, sizeof(uint32_t) * c->flow_slots));
     HIPCHK(c, memset_sync(F.first, 0xff, sizeof(uint32_t) * c->flow_slots));
-    HIPCHK(c, memset_sync(F.bitmap, 0, sizeof(uint32_t) * c->flow_words));
+    HIPCHK(c, memset_sync(F.missmask, 0, sizeof(uint64_t) * c->flow_words));
+    HIPCHK(c, memset_sync(F.firstmask, 0, sizeof(uint64_t) * c->flow_words));
+    c->flow_epoch = 0;
     HIPCHK(c, memset_sync(F.state, 0, sizeof(uint32_t) * 16));
-    const uint32_t big = 1;   // matches the host hint below
-    HIPCHK(c, hipMemcpy(F.state + kFsBig, &big, sizeof big, hipMemcpyHostToDevice));
-    HIPCHK(c, memset_sync(F.tickets, 0, sizeof(uint32_t) * 32 * kTicketShards));
-    *(volatile uint32_t *)c->flow_hmiss = 0xffffffffu;   // an empty table expects new flows
+    // an empty table expects many new flows: the grid-wide finish first
+    const uint32_t big = kHintBig;
+    HIPCHK(c, hipMemcpy(F.state + kFsHint, &big, sizeof big, hipMemcpyHostToDevice));
+    *(volatile uint32_t *)c->flow_hint = kHintBig;
     return FCGPU_OK;
 }
 
 int fcgpu_flow_enable(fcgpu_ctx *c, uint32_t max_flows) {
     if (!c) return FCGPU_EINVAL;
     if (max_flows > FCGPU_MAX_FLOWS) return fail(c, FCGPU_EINVAL, "max_flows above FCGPU_MAX_FLOWS");
+    static_assert(FCGPU_FLOW_MAX_BATCH == 64u * kLdsWords, "fcgpu_flow.hh kLdsWords");
+    if (max_flows && c->max_batch > FCGPU_FLOW_MAX_BATCH)
+        return fail(c, FCGPU_EINVAL, "flow table: the context's max_batch is above FCGPU_FLOW_MAX_BATCH");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipDeviceSynchronize());
     flow_free(c);
@@ -454,26 +460,20 @@ int fcgpu_flow_enable(fcgpu_ctx *c, uint32_t max_flows) {
     // fills the table): keep the load at or under 1/2
     uint32_t slots = 1024;
     while (slots < 2 * (max_flows + c->max_batch)) slots <<= 1;
-    const uint32_t words = (c->max_batch + 31) / 32 + 1;
+    const uint32_t words = (c->max_batch + 63) / 64 + 1;
     FlowArgs &F = c->fl;
     HIPCHK(c, hipMalloc(&F.slots, sizeof(uint4) * slots));
     HIPCHK(c, hipMalloc(&F.claim, sizeof(uint32_t) * slots));
     HIPCHK(c, hipMalloc(&F.first, sizeof(uint32_t) * slots));
-    HIPCHK(c, hipMalloc(&F.miss_pkt, sizeof(uint32_t) * c->max_batch));
     HIPCHK(c, hipMalloc(&F.miss_key, sizeof(uint4) * c->max_batch));
     HIPCHK(c, hipMalloc(&F.miss_slot, sizeof(uint32_t) * c->max_batch));
     HIPCHK(c, hipMalloc(&F.miss_first, sizeof(uint32_t) * c->max_batch));
-    HIPCHK(c, hipMalloc(&F.bitmap, sizeof(uint32_t) * words));
+    HIPCHK(c, hipMalloc(&F.missmask, sizeof(uint64_t) * words));
+    HIPCHK(c, hipMalloc(&F.firstmask, sizeof(uint64_t) * words));
     HIPCHK(c, hipMalloc(&F.wordpre, sizeof(uint32_t) * words));
     HIPCHK(c, hipMalloc(&F.state, sizeof(uint32_t) * 16));
-    HIPCHK(c, hipMalloc(&F.tickets, sizeof(uint32_t) * 32 * kTicketShards));
-    HIPCHK(c, hipHostMalloc((void **)&c->flow_hmiss, sizeof(uint32_t), hipHostMallocMapped));
-    HIPCHK(c, hipHostGetDevicePointer((void **)&F.host_miss, c->flow_hmiss, 0));
-    {   // experiment knob: the new-flow pass in k_rx's last workgroup instead of
-        // a dependent launch -- slower per batch at steady state
-        const char *e = getenv("FCGPU_FLOW_INLINE");
-        F.inline_finish = e && atoi(e) != 0;
-    }
+    HIPCHK(c, hipHostMalloc((void **)&c->flow_hint, sizeof(uint32_t), hipHostMallocMapped));
+    HIPCHK(c, hipHostGetDevicePointer((void **)&F.host_hint, c->flow_hint, 0));
     F.mask = slots - 1;
     F.max_flows = max_flows;
     c->max_flows = max_flows;
@@ -496,10 +496,7 @@ int fcgpu_flow_count(fcgpu_ctx *c, uint32_t *count) {
     if (!c->fl.slots) return FCGPU_OK;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipDeviceSynchronize());
-    uint32_t st[3] = {0, 0, 0};
-    HIPCHK(c, hipMemcpy(st, c->fl.state, sizeof st, hipMemcpyDeviceToHost));
-    if (st[kFsStuck]) return fail(c, FCGPU_ERUNTIME, "flow table: a k_rx completion wait timed out");
-    *count = st[kFsNext];
+    HIPCHK(c, hipMemcpy(count, c->fl.state + kFsNext, sizeof(uint32_t), hipMemcpyDeviceToHost));
     return FCGPU_OK;
 }
 
@@ -684,9 +681,10 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     a.cfg = c->dcfg;
     a.fl = c->fl;
     a.fl.flowid = o->flowid;
-    // a large batch of new flows goes to k_flow_finish's 1024 threads; the
-    // previous batch's count (maybe older: no sync) predicts this one's
-    a.fl.defer = a.fl.slots && (!a.fl.inline_finish || *(volatile uint32_t *)c->flow_hmiss > kInlineFinish);
+    if (a.fl.slots) {
+        if (++c->flow_epoch == 0) ++c->flow_epoch;   // never 0 (the cleared state)
+        a.fl.epoch = c->flow_epoch;
+    }
     a.ip_rw = o->ip_rw;
     if (a.fl.slots && c->cfg.check_mode != FCGPU_CHECK_IP4 && c->cfg.check_mode != FCGPU_MARK_IP4)
         return fail(c, FCGPU_EINVAL, "the flow table needs an IPv4 check mode (CHECK_IP4 or MARK_IP4)");
@@ -698,8 +696,17 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, a, s, c->timing ? ev[0].a : nullptr,
                   c->timing ? ev[0].b : nullptr);
     HIPCHK(c, hipGetLastError());
-    if (a.fl.defer) {   // the batch's new flows get their IDs (fcgpu_flow.hh)
-        hipLaunchKernelGGL(k_flow_finish, dim3(1), dim3(kFinishBlock), 0, s, a.fl, (n + 31) / 32);
+    if (a.fl.slots) {   // the batch's new flows get their IDs (fcgpu_flow.hh)
+        const uint32_t nw = (n + 63) / 64;
+        // the last finish's class of misses (no sync: maybe older) predicts this one's
+        if (*(volatile uint32_t *)c->flow_hint == kHintBig) {
+            const uint32_t g = std::max(1u, std::min((n + kFlowGridBlock - 1) / kFlowGridBlock, 2048u));
+            hipLaunchKernelGGL(k_flow_mark, dim3(g), dim3(kFlowGridBlock), 0, s, a.fl, nw);
+            hipLaunchKernelGGL(k_flow_scan, dim3(1), dim3(kFinishBlock), 0, s, a.fl, nw);
+            hipLaunchKernelGGL(k_flow_assign, dim3(g), dim3(kFlowGridBlock), 0, s, a.fl, nw);
+        } else {
+            hipLaunchKernelGGL(k_flow_finish, dim3(1), dim3(kFinishBlock), 0, s, a.fl, nw);
+        }
         HIPCHK(c, hipGetLastError());
     }
     if (want_global) {

@@ -62,26 +62,24 @@ struct FlowArgs {
     uint4 *slots;
     uint32_t mask;           // slots - 1
     uint32_t max_flows;
-    uint32_t *claim;         // [slots] miss entry + 1 claiming a slot this batch
+    uint32_t *claim;         // [slots] claiming miss packet + 1 (this batch)
     uint32_t *first;         // [slots] min packet index of the claiming flow
-    uint32_t *host_miss;     // mapped host word: the last batch's miss count (policy hint)
-    uint32_t inline_finish;  // the last k_rx workgroup runs the new-flow pass (FCGPU_FLOW_INLINE)
-    uint32_t defer;          // k_flow_finish follows k_rx: the last workgroup only
-                             // finishes batches of at most kInlineFinish misses
-    uint32_t *miss_pkt;      // [max_batch]
+    // per packet of the batch, meaningful where its missmask bit is set
     uint4 *miss_key;         // [max_batch]
     uint32_t *miss_slot;     // [max_batch]
     uint32_t *miss_first;    // [max_batch]
-    uint32_t *bitmap;        // [words] first-appearance bits of this batch's new flows
-    uint32_t *wordpre;       // [words] exclusive popcount prefix
+    uint64_t *missmask;      // [words64] bit i: packet i missed (every wave writes its word)
+    uint64_t *firstmask;     // [words64] bit i: packet i is a new flow's first packet
+    uint32_t *wordpre;       // [words64] exclusive popcount prefix of firstmask
     uint32_t *state;         // kFs* words below
-    uint32_t *tickets;       // [kTicketShards * 32] workgroups done, one 128-B line per shard
+    uint32_t *host_hint;     // mapped host word: size class of the last batch's misses (kHint*)
     uint32_t *flowid;        // [n] output (may be null)
+    uint32_t epoch;          // this batch's number (never 0)
 };
-constexpr uint32_t kFsNext = 0, kFsMiss = 1;   // next flow ID; misses appended this batch
-constexpr uint32_t kFsStuck = 2;               // the completion wait timed out (never expected)
-constexpr uint32_t kFsBig = 3;                 // the host hint says "more than kInlineFinish"
-constexpr uint32_t kTicketShards = 64;         // FlowArgs::tickets
+constexpr uint32_t kFsNext = 0;   // next flow ID
+constexpr uint32_t kFsBase = 1;   // the ID base of the batch being finished (grid-wide finish)
+constexpr uint32_t kFsMissed = 2; // epoch of the last batch with a miss
+constexpr uint32_t kFsHint = 3;   // the hint last published
 constexpr uint32_t kFlowMiss = 0xfffffffdu;
 constexpr uint32_t kSlotNone = 0xffffffffu;
 
@@ -823,7 +821,7 @@ __device__ __forceinline__ FlowProbe flow_issue(const FlowArgs &F, const FrameVi
     return q;
 }
 // A miss claims its key's slot right away (see fcgpu_flow.hh): its key is
-// published in the miss list before the CAS (release fence), and a lane that
+// published in the miss list before the CAS (flow_resolve), and a lane that
 // finds another miss's claim reads that key with agent-scope loads.
 __device__ __forceinline__ uint32_t flow_claim(const FlowArgs &F, uint4 k, uint32_t pos, uint32_t e) {
     if (__hip_atomic_load(&F.state[kFsNext], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= F.max_flows)
@@ -846,8 +844,7 @@ __device__ __forceinline__ uint32_t flow_claim(const FlowArgs &F, uint4 k, uint3
     return kSlotNone;
 }
 
-// Returns whether the wave appended misses.
-__device__ __forceinline__ bool flow_resolve(const FlowArgs &F, FlowProbe &q, bool live, uint32_t i) {
+__device__ __forceinline__ void flow_resolve(const FlowArgs &F, FlowProbe &q, bool live, uint32_t i) {
     uint32_t id = FCGPU_FLOW_NONE;
     if (q.want) {
         id = kFlowMiss;
@@ -858,196 +855,35 @@ __device__ __forceinline__ bool flow_resolve(const FlowArgs &F, FlowProbe &q, bo
             q.sl = F.slots[q.pos];
         }
     }
-    const uint64_t mm = __ballot(id == kFlowMiss);
-    if (mm) {
-        const uint32_t lane = threadIdx.x & 63;
-        const uint32_t lead = (uint32_t)__builtin_ctzll(mm);
-        uint32_t base = 0;
-        if (lane == lead) base = atomicAdd(&F.state[kFsMiss], (uint32_t)__popcll(mm));
-        base = __shfl(base, (int)lead);
-        if (id == kFlowMiss) {
-            const uint32_t e = base + (uint32_t)__popcll(mm & ((1ull << lane) - 1ull));
-            F.miss_pkt[e] = i;
-            F.miss_key[e] = q.key;
-            __threadfence();
-            const uint32_t slot = flow_claim(F, q.key, q.pos, e);   // q.pos: first empty slot
-            F.miss_slot[e] = slot;
-            if (slot != kSlotNone) atomicMin(&F.first[slot], i);
-        }
+    // No miss list and no counter: a miss keeps its packet index (its record
+    // lives at index i), the wave writes its 64-bit miss word, and a wave with
+    // misses stamps the batch's epoch -- plain stores: only the next launch
+    // reads them, and the XCD's L2 absorbs the repeated stamp. (An atomic on
+    // one miss counter per wave with misses, or a coherent store of the stamp
+    // that the wave then waits for, serialised at ~30 ns each at the memory:
+    // 10k misses cost 300 us.)
+    const uint64_t mm = __ballot(id == kFlowMiss), lv = __ballot(live);
+    if ((threadIdx.x & 63) == 0 && lv) {
+        F.missmask[i >> 6] = mm;
+        if (mm) F.state[kFsMissed] = F.epoch;
+    }
+    if (id == kFlowMiss) {
+        // publish the key to lanes that will find this miss's claim: agent-
+        // scope stores, acknowledged at the coherence point (vmcnt) before
+        // the CAS issues. (__threadfence would also write back and
+        // invalidate this XCD's whole L2 -- buffer_wbl2/inv sc1 -- once per
+        // wave with a miss.)
+        uint32_t *kp = reinterpret_cast<uint32_t *>(&F.miss_key[i]);
+        __hip_atomic_store(kp + 0, q.key.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(kp + 1, q.key.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(kp + 2, q.key.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(kp + 3, q.key.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t slot = flow_claim(F, q.key, q.pos, i);   // q.pos: first empty slot
+        F.miss_slot[i] = slot;
+        if (slot != kSlotNone) atomicMin(&F.first[slot], i);
     }
     if (live && F.flowid) F.flowid[i] = id;
-    return mm != 0;
-}
-
-// ---- the batch's new-flow pass (see fcgpu_flow.hh) -------------------------
-// IDs go to new flows in order of first appearance. The last k_rx workgroup to
-// finish (a ticket) runs the pass itself -- for up to kInlineFinish misses with
-// ranks from an LDS compare (flow_finish_small), beyond that with the bitmap
-// pass (flow_finish_block) unless the host queued k_flow_finish (defer), which
-// does the same with 1024 threads. Steady state (no misses) costs one atomic
-// per workgroup and no launch.
-constexpr uint32_t kInlineFinish = kTile;
-
-__device__ __forceinline__ uint32_t ld_agent(const uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The flow's ID (FULL past max_flows or without a slot); its first packet
-// commits the slot (key + tag) and frees the claim. A flow the table had no
-// ID left for is committed as FULL too, so later lookups of keys that probe
-// past this slot still find their own.
-__device__ __forceinline__ uint32_t flow_commit(const FlowArgs &F, uint32_t e, uint32_t pkt, uint32_t slot,
-                                                uint32_t fp, uint32_t next, uint32_t rank) {
-    uint32_t id = FCGPU_FLOW_FULL;
-    if (slot != kSlotNone) {
-        if (next + rank < F.max_flows) id = next + rank;
-        if (pkt == fp) {
-            const uint4 k = F.miss_key[e];
-            F.slots[slot] = make_uint4(k.x, k.y, k.z, k.w | ((id != FCGPU_FLOW_FULL ? id + 1u : kTagFull) << 8));
-            F.claim[slot] = 0;
-            F.first[slot] = 0xffffffffu;
-        }
-    }
-    if (F.flowid) F.flowid[pkt] = id;
-    return id;
-}
-
-__device__ __forceinline__ void flow_advance(const FlowArgs &F, uint32_t next, uint32_t total) {
-    const uint32_t room = next < F.max_flows ? F.max_flows - next : 0u;
-    F.state[kFsNext] = next + (total < room ? total : room);
-    F.state[kFsMiss] = 0;
-}
-
-// m <= blockDim.x misses, one per thread: a miss's rank is the number of
-// first appearances (packet indices) before its flow's first packet.
-__device__ __forceinline__ void flow_finish_small(const FlowArgs &F, uint32_t m, uint32_t *s_f) {
-    const uint32_t t = threadIdx.x;
-    const uint32_t next = ld_agent(&F.state[kFsNext]);
-    uint32_t pkt = 0, slot = kSlotNone, fp = kSlotNone;
-    if (t < m) {
-        pkt = F.miss_pkt[t];
-        slot = F.miss_slot[t];
-        if (slot != kSlotNone) fp = ld_agent(&F.first[slot]);
-    }
-    if (t < blockDim.x) s_f[t] = (slot != kSlotNone && fp == pkt) ? pkt : 0xffffffffu;
-    __syncthreads();
-    uint32_t rank = 0, total = 0;
-    for (uint32_t j = 0; j < m; ++j) {
-        const uint32_t v = s_f[j];
-        rank += v < fp;
-        total += v != 0xffffffffu;
-    }
-    if (t < m) flow_commit(F, t, pkt, slot, fp, next, rank);
-    if (t == 0) flow_advance(F, next, total);
-}
-
-// Any m, one block of BS threads: the first packet of each new flow sets its
-// bit in a bitmap over packet indices; an exclusive popcount prefix over the
-// bitmap words gives each first appearance its rank.
-template <int BS>
-__device__ void flow_finish_block(const FlowArgs &F, uint32_t nwords, uint32_t m, uint32_t *s_w) {
-    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const uint32_t next = ld_agent(&F.state[kFsNext]);
-    for (uint32_t e = t; e < m; e += BS) {
-        const uint32_t slot = F.miss_slot[e];
-        uint32_t fp = kSlotNone;
-        if (slot != kSlotNone) {
-            fp = ld_agent(&F.first[slot]);
-            const uint32_t pkt = F.miss_pkt[e];
-            if (fp == pkt) atomicOr(&F.bitmap[pkt >> 5], 1u << (pkt & 31));
-        }
-        F.miss_first[e] = fp;
-    }
-    __syncthreads();
-    // thread t owns a contiguous chunk of words
-    const uint32_t per = (nwords + BS - 1) / BS, w0 = t * per;
-    uint32_t sum = 0;
-    for (uint32_t j = 0; j < per; ++j)
-        if (w0 + j < nwords) sum += (uint32_t)__popc(ld_agent(&F.bitmap[w0 + j]));
-    const uint32_t incl = wave_incl_scan(sum);
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    uint32_t run = incl - sum, total = 0;
-    for (uint32_t w = 0; w < BS / 64; ++w) {
-        run += w < wave ? s_w[w] : 0u;
-        total += s_w[w];
-    }
-    for (uint32_t j = 0; j < per; ++j) {
-        if (w0 + j < nwords) {
-            F.wordpre[w0 + j] = run;
-            run += (uint32_t)__popc(ld_agent(&F.bitmap[w0 + j]));
-        }
-    }
-    __syncthreads();
-    for (uint32_t e = t; e < m; e += BS) {
-        const uint32_t pkt = F.miss_pkt[e], slot = F.miss_slot[e], fp = F.miss_first[e];
-        uint32_t rank = 0;
-        if (slot != kSlotNone) {
-            const uint32_t w = fp >> 5;
-            rank = ld_agent(&F.wordpre[w]) + (uint32_t)__popc(ld_agent(&F.bitmap[w]) & ((1u << (fp & 31)) - 1u));
-        }
-        flow_commit(F, e, pkt, slot, fp, next, rank);
-    }
-    __syncthreads();
-    for (uint32_t w = t; w < nwords; w += BS) F.bitmap[w] = 0;
-    if (t == 0) flow_advance(F, next, total);
-}
-
-// k_rx's last workgroup (lds: the block's window buffer, free once the tile is done).
-// Agent-scope fences write back / invalidate the XCD's L2 on gfx950 (the L2s
-// of the 8 XCDs are not coherent with each other), so they run only where
-// there is something to publish: a workgroup that appended misses releases
-// them before taking its ticket; the last workgroup acquires only if the
-// batch has misses (the miss counter itself is an atomic).
-__device__ __forceinline__ void flow_epilogue(const RxArgs &A, uint32_t *lds, bool missed) {
-    const FlowArgs &F = A.fl;
-    uint32_t *s_f = lds, *s_w = lds + kTile;
-    if (!F.inline_finish) return;     // k_flow_finish does it (the default)
-    if (__syncthreads_or(missed)) __threadfence();
-    // Completion count without a returning atomic: every other workgroup adds
-    // 1 to counter b % 64 (one 128-B line each, fire and forget); the last
-    // workgroup of the grid -- dispatched after all the others, so they are
-    // resident or done and its wait always ends -- waits for the 64 counters
-    // to reach their quotas. (A returning ticket per workgroup, even sharded,
-    // cost 3.5 us per 1M packets: each workgroup held its slot for the
-    // round trip.)
-    const uint32_t b = blockIdx.x, last = gridDim.x - 1;
-    if (b != last) {
-        if (threadIdx.x == 0)
-            __hip_atomic_fetch_add(&F.tickets[(b % kTicketShards) * 32], 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    if (threadIdx.x < kTicketShards && threadIdx.x < gridDim.x) {
-        const uint32_t sh = threadIdx.x;
-        uint32_t quota = (gridDim.x - sh + kTicketShards - 1) / kTicketShards;
-        if (last % kTicketShards == sh) --quota;      // this workgroup does not count itself
-        // bounded: a count that never arrives (a bug) flags kFsStuck instead of hanging
-        uint32_t spins = 0;
-        while (ld_agent(&F.tickets[sh * 32]) < quota) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins == (1u << 24)) {
-                atomicOr(&F.state[kFsStuck], 1u);
-                break;
-            }
-        }
-        __hip_atomic_store(&F.tickets[sh * 32], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    const uint32_t m = ld_agent(&F.state[kFsMiss]);
-    // the host's hint changes only when the batch crosses kInlineFinish (a
-    // store over PCIe at the end of every kernel would cost its latency)
-    if (threadIdx.x == 0 && F.host_miss) {
-        const uint32_t big = m > kInlineFinish;
-        if (big != ld_agent(&F.state[kFsBig])) {
-            F.state[kFsBig] = big;
-            __hip_atomic_store(F.host_miss, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-    if (m == 0) return;
-    __threadfence();                  // acquire every other workgroup's misses
-    if (m <= kInlineFinish) flow_finish_small(F, m, s_f);
-    else if (!F.defer) flow_finish_block<kTile>(F, (A.n + 31) / 32, m, s_w);
 }
 
 // ---- header rewrites after the classifier ----------------
@@ -1115,7 +951,7 @@ __device__ __forceinline__ void rw_stage(const DevCfg &c, const FrameView &f, ui
 // optionally the tile's stable per-output partition (CLASSIFY_EACH_PACKET on a
 // 256-packet PacketBatch).
 template <int CM, bool CK, int PART, bool PROG, bool L4, bool FAST, bool FLOW>
-__device__ __forceinline__ bool rx_tile(const RxArgs &A, uint32_t tile, uint2 d, const uint8_t *wl,
+__device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d, const uint8_t *wl,
                                         uint32_t (*s_cnt)[kMaxBins], const uint4 *sprog) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t i = tile * kTile + threadIdx.x;
@@ -1218,8 +1054,7 @@ __device__ __forceinline__ bool rx_tile(const RxArgs &A, uint32_t tile, uint2 d,
             if (A.tile_perm) A.tile_perm[pos] = (uint8_t)threadIdx.x;
         }
     }
-    bool missed = false;
-    if (FLOW) missed = flow_resolve(A.fl, fq, live, i);
+    if (FLOW) flow_resolve(A.fl, fq, live, i);
     // counters: one atomic per non-zero bin per tile, sharded by tile. "count"
     // and "drops" are not kept here: both follow from these bins on read
     // (fcgpu_counters_derive), which saves an atomic per tile (-0.4 us / 1M).
@@ -1230,7 +1065,6 @@ __device__ __forceinline__ bool rx_tile(const RxArgs &A, uint32_t tile, uint2 d,
             else atomicAdd(&ctr[FCGPU_CTR_REASON + (t - nb)], (unsigned long long)tot);
         }
     }
-    return missed;
 }
 
 
@@ -1257,9 +1091,7 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
     if (prog_lds && threadIdx.x < A.cfg.prog_n) s_prog[threadIdx.x] = A.cfg.prog[threadIdx.x];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (prog_lds) __syncthreads();
-    const bool missed = rx_tile<CM, CK, PART, PROG, L4, FAST, FLOW>(A, tile, d, wl, s_cnt,
-                                                                    prog_lds ? s_prog : nullptr);
-    if constexpr (FLOW) flow_epilogue(A, reinterpret_cast<uint32_t *>(s_win), missed);
+    rx_tile<CM, CK, PART, PROG, L4, FAST, FLOW>(A, tile, d, wl, s_cnt, prog_lds ? s_prog : nullptr);
 }
 
 // Exclusive scan of one output's per-tile counts (in place) and its total.

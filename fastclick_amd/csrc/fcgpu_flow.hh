@@ -7,35 +7,346 @@
 //
 //   k_rx (flow_issue / flow_resolve, fcgpu_device.hh): every checked packet
 //     looks its IPFlow5ID up in the table. A miss -- a flow the table has not
-//     seen -- appends (packet, key) to the batch's miss list and claims a slot
-//     for its key: the first miss of a key to reach an empty slot claims it
-//     (CAS on `claim`), later misses of the same key find the claim and compare
-//     keys, so all misses of one key end on one slot; atomicMin leaves the
-//     flow's first packet index in `first`.
-//   the finish: the first packet of each new flow gets rank = the number of
-//     first appearances before it; ID = next + rank. The first packet commits
-//     the slot (key + tag) and frees the claim; every miss gets its flow's ID;
-//     the counter advances. The last k_rx workgroup to finish runs it
-//     (flow_epilogue, fcgpu_device.hh): up to kInlineFinish misses by an LDS
-//     compare, more with a bitmap over packet indices and an exclusive popcount
-//     prefix over its words -- unless the host expects a large batch of new
-//     flows (the previous batch's miss count, read from a mapped word) and
-//     queued k_flow_finish, the same bitmap pass on 1024 threads.
+//     seen -- keeps its record (key, slot) at its packet index and claims a
+//     slot for its key: the first miss of a key to reach an empty slot claims
+//     it (CAS on `claim`), later misses of the same key find the claim and
+//     compare keys, so all misses of one key end on one slot; atomicMin leaves
+//     the flow's first packet index in `first`. Each wave writes its 64-bit
+//     miss word; a wave with a miss stamps the batch's epoch.
+//   the finish (this file, after k_rx on the same stream): the first packet of
+//     each new flow gets rank = the number of first appearances before it;
+//     ID = next + rank. The first packet commits the slot (key + tag) and
+//     frees the claim; every miss gets its flow's ID; the counter advances.
 //
-// With no new flows (steady state) nothing but the ticket runs.
+// Two shapes of finish, chosen by the host from a hint the previous finish
+// published in mapped host memory (the size class of its batch's misses):
+//
+//   k_flow_finish (one block): batch without misses (epoch not stamped) ->
+//     returns at its first load; up to kSmallFinish (4096) misses -> the
+//     misses are compacted in packet order from the miss words into LDS, four
+//     per thread; a block scan ranks the first packets and every miss finds
+//     its flow's first packet by binary search; more (the hint was wrong) -> the grid-wide pass inside this block
+//     (slow: milliseconds for 1M misses).
+//   k_flow_mark / k_flow_scan / k_flow_assign (grid-wide, for batches with
+//     many misses): each wave marks the first packets among its 64 packets
+//     as a 64-bit word; an exclusive popcount prefix over those words (one
+//     block, coalesced loads transposed through LDS) ranks them; every miss takes its
+//     ID. Nothing needs clearing: every word is rewritten each batch.
 #pragma once
 #include "fcgpu_device.hh"
 
 namespace fcgpu {
 
 constexpr int kFinishBlock = 1024;
+constexpr uint32_t kSmallFinish = 4 * kFinishBlock;   // misses k_flow_finish ranks in LDS
+// hint classes (FlowArgs::host_hint)
+constexpr uint32_t kHintNone = 0, kHintSmall = 1, kHintBig = 2;
 
-// nwords = ceil(n / 32) of this batch. One block of kFinishBlock threads.
-__global__ __launch_bounds__(kFinishBlock) void k_flow_finish(FlowArgs F, uint32_t nwords) {
+__device__ __forceinline__ uint32_t hint_class(uint32_t m) {
+    return m == 0 ? kHintNone : m <= kSmallFinish ? kHintSmall : kHintBig;
+}
+// Written only when the class changes: a store over the host link costs its
+// latency at the end of the launch.
+__device__ __forceinline__ void publish_hint(const FlowArgs &F, uint32_t m) {
+    const uint32_t h = hint_class(m);
+    if (h != F.state[kFsHint]) {
+        F.state[kFsHint] = h;
+        __hip_atomic_store(F.host_hint, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// The flow's ID (FULL past max_flows or without a slot); its first packet
+// commits the slot (key + tag) and frees the claim. A flow the table had no
+// ID left for is committed as FULL too, so later lookups of keys that probe
+// past this slot still find their own.
+__device__ __forceinline__ void flow_commit(const FlowArgs &F, uint32_t i, uint32_t slot, uint32_t fp,
+                                            uint32_t base, uint32_t rank) {
+    uint32_t id = FCGPU_FLOW_FULL;
+    if (slot != kSlotNone) {
+        if (base + rank < F.max_flows) id = base + rank;
+        if (i == fp) {
+            const uint4 k = F.miss_key[i];
+            F.slots[slot] = make_uint4(k.x, k.y, k.z, k.w | ((id != FCGPU_FLOW_FULL ? id + 1u : kTagFull) << 8));
+            F.claim[slot] = 0;
+            F.first[slot] = 0xffffffffu;
+        }
+    }
+    if (F.flowid) F.flowid[i] = id;
+}
+
+__device__ __forceinline__ uint32_t flow_next_after(const FlowArgs &F, uint32_t next, uint32_t total) {
+    const uint32_t room = next < F.max_flows ? F.max_flows - next : 0u;
+    return next + (total < room ? total : room);
+}
+
+// The wave's 64 packets from i0 (a multiple of 64): the first packet of each
+// new flow sets its bit in the wave's first-packet word (written even when 0).
+__device__ __forceinline__ void flow_mark_wave(const FlowArgs &F, uint32_t i0) {
+    const uint32_t lane = threadIdx.x & 63, i = i0 + lane;
+    const uint64_t mw = F.missmask[i0 >> 6];
+    bool isfirst = false;
+    if ((mw >> lane) & 1u) {
+        const uint32_t slot = F.miss_slot[i];
+        uint32_t fp = kSlotNone;
+        if (slot != kSlotNone) {
+            fp = F.first[slot];
+            isfirst = fp == i;
+        }
+        F.miss_first[i] = fp;
+    }
+    const uint64_t fm = __ballot(isfirst);
+    if (lane == 0) F.firstmask[i0 >> 6] = fm;
+}
+
+__device__ __forceinline__ void flow_assign_wave(const FlowArgs &F, uint32_t i0, uint32_t base) {
+    const uint32_t lane = threadIdx.x & 63, i = i0 + lane;
+    const uint64_t mw = F.missmask[i0 >> 6];
+    if ((mw >> lane) & 1u) {
+        const uint32_t slot = F.miss_slot[i], fp = F.miss_first[i];
+        uint32_t rank = 0;
+        if (slot != kSlotNone) {
+            const uint32_t w = fp >> 6;
+            rank = F.wordpre[w] + (uint32_t)__popcll(F.firstmask[w] & ((1ull << (fp & 63)) - 1ull));
+        }
+        flow_commit(F, i, slot, fp, base, rank);
+    }
+}
+
+// Block-wide exclusive scan of one value per thread; total to every thread.
+template <int BS>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, uint32_t &total) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_scan(v);
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t carry = 0;
+    total = 0;
+    for (uint32_t w = 0; w < BS / 64; ++w) {
+        carry += w < wave ? s_w[w] : 0u;
+        total += s_w[w];
+    }
+    __syncthreads();                  // s_w free again
+    return carry + incl - v;
+}
+
+// The mask words are read coalesced (a word per lane, 16 loads in flight per
+// thread) and their popcounts transposed through LDS to the thread-contiguous
+// order a block scan needs. (Reading 16 contiguous words per thread instead
+// touched 64 lines per load instruction: 25 us for two 128-KB masks.)
+constexpr uint32_t kLdsWords = (1u << 14) + 64;   // batches up to 1M + 4096 packets
+
+// s_pre[w] = popcount(mask[w]) for w < nw (nw <= kLdsWords); returns this
+// thread's share of the total, and of mask2's in `other`. Fixed trip count,
+// predicated loads: all of a thread's loads are in flight together (a loop
+// with a bound check per step waited for each load in turn: ~16 us).
+template <int BS, bool TWO>
+__device__ __forceinline__ uint32_t popc_to_lds(const uint64_t *mask, uint32_t nw, uint32_t *s_pre,
+                                                const uint64_t *mask2, uint32_t &other) {
+    constexpr uint32_t kIt = (kLdsWords + BS - 1) / BS;
+    uint64_t a[kIt], b[kIt];
+#pragma unroll
+    for (uint32_t k = 0; k < kIt; ++k) {
+        const uint32_t w = threadIdx.x + k * BS, wc = w < nw ? w : nw - 1;   // clamped: no branch
+        a[k] = mask[wc];
+        b[k] = TWO ? mask2[wc] : 0ull;
+    }
+    uint32_t c = 0, c2 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kIt; ++k) {
+        const uint32_t w = threadIdx.x + k * BS;
+        const uint32_t v = w < nw ? (uint32_t)__popcll(a[k]) : 0u;
+        if (w < nw) s_pre[w] = v;
+        c += v;
+        c2 += w < nw ? (uint32_t)__popcll(b[k]) : 0u;
+    }
+    other = c2;
+    return c;
+}
+
+// One block over the nw 64-bit words: exclusive popcount prefix of the
+// first-packet words into wordpre; returns {new flows, misses}.
+template <int BS>
+__device__ uint2 mask_prefix(const FlowArgs &F, uint32_t nw, uint32_t *s_w, uint32_t *s_pre) {
+    uint32_t cm;
+    popc_to_lds<BS, true>(F.firstmask, nw, s_pre, F.missmask, cm);
+    __syncthreads();
+    const uint32_t per = (nw + BS - 1) / BS, w0 = threadIdx.x * per;
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < per; ++k)
+        if (w0 + k < nw) sum += s_pre[w0 + k];
+    uint32_t tf, tm;
+    uint32_t off = block_excl_scan<BS>(sum, s_w, tf);
+    block_excl_scan<BS>(cm, s_w, tm);
+    for (uint32_t k = 0; k < per; ++k) {
+        if (w0 + k < nw) {
+            const uint32_t c = s_pre[w0 + k];
+            s_pre[w0 + k] = off;
+            off += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < nw; w += BS) F.wordpre[w] = s_pre[w];
+    return make_uint2(tf, tm);
+}
+
+// nw = ceil(n / 64) of this batch (<= kLdsWords). One block of kFinishBlock
+// threads. The misses are taken in packet order, kSmallFinish at a time: a
+// chunk's misses are compacted into LDS, their slots and first packets loaded
+// together, the first packets ranked by a block scan (plus the first packets
+// of earlier chunks), and every other miss finds its flow's first packet in
+// the chunk by binary search -- or, when it lay in an earlier chunk, takes
+// the ID from the slot that chunk committed. Cost grows with the misses, not the
+// batch: one chunk for <= 4096 misses.
+__global__ __launch_bounds__(kFinishBlock) void k_flow_finish(FlowArgs F, uint32_t nw) {
+    constexpr uint32_t kQ = kSmallFinish / kFinishBlock;     // misses per thread per chunk
+    constexpr uint32_t kIt = (kLdsWords + kFinishBlock - 1) / kFinishBlock;
+    __shared__ uint32_t s_idx[kSmallFinish], s_f[kSmallFinish], s_pre[kLdsWords + 1];
     __shared__ uint32_t s_w[kFinishBlock / 64];
-    const uint32_t m = F.state[kFsMiss];
-    if (m == 0) return;          // no new flows, or the last k_rx workgroup took them
-    flow_finish_block<kFinishBlock>(F, nwords, m, s_w);
+    const uint32_t t = threadIdx.x;
+    if (F.state[kFsMissed] != F.epoch) {      // no misses in this batch
+        if (t == 0) publish_hint(F, 0);
+        return;
+    }
+    const uint32_t next = F.state[kFsNext];
+    // miss words: word w = t + k * kFinishBlock stays in registers; its
+    // popcount goes to LDS, becomes the word's first miss index (exclusive
+    // prefix in word order, via thread-contiguous chunks of LDS)
+    uint64_t a[kIt];
+#pragma unroll
+    for (uint32_t k = 0; k < kIt; ++k) {
+        const uint32_t w = t + k * kFinishBlock;
+        a[k] = F.missmask[w < nw ? w : nw - 1];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kIt; ++k) {
+        const uint32_t w = t + k * kFinishBlock;
+        if (w < nw) s_pre[w] = (uint32_t)__popcll(a[k]);
+        else a[k] = 0;
+    }
+    __syncthreads();
+    const uint32_t per = (nw + kFinishBlock - 1) / kFinishBlock, w0 = t * per;
+    uint32_t c = 0;
+    for (uint32_t k = 0; k < per; ++k)
+        if (w0 + k < nw) c += s_pre[w0 + k];
+    uint32_t m;
+    uint32_t off = block_excl_scan<kFinishBlock>(c, s_w, m);
+    for (uint32_t k = 0; k < per; ++k) {
+        if (w0 + k < nw) {
+            const uint32_t v = s_pre[w0 + k];
+            s_pre[w0 + k] = off;
+            off += v;
+        }
+    }
+    if (t == 0) s_pre[nw] = m;
+    __syncthreads();
+    uint32_t nfirst_before = 0;
+    for (uint32_t c0 = 0; c0 < m; c0 += kSmallFinish) {
+        const uint32_t cn = m - c0 < kSmallFinish ? m - c0 : kSmallFinish;
+#pragma unroll
+        for (uint32_t k = 0; k < kIt; ++k) {
+            uint64_t x = a[k];
+            if (!x) continue;
+            const uint32_t w = t + k * kFinishBlock;
+            uint32_t e = s_pre[w];
+            if (e >= c0 + cn || s_pre[w + 1] <= c0) continue;
+            while (x) {
+                if (e >= c0 && e < c0 + cn) s_idx[e - c0] = w * 64 + (uint32_t)__builtin_ctzll(x);
+                ++e;
+                x &= x - 1;
+            }
+        }
+        __syncthreads();
+        // kQ consecutive entries per thread; loads from clamped indices and
+        // results selected, so all of them are in flight at once
+        const uint32_t e0 = t * kQ;
+        uint32_t pkt[kQ], slot[kQ], fp[kQ];
+#pragma unroll
+        for (uint32_t q = 0; q < kQ; ++q) {
+            pkt[q] = e0 + q < cn ? s_idx[e0 + q] : 0u;
+            const uint32_t sl = F.miss_slot[pkt[q]];
+            slot[q] = e0 + q < cn ? sl : kSlotNone;
+        }
+        uint32_t nfirst = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kQ; ++q) {
+            // agent-scope: a slot committed by an earlier chunk has first[] reset
+            const uint32_t f = __hip_atomic_load(&F.first[slot[q] != kSlotNone ? slot[q] : 0u], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            fp[q] = slot[q] != kSlotNone ? f : kSlotNone;
+            nfirst += slot[q] != kSlotNone && fp[q] == pkt[q];
+        }
+        uint32_t nf;
+        uint32_t r = nfirst_before + block_excl_scan<kFinishBlock>(nfirst, s_w, nf);
+#pragma unroll
+        for (uint32_t q = 0; q < kQ; ++q) {
+            if (e0 + q < cn) s_f[e0 + q] = r;
+            r += slot[q] != kSlotNone && fp[q] == pkt[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t q = 0; q < kQ; ++q) {
+            if (e0 + q >= cn) continue;
+            if (slot[q] != kSlotNone && fp[q] == 0xffffffffu) {
+                // the flow's first packet was in an earlier chunk: its slot
+                // holds the ID already
+                const uint32_t tag = __hip_atomic_load(reinterpret_cast<const uint32_t *>(&F.slots[slot[q]]) + 3,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (F.flowid) F.flowid[pkt[q]] = flow_tag_id(tag);
+                continue;
+            }
+            uint32_t rank = 0;
+            if (slot[q] != kSlotNone) {
+                uint32_t lo = 0, hi = cn;         // the entry of fp in this chunk
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_idx[mid] < fp[q]) lo = mid + 1;
+                    else hi = mid;
+                }
+                rank = s_f[lo];
+            }
+            flow_commit(F, pkt[q], slot[q], fp[q], next, rank);
+        }
+        nfirst_before += nf;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // commits done before the next chunk looks
+        __syncthreads();                      // s_idx / s_f reused by the next chunk
+    }
+    if (t == 0) {
+        F.state[kFsNext] = flow_next_after(F, next, nfirst_before);
+        publish_hint(F, m);
+    }
+}
+
+// ---- grid-wide finish (the hint says many misses) ---------------------------
+constexpr int kFlowGridBlock = 256;
+
+__global__ __launch_bounds__(kFlowGridBlock) void k_flow_mark(FlowArgs F, uint32_t nw) {
+    if (F.state[kFsMissed] != F.epoch) return;
+    for (uint32_t i0 = blockIdx.x * kFlowGridBlock + (threadIdx.x & ~63u); i0 < nw * 64;
+         i0 += gridDim.x * kFlowGridBlock)
+        flow_mark_wave(F, i0);
+}
+
+__global__ __launch_bounds__(kFinishBlock) void k_flow_scan(FlowArgs F, uint32_t nw) {
+    __shared__ uint32_t s_w[kFinishBlock / 64], s_pre[kLdsWords];
+    if (F.state[kFsMissed] != F.epoch) {
+        if (threadIdx.x == 0) publish_hint(F, 0);
+        return;
+    }
+    const uint2 tot = mask_prefix<kFinishBlock>(F, nw, s_w, s_pre);
+    if (threadIdx.x == 0) {
+        const uint32_t next = F.state[kFsNext];
+        F.state[kFsBase] = next;
+        F.state[kFsNext] = flow_next_after(F, next, tot.x);
+        publish_hint(F, tot.y);
+    }
+}
+
+__global__ __launch_bounds__(kFlowGridBlock) void k_flow_assign(FlowArgs F, uint32_t nw) {
+    if (F.state[kFsMissed] != F.epoch) return;
+    const uint32_t base = F.state[kFsBase];
+    for (uint32_t i0 = blockIdx.x * kFlowGridBlock + (threadIdx.x & ~63u); i0 < nw * 64;
+         i0 += gridDim.x * kFlowGridBlock)
+        flow_assign_wave(F, i0, base);
 }
 
 }  // namespace fcgpu

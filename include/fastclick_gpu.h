@@ -314,12 +314,14 @@ int  fcgpu_set_program(fcgpu_ctx *ctx, uint32_t kind, const fcgpu_step *steps, u
  *   max_flows: IDs 0 .. max_flows-1 (the table holds 2x that many slots, up to
  *     2^23 flows); a packet of a new flow beyond that gets FCGPU_FLOW_FULL (the
  *     manager kills it, virtualflowmanager.hh:262-266). 0 disables the table.
- * Each fcgpu_process with flow enabled runs one extra pass over the batch's
- * new flows (four small launches); fcgpu_process_host processes the batch in
- * order on one stream. */
+ * Each fcgpu_process with flow enabled adds a pass over the batch's new flows
+ * after the receive kernel (one launch, three after a batch with many new
+ * flows); fcgpu_process_host processes the batch in order on one stream.
+ * The context's max_batch must be at most FCGPU_FLOW_MAX_BATCH. */
 #define FCGPU_FLOW_NONE 0xffffffffu
 #define FCGPU_FLOW_FULL 0xfffffffeu
 #define FCGPU_MAX_FLOWS (1u << 23)
+#define FCGPU_FLOW_MAX_BATCH (64u * ((1u << 14) + 64))
 int  fcgpu_flow_enable(fcgpu_ctx *ctx, uint32_t max_flows);
 /* Forget every flow (IDs restart at 0). */
 int  fcgpu_flow_reset(fcgpu_ctx *ctx);

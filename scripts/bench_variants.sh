@@ -20,7 +20,6 @@ has c2_ipc16 && run c2_ipc16 --classify ipclass16 --steps 200 --warmup 20 --no-c
 has c4_ipc16 && run c4_ipc16 --workload c4 --classify ipclass16 --steps 200 --warmup 20 ${CPU_ARGS:---cpu-seconds 10}
 has c2_flow && run c2_flow --flow-capacity 1048576 --steps 200 --warmup 20 --no-cpu
 has c3_flow && run c3_flow --workload c3 --flow-capacity 1048576 --steps 200 --warmup 20 --no-cpu
-has c2_flow_inline && FCGPU_FLOW_INLINE=1 run c2_flow_inline --flow-capacity 1048576 --steps 200 --warmup 20 --no-cpu
 has c4_flow && run c4_flow --workload c4 --flow-capacity 2097152 --steps 200 --warmup 20 --no-cpu
 has c2_global && run c2_global --partition global --steps 200 --warmup 20 --no-cpu
 has c2_noperm && run c2_noperm --no-perm --steps 200 --warmup 20 --no-cpu

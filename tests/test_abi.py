@@ -68,6 +68,20 @@ def test_field_offsets_match_c_compiler(tmp_path):
     assert seen == sum(len(st._fields_) + 1 for st in structs.values())
 
 
+def test_header_constants_match_python():
+    """Every numeric #define FCGPU_X in fastclick_gpu.h has N.X with the same value."""
+    src = open(os.path.join(ROOT, "include", "fastclick_gpu.h")).read()
+    seen = 0
+    for name, val in re.findall(r"^#define\s+FCGPU_(\w+)\s+([^/\n]+)", src, flags=re.M):
+        expr = re.sub(r"(\d)u\b", r"\1", val.strip())
+        if not re.fullmatch(r"[\d\sx+\-*()<a-fA-F]+", expr):
+            continue
+        assert hasattr(N, name), name
+        assert getattr(N, name) == eval(expr, {}), (name, val)
+        seen += 1
+    assert seen >= 30
+
+
 def test_open_without_device_fails_loudly():
     import torch
     if torch.cuda.is_available():

@@ -149,6 +149,23 @@ def test_gpu_flow_mark_and_program_modes(oracle):
 
 
 @pytest.mark.gpu
+def test_gpu_flow_max_batch():
+    """The new-flow pass keeps one word per 64 packets in LDS: a context whose
+    max_batch is above FCGPU_FLOW_MAX_BATCH cannot enable the table."""
+    ctx = N.Context(0, N.FLOW_MAX_BATCH + 1, flow_cfg())
+    try:
+        with pytest.raises(RuntimeError, match="FLOW_MAX_BATCH"):
+            ctx.flow_enable(1024)
+    finally:
+        ctx.close()
+    ctx = N.Context(0, N.FLOW_MAX_BATCH, flow_cfg())
+    try:
+        ctx.flow_enable(1024)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
 def test_gpu_flow_rejects_auto_mode():
     from fastclick_amd import device
     b = synth.c5(1024, seed=3)
@@ -171,23 +188,19 @@ def _with_new(base, k, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("inline", [False, True])
 @pytest.mark.parametrize("max_flows", [1 << 16, 2_600])
-def test_gpu_flow_finish_paths(oracle, monkeypatch, max_flows, inline):
-    """Every path of the new-flow pass (fcgpu_flow.hh). Default: k_flow_finish
-    after every k_rx. With FCGPU_FLOW_INLINE=1: a cold table goes to
-    k_flow_finish; after a large batch a small one (<= 256 misses) is finished
-    by the last k_rx workgroup's LDS ranks while the queued k_flow_finish finds
-    nothing left; after a small batch a large one is finished by that
-    workgroup's bitmap pass (no k_flow_finish queued). Batches with no misses
-    and with one new flow on the last packet; with max_flows 2,600 the table
+def test_gpu_flow_finish_paths(oracle, max_flows):
+    """Every shape of the new-flow pass (fcgpu_flow.hh), chosen from the class
+    of the previous batch's misses: a cold table -> the grid-wide kernels; a
+    small batch (100 misses) after a large one -> grid-wide again; then
+    k_flow_finish's LDS ranks (200); a large batch there (6,000 > 4,096, the
+    hint was wrong) -> k_flow_finish in two chunks (ranks of first packets
+    carried across through frank[]); grid-wide
+    (5,000); no misses; LDS ranks with 150 and 3,000 misses (several per
+    thread); one new flow on the last packet. With max_flows 2,600 the table
     fills inside these paths (FCGPU_FLOW_FULL)."""
-    if inline:
-        monkeypatch.setenv("FCGPU_FLOW_INLINE", "1")
-    else:
-        monkeypatch.delenv("FCGPU_FLOW_INLINE", raising=False)
     base = synth.c3(20_000, nflows=2_000, seed=60)
-    plan = [(0, 0), (100, 1), (200, 2), (3_000, 3), (5_000, 4), (0, 5), (150, 6)]
+    plan = [(0, 0), (100, 1), (200, 2), (6_000, 3), (5_000, 4), (0, 5), (150, 6), (3_000, 7)]
     bs = [base if k == 0 and s == 0 else _with_new(base, k, 61 + s) for k, s in plan]
     last = [base.frame(i) for i in range(base.n)] + [synth.c4(1, seed=99).frame(0)]
     bs.append(synth.from_frames(last))
