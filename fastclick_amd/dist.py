@@ -11,6 +11,17 @@ ordered per-output list is wanted, an all-gather of the per-rank per-output
 counts gives every shard its output offsets (concatenating shard outputs in
 rank order preserves CLASSIFY_EACH_PACKET order).
 
+With a flow table (fcgpu_flow_enable) the path is stateful per flow. FastClick
+keeps one flow table per core and relies on the NIC's RSS hash to send every
+packet of a flow to the same core. The GPU analogue:
+batches whose packets arrive on any GPU are re-sharded by flow first.
+`exchange_by_flow` moves each packet to the rank its flow hash names, with one
+RCCL all-to-all of counts and one of frame bytes over xGMI. Every flow then
+lives in exactly one rank's table. The owner of a packet is the device
+classifier's output with LB_MODE hash over `world` outputs: the
+FlowSwitch/LoadBalancer formula on the IPFlowID hash, a function of the
+5-tuple.
+
 Backend-agnostic: "nccl" (RCCL over xGMI) on GPUs, "gloo" in CPU tests.
 """
 from __future__ import annotations
@@ -47,3 +58,54 @@ def output_offsets(local_counts, group=None):
     stacked = torch.stack(parts)                  # [world, nout]
     before = stacked[:rank].sum(0) if rank else torch.zeros_like(local_counts)
     return before, stacked.sum(0)
+
+
+def exchange_by_flow(arena, desc, owner, group=None):
+    """Re-shard one rank's packets by owner rank (an all-to-all over `group`).
+
+    arena: uint8 tensor of frame bytes; desc: int32 [n, 2] (offset, length)
+    into it; owner: int64 [n], the destination rank of each packet (-1 keeps
+    nothing: the packet is dropped here, e.g. one that failed the checks).
+    Returns (arena_recv, desc_recv, src): the frames this rank now owns,
+    packed back to back in (source rank, source index) order, their
+    descriptors, and src = source_rank << 32 | source_index per packet.
+    The frames keep their bytes and lengths exactly.
+    """
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    rank = dist.get_rank(group) if world > 1 else 0
+    dev = arena.device
+    owner = owner.to(torch.int64)
+    if owner.numel() and int(owner.max()) >= world:
+        raise ValueError(f"owner rank {int(owner.max())} outside a world of {world}")
+    keep = owner >= 0
+    idx = torch.nonzero(keep).flatten()
+    dst = owner[idx]
+    order = idx[torch.argsort(dst, stable=True)]             # packets grouped by destination
+    off = desc[order, 0].to(torch.int64) & 0xFFFFFFFF
+    ln = desc[order, 1].to(torch.int64) & 0xFFFFFFFF
+    send_n = torch.bincount(owner[order], minlength=world)
+    # byte gather: every byte of every frame, frames back to back in send order
+    starts = torch.cumsum(ln, 0) - ln
+    total = int(ln.sum())
+    pos = torch.arange(total, device=dev) - torch.repeat_interleave(starts, ln)
+    payload = arena[torch.repeat_interleave(off, ln) + pos] if total else arena[:0]
+    send_b = torch.zeros(world, dtype=torch.int64, device=dev).index_add_(0, owner[order], ln)
+    meta = torch.stack([ln, (rank << 32) | order], 1)        # [m, 2] length, source tag
+    if world == 1:
+        recv_n, recv_b, rmeta, rpay = send_n, send_b, meta, payload
+    else:
+        cnt = torch.stack([send_n, send_b], 1).contiguous()
+        rcnt = torch.empty_like(cnt)
+        dist.all_to_all_single(rcnt, cnt, group=group)       # [world, 2] from every rank
+        recv_n, recv_b = rcnt[:, 0], rcnt[:, 1]
+        sn, rn = send_n.tolist(), recv_n.tolist()
+        rmeta = torch.empty(int(sum(rn)), 2, dtype=torch.int64, device=dev)
+        dist.all_to_all_single(rmeta, meta.contiguous(), rn, sn, group=group)
+        rpay = torch.empty(int(recv_b.sum()), dtype=torch.uint8, device=dev)
+        dist.all_to_all_single(rpay, payload.contiguous(), recv_b.tolist(), send_b.tolist(), group=group)
+    rlen = rmeta[:, 0]
+    roff = torch.cumsum(rlen, 0) - rlen
+    desc_recv = torch.stack([roff, rlen], 1).to(torch.int32)
+    return rpay, desc_recv, rmeta[:, 1]
