@@ -22,23 +22,25 @@
 // published in mapped host memory (the size class of its batch's misses):
 //
 //   k_flow_finish (one block): batch without misses (epoch not stamped) ->
-//     returns at its first load; up to kSmallFinish (4096) misses -> the
-//     misses are compacted in packet order from the miss words into LDS, four
-//     per thread; a block scan ranks the first packets and every miss finds
-//     its flow's first packet by binary search; more (the hint was wrong) -> the grid-wide pass inside this block
-//     (slow: milliseconds for 1M misses).
+//     returns at its first load; otherwise the misses in packet order, 1024
+//     at a time (one chunk when the hint is right): compacted from the miss
+//     words into LDS, one per thread; a block scan ranks the first packets
+//     and every miss finds its flow's first packet by binary search.
 //   k_flow_mark / k_flow_scan / k_flow_assign (grid-wide, for batches with
 //     many misses): each wave marks the first packets among its 64 packets
 //     as a 64-bit word; an exclusive popcount prefix over those words (one
-//     block, coalesced loads transposed through LDS) ranks them; every miss takes its
-//     ID. Nothing needs clearing: every word is rewritten each batch.
+//     block, coalesced loads transposed through LDS) ranks them; every miss
+//     takes its ID. Nothing needs clearing: every word is rewritten each batch.
 #pragma once
 #include "fcgpu_device.hh"
 
 namespace fcgpu {
 
 constexpr int kFinishBlock = 1024;
-constexpr uint32_t kSmallFinish = 4 * kFinishBlock;   // misses k_flow_finish ranks in LDS
+// misses per k_flow_finish chunk, one per thread (four per thread made the
+// commit stage of a 4000-miss chunk take 35 us: one CU's stores to random
+// slots; the grid-wide pass does such batches in ~24 us)
+constexpr uint32_t kSmallFinish = kFinishBlock;
 // hint classes (FlowArgs::host_hint)
 constexpr uint32_t kHintNone = 0, kHintSmall = 1, kHintBig = 2;
 
@@ -134,6 +136,11 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, u
 // order a block scan needs. (Reading 16 contiguous words per thread instead
 // touched 64 lines per load instruction: 25 us for two 128-KB masks.)
 constexpr uint32_t kLdsWords = (1u << 14) + 64;   // batches up to 1M + 4096 packets
+// s_pre is padded by one word per 16, so a thread walking 16 consecutive words
+// hits distinct banks (unpadded, the 64 lanes of a wave shared two banks: 8 us
+// of the 13.5 us a 100-miss finish took)
+constexpr uint32_t kLdsPadded = kLdsWords + kLdsWords / 16 + 2;
+__device__ __forceinline__ uint32_t lw(uint32_t w) { return w + (w >> 4); }
 
 // s_pre[w] = popcount(mask[w]) for w < nw (nw <= kLdsWords); returns this
 // thread's share of the total, and of mask2's in `other`. Fixed trip count,
@@ -155,7 +162,7 @@ __device__ __forceinline__ uint32_t popc_to_lds(const uint64_t *mask, uint32_t n
     for (uint32_t k = 0; k < kIt; ++k) {
         const uint32_t w = threadIdx.x + k * BS;
         const uint32_t v = w < nw ? (uint32_t)__popcll(a[k]) : 0u;
-        if (w < nw) s_pre[w] = v;
+        if (w < nw) s_pre[lw(w)] = v;
         c += v;
         c2 += w < nw ? (uint32_t)__popcll(b[k]) : 0u;
     }
@@ -173,19 +180,19 @@ __device__ uint2 mask_prefix(const FlowArgs &F, uint32_t nw, uint32_t *s_w, uint
     const uint32_t per = (nw + BS - 1) / BS, w0 = threadIdx.x * per;
     uint32_t sum = 0;
     for (uint32_t k = 0; k < per; ++k)
-        if (w0 + k < nw) sum += s_pre[w0 + k];
+        if (w0 + k < nw) sum += s_pre[lw(w0 + k)];
     uint32_t tf, tm;
     uint32_t off = block_excl_scan<BS>(sum, s_w, tf);
     block_excl_scan<BS>(cm, s_w, tm);
     for (uint32_t k = 0; k < per; ++k) {
         if (w0 + k < nw) {
-            const uint32_t c = s_pre[w0 + k];
-            s_pre[w0 + k] = off;
+            const uint32_t c = s_pre[lw(w0 + k)];
+            s_pre[lw(w0 + k)] = off;
             off += c;
         }
     }
     __syncthreads();
-    for (uint32_t w = threadIdx.x; w < nw; w += BS) F.wordpre[w] = s_pre[w];
+    for (uint32_t w = threadIdx.x; w < nw; w += BS) F.wordpre[w] = s_pre[lw(w)];
     return make_uint2(tf, tm);
 }
 
@@ -196,11 +203,11 @@ __device__ uint2 mask_prefix(const FlowArgs &F, uint32_t nw, uint32_t *s_w, uint
 // of earlier chunks), and every other miss finds its flow's first packet in
 // the chunk by binary search -- or, when it lay in an earlier chunk, takes
 // the ID from the slot that chunk committed. Cost grows with the misses, not the
-// batch: one chunk for <= 4096 misses.
+// batch: one chunk for <= 1024 misses.
 __global__ __launch_bounds__(kFinishBlock) void k_flow_finish(FlowArgs F, uint32_t nw) {
     constexpr uint32_t kQ = kSmallFinish / kFinishBlock;     // misses per thread per chunk
     constexpr uint32_t kIt = (kLdsWords + kFinishBlock - 1) / kFinishBlock;
-    __shared__ uint32_t s_idx[kSmallFinish], s_f[kSmallFinish], s_pre[kLdsWords + 1];
+    __shared__ uint32_t s_idx[kSmallFinish], s_f[kSmallFinish], s_pre[kLdsPadded];
     __shared__ uint32_t s_w[kFinishBlock / 64];
     const uint32_t t = threadIdx.x;
     if (F.state[kFsMissed] != F.epoch) {      // no misses in this batch
@@ -211,44 +218,47 @@ __global__ __launch_bounds__(kFinishBlock) void k_flow_finish(FlowArgs F, uint32
     // miss words: word w = t + k * kFinishBlock stays in registers; its
     // popcount goes to LDS, becomes the word's first miss index (exclusive
     // prefix in word order, via thread-contiguous chunks of LDS)
-    uint64_t a[kIt];
+    {
+        uint64_t a[kIt];
 #pragma unroll
-    for (uint32_t k = 0; k < kIt; ++k) {
-        const uint32_t w = t + k * kFinishBlock;
-        a[k] = F.missmask[w < nw ? w : nw - 1];
-    }
+        for (uint32_t k = 0; k < kIt; ++k) {
+            const uint32_t w = t + k * kFinishBlock;
+            a[k] = F.missmask[w < nw ? w : nw - 1];
+        }
 #pragma unroll
-    for (uint32_t k = 0; k < kIt; ++k) {
-        const uint32_t w = t + k * kFinishBlock;
-        if (w < nw) s_pre[w] = (uint32_t)__popcll(a[k]);
-        else a[k] = 0;
+        for (uint32_t k = 0; k < kIt; ++k) {
+            const uint32_t w = t + k * kFinishBlock;
+            if (w < nw) s_pre[lw(w)] = (uint32_t)__popcll(a[k]);
+        }
     }
     __syncthreads();
     const uint32_t per = (nw + kFinishBlock - 1) / kFinishBlock, w0 = t * per;
     uint32_t c = 0;
     for (uint32_t k = 0; k < per; ++k)
-        if (w0 + k < nw) c += s_pre[w0 + k];
+        if (w0 + k < nw) c += s_pre[lw(w0 + k)];
     uint32_t m;
     uint32_t off = block_excl_scan<kFinishBlock>(c, s_w, m);
     for (uint32_t k = 0; k < per; ++k) {
         if (w0 + k < nw) {
-            const uint32_t v = s_pre[w0 + k];
-            s_pre[w0 + k] = off;
+            const uint32_t v = s_pre[lw(w0 + k)];
+            s_pre[lw(w0 + k)] = off;
             off += v;
         }
     }
-    if (t == 0) s_pre[nw] = m;
+    if (t == 0) s_pre[lw(nw)] = m;
     __syncthreads();
     uint32_t nfirst_before = 0;
     for (uint32_t c0 = 0; c0 < m; c0 += kSmallFinish) {
         const uint32_t cn = m - c0 < kSmallFinish ? m - c0 : kSmallFinish;
-#pragma unroll
+        // (the words are re-read where they hold misses: keeping all 17 per
+        // thread in registers spilled to scratch)
         for (uint32_t k = 0; k < kIt; ++k) {
-            uint64_t x = a[k];
-            if (!x) continue;
             const uint32_t w = t + k * kFinishBlock;
-            uint32_t e = s_pre[w];
-            if (e >= c0 + cn || s_pre[w + 1] <= c0) continue;
+            if (w >= nw) break;
+            uint32_t e = s_pre[lw(w)];
+            const uint32_t e1 = s_pre[lw(w + 1)];
+            if (e == e1 || e >= c0 + cn || e1 <= c0) continue;
+            uint64_t x = F.missmask[w];
             while (x) {
                 if (e >= c0 && e < c0 + cn) s_idx[e - c0] = w * 64 + (uint32_t)__builtin_ctzll(x);
                 ++e;
@@ -327,7 +337,7 @@ __global__ __launch_bounds__(kFlowGridBlock) void k_flow_mark(FlowArgs F, uint32
 }
 
 __global__ __launch_bounds__(kFinishBlock) void k_flow_scan(FlowArgs F, uint32_t nw) {
-    __shared__ uint32_t s_w[kFinishBlock / 64], s_pre[kLdsWords];
+    __shared__ uint32_t s_w[kFinishBlock / 64], s_pre[kLdsPadded];
     if (F.state[kFsMissed] != F.epoch) {
         if (threadIdx.x == 0) publish_hint(F, 0);
         return;

@@ -193,12 +193,12 @@ def test_gpu_flow_finish_paths(oracle, max_flows):
     """Every shape of the new-flow pass (fcgpu_flow.hh), chosen from the class
     of the previous batch's misses: a cold table -> the grid-wide kernels; a
     small batch (100 misses) after a large one -> grid-wide again; then
-    k_flow_finish's LDS ranks (200); a large batch there (6,000 > 4,096, the
-    hint was wrong) -> k_flow_finish in two chunks (ranks of first packets
-    carried across through frank[]); grid-wide
-    (5,000); no misses; LDS ranks with 150 and 3,000 misses (several per
-    thread); one new flow on the last packet. With max_flows 2,600 the table
-    fills inside these paths (FCGPU_FLOW_FULL)."""
+    k_flow_finish with one chunk (200); a large batch there (6,000, the hint
+    was wrong) -> k_flow_finish in six 1024-miss chunks, later chunks taking
+    the IDs of flows that began in earlier ones from their committed slots;
+    grid-wide (5,000); no misses; one chunk (150); three chunks (3,000); one
+    new flow on the last packet. With max_flows 2,600 the table fills inside
+    these paths (FCGPU_FLOW_FULL)."""
     base = synth.c3(20_000, nflows=2_000, seed=60)
     plan = [(0, 0), (100, 1), (200, 2), (6_000, 3), (5_000, 4), (0, 5), (150, 6), (3_000, 7)]
     bs = [base if k == 0 and s == 0 else _with_new(base, k, 61 + s) for k, s in plan]
