@@ -312,7 +312,8 @@ def main():
                 "packets_per_step_per_gpu": n,
                 "hbm_batches": args.nbuf,
                 "nports": args.nports,
-                "parallelism": f"batch-sharded x{world}, counters all-reduced (RCCL)",
+                "parallelism": f"batch-sharded x{world}, counters all-reduced "
+                               f"({'RCCL' if args.backend == 'nccl' else 'gloo'})",
             },
             "roofline": roof,
             "cpu_baseline": cpu,
