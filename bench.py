@@ -7,14 +7,25 @@ step = one pass of the hot path over one batch:
     CheckIPHeader(OFFSET 14, CHECKSUM true) -> AggregateHash (IPFlowID low 32)
     -> FlowSwitch LB_MODE hash over 16 outputs -> stable per-port partition
 
-i.e. k_rx + k_scan + k_part of libfcgpu.so. Steps rotate over --nbuf distinct
-batches placed in different HBM regions (default 16 x 72 MB = 1.15 GB > the
-256 MB Infinity Cache), so every step reads its packets from HBM.
+i.e. k_rx of libfcgpu.so (plus k_scan + k_part with --partition global).
+Steps rotate over --nbuf distinct batches placed in different HBM regions
+(default 16 x 72 MB of touched bytes = 1.15 GB > the 256 MB Infinity Cache),
+so every step reads its packets from HBM. Consecutive steps alternate over
+--streams HIP streams (default 2: two rx queues feeding one GPU, each batch
+with its own outputs), so one batch's tail overlaps the next one's head. The
+timed steps are submitted by one fcgpu_process_jobs call (the C ABI loops
+over them; no per-step Python on the launch path).
 
-Multi-GPU (torchrun, one process per GPU): each rank processes its own batch
-per step (weak scaling, no data-path collective); the per-port / per-reason
-counters are summed across ranks with one all-reduce over RCCL at the end of
-the timed region (the reference sums per-thread counters on read).
+Multi-GPU: one process per GPU (torchrun, or `--gpus N` without WORLD_SIZE,
+which starts the N local rank processes itself). --shard weak (default):
+every rank processes its own 1M-packet batches (scaling "weak", no data-path
+collective). --shard strong (configs[3], C4): one 1M-packet batch per step is
+split over the ranks with dist.shard_range (131,072 packets per GPU at N=8;
+every shard is a whole number of 256-packet PacketBatches, so no per-step
+exchange is needed either). After the timed region the per-port / per-reason
+counters are all-reduced over RCCL (the reference sums per-thread counters on
+read, include/click/sync.hh:384) and the per-output offsets all-gathered
+(dist.output_offsets); both are checked.
 
 rank 0 prints ONE JSON line (contract in the task statement).
 """
@@ -27,22 +38,25 @@ import subprocess
 import sys
 import time
 
-import numpy as np
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 PKT_BYTES_READ = 72          # 64-B header window + 8-B descriptor
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+METRIC = "Mpps device-resident, 64 B IPv4 cksum+classify, 1/2/4/8 MI355X"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU). Under torchrun it must equal WORLD_SIZE; without "
+                         "WORLD_SIZE, N > 1 starts the N local rank processes")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--packets", type=int, default=1 << 20)
+    ap.add_argument("--packets", type=int, default=1 << 20,
+                    help="packets per step per GPU (weak) or per step in total (strong)")
+    ap.add_argument("--shard", choices=["weak", "strong"], default="weak")
     ap.add_argument("--nbuf", type=int, default=16)
     ap.add_argument("--nports", type=int, default=16)
     ap.add_argument("--no-perm", action="store_true", help="skip the partition")
@@ -50,25 +64,29 @@ def parse():
                     help="tile: each 256-packet tile is one classified PacketBatch (1 launch); "
                          "global: the whole batch is one (3 launches)")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
-    ap.add_argument("--timing-every", type=int, default=8,
-                    help="bracket every k-th step's kernels with HIP events (ext-launch "
-                         "start/stop on the launch stream); sampling keeps the event cost "
-                         "out of most steps")
-    ap.add_argument("--streams", type=int, default=1,
-                    help="HIP streams the consecutive steps alternate over (each with its own "
-                         "context and output buffers), so one batch's tail overlaps the next "
-                         "batch's head, as back-to-back NIC batches would")
+    ap.add_argument("--timing-every", type=int, default=4,
+                    help="bracket every k-th launch with HIP events (hipExtLaunchKernelGGL start/stop "
+                         "on the launch stream; created before the timed region)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the consecutive steps alternate over (each with its own output "
+                         "buffers), as batches of several rx queues would")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse "
                          "several ranks on one GPU)")
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default=None,
                     help="c2: one 5-tuple (BASELINE configs[1], the headline); c3: IMIX "
                          "64/570/1500 B 7:4:1 over 10k 5-tuples (configs[2]); c4: independent "
                          "uniform random 5-tuples (configs[3]); c5: 50%% 802.1Q + 30%% IPv6 mix "
-                         "through StripEtherVLANHeader + CheckIP6Header/CheckIPHeader (configs[4])")
+                         "through StripEtherVLANHeader + CheckIP6Header/CheckIPHeader (configs[4]). "
+                         "Default c2, or c4 with --shard strong")
+    ap.add_argument("--frame-bytes", type=int, default=64,
+                    help="c2/c4 frame size on the wire (64..1518; captured = size - 4 FCS bytes, "
+                         "ip_len = captured - 14, fastudpflows.cc:146-175); the kernel still reads "
+                         "the 64-B header window of every frame")
     ap.add_argument("--flow-capacity", type=int, default=0,
                     help="> 0: the device flow table (FlowIPManagerHMP flow IDs, fcgpu_flow_enable) "
-                         "behind the check, with this many IDs; its new-flow pass runs every step")
+                         "behind the check, with this many IDs; its new-flow pass runs every step "
+                         "(one stream: the table assigns IDs in batch order)")
     ap.add_argument("--classify", choices=["lb", "ipclass16"], default="lb",
                     help="lb: FlowSwitch LB_MODE hash x16 (headline); ipclass16: the survey's "
                          "IPClassifier with 15 UDP dst-port ranges + '-' (program printed by the "
@@ -76,16 +94,29 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    return ap.parse_args()
+    a = ap.parse_args(argv)
+    if a.workload is None:
+        a.workload = "c4" if a.shard == "strong" else "c2"
+    if a.frame_bytes != 64 and a.workload not in ("c2", "c4"):
+        ap.error("--frame-bytes applies to c2/c4")
+    if not 64 <= a.frame_bytes <= 1518:
+        ap.error("--frame-bytes must be in [64, 1518]")
+    if a.flow_capacity and a.streams > 1:
+        # one table per context, IDs in batch order: a second stream would
+        # either race on the table's scratch or need a second table
+        a.streams = 1
+    if a.partition == "global" and a.streams > 1 and not a.no_perm:
+        a.streams = 1    # the whole-batch partition uses context scratch
+    return a
 
 
 WORKLOADS = {
-    "c2": "C2: 64 B IPv4/UDP (60-B frames in 64-B slots), 1M-packet device-resident batch, single 5-tuple",
-    "c3": "C3: IMIX 64/570/1500 B (7:4:1) IPv4/UDP, 10k uniform 5-tuples, 1M-packet device-resident batch "
+    "c2": "C2: {F} B IPv4/UDP ({C}-B frames in {S}-B slots), {N}-packet device-resident batch, single 5-tuple",
+    "c3": "C3: IMIX 64/570/1500 B (7:4:1) IPv4/UDP, 10k uniform 5-tuples, {N}-packet device-resident batch "
           "(first 64 B of each frame read)",
-    "c4": "C4: 64 B IPv4/UDP (60-B frames in 64-B slots), 1M-packet device-resident batch, independent "
+    "c4": "C4: {F} B IPv4/UDP ({C}-B frames in {S}-B slots), {N}-packet device-resident batch, independent "
           "uniform 5-tuples",
-    "c5": "C5: 50% 802.1Q-tagged, 30% IPv6 (80-B frames) / 70% IPv4 (60-B), 1M-packet device-resident batch",
+    "c5": "C5: 50% 802.1Q-tagged, 30% IPv6 (80-B frames) / 70% IPv4 (60-B), {N}-packet device-resident batch",
 }
 
 
@@ -96,20 +127,45 @@ def ipclass16_program():
     return progs["ipclass16"]["program"]
 
 
-def cpu_baseline(seconds: float, flows: int = 1, program: str | None = None):
-    """Reported CPU baseline: the scalar restatement of the reference elements
-    (oracle/cpu_baseline.cc: 32-packet linked-list PacketBatch, CheckIPHeader ->
-    AggregateHash -> FlowSwitch hash -> CLASSIFY_EACH_PACKET, atomic counters),
-    one pipeline per core, on this host."""
-    exe = os.path.join(ROOT, "oracle", "_build", "fc_cpu_baseline")
-    if not os.path.exists(exe):
-        try:
-            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "baseline"])
-        except Exception:
-            return None
-    cores = len(os.sched_getaffinity(0))
-    cores = max(1, min(cores, 16))
-    cmd = [exe, "--seconds", str(seconds), "--threads", str(cores), "--flows", str(flows)]
+# ---- host CPU description and the reported CPU baseline --------------------
+
+def host_cpu_info():
+    """nproc, the CPUs this process may run on, the cgroup CPU quota and the
+    model. On the GPU box nproc shows the whole machine; the job's share is
+    the quota (or 16 CPUs per GPU, the box's stated share)."""
+    info = dict(nproc=os.cpu_count(), affinity=len(os.sched_getaffinity(0)), cgroup_quota=None, model=None)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            info["cgroup_quota"] = round(int(q) / int(per), 2)
+    except Exception:
+        pass
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+    except Exception:
+        pass
+    share = info["affinity"]
+    if info["cgroup_quota"]:
+        share = min(share, max(1, int(info["cgroup_quota"])))
+    why = "affinity" if share == info["affinity"] else "cgroup quota"
+    if os.environ.get("GRAFT_REPO_ROOT") and share > 16:
+        share, why = 16, "the GPU box's CPU share per GPU"
+    env = os.environ.get("FCGPU_CPU_THREADS")
+    if env:
+        share, why = max(1, int(env)), "FCGPU_CPU_THREADS"
+    info["threads_used"] = share
+    info["threads_basis"] = why
+    return info
+
+
+def _run_cpu(exe, seconds, threads, flows, stages, program):
+    cmd = [exe, "--seconds", str(seconds), "--threads", str(threads), "--flows", str(flows),
+           "--stages", str(stages)]
     tmp = None
     if program is not None:
         import tempfile
@@ -119,210 +175,359 @@ def cpu_baseline(seconds: float, flows: int = 1, program: str | None = None):
         cmd += ["--program", tmp.name]
     try:
         out = subprocess.run(cmd, capture_output=True, text=True, timeout=seconds * 4 + 60)
-        res = json.loads(out.stdout.strip().splitlines()[-1])
-    except Exception as e:  # reported baseline only
-        print(f"cpu baseline failed: {e}", file=sys.stderr)
-        return None
+        return json.loads(out.stdout.strip().splitlines()[-1])
     finally:
         if tmp is not None:
             os.unlink(tmp.name)
-    return dict(value=round(res["mpps"], 3), unit="Mpps", cores=res["threads"], kind="port",
-                sample=res["sample"], mpps_1core=round(res.get("mpps_1core", 0.0), 3))
+
+
+def cpu_baseline(seconds: float, flows: int = 1, program: str | None = None):
+    """Reported CPU baseline: the scalar restatement of the reference elements
+    (oracle/cpu_baseline.cc: 32-packet linked-list PacketBatch, atomic
+    counters, one pipeline per core) on this host: the C2 chain
+    Strip(14) -> CheckIPHeader(CHECKSUM true) -> AggregateHash -> FlowSwitch
+    hash x16 (or the IPClassifier program) -> Discard, and beside it C1's
+    Strip(14) -> CheckIPHeader(CHECKSUM true) -> Discard."""
+    exe = os.path.join(ROOT, "oracle", "_build", "fc_cpu_baseline")
+    if not os.path.exists(exe):
+        try:
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "baseline"])
+        except Exception:
+            return None
+    info = host_cpu_info()
+    th = info["threads_used"]
+    try:
+        main = _run_cpu(exe, seconds * 2 / 3, th, flows, 3, program)
+        c1 = _run_cpu(exe, seconds / 3, th, 4096, 1, None)
+    except Exception as e:  # reported baseline only
+        print(f"cpu baseline failed: {e}", file=sys.stderr)
+        return None
+    return dict(value=round(main["mpps"], 3), unit="Mpps", cores=main["threads"], kind="port",
+                sample=main["sample"], mpps_1core=round(main.get("mpps_1core", 0.0), 3),
+                c1_value=round(c1["mpps"], 3), c1_mpps_1core=round(c1.get("mpps_1core", 0.0), 3),
+                c1_sample=c1["sample"], nproc=info["nproc"], affinity=info["affinity"],
+                cgroup_quota=info["cgroup_quota"], cores_basis=info["threads_basis"], cpu_model=info["model"])
+
+
+# ---- launching the local ranks ---------------------------------------------
+
+def spawn_local_ranks(args) -> int:
+    """`--gpus N` without WORLD_SIZE: start N rank processes of this script
+    (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, 127.0.0.1), wait, return the
+    worst exit code. Runs before anything touches the GPU, and starts the
+    ranks as children (never exec)."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        for p in procs:
+            code = p.wait()
+            rc = rc or code
+            if code:
+                for q in procs:          # one rank failed: the others would hang in a collective
+                    if q.poll() is None:
+                        q.kill()
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+                q.wait()
+    return rc
+
+
+# ---- the rank ----------------------------------------------------------------
+
+def shard_of(args, world, rank):
+    """(lo, hi) packet range of this rank within a step's batch."""
+    from fastclick_amd.dist import shard_range
+    if args.shard == "strong":
+        return shard_range(args.packets, world, rank)
+    return 0, args.packets
+
+
+def make_host_batch(args):
+    from fastclick_amd import synth
+    n = args.packets
+    if args.workload in ("c2", "c4") and args.frame_bytes != 64:
+        import numpy as np
+        cap = args.frame_bytes - 4
+        if args.workload == "c2":
+            hdr = synth.build_headers(n, src=synth.ip4(10, 0, 0, 1), dst=synth.ip4(10, 0, 0, 2),
+                                      sport=1234, dport=5678, frame_len=cap, width=64)
+        else:
+            rng = np.random.default_rng(4)
+            hdr = synth.build_headers(n, **synth._rand_flows(rng, n), frame_len=cap, width=64)
+        return synth.pack(hdr, cap, meta=dict(config=args.workload.upper(), frame_bytes=args.frame_bytes))
+    return dict(c2=synth.c2, c3=synth.c3, c4=synth.c4, c5=synth.c5)[args.workload](n)
+
+
+class DeviceProcessor:
+    """The hot path on this rank's GPU: nbuf HBM-resident copies of the
+    batch, one context, --streams output sets; steps submitted through
+    fcgpu_process_jobs."""
+
+    def __init__(self, args, lo, hi, gpu):
+        import numpy as np
+        import torch
+        from fastclick_amd import _native as N
+        from fastclick_amd.device import DeviceOutputs
+        self.N, self.torch, self.args = N, torch, args
+        dev = torch.device("cuda", gpu)
+        self.dev = dev
+        host = make_host_batch(args)
+        self.frame_meta = dict(slot=int(host.desc[1, 0] - host.desc[0, 0]) if host.n > 1 else 64,
+                               captured=int(host.desc[0, 1]))
+        n = hi - lo
+        self.n = n
+        arena = torch.from_numpy(np.ascontiguousarray(host.arena)).to(dev)
+        desc = torch.from_numpy(np.ascontiguousarray(host.desc[lo:hi]).view(np.int32)).to(dev)
+        del host
+        # nbuf copies at distinct HBM addresses (device-side copies)
+        self.bufs = [(arena, desc)] + [(arena.clone(), desc.clone()) for _ in range(args.nbuf - 1)]
+        program = None
+        if args.classify == "ipclass16":
+            from fastclick_amd import click
+            steps, oe = click.parse_program(ipclass16_program())
+            program = (N.PROG_IPFILTER, steps, oe)
+            args.nports = 16
+        self.auto = args.workload == "c5"
+        cfg = N.make_cfg(check_mode=N.CHECK_AUTO if self.auto else N.CHECK_IP4, offset=0 if self.auto else 14,
+                         checksum=True, hash_mode=N.HASH_FLOWID,
+                         classify=N.CLS_LB_HASH if program is None else N.CLS_PROGRAM, nports=args.nports)
+        part = N.PART_TILE if args.partition == "tile" else N.PART_GLOBAL
+        tile = part == N.PART_TILE
+        self.ctx = N.Context(gpu, max(n, 1), cfg)
+        if program is not None:
+            self.ctx.set_program(*program)
+        if args.flow_capacity:
+            self.ctx.flow_enable(args.flow_capacity)
+        self.streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
+        self.outs = [DeviceOutputs(max(n, 1), args.nports, device=dev, verdict=True, hash=True, anno=False,
+                                   perm=(not args.no_perm) and not tile,
+                                   tile_perm=(not args.no_perm) and tile, port_start=not args.no_perm,
+                                   partition=part, flowid=args.flow_capacity > 0)
+                     for _ in self.streams]
+        self.ctr = torch.zeros(N.CTR_SHARDS, N.NCOUNTERS, dtype=torch.int64, device=dev)
+        self.timing_every = 0 if args.no_timing else max(1, args.timing_every)
+
+    def _jobs(self, first, count):
+        specs = []
+        ns = len(self.streams)
+        for k in range(first, first + count):
+            a, d = self.bufs[k % len(self.bufs)]
+            j = k % ns
+            specs.append((a.data_ptr(), d.data_ptr(), self.n, self.streams[j].cuda_stream, self.outs[j].ptrs()))
+        return self.ctx.jobs(specs)
+
+    def warmup(self, steps):
+        self.ctx.set_timing(self.timing_every)      # creates the event pool now
+        self.ctx.run_jobs(self._jobs(0, steps))
+        self.torch.cuda.synchronize()
+        self.ctx.read_timing()                      # drop warmup samples
+        self.ctx.use_counters(self.ctr.data_ptr())  # timed steps count into the tensor
+        self.timed = self._jobs(steps, self.args.steps)   # built before t0
+
+    def run_timed(self):
+        self.ctx.run_jobs(self.timed)
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def counters(self):
+        return self.ctr
+
+    def timing(self):
+        if not self.timing_every:
+            return None
+        ms, cnt = self.ctx.read_timing()
+        return dict(k_rx_ms=ms[0] / max(cnt[0], 1), k_scan_ms=ms[1] / max(cnt[1], 1),
+                    k_part_ms=ms[2] / max(cnt[2], 1), launches=cnt)
+
+    def close(self):
+        self.ctx.close()
+
+
+def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_collectives):
+    """One rank of the benchmark: build, warm up, time exactly args.steps
+    steps between barrier + device sync on both sides, take the max over
+    ranks, reduce the counters and output offsets (after the timed region),
+    check them, and return the JSON line (rank 0) or None.
+
+    processor_factory(args, lo, hi, gpu) -> an object with warmup(k),
+    run_timed(), sync(), counters() (int64 [CTR_SHARDS, NCOUNTERS] tensor),
+    timing() and close(). Tests drive this with a CPU processor."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from fastclick_amd import _native as N
+    from fastclick_amd.dist import output_offsets, reduce_counters
+
+    lo, hi = shard_of(args, world, rank)
+    proc = processor_factory(args, lo, hi, gpu)
+    try:
+        proc.warmup(args.warmup)
+        if world > 1:
+            dist.barrier()
+        proc.sync()
+        t0 = time.perf_counter()
+        proc.run_timed()
+        proc.sync()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        timing = proc.timing()
+
+        # after the timed region: max time over ranks, counters summed over
+        # ranks (RCCL all-reduce of the device vector), per-output offsets
+        t_red = time.perf_counter()
+        ctr = proc.counters()
+        glob = reduce_counters(ctr if backend == "nccl" else ctr.cpu())
+        if backend == "nccl":
+            torch.cuda.synchronize()
+        red_ms = (time.perf_counter() - t_red) * 1e3
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev_for_collectives)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        gv = N.derive_counters(glob.cpu().numpy())
+        local = N.derive_counters(ctr.sum(0).cpu().numpy())
+        nb = args.nports + 1
+        lport = torch.from_numpy(local[N.CTR_PORT:N.CTR_PORT + nb].astype(np.int64)).to(dev_for_collectives)
+        before, gtot = output_offsets(lport)
+        gtot = gtot.cpu().numpy()
+    finally:
+        proc.close()
+
+    total_pkts = (args.packets if args.shard == "strong" else args.packets * world) * args.steps
+    valid = int(gv[N.CTR_COUNT])
+    expect_valid = total_pkts if args.workload in ("c2", "c4") else None
+    if expect_valid is not None and valid != expect_valid:
+        raise AssertionError(f"valid count {valid} != {expect_valid}")
+    if not np.array_equal(gtot, gv[N.CTR_PORT:N.CTR_PORT + nb].astype(np.int64)):
+        raise AssertionError("all-gathered per-output counts disagree with the all-reduced counters")
+    if rank != 0:
+        return None
+    mpps = total_pkts / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+    per_gpu = hi - lo
+    roof = None
+    if timing:
+        kernel_s = timing["k_rx_ms"] * 1e-3
+        step_s = ms_per_step * 1e-3
+        nstreams = max(1, args.streams)
+        # one stream: bytes per launch / the launch's own duration. Several
+        # streams overlap launches, so a launch's duration includes its
+        # neighbours' share of HBM: the step time is the per-launch figure
+        basis = "kernel" if nstreams == 1 else "step"
+        t_launch = kernel_s if basis == "kernel" else step_s
+        achieved = PKT_BYTES_READ * per_gpu / t_launch / 1e9
+        traffic = None
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("packets") == per_gpu and tj.get("workload", "c2") == args.workload \
+                    and tj.get("frame_bytes", 64) == args.frame_bytes:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            pass
+        roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, kernel="k_rx", basis=basis,
+                    bytes_per_launch=PKT_BYTES_READ * per_gpu,
+                    kernel_ms=round(timing["k_rx_ms"], 5),
+                    kernel_frac=round(PKT_BYTES_READ * per_gpu / kernel_s / 1e9 / HBM_PEAK_GBS, 4),
+                    scan_ms=round(timing["k_scan_ms"], 5), part_ms=round(timing["k_part_ms"], 5),
+                    sampled_launches=timing["launches"][0])
+    cpu = None
+    if world == 1 and not args.no_cpu and args.workload in ("c2", "c3", "c4") and not args.flow_capacity:
+        cpu = cpu_baseline(args.cpu_seconds, flows=dict(c2=1, c3=10000).get(args.workload, 4096),
+                           program=ipclass16_program() if args.classify == "ipclass16" else None)
+    fb = args.frame_bytes
+    slot = max(64, (fb - 4 + 63) // 64 * 64)
+    wl = WORKLOADS[args.workload].format(F=fb, C=fb - 4, S=slot, N=per_gpu)
+    auto = args.workload == "c5"
+    line = {
+        "metric": METRIC,
+        "value": round(mpps, 1),
+        "unit": "Mpps",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": args.shard,
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {
+            "workload": (wl
+                         + ("; StripEtherVLANHeader + CheckIP6Header/CheckIPHeader(CHECKSUM true)"
+                            if auto else "; CheckIPHeader(CHECKSUM true)")
+                         + (f" + FlowIPManagerHMP flow table ({args.flow_capacity} IDs)"
+                            if args.flow_capacity else "")
+                         + " + AggregateHash + "
+                         + ("FlowSwitch hash 16 outputs" if args.classify == "lb" else
+                            "IPClassifier(15 UDP dst-port ranges, -) 16 outputs")
+                         + ("" if args.no_perm else
+                            " + stable per-port partition of every 256-packet PacketBatch"
+                            if args.partition == "tile" else
+                            " + stable per-port partition of the whole batch")),
+            "classify": args.classify,
+            "partition": "none" if args.no_perm else args.partition,
+            "streams": max(1, args.streams),
+            "frame_bytes": fb,
+            "packets_per_step_per_gpu": per_gpu,
+            "packets_per_step": args.packets if args.shard == "strong" else args.packets * world,
+            "hbm_batches": args.nbuf,
+            "nports": args.nports,
+            "parallelism": (f"batch-sharded x{world}" if args.shard == "weak" else
+                            f"one batch split x{world} (dist.shard_range)")
+                           + f", counters all-reduced after the timed region "
+                             f"({'RCCL' if backend == 'nccl' else 'gloo'}, {red_ms:.3f} ms)",
+        },
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+    return line
 
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(spawn_local_ranks(args))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one process per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
     ndev = torch.cuda.device_count()
-    gpu = local % max(ndev, 1)
+    if ndev == 0:
+        raise SystemExit("bench.py: no HIP device visible")
+    gpu = local % ndev
     if world > 1:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
             dist.init_process_group("gloo")
     torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
-    local = gpu
-
-    from fastclick_amd import synth, _native as N
-    from fastclick_amd.device import DeviceBatch, DeviceOutputs
-
-    n = args.packets
-    host = dict(c2=synth.c2, c3=synth.c3, c4=synth.c4, c5=synth.c5)[args.workload](n)
-    # nbuf distinct copies at distinct HBM addresses
-    bufs = []
-    for k in range(args.nbuf):
-        bufs.append(DeviceBatch.upload(host, device=dev))
-    del host
-    program = None
-    if args.classify == "ipclass16":
-        from fastclick_amd import click
-        text = ipclass16_program()
-        steps, oe = click.parse_program(text)
-        program = (N.PROG_IPFILTER, steps, oe)
-        args.nports = 16
-    auto = args.workload == "c5"
-    cfg = N.make_cfg(check_mode=N.CHECK_AUTO if auto else N.CHECK_IP4, offset=0 if auto else 14,
-                     checksum=True, hash_mode=N.HASH_FLOWID,
-                     classify=N.CLS_LB_HASH if program is None else N.CLS_PROGRAM, nports=args.nports)
-    part = N.PART_TILE if args.partition == "tile" else N.PART_GLOBAL
-    tile = part == N.PART_TILE
-    nstreams = max(1, args.streams)
-    # per stream: its own context (workspace) and output buffers
-    ctxs, streams, optrs, outs_keep = [], [], [], []
-    for _ in range(nstreams):
-        ctxs.append(N.Context(local, n, cfg))
-        if program is not None:
-            ctxs[-1].set_program(*program)
-        if args.flow_capacity:
-            ctxs[-1].flow_enable(args.flow_capacity)
-        streams.append(torch.cuda.Stream(dev))
-        o = DeviceOutputs(n, args.nports, device=dev, verdict=True, hash=True, anno=False,
-                          perm=(not args.no_perm) and not tile, tile_perm=(not args.no_perm) and tile,
-                          port_start=not args.no_perm, partition=part, flowid=args.flow_capacity > 0)
-        outs_keep.append(o)
-        optrs.append(o.ptrs())
-    ctx = ctxs[0]
-    # the first stream also carries the counter all-reduce; it waits for the others
-    main_stream = streams[0]
-    torch.cuda.set_stream(main_stream)
-
-    def step(k):
-        j = k % nstreams
-        b = bufs[k % len(bufs)]
-        ctxs[j].process(b.arena.data_ptr(), b.desc.data_ptr(), n, stream=streams[j].cuda_stream,
-                        **optrs[j])
-
-    for k in range(args.warmup):
-        step(k)
-    torch.cuda.synchronize()
-    # counters accumulate straight into a torch tensor so RCCL can reduce them
-    ctr_t = torch.zeros(N.CTR_SHARDS, N.NCOUNTERS, dtype=torch.int64, device=dev)
-    torch.cuda.synchronize()
-    for c in ctxs:
-        c.use_counters(ctr_t.data_ptr())
-    timing_on = not args.no_timing
-    if timing_on:
-        for c in ctxs:
-            c.read_timing()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    every = max(1, args.timing_every)
-    for k in range(args.steps):
-        if timing_on and k % every == 0:
-            c = ctxs[k % nstreams]
-            c.set_timing(True)
-            step(k)
-            c.set_timing(False)
-        else:
-            step(k)
-    for s_ in streams[1:]:
-        main_stream.wait_stream(s_)
-    if world > 1:
-        # per-port / per-reason counters summed across GPUs: one RCCL all-reduce
-        # of the device counter vector (xGMI), like PER_THREAD_SUM on read
-        from fastclick_amd.dist import reduce_counters
-        glob = reduce_counters(ctr_t if args.backend == "nccl" else ctr_t.cpu())
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=dev if args.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        total_valid = int(N.derive_counters(glob.cpu().numpy())[N.CTR_COUNT])
-    else:
-        total_valid = int(N.derive_counters(ctr_t.sum(0).cpu().numpy())[N.CTR_COUNT])
-
-    timing = None
-    if not args.no_timing:
-        ms, cnt = [0.0] * 3, [0] * 3
-        for c in ctxs:
-            m_, c_ = c.read_timing()
-            ms = [a + b for a, b in zip(ms, m_)]
-            cnt = [a + b for a, b in zip(cnt, c_)]
-        timing = dict(k_rx_ms=ms[0] / max(cnt[0], 1), k_scan_ms=ms[1] / max(cnt[1], 1),
-                      k_part_ms=ms[2] / max(cnt[2], 1), launches=cnt)
-
-    total_pkts = n * args.steps * world
-    assert total_valid == total_pkts, f"valid count {total_valid} != {total_pkts}"
-    mpps = total_pkts / elapsed / 1e6
-    ms_per_step = elapsed / args.steps * 1e3
-
-    if rank == 0:
-        roof = None
-        if timing:
-            t_launch = timing["k_rx_ms"] * 1e-3
-            achieved = PKT_BYTES_READ * n / t_launch / 1e9
-            traffic = None
-            try:
-                with open(args.traffic_json) as f:
-                    tj = json.load(f)
-                if tj.get("packets") == n:
-                    traffic = tj.get("hbm_bytes_per_launch")
-            except Exception:
-                pass
-            roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
-                        kernel="k_rx", kernel_ms=round(timing["k_rx_ms"], 5),
-                        scan_ms=round(timing["k_scan_ms"], 5), part_ms=round(timing["k_part_ms"], 5))
-        cpu = None
-        if world == 1 and not args.no_cpu and not auto and not args.flow_capacity:
-            cpu = cpu_baseline(args.cpu_seconds, flows=dict(c2=1, c3=10000).get(args.workload, 4096),
-                               program=ipclass16_program() if program is not None else None)
-        line = {
-            "metric": "Mpps device-resident, 64 B IPv4 cksum+classify, 1/2/4/8 MI355X",
-            "value": round(mpps, 1),
-            "unit": "Mpps",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 5),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic",
-            "config": {
-                "workload": (WORKLOADS[args.workload]
-                             + ("; StripEtherVLANHeader + CheckIP6Header/CheckIPHeader(CHECKSUM true)"
-                                if auto else "; CheckIPHeader(CHECKSUM true)")
-                             + (f" + FlowIPManagerHMP flow table ({args.flow_capacity} IDs)"
-                                if args.flow_capacity else "")
-                             + " + AggregateHash + "
-                             + ("FlowSwitch hash 16 outputs" if program is None else
-                                "IPClassifier(15 UDP dst-port ranges, -) 16 outputs")
-                             + ("" if args.no_perm else
-                                " + stable per-port partition of every 256-packet PacketBatch"
-                                if args.partition == "tile" else
-                                " + stable per-port partition of the whole 1M-packet batch")),
-                "classify": args.classify,
-                "partition": "none" if args.no_perm else args.partition,
-                "streams": nstreams,
-                "packets_per_step_per_gpu": n,
-                "hbm_batches": args.nbuf,
-                "nports": args.nports,
-                "parallelism": f"batch-sharded x{world}, counters all-reduced "
-                               f"({'RCCL' if args.backend == 'nccl' else 'gloo'})",
-            },
-            "roofline": roof,
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(line), flush=True)
-    for c in ctxs:
-        c.close()
-    if world > 1:
-        dist.destroy_process_group()
+    try:
+        line = rank_main(args, DeviceProcessor, world=world, rank=rank, gpu=gpu, backend=args.backend,
+                         dev_for_collectives=torch.device("cuda", gpu) if args.backend == "nccl" else "cpu")
+        if line is not None:
+            print(json.dumps(line), flush=True)
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -14,7 +14,7 @@ LIBFCGPU = os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 9
+ABI_VERSION = 10
 SPAN_SLOTS = 3
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
@@ -122,6 +122,17 @@ class fcgpu_out(C.Structure):
     ]
 
 
+class fcgpu_job(C.Structure):
+    _fields_ = [
+        ("arena", C.c_void_p),
+        ("desc", C.c_void_p),
+        ("n", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("stream", C.c_void_p),
+        ("out", fcgpu_out),
+    ]
+
+
 class fcgpu_step(C.Structure):
     _fields_ = [
         ("offset", C.c_int32),
@@ -143,6 +154,7 @@ FCGPU_SYMBOLS = {
     "fcgpu_close": (None, [C.c_void_p]),
     "fcgpu_process": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                 C.POINTER(fcgpu_out), C.c_void_p]),
+    "fcgpu_process_jobs": (C.c_int, [C.c_void_p, C.POINTER(fcgpu_job), C.c_uint32, C.c_void_p]),
     "fcgpu_process_host": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_void_p, C.c_uint32,
                                      C.POINTER(fcgpu_out)]),
     "fcgpu_set_program": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(fcgpu_step), C.c_uint32,
@@ -306,6 +318,25 @@ class Context:
         self._chk(self.lib.fcgpu_process(self.h, arena_ptr, desc_ptr, n, C.byref(out),
                                          stream or None), "fcgpu_process")
 
+    def jobs(self, specs):
+        """Prepare an fcgpu_job array from (arena_ptr, desc_ptr, n, stream, outputs-dict)
+        tuples; run it with run_jobs (no per-job Python work on the launch path)."""
+        arr = (fcgpu_job * max(len(specs), 1))()
+        for k, (arena, desc, n, stream, o) in enumerate(specs):
+            arr[k].arena = arena
+            arr[k].desc = desc
+            arr[k].n = n
+            arr[k].stream = stream or None
+            arr[k].out = fcgpu_out(o.get("verdict") or None, o.get("hash") or None, o.get("anno") or None,
+                                   o.get("perm") or None, o.get("port_start") or None,
+                                   o.get("tile_count") or None, o.get("partition", PART_GLOBAL), 0,
+                                   o.get("tile_perm") or None, o.get("flowid") or None, o.get("ip_rw") or None)
+        return arr, len(specs)
+
+    def run_jobs(self, prepared, stream=0):
+        arr, n = prepared
+        self._chk(self.lib.fcgpu_process_jobs(self.h, arr, n, stream or None), "fcgpu_process_jobs")
+
     def process_host(self, frames, lens_ptr, n, *, verdict=0, hash=0, anno=0, perm=0,
                      port_start=0, tile_count=0, partition=PART_GLOBAL, tile_perm=0, flowid=0, ip_rw=0):
         out = fcgpu_out(verdict or None, hash or None, anno or None, perm or None,
@@ -365,8 +396,9 @@ class Context:
     def use_counters(self, dptr: int):
         self._chk(self.lib.fcgpu_use_counters(self.h, dptr or None), "fcgpu_use_counters")
 
-    def set_timing(self, on: bool):
-        self._chk(self.lib.fcgpu_set_timing(self.h, 1 if on else 0), "fcgpu_set_timing")
+    def set_timing(self, every):
+        """every: bracket every k-th launch with events (True = 1, False/0 = off)."""
+        self._chk(self.lib.fcgpu_set_timing(self.h, int(every)), "fcgpu_set_timing")
 
     def read_timing(self):
         ms = (C.c_double * 3)()

@@ -43,6 +43,7 @@ struct EvPair {
     int stage;
 };
 
+constexpr size_t kTimingEvents = 6 * 64;     // pre-created by fcgpu_set_timing
 constexpr uint32_t kChunk = 131072;         // packets per host-pipeline chunk (whole tiles)
 constexpr int kSlots = 3;                   // chunks in flight: gather / copy+kernel / drain
 
@@ -192,8 +193,9 @@ struct fcgpu_ctx {
     FlowArgs fl{};            // device pointers; fl.slots == nullptr: disabled
     uint32_t *flow_hint = nullptr;    // mapped: size class of the last finish's misses (kHint*)
     uint32_t flow_epoch = 0;          // batches through the table (FlowArgs::epoch)
-    // timing
-    bool timing = false;
+    // timing: every timing_every-th launch is bracketed by events (0 = off)
+    uint32_t timing_every = 0;
+    uint64_t timing_seq = 0;
     std::vector<EvPair> pending;
     std::vector<hipEvent_t> free_ev;
     std::string err;
@@ -639,17 +641,26 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     return FCGPU_OK;
 }
 
-int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, uint32_t n,
-                  const fcgpu_out *o, void *stream) {
-    if (!c || !o) return FCGPU_EINVAL;
+// Argument checks shared by fcgpu_process and fcgpu_process_jobs.
+static int check_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, uint32_t n,
+                         const fcgpu_out *o) {
     if (!c->configured) return fail(c, FCGPU_EINVAL, "not configured");
     if (c->cfg.classify == FCGPU_CLS_PROGRAM && !c->d_prog && c->prog_all < 0)
         return fail(c, FCGPU_EINVAL, "FCGPU_CLS_PROGRAM without fcgpu_set_program");
     if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "batch larger than max_batch");
+    if (n && (!d_arena || !d_desc)) return fail(c, FCGPU_EINVAL, "null arena/desc");
+    if (o->partition > FCGPU_PART_TILE) return fail(c, FCGPU_EINVAL, "bad partition mode");
+    if (o->partition == FCGPU_PART_TILE && ((o->perm || o->tile_perm) != (o->tile_count != nullptr)))
+        return fail(c, FCGPU_EINVAL, "FCGPU_PART_TILE needs tile_count and perm and/or tile_perm");
+    if (c->fl.slots && c->cfg.check_mode != FCGPU_CHECK_IP4 && c->cfg.check_mode != FCGPU_MARK_IP4)
+        return fail(c, FCGPU_EINVAL, "the flow table needs an IPv4 check mode (CHECK_IP4 or MARK_IP4)");
+    return FCGPU_OK;
+}
+
+// One batch's launches on stream s (arguments checked, device current).
+static int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, uint32_t n,
+                       const fcgpu_out *o, hipStream_t s) {
     if (n == 0) return FCGPU_OK;
-    if (!d_arena || !d_desc) return fail(c, FCGPU_EINVAL, "null arena/desc");
-    hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream, as in HIP
-    HIPCHK(c, hipSetDevice(c->device));
     const uint32_t ntiles = (n + kTile - 1) / kTile;
     const uint32_t nports = c->cfg.nports;
     uint16_t *verdict = o->verdict;
@@ -658,10 +669,7 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
         verdict = c->d_verdict;
     }
     const bool tile = o->partition == FCGPU_PART_TILE;
-    if (o->partition > FCGPU_PART_TILE) return fail(c, FCGPU_EINVAL, "bad partition mode");
     const bool tperm = o->perm || o->tile_perm;
-    if (tile && (tperm != (o->tile_count != nullptr)))
-        return fail(c, FCGPU_EINVAL, "FCGPU_PART_TILE needs tile_count and perm and/or tile_perm");
     const bool want_global = !tile && (o->perm || o->port_start);
     const int part = tile && tperm ? kPartTile : (want_global ? kPartGlobal : kPartNone);
     RxArgs a;
@@ -686,15 +694,15 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
         a.fl.epoch = c->flow_epoch;
     }
     a.ip_rw = o->ip_rw;
-    if (a.fl.slots && c->cfg.check_mode != FCGPU_CHECK_IP4 && c->cfg.check_mode != FCGPU_MARK_IP4)
-        return fail(c, FCGPU_EINVAL, "the flow table needs an IPv4 check mode (CHECK_IP4 or MARK_IP4)");
 
+    // sampled timing: every timing_every-th launch of this context
+    const bool timed = c->timing_every && (c->timing_seq++ % c->timing_every) == 0;
     EvPair ev[3];
-    if (c->timing)
+    if (timed)
         for (int k = 0; k < 3; ++k) { ev[k].a = take_event(c); ev[k].b = take_event(c); ev[k].stage = k; }
 
-    launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, a, s, c->timing ? ev[0].a : nullptr,
-                  c->timing ? ev[0].b : nullptr);
+    launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, a, s, timed ? ev[0].a : nullptr,
+                  timed ? ev[0].b : nullptr);
     HIPCHK(c, hipGetLastError());
     if (a.fl.slots) {   // the batch's new flows get their IDs (fcgpu_flow.hh)
         const uint32_t nw = (n + 63) / 64;
@@ -710,16 +718,16 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
         HIPCHK(c, hipGetLastError());
     }
     if (want_global) {
-        if (c->timing) hipEventRecord(ev[1].a, s);
+        if (timed) hipEventRecord(ev[1].a, s);
         hipLaunchKernelGGL(k_scan, dim3(nports + 1), dim3(1024), 0, s, c->d_tilecnt, ntiles, c->d_totals);
         HIPCHK(c, hipGetLastError());
-        if (c->timing) { hipEventRecord(ev[1].b, s); hipEventRecord(ev[2].a, s); }
+        if (timed) { hipEventRecord(ev[1].b, s); hipEventRecord(ev[2].a, s); }
         hipLaunchKernelGGL(k_part, dim3(o->perm ? ntiles : 1), dim3(kTile), 0, s, verdict, o->perm ? n : 0u,
                            ntiles, nports, c->d_tilecnt, c->d_totals, o->perm, o->port_start);
         HIPCHK(c, hipGetLastError());
-        if (c->timing) hipEventRecord(ev[2].b, s);
+        if (timed) hipEventRecord(ev[2].b, s);
     }
-    if (c->timing) {
+    if (timed) {
         c->pending.push_back(ev[0]);
         if (want_global) {
             c->pending.push_back(ev[1]);
@@ -727,6 +735,38 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
         } else {
             for (int k = 1; k < 3; ++k) { c->free_ev.push_back(ev[k].a); c->free_ev.push_back(ev[k].b); }
         }
+    }
+    return FCGPU_OK;
+}
+
+int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, uint32_t n,
+                  const fcgpu_out *o, void *stream) {
+    if (!c || !o) return FCGPU_EINVAL;
+    int rc = check_process(c, d_arena, d_desc, n, o);
+    if (rc != FCGPU_OK || n == 0) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    return process_one(c, d_arena, d_desc, n, o, (hipStream_t)stream);   // NULL = the null stream
+}
+
+int fcgpu_process_jobs(fcgpu_ctx *c, const fcgpu_job *jobs, uint32_t njobs, void *stream) {
+    if (!c || (njobs && !jobs)) return FCGPU_EINVAL;
+    // every job is checked before any is launched: a bad job launches nothing
+    bool split = false;
+    for (uint32_t k = 0; k < njobs; ++k) {
+        const fcgpu_job &j = jobs[k];
+        int rc = check_process(c, j.arena, j.desc, j.n, &j.out);
+        if (rc != FCGPU_OK) return rc;
+        const bool shared = c->fl.slots || (j.out.partition == FCGPU_PART_GLOBAL && (j.out.perm || j.out.port_start));
+        if (j.stream && j.stream != stream) split = true;
+        if (split && shared)
+            return fail(c, FCGPU_EINVAL, "jobs on several streams: the flow table and the whole-batch "
+                                         "partition use context scratch (one stream only)");
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    for (uint32_t k = 0; k < njobs; ++k) {
+        const fcgpu_job &j = jobs[k];
+        int rc = process_one(c, j.arena, j.desc, j.n, &j.out, (hipStream_t)(j.stream ? j.stream : stream));
+        if (rc != FCGPU_OK) return rc;
     }
     return FCGPU_OK;
 }
@@ -1111,9 +1151,20 @@ int fcgpu_use_counters(fcgpu_ctx *c, uint64_t *d) {
     return FCGPU_OK;
 }
 
-int fcgpu_set_timing(fcgpu_ctx *c, int enable) {
-    if (!c) return FCGPU_EINVAL;
-    c->timing = enable != 0;
+int fcgpu_set_timing(fcgpu_ctx *c, int every) {
+    if (!c || every < 0) return FCGPU_EINVAL;
+    c->timing_every = (uint32_t)every;
+    c->timing_seq = 0;
+    if (every) {
+        // create the events now, not inside a timed region: a sampled launch
+        // takes 6 (three stages x start/stop)
+        HIPCHK(c, hipSetDevice(c->device));
+        while (c->free_ev.size() < kTimingEvents) {
+            hipEvent_t e = nullptr;
+            HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+            c->free_ev.push_back(e);
+        }
+    }
     return FCGPU_OK;
 }
 

@@ -27,6 +27,9 @@ Backend-agnostic: "nccl" (RCCL over xGMI) on GPUs, "gloo" in CPU tests.
 from __future__ import annotations
 
 
+ARENA_PAD = 256   # zeroed bytes after a received arena (include/fastclick_gpu.h over-read)
+
+
 def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
     """Contiguous [begin, end) packet range of `rank` among `world` shards."""
     if world <= 0 or not 0 <= rank < world:
@@ -67,9 +70,11 @@ def exchange_by_flow(arena, desc, owner, group=None):
     into it; owner: int64 [n], the destination rank of each packet (-1 keeps
     nothing: the packet is dropped here, e.g. one that failed the checks).
     Returns (arena_recv, desc_recv, src): the frames this rank now owns,
-    packed back to back in (source rank, source index) order, their
-    descriptors, and src = source_rank << 32 | source_index per packet.
-    The frames keep their bytes and lengths exactly.
+    packed back to back in (source rank, source index) order and followed by
+    ARENA_PAD zero bytes (the header-window over-read the ABI allows), their
+    descriptors (uint32 offset/length bit patterns in int32), and
+    src = source_rank << 32 | source_index per packet. The frames keep their
+    bytes and lengths exactly.
     """
     import torch
     import torch.distributed as dist
@@ -86,11 +91,7 @@ def exchange_by_flow(arena, desc, owner, group=None):
     off = desc[order, 0].to(torch.int64) & 0xFFFFFFFF
     ln = desc[order, 1].to(torch.int64) & 0xFFFFFFFF
     send_n = torch.bincount(owner[order], minlength=world)
-    # byte gather: every byte of every frame, frames back to back in send order
-    starts = torch.cumsum(ln, 0) - ln
-    total = int(ln.sum())
-    pos = torch.arange(total, device=dev) - torch.repeat_interleave(starts, ln)
-    payload = arena[torch.repeat_interleave(off, ln) + pos] if total else arena[:0]
+    payload = _gather_frames(arena, off, ln)
     send_b = torch.zeros(world, dtype=torch.int64, device=dev).index_add_(0, owner[order], ln)
     meta = torch.stack([ln, (rank << 32) | order], 1)        # [m, 2] length, source tag
     if world == 1:
@@ -107,5 +108,40 @@ def exchange_by_flow(arena, desc, owner, group=None):
         dist.all_to_all_single(rpay, payload.contiguous(), recv_b.tolist(), send_b.tolist(), group=group)
     rlen = rmeta[:, 0]
     roff = torch.cumsum(rlen, 0) - rlen
-    desc_recv = torch.stack([roff, rlen], 1).to(torch.int32)
-    return rpay, desc_recv, rmeta[:, 1]
+    if rpay.numel() >= (1 << 32) - ARENA_PAD:
+        raise ValueError("received frames exceed the 4 GiB a uint32 descriptor offset addresses")
+    # the ABI's over-read contract (include/fastclick_gpu.h): the arena stays
+    # readable 128 B past every frame start and 16 B past every frame end
+    arena_recv = torch.zeros(rpay.numel() + ARENA_PAD, dtype=torch.uint8, device=dev)
+    arena_recv[:rpay.numel()] = rpay
+    # offsets/lengths are uint32 bit patterns in an int32 tensor (DeviceBatch layout)
+    desc_recv = torch.stack([roff, rlen], 1).to(torch.int64)
+    desc_recv = torch.where(desc_recv >= (1 << 31), desc_recv - (1 << 32), desc_recv).to(torch.int32)
+    return arena_recv, desc_recv, rmeta[:, 1]
+
+
+def _gather_frames(arena, off, ln, chunk_bytes=1 << 24):
+    """Frames [off[k], off[k] + ln[k]) of arena, back to back. Gathers in
+    chunks of whole frames of about chunk_bytes, so the int64 byte index
+    never exceeds ~8 x chunk_bytes of temporary memory."""
+    import torch
+    total = int(ln.sum()) if ln.numel() else 0
+    out = torch.empty(total, dtype=torch.uint8, device=arena.device)
+    if total == 0:
+        return out
+    ends = torch.cumsum(ln, 0)
+    starts = ends - ln
+    bounds = [0]
+    if total > chunk_bytes:
+        cut = torch.searchsorted(ends, torch.arange(chunk_bytes, total, chunk_bytes, device=ln.device))
+        bounds += sorted(set(int(c) + 1 for c in cut.tolist()))
+    if bounds[-1] != ln.numel():
+        bounds.append(ln.numel())
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        if b <= a:
+            continue
+        o, l, s0 = off[a:b], ln[a:b], int(starts[a])
+        m = int(l.sum())
+        pos = torch.arange(m, device=arena.device) - torch.repeat_interleave(starts[a:b] - s0, l)
+        out[s0:s0 + m] = arena[torch.repeat_interleave(o, l) + pos]
+    return out

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 9
+#define FCGPU_ABI_VERSION 10
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -240,6 +240,25 @@ void fcgpu_close(fcgpu_ctx *ctx);
 int  fcgpu_process(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_desc,
                    uint32_t n, const fcgpu_out *d_out, void *stream);
 
+/* Several independent device-resident batches in one call -- e.g. the
+ * batches of several rx queues, or a ring of batches a NIC filled: job k is
+ * processed exactly as fcgpu_process(ctx, jobs[k].arena, jobs[k].desc,
+ * jobs[k].n, &jobs[k].out, jobs[k].stream ? jobs[k].stream : stream), in
+ * order, with one argument check and one device switch for the set. Jobs on
+ * different streams run concurrently (their outputs must not overlap); that
+ * is rejected when the context has a flow table or a job asks for a
+ * whole-batch partition (both use context scratch). Every job is checked
+ * before the first is launched. */
+typedef struct fcgpu_job {
+    const uint8_t  *arena;
+    const uint32_t *desc;
+    uint32_t        n;
+    uint32_t        reserved;
+    void           *stream;   /* hipStream_t or NULL (the call's stream)            */
+    fcgpu_out       out;
+} fcgpu_job;
+int  fcgpu_process_jobs(fcgpu_ctx *ctx, const fcgpu_job *jobs, uint32_t njobs, void *stream);
+
 /* Host-resident batch: frames[i] points at packet i's data (length lens[i]).
  * The first min(len, 128) bytes of every frame are gathered into pinned
  * staging, copied H2D, processed, and the requested outputs copied D2H into the
@@ -357,10 +376,13 @@ int  fcgpu_counters_device(fcgpu_ctx *ctx, uint64_t **d_counters);
 int  fcgpu_use_counters(fcgpu_ctx *ctx, uint64_t *d_counters);
 
 /* Per-kernel timing with HIP events on the launch stream (off by default).
+ * fcgpu_set_timing(ctx, k): k > 0 brackets every k-th launch of the context
+ * (1 = every launch) with start/stop events recorded by the launch itself;
+ * the events are created by this call, not on the launch path. 0 = off.
  * fcgpu_read_timing returns, per stage (0 = fused check/hash/classify,
  * 1 = count scan, 2 = partition scatter), the summed milliseconds and launches
  * since the last read, and resets them. Synchronises the context stream. */
-int  fcgpu_set_timing(fcgpu_ctx *ctx, int enable);
+int  fcgpu_set_timing(fcgpu_ctx *ctx, int every);
 int  fcgpu_read_timing(fcgpu_ctx *ctx, double *ms, uint32_t *launches, int nstages);
 
 const char *fcgpu_last_error(fcgpu_ctx *ctx);   /* ctx may be NULL (open errors) */

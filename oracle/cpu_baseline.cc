@@ -337,12 +337,17 @@ int main(int argc, char **argv) {
     };
     double one = run(1, seconds / 2);
     double all = threads > 1 ? run(threads, seconds / 2) : one;
-    printf("{\"mpps\": %.3f, \"mpps_1core\": %.3f, \"threads\": %d, \"sample\": \"%s\"}\n", all, one, threads,
-           ("C2-shaped 60-B UDP/IPv4 trace (4096 pkts, " + std::to_string(flows) +
-            " flow(s)) replayed in 32-packet linked-list batches: Strip(14) -> CheckIPHeader(CHECKSUM true) -> "
-            "AggregateHash -> " + (progfile.empty() ? std::string("FlowSwitch hash x16") : std::string("IPClassifier program x16")) +
-            " -> Discard; " + std::to_string(seconds / 2) +
-            " s at 1 thread + " + std::to_string(seconds / 2) + " s at all threads")
+    std::string chain = "Strip(14)";
+    if (stages >= 1) chain += " -> CheckIPHeader(CHECKSUM true)";
+    if (stages >= 2) chain += " -> AggregateHash";
+    if (stages >= 3) chain += progfile.empty() ? " -> FlowSwitch hash x16" : " -> IPClassifier program x16";
+    chain += " -> Discard";
+    printf("{\"mpps\": %.3f, \"mpps_1core\": %.3f, \"threads\": %d, \"stages\": %d, \"sample\": \"%s\"}\n", all,
+           one, threads, stages,
+           ("60-B UDP/IPv4 trace (4096 pkts, " + std::to_string(flows) +
+            " flow(s)) replayed in 32-packet linked-list batches: " + chain + "; " +
+            std::to_string(seconds / 2) + " s at 1 thread + " + std::to_string(seconds / 2) + " s at " +
+            std::to_string(threads) + " threads")
                .c_str());
     return 0;
 }

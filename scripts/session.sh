@@ -1,0 +1,57 @@
+#!/bin/bash
+# One GPU-box session of named steps (STEPS="a,b,c"). Every GPU step runs under
+# its own time limit; the session stops at the first step that faults, aborts
+# or times out (any exit code other than 0/1). Logs: gpurun_out/<step>.log,
+# rocprofv3 output: gpurun_out/prof_<step>/.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name $(date +%T)"; timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -n 3 "gpurun_out/$name.log" | cut -c1-1500
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+kt() {  # name timeout bench-args...: kernel trace + stats of a bench command
+  local name=$1 t=$2; shift 2
+  step "$name" "$t" rocprofv3 --kernel-trace --stats -f csv -d "gpurun_out/prof_$name" -o run -- python3 bench.py "$@"
+}
+pmc() {  # name counters... -- bench-args...
+  local name=$1; shift
+  local ctrs=()
+  while [ "$1" != "--" ]; do ctrs+=("$1"); shift; done; shift
+  step "$name" 120 rocprofv3 --pmc "${ctrs[@]}" --kernel-include-regex k_rx -f csv -d "gpurun_out/prof_$name" -o run -- python3 bench.py "$@"
+}
+DRV="--gpus 1 --steps 20 --warmup 5"
+IFS=, read -ra ST <<< "${STEPS:-tests,smoke,bench}"
+for s in "${ST[@]}"; do
+  case $s in
+    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 300 python bench.py $DRV ;;
+    bench_s1) step bench_s1 300 python bench.py $DRV --streams 1 --no-cpu ;;
+    bench_long) step bench_long 300 python bench.py --steps 200 --warmup 20 --no-cpu ;;
+    bench_long_s1) step bench_long_s1 300 python bench.py --steps 200 --warmup 20 --no-cpu --streams 1 ;;
+    kt_drv) kt kt_drv 300 $DRV --no-cpu ;;
+    kt_drv_s1) kt kt_drv_s1 300 $DRV --no-cpu --streams 1 ;;
+    kt_long) kt kt_long 300 --steps 200 --warmup 20 --no-cpu ;;
+    pmc) pmc pmc_fetch FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1
+         pmc pmc_write WRITE_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1
+         pmc pmc_ea TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1 ;;
+    sweep) for fb in 64 128 256 512 1024 1500; do
+             step "sweep_$fb" 300 python bench.py --steps 200 --warmup 20 --no-cpu --frame-bytes $fb
+             step "sweep_s1_$fb" 300 python bench.py --steps 200 --warmup 20 --no-cpu --frame-bytes $fb --streams 1
+           done ;;
+    variants) for v in "--workload c3" "--workload c4" "--workload c5" "--classify ipclass16" \
+                       "--workload c4 --classify ipclass16" "--flow-capacity 1" "--workload c3 --flow-capacity 20000" \
+                       "--workload c4 --flow-capacity 2000000" "--partition global" "--no-perm" "--shard strong"; do
+                n=$(echo "$v" | tr -d ' -' | cut -c1-40)
+                step "var_$n" 300 python bench.py --steps 200 --warmup 20 --no-cpu $v
+              done ;;
+    host) step host_rate 600 python scripts/host_rate.py ;;
+    dist2) step dist2 300 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 --no-cpu ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+exit 0

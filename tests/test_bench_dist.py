@@ -1,0 +1,135 @@
+"""bench.py's own rank function at world size 2 (gloo, CPU).
+
+bench.rank_main is the code every bench rank runs: shard selection, warmup,
+the barrier-bracketed timed region, max-over-ranks timing, the counter
+all-reduce and the per-output offset all-gather, and the checks on them. Here
+it runs with a CPU stand-in for the device processor whose counters come from
+the C oracle on the rank's shard (this host has no GPU); the GPU case is
+test_gpu_bench_two_ranks (two ranks sharing cuda:0 over gloo).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class OracleProcessor:
+    """CPU stand-in with DeviceProcessor's interface: each step's counters
+    are the oracle's counters of this rank's shard of the step's batch."""
+
+    def __init__(self, args, lo, hi, gpu):
+        import bench
+        from fastclick_amd import synth, _native as N
+        from oracle import oracle as O
+        b = bench.make_host_batch(args)
+        shard = synth.Batch(arena=b.arena, desc=np.ascontiguousarray(b.desc[lo:hi]))
+        cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=args.nports)
+        self.per_step = O.process_batch(cfg, shard)["counters"].astype(np.int64)
+        self.steps = args.steps
+        self.ctr = torch.zeros(N.CTR_SHARDS, N.NCOUNTERS, dtype=torch.int64)
+        self.n = hi - lo
+
+    def warmup(self, k):
+        pass
+
+    def run_timed(self):
+        self.ctr[3] += torch.from_numpy(self.per_step * self.steps)
+
+    def sync(self):
+        pass
+
+    def counters(self):
+        return self.ctr
+
+    def timing(self):
+        return None
+
+    def close(self):
+        pass
+
+
+def _rank(rank, world, port, argv, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        args = bench.parse(argv)
+        line = bench.rank_main(args, OracleProcessor, world=world, rank=rank, gpu=0, backend="gloo",
+                               dev_for_collectives="cpu")
+        lo, hi = bench.shard_of(args, world, rank)
+        q.put((rank, line, lo, hi))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_two(argv):
+    world = 2
+    port = 29700 + (os.getpid() % 500)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, argv, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.timeout(300)
+def test_bench_rank_main_strong_two_ranks(oracle):
+    """--shard strong: one 20,000-packet C4 batch per step split in two; the
+    all-reduced valid count is steps x the whole batch, n_gpus is 2, and the
+    two shards tile the batch."""
+    res = _run_two(["--gpus", "2", "--shard", "strong", "--packets", "20000", "--steps", "3",
+                    "--warmup", "1", "--no-cpu", "--nbuf", "1"])
+    line = res[0][1]
+    assert res[1][1] is None
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["config"]["packets_per_step"] == 20000
+    assert (res[0][2], res[0][3], res[1][2], res[1][3]) == (0, 10000, 10000, 20000)
+    assert line["value"] > 0 and line["steps"] == 3
+
+
+@pytest.mark.timeout(300)
+def test_bench_rank_main_weak_two_ranks(oracle):
+    """--shard weak: every rank its own batch; total = world x steps x n."""
+    res = _run_two(["--gpus", "2", "--packets", "5000", "--steps", "2", "--warmup", "1",
+                    "--no-cpu", "--nbuf", "1"])
+    line = res[0][1]
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["packets_per_step"] == 10000
+
+
+def test_bench_rejects_world_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_gpu_bench_two_ranks():
+    """`bench.py --gpus 2 --backend gloo` without WORLD_SIZE starts two local
+    ranks (both on cuda:0 here), each running the device path; the line
+    reports n_gpus 2 and the all-reduced valid count checks out inside."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    for shard in ("weak", "strong"):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                            "--shard", shard, "--packets", "65536", "--steps", "4", "--warmup", "2",
+                            "--nbuf", "2", "--no-cpu"], env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        line = json.loads(r.stdout.strip().splitlines()[-1])
+        assert line["n_gpus"] == 2 and line["scaling"] == shard
+        assert line["config"]["packets_per_step"] == (131072 if shard == "weak" else 65536)

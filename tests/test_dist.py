@@ -189,3 +189,20 @@ def test_gpu_exchange_pack_and_flow_table(oracle):
     res = device.process_batches([rb], fcfg, max_flows=1 << 16, anno=False, perm=False)
     ids = oracle.FlowTable(1 << 16).batch(rb, oracle.process_batch(fcfg, rb))
     assert np.array_equal(res[0]["flowid"], ids)
+
+
+def test_gather_frames_chunked_matches_whole():
+    """_gather_frames in small chunks equals a per-frame concatenation, and
+    exchange_by_flow's received arena carries the ABI's zeroed tail."""
+    rng = np.random.default_rng(5)
+    arena = torch.from_numpy(rng.integers(0, 256, 50_000, dtype=np.uint8))
+    ln = torch.from_numpy(rng.integers(0, 300, 200)).to(torch.int64)
+    off = torch.from_numpy(rng.integers(0, 49_000 - 300, 200)).to(torch.int64)
+    want = np.concatenate([arena.numpy()[o:o + n] for o, n in zip(off.tolist(), ln.tolist())])
+    for chunk in (1, 97, 1000, 1 << 24):
+        got = D._gather_frames(arena, off, ln, chunk_bytes=chunk)
+        assert np.array_equal(got.numpy(), want)
+    desc = torch.stack([off, ln], 1).to(torch.int32)
+    ra, rd, _ = D.exchange_by_flow(arena, desc, torch.zeros(200, dtype=torch.int64))
+    assert ra.numel() == int(ln.sum()) + D.ARENA_PAD and int(ra[-D.ARENA_PAD:].sum()) == 0
+    assert np.array_equal(ra[:int(ln.sum())].numpy(), want)

@@ -297,3 +297,51 @@ def test_l4_checks_misaligned_and_host(dev, oracle, mode):
     assert np.array_equal(verdict & 0xFF, exp["reason"]) and np.array_equal(verdict >> 8, exp["port"])
     assert np.array_equal(hsh, exp["hash"])
     ctx.close()
+
+
+def test_process_jobs_two_streams(dev, oracle):
+    """fcgpu_process_jobs: six batches (three C4 shapes with errors) on two
+    streams in one call give each batch the oracle's verdicts, hashes and
+    tile partition; the counters sum over the jobs; a bad job in the list
+    launches nothing (FCGPU_EINVAL before the first launch)."""
+    import torch
+    from fastclick_amd.device import DeviceBatch, DeviceOutputs
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16, badsrc=BADSRC)
+    batches = []
+    for s in range(3):
+        b = synth.c4(30_000 + 1_001 * s, seed=60 + s)
+        synth.inject_errors(b, 0.02, seed=70 + s)
+        batches.append(b)
+    exps = [oracle.process_batch(cfg, b) for b in batches]
+    ctx = N.Context(0, 40_000, cfg)
+    try:
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        dbs = [DeviceBatch.upload(b, device="cuda:0") for b in batches]
+        outs, specs = [], []
+        for k in range(6):
+            b = dbs[k % 3]
+            o = DeviceOutputs(b.n, 16, device="cuda:0", perm=True, partition=N.PART_TILE, anno=False)
+            outs.append(o)
+            specs.append((b.arena.data_ptr(), b.desc.data_ptr(), b.n, streams[k % 2].cuda_stream, o.ptrs()))
+        ctx.run_jobs(ctx.jobs(specs))
+        torch.cuda.synchronize()
+        for k in range(6):
+            got = outs[k].numpy()
+            exp = exps[k % 3]
+            assert np.array_equal(got["reason"], exp["reason"]), k
+            assert np.array_equal(got["port"], exp["port"]), k
+            ok = exp["reason"] == N.R_OK
+            assert np.array_equal(got["hash"][ok], exp["hash"][ok]), k
+            assert np.array_equal(got["tile_count"], exp["tile_count"]), k
+            assert np.array_equal(got["perm_tile"], exp["perm_tile"]), k
+        want = sum(2 * e["counters"].astype(np.int64) for e in exps)
+        assert np.array_equal(np.array(ctx.counters(), np.int64), want)
+        # one bad job (n > max_batch) -> error, and no job of the list ran
+        before = np.array(ctx.counters(), np.int64)
+        bad = list(specs[:2]) + [(specs[0][0], specs[0][1], 50_000, None, outs[0].ptrs())]
+        with pytest.raises(RuntimeError):
+            ctx.run_jobs(ctx.jobs(bad))
+        torch.cuda.synchronize()
+        assert np.array_equal(np.array(ctx.counters(), np.int64), before)
+    finally:
+        ctx.close()
