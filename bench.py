@@ -64,9 +64,11 @@ def parse(argv=None):
                     help="tile: each 256-packet tile is one classified PacketBatch (1 launch); "
                          "global: the whole batch is one (3 launches)")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
-    ap.add_argument("--timing-every", type=int, default=4,
-                    help="bracket every k-th launch with HIP events (hipExtLaunchKernelGGL start/stop "
-                         "on the launch stream; created before the timed region)")
+    ap.add_argument("--timing-every", type=int, default=0,
+                    help="bracket every k-th timed launch with HIP events (hipExtLaunchKernelGGL "
+                         "start/stop on the launch stream; created before the timed region). Each "
+                         "event idles the queue ~4 us, so the default samples sparsely: 8, or "
+                         "steps/2 below 64 steps")
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams the consecutive steps alternate over (each with its own output "
                          "buffers), as batches of several rx queues would")
@@ -315,7 +317,8 @@ class DeviceProcessor:
                                    partition=part, flowid=args.flow_capacity > 0)
                      for _ in self.streams]
         self.ctr = torch.zeros(N.CTR_SHARDS, N.NCOUNTERS, dtype=torch.int64, device=dev)
-        self.timing_every = 0 if args.no_timing else max(1, args.timing_every)
+        self.timing_every = 0 if args.no_timing else (
+            args.timing_every or (8 if args.steps >= 64 else max(1, args.steps // 2)))
 
     def _jobs(self, first, count):
         specs = []
@@ -327,12 +330,14 @@ class DeviceProcessor:
         return self.ctx.jobs(specs)
 
     def warmup(self, steps):
+        warm = self._jobs(0, steps)
+        self.timed = self._jobs(steps, self.args.steps)   # built before the warmup
         self.ctx.set_timing(self.timing_every)      # creates the event pool now
-        self.ctx.run_jobs(self._jobs(0, steps))
+        self.ctx.run_jobs(warm)
         self.torch.cuda.synchronize()
         self.ctx.read_timing()                      # drop warmup samples
+        self.ctx.set_timing(self.timing_every)      # sample count restarts at the timed region
         self.ctx.use_counters(self.ctr.data_ptr())  # timed steps count into the tensor
-        self.timed = self._jobs(steps, self.args.steps)   # built before t0
 
     def run_timed(self):
         self.ctx.run_jobs(self.timed)

@@ -23,11 +23,12 @@ ARCH = "gfx950"
 
 FCGPU_SRC = [os.path.join(CSRC, "fcgpu_api.hip")]
 FCGPU_DEPS = FCGPU_SRC + [os.path.join(CSRC, "fcgpu_device.hh"), os.path.join(CSRC, "fcgpu_flow.hh"),
-                          os.path.join(INC, "fastclick_gpu.h")]
+                          os.path.join(CSRC, "capture.hh"), os.path.join(INC, "fastclick_gpu.h")]
 FCCLICK_SRC = [os.path.join(CSRC, "host", f) for f in ("fcclick_capi.cc", "pcap_reader.cc")]
 FCCLICK_DEPS = FCCLICK_SRC + [os.path.join(CSRC, "host", f) for f in
-                              ("click_model.hh", "gpu_element.hh", "program_text.hh")] + \
-    [os.path.join(INC, f) for f in ("fcclick.h", "fcpcap.h", "fastclick_gpu.h")]
+                              ("click_model.hh", "click_args.hh", "gpu_core.hh", "gpu_element.hh",
+                               "program_text.hh")] + \
+    [os.path.join(CSRC, "capture.hh")] + [os.path.join(INC, f) for f in ("fcclick.h", "fcpcap.h", "fastclick_gpu.h")]
 
 
 def _stale(out, deps):
@@ -56,7 +57,7 @@ def build_fcclick(force=False):
     if not all(os.path.exists(p) for p in FCCLICK_SRC):
         return None
     if force or _stale(out, FCCLICK_DEPS + [os.path.join(LIB, "libfcgpu.so")]):
-        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra",
+        _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra",
               f"-I{INC}", *FCCLICK_SRC, "-o", out, f"-L{LIB}", "-lfcgpu",
               "-Wl,-rpath,$ORIGIN"])
     return out

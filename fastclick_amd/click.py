@@ -23,7 +23,8 @@ class fcclick_result(C.Structure):
     _fields_ = [("out_port", C.c_void_p), ("out_seq", C.c_void_p), ("out_agg", C.c_void_p),
                 ("out_dst", C.c_void_p), ("out_len", C.c_void_p), ("out_nh", C.c_void_p),
                 ("out_batches", C.c_void_p), ("handlers", C.c_char_p), ("handlers_cap", C.c_size_t),
-                ("out_paint", C.c_void_p), ("out_flow", C.c_void_p), ("out_ip8", C.c_void_p)]
+                ("out_paint", C.c_void_p), ("out_flow", C.c_void_p), ("out_ip8", C.c_void_p),
+                ("out_parked", C.c_void_p)]
 
 
 def load():
@@ -43,9 +44,15 @@ def load():
     lib.fcclick_run.restype = C.c_int
     lib.fcclick_run.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                 C.POINTER(fcclick_result), C.c_char_p, C.c_size_t]
+    lib.fcclick_run_ex.restype = C.c_int
+    lib.fcclick_run_ex.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                   C.c_uint32, C.POINTER(fcclick_result), C.c_char_p, C.c_size_t]
     lib.fcclick_bench.restype = C.c_int
     lib.fcclick_bench.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.POINTER(C.c_double), C.c_char_p, C.c_size_t]
+    lib.fcclick_bench_threads.restype = C.c_int
+    lib.fcclick_bench_threads.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                          C.c_uint32, C.c_uint32, C.POINTER(C.c_double), C.c_char_p, C.c_size_t]
     _lib = lib
     return lib
 
@@ -75,9 +82,10 @@ def parse_program(text: str):
 
 
 PER_PACKET = 0xFFFFFFFF   # burst value: the source calls push(0, p) per packet (fcclick.h)
+TIMER_FLUSH = 1           # fcclick_run_ex flag: end with the element's timer, not flush()
 
 
-def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1):
+def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1, timer_flush: bool = False):
     lib = load()
     n = batch.n
     arena = np.ascontiguousarray(batch.arena)
@@ -86,14 +94,15 @@ def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1):
                                             ("dst", np.uint32), ("len", np.uint32), ("nh", np.int32),
                                             ("paint", np.uint8), ("flow", np.uint32), ("ip8", np.uint32))}
     nb = np.zeros(1, np.uint32)
+    parked = np.zeros(1, np.uint32)
     hbuf = C.create_string_buffer(4096)
     res = fcclick_result(out["port"].ctypes.data, out["seq"].ctypes.data, out["agg"].ctypes.data,
                          out["dst"].ctypes.data, out["len"].ctypes.data, out["nh"].ctypes.data,
                          nb.ctypes.data, C.cast(hbuf, C.c_char_p), 4096, out["paint"].ctypes.data,
-                         out["flow"].ctypes.data, out["ip8"].ctypes.data)
+                         out["flow"].ctypes.data, out["ip8"].ctypes.data, parked.ctypes.data)
     err = C.create_string_buffer(512)
-    rc = lib.fcclick_run(conf.encode(), arena.ctypes.data, desc.ctypes.data, n, burst, nsinks,
-                         C.byref(res), err, 512)
+    rc = lib.fcclick_run_ex(conf.encode(), arena.ctypes.data, desc.ctypes.data, n, burst, nsinks,
+                            TIMER_FLUSH if timer_flush else 0, C.byref(res), err, 512)
     if rc == -1:
         raise ConfigError(err.value.decode())
     if rc != 0:
@@ -108,18 +117,21 @@ def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1):
         elif name is not None:
             handlers[name] += "\n" + line
     out["batches"] = int(nb[0])
+    out["parked"] = int(parked[0])
     out["handlers"] = handlers
     return out
 
 
-def bench_element(conf: str, batch, *, burst: int = 32, reps: int = 5) -> float:
+def bench_element(conf: str, batch, *, burst: int = 32, reps: int = 5, threads: int = 1) -> float:
+    """Packets/s through the element (threads > 1: that many instances, one
+    per thread, each with its own GPU context; the sum of their rates)."""
     lib = load()
     arena = np.ascontiguousarray(batch.arena)
     desc = np.ascontiguousarray(batch.desc, dtype=np.uint32)
     pps = C.c_double()
     err = C.create_string_buffer(512)
-    rc = lib.fcclick_bench(conf.encode(), arena.ctypes.data, desc.ctypes.data, batch.n, burst, reps,
-                           C.byref(pps), err, 512)
+    rc = lib.fcclick_bench_threads(conf.encode(), arena.ctypes.data, desc.ctypes.data, batch.n, burst, reps,
+                                   threads, C.byref(pps), err, 512)
     if rc != 0:
         raise RuntimeError(err.value.decode())
     return pps.value

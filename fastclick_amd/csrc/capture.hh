@@ -1,0 +1,60 @@
+// capture.hh -- how many leading bytes of each frame a host-resident batch
+// must hand to the device (host code shared by fcgpu_process_host and the
+// GPUIPCheckClassify element's staging).
+//
+// The device reads a frame's header window and, past it, whatever the
+// configured chain looks at; bytes beyond that never decide a verdict, an
+// annotation or an output. Staging only the reach (rounded up to whole 64-B
+// slots, at least 128 B) keeps the PCIe copy at ~64-128 B per packet.
+#pragma once
+#include <stdint.h>
+#include "../../include/fastclick_gpu.h"
+
+namespace fcgpu {
+
+constexpr uint32_t kCaptureWhole = 0xffffffffu;
+constexpr uint32_t kCaptureMin = 128;
+
+// Bytes from the frame start a decision program may read (IPFilter offsets
+// >= 512 are transport-relative, >= 256 network-relative, else MAC - 2,
+// elements/ip/ipfilter.hh:393-481; Classifier offsets are frame-relative).
+// `l3` is the farthest a network header can start; `l4` the farthest a
+// transport header can start.
+inline uint32_t program_reach(uint32_t kind, const fcgpu_step *steps, uint32_t n, uint32_t l3, uint32_t l4) {
+    uint32_t r = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        const int32_t o = steps[k].offset;
+        uint32_t end;
+        if (kind == FCGPU_PROG_IPFILTER)
+            end = o >= 512 ? l4 + (uint32_t)(o - 512) + 4 : o >= 256 ? l3 + (uint32_t)(o - 256) + 4
+                                                                   : (o > 2 ? (uint32_t)o - 2 : 0u) + 4;
+        else
+            end = (o > 0 ? (uint32_t)o : 0u) + 4;
+        r = end > r ? end : r;
+    }
+    return r;
+}
+
+// prog_reach: program_reach() of the installed program (0 without one).
+inline uint32_t capture_bytes(const fcgpu_cfg &c, uint32_t prog_reach) {
+    // the L4 checksum covers the segment, PROCESS_EH follows any number of
+    // extension headers: whole frames
+    if (c.l4_mode != FCGPU_L4_NONE && c.l4_checksum) return kCaptureWhole;
+    const bool autom = c.check_mode == FCGPU_CHECK_AUTO;
+    if (autom && c.process_eh) return kCaptureWhole;
+    const uint32_t l3 = (uint32_t)c.offset + (autom ? 18u : 0u);   // StripEtherVLANHeader: 14 or 18
+    // IPv4: up to 60 B of header then the L4 words the checks and hashes read
+    // (ports, UDP length/checksum, TCP offset: 16 B); IPv6: 40 B + the same
+    const uint32_t l4 = l3 + 60;
+    uint32_t need = l4 + 16;
+    if (c.classify == FCGPU_CLS_HASHSWITCH) {
+        const uint32_t e = (uint32_t)c.hs_offset + (uint32_t)c.hs_length;
+        need = e > need ? e : need;
+    }
+    if (c.classify == FCGPU_CLS_HASH_IP && need < 34) need = 34;
+    if (prog_reach > need) need = prog_reach;
+    need = (need + 63) & ~63u;
+    return need < kCaptureMin ? kCaptureMin : need;
+}
+
+}  // namespace fcgpu

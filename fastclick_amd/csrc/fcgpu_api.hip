@@ -25,6 +25,7 @@
 
 #include "fcgpu_device.hh"
 #include "fcgpu_flow.hh"
+#include "capture.hh"
 
 #pragma clang diagnostic ignored "-Wunused-result"
 #pragma clang diagnostic ignored "-Wunused-value"
@@ -168,8 +169,9 @@ struct fcgpu_ctx {
     unsigned long long *d_ctr = nullptr;      // active counter vector
     unsigned long long *d_ctr_own = nullptr;  // context-owned vector
     uint4 *d_prog = nullptr;                  // decision program (FCGPU_CLS_PROGRAM)
-    uint32_t prog_n = 0, prog_kind = 0;
+    uint32_t prog_n = 0, prog_kind = 0, prog_q = 0, prog_tab = 0;
     int32_t prog_all = -1;
+    std::vector<fcgpu_step> prog_host;   // the installed program (capture reach)
     uint16_t *d_verdict = nullptr;   // scratch verdicts when the caller wants perm only
     // host-resident staging
     uint8_t *h_arena = nullptr, *d_arena = nullptr;
@@ -201,10 +203,16 @@ struct fcgpu_ctx {
     std::string err;
 };
 
-// Bytes of each frame the host paths stage: the 128-B header window, or the
-// whole frame when the L4 checksum covers the segment.
+// Bytes of each frame the host paths stage (capture.hh): the reach of the
+// configured chain, at least 128 B, or whole frames (L4 checksum, PROCESS_EH).
 static uint32_t host_capture(const fcgpu_ctx *c) {
-    return (c->cfg.l4_mode != FCGPU_L4_NONE && c->cfg.l4_checksum) ? 0xffffffffu : kHostCap;
+    const bool autom = c->cfg.check_mode == FCGPU_CHECK_AUTO;
+    const uint32_t l3 = (uint32_t)c->cfg.offset + (autom ? 18u : 0u);
+    const uint32_t reach = c->cfg.classify == FCGPU_CLS_PROGRAM && !c->prog_host.empty()
+                               ? program_reach(c->prog_kind, c->prog_host.data(), (uint32_t)c->prog_host.size(),
+                                               l3, l3 + 60)
+                               : 0u;
+    return capture_bytes(c->cfg, reach);
 }
 
 // hipMemset can complete after work already queued on non-blocking streams
@@ -389,6 +397,88 @@ static int process_host_whole(fcgpu_ctx *c, const uint8_t *const *frames, const 
     return FCGPU_OK;
 }
 
+
+// Jump tables for runs of steps that test one word (SURVEY 8(a) A11 programs:
+// a rule's fields, and above all a port range the reference's compiler splits
+// into a chain of mask tests on the transport word). Lanes of a wave walking
+// such a chain for different port values leave it at different steps; a
+// table gives every lane the chain's outcome in one step. For each entry step
+// e (step 0, and every step reached by a jump from a step at another offset)
+// the run R(e) = steps reachable from e through steps at e's offset. If the
+// bits R's masks test span at most kTabBits bits of the big-endian word, e
+// becomes a table step: tab[(bswap(word) >> lo) & (2^w - 1)] = where a walk
+// from e with that word leaves R (an output <= 0 or a step outside R), and
+// its original step is appended as the fallback for words that are not
+// entirely inside the packet (the length-checked rules decide those). The
+// steps keep their indices; dev grows by the fallback copies and the tables.
+// Returns the step count (copies included); tab_q = uint4 index of the tables.
+static uint32_t build_tables(std::vector<uint4> &dev, uint32_t nsteps, uint32_t &tab_q) {
+    constexpr uint32_t kTabBits = 8, kTabBudget = 2048;     // entries per table, in total
+    auto off_of = [&](uint32_t k) { return (int16_t)(dev[k].x & 0xffff); };
+    auto yes_of = [&](const uint4 &st) { return (int32_t)(int16_t)(st.w & 0xffff); };
+    auto no_of = [&](const uint4 &st) { return (int32_t)(int16_t)(st.w >> 16); };
+    std::vector<char> entry(nsteps, 0);
+    entry[0] = 1;
+    for (uint32_t k = 0; k < nsteps; ++k)
+        for (int32_t t : {yes_of(dev[k]), no_of(dev[k])})
+            if (t > 0 && off_of((uint32_t)t) != off_of(k)) entry[t] = 1;
+    std::vector<uint4> copies;
+    std::vector<uint16_t> tabs;
+    std::vector<int> inr(nsteps, -1);
+    for (uint32_t e = 0; e < nsteps; ++e) {
+        if (!entry[e]) continue;
+        // the run from e
+        std::vector<uint32_t> run{e}, todo{e};
+        inr[e] = (int)e;
+        uint32_t mbe = 0;
+        while (!todo.empty()) {
+            const uint32_t k = todo.back();
+            todo.pop_back();
+            mbe |= __builtin_bswap32(dev[k].z);
+            for (int32_t t : {yes_of(dev[k]), no_of(dev[k])})
+                if (t > 0 && inr[t] != (int)e && off_of((uint32_t)t) == off_of(e)) {
+                    inr[t] = (int)e;
+                    run.push_back((uint32_t)t);
+                    todo.push_back((uint32_t)t);
+                }
+        }
+        if (run.size() < 2 || mbe == 0) continue;
+        const uint32_t lo = __builtin_ctz(mbe), w = 32 - __builtin_clz(mbe) - lo;
+        if (w > kTabBits || tabs.size() + (1u << w) > kTabBudget) continue;
+        const uint32_t base = (uint32_t)tabs.size();
+        for (uint32_t idx = 0; idx < (1u << w); ++idx) {
+            const uint32_t word = __builtin_bswap32(idx << lo);   // the packet word as the device loads it
+            int32_t pos = (int32_t)e, j = -kProgUnmatched;
+            for (size_t hops = 0; hops <= run.size(); ++hops) {
+                const uint4 &st = dev[pos];
+                j = (word & st.z) == st.y ? yes_of(st) : no_of(st);
+                if (j <= 0 || inr[j] != (int)e) break;
+                pos = j;
+                j = -kProgUnmatched;                                // a cycle inside the run
+            }
+            tabs.push_back((uint16_t)(int16_t)j);
+        }
+        copies.push_back(dev[e]);
+        const uint32_t copy_at = nsteps + (uint32_t)copies.size() - 1;
+        dev[e].x = (dev[e].x & 0xffffu) | (kStepTable << 16);
+        dev[e].y = base;
+        dev[e].z = lo | (w << 8);
+        dev[e].w = copy_at;
+    }
+    dev.resize(nsteps);
+    dev.insert(dev.end(), copies.begin(), copies.end());
+    tab_q = (uint32_t)dev.size();
+    tabs.resize((tabs.size() + 7) & ~(size_t)7, 0);
+    for (size_t k = 0; k < tabs.size(); k += 8) {
+        uint4 q;
+        q.x = tabs[k] | (uint32_t)tabs[k + 1] << 16;
+        q.y = tabs[k + 2] | (uint32_t)tabs[k + 3] << 16;
+        q.z = tabs[k + 4] | (uint32_t)tabs[k + 5] << 16;
+        q.w = tabs[k + 6] | (uint32_t)tabs[k + 7] << 16;
+        dev.push_back(q);
+    }
+    return nsteps + (uint32_t)copies.size();
+}
 
 extern "C" {
 
@@ -635,6 +725,8 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     memcpy(d.bad6, cfg->bad6, sizeof(d.bad6));
     d.prog = c->d_prog;
     d.prog_n = c->prog_n;
+    d.prog_q = c->prog_q;
+    d.prog_tab = c->prog_tab;
     d.prog_kind = c->prog_kind;
     d.prog_all = c->prog_all;
     c->configured = true;
@@ -695,8 +787,10 @@ static int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_d
     }
     a.ip_rw = o->ip_rw;
 
-    // sampled timing: every timing_every-th launch of this context
-    const bool timed = c->timing_every && (c->timing_seq++ % c->timing_every) == 0;
+    // sampled timing: the timing_every-th, 2*timing_every-th, ... launch since
+    // fcgpu_set_timing (not the first: a start event ahead of an idle queue's
+    // first launch would delay it)
+    const bool timed = c->timing_every && (++c->timing_seq % c->timing_every) == 0;
     EvPair ev[3];
     if (timed)
         for (int k = 0; k < 3; ++k) { ev[k].a = take_event(c); ev[k].b = take_event(c); ev[k].stage = k; }
@@ -757,7 +851,7 @@ int fcgpu_process_jobs(fcgpu_ctx *c, const fcgpu_job *jobs, uint32_t njobs, void
         int rc = check_process(c, j.arena, j.desc, j.n, &j.out);
         if (rc != FCGPU_OK) return rc;
         const bool shared = c->fl.slots || (j.out.partition == FCGPU_PART_GLOBAL && (j.out.perm || j.out.port_start));
-        if (j.stream && j.stream != stream) split = true;
+        if ((j.stream ? j.stream : stream) != (jobs[0].stream ? jobs[0].stream : stream)) split = true;
         if (split && shared)
             return fail(c, FCGPU_EINVAL, "jobs on several streams: the flow table and the whole-batch "
                                          "partition use context scratch (one stream only)");
@@ -1129,13 +1223,20 @@ int fcgpu_set_program(fcgpu_ctx *c, uint32_t kind, const fcgpu_step *steps, uint
         dev[k].z = st.mask;
         dev[k].w = (uint32_t)(uint16_t)y | ((uint32_t)(uint16_t)n << 16);
     }
+    uint32_t tab_q = 0;
+    const uint32_t total_n = nsteps ? build_tables(dev, nsteps, tab_q) : 0;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipDeviceSynchronize());
     hipFree(c->d_prog);
     c->d_prog = nullptr;
     HIPCHK(c, hipMalloc(&c->d_prog, sizeof(uint4) * dev.size()));
     HIPCHK(c, hipMemcpy(c->d_prog, dev.data(), sizeof(uint4) * dev.size(), hipMemcpyHostToDevice));
-    c->prog_n = nsteps;
+    c->prog_host.assign(steps, steps + nsteps);
+    c->prog_n = total_n;
+    c->prog_q = (uint32_t)dev.size();
+    c->prog_tab = tab_q;
+    c->dcfg.prog_q = c->prog_q;
+    c->dcfg.prog_tab = c->prog_tab;
     c->prog_kind = kind;
     c->prog_all = nsteps == 0 ? output_everything : -1;
     c->dcfg.prog = c->d_prog;

@@ -45,15 +45,23 @@ struct DevCfg {
     uint32_t l4_checksum;
     uint32_t rewrite;         // FCGPU_RW_*
     uint32_t ttl_multicast;
-    const uint4 *prog;        // decision program (FCGPU_CLS_PROGRAM), 16 B per step
-    uint32_t prog_n;
+    const uint4 *prog;        // decision program (FCGPU_CLS_PROGRAM), 16 B per step, then tables
+    uint32_t prog_n;          // steps (table-step fallback copies included)
+    uint32_t prog_q;          // uint4 words of steps + tables
+    uint32_t prog_tab;        // uint4 index where the int16 jump tables start
     uint32_t prog_kind;
     int32_t prog_all;         // >= 0: empty program, every packet -> this output
 };
 
 // Device step: x = (u16)offset | flags << 16, y = value, z = mask,
 // w = (u16)yes | (u16)no << 16 (signed 16-bit jumps).
+// Table step (flag kStepTable, built by fcgpu_set_program from a run of steps
+// that all test the word at one offset): when the word is inside the packet,
+// the run's outcome is tab[y + ((bswap(word) >> (z & 31)) & ((1 << (z >> 8)) - 1))]
+// (an int16 jump), else the walk continues at step w, a copy of the original
+// step, so short packets keep the step-by-step length-checked semantics.
 constexpr int32_t kProgUnmatched = 0x7fff;
+constexpr uint32_t kStepTable = 2u;       // in the flags (x >> 16)
 
 // Flow table state (fcgpu_flow_enable). Slot = {saddr, daddr, ports, tag} with
 // tag = proto | (flow id + 1) << 8; tag 0 = empty. Linear probing, never more
@@ -208,11 +216,17 @@ __device__ __forceinline__ uint32_t run_program_on(const DevCfg &c, const FrameV
     // split into mask tests): keep the last one instead of re-reading it
     int lastb = INT32_MIN;
     uint32_t lastw = 0;
+    const uint16_t *tab = reinterpret_cast<const uint16_t *>(prog + c.prog_tab);
     for (uint32_t it = 0; it <= c.prog_n; ++it) {
         const uint4 st = prog[pos];
         const int off = (int16_t)(st.x & 0xffff);
         const uint32_t m = st.z;
+        const bool table = (st.x >> 16) & kStepTable;
         bool avail = off + 4 <= plen;
+        if (table && !avail) {            // short word: the original steps decide
+            pos = (int)st.w;
+            continue;
+        }
         if (!avail && off < plen) {
             const int a = plen - off;
             avail = !((m >> 24) || (((m >> 16) & 0xff) && a <= 2) || (((m >> 8) & 0xff) && a == 1));
@@ -224,8 +238,13 @@ __device__ __forceinline__ uint32_t run_program_on(const DevCfg &c, const FrameV
                 lastw = prog_word(f, b);
                 lastb = b;
             }
-            const uint32_t data = lastw & m;
-            j = data == st.y ? (int16_t)(st.w & 0xffff) : (int16_t)(st.w >> 16);
+            if (table) {
+                const uint32_t idx = (__builtin_bswap32(lastw) >> (m & 31)) & ((1u << (m >> 8)) - 1u);
+                j = (int16_t)tab[st.y + idx];
+            } else {
+                const uint32_t data = lastw & m;
+                j = data == st.y ? (int16_t)(st.w & 0xffff) : (int16_t)(st.w >> 16);
+            }
         } else {
             j = ((st.x >> 16) & FCGPU_STEP_SHORT_YES) ? (int16_t)(st.w & 0xffff) : (int16_t)(st.w >> 16);
         }
@@ -237,12 +256,14 @@ __device__ __forceinline__ uint32_t run_program_on(const DevCfg &c, const FrameV
 
 // Steps come from the workgroup's LDS copy when the program fits (sprog !=
 // nullptr, block-uniform), else from global memory.
-constexpr uint32_t kProgLds = 128;          // steps cached in LDS (<= 2 KiB)
+// Steps + tables cached in LDS: <= 2.5 KiB keeps 8 workgroups (17.6 KB of
+// header windows and counts each) within a CU's 160 KB.
+constexpr uint32_t kProgLdsQ = 160;
 __host__ __device__ inline bool prog_in_lds(const DevCfg &c) {
-    return c.classify == FCGPU_CLS_PROGRAM && c.prog_all < 0 && c.prog_n <= kProgLds;
+    return c.classify == FCGPU_CLS_PROGRAM && c.prog_all < 0 && c.prog_q <= kProgLdsQ;
 }
 // dynamic LDS of a k_rx launch: only program mode pays for the step cache
-inline size_t prog_lds_bytes(const DevCfg &c) { return prog_in_lds(c) ? sizeof(uint4) * c.prog_n : 0; }
+inline size_t prog_lds_bytes(const DevCfg &c) { return prog_in_lds(c) ? sizeof(uint4) * c.prog_q : 0; }
 __device__ __forceinline__ uint32_t run_program(const DevCfg &c, const FrameView &f, const fcgpu_anno &an,
                                                 const uint4 *sprog) {
     if (sprog) return run_program_on(c, f, an, sprog);
@@ -1088,7 +1109,7 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
     for (int k = 0; k < 4; ++k) glds16(win_src(A.arena, d.x, lane, k), wl + k * 1024);
     // decision program: the block's LDS copy when it fits (block-uniform)
     const bool prog_lds = PROG && prog_in_lds(A.cfg);
-    if (prog_lds && threadIdx.x < A.cfg.prog_n) s_prog[threadIdx.x] = A.cfg.prog[threadIdx.x];
+    if (prog_lds && threadIdx.x < A.cfg.prog_q) s_prog[threadIdx.x] = A.cfg.prog[threadIdx.x];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (prog_lds) __syncthreads();
     rx_tile<CM, CK, PART, PROG, L4, FAST, FLOW>(A, tile, d, wl, s_cnt, prog_lds ? s_prog : nullptr);

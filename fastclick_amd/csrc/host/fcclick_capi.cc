@@ -1,5 +1,7 @@
 // fcclick_capi.cc -- C ABI of the host harness (include/fcclick.h).
+#include <algorithm>
 #include <chrono>
+#include <thread>
 #include <memory>
 #include <string>
 #include <vector>
@@ -131,8 +133,9 @@ extern "C" int fcclick_parse_program(const char *text, fcgpu_step *steps, uint32
     return 0;
 }
 
-extern "C" int fcclick_run(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
-                           uint32_t burst, uint32_t nsinks, fcclick_result *res, char *err, size_t errcap) {
+extern "C" int fcclick_run_ex(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                              uint32_t burst, uint32_t nsinks, uint32_t flags, fcclick_result *res, char *err,
+                              size_t errcap) {
     std::string e;
     auto el = make_element(conf, e);
     if (!el || el->initialize(e) < 0) {
@@ -176,7 +179,19 @@ extern "C" int fcclick_run(const char *conf, const uint8_t *arena, const uint32_
         else
             el->push_batch(0, PacketBatch::make_from_list(head, prev, m));
     }
-    el->flush();
+    if (flags & FCCLICK_TIMER_FLUSH) {
+        // the source has stopped: only the element's Timer can release what it
+        // still holds (MinBatch's timer, minbatch.cc:35,57-76)
+        auto now = []() {
+            return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                       std::chrono::steady_clock::now().time_since_epoch()).count();
+        };
+        if (res && res->out_parked) *res->out_parked = el->held();
+        for (int k = 0; k < 100000 && el->run_timer(now()); ++k)
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+    } else {
+        el->flush();
+    }
     if (res) {
         if (res->out_batches) *res->out_batches = nbatch;
         if (res->handlers && res->handlers_cap) {
@@ -195,14 +210,18 @@ extern "C" int fcclick_run(const char *conf, const uint8_t *arena, const uint32_
     return 0;
 }
 
-extern "C" int fcclick_bench(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
-                             uint32_t burst, uint32_t reps, double *pps, char *err, size_t errcap) {
-    std::string e;
+extern "C" int fcclick_run(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                           uint32_t burst, uint32_t nsinks, fcclick_result *res, char *err, size_t errcap) {
+    return fcclick_run_ex(conf, arena, desc, n, burst, nsinks, 0, res, err, errcap);
+}
+
+namespace {
+// One element instance (its own GPU context, like one Click thread) pushed
+// `reps` times through the trace; returns packets per second, or < 0.
+double bench_one(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n, uint32_t burst,
+                 uint32_t reps, std::string &e) {
     auto el = make_element(conf, e);
-    if (!el || el->initialize(e) < 0) {
-        copy_err(e, err, errcap);
-        return -1;
-    }
+    if (!el || el->initialize(e) < 0) return -1.0;
     const bool per_packet = burst == FCCLICK_PER_PACKET;
     if (burst == 0) burst = 32;
     if (per_packet) burst = 32;
@@ -212,11 +231,16 @@ extern "C" int fcclick_bench(const char *conf, const uint8_t *arena, const uint3
         sinks.emplace_back(new Sink((int)k, nullptr, &seq, &nbatch));
         el->connect_output((int)k, sinks.back().get(), 0);
     }
+    // a DPDK-style mempool: as many packets as the element can hold plus the
+    // bursts in flight, recycled LIFO (packets freed by the sinks are reused
+    // first, as a mempool's per-core cache does) -- not one packet per frame
     const uint32_t headroom = 128;
-    PacketPool pool(n, headroom + max_len(desc, n) + 64, headroom);
+    const uint32_t pool_n = std::max<uint32_t>(4096, el->max_held() + 4 * burst + 4096);
+    PacketPool pool(pool_n, headroom + max_len(desc, n) + 64, headroom);
     auto one = [&]() {
         for (uint32_t i = 0; i < n; i += burst) {
             uint32_t m = n - i < burst ? n - i : burst;
+            if (pool.available() < m) el->flush();      // never expected: the pool covers max_held
             Packet *head = nullptr, *prev = nullptr;
             for (uint32_t j = 0; j < m; ++j) {
                 Packet *p = pool.make(arena + desc[2 * (i + j)], desc[2 * (i + j) + 1]);
@@ -239,12 +263,45 @@ extern "C" int fcclick_bench(const char *conf, const uint8_t *arena, const uint3
     auto t0 = std::chrono::steady_clock::now();
     for (uint32_t r = 0; r < reps; ++r) one();
     auto t1 = std::chrono::steady_clock::now();
-    double s = std::chrono::duration<double>(t1 - t0).count();
-    if (pps) *pps = (double)n * reps / s;
-    std::string er = el->read_handler("error");
-    if (!er.empty()) {
-        copy_err(er, err, errcap);
-        return -2;
+    const double s = std::chrono::duration<double>(t1 - t0).count();
+    e = el->read_handler("error");
+    if (!e.empty()) return -2.0;
+    return (double)n * reps / s;
+}
+}  // namespace
+
+extern "C" int fcclick_bench(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                             uint32_t burst, uint32_t reps, double *pps, char *err, size_t errcap) {
+    std::string e;
+    const double r = bench_one(conf, arena, desc, n, burst, reps, e);
+    if (r < 0) {
+        copy_err(e, err, errcap);
+        return r == -1.0 ? -1 : -2;
     }
+    if (pps) *pps = r;
+    return 0;
+}
+
+extern "C" int fcclick_bench_threads(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                                     uint32_t burst, uint32_t reps, uint32_t threads, double *pps, char *err,
+                                     size_t errcap) {
+    if (threads == 0) threads = 1;
+    std::vector<double> r(threads, 0.0);
+    std::vector<std::string> es(threads);
+    std::vector<std::thread> th;
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t t = 0; t < threads; ++t)
+        th.emplace_back([&, t]() { r[t] = bench_one(conf, arena, desc, n, burst, reps, es[t]); });
+    for (auto &x : th) x.join();
+    (void)t0;
+    double tot = 0;
+    for (uint32_t t = 0; t < threads; ++t) {
+        if (r[t] < 0) {
+            copy_err(es[t], err, errcap);
+            return r[t] == -1.0 ? -1 : -2;
+        }
+        tot += r[t];
+    }
+    if (pps) *pps = tot;
     return 0;
 }

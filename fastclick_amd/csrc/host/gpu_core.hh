@@ -1,0 +1,704 @@
+// gpu_core.hh -- the logic of the GPUIPCheckClassify element, written once for
+// two packet models:
+//   - FastClick's (fastclick_pkg/gpuipcheckclassify.{hh,cc}: Packet /
+//     PacketBatch of include/click/packet.hh and packetbatch.hh), and
+//   - the test harness's (click_model.hh, driven by tests through libfcclick).
+// A policy class P maps the few Packet/PacketBatch operations the element
+// needs onto each model (see ModelPolicy in gpu_element.hh and ClickPolicy in
+// fastclick_pkg/gpuipcheckclassify.hh), so the code the tests exercise is the
+// code the FastClick element runs.
+//
+// Replaces the CPU chain
+//     [Strip(14) | StripEtherVLANHeader] -> CheckIPHeader / CheckIP6Header
+//         -> AggregateHash -> FlowSwitch(LB_MODE hash) | HashSwitch | IPClassifier
+// with one element: push_batch stages every packet's leading bytes (the reach
+// of the configured chain, capture.hh) into pinned memory while the packet is
+// still in the CPU cache, BATCH packets form one device batch that goes to
+// the GPU asynchronously (fcgpu_span_submit: H2D copy, kernels, D2H of the
+// results), and while it is there the next batch is staged in the other slot
+// (double buffering). A slot's results are applied when the slot is needed
+// again, on flush(), or when the TIMER fires: annotations are written into
+// the packets and one PacketBatch per output run leaves in input order
+// (CLASSIFY_EACH_PACKET, include/click/packetbatch.hh:259-307). Invalid
+// packets leave on output N when it exists, else are killed
+// (CheckIPHeader::drop, elements/ip/checkipheader.cc:143-161).
+//
+// Accumulation follows MinBatch (elements/standard/minbatch.cc:57-76): a
+// batch leaves when BATCH packets are staged or TIMER microseconds after its
+// first packet, whichever comes first (TIMER -1: only on BATCH or flush()).
+// Every packet the element receives leaves exactly once: pushed on one
+// output, or killed (GPU/runtime errors kill the batch and are reported
+// through the `error` handler -- there is no CPU fallback).
+//
+// Keyword arguments mirror the replaced elements:
+//   OFFSET, CHECKSUM (default FALSE: checkipheader.cc:110), BADSRC, GOODDST,
+//   VERBOSE, DETAILS                         -- CheckIPHeader
+//   NATIVE_VLAN (default 0)                  -- StripEtherVLANHeader
+//   VLAN_ETHERTYPE (default 0x8100)          -- VLANDecap(ETHERTYPE) + Strip(14) (MODE AUTO)
+//   MODE MARK6                               -- MarkIP6Header(OFFSET)
+//   BADADDRS, PROCESS_EH                     -- CheckIP6Header (IPv6, MODE AUTO)
+//   N / LB_MODE hash|hash_agg|hash_ip        -- FlowSwitch / LoadBalancer
+//   HASHSWITCH "OFFSET LENGTH"               -- HashSwitch
+//   PROGRAM "<program text>", PROGRAM_KIND IPFILTER|CLASSIFIER
+//                                            -- IPFilter / IPClassifier / Classifier:
+//     the compiled program as the reference's `program` handler prints it
+//     (lines separated by newlines or '|', program_text.hh); N is the
+//     classifier's output count. Packets no rule matches are killed, as
+//     CLASSIFY_EACH_PACKET kills a packet whose port is out of range.
+//   L4 UDP|TCP, L4_CHECKSUM (default true)   -- CheckUDPHeader / CheckTCPHeader
+//     behind the IPv4 check (MODE CHECK or MARK); their drops join output N
+//   COLOR (PAINT annotation on every packet)  -- IPInputCombo (with OFFSET 14,
+//     CHECKSUM true, STRIP true and no invalid output: ipinputcombo.cc:65-141)
+//   FLOW_CAPACITY n, FLOWID_ANNO o (default 28)
+//                                            -- FlowIPManagerHMP (CAPACITY) behind the
+//     checks: each checked IPv4 packet gets its flow's ID (IPFlow5ID, IDs in
+//     order of first appearance, elements/research/flowipmanagerhmp.cc:96-126)
+//     in the 4-byte annotation at FLOWID_ANNO; a new flow beyond the capacity
+//     is killed (as the IMP managers do when their flow stack is empty).
+//   DEC_TTL, TTL_MULTICAST (default true), SET_CHECKSUM
+//                                            -- DecIPTTL / SetIPChecksum after the
+//     classifier (IPv4): TTL-expired packets (DecIPTTL output 1) join output N,
+//     headers SetIPChecksum rejects are killed; the rewritten ttl/checksum
+//     bytes are written back into each packet.
+//   MODE CHECK|MARK|AUTO, HASH NONE|FLOWID|FLOW5ID, STRIP, DEVICE,
+//   BATCH (packets per device batch, default 8192; 0: each incoming
+//   PacketBatch is one), TIMER (us, default 100; -1 none),
+//   PARTITION TILE (default: each 256-packet tile classified as one batch,
+//   one fused launch) | GLOBAL (the whole device batch as one, three launches)
+// Handlers: count, drops, drop_details (DETAILS true), port_counts,
+// flow_count, flow_drops, error.
+#pragma once
+#include <inttypes.h>
+#include <arpa/inet.h>
+#include <stdio.h>
+#include <string.h>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "click_args.hh"
+#include "program_text.hh"
+#include "../capture.hh"
+#include "../../../include/fastclick_gpu.h"
+
+namespace fcx {
+
+template <class P>
+class RxCore {
+  public:
+    using Packet = typename P::Packet;
+    using Batch = typename P::Batch;
+    static constexpr uint32_t kSlots = 2;          // batches staged / in flight
+    static constexpr uint32_t kMaxBatch = 8192;    // MAX_BATCH_SIZE (packetbatch.hh:416)
+
+    RxCore() { fcgpu_default_cfg(&_cfg); }
+    ~RxCore() { release(); }
+    RxCore(const RxCore &) = delete;
+    RxCore &operator=(const RxCore &) = delete;
+
+    std::string name = "GPUIPCheckClassify";       // for chatter: the element's name
+
+    // ---- configuration (keyword arguments, "KEY value" strings) ------------
+    int configure(const std::vector<std::string> &conf, std::string &errh) {
+        fcgpu_default_cfg(&_cfg);
+        _cfg.checksum = 0;
+        bool strip_set = false;
+        for (const auto &raw : conf) {
+            ConfArg a = parse_arg(raw);
+            const std::string &k = a.key, &v = a.value;
+            long n;
+            bool b;
+            if (k == "OFFSET") {
+                if (!parse_int(v, n) || n < 0 || n > 255) return err(errh, "OFFSET expects an integer in [0,255]");
+                _cfg.offset = (int32_t)n;
+            } else if (k == "CHECKSUM") {
+                if (!parse_bool(v, b)) return err(errh, "CHECKSUM expects true/false");
+                _cfg.checksum = b;
+            } else if (k == "VERBOSE") {
+                if (!parse_bool(v, _verbose)) return err(errh, "VERBOSE expects true/false");
+            } else if (k == "DETAILS") {
+                if (!parse_bool(v, _details)) return err(errh, "DETAILS expects true/false");
+            } else if (k == "BADSRC" || k == "GOODDST") {
+                std::istringstream ss(v);
+                std::string w;
+                uint32_t *dst = k == "BADSRC" ? _cfg.badsrc : _cfg.gooddst;
+                uint32_t &cnt = k == "BADSRC" ? _cfg.nbadsrc : _cfg.ngooddst;
+                cnt = 0;
+                while (ss >> w) {
+                    uint32_t ip;
+                    if (!parse_ip4(w, ip)) return err(errh, k + " expects IP addresses");
+                    if (cnt >= FCGPU_MAX_ADDRS) return err(errh, k + ": too many addresses");
+                    dst[cnt++] = ip;
+                }
+            } else if (k == "VLAN_ETHERTYPE") {
+                // VLANDecap ETHERTYPE (vlandecap.cc:35-45): the tag protocol removed
+                if (!parse_int(v, n) || n < 0 || n > 0xFFFF) return err(errh, "bad VLAN_ETHERTYPE");
+                _cfg.vlan_ethertype = (uint32_t)n;
+            } else if (k == "NATIVE_VLAN") {
+                if (!parse_int(v, n) || n > 0xFFF) return err(errh, "bad NATIVE_VLAN");
+                _cfg.native_vlan = n >= 0 ? (int32_t)n : -1;
+            } else if (k == "N" || k == "NPORTS") {
+                if (!parse_int(v, n) || n < 1 || n > FCGPU_MAX_PORTS) return err(errh, "N out of range");
+                _cfg.nports = (uint32_t)n;
+                if (_cfg.classify == FCGPU_CLS_NONE) _cfg.classify = FCGPU_CLS_LB_HASH;
+            } else if (k == "LB_MODE") {
+                if (v == "hash" || v == "hash_agg") _cfg.classify = FCGPU_CLS_LB_HASH;
+                else if (v == "hash_ip") _cfg.classify = FCGPU_CLS_HASH_IP;
+                else return err(errh, "unsupported LB_MODE " + v);
+            } else if (k == "HASHSWITCH") {
+                long o, l;
+                std::istringstream ss(v);
+                std::string a1, a2;
+                ss >> a1 >> a2;
+                if (!parse_int(a1, o) || !parse_int(a2, l) || l <= 0 || o < 0)
+                    return err(errh, "HASHSWITCH expects OFFSET LENGTH (length must be > 0)");
+                _cfg.classify = FCGPU_CLS_HASHSWITCH;
+                _cfg.hs_offset = (int32_t)o;
+                _cfg.hs_length = (int32_t)l;
+            } else if (k == "L4") {
+                if (v == "UDP") _cfg.l4_mode = FCGPU_L4_UDP;
+                else if (v == "TCP") _cfg.l4_mode = FCGPU_L4_TCP;
+                else if (v == "NONE") _cfg.l4_mode = FCGPU_L4_NONE;
+                else return err(errh, "L4 expects UDP, TCP or NONE");
+            } else if (k == "L4_CHECKSUM") {
+                if (!parse_bool(v, b)) return err(errh, "L4_CHECKSUM expects true/false");
+                _cfg.l4_checksum = b;
+            } else if (k == "COLOR") {
+                if (!parse_int(v, n) || n < 0 || n > 255) return err(errh, "COLOR expects an integer in [0,255]");
+                _color = (int)n;
+            } else if (k == "PROGRAM") {
+                std::string text = v;
+                if (text.size() >= 2 && text.front() == '"' && text.back() == '"') text = text.substr(1, text.size() - 2);
+                std::string e = parse_program(text, _prog);
+                if (!e.empty()) return err(errh, "PROGRAM: " + e);
+                _cfg.classify = FCGPU_CLS_PROGRAM;
+            } else if (k == "PROGRAM_KIND") {
+                if (v == "IPFILTER") _prog_kind = FCGPU_PROG_IPFILTER;
+                else if (v == "CLASSIFIER") _prog_kind = FCGPU_PROG_CLASSIFIER;
+                else return err(errh, "PROGRAM_KIND expects IPFILTER or CLASSIFIER");
+            } else if (k == "MODE") {
+                if (v == "CHECK") _cfg.check_mode = FCGPU_CHECK_IP4;
+                else if (v == "MARK") _cfg.check_mode = FCGPU_MARK_IP4;
+                else if (v == "AUTO") _cfg.check_mode = FCGPU_CHECK_AUTO;
+                else if (v == "MARK6") _cfg.check_mode = FCGPU_MARK_IP6;
+                else return err(errh, "MODE expects CHECK, MARK, AUTO or MARK6");
+            } else if (k == "HASH") {
+                if (v == "NONE") _cfg.hash_mode = FCGPU_HASH_NONE;
+                else if (v == "FLOWID") _cfg.hash_mode = FCGPU_HASH_FLOWID;
+                else if (v == "FLOW5ID") _cfg.hash_mode = FCGPU_HASH_FLOW5ID;
+                else return err(errh, "HASH expects NONE, FLOWID or FLOW5ID");
+            } else if (k == "STRIP") {
+                if (!parse_bool(v, _strip)) return err(errh, "STRIP expects true/false");
+                strip_set = true;
+            } else if (k == "BATCH") {
+                if (!parse_int(v, n) || n < 0 || n > (1L << 24)) return err(errh, "bad BATCH");
+                _batch = (uint32_t)n;                  // 0: every incoming PacketBatch is one device batch
+            } else if (k == "TIMER") {
+                if (!parse_int(v, n) || n < -1 || n > 10000000) return err(errh, "TIMER expects microseconds (-1: none)");
+                _timer_us = n;
+            } else if (k == "DEVICE") {
+                if (!parse_int(v, n) || n < 0) return err(errh, "bad DEVICE");
+                _device = (int)n;
+            } else if (k == "PARTITION") {
+                if (v == "TILE") _partition = FCGPU_PART_TILE;
+                else if (v == "GLOBAL") _partition = FCGPU_PART_GLOBAL;
+                else return err(errh, "PARTITION expects TILE or GLOBAL");
+            } else if (k == "BADADDRS") {
+                // CheckIP6Header::configure (checkip6header.cc:47-87): the list
+                // adds to the default ff..ff, duplicates dropped
+                std::istringstream ss(v);
+                std::string w;
+                while (ss >> w) {
+                    uint8_t a[16];
+                    if (inet_pton(AF_INET6, w.c_str(), a) != 1) return err(errh, "BADADDRS expects IPv6 addresses");
+                    bool dup = false;
+                    for (uint32_t j = 0; j < _cfg.nbad6; ++j) dup |= memcmp(_cfg.bad6[j], a, 16) == 0;
+                    if (dup) continue;
+                    if (_cfg.nbad6 >= FCGPU_MAX_ADDRS) return err(errh, "BADADDRS: too many addresses");
+                    memcpy(_cfg.bad6[_cfg.nbad6++], a, 16);
+                }
+            } else if (k == "DEC_TTL" || k == "SET_CHECKSUM" || k == "TTL_MULTICAST") {
+                if (!parse_bool(v, b)) return err(errh, k + " expects true/false");
+                if (k == "TTL_MULTICAST") _cfg.ttl_multicast = b;
+                else {
+                    const uint32_t f = k == "DEC_TTL" ? FCGPU_RW_DECTTL : FCGPU_RW_SETCKSUM;
+                    _cfg.rewrite = b ? (_cfg.rewrite | f) : (_cfg.rewrite & ~f);
+                }
+            } else if (k == "FLOW_CAPACITY") {
+                if (!parse_int(v, n) || n < 0 || n > (long)FCGPU_MAX_FLOWS) return err(errh, "bad FLOW_CAPACITY");
+                _flow_cap = (uint32_t)n;
+            } else if (k == "FLOWID_ANNO") {
+                if (!parse_int(v, n) || n < 0 || n > P::kAnnoSize - 4) return err(errh, "bad FLOWID_ANNO");
+                _flow_anno = (int)n;
+            } else if (k == "PROCESS_EH") {
+                if (!parse_bool(v, b)) return err(errh, "PROCESS_EH expects true/false");
+                _cfg.process_eh = b;
+            } else if (k.empty()) {
+                return err(errh, "too many arguments");        // Args::complete(): OFFSET is keyword-only
+            } else {
+                return err(errh, "unknown keyword " + k);
+            }
+        }
+        if (!strip_set) _strip = (_cfg.check_mode == FCGPU_CHECK_AUTO);
+        const bool ip4 = _cfg.check_mode == FCGPU_CHECK_IP4 || _cfg.check_mode == FCGPU_MARK_IP4;
+        if (_cfg.l4_mode != FCGPU_L4_NONE && !ip4) return err(errh, "L4 needs MODE CHECK or MARK");
+        if (_flow_cap && !ip4) return err(errh, "FLOW_CAPACITY needs MODE CHECK or MARK");
+        if (_cfg.rewrite && !ip4) return err(errh, "DEC_TTL / SET_CHECKSUM need MODE CHECK or MARK");
+        if (_cfg.classify == FCGPU_CLS_PROGRAM) {
+            if (_prog.output_everything >= (int32_t)_cfg.nports && _prog.output_everything != 0x7fff)
+                return err(errh, "PROGRAM sends everything to a missing output");
+            for (const auto &st : _prog.steps)
+                if ((st.yes <= 0 && -st.yes >= (int32_t)_cfg.nports && st.yes != -2147483647) ||
+                    (st.no <= 0 && -st.no >= (int32_t)_cfg.nports && st.no != -2147483647))
+                    return err(errh, "PROGRAM jumps to an output >= N");
+        }
+        return 0;
+    }
+
+    int64_t timer_us() const { return _timer_us; }
+    uint32_t nports() const { return _cfg.nports; }
+
+    // ---- device context and staging slots ----------------------------------
+    int initialize(std::string &errh) {
+        // BATCH packets, or (BATCH 0) a whole incoming PacketBatch (16-bit count)
+        _cap = _batch ? _batch : 65536;
+        int rc = fcgpu_open(_device, _cap, &_ctx);
+        if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_open: ") + fcgpu_last_error(nullptr));
+        rc = fcgpu_configure(_ctx, &_cfg);
+        if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_configure: ") + fcgpu_last_error(_ctx));
+        uint32_t reach = 0;
+        if (_cfg.classify == FCGPU_CLS_PROGRAM) {
+            rc = fcgpu_set_program(_ctx, _prog_kind, _prog.steps.data(), (uint32_t)_prog.steps.size(),
+                                   _prog.output_everything);
+            if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_set_program: ") + fcgpu_last_error(_ctx));
+            const uint32_t l3 = (uint32_t)_cfg.offset + (_cfg.check_mode == FCGPU_CHECK_AUTO ? 18u : 0u);
+            reach = fcgpu::program_reach(_prog_kind, _prog.steps.data(), (uint32_t)_prog.steps.size(), l3, l3 + 60);
+        }
+        if (_flow_cap) {
+            rc = fcgpu_flow_enable(_ctx, _flow_cap);
+            if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_flow_enable: ") + fcgpu_last_error(_ctx));
+        }
+        _capture = fcgpu::capture_bytes(_cfg, reach);
+        const size_t per = _capture == fcgpu::kCaptureWhole ? 1536 : _capture;
+        for (Slot &s : _slot) {
+            if (!s.alloc(_cap, (size_t)_cap * per + 65536, _cfg.nports, _partition, _flow_cap != 0,
+                         _cfg.rewrite != 0))
+                return err(errh, "cannot allocate pinned staging (fcgpu_host_alloc)");
+        }
+        return 0;
+    }
+
+    // Kill whatever is still staged or in flight (router cleanup).
+    void release() {
+        for (uint32_t k = 0; k < kSlots; ++k) {
+            Slot &s = _slot[k];
+            if (s.inflight && _ctx) fcgpu_span_wait(_ctx, k);
+            s.inflight = false;
+            for (uint32_t i = 0; i < s.n; ++i) P::kill(s.pkts[i]);
+            s.n = 0;
+            s.used = 0;
+            s.free();
+        }
+        if (_ctx) fcgpu_close(_ctx);
+        _ctx = nullptr;
+    }
+
+    // ---- data path -----------------------------------------------------------
+    // A PacketBatch's packets, in order (the element owns them from here).
+    template <class Emit>
+    void push_list(Packet *p, Emit &&emit) {
+        while (p) {
+            Packet *nx = P::next(p);
+            stage(p, emit);
+            p = nx;
+        }
+        if (!_batch && _slot[_cur].n) submit(emit);      // BATCH 0: one device batch per PacketBatch
+    }
+    template <class Emit>
+    void push_one(Packet *p, Emit &&emit) {
+        stage(p, emit);
+        if (!_batch) submit(emit);
+    }
+
+    // Everything staged goes to the device and every batch in flight
+    // completes, in order.
+    template <class Emit>
+    void flush(Emit &&emit) {
+        if (_slot[_cur].n) submit(emit);
+        for (uint32_t k = 0; k < kSlots; ++k) {
+            const uint32_t j = (_cur + k) % kSlots;      // oldest first
+            if (_slot[j].inflight) complete(j, emit);
+        }
+    }
+
+    // The TIMER: batches in flight complete (they left before anything
+    // staged), and a partial batch staged at least TIMER us ago goes to the
+    // device and completes too. Returns true while packets remain staged:
+    // the caller reschedules the timer for due_ns().
+    template <class Emit>
+    bool run_timer(uint64_t now_ns, Emit &&emit) {
+        Slot &s = _slot[_cur];
+        if (s.n && now_ns >= due_ns()) {
+            flush(emit);
+            return false;
+        }
+        for (uint32_t k = 1; k < kSlots; ++k) {
+            const uint32_t j = (_cur + k) % kSlots;      // oldest first
+            if (_slot[j].inflight) complete(j, emit);
+        }
+        return s.n != 0;
+    }
+    // ns at which the staged partial batch is due (valid while staged() > 0)
+    uint64_t due_ns() const { return _slot[_cur].t_first + (uint64_t)(_timer_us < 0 ? 0 : _timer_us) * 1000ull; }
+    uint32_t staged() const { return _slot[_cur].n; }
+    uint32_t held() const {
+        uint32_t h = 0;
+        for (const Slot &s : _slot) h += s.n;
+        return h;
+    }
+    uint32_t max_held() const { return kSlots * (_cap ? _cap : (_batch ? _batch : 65536)); }
+    bool idle() const {
+        for (const Slot &s : _slot)
+            if (s.n || s.inflight) return false;
+        return true;
+    }
+
+    // ---- handlers ------------------------------------------------------------
+    // This core's counters (fcgpu_read_counters), flow IDs issued, flows dropped.
+    void counters(uint64_t (&c)[FCGPU_NCOUNTERS], uint64_t &flows, uint64_t &flow_drops) {
+        memset(c, 0, sizeof c);
+        if (_ctx) fcgpu_read_counters(_ctx, c, FCGPU_NCOUNTERS);
+        uint32_t f = 0;
+        if (_ctx && _flow_cap) fcgpu_flow_count(_ctx, &f);
+        flows = f;
+        flow_drops = _flow_drops;
+    }
+    bool details() const { return _details; }
+
+    // Handler text from (summed) counters, in the replaced elements' formats.
+    static std::string format_handler(const std::string &h, const uint64_t (&c)[FCGPU_NCOUNTERS], uint32_t nports,
+                                      bool details, uint64_t flows, uint64_t flow_drops, const std::string &error) {
+        std::ostringstream s;
+        if (h == "count") s << c[FCGPU_CTR_COUNT];
+        else if (h == "drops") s << c[FCGPU_CTR_DROPS];
+        else if (h == "drop_details" && details) {
+            char line[96];
+            for (int i = 0; i < 6; ++i) {     // checkipheader.cc:247-256 format
+                snprintf(line, sizeof line, "%15" PRIu64 " packets due to: %24s\n", c[FCGPU_CTR_REASON + i],
+                         kReasonTexts[i]);
+                s << line;
+            }
+        } else if (h == "port_counts") {
+            for (uint32_t p = 0; p <= nports; ++p) s << (p ? " " : "") << c[FCGPU_CTR_PORT + p];
+        } else if (h == "flow_count") s << flows;
+        else if (h == "flow_drops") s << flow_drops;
+        else if (h == "error") s << error;
+        return s.str();
+    }
+    std::string read_handler(const std::string &h) {
+        uint64_t c[FCGPU_NCOUNTERS];
+        uint64_t flows, drops;
+        counters(c, flows, drops);
+        return format_handler(h, c, _cfg.nports, _details, flows, drops, _error);
+    }
+    const std::string &error() const { return _error; }
+
+    // CheckIPHeader::reason_texts (elements/ip/checkipheader.cc:35-38)
+    static constexpr const char *kReasonTexts[6] = {"tiny packet", "bad IPv4 version", "bad IPv4 header length",
+                                                    "bad IPv4 length", "bad IPv4 checksum", "bad source address"};
+
+  private:
+    // One device batch: the staged bytes and descriptors (pinned, so the H2D
+    // copy is DMA), the packets, and the pinned result arrays the D2H copies
+    // land in.
+    struct Slot {
+        uint8_t *span = nullptr;
+        size_t span_cap = 0, used = 0;
+        uint32_t *desc = nullptr;
+        std::vector<Packet *> pkts;
+        uint32_t n = 0;
+        bool inflight = false;
+        bool holes = false;        // a packet freed while its results were applied
+        uint64_t t_first = 0;
+        uint16_t *verdict = nullptr, *tile_count = nullptr;
+        uint32_t *hash = nullptr, *perm = nullptr, *start = nullptr, *flowid = nullptr, *iprw = nullptr;
+        fcgpu_anno *anno = nullptr;
+        uint8_t *tperm = nullptr;
+        std::vector<uint32_t> keep;
+
+        template <class T>
+        static bool get(T *&p, size_t count) {
+            p = static_cast<T *>(fcgpu_host_alloc(sizeof(T) * (count ? count : 1)));
+            return p != nullptr;
+        }
+        bool alloc(uint32_t cap, size_t span_bytes, uint32_t nports, uint32_t part, bool flow, bool rw) {
+            pkts.resize(cap);
+            keep.resize(cap);
+            span_cap = span_bytes;
+            const size_t tiles = (cap + FCGPU_TILE - 1) / FCGPU_TILE;
+            bool ok = get(span, span_cap) && get(desc, 2 * (size_t)cap) && get(verdict, cap) && get(hash, cap) &&
+                      get(anno, cap);
+            if (part == FCGPU_PART_TILE) ok = ok && get(tperm, cap + FCGPU_TILE) && get(tile_count, (nports + 1) * tiles);
+            else ok = ok && get(perm, cap) && get(start, FCGPU_MAX_PORTS + 2);
+            if (flow) ok = ok && get(flowid, cap);
+            if (rw) ok = ok && get(iprw, cap);
+            return ok;
+        }
+        void free() {
+            for (void *p : {(void *)span, (void *)desc, (void *)verdict, (void *)tile_count, (void *)hash, (void *)perm,
+                            (void *)start, (void *)flowid, (void *)iprw, (void *)anno, (void *)tperm})
+                fcgpu_host_free(p);
+            span = nullptr;
+            desc = nullptr;
+            verdict = tile_count = nullptr;
+            hash = perm = start = flowid = iprw = nullptr;
+            anno = nullptr;
+            tperm = nullptr;
+        }
+    };
+
+    int err(std::string &errh, const std::string &m) {
+        errh = name + ": " + m;
+        return -1;
+    }
+
+    // Copy the packet's leading bytes into the current slot (64-B aligned
+    // records), remember the packet; a full slot goes to the device.
+    template <class Emit>
+    inline void stage(Packet *p, Emit &emit) {
+        Slot *s = &_slot[_cur];
+        const uint32_t len = P::length(p);
+        const uint32_t cp = len < _capture ? len : _capture;
+        const size_t rec = cp ? ((size_t)cp + 63) & ~(size_t)63 : 64;
+        if (s->n && s->used + rec > s->span_cap) {       // whole frames overflowing the span
+            submit(emit);
+            s = &_slot[_cur];
+        }
+        if (s->n == 0) {
+            if (!_ctx) {                                 // not initialized / released
+                P::kill(p);
+                return;
+            }
+            s->t_first = _timer_us >= 0 ? P::now_ns() : 0;
+        }
+        uint8_t *dst = s->span + s->used;
+        const uint8_t *src = P::data(p);
+        if (cp == 128 || (cp > 64 && cp <= 128)) {
+            memcpy(dst, src, 64);
+            memcpy(dst + 64, src + 64, cp - 64);
+        } else if (cp == 64) {
+            memcpy(dst, src, 64);
+        } else {
+            memcpy(dst, src, cp);
+        }
+        s->desc[2 * s->n] = (uint32_t)s->used;
+        s->desc[2 * s->n + 1] = len;
+        s->pkts[s->n++] = p;
+        s->used += rec;
+        if (s->n == _cap || (_batch && s->n >= _batch)) submit(emit);
+    }
+
+    // The current slot goes to the device (asynchronous); the next slot is
+    // made free, completing the batch in it first if it is still in flight.
+    template <class Emit>
+    void submit(Emit &emit) {
+        const uint32_t k = _cur;
+        Slot &s = _slot[k];
+        fcgpu_out o{};
+        o.verdict = s.verdict;
+        o.hash = s.hash;
+        o.anno = s.anno;
+        o.partition = _partition;
+        if (_partition == FCGPU_PART_TILE) {
+            o.tile_perm = s.tperm;
+            o.tile_count = s.tile_count;
+        } else {
+            o.perm = s.perm;
+            o.port_start = s.start;
+        }
+        o.flowid = s.flowid;
+        o.ip_rw = s.iprw;
+        const int rc = fcgpu_span_submit(_ctx, k, s.span, s.used, s.desc, s.n, &o);
+        if (rc != FCGPU_OK) {
+            fail_slot(s, fcgpu_last_error(_ctx));
+        } else {
+            s.inflight = true;
+        }
+        _cur = (_cur + 1) % kSlots;
+        if (_slot[_cur].inflight) complete(_cur, emit);
+    }
+
+    void fail_slot(Slot &s, const char *msg) {
+        // no CPU fallback: report, drop the batch, keep running
+        _error = msg ? msg : "GPU processing failed";
+        P::chatter(name + ": GPU processing failed: " + _error);
+        for (uint32_t i = 0; i < s.n; ++i) P::kill(s.pkts[i]);
+        s.n = 0;
+        s.used = 0;
+        s.inflight = false;
+    }
+
+    // The first drop's chatter, as the replaced checker prints it
+    // (checkipheader.cc:146, checkip6header.cc:93, checkudpheader.cc:77,
+    // checktcpheader.cc:78).
+    void drop_chatter(uint32_t reason) {
+        if (_warned && !_verbose) return;
+        _warned = true;
+        std::string m;
+        if (reason < 6) m = name + ": IP header check failed: " + kReasonTexts[reason];
+        else if (reason == FCGPU_R_BAD_IP6) m = "IP6 header check failed";
+        else if (reason >= FCGPU_R_L4_PROTO && reason <= FCGPU_R_L4_CKSUM) {
+            static const char *const udp[3] = {"not UDP", "bad packet length", "bad UDP checksum"};
+            static const char *const tcp[3] = {"not TCP", "bad packet length", "bad TCP checksum"};
+            const uint32_t r = reason - FCGPU_R_L4_PROTO;
+            m = _cfg.l4_mode == FCGPU_L4_UDP ? std::string("UDP header check failed: ") + udp[r]
+                                             : name + ": TCP header check failed: " + tcp[r];
+        } else {
+            return;    // VLAN reject, TTL expiry: the replaced elements print nothing
+        }
+        P::chatter(m);
+    }
+
+    // Results of slot k back into its packets, then its output runs leave.
+    template <class Emit>
+    void complete(uint32_t k, Emit &emit) {
+        Slot &s = _slot[k];
+        const int rc = fcgpu_span_wait(_ctx, k);
+        s.inflight = false;
+        if (rc != FCGPU_OK) {
+            fail_slot(s, fcgpu_last_error(_ctx));
+            return;
+        }
+        const uint32_t n = s.n;
+        s.holes = false;
+        const bool hashing = _cfg.hash_mode != FCGPU_HASH_NONE;
+        const bool autom = _cfg.check_mode == FCGPU_CHECK_AUTO;
+        for (uint32_t i = 0; i < n; ++i) {
+            Packet *p = s.pkts[i];
+            const fcgpu_anno &a = s.anno[i];
+            const uint32_t reason = s.verdict[i] & 0xff;
+            if (_color >= 0) P::set_anno_u8(p, P::kPaint, (uint8_t)_color);     // SET_PAINT_ANNO
+            if (autom && reason != FCGPU_R_VLAN_REJECT)
+                P::set_anno_u16(p, P::kVlanTci, a.vlan_tci);                     // StripEtherVLANHeader
+            if (reason == FCGPU_R_OK || reason >= FCGPU_R_NO_MATCH) {
+                if (s.iprw && s.iprw[i]) {                                       // DecIPTTL / SetIPChecksum
+                    Packet *q = P::write_bytes(p, a.nh + 8u, &s.iprw[i], 4);
+                    if (!q) {                                                    // uniqueify failed: freed
+                        s.pkts[i] = nullptr;
+                        s.holes = true;
+                        continue;
+                    }
+                    s.pkts[i] = p = q;
+                }
+                P::set_headers(p, a.nh, a.th);                                   // set_ip_header / set_ip6_header
+                if (a.length < P::length(p)) P::take(p, P::length(p) - a.length);
+                if (a.ipver == 6) P::set_anno_u8(p, P::kIp6Nxt, a.ip6_nxt);
+                else P::set_anno_u32(p, P::kDstIp, a.dst_ip);
+                if (hashing && reason <= FCGPU_R_NO_MATCH)                       // AggregateHash (not after an L4 drop)
+                    P::set_anno_u32(p, P::kAggregate, s.hash[i]);
+                if (s.flowid && s.flowid[i] != FCGPU_FLOW_NONE && s.flowid[i] != FCGPU_FLOW_FULL)
+                    P::set_anno_u32(p, _flow_anno, s.flowid[i]);
+                if (_strip) P::pull(p, a.nh);
+                if (reason > FCGPU_R_NO_MATCH) drop_chatter(reason);
+            } else {
+                drop_chatter(reason);
+                // the replaced Strip / StripEtherVLANHeader ran before the checker
+                if (_strip && reason != FCGPU_R_VLAN_REJECT) P::pull(p, autom ? a.nh : (uint32_t)_cfg.offset);
+            }
+        }
+        const uint32_t nb = _cfg.nports + 1;
+        if (_partition == FCGPU_PART_GLOBAL) {
+            // one batch per output in port order, input order within a port
+            for (uint32_t port = 0; port < nb; ++port)
+                emit_run(s, port, s.start[port], s.start[port + 1], [&s](uint32_t j) { return s.perm[j]; }, emit);
+        } else {
+            // every FCGPU_TILE-packet tile is one classified PacketBatch: its
+            // runs leave in port order, tiles in input order
+            const uint32_t ntiles = (n + FCGPU_TILE - 1) / FCGPU_TILE;
+            for (uint32_t t = 0; t < ntiles; ++t) {
+                const uint32_t base = t * FCGPU_TILE;
+                uint32_t b = base;
+                auto idx = [&s, base](uint32_t j) { return base + s.tperm[j]; };
+                const uint16_t *tc = s.tile_count + (size_t)t * nb;
+                for (uint32_t port = 0; port < nb; ++port) {
+                    const uint32_t c = tc[port];
+                    if (c) emit_run(s, port, b, b + c, idx, emit);
+                    b += c;
+                }
+            }
+        }
+        s.n = 0;
+        s.used = 0;
+    }
+
+    // link the packets idx(b) .. idx(e-1) into PacketBatches of <= kMaxBatch
+    template <class Idx, class Emit>
+    void emit_run(Slot &s, uint32_t port, uint32_t b, uint32_t e, Idx idx, Emit &emit) {
+        const bool nomatch = port == _cfg.nports && _cfg.classify == FCGPU_CLS_PROGRAM;
+        const bool last = port == _cfg.nports;
+        if (nomatch || (last && _cfg.rewrite) || s.flowid || s.holes) {
+            // the last list mixes invalid packets (output N) and packets no
+            // rule matched or SetIPChecksum rejected (killed); a full flow
+            // table kills new flows. The rest keep input order.
+            uint32_t w = 0;
+            for (uint32_t j = b; j < e; ++j) {
+                const uint32_t i = idx(j);
+                Packet *p = s.pkts[i];
+                const uint32_t r = s.verdict[i] & 0xff;
+                if (!p) continue;                                     // freed by a failed uniqueify
+                if ((nomatch && r == FCGPU_R_NO_MATCH) || (last && r == FCGPU_R_SETCKSUM_BAD)) {
+                    P::kill(p);
+                } else if (s.flowid && s.flowid[i] == FCGPU_FLOW_FULL) {
+                    ++_flow_drops;
+                    P::kill(p);
+                } else {
+                    s.keep[w++] = i;
+                }
+            }
+            for (uint32_t a = 0; a < w;) {
+                const uint32_t k = w - a < kMaxBatch ? w - a : kMaxBatch;
+                Packet *head = s.pkts[s.keep[a]], *prev = head;
+                for (uint32_t j = 1; j < k; ++j) {
+                    Packet *q = s.pkts[s.keep[a + j]];
+                    P::set_next(prev, q);
+                    prev = q;
+                }
+                emit((int)port, P::make_batch(head, prev, k));
+                a += k;
+            }
+            return;
+        }
+        while (b < e) {
+            const uint32_t m = e - b < kMaxBatch ? e - b : kMaxBatch;
+            Packet *head = s.pkts[idx(b)], *prev = head;
+            for (uint32_t j = 1; j < m; ++j) {
+                Packet *q = s.pkts[idx(b + j)];
+                P::set_next(prev, q);
+                prev = q;
+            }
+            emit((int)port, P::make_batch(head, prev, m));
+            b += m;
+        }
+    }
+
+    fcgpu_cfg _cfg;
+    fcgpu_ctx *_ctx = nullptr;
+    ParsedProgram _prog;
+    uint32_t _prog_kind = FCGPU_PROG_IPFILTER;
+    int _color = -1;
+    uint32_t _flow_cap = 0;
+    int _flow_anno = 28;
+    uint64_t _flow_drops = 0;
+    int _device = 0;
+    uint32_t _batch = 8192;
+    int64_t _timer_us = 100;
+    uint32_t _cap = 0;
+    uint32_t _capture = fcgpu::kCaptureMin;
+    uint32_t _partition = FCGPU_PART_TILE;
+    bool _verbose = false, _details = false, _strip = false, _warned = false;
+    std::string _error;
+    Slot _slot[kSlots];
+    uint32_t _cur = 0;
+};
+
+}  // namespace fcx

@@ -376,9 +376,11 @@ int  fcgpu_counters_device(fcgpu_ctx *ctx, uint64_t **d_counters);
 int  fcgpu_use_counters(fcgpu_ctx *ctx, uint64_t *d_counters);
 
 /* Per-kernel timing with HIP events on the launch stream (off by default).
- * fcgpu_set_timing(ctx, k): k > 0 brackets every k-th launch of the context
- * (1 = every launch) with start/stop events recorded by the launch itself;
- * the events are created by this call, not on the launch path. 0 = off.
+ * fcgpu_set_timing(ctx, k): k > 0 brackets the k-th, 2k-th, ... launch of the
+ * context after this call (1 = every launch) with start/stop events recorded
+ * by the launch itself; the events are created by this call, not on the
+ * launch path. 0 = off. (Each recorded event idles the queue for a few us,
+ * so sparse sampling keeps the measured region representative.)
  * fcgpu_read_timing returns, per stage (0 = fused check/hash/classify,
  * 1 = count scan, 2 = partition scatter), the summed milliseconds and launches
  * since the last read, and resets them. Synchronises the context stream. */

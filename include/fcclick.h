@@ -48,6 +48,8 @@ typedef struct fcclick_result {
     uint32_t *out_flow;     /* [n] anno u32 @28 (FLOWID_ANNO default) on departure (may be NULL) */
     uint32_t *out_ip8;      /* [n] network header bytes 8..11 (ttl, proto, checksum) on
                                departure, little-endian (may be NULL)                  */
+    uint32_t *out_parked;   /* [1] FCCLICK_TIMER_FLUSH: packets the element still held when
+                               the source stopped (may be NULL)                          */
 } fcclick_result;
 
 /* burst value for a non-batch upstream: the source calls the element's
@@ -63,11 +65,27 @@ typedef struct fcclick_result {
 int fcclick_run(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
                 uint32_t burst, uint32_t nsinks, fcclick_result *res, char *err, size_t errcap);
 
-/* Host-resident rate: repeat the same run `reps` times (packets recycled into
- * the pool, sinks discard), return packets per second through the element
+/* fcclick_run with flags: FCCLICK_TIMER_FLUSH ends the run by firing the
+ * element's timer (run_timer at the current time, repeated while it asks to
+ * be rescheduled) instead of calling flush(): what a graph whose source has
+ * gone quiet relies on to release the last partial batch. */
+#define FCCLICK_TIMER_FLUSH 1u
+int fcclick_run_ex(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                   uint32_t burst, uint32_t nsinks, uint32_t flags, fcclick_result *res, char *err,
+                   size_t errcap);
+
+/* Host-resident rate: repeat the same run `reps` times (packets recycled
+ * LIFO into a mempool sized to what the element can hold, sinks discard), return packets per second through the element
  * including gather, PCIe copies, kernels and relinking. */
 int fcclick_bench(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
                   uint32_t burst, uint32_t reps, double *pps, char *err, size_t errcap);
+
+/* The same with `threads` element instances, one per thread (each with its
+ * own GPU context and packet pool, as Click threads with their own rx queue
+ * would be); *pps = the sum of the threads' rates. */
+int fcclick_bench_threads(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                          uint32_t burst, uint32_t reps, uint32_t threads, double *pps, char *err,
+                          size_t errcap);
 
 #ifdef __cplusplus
 }

@@ -121,13 +121,18 @@ def main():
         out[f"process_host_mpps_1M_tile_t{threads}"] = round(raw_host(1 << 20, threads, tile=True), 2)
         out[f"process_host_mpps_1M_tile_t{threads}_pinned"] = round(
             raw_host(1 << 20, threads, tile=True, pinned=True), 2)
-    b = synth.c2(1 << 20)
-    for batch in (4096, 65536, 262144):
-        conf = f"GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BATCH {batch})"
-        out[f"element_mpps_batch{batch}"] = round(K.bench_element(conf, b, burst=32, reps=3) / 1e6, 2)
-    conf = "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BATCH 65536)"
-    out["element_mpps_batch65536_per_packet_push"] = round(
-        K.bench_element(conf, b, burst=K.PER_PACKET, reps=3) / 1e6, 2)
+    # the element behind a BURST-32 source: a 64K-packet C2 trace replayed
+    # through a mempool-sized packet pool (fcclick_bench), single flow as the
+    # C2-chain CPU baseline
+    b = synth.c2(1 << 16)
+    base = "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BATCH {})"
+    for batch in (4096, 8192, 16384, 65536):
+        out[f"element_mpps_batch{batch}"] = round(K.bench_element(base.format(batch), b, burst=32, reps=40) / 1e6, 2)
+    for t in (2, 4, 8):
+        out[f"element_mpps_batch8192_threads{t}"] = round(
+            K.bench_element(base.format(8192), b, burst=32, reps=40, threads=t) / 1e6, 2)
+    out["element_mpps_batch8192_per_packet_push"] = round(
+        K.bench_element(base.format(8192), b, burst=K.PER_PACKET, reps=20) / 1e6, 2)
     print(json.dumps(out))
 
 

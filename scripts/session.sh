@@ -36,9 +36,24 @@ for s in "${ST[@]}"; do
     kt_drv) kt kt_drv 300 $DRV --no-cpu ;;
     kt_drv_s1) kt kt_drv_s1 300 $DRV --no-cpu --streams 1 ;;
     kt_long) kt kt_long 300 --steps 200 --warmup 20 --no-cpu ;;
+    kt_w40) kt kt_w40 300 --gpus 1 --steps 20 --warmup 40 --no-cpu ;;
+    kt_w40_s1) kt kt_w40_s1 300 --gpus 1 --steps 20 --warmup 40 --no-cpu --streams 1 ;;
+    bench2) step bench2 300 python bench.py $DRV --no-cpu ;;
+    bench3) step bench3 300 python bench.py $DRV --no-cpu ;;
     pmc) pmc pmc_fetch FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1
          pmc pmc_write WRITE_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1
          pmc pmc_ea TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1 ;;
+    pmc_var) pmc pmc_fetch_fb128 FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1 --frame-bytes 128
+             pmc pmc_fetch_fb1500 FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1 --frame-bytes 1500
+             pmc pmc_fetch_c3 FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1 --workload c3
+             pmc pmc_fetch_c4flow FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --workload c4 --flow-capacity 2000000
+             pmc pmc_ea_c4flow TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum -- --steps 40 --warmup 4 --no-cpu --no-timing --workload c4 --flow-capacity 2000000
+             pmc pmc_write_c4flow WRITE_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --workload c4 --flow-capacity 2000000 ;;
+    flowvar) for v in "--flow-capacity 1" "--workload c3 --flow-capacity 20000" "--workload c4 --flow-capacity 2000000" \
+                      "--partition global" "--classify ipclass16" "--workload c4 --classify ipclass16"; do
+                n=$(echo "$v" | tr -d ' -' | cut -c1-40)
+                step "var_$n" 300 python bench.py --steps 200 --warmup 20 --no-cpu $v
+              done ;;
     sweep) for fb in 64 128 256 512 1024 1500; do
              step "sweep_$fb" 300 python bench.py --steps 200 --warmup 20 --no-cpu --frame-bytes $fb
              step "sweep_s1_$fb" 300 python bench.py --steps 200 --warmup 20 --no-cpu --frame-bytes $fb --streams 1

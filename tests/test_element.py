@@ -249,3 +249,37 @@ def test_element_dec_ttl_golden():
         assert np.array_equal(r["ip8"][ok], g[key][ok]), key
         if key != "decset":
             assert (r["port"][g[key + "_expired"]] == 2).all(), key
+
+
+@pytest.mark.gpu
+def test_element_timer_releases_tail(oracle):
+    """A partial batch (fewer packets than BATCH) is released by the TIMER
+    once the source goes quiet -- MinBatch's timer (minbatch.cc:35,57-76) --
+    with the same outputs flush() gives; with TIMER -1 nothing releases it."""
+    from fastclick_amd import click as K
+    b = synth.c4(3_000, seed=510)
+    synth.inject_errors(b, 0.03, seed=511)
+    conf = CONF[:-1] + ", BATCH 100000, TIMER 200)"
+    r = K.run_element(conf, b, burst=32, nsinks=17, timer_flush=True)
+    assert r["parked"] == b.n                      # all parked when the source stopped
+    ref = K.run_element(conf, b, burst=32, nsinks=17)
+    for k in ("port", "seq", "agg", "len"):
+        assert np.array_equal(r[k], ref[k]), k
+    e = expected(b, _cfg_for_conf(), oracle)
+    assert np.array_equal(r["port"], e["port"].astype(np.uint32))
+    r2 = K.run_element(CONF[:-1] + ", BATCH 100000, TIMER -1)", b, burst=32, nsinks=17, timer_flush=True)
+    assert r2["parked"] == b.n and (r2["port"] == 0xFFFFFFFF).all()
+
+
+@pytest.mark.gpu
+def test_element_drop_chatter_text(capfd):
+    """The first drop prints CheckIPHeader's message with the reason text
+    (checkipheader.cc:146: "%s: IP header check failed: %s")."""
+    from fastclick_amd import click as K
+    b = synth.c2(600)
+    o = int(b.desc[5, 0]) + 14
+    b.arena[o + 10] ^= 0x40                        # packet 5: bad checksum, the first drop
+    K.run_element(CONF, b, burst=32, nsinks=17)
+    err = capfd.readouterr().err
+    assert "GPUIPCheckClassify: IP header check failed: bad IPv4 checksum" in err
+    assert err.count("IP header check failed") == 1      # once, not VERBOSE

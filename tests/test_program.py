@@ -299,3 +299,61 @@ def test_gpu_reference_test_programs(dev):
 def test_gpu_reference_short_packet_cases(dev):
     for part in (N.PART_GLOBAL, N.PART_TILE):
         _run_short_cases(lambda cfg, b, prog: dev.process_batch(b, cfg, partition=part, program=prog))
+
+
+def chain_program(rng, nout, nsteps):
+    """Programs shaped like the reference's compilation of port-range rules:
+    mostly runs of mask tests on one transport/network word (contiguous bit
+    ranges of the big-endian word, some wider than a jump table takes), mixed
+    with tests on other words, forward jumps, outputs, [X] and short->yes.
+    fcgpu_set_program turns the runs into jump tables; the oracle walks the
+    steps as given."""
+    steps = []
+    for k in range(nsteps):
+        o = int(rng.choice([512, 512, 512, 516, 264, 260, 268]))
+        width = int(rng.integers(1, 13))
+        lo = int(rng.integers(0, 33 - width))
+        m_be = ((1 << width) - 1) << lo
+        mask = int.from_bytes(m_be.to_bytes(4, "big"), "little")
+        value = int(rng.integers(0, 1 << 32)) & mask
+
+        def jump():
+            r = rng.random()
+            if r < 0.6 and k + 1 < nsteps:
+                return int(rng.integers(k + 1, min(nsteps, k + 6)))
+            if r < 0.9:
+                return -int(rng.integers(0, nout))
+            return -2147483647
+        steps.append((o, value, mask, jump(), jump(), int(rng.random() < 0.3)))
+    return steps
+
+
+@pytest.mark.gpu
+def test_gpu_chain_programs_tables_vs_oracle(dev, oracle):
+    """Jump-table steps (runs on one word) give the oracle's outputs, including
+    packets whose tested word is cut short (the table step then falls back to
+    the original steps' length-checked rules)."""
+    rng = np.random.default_rng(4242)
+    b = synth.c4(30_000, seed=44)
+    # ~15 % datagrams with 0..7 transport bytes: ip_len, frame length, checksum
+    A = b.arena
+    for i in np.nonzero(rng.random(b.n) < 0.15)[0]:
+        k = int(rng.integers(0, 8))
+        o = int(b.desc[i, 0]) + 14
+        L = 20 + k
+        A[o + 2], A[o + 3] = L >> 8, L & 0xFF
+        b.desc[i, 1] = 14 + L
+        synth._refresh_cksum(A, o)
+    synth.inject_errors(b, 0.01, seed=45)
+    outcomes = set()
+    for trial in range(8):
+        nout = int(rng.integers(2, 20))
+        nsteps = int(rng.integers(3, 60 if trial < 6 else 400))
+        prog = (N.PROG_IPFILTER, chain_program(rng, nout, nsteps), -1)
+        cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_PROGRAM, nports=nout)
+        exp = oracle.process_batch(cfg, b, program=prog)
+        got = dev.process_batch(b, cfg, partition=N.PART_TILE, program=prog)
+        compare(got, exp, ctx=f"chain trial={trial}")
+        assert np.array_equal(got["counters"], exp["counters"])
+        outcomes |= set(np.unique(exp["port"]).tolist())
+    assert len(outcomes) > 5
