@@ -195,6 +195,7 @@ struct fcgpu_ctx {
     FlowArgs fl{};            // device pointers; fl.slots == nullptr: disabled
     uint32_t *flow_hint = nullptr;    // mapped: size class of the last finish's misses (kHint*)
     uint32_t flow_epoch = 0;          // batches through the table (FlowArgs::epoch)
+    hipEvent_t flow_order[2] = {nullptr, nullptr};   // orders fcgpu_process against span submissions
     // timing: every timing_every-th launch is bracketed by events (0 = off)
     uint32_t timing_every = 0;
     uint64_t timing_seq = 0;
@@ -565,6 +566,8 @@ int fcgpu_flow_enable(fcgpu_ctx *c, uint32_t max_flows) {
     HIPCHK(c, hipMalloc(&F.wordpre, sizeof(uint32_t) * words));
     HIPCHK(c, hipMalloc(&F.state, sizeof(uint32_t) * 16));
     HIPCHK(c, hipHostMalloc((void **)&c->flow_hint, sizeof(uint32_t), hipHostMallocMapped));
+    for (auto &e : c->flow_order)
+        if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(c, hipHostGetDevicePointer((void **)&F.host_hint, c->flow_hint, 0));
     F.mask = slots - 1;
     F.max_flows = max_flows;
@@ -624,6 +627,8 @@ void fcgpu_close(fcgpu_ctx *c) {
             if (sp.own) hipStreamDestroy(sp.own);
         }
         flow_free(c);
+        for (auto e : c->flow_order)
+            if (e) hipEventDestroy(e);
         hipHostFree(c->h_arena);
         hipHostFree(c->h_desc);
         if (c->stream) hipStreamDestroy(c->stream);
@@ -795,6 +800,14 @@ static int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_d
     if (timed)
         for (int k = 0; k < 3; ++k) { ev[k].a = take_event(c); ev[k].b = take_event(c); ev[k].stage = k; }
 
+    // the flow table's per-batch scratch is shared by every stream the
+    // context launches on: a batch on another stream than the one the span
+    // submissions use waits for that stream, and that stream for it
+    const bool cross = a.fl.slots && c->stream && s != c->stream;
+    if (cross) {
+        HIPCHK(c, hipEventRecord(c->flow_order[0], c->stream));
+        HIPCHK(c, hipStreamWaitEvent(s, c->flow_order[0], 0));
+    }
     launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, a, s, timed ? ev[0].a : nullptr,
                   timed ? ev[0].b : nullptr);
     HIPCHK(c, hipGetLastError());
@@ -810,6 +823,10 @@ static int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_d
             hipLaunchKernelGGL(k_flow_finish, dim3(1), dim3(kFinishBlock), 0, s, a.fl, nw);
         }
         HIPCHK(c, hipGetLastError());
+        if (cross) {
+            HIPCHK(c, hipEventRecord(c->flow_order[1], s));
+            HIPCHK(c, hipStreamWaitEvent(c->stream, c->flow_order[1], 0));
+        }
     }
     if (want_global) {
         if (timed) hipEventRecord(ev[1].a, s);

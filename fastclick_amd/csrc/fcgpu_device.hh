@@ -805,14 +805,17 @@ __device__ __forceinline__ uint32_t flow_tag_id(uint32_t tag) {
     return (tag >> 8) == kTagFull ? FCGPU_FLOW_FULL : (tag >> 8) - 1u;
 }
 // IPFlow5ID(p) (lib/ipflowid.cc:29-46,91-94): saddr, daddr, the first L4 word
-// (sport, dport; 0 for non-first fragments), ip_p.
+// (sport, dport), ip_p. A non-first fragment returns before assign(): its
+// addresses stay 0 (IPAddress(), ipaddress.hh:21-22) and its ports unset
+// (defined as 0), so it keys on ip_p alone.
 __device__ __forceinline__ uint4 flow_key(const FrameView &f, const fcgpu_anno &an) {
     uint4 k;
-    k.x = f.rd32(an.nh + 12);
-    k.y = f.rd32(an.nh + 16);
     const uint32_t w1 = f.rd32(an.nh + 4);          // id, frag offset
     const uint32_t w2 = f.rd32(an.nh + 8);          // ttl, proto, sum
-    k.z = (bswap16(w1 >> 16) & 0x1fff) == 0 ? f.rd32(an.th) : 0u;
+    const bool first = (bswap16(w1 >> 16) & 0x1fff) == 0;
+    k.x = first ? f.rd32(an.nh + 12) : 0u;
+    k.y = first ? f.rd32(an.nh + 16) : 0u;
+    k.z = first ? f.rd32(an.th) : 0u;
     k.w = (w2 >> 8) & 0xffu;
     return k;
 }
@@ -1066,9 +1069,9 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d,
             const uint32_t s64 = __shfl(incl, 63) + w64;
             if (bin == 64) mine = s64;
         }
-        // stage the tile's permutation in LDS, then write it out coalesced
-        // (a full tile: 4 x 256 B of perm, one dword per lane of wave 0 for
-        // tile_perm) instead of one scattered store per packet
+        // each lane stores its own permutation entry (scattered within the
+        // tile's 256-entry run; staging the run in LDS for coalesced stores
+        // measured 1 % slower, profiles/r01_kernel_experiments)
         if (live) {
             const size_t pos = (size_t)tile * kTile + mine + rank;
             if (A.perm) A.perm[pos] = i;

@@ -328,11 +328,15 @@ int  fcgpu_set_program(fcgpu_ctx *ctx, uint32_t kind, const fcgpu_step *steps, u
  * (saddr, daddr, sport, dport, proto) flow; a flow seen for the first time gets
  * the next ID (0, 1, 2, ... in packet order, persistent across batches: the
  * `_current.fetch_and_add(1)` of flowipmanagerhmp.cc:99-102 on one thread).
- * Non-first fragments use ports 0 (the reference leaves them uninitialised,
- * lib/ipflowid.cc:34-38). IPv4 check modes only.
+ * Non-first fragments key on ip_p alone: IPFlowID(p) returns before
+ * assign() for them (lib/ipflowid.cc:34-38), so their addresses stay 0 and
+ * their ports unset (defined as 0 here). IPv4 check modes only.
  *   max_flows: IDs 0 .. max_flows-1 (the table holds 2x that many slots, up to
  *     2^23 flows); a packet of a new flow beyond that gets FCGPU_FLOW_FULL (the
  *     manager kills it, virtualflowmanager.hh:262-266). 0 disables the table.
+ * Batches are assigned IDs in the order the context receives them; a
+ * fcgpu_process on a caller's stream is ordered after (and before) the
+ * context's own span submissions, so mixing the two entry points is safe.
  * Each fcgpu_process with flow enabled adds a pass over the batch's new flows
  * after the receive kernel (one launch, three after a batch with many new
  * flows); fcgpu_process_host processes the batch in order on one stream.

@@ -593,11 +593,16 @@ void fco_flow_batch(fco_flowtab *t, const uint8_t *arena, const uint32_t *desc, 
             continue;
         const uint8_t *nh = arena + desc[2 * i] + anno[i].nh;
         const uint8_t *th = arena + desc[2 * i] + anno[i].th;
-        uint32_t s, d, p = 0, pr = nh[9];
-        memcpy(&s, nh + 12, 4);
-        memcpy(&d, nh + 16, 4);
-        if (((((uint32_t)nh[6] << 8) | nh[7]) & 0x1fff) == 0)   /* IP_FIRSTFRAG */
+        /* IPFlow5ID(p) (lib/ipflowid.cc:29-46, :91-94): a non-first fragment
+         * returns before assign(), so its addresses stay IPAddress() = 0
+         * (ipaddress.hh:21-22) and its ports unset (defined here as 0);
+         * only ip_p is filled in */
+        uint32_t s = 0, d = 0, p = 0, pr = nh[9];
+        if (((((uint32_t)nh[6] << 8) | nh[7]) & 0x1fff) == 0) {   /* IP_FIRSTFRAG */
+            memcpy(&s, nh + 12, 4);
+            memcpy(&d, nh + 16, 4);
             memcpy(&p, th, 4);
+        }
         if (2 * (t->n + 1) > t->cap) fco_flow_grow(t);
         fco_flow_ent *e = fco_flow_slot(t, s, d, p, pr);
         if (!e->used) {

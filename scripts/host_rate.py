@@ -115,8 +115,8 @@ def main():
     out["pcap_ingress_mpps_4M_mapped"] = round(m, 2)
     out["pcap_mapped_registered"] = bool(reg)
     out["process_host_mpps_1M_global"] = round(raw_host(1 << 20), 2)
-    chunk = os.environ.get("FCGPU_HOST_CHUNK", "65536")
-    out["chunk"] = int(chunk)
+    # fcgpu_process_host's pipeline chunk (kChunk in fcgpu_api.hip, overridable)
+    out["chunk"] = int(os.environ.get("FCGPU_HOST_CHUNK", "131072"))
     for threads in (1, 4, 8):
         out[f"process_host_mpps_1M_tile_t{threads}"] = round(raw_host(1 << 20, threads, tile=True), 2)
         out[f"process_host_mpps_1M_tile_t{threads}_pinned"] = round(

@@ -211,3 +211,33 @@ def test_gpu_flow_finish_paths(oracle, max_flows):
         o = exp[sum(x.n for x in bs[:j]):][:b.n]
         assert np.array_equal(r["flowid"], o), f"batch {j}: {np.count_nonzero(r['flowid'] != o)} IDs differ"
     assert cnt == ecnt
+
+
+def test_oracle_nonfirst_fragments_key_on_proto(oracle):
+    """IPFlow5ID(p) of a non-first fragment keeps only ip_p (lib/ipflowid.cc:
+    34-38: IPFlowID returns before assign(), addresses stay 0): all non-first
+    fragments of one protocol are one flow, whatever their addresses."""
+    b = synth.c4(4_000, seed=61)
+    frag = set_fragment(b, 0.2, seed=62)
+    cfg = flow_cfg()
+    ids, _ = oracle_flows(oracle, cfg, [b], 1 << 16)
+    r = oracle.process_batch(cfg, b)
+    nf = np.zeros(b.n, bool)
+    nf[frag] = True
+    nf &= r["reason"] == N.R_OK
+    assert nf.sum() > 100 and len(np.unique(ids[nf])) == 1
+    assert not np.isin(ids[~nf & (r["reason"] == N.R_OK)], ids[nf]).any()
+
+
+@pytest.mark.gpu
+def test_gpu_nonfirst_fragments_flow(oracle):
+    from fastclick_amd import device
+    b = synth.c4(30_000, seed=63)
+    set_fragment(b, 0.15, seed=64)
+    synth.inject_errors(b, 0.01, seed=65)
+    cfg = flow_cfg()
+    batches = split(b, [10_000, 20_000])
+    exp, cnt = oracle_flows(oracle, cfg, batches, 1 << 16)
+    got = device.process_batches(batches, cfg, max_flows=1 << 16, anno=False, perm=False)
+    assert np.array_equal(np.concatenate([g["flowid"] for g in got]), exp)
+    assert got[-1]["flow_count"] == cnt
