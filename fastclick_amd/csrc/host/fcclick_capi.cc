@@ -57,6 +57,16 @@ class Sink : public Element {
     uint32_t *_seq, *_nbatch;
 };
 
+// The harness floor: a BatchElement that forwards every PacketBatch to output
+// 0 unchanged (what the source and sinks cost without the GPU element).
+class Pass : public Element {
+  public:
+    const char *class_name() const override { return "Pass"; }
+    int configure(const std::vector<std::string> &, std::string &) override { return 0; }
+    void push_batch(int, PacketBatch *b) override { output_push_batch(0, b); }
+    uint32_t max_held() const override { return 0; }
+};
+
 bool parse_element(const char *conf, std::string &cls, std::vector<std::string> &args, std::string &err) {
     std::string s = trim(conf ? conf : "");
     size_t lp = s.find('(');
@@ -82,6 +92,7 @@ std::unique_ptr<Element> make_element(const char *conf, std::string &err) {
     }
     std::unique_ptr<Element> e;
     if (cls == "GPUIPCheckClassify") e.reset(new GPUIPCheckClassify());
+    else if (cls == "Pass") e.reset(new Pass());
     else {
         err = "unknown element class '" + cls + "'";
         return nullptr;

@@ -61,7 +61,7 @@
 //     headers SetIPChecksum rejects are killed; the rewritten ttl/checksum
 //     bytes are written back into each packet.
 //   MODE CHECK|MARK|AUTO, HASH NONE|FLOWID|FLOW5ID, STRIP, DEVICE,
-//   BATCH (packets per device batch, default 8192; 0: each incoming
+//   BATCH (packets per device batch, default 16384; 0: each incoming
 //   PacketBatch is one), TIMER (us, default 100; -1 none),
 //   PARTITION TILE (default: each 256-packet tile classified as one batch,
 //   one fused launch) | GLOBAL (the whole device batch as one, three launches)
@@ -337,6 +337,7 @@ class RxCore {
     // the caller reschedules the timer for due_ns().
     template <class Emit>
     bool run_timer(uint64_t now_ns, Emit &&emit) {
+        if (_timer_us < 0) return false;                  // TIMER -1: no timer
         Slot &s = _slot[_cur];
         if (s.n && now_ns >= due_ns()) {
             flush(emit);
@@ -462,6 +463,18 @@ class RxCore {
         return -1;
     }
 
+    // cp bytes, no byte read outside [src, src + cp): 16-B moves, the last
+    // one overlapping its predecessor (a frame is 60 B in the headline case)
+    static inline void copy_head(uint8_t *dst, const uint8_t *src, uint32_t cp) {
+        if (cp >= 16) {
+            uint32_t k = 0;
+            for (; k + 16 <= cp; k += 16) memcpy(dst + k, src + k, 16);
+            if (k < cp) memcpy(dst + cp - 16, src + cp - 16, 16);
+        } else {
+            memcpy(dst, src, cp);
+        }
+    }
+
     // Copy the packet's leading bytes into the current slot (64-B aligned
     // records), remember the packet; a full slot goes to the device.
     template <class Emit>
@@ -481,16 +494,7 @@ class RxCore {
             }
             s->t_first = _timer_us >= 0 ? P::now_ns() : 0;
         }
-        uint8_t *dst = s->span + s->used;
-        const uint8_t *src = P::data(p);
-        if (cp == 128 || (cp > 64 && cp <= 128)) {
-            memcpy(dst, src, 64);
-            memcpy(dst + 64, src + 64, cp - 64);
-        } else if (cp == 64) {
-            memcpy(dst, src, 64);
-        } else {
-            memcpy(dst, src, cp);
-        }
+        copy_head(s->span + s->used, P::data(p), cp);
         s->desc[2 * s->n] = (uint32_t)s->used;
         s->desc[2 * s->n + 1] = len;
         s->pkts[s->n++] = p;
@@ -575,6 +579,7 @@ class RxCore {
         const bool autom = _cfg.check_mode == FCGPU_CHECK_AUTO;
         for (uint32_t i = 0; i < n; ++i) {
             Packet *p = s.pkts[i];
+            if (i + 8 < n) __builtin_prefetch(s.pkts[i + 8], 1);    // staged long ago: out of L1/L2
             const fcgpu_anno &a = s.anno[i];
             const uint32_t reason = s.verdict[i] & 0xff;
             if (_color >= 0) P::set_anno_u8(p, P::kPaint, (uint8_t)_color);     // SET_PAINT_ANNO
@@ -690,7 +695,7 @@ class RxCore {
     int _flow_anno = 28;
     uint64_t _flow_drops = 0;
     int _device = 0;
-    uint32_t _batch = 8192;
+    uint32_t _batch = 16384;
     int64_t _timer_us = 100;
     uint32_t _cap = 0;
     uint32_t _capture = fcgpu::kCaptureMin;

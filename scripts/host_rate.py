@@ -108,7 +108,8 @@ def pcap_mpps(n=1 << 22, chunk_pkts=1 << 18, threads=1, mapped=False):
 
 
 def main():
-    out = {"h2d_pinned_gbs": round(h2d_gbs(), 2)}
+    out = {"h2d_pinned_gbs": round(h2d_gbs(), 2),
+           "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)")}
     for t in (1, 4):
         out[f"pcap_ingress_mpps_4M_t{t}"] = round(pcap_mpps(threads=t), 2)
     m, reg = pcap_mpps(mapped=True)
@@ -126,13 +127,15 @@ def main():
     # C2-chain CPU baseline
     b = synth.c2(1 << 16)
     base = "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BATCH {})"
-    for batch in (4096, 8192, 16384, 65536):
+    # the harness floor (source + sinks, no element work)
+    out["harness_floor_mpps"] = round(K.bench_element("Pass", b, burst=32, reps=40) / 1e6, 2)
+    for batch in (4096, 8192, 16384, 32768, 65536):
         out[f"element_mpps_batch{batch}"] = round(K.bench_element(base.format(batch), b, burst=32, reps=40) / 1e6, 2)
     for t in (2, 4, 8):
-        out[f"element_mpps_batch8192_threads{t}"] = round(
-            K.bench_element(base.format(8192), b, burst=32, reps=40, threads=t) / 1e6, 2)
-    out["element_mpps_batch8192_per_packet_push"] = round(
-        K.bench_element(base.format(8192), b, burst=K.PER_PACKET, reps=20) / 1e6, 2)
+        out[f"element_mpps_batch16384_threads{t}"] = round(
+            K.bench_element(base.format(16384), b, burst=32, reps=40, threads=t) / 1e6, 2)
+    out["element_mpps_batch16384_per_packet_push"] = round(
+        K.bench_element(base.format(16384), b, burst=K.PER_PACKET, reps=20) / 1e6, 2)
     print(json.dumps(out))
 
 

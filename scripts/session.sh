@@ -65,6 +65,7 @@ for s in "${ST[@]}"; do
                 step "var_$n" 300 python bench.py --steps 200 --warmup 20 --no-cpu $v
               done ;;
     host) step host_rate 600 python scripts/host_rate.py ;;
+    host_q16) GPU_MAX_HW_QUEUES=16 step host_rate_q16 600 python scripts/host_rate.py ;;
     kgather) step kgather 180 ./scripts/kgather 64 ;;
     dist2) step dist2 300 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 --no-cpu ;;
     *) echo "unknown step $s"; exit 2 ;;
