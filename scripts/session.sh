@@ -37,6 +37,8 @@ for s in "${ST[@]}"; do
     kt_drv_s1) kt kt_drv_s1 300 $DRV --no-cpu --streams 1 ;;
     kt_long) kt kt_long 300 --steps 200 --warmup 20 --no-cpu ;;
     kt_w40) kt kt_w40 300 --gpus 1 --steps 20 --warmup 40 --no-cpu ;;
+    kt_notime) kt kt_notime 300 $DRV --no-cpu --no-timing ;;
+    kt_notime_s1) kt kt_notime_s1 300 $DRV --no-cpu --no-timing --streams 1 ;;
     kt_w40_s1) kt kt_w40_s1 300 --gpus 1 --steps 20 --warmup 40 --no-cpu --streams 1 ;;
     bench2) step bench2 300 python bench.py $DRV --no-cpu ;;
     bench3) step bench3 300 python bench.py $DRV --no-cpu ;;
