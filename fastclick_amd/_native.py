@@ -14,7 +14,7 @@ LIBFCGPU = os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 10
+ABI_VERSION = 11
 SPAN_SLOTS = 3
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
@@ -40,6 +40,9 @@ CTR_COUNT, CTR_DROPS, CTR_REASON, CTR_PORT = 0, 1, 2, 16
 NCOUNTERS = CTR_PORT + MAX_PORTS + 1
 CTR_SHARDS = 64
 PART_GLOBAL, PART_TILE = 0, 1
+OUT_VERDICT, OUT_HASH, OUT_ANNO, OUT_PERM, OUT_PORT_START, OUT_TILE_COUNT, OUT_TILE_PERM, OUT_FLOWID, \
+    OUT_IP_RW = (1 << k for k in range(9))
+OUT_ABSENT = (1 << 64) - 1
 TILE = 256
 
 REASON_TEXTS = ["tiny packet", "bad IPv4 version", "bad IPv4 header length",
@@ -133,6 +136,11 @@ class fcgpu_job(C.Structure):
     ]
 
 
+class fcgpu_block_layout(C.Structure):
+    _fields_ = [(k, C.c_size_t) for k in ("verdict", "hash", "anno", "perm", "port_start", "tile_count",
+                                          "tile_perm", "flowid", "ip_rw", "bytes")]
+
+
 class fcgpu_step(C.Structure):
     _fields_ = [
         ("offset", C.c_int32),
@@ -163,6 +171,10 @@ FCGPU_SYMBOLS = {
     "fcgpu_span_submit": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32,
                                     C.POINTER(fcgpu_out)]),
     "fcgpu_span_wait": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "fcgpu_span_poll": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "fcgpu_block_layout_for": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]),
+    "fcgpu_span_submit_block": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t,
+                                          C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32]),
     "fcgpu_flow_enable": (C.c_int, [C.c_void_p, C.c_uint32]),
     "fcgpu_flow_reset": (C.c_int, [C.c_void_p]),
     "fcgpu_flow_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),

@@ -140,6 +140,8 @@ struct SpanSlot {
     uint32_t *d_h = nullptr, *d_perm = nullptr, *d_start = nullptr, *d_fl = nullptr, *d_rw = nullptr;
     fcgpu_anno *d_an = nullptr;
     uint8_t *d_tp = nullptr;
+    uint8_t *d_in = nullptr, *d_res = nullptr;   // block submissions
+    size_t in_cap = 0, res_cap = 0;
     bool busy = false;
 };
 
@@ -622,7 +624,7 @@ void fcgpu_close(fcgpu_ctx *c) {
             if (sp.s) hipStreamSynchronize(sp.s);
             for (void *p : {(void *)sp.d_span, (void *)sp.d_desc, (void *)sp.d_v, (void *)sp.d_tc, (void *)sp.d_h,
                             (void *)sp.d_perm, (void *)sp.d_start, (void *)sp.d_fl, (void *)sp.d_rw, (void *)sp.d_an,
-                            (void *)sp.d_tp})
+                            (void *)sp.d_tp, (void *)sp.d_in, (void *)sp.d_res})
                 hipFree(p);
             if (sp.own) hipStreamDestroy(sp.own);
         }
@@ -1136,6 +1138,98 @@ int fcgpu_span_submit(fcgpu_ctx *c, uint32_t slot, const uint8_t *h_span, size_t
         (rc = back(h->tile_perm, sp.d_tp, n)) || (rc = back(h->flowid, sp.d_fl, sizeof(uint32_t) * n)) ||
         (rc = back(h->ip_rw, sp.d_rw, sizeof(uint32_t) * n)))
         return rc;
+    sp.busy = true;
+    return FCGPU_OK;
+}
+
+int fcgpu_span_poll(fcgpu_ctx *c, uint32_t slot) {
+    if (!c || slot >= FCGPU_SPAN_SLOTS) return FCGPU_EINVAL;
+    SpanSlot &sp = c->span[slot];
+    if (!sp.busy) return 1;
+    const hipError_t e = hipStreamQuery(sp.s);
+    if (e == hipSuccess) return 1;
+    if (e == hipErrorNotReady) return 0;
+    return fail(c, FCGPU_ERUNTIME, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+}
+
+int fcgpu_block_layout_for(const fcgpu_ctx *c, uint32_t n, uint32_t outputs, uint32_t partition, fcgpu_block_layout *L) {
+    if (!c || !L || partition > FCGPU_PART_TILE) return FCGPU_EINVAL;
+    const size_t nb = c->cfg.nports + 1, tiles = (n + kTile - 1) / kTile;
+    size_t off = 0;
+    auto put = [&](size_t &field, uint32_t bit, size_t bytes) {
+        field = FCGPU_OUT_ABSENT;
+        if (!(outputs & bit)) return;
+        off = (off + 255) & ~(size_t)255;
+        field = off;
+        off += bytes;
+    };
+    put(L->verdict, FCGPU_OUT_VERDICT, 2ull * n);
+    put(L->hash, FCGPU_OUT_HASH, 4ull * n);
+    put(L->anno, FCGPU_OUT_ANNO, sizeof(fcgpu_anno) * n);
+    put(L->perm, FCGPU_OUT_PERM, 4ull * n);
+    put(L->port_start, FCGPU_OUT_PORT_START, 4ull * (FCGPU_MAX_PORTS + 2));
+    put(L->tile_count, FCGPU_OUT_TILE_COUNT, 2ull * nb * tiles);
+    put(L->tile_perm, FCGPU_OUT_TILE_PERM, (size_t)n);
+    put(L->flowid, FCGPU_OUT_FLOWID, 4ull * n);
+    put(L->ip_rw, FCGPU_OUT_IP_RW, 4ull * n);
+    L->bytes = (off + 255) & ~(size_t)255;
+    return FCGPU_OK;
+}
+
+int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_t in_bytes, size_t desc_off,
+                            size_t frames_off, uint32_t n, void *h_out, uint32_t outputs, uint32_t partition) {
+    if (!c || slot >= FCGPU_SPAN_SLOTS || (n && (!h_in || !h_out))) return FCGPU_EINVAL;
+    if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "batch larger than max_batch");
+    if (desc_off + 8ull * n > in_bytes || frames_off > in_bytes || (desc_off & 7))
+        return fail(c, FCGPU_EINVAL, "block: descriptors (8-B aligned) or frames outside in_bytes");
+    if (in_bytes - frames_off > 0xffffffffull - kArenaPad) return fail(c, FCGPU_EINVAL, "frames larger than 4 GiB");
+    SpanSlot &sp = c->span[slot];
+    if (sp.busy) return fail(c, FCGPU_EINVAL, "span slot busy: fcgpu_span_wait it first");
+    fcgpu_block_layout L;
+    if (fcgpu_block_layout_for(c, n, outputs, partition, &L) != FCGPU_OK) return fail(c, FCGPU_EINVAL, "bad block layout");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!sp.own) HIPCHK(c, hipStreamCreateWithFlags(&sp.own, hipStreamNonBlocking));
+    if (in_bytes + kArenaPad > sp.in_cap) {
+        HIPCHK(c, hipStreamSynchronize(sp.own));
+        hipFree(sp.d_in);
+        sp.d_in = nullptr;
+        sp.in_cap = 0;
+        const size_t cap = (in_bytes + kArenaPad + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+        HIPCHK(c, hipMalloc(&sp.d_in, cap));
+        HIPCHK(c, memset_sync(sp.d_in, 0, cap));
+        sp.in_cap = cap;
+    }
+    if (L.bytes > sp.res_cap) {
+        HIPCHK(c, hipStreamSynchronize(sp.own));
+        hipFree(sp.d_res);
+        sp.d_res = nullptr;
+        sp.res_cap = 0;
+        fcgpu_block_layout M;    // room for a full batch with these outputs
+        fcgpu_block_layout_for(c, c->max_batch, outputs, partition, &M);
+        const size_t cap = std::max(M.bytes, L.bytes);
+        HIPCHK(c, hipMalloc(&sp.d_res, cap));
+        sp.res_cap = cap;
+    }
+    if (c->fl.slots && !c->stream) HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    sp.s = c->fl.slots ? c->stream : sp.own;
+    hipStream_t s = sp.s;
+    if (n == 0) return FCGPU_OK;
+    HIPCHK(c, hipMemcpyAsync(sp.d_in, h_in, in_bytes, hipMemcpyHostToDevice, s));
+    auto at = [&](size_t o) -> void * { return o == FCGPU_OUT_ABSENT ? nullptr : sp.d_res + o; };
+    fcgpu_out d{};
+    d.verdict = (uint16_t *)at(L.verdict);
+    d.hash = (uint32_t *)at(L.hash);
+    d.anno = (fcgpu_anno *)at(L.anno);
+    d.perm = (uint32_t *)at(L.perm);
+    d.port_start = (uint32_t *)at(L.port_start);
+    d.tile_count = (uint16_t *)at(L.tile_count);
+    d.partition = partition;
+    d.tile_perm = (uint8_t *)at(L.tile_perm);
+    d.flowid = (uint32_t *)at(L.flowid);
+    d.ip_rw = (uint32_t *)at(L.ip_rw);
+    int rc = fcgpu_process(c, sp.d_in + frames_off, reinterpret_cast<const uint32_t *>(sp.d_in + desc_off), n, &d, s);
+    if (rc != FCGPU_OK) return rc;
+    HIPCHK(c, hipMemcpyAsync(h_out, sp.d_res, L.bytes, hipMemcpyDeviceToHost, s));
     sp.busy = true;
     return FCGPU_OK;
 }

@@ -280,11 +280,16 @@ class RxCore {
         }
         _capture = fcgpu::capture_bytes(_cfg, reach);
         const size_t per = _capture == fcgpu::kCaptureWhole ? 1536 : _capture;
-        for (Slot &s : _slot) {
-            if (!s.alloc(_cap, (size_t)_cap * per + 65536, _cfg.nports, _partition, _flow_cap != 0,
-                         _cfg.rewrite != 0))
+        _outputs = FCGPU_OUT_VERDICT | FCGPU_OUT_HASH | FCGPU_OUT_ANNO |
+                   (_partition == FCGPU_PART_TILE ? FCGPU_OUT_TILE_PERM | FCGPU_OUT_TILE_COUNT
+                                                  : FCGPU_OUT_PERM | FCGPU_OUT_PORT_START) |
+                   (_flow_cap ? FCGPU_OUT_FLOWID : 0u) | (_cfg.rewrite ? FCGPU_OUT_IP_RW : 0u);
+        fcgpu_block_layout L;
+        if (fcgpu_block_layout_for(_ctx, _cap, _outputs, _partition, &L) != FCGPU_OK)
+            return err(errh, "fcgpu_block_layout_for failed");
+        for (Slot &s : _slot)
+            if (!s.alloc(_cap, (size_t)_cap * per + 65536, L.bytes))
                 return err(errh, "cannot allocate pinned staging (fcgpu_host_alloc)");
-        }
         return 0;
     }
 
@@ -413,48 +418,53 @@ class RxCore {
     // copy is DMA), the packets, and the pinned result arrays the D2H copies
     // land in.
     struct Slot {
-        uint8_t *span = nullptr;
-        size_t span_cap = 0, used = 0;
-        uint32_t *desc = nullptr;
+        // pinned input block: [descriptors: cap x 8 B][frames]; pinned result
+        // block laid out by fcgpu_block_layout_for -- one copy each way per batch
+        uint8_t *in = nullptr, *res = nullptr;
+        size_t in_cap = 0, frames_off = 0, used = 0;
+        uint8_t *span = nullptr;          // in + frames_off
+        uint32_t *desc = nullptr;         // in
         std::vector<Packet *> pkts;
+        std::vector<uint32_t> keep;
         uint32_t n = 0;
         bool inflight = false;
         bool holes = false;        // a packet freed while its results were applied
         uint64_t t_first = 0;
+        // the result arrays of the completed batch (inside res)
         uint16_t *verdict = nullptr, *tile_count = nullptr;
         uint32_t *hash = nullptr, *perm = nullptr, *start = nullptr, *flowid = nullptr, *iprw = nullptr;
         fcgpu_anno *anno = nullptr;
         uint8_t *tperm = nullptr;
-        std::vector<uint32_t> keep;
 
-        template <class T>
-        static bool get(T *&p, size_t count) {
-            p = static_cast<T *>(fcgpu_host_alloc(sizeof(T) * (count ? count : 1)));
-            return p != nullptr;
-        }
-        bool alloc(uint32_t cap, size_t span_bytes, uint32_t nports, uint32_t part, bool flow, bool rw) {
+        bool alloc(uint32_t cap, size_t frame_bytes, size_t res_bytes) {
             pkts.resize(cap);
             keep.resize(cap);
-            span_cap = span_bytes;
-            const size_t tiles = (cap + FCGPU_TILE - 1) / FCGPU_TILE;
-            bool ok = get(span, span_cap) && get(desc, 2 * (size_t)cap) && get(verdict, cap) && get(hash, cap) &&
-                      get(anno, cap);
-            if (part == FCGPU_PART_TILE) ok = ok && get(tperm, cap + FCGPU_TILE) && get(tile_count, (nports + 1) * tiles);
-            else ok = ok && get(perm, cap) && get(start, FCGPU_MAX_PORTS + 2);
-            if (flow) ok = ok && get(flowid, cap);
-            if (rw) ok = ok && get(iprw, cap);
-            return ok;
+            frames_off = ((size_t)cap * 8 + 255) & ~(size_t)255;
+            in_cap = frames_off + frame_bytes;
+            in = static_cast<uint8_t *>(fcgpu_host_alloc(in_cap));
+            res = static_cast<uint8_t *>(fcgpu_host_alloc(res_bytes ? res_bytes : 1));
+            span = in ? in + frames_off : nullptr;
+            desc = reinterpret_cast<uint32_t *>(in);
+            return in && res;
         }
         void free() {
-            for (void *p : {(void *)span, (void *)desc, (void *)verdict, (void *)tile_count, (void *)hash, (void *)perm,
-                            (void *)start, (void *)flowid, (void *)iprw, (void *)anno, (void *)tperm})
-                fcgpu_host_free(p);
-            span = nullptr;
+            fcgpu_host_free(in);
+            fcgpu_host_free(res);
+            in = res = span = nullptr;
             desc = nullptr;
-            verdict = tile_count = nullptr;
-            hash = perm = start = flowid = iprw = nullptr;
-            anno = nullptr;
-            tperm = nullptr;
+        }
+        // point the result arrays at their place in res for an n-packet batch
+        void map(const fcgpu_block_layout &L) {
+            auto at = [this](size_t o) -> void * { return o == FCGPU_OUT_ABSENT ? nullptr : res + o; };
+            verdict = (uint16_t *)at(L.verdict);
+            hash = (uint32_t *)at(L.hash);
+            anno = (fcgpu_anno *)at(L.anno);
+            perm = (uint32_t *)at(L.perm);
+            start = (uint32_t *)at(L.port_start);
+            tile_count = (uint16_t *)at(L.tile_count);
+            tperm = (uint8_t *)at(L.tile_perm);
+            flowid = (uint32_t *)at(L.flowid);
+            iprw = (uint32_t *)at(L.ip_rw);
         }
     };
 
@@ -483,7 +493,7 @@ class RxCore {
         const uint32_t len = P::length(p);
         const uint32_t cp = len < _capture ? len : _capture;
         const size_t rec = cp ? ((size_t)cp + 63) & ~(size_t)63 : 64;
-        if (s->n && s->used + rec > s->span_cap) {       // whole frames overflowing the span
+        if (s->n && s->frames_off + s->used + rec > s->in_cap) {   // whole frames overflowing the block
             submit(emit);
             s = &_slot[_cur];
         }
@@ -508,21 +518,8 @@ class RxCore {
     void submit(Emit &emit) {
         const uint32_t k = _cur;
         Slot &s = _slot[k];
-        fcgpu_out o{};
-        o.verdict = s.verdict;
-        o.hash = s.hash;
-        o.anno = s.anno;
-        o.partition = _partition;
-        if (_partition == FCGPU_PART_TILE) {
-            o.tile_perm = s.tperm;
-            o.tile_count = s.tile_count;
-        } else {
-            o.perm = s.perm;
-            o.port_start = s.start;
-        }
-        o.flowid = s.flowid;
-        o.ip_rw = s.iprw;
-        const int rc = fcgpu_span_submit(_ctx, k, s.span, s.used, s.desc, s.n, &o);
+        const int rc = fcgpu_span_submit_block(_ctx, k, s.in, s.frames_off + s.used, 0, s.frames_off, s.n, s.res,
+                                               _outputs, _partition);
         if (rc != FCGPU_OK) {
             fail_slot(s, fcgpu_last_error(_ctx));
         } else {
@@ -575,6 +572,9 @@ class RxCore {
         }
         const uint32_t n = s.n;
         s.holes = false;
+        fcgpu_block_layout L;
+        fcgpu_block_layout_for(_ctx, n, _outputs, _partition, &L);
+        s.map(L);
         const bool hashing = _cfg.hash_mode != FCGPU_HASH_NONE;
         const bool autom = _cfg.check_mode == FCGPU_CHECK_AUTO;
         for (uint32_t i = 0; i < n; ++i) {
@@ -700,6 +700,7 @@ class RxCore {
     uint32_t _cap = 0;
     uint32_t _capture = fcgpu::kCaptureMin;
     uint32_t _partition = FCGPU_PART_TILE;
+    uint32_t _outputs = 0;                       // FCGPU_OUT_* the element asks for
     bool _verbose = false, _details = false, _strip = false, _warned = false;
     std::string _error;
     Slot _slot[kSlots];

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 10
+#define FCGPU_ABI_VERSION 11
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -287,6 +287,38 @@ int  fcgpu_process_host(fcgpu_ctx *ctx, const uint8_t *const *frames,
 int  fcgpu_span_submit(fcgpu_ctx *ctx, uint32_t slot, const uint8_t *h_span, size_t span_bytes,
                        const uint32_t *h_desc, uint32_t n, const fcgpu_out *h_out);
 int  fcgpu_span_wait(fcgpu_ctx *ctx, uint32_t slot);
+/* Non-blocking: 1 if the slot's submission has completed (or none is in
+ * flight), 0 if it is still running, < 0 on error. */
+int  fcgpu_span_poll(fcgpu_ctx *ctx, uint32_t slot);
+
+/* Block submissions: one H2D copy in, one D2H copy out per batch (instead of
+ * one per array), for callers that stage into one pinned buffer -- the
+ * GPUIPCheckClassify element. h_in holds the descriptors at desc_off and the
+ * frames at frames_off (descriptor offsets are relative to frames_off); the
+ * first in_bytes of h_in are copied, and the device copy is padded for the
+ * header-window over-read. The requested outputs (FCGPU_OUT_* mask) come back
+ * in h_out at the offsets fcgpu_block_layout_for() gives for (n, outputs,
+ * partition) -- each array 256-B aligned, in the order of the mask bits.
+ * Completion, slots and streams as fcgpu_span_submit. */
+#define FCGPU_OUT_VERDICT    (1u << 0)
+#define FCGPU_OUT_HASH       (1u << 1)
+#define FCGPU_OUT_ANNO       (1u << 2)
+#define FCGPU_OUT_PERM       (1u << 3)   /* GLOBAL: with port_start; TILE: packet indices */
+#define FCGPU_OUT_PORT_START (1u << 4)   /* GLOBAL                                       */
+#define FCGPU_OUT_TILE_COUNT (1u << 5)   /* TILE                                         */
+#define FCGPU_OUT_TILE_PERM  (1u << 6)   /* TILE                                         */
+#define FCGPU_OUT_FLOWID     (1u << 7)
+#define FCGPU_OUT_IP_RW      (1u << 8)
+#define FCGPU_OUT_ABSENT     ((size_t)-1)
+typedef struct fcgpu_block_layout {
+    size_t verdict, hash, anno, perm, port_start, tile_count, tile_perm, flowid, ip_rw;  /* byte offsets */
+    size_t bytes;                                                                       /* block size   */
+} fcgpu_block_layout;
+int  fcgpu_block_layout_for(const fcgpu_ctx *ctx, uint32_t n, uint32_t outputs, uint32_t partition,
+                        fcgpu_block_layout *out);
+int  fcgpu_span_submit_block(fcgpu_ctx *ctx, uint32_t slot, const void *h_in, size_t in_bytes,
+                             size_t desc_off, size_t frames_off, uint32_t n, void *h_out, uint32_t outputs,
+                             uint32_t partition);
 
 /* Decision programs. A program is the step list the
  * reference's own compiler produces and prints through the `program` handler
