@@ -14,7 +14,7 @@ LIBFCGPU = os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 11
+ABI_VERSION = 12
 SPAN_SLOTS = 3
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
@@ -141,6 +141,14 @@ class fcgpu_block_layout(C.Structure):
                                           "tile_perm", "flowid", "ip_rw", "bytes")]
 
 
+class fcgpu_mbuf_layout(C.Structure):
+    _fields_ = [("buf_addr", C.c_uint32), ("data_off", C.c_uint32), ("data_len", C.c_uint32),
+                ("header_bytes", C.c_uint32)]
+
+
+MBUF_LAYOUT_DPDK = (0, 16, 40, 64)      # FCGPU_MBUF_LAYOUT_DPDK (rte_mbuf, DPDK >= 20.11)
+
+
 class fcgpu_step(C.Structure):
     _fields_ = [
         ("offset", C.c_int32),
@@ -180,6 +188,9 @@ FCGPU_SYMBOLS = {
     "fcgpu_flow_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "fcgpu_host_alloc": (C.c_void_p, [C.c_size_t]),
     "fcgpu_host_free": (None, [C.c_void_p]),
+    "fcgpu_pool_register": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    "fcgpu_process_mbufs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(fcgpu_mbuf_layout),
+                                      C.POINTER(fcgpu_out), C.c_void_p]),
     "fcgpu_host_register": (C.c_int, [C.c_void_p, C.c_size_t, C.c_int]),
     "fcgpu_host_unregister": (C.c_int, [C.c_void_p]),
     "fcgpu_read_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
@@ -348,6 +359,20 @@ class Context:
     def run_jobs(self, prepared, stream=0):
         arr, n = prepared
         self._chk(self.lib.fcgpu_process_jobs(self.h, arr, n, stream or None), "fcgpu_process_jobs")
+
+    def pool_register(self, base: int, nbytes: int):
+        """Register a packet-buffer pool (mbuf headers + data rooms) for fcgpu_process_mbufs."""
+        self._chk(self.lib.fcgpu_pool_register(self.h, base, nbytes), "fcgpu_pool_register")
+
+    def process_mbufs(self, ptrs_addr: int, n: int, layout=MBUF_LAYOUT_DPDK, stream=0, **outs):
+        """ptrs_addr: host array of n mbuf pointers (uint64) inside the registered pool."""
+        lay = fcgpu_mbuf_layout(*layout)
+        o = fcgpu_out(outs.get("verdict") or None, outs.get("hash") or None, outs.get("anno") or None,
+                      outs.get("perm") or None, outs.get("port_start") or None, outs.get("tile_count") or None,
+                      outs.get("partition", PART_GLOBAL), 0, outs.get("tile_perm") or None,
+                      outs.get("flowid") or None, outs.get("ip_rw") or None)
+        self._chk(self.lib.fcgpu_process_mbufs(self.h, ptrs_addr, n, C.byref(lay), C.byref(o), stream or None),
+                  "fcgpu_process_mbufs")
 
     def process_host(self, frames, lens_ptr, n, *, verdict=0, hash=0, anno=0, perm=0,
                      port_start=0, tile_count=0, partition=PART_GLOBAL, tile_perm=0, flowid=0, ip_rw=0):

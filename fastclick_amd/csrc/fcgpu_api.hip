@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <condition_variable>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -198,6 +199,12 @@ struct fcgpu_ctx {
     uint32_t *flow_hint = nullptr;    // mapped: size class of the last finish's misses (kHint*)
     uint32_t flow_epoch = 0;          // batches through the table (FlowArgs::epoch)
     hipEvent_t flow_order[2] = {nullptr, nullptr};   // orders fcgpu_process against span submissions
+    // mbuf ingress (fcgpu_pool_register / fcgpu_process_mbufs)
+    uint64_t pool_host = 0, pool_bytes = 0;
+    uint8_t *pool_dev = nullptr;
+    bool pool_owned = false;          // this context holds a reference on the pool's registration
+    uint64_t *d_mptr = nullptr;
+    uint2 *d_mdesc = nullptr;
     // timing: every timing_every-th launch is bracketed by events (0 = off)
     uint32_t timing_every = 0;
     uint64_t timing_seq = 0;
@@ -228,6 +235,22 @@ static hipError_t memset_sync(void *p, int v, size_t bytes) {
 }
 
 static std::string g_open_err;
+
+// Pools registered by fcgpu_pool_register, with the number of contexts using each.
+static std::mutex g_pool_mu;
+static std::map<std::pair<uint64_t, uint64_t>, uint32_t> g_pools;
+
+static void pool_release(fcgpu_ctx *c) {
+    if (!c->pool_host || !c->pool_owned) return;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    auto it = g_pools.find({c->pool_host, c->pool_bytes});
+    if (it != g_pools.end() && --it->second == 0) {
+        hipHostUnregister((void *)c->pool_host);
+        (void)hipGetLastError();
+        g_pools.erase(it);
+    }
+    c->pool_owned = false;
+}
 
 static int fail(fcgpu_ctx *c, int code, const std::string &msg) {
     if (c) c->err = msg;
@@ -629,6 +652,9 @@ void fcgpu_close(fcgpu_ctx *c) {
             if (sp.own) hipStreamDestroy(sp.own);
         }
         flow_free(c);
+        hipFree(c->d_mptr);
+        hipFree(c->d_mdesc);
+        pool_release(c);
         for (auto e : c->flow_order)
             if (e) hipEventDestroy(e);
         hipHostFree(c->h_arena);
@@ -1258,6 +1284,73 @@ int fcgpu_host_register(void *p, size_t bytes, int read_only) {
 int fcgpu_host_unregister(void *p) {
     if (!p) return FCGPU_EINVAL;
     return hipHostUnregister(p) == hipSuccess ? FCGPU_OK : FCGPU_ERUNTIME;
+}
+
+int fcgpu_pool_register(fcgpu_ctx *c, void *base, size_t bytes) {
+    if (!c || !base || bytes < 4096) return fail(c, FCGPU_EINVAL, "fcgpu_pool_register: bad pool");
+    if (bytes > 0xffffffffull - kArenaPad) return fail(c, FCGPU_EINVAL, "pool larger than 4 GiB (u32 frame offsets)");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->pool_host) {
+        HIPCHK(c, hipDeviceSynchronize());
+        pool_release(c);
+        c->pool_host = c->pool_bytes = 0;
+        c->pool_dev = nullptr;
+    }
+    // several contexts (one per rx queue / thread) may share one pool: the
+    // library pins it once and unpins it when the last of them lets go
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        auto it = g_pools.find({(uint64_t)base, bytes});
+        if (it != g_pools.end()) {
+            ++it->second;
+        } else {
+            hipError_t e = hipHostRegister(base, bytes, hipHostRegisterMapped);
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                return fail(c, FCGPU_ERUNTIME, std::string("hipHostRegister(pool): ") + hipGetErrorString(e));
+            }
+            g_pools[{(uint64_t)base, bytes}] = 1;
+        }
+    }
+    c->pool_owned = true;
+    void *dev = nullptr;
+    HIPCHK(c, hipHostGetDevicePointer(&dev, base, 0));
+    c->pool_host = (uint64_t)base;
+    c->pool_bytes = bytes;
+    c->pool_dev = static_cast<uint8_t *>(dev);
+    if (!c->d_mptr) {
+        HIPCHK(c, hipMalloc(&c->d_mptr, sizeof(uint64_t) * c->max_batch));
+        HIPCHK(c, hipMalloc(&c->d_mdesc, sizeof(uint2) * c->max_batch));
+    }
+    return FCGPU_OK;
+}
+
+int fcgpu_process_mbufs(fcgpu_ctx *c, void *const *mbufs, uint32_t n, const fcgpu_mbuf_layout *L,
+                        const fcgpu_out *o, void *stream) {
+    if (!c || !o || !L || (n && !mbufs)) return FCGPU_EINVAL;
+    if (!c->pool_host) return fail(c, FCGPU_EINVAL, "fcgpu_process_mbufs: no pool registered (fcgpu_pool_register)");
+    if (L->header_bytes > 64 || L->buf_addr + 8 > L->header_bytes || L->data_off + 2 > L->header_bytes ||
+        L->data_len + 2 > L->header_bytes || (L->buf_addr & 7) || (L->data_off & 1) || (L->data_len & 1))
+        return fail(c, FCGPU_EINVAL, "bad mbuf layout (fields aligned, inside header_bytes <= 64)");
+    int rc = check_process(c, c->pool_dev, reinterpret_cast<const uint32_t *>(c->d_mdesc), n, o);
+    if (rc != FCGPU_OK || n == 0) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(c, hipMemcpyAsync(c->d_mptr, mbufs, sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
+    MbufArgs a;
+    a.ptrs = c->d_mptr;
+    a.n = n;
+    a.pool_host = c->pool_host;
+    a.pool_bytes = c->pool_bytes;
+    a.pool_dev = c->pool_dev;
+    a.f_buf = L->buf_addr;
+    a.f_off = L->data_off;
+    a.f_len = L->data_len;
+    a.hdr = L->header_bytes;
+    a.desc = c->d_mdesc;
+    hipLaunchKernelGGL(k_mbuf_desc, dim3((n + 255) / 256), dim3(256), 0, s, a);
+    HIPCHK(c, hipGetLastError());
+    return process_one(c, c->pool_dev, reinterpret_cast<const uint32_t *>(c->d_mdesc), n, o, s);
 }
 
 int fcgpu_set_host_threads(fcgpu_ctx *c, uint32_t nthreads) {

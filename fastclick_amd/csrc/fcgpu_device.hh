@@ -1194,4 +1194,63 @@ __global__ __launch_bounds__(kTile) void k_part(const uint16_t *verdict, uint32_
     }
 }
 
+// ---- mbuf ingress: descriptors from the mbufs themselves -------------------
+// One lane per mbuf pointer (host virtual address). The pointer and the frame
+// are checked against the registered pool before anything is dereferenced;
+// the header fields are read from host memory over PCIe (header_bytes <= 64). desc[i] = (frame
+// offset from the pool base, data_len), or (0, 0) for a pointer or frame
+// outside the pool (or too close to its end for the header-window read).
+struct MbufArgs {
+    const uint64_t *ptrs;     // [n] host virtual addresses of the mbufs (device copy)
+    uint32_t n;
+    uint64_t pool_host;       // registered pool: host VA
+    uint64_t pool_bytes;
+    const uint8_t *pool_dev;  // its device address
+    uint32_t f_buf, f_off, f_len, hdr;   // fcgpu_mbuf_layout
+    uint2 *desc;              // [n] out
+};
+// The mbuf headers travel over PCIe: each wave fetches its 64 mbufs' first 64
+// bytes as whole 64-B segments (4 lanes x 16 B per mbuf, LDS-DMA, the k_rx
+// window pattern) -- one read request per mbuf instead of one per field --
+// then each lane takes its fields from LDS.
+__global__ __launch_bounds__(256) void k_mbuf_desc(MbufArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_hdr[4 * kWave * 64];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    uint64_t m = i < a.n ? a.ptrs[i] : 0;
+    // a pointer outside the pool is never dereferenced: read the pool's first
+    // header instead and discard it
+    const bool inpool = m >= a.pool_host && m - a.pool_host + 64 <= a.pool_bytes && a.hdr <= 64;
+    const uint64_t src = inpool ? m - a.pool_host : 0;
+    uint8_t *hl = s_hdr + wave * (kWave * 64);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t p = k * 16 + (lane >> 2);
+        const uint32_t lo = __shfl((uint32_t)src, (int)p), hi = __shfl((uint32_t)(src >> 32), (int)p);
+        const uint64_t o = ((uint64_t)hi << 32 | lo) + (lane & 3) * 16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(a.pool_dev + o),
+                                         (__attribute__((address_space(3))) void *)(hl + k * 1024), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    if (i >= a.n) return;
+    // row p of instruction k sits at k*1024 + (p%16)*64: this lane's is lane/16, lane%16
+    const uint8_t *h = hl + (lane >> 4) * 1024 + (lane & 15) * 64;
+    uint2 d = make_uint2(0, 0);
+    if (inpool) {
+        uint64_t buf;
+        uint16_t off, len;
+        memcpy(&buf, h + a.f_buf, 8);
+        memcpy(&off, h + a.f_off, 2);
+        memcpy(&len, h + a.f_len, 2);
+        const uint64_t f = buf + off;
+        // the ABI's over-read allowance (128 B past the start, 16 B past the
+        // end of every frame) must stay inside the registered pool too
+        const uint64_t reach = len + 16u > 128u ? len + 16u : 128u;
+        if (f >= a.pool_host && f - a.pool_host + reach <= a.pool_bytes)
+            d = make_uint2((uint32_t)(f - a.pool_host), len);
+    }
+    a.desc[i] = d;
+}
+
 }  // namespace fcgpu

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 11
+#define FCGPU_ABI_VERSION 12
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -393,6 +393,33 @@ void fcgpu_host_free(void *p);
  * such as an mmapped pcap are registered read-only). */
 int  fcgpu_host_register(void *p, size_t bytes, int read_only);
 int  fcgpu_host_unregister(void *p);
+
+/* mbuf ingress: the batch FromDPDKDevice::_run_task gets
+ * from rte_eth_rx_burst (elements/userlevel/fromdpdkdevice.cc:374-456) goes to
+ * the GPU as the array of mbuf pointers itself -- no Packet objects, no host
+ * copy of the frames. The packet-buffer pool (a DPDK mempool's memory: mbuf
+ * headers and data rooms, < 4 GiB) is registered once per context (contexts
+ * of other threads registering the same pool share one pinning, released
+ * with the last of them); each call copies the
+ * n pointers H2D, a kernel reads every mbuf's buf_addr / data_off / data_len
+ * straight from host memory and builds the batch's descriptors, and k_rx
+ * reads the frames' header windows from the pool over PCIe (zero copy).
+ * Outputs go to device memory (d_out), as fcgpu_process. A pointer (or a
+ * frame) outside the registered pool is never dereferenced: that packet is
+ * processed as an empty frame (FCGPU_R_MINISCULE / not checked). Field
+ * offsets are the caller's mbuf layout; FCGPU_MBUF_LAYOUT_DPDK is rte_mbuf's
+ * (DPDK >= 20.11: buf_addr @0, data_off @16, data_len @40). Asynchronous on
+ * `stream`; mbufs[] may be reused when the call returns. */
+typedef struct fcgpu_mbuf_layout {
+    uint32_t buf_addr;        /* offset of the void *buf_addr field          */
+    uint32_t data_off;        /* offset of the uint16_t data_off field       */
+    uint32_t data_len;        /* offset of the uint16_t data_len field       */
+    uint32_t header_bytes;    /* bytes of the mbuf header read (>= every field end, <= 64) */
+} fcgpu_mbuf_layout;
+#define FCGPU_MBUF_LAYOUT_DPDK {0u, 16u, 40u, 64u}
+int  fcgpu_pool_register(fcgpu_ctx *ctx, void *base, size_t bytes);
+int  fcgpu_process_mbufs(fcgpu_ctx *ctx, void *const *mbufs, uint32_t n, const fcgpu_mbuf_layout *layout,
+                         const fcgpu_out *d_out, void *stream);
 
 int  fcgpu_read_counters(fcgpu_ctx *ctx, uint64_t *out, int n);
 /* The device keeps the per-reason and per-output bins only; "count" and

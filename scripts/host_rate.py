@@ -107,6 +107,45 @@ def pcap_mpps(n=1 << 22, chunk_pkts=1 << 18, threads=1, mapped=False):
     return best if not mapped else (best, reg)
 
 
+def mbuf_mpps(n=1 << 18, reps=48, order="shuffled", streams=1):
+    """mbuf ingress (fcgpu_process_mbufs): n C2 frames in a DPDK-style
+    mempool in page-locked host memory (128-B header, 128-B headroom,
+    2048-B data room per element); each call hands the device the array of n
+    mbuf pointers, the GPU builds descriptors from the mbuf headers and reads
+    the header windows over PCIe (zero copy); outputs stay on the device."""
+    import mmap
+    from tests.test_mbuf import make_pool
+    from fastclick_amd.device import DeviceOutputs
+    rng = np.random.default_rng(1)
+    frames = synth.c2(n).frames()
+    buf, arr, base, size, ptrs = make_pool(frames, rng)
+    if order == "sequential":
+        ptrs = np.sort(ptrs)
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16)
+    # one context per rx queue (stream): the pool is registered by the first
+    ctxs = [N.Context(0, n, cfg) for _ in range(streams)]
+    try:
+        for c in ctxs:            # the first registers the pool, the others share it
+            c.pool_register(base, size)
+        ss = [torch.cuda.Stream() for _ in range(streams)]
+        outs = [DeviceOutputs(n, 16, device="cuda", perm=True, partition=N.PART_TILE) for _ in range(streams)]
+        for k in range(streams):
+            ctxs[k].process_mbufs(ptrs.ctypes.data, n, stream=ss[k].cuda_stream, **outs[k].ptrs())
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for r in range(reps):
+            k = r % streams
+            ctxs[k].process_mbufs(ptrs.ctypes.data, n, stream=ss[k].cuda_stream, **outs[k].ptrs())
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        tot = sum(int(c.counters()[N.CTR_COUNT]) for c in ctxs)
+        assert tot == n * (reps + streams), tot
+    finally:
+        for c in ctxs:
+            c.close()
+    return n * reps / dt / 1e6
+
+
 def main():
     out = {"h2d_pinned_gbs": round(h2d_gbs(), 2),
            "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)")}
@@ -115,6 +154,10 @@ def main():
     m, reg = pcap_mpps(mapped=True)
     out["pcap_ingress_mpps_4M_mapped"] = round(m, 2)
     out["pcap_mapped_registered"] = bool(reg)
+    out["mbuf_ingress_mpps_256k_shuffled"] = round(mbuf_mpps(), 2)
+    out["mbuf_ingress_mpps_256k_sequential"] = round(mbuf_mpps(order="sequential"), 2)
+    out["mbuf_ingress_mpps_256k_shuffled_2streams"] = round(mbuf_mpps(streams=2), 2)
+    out["mbuf_ingress_mpps_256k_shuffled_4streams"] = round(mbuf_mpps(streams=4), 2)
     out["process_host_mpps_1M_global"] = round(raw_host(1 << 20), 2)
     # fcgpu_process_host's pipeline chunk (kChunk in fcgpu_api.hip, overridable)
     out["chunk"] = int(os.environ.get("FCGPU_HOST_CHUNK", "131072"))
