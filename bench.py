@@ -89,10 +89,14 @@ def parse(argv=None):
                     help="> 0: the device flow table (FlowIPManagerHMP flow IDs, fcgpu_flow_enable) "
                          "behind the check, with this many IDs; its new-flow pass runs every step "
                          "(one stream: the table assigns IDs in batch order)")
-    ap.add_argument("--classify", choices=["lb", "ipclass16"], default="lb",
-                    help="lb: FlowSwitch LB_MODE hash x16 (headline); ipclass16: the survey's "
+    ap.add_argument("--classify", choices=["lb", "lbcrc", "ipclass16"], default="lb",
+                    help="lb: FlowSwitch LB_MODE hash x16 (headline); lbcrc: LB_MODE hash_crc x16 "
+                         "(CRC32-C of the IPFlow5ID, DPDK builds); ipclass16: the survey's "
                          "IPClassifier with 15 UDP dst-port ranges + '-' (program printed by the "
                          "reference compiler, tests/golden/reftests.json)")
+    ap.add_argument("--prefault", type=int, default=1,
+                    help="1: read every rotating batch once before the warmup (page translations "
+                         "resident, GPU clocks up); 0: off")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -300,9 +304,10 @@ class DeviceProcessor:
             program = (N.PROG_IPFILTER, steps, oe)
             args.nports = 16
         self.auto = args.workload == "c5"
+        classify = (N.CLS_PROGRAM if program is not None else
+                    N.CLS_LB_CRC if args.classify == "lbcrc" else N.CLS_LB_HASH)
         cfg = N.make_cfg(check_mode=N.CHECK_AUTO if self.auto else N.CHECK_IP4, offset=0 if self.auto else 14,
-                         checksum=True, hash_mode=N.HASH_FLOWID,
-                         classify=N.CLS_LB_HASH if program is None else N.CLS_PROGRAM, nports=args.nports)
+                         checksum=True, hash_mode=N.HASH_FLOWID, classify=classify, nports=args.nports)
         part = N.PART_TILE if args.partition == "tile" else N.PART_GLOBAL
         tile = part == N.PART_TILE
         self.ctx = N.Context(gpu, max(n, 1), cfg)
@@ -330,6 +335,15 @@ class DeviceProcessor:
         return self.ctx.jobs(specs)
 
     def warmup(self, steps):
+        if self.args.prefault:
+            # touch every rotating batch once (a read-only reduction), so the
+            # timed steps meet resident page translations, as buffers a NIC
+            # keeps filling would be; the warmup steps that follow stream
+            # 72 MB each, so none of this is left in the Infinity Cache
+            for a, d in self.bufs:
+                a.max()
+                d.max()
+            self.torch.cuda.synchronize()
         warm = self._jobs(0, steps)
         self.timed = self._jobs(steps, self.args.steps)   # built before the warmup
         self.ctx.set_timing(self.timing_every)      # creates the event pool now
@@ -477,8 +491,9 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                          + (f" + FlowIPManagerHMP flow table ({args.flow_capacity} IDs)"
                             if args.flow_capacity else "")
                          + " + AggregateHash + "
-                         + ("FlowSwitch hash 16 outputs" if args.classify == "lb" else
-                            "IPClassifier(15 UDP dst-port ranges, -) 16 outputs")
+                         + ({"lb": "FlowSwitch hash 16 outputs",
+                             "lbcrc": "FlowSwitch LB_MODE hash_crc 16 outputs"}.get(
+                                args.classify, "IPClassifier(15 UDP dst-port ranges, -) 16 outputs"))
                          + ("" if args.no_perm else
                             " + stable per-port partition of every 256-packet PacketBatch"
                             if args.partition == "tile" else

@@ -30,7 +30,7 @@ def reason_slot(r: int) -> int:
     return r if r < 6 else r - 1
 CHECK_IP4, MARK_IP4, CHECK_AUTO, MARK_IP6 = 0, 1, 2, 3
 HASH_NONE, HASH_FLOWID, HASH_FLOW5ID = 0, 1, 2
-CLS_NONE, CLS_LB_HASH, CLS_HASH_IP, CLS_HASHSWITCH, CLS_PROGRAM = 0, 1, 2, 3, 4
+CLS_NONE, CLS_LB_HASH, CLS_HASH_IP, CLS_HASHSWITCH, CLS_PROGRAM, CLS_LB_CRC = 0, 1, 2, 3, 4, 5
 PROG_IPFILTER, PROG_CLASSIFIER = 0, 1
 STEP_SHORT_YES = 1
 MAX_STEPS = 8192

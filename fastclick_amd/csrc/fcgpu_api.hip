@@ -34,6 +34,7 @@
 using namespace fcgpu;
 
 static_assert(kTile == FCGPU_TILE, "tile size is part of the ABI");
+static_assert(kCrcTabQ == kTile, "k_rx copies the CRC tables with one uint4 per thread");
 static constexpr size_t kCtrWords = (size_t)FCGPU_CTR_SHARDS * FCGPU_NCOUNTERS;
 
 namespace {
@@ -172,6 +173,7 @@ struct fcgpu_ctx {
     unsigned long long *d_ctr = nullptr;      // active counter vector
     unsigned long long *d_ctr_own = nullptr;  // context-owned vector
     uint4 *d_prog = nullptr;                  // decision program (FCGPU_CLS_PROGRAM)
+    uint4 *d_crc = nullptr;                   // LB_CRC slicing tables (crc32c_u32_tab)
     uint32_t prog_n = 0, prog_kind = 0, prog_q = 0, prog_tab = 0;
     int32_t prog_all = -1;
     std::vector<fcgpu_step> prog_host;   // the installed program (capture reach)
@@ -285,7 +287,7 @@ static hipEvent_t take_event(fcgpu_ctx *c) {
 // itself (timestamps of the kernel, not of the stream around it).
 template <int CM, bool CK, int PART, bool PROG, bool L4, bool FLOW = false>
 static void launch_rx(const RxArgs &a, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-    const size_t lds = PROG ? prog_lds_bytes(a.cfg) : 0;
+    const size_t lds = prog_lds_bytes(a.cfg);   // program steps (PROG) or CRC tables (LB_CRC), else 0
     if (ev0)
         hipExtLaunchKernelGGL((k_rx<CM, CK, PART, PROG, L4, FLOW>), dim3(a.ntiles), dim3(kTile), lds, s, ev0, ev1,
                               0, a);
@@ -631,6 +633,7 @@ void fcgpu_close(fcgpu_ctx *c) {
         hipFree(c->d_totals);
         hipFree(c->d_ctr_own);
         hipFree(c->d_prog);
+        hipFree(c->d_crc);
         hipFree(c->d_verdict);
         hipFree(c->d_arena);
         hipFree(c->d_desc);
@@ -715,7 +718,9 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     const bool ip4mode = cfg->check_mode == FCGPU_CHECK_IP4 || cfg->check_mode == FCGPU_MARK_IP4;
     if (cfg->vlan_ethertype > 0xffff) return fail(c, FCGPU_EINVAL, "bad vlan_ethertype");
     if (cfg->hash_mode > FCGPU_HASH_FLOW5ID) return fail(c, FCGPU_EINVAL, "bad hash_mode");
-    if (cfg->classify > FCGPU_CLS_PROGRAM) return fail(c, FCGPU_EINVAL, "bad classify mode");
+    if (cfg->classify > FCGPU_CLS_LB_CRC) return fail(c, FCGPU_EINVAL, "bad classify mode");
+    if (cfg->classify == FCGPU_CLS_LB_CRC && !(cfg->check_mode == FCGPU_CHECK_IP4 || cfg->check_mode == FCGPU_MARK_IP4))
+        return fail(c, FCGPU_EINVAL, "LB_MODE hash_crc hashes IPFlow5ID: IPv4 check modes only");
     if (cfg->l4_mode > FCGPU_L4_TCP) return fail(c, FCGPU_EINVAL, "bad l4_mode");
     if (cfg->l4_mode != FCGPU_L4_NONE && !ip4mode)
         return fail(c, FCGPU_EINVAL, "l4_mode needs an IPv4 check mode (CHECK_IP4 or MARK_IP4)");
@@ -756,6 +761,21 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     memcpy(d.badsrc, cfg->badsrc, sizeof(d.badsrc));
     memcpy(d.gooddst, cfg->gooddst, sizeof(d.gooddst));
     memcpy(d.bad6, cfg->bad6, sizeof(d.bad6));
+    if (cfg->classify == FCGPU_CLS_LB_CRC && !c->d_crc) {
+        // T_k[b] = crc32c_u32(b << 8k, 0): rte_hash_crc_4byte's 32 shift steps
+        // are linear, so a word is four lookups (fcgpu_device.hh)
+        std::vector<uint32_t> t(1024);
+        for (uint32_t k = 0; k < 4; ++k)
+            for (uint32_t b = 0; b < 256; ++b) {
+                uint32_t x = b << (8 * k);
+                for (int j = 0; j < 32; ++j) x = (x >> 1) ^ (0x82F63B78u & (0u - (x & 1u)));
+                t[256 * k + b] = x;
+            }
+        HIPCHK(c, hipSetDevice(c->device));
+        HIPCHK(c, hipMalloc(&c->d_crc, sizeof(uint32_t) * 1024));
+        HIPCHK(c, hipMemcpy(c->d_crc, t.data(), sizeof(uint32_t) * 1024, hipMemcpyHostToDevice));
+    }
+    d.crc_tab = cfg->classify == FCGPU_CLS_LB_CRC ? c->d_crc : nullptr;
     d.prog = c->d_prog;
     d.prog_n = c->prog_n;
     d.prog_q = c->prog_q;

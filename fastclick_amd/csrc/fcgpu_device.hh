@@ -51,6 +51,7 @@ struct DevCfg {
     uint32_t prog_tab;        // uint4 index where the int16 jump tables start
     uint32_t prog_kind;
     int32_t prog_all;         // >= 0: empty program, every packet -> this output
+    const uint4 *crc_tab;     // FCGPU_CLS_LB_CRC: 4 x 256 u32 slicing tables (1 KB each)
 };
 
 // Device step: x = (u16)offset | flags << 16, y = value, z = mask,
@@ -177,6 +178,36 @@ __device__ __forceinline__ int lb_port(uint32_t h, uint32_t n, uint32_t m) {
     return n == 1 ? 0 : (int)(x - q * n);
 }
 
+// rte_hash_crc_4byte(data, crc) (DPDK rte_hash_crc.h: _mm_crc32_u32(crc, data)):
+// CRC32-C, reflected polynomial 0x82F63B78, no inversion -- a reflected CRC
+// takes the 32-bit word at once (xor) and shifts it through bit by bit.
+__device__ __forceinline__ uint32_t crc32c_u32(uint32_t data, uint32_t crc) {
+    crc ^= data;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) crc = (crc >> 1) ^ (0x82F63B78u & (0u - (crc & 1u)));
+    return crc;
+}
+// The same through byte-sliced tables: the 32 shifts are linear over GF(2),
+// so crc32c_u32(d, c) = XOR_k T_k[byte k of (c ^ d)] with T_k[b] =
+// crc32c_u32(b << 8k, 0) -- four LDS reads instead of 32 shift steps. The
+// tables (4 KB) are built on the host (fcgpu_configure) and copied to LDS by
+// the workgroups of an LB_CRC launch.
+__device__ __forceinline__ uint32_t crc32c_u32_tab(const uint32_t *t, uint32_t data, uint32_t crc) {
+    const uint32_t x = crc ^ data;
+    return t[x & 0xff] ^ t[256 + ((x >> 8) & 0xff)] ^ t[512 + ((x >> 16) & 0xff)] ^ t[768 + (x >> 24)];
+}
+// ipv4_hash_crc(IPFlow5ID, 0) (include/click/dpdk_glue.hh:13-27): proto, saddr,
+// daddr, then the ports word; a non-first fragment's IPFlow5ID has zero
+// addresses and (here) zero ports (lib/ipflowid.cc:34-38)
+__device__ __forceinline__ uint32_t flow5_crc(const uint4 *dyn, uint32_t proto, uint32_t sa, uint32_t da,
+                                              uint32_t ports) {
+    if (dyn) {
+        const uint32_t *t = reinterpret_cast<const uint32_t *>(dyn);
+        return crc32c_u32_tab(t, ports, crc32c_u32_tab(t, da, crc32c_u32_tab(t, sa, crc32c_u32_tab(t, proto, 0u))));
+    }
+    return crc32c_u32(ports, crc32c_u32(da, crc32c_u32(sa, crc32c_u32(proto, 0u))));
+}
+
 // HashSwitch::process / LoadBalancer::hash_ip byte-sum (hashswitch.cc:50-66,
 // loadbalancer.hh:227-243)
 __device__ __forceinline__ int bytesum_port(const FrameView &f, uint32_t len, int o, int l, uint32_t n) {
@@ -262,8 +293,13 @@ constexpr uint32_t kProgLdsQ = 160;
 __host__ __device__ inline bool prog_in_lds(const DevCfg &c) {
     return c.classify == FCGPU_CLS_PROGRAM && c.prog_all < 0 && c.prog_q <= kProgLdsQ;
 }
-// dynamic LDS of a k_rx launch: only program mode pays for the step cache
-inline size_t prog_lds_bytes(const DevCfg &c) { return prog_in_lds(c) ? sizeof(uint4) * c.prog_q : 0; }
+// dynamic LDS of a k_rx launch: only program mode pays for the step cache,
+// only LB_CRC for its 4-KB slicing tables
+constexpr uint32_t kCrcTabQ = 256;          // 4 x 256 u32 = 256 uint4
+__host__ __device__ inline bool crc_in_lds(const DevCfg &c) { return c.classify == FCGPU_CLS_LB_CRC && c.crc_tab; }
+inline size_t prog_lds_bytes(const DevCfg &c) {
+    return prog_in_lds(c) ? sizeof(uint4) * c.prog_q : crc_in_lds(c) ? sizeof(uint4) * kCrcTabQ : 0;
+}
 __device__ __forceinline__ uint32_t run_program(const DevCfg &c, const FrameView &f, const fcgpu_anno &an,
                                                 const uint4 *sprog) {
     if (sprog) return run_program_on(c, f, an, sprog);
@@ -416,6 +452,14 @@ __device__ __forceinline__ void process_packet(const DevCfg &c, const FrameView 
     r.hash = hv;
     switch (c.classify) {
     case FCGPU_CLS_LB_HASH: r.port = (uint32_t)lb_port(hv, c.nports, c.lb_magic); break;
+    case FCGPU_CLS_LB_CRC: {
+        const uint32_t w1 = f.rd32(an.nh + 4), w2 = f.rd32(an.nh + 8);
+        const bool first = (bswap16(w1 >> 16) & 0x1fff) == 0;
+        const uint32_t crc = flow5_crc(sprog, (w2 >> 8) & 0xff, first ? f.rd32(an.nh + 12) : 0u,
+                                       first ? f.rd32(an.nh + 16) : 0u, first ? f.rd32(an.th) : 0u);
+        r.port = (uint32_t)lb_port(crc, c.nports, c.lb_magic);
+        break;
+    }
     case FCGPU_CLS_HASH_IP: r.port = (uint32_t)bytesum_port(f, an.length, 26, 8, c.nports); break;
     case FCGPU_CLS_HASHSWITCH:
         r.port = (uint32_t)bytesum_port(f, an.length, c.hs_offset, c.hs_length, c.nports);
@@ -491,9 +535,16 @@ __device__ __forceinline__ bool ip4_fast(const DevCfg &c, const FrameView &f, ui
         if (c.hash_mode == FCGPU_HASH_FLOW5ID) hv ^= (h[2] >> 8) & 0xff;
     }
     uint32_t port = 0;
-    if (c.classify == FCGPU_CLS_LB_HASH) port = (uint32_t)lb_port(hv, c.nports, c.lb_magic);
-    else if (c.classify != FCGPU_CLS_NONE && (!PROG || c.classify != FCGPU_CLS_PROGRAM))
+    if (c.classify == FCGPU_CLS_LB_HASH) {
+        port = (uint32_t)lb_port(hv, c.nports, c.lb_magic);
+    } else if (c.classify == FCGPU_CLS_LB_CRC) {       // wave-uniform
+        const bool first = (bswap16(h[1] >> 16) & 0x1fff) == 0;
+        const uint32_t crc = flow5_crc(sprog, (h[2] >> 8) & 0xff, first ? h[3] : 0u, first ? h[4] : 0u,
+                                       first ? h[5] : 0u);
+        port = (uint32_t)lb_port(crc, c.nports, c.lb_magic);
+    } else if (c.classify != FCGPU_CLS_NONE && (!PROG || c.classify != FCGPU_CLS_PROGRAM)) {
         return false;                                  // byte-sum classifiers: general path
+    }
     r.reason = reason;
     r.hash = ok ? hv : 0u;
     fcgpu_anno &an = r.an;
@@ -1101,7 +1152,7 @@ template <int CM, bool CK, int PART, bool PROG, bool L4, bool FLOW = false,
 __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4 * kWave * kWin];
     __shared__ uint32_t s_cnt[4][kMaxBins];
-    extern __shared__ uint4 s_prog[];           // prog_lds_bytes(cfg) at launch
+    extern __shared__ uint4 s_prog[];           // prog_lds_bytes(cfg) at launch: program steps or CRC tables
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t tile = blockIdx.x;
     const uint32_t i = tile * kTile + threadIdx.x;
@@ -1112,10 +1163,12 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
     for (int k = 0; k < 4; ++k) glds16(win_src(A.arena, d.x, lane, k), wl + k * 1024);
     // decision program: the block's LDS copy when it fits (block-uniform)
     const bool prog_lds = PROG && prog_in_lds(A.cfg);
+    const bool crc_lds = !PROG && crc_in_lds(A.cfg);          // block-uniform
     if (prog_lds && threadIdx.x < A.cfg.prog_q) s_prog[threadIdx.x] = A.cfg.prog[threadIdx.x];
+    if (crc_lds) s_prog[threadIdx.x] = A.cfg.crc_tab[threadIdx.x];   // kCrcTabQ == kTile
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (prog_lds) __syncthreads();
-    rx_tile<CM, CK, PART, PROG, L4, FAST, FLOW>(A, tile, d, wl, s_cnt, prog_lds ? s_prog : nullptr);
+    if (prog_lds || crc_lds) __syncthreads();
+    rx_tile<CM, CK, PART, PROG, L4, FAST, FLOW>(A, tile, d, wl, s_cnt, prog_lds || crc_lds ? s_prog : nullptr);
 }
 
 // Exclusive scan of one output's per-tile counts (in place) and its total.

@@ -214,6 +214,9 @@ extern "C" int fcclick_run_ex(const char *conf, const uint8_t *arena, const uint
         }
     }
     std::string er = el->read_handler("error");
+    // what the element still holds (TIMER -1 and no flush) is killed back into
+    // the pool: the element goes before the pool does
+    el.reset();
     if (!er.empty()) {
         copy_err(er, err, errcap);
         return -2;
@@ -276,6 +279,7 @@ double bench_one(const char *conf, const uint8_t *arena, const uint32_t *desc, u
     auto t1 = std::chrono::steady_clock::now();
     const double s = std::chrono::duration<double>(t1 - t0).count();
     e = el->read_handler("error");
+    el.reset();                      // before the pool its packets belong to
     if (!e.empty()) return -2.0;
     return (double)n * reps / s;
 }

@@ -37,7 +37,7 @@
 //   VLAN_ETHERTYPE (default 0x8100)          -- VLANDecap(ETHERTYPE) + Strip(14) (MODE AUTO)
 //   MODE MARK6                               -- MarkIP6Header(OFFSET)
 //   BADADDRS, PROCESS_EH                     -- CheckIP6Header (IPv6, MODE AUTO)
-//   N / LB_MODE hash|hash_agg|hash_ip        -- FlowSwitch / LoadBalancer
+//   N / LB_MODE hash|hash_agg|hash_ip|hash_crc -- FlowSwitch / LoadBalancer
 //   HASHSWITCH "OFFSET LENGTH"               -- HashSwitch
 //   PROGRAM "<program text>", PROGRAM_KIND IPFILTER|CLASSIFIER
 //                                            -- IPFilter / IPClassifier / Classifier:
@@ -144,6 +144,7 @@ class RxCore {
             } else if (k == "LB_MODE") {
                 if (v == "hash" || v == "hash_agg") _cfg.classify = FCGPU_CLS_LB_HASH;
                 else if (v == "hash_ip") _cfg.classify = FCGPU_CLS_HASH_IP;
+                else if (v == "hash_crc") _cfg.classify = FCGPU_CLS_LB_CRC;
                 else return err(errh, "unsupported LB_MODE " + v);
             } else if (k == "HASHSWITCH") {
                 long o, l;
@@ -244,6 +245,7 @@ class RxCore {
         if (_cfg.l4_mode != FCGPU_L4_NONE && !ip4) return err(errh, "L4 needs MODE CHECK or MARK");
         if (_flow_cap && !ip4) return err(errh, "FLOW_CAPACITY needs MODE CHECK or MARK");
         if (_cfg.rewrite && !ip4) return err(errh, "DEC_TTL / SET_CHECKSUM need MODE CHECK or MARK");
+        if (_cfg.classify == FCGPU_CLS_LB_CRC && !ip4) return err(errh, "LB_MODE hash_crc needs MODE CHECK or MARK");
         if (_cfg.classify == FCGPU_CLS_PROGRAM) {
             if (_prog.output_everything >= (int32_t)_cfg.nports && _prog.output_everything != 0x7fff)
                 return err(errh, "PROGRAM sends everything to a missing output");

@@ -104,6 +104,12 @@ extern "C" {
 #define FCGPU_CLS_HASHSWITCH 3  /* HashSwitch(hs_offset, hs_length), nports = MAX        */
 #define FCGPU_CLS_PROGRAM    4  /* decision program set by fcgpu_set_program: IPFilter /
                                    IPClassifier or Classifier                          */
+#define FCGPU_CLS_LB_CRC     5  /* LoadBalancer direct_hash_crc (DPDK builds,
+                                   include/click/loadbalancer.hh:563-569): c = CRC32-C of
+                                   the IPFlow5ID words proto, saddr, daddr, ports from 0
+                                   (ipv4_hash_crc, include/click/dpdk_glue.hh:13-27, via
+                                   rte_hash_crc_4byte = the SSE4.2 crc32 instruction), port =
+                                   ((c>>16) ^ (c&0xffff)) % nports. IPv4 check modes only */
 
 /* l4_mode: a CheckUDPHeader / CheckTCPHeader after the IPv4 check (CHECK_IP4 or
  * MARK_IP4 only). The checksum covers the whole L4 segment, so with

@@ -107,6 +107,29 @@ int fco_lb_hash_port(uint32_t h, int n)
     return (int)(((h >> 16) ^ (h & 65535)) % (uint32_t)n);
 }
 
+/* rte_hash_crc_4byte (DPDK rte_hash_crc.h, crc32c_sse42_u32 = _mm_crc32_u32(init,
+ * data); crc32c_1word in software): CRC32-C, reflected polynomial 0x82F63B78, no
+ * pre/post inversion. */
+uint32_t fco_crc32c_u32(uint32_t data, uint32_t crc)
+{
+    crc ^= data;
+    for (int k = 0; k < 32; k++)
+        crc = (crc >> 1) ^ (0x82F63B78u & (0u - (crc & 1u)));
+    return crc;
+}
+
+/* ipv4_hash_crc(&IPFlow5ID, sizeof, 0) (include/click/dpdk_glue.hh:13-27): proto,
+ * saddr, daddr, then the ports word (the struct's third u32), folded as
+ * direct_hash_crc does (include/click/loadbalancer.hh:563-569). */
+int fco_lb_crc_port(uint32_t proto, uint32_t saddr, uint32_t daddr, uint32_t ports, int n)
+{
+    uint32_t c = fco_crc32c_u32(proto, 0);
+    c = fco_crc32c_u32(saddr, c);
+    c = fco_crc32c_u32(daddr, c);
+    c = fco_crc32c_u32(ports, c);
+    return (int)(((c >> 16) ^ (c & 65535)) % (uint32_t)n);
+}
+
 /* include/click/loadbalancer.hh:227-243 (hash_ip). */
 int fco_hash_ip_port(const uint8_t *data, uint32_t len, int n)
 {
@@ -466,6 +489,15 @@ void fco_process_packet(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, fco_
     int port = 0;
     switch (c->classify) {
     case FCGPU_CLS_LB_HASH:    port = fco_lb_hash_port(h, (int)c->nports); break;
+    case FCGPU_CLS_LB_CRC: {
+        /* IPFlow5ID(p): a non-first fragment keeps zero addresses (and, here,
+         * zero ports), lib/ipflowid.cc:34-38 */
+        const uint8_t *nh = f + a->nh, *th = f + a->th;
+        int first = (be16(nh + 6) & 0x1fff) == 0;
+        port = fco_lb_crc_port(nh[9], first ? le32(nh + 12) : 0, first ? le32(nh + 16) : 0,
+                               first ? le32(th) : 0, (int)c->nports);
+        break;
+    }
     case FCGPU_CLS_HASH_IP:    port = fco_hash_ip_port(f, a->length, (int)c->nports); break;
     case FCGPU_CLS_HASHSWITCH: port = fco_hashswitch_port(f, a->length, c->hs_offset,
                                                            c->hs_length, (int)c->nports); break;

@@ -74,6 +74,8 @@ uint32_t fco_ipflowid_hash(uint32_t saddr_raw, uint16_t sport_net,
 uint32_t fco_ip6flowid_hash(const uint8_t src[16], uint16_t sport_net,
                             const uint8_t dst[16], uint16_t dport_net); /* A15 */
 int fco_lb_hash_port(uint32_t h, int n);                         /* A8 direct_hash */
+uint32_t fco_crc32c_u32(uint32_t data, uint32_t crc);           /* rte_hash_crc_4byte */
+int fco_lb_crc_port(uint32_t proto, uint32_t saddr, uint32_t daddr, uint32_t ports, int n); /* A8 direct_hash_crc */
 int fco_hash_ip_port(const uint8_t *data, uint32_t len, int n);  /* A8 hash_ip */
 int fco_hashswitch_port(const uint8_t *data, uint32_t len, int off, int l, int n); /* A9 */
 void fco_classify_each_packet(int nbatches, const int *port, uint32_t n,

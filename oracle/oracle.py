@@ -41,6 +41,8 @@ def load():
     lib.fco_ip6flowid_hash.argtypes = [C.c_void_p, C.c_uint16, C.c_void_p, C.c_uint16]
     lib.fco_lb_hash_port.restype = C.c_int
     lib.fco_lb_hash_port.argtypes = [C.c_uint32, C.c_int]
+    lib.fco_crc32c_u32.restype = C.c_uint32
+    lib.fco_crc32c_u32.argtypes = [C.c_uint32, C.c_uint32]
     lib.fco_process_batch2.restype = None
     lib.fco_process_batch2.argtypes = [C.POINTER(N.fcgpu_cfg), C.c_void_p, C.c_void_p, C.c_uint32,
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,

@@ -38,6 +38,8 @@ for s in "${ST[@]}"; do
     kt_long) kt kt_long 300 --steps 200 --warmup 20 --no-cpu ;;
     kt_w40) kt kt_w40 300 --gpus 1 --steps 20 --warmup 40 --no-cpu ;;
     kt_notime) kt kt_notime 300 $DRV --no-cpu --no-timing ;;
+    kt_nopf) kt kt_nopf 300 $DRV --no-cpu --prefault 0 ;;
+    kt_nopf_s1) kt kt_nopf_s1 300 $DRV --no-cpu --prefault 0 --streams 1 ;;
     kt_notime_s1) kt kt_notime_s1 300 $DRV --no-cpu --no-timing --streams 1 ;;
     kt_w40_s1) kt kt_w40_s1 300 --gpus 1 --steps 20 --warmup 40 --no-cpu --streams 1 ;;
     bench2) step bench2 300 python bench.py $DRV --no-cpu ;;
@@ -51,6 +53,10 @@ for s in "${ST[@]}"; do
              pmc pmc_fetch_c4flow FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --workload c4 --flow-capacity 2000000
              pmc pmc_ea_c4flow TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum -- --steps 40 --warmup 4 --no-cpu --no-timing --workload c4 --flow-capacity 2000000
              pmc pmc_write_c4flow WRITE_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --workload c4 --flow-capacity 2000000 ;;
+    crcvar) for v in "--classify lbcrc" "--workload c4 --classify lbcrc"; do
+                n=$(echo "$v" | tr -d ' -' | cut -c1-40)
+                step "var_$n" 300 python bench.py --steps 200 --warmup 20 --no-cpu $v
+              done ;;
     flowvar) for v in "--flow-capacity 1" "--workload c3 --flow-capacity 20000" "--workload c4 --flow-capacity 2000000" \
                       "--partition global" "--classify ipclass16" "--workload c4 --classify ipclass16"; do
                 n=$(echo "$v" | tr -d ' -' | cut -c1-40)
