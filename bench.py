@@ -89,6 +89,12 @@ def parse(argv=None):
                     help="> 0: the device flow table (FlowIPManagerHMP flow IDs, fcgpu_flow_enable) "
                          "behind the check, with this many IDs; its new-flow pass runs every step "
                          "(one stream: the table assigns IDs in batch order)")
+    ap.add_argument("--flow-manager", choices=["hmp", "imp"], default="hmp",
+                    help="hmp: FlowIPManagerHMP IDs 0,1,2,...; imp: VirtualFlowManagerIMP (free-ID "
+                         "stack; with --flow-timeout, every packet stamps its flow and the maintainer "
+                         "run is timed outside the timed region: flow_maintain_ms)")
+    ap.add_argument("--flow-timeout", type=int, default=0, help="imp: TIMEOUT in s (0: none)")
+    ap.add_argument("--flow-recycle-ms", type=int, default=1000, help="imp: RECYCLE_INTERVAL in ms")
     ap.add_argument("--classify", choices=["lb", "lbcrc", "ipclass16"], default="lb",
                     help="lb: FlowSwitch LB_MODE hash x16 (headline); lbcrc: LB_MODE hash_crc x16 "
                          "(CRC32-C of the IPFlow5ID, DPDK builds); ipclass16: the survey's "
@@ -313,8 +319,14 @@ class DeviceProcessor:
         self.ctx = N.Context(gpu, max(n, 1), cfg)
         if program is not None:
             self.ctx.set_program(*program)
+        self.maintain_ms = None
         if args.flow_capacity:
-            self.ctx.flow_enable(args.flow_capacity)
+            if args.flow_manager == "imp":
+                self.ctx.flow_configure(N.FLOW_MGR_IMP, args.flow_capacity, args.flow_timeout,
+                                        args.flow_recycle_ms)
+                self.ctx.flow_set_time(1_000_000)
+            else:
+                self.ctx.flow_enable(args.flow_capacity)
         self.streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
         self.outs = [DeviceOutputs(max(n, 1), args.nports, device=dev, verdict=True, hash=True, anno=False,
                                    perm=(not args.no_perm) and not tile,
@@ -350,8 +362,28 @@ class DeviceProcessor:
         self.ctx.run_jobs(warm)
         self.torch.cuda.synchronize()
         self.ctx.read_timing()                      # drop warmup samples
+        if self.args.flow_capacity and self.args.flow_manager == "imp" and self.args.flow_timeout:
+            self._time_maintainer()
         self.ctx.set_timing(self.timing_every)      # sample count restarts at the timed region
         self.ctx.use_counters(self.ctr.data_ptr())  # timed steps count into the tensor
+
+    def _time_maintainer(self):
+        """Maintainer runs at the batches' own time stamp until one walks the
+        wheel bucket holding the batch's flows (lastseen not in the past:
+        every flow is rescheduled, virtualflowmanager.hh:174-180, so the table
+        is unchanged); that run's device time, table rebuild included."""
+        torch = self.torch
+        s = self.streams[0]
+        best = 0.0
+        te = self.args.flow_timeout * max(1, 1000 // self.args.flow_recycle_ms)
+        for _ in range(min(te + 2, 256)):             # run te + 1 walks the warmup's bucket
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            self.ctx.flow_maintain(1_000_000, stream=s.cuda_stream)
+            e1.record(s)
+            torch.cuda.synchronize()
+            best = max(best, e0.elapsed_time(e1))
+        self.maintain_ms = best
 
     def run_timed(self):
         self.ctx.run_jobs(self.timed)
@@ -402,6 +434,7 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
             dist.barrier()
         elapsed = time.perf_counter() - t0
         timing = proc.timing()
+        maintain_ms = getattr(proc, "maintain_ms", None)
 
         # after the timed region: max time over ranks, counters summed over
         # ranks (RCCL all-reduce of the device vector), per-output offsets
@@ -488,7 +521,10 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
             "workload": (wl
                          + ("; StripEtherVLANHeader + CheckIP6Header/CheckIPHeader(CHECKSUM true)"
                             if auto else "; CheckIPHeader(CHECKSUM true)")
-                         + (f" + FlowIPManagerHMP flow table ({args.flow_capacity} IDs)"
+                         + ((f" + FlowIPManagerHMP flow table ({args.flow_capacity} IDs)"
+                             if args.flow_manager == "hmp" else
+                             f" + VirtualFlowManagerIMP flow table (CAPACITY {args.flow_capacity}, "
+                             f"TIMEOUT {args.flow_timeout}, RECYCLE_INTERVAL {args.flow_recycle_ms} ms)")
                             if args.flow_capacity else "")
                          + " + AggregateHash + "
                          + ({"lb": "FlowSwitch hash 16 outputs",
@@ -506,6 +542,7 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
             "packets_per_step": args.packets if args.shard == "strong" else args.packets * world,
             "hbm_batches": args.nbuf,
             "nports": args.nports,
+            **({"flow_maintain_ms": round(maintain_ms, 4)} if maintain_ms is not None else {}),
             "parallelism": (f"batch-sharded x{world}" if args.shard == "weak" else
                             f"one batch split x{world} (dist.shard_range)")
                            + f", counters all-reduced after the timed region "

@@ -14,7 +14,7 @@ LIBFCGPU = os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 12
+ABI_VERSION = 13
 SPAN_SLOTS = 3
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
@@ -107,6 +107,17 @@ FLOW_NONE = 0xFFFFFFFF
 FLOW_FULL = 0xFFFFFFFE
 FLOW_MAX_BATCH = 64 * ((1 << 14) + 64)   # FCGPU_FLOW_MAX_BATCH
 MAX_FLOWS = 1 << 23
+FLOW_MGR_HMP = 0
+FLOW_MGR_IMP = 1
+
+
+class fcgpu_flow_config(C.Structure):
+    _fields_ = [("manager", C.c_uint32), ("capacity", C.c_uint32), ("timeout_s", C.c_uint32),
+                ("recycle_ms", C.c_uint32)]
+
+
+class fcgpu_flow_stat(C.Structure):
+    _fields_ = [(k, C.c_uint32) for k in ("manager", "capacity", "count", "free_ids", "pending", "epochs")]
 
 
 class fcgpu_out(C.Structure):
@@ -186,6 +197,10 @@ FCGPU_SYMBOLS = {
     "fcgpu_flow_enable": (C.c_int, [C.c_void_p, C.c_uint32]),
     "fcgpu_flow_reset": (C.c_int, [C.c_void_p]),
     "fcgpu_flow_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
+    "fcgpu_flow_configure": (C.c_int, [C.c_void_p, C.POINTER(fcgpu_flow_config)]),
+    "fcgpu_flow_set_time": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "fcgpu_flow_maintain": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
+    "fcgpu_flow_stats": (C.c_int, [C.c_void_p, C.POINTER(fcgpu_flow_stat)]),
     "fcgpu_host_alloc": (C.c_void_p, [C.c_size_t]),
     "fcgpu_host_free": (None, [C.c_void_p]),
     "fcgpu_pool_register": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
@@ -405,6 +420,23 @@ class Context:
     def flow_enable(self, max_flows: int):
         """Device flow table (FlowIPManagerHMP semantics); 0 disables it."""
         self._chk(self.lib.fcgpu_flow_enable(self.h, max_flows), "fcgpu_flow_enable")
+
+    def flow_configure(self, manager=FLOW_MGR_IMP, capacity=65536, timeout_s=0, recycle_ms=1000):
+        """Flow manager: FLOW_MGR_HMP (IDs 0, 1, ...) or FLOW_MGR_IMP (free-ID
+        stack, timeouts on a timer wheel); capacity 0 disables the table."""
+        fc = fcgpu_flow_config(manager, capacity, timeout_s, recycle_ms)
+        self._chk(self.lib.fcgpu_flow_configure(self.h, C.byref(fc)), "fcgpu_flow_configure")
+
+    def flow_set_time(self, now_ms: int):
+        self._chk(self.lib.fcgpu_flow_set_time(self.h, now_ms & 0xFFFFFFFF), "fcgpu_flow_set_time")
+
+    def flow_maintain(self, now_ms: int, stream=None):
+        self._chk(self.lib.fcgpu_flow_maintain(self.h, now_ms & 0xFFFFFFFF, stream), "fcgpu_flow_maintain")
+
+    def flow_stats(self) -> dict:
+        st = fcgpu_flow_stat()
+        self._chk(self.lib.fcgpu_flow_stats(self.h, C.byref(st)), "fcgpu_flow_stats")
+        return {k: getattr(st, k) for k, _ in fcgpu_flow_stat._fields_}
 
     def flow_reset(self):
         self._chk(self.lib.fcgpu_flow_reset(self.h), "fcgpu_flow_reset")

@@ -200,6 +200,10 @@ struct fcgpu_ctx {
     FlowArgs fl{};            // device pointers; fl.slots == nullptr: disabled
     uint32_t *flow_hint = nullptr;    // mapped: size class of the last finish's misses (kHint*)
     uint32_t flow_epoch = 0;          // batches through the table (FlowArgs::epoch)
+    fcgpu_flow_config flow_conf{};    // the manager (fcgpu_flow_configure)
+    uint4 *flow_spare = nullptr;      // IMP with timeouts: the slot array a maintainer run rebuilds into
+    MaintArgs maint{};                // IMP with timeouts: released list, run numbers, timeout parameters
+    uint32_t flow_now = 0;            // fcgpu_flow_set_time
     hipEvent_t flow_order[2] = {nullptr, nullptr};   // orders fcgpu_process against span submissions
     // mbuf ingress (fcgpu_pool_register / fcgpu_process_mbufs)
     uint64_t pool_host = 0, pool_bytes = 0;
@@ -541,15 +545,20 @@ static void flow_free(fcgpu_ctx *c) {
     FlowArgs &F = c->fl;
     for (void *p : {(void *)F.slots, (void *)F.claim, (void *)F.first, (void *)F.miss_key, (void *)F.miss_slot,
                     (void *)F.miss_first, (void *)F.missmask, (void *)F.firstmask, (void *)F.wordpre,
-                    (void *)F.state})
+                    (void *)F.state, (void *)F.stack, (void *)F.lastseen, (void *)F.wheel, (void *)F.wheel_len,
+                    (void *)c->flow_spare, (void *)c->maint.qbsr, (void *)c->maint.dead, (void *)c->maint.rbuf,
+                    (void *)c->maint.counts})
         if (p) hipFree(p);
     if (c->flow_hint) hipHostFree(c->flow_hint);
     c->flow_hint = nullptr;
+    c->flow_spare = nullptr;
     F = FlowArgs{};
+    c->maint = MaintArgs{};
+    c->flow_conf = fcgpu_flow_config{};
     c->max_flows = c->flow_slots = c->flow_words = 0;
 }
 
-// Empty table, IDs from 0 (synchronous).
+// Empty table, IDs from the start (synchronous).
 static int flow_clear(fcgpu_ctx *c) {
     FlowArgs &F = c->fl;
     HIPCHK(c, memset_sync(F.slots, 0, sizeof(uint4) * c->flow_slots));
@@ -559,6 +568,19 @@ static int flow_clear(fcgpu_ctx *c) {
     HIPCHK(c, memset_sync(F.firstmask, 0, sizeof(uint64_t) * c->flow_words));
     c->flow_epoch = 0;
     HIPCHK(c, memset_sync(F.state, 0, sizeof(uint32_t) * 16));
+    if (F.stack) {
+        // FlowManagerIMPState: 0 .. cap-1 pushed in order (virtualflowmanager.hh:113-115);
+        // the device stack holds 1 .. cap-1 (ID 0 is the reference's "full")
+        std::vector<uint32_t> ids(c->max_flows);
+        for (uint32_t i = 0; i < c->max_flows; ++i) ids[i] = i + 1;
+        HIPCHK(c, hipMemcpy(F.stack, ids.data(), sizeof(uint32_t) * ids.size(), hipMemcpyHostToDevice));
+    }
+    if (F.lastseen) {
+        HIPCHK(c, memset_sync(F.lastseen, 0, sizeof(uint32_t) * F.wstride));
+        HIPCHK(c, memset_sync(F.wheel_len, 0, sizeof(uint32_t) * (F.wmask + 1)));
+        HIPCHK(c, memset_sync(c->maint.dead, 0, sizeof(uint32_t) * F.wstride));
+        c->maint.seq = 0;
+    }
     // an empty table expects many new flows: the grid-wide finish first
     const uint32_t big = kHintBig;
     HIPCHK(c, hipMemcpy(F.state + kFsHint, &big, sizeof big, hipMemcpyHostToDevice));
@@ -566,16 +588,43 @@ static int flow_clear(fcgpu_ctx *c) {
     return FCGPU_OK;
 }
 
-int fcgpu_flow_enable(fcgpu_ctx *c, uint32_t max_flows) {
-    if (!c) return FCGPU_EINVAL;
-    if (max_flows > FCGPU_MAX_FLOWS) return fail(c, FCGPU_EINVAL, "max_flows above FCGPU_MAX_FLOWS");
+static uint32_t pow2_at_least(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+int fcgpu_flow_configure(fcgpu_ctx *c, const fcgpu_flow_config *fc) {
+    if (!c || !fc) return FCGPU_EINVAL;
+    if (fc->manager != FCGPU_FLOW_MGR_HMP && fc->manager != FCGPU_FLOW_MGR_IMP)
+        return fail(c, FCGPU_EINVAL, "flow manager: FCGPU_FLOW_MGR_HMP or FCGPU_FLOW_MGR_IMP");
+    const bool imp = fc->manager == FCGPU_FLOW_MGR_IMP;
+    if (!imp && fc->timeout_s) return fail(c, FCGPU_EINVAL, "flow timeouts need FCGPU_FLOW_MGR_IMP");
+    // IMP: CAPACITY rounded up to a power of two (virtualflowmanager.hh:85), IDs 1 .. cap-1
+    const uint32_t cap = imp && fc->capacity ? pow2_at_least(std::max(fc->capacity, 2u)) : fc->capacity;
+    const uint32_t max_flows = imp && cap ? cap - 1u : cap;
+    if (cap > FCGPU_MAX_FLOWS) return fail(c, FCGPU_EINVAL, "flow capacity above FCGPU_MAX_FLOWS");
+    uint32_t eps = 0, te = 0, nb = 0;
+    if (imp && fc->timeout_s) {
+        if (fc->recycle_ms < 1 || fc->recycle_ms > 65535)
+            return fail(c, FCGPU_EINVAL, "flow recycle interval must be 1 .. 65535 ms");
+        // parse (:58-79): epochs per second, timeout in epochs; TimerWheel::initialize
+        eps = std::max(1u, 1000u / fc->recycle_ms);
+        te = fc->timeout_s * eps;
+        nb = pow2_at_least(te + 2u);
+        if ((uint64_t)fc->timeout_s * eps + 2u > kMaxWheel)
+            return fail(c, FCGPU_EINVAL, "flow timeout too long for the recycle interval (timer wheel above 16384 epochs)");
+        // the maintainer's per-chunk counts: (cap / 1024) x (TE + 1) words
+        if ((uint64_t)((cap + kMaintChunk - 1) / kMaintChunk) * (te + 1u) > (1ull << 26))
+            return fail(c, FCGPU_EINVAL, "flow timeout in epochs x capacity too large for the maintainer (timer wheel)");
+    }
     static_assert(FCGPU_FLOW_MAX_BATCH == 64u * kLdsWords, "fcgpu_flow.hh kLdsWords");
-    if (max_flows && c->max_batch > FCGPU_FLOW_MAX_BATCH)
+    if (cap && c->max_batch > FCGPU_FLOW_MAX_BATCH)
         return fail(c, FCGPU_EINVAL, "flow table: the context's max_batch is above FCGPU_FLOW_MAX_BATCH");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipDeviceSynchronize());
     flow_free(c);
-    if (max_flows == 0) return FCGPU_OK;
+    if (cap == 0) return FCGPU_OK;
     // at most max_flows IDs plus one batch of FULL markers (the batch that
     // fills the table): keep the load at or under 1/2
     uint32_t slots = 1024;
@@ -592,6 +641,24 @@ int fcgpu_flow_enable(fcgpu_ctx *c, uint32_t max_flows) {
     HIPCHK(c, hipMalloc(&F.firstmask, sizeof(uint64_t) * words));
     HIPCHK(c, hipMalloc(&F.wordpre, sizeof(uint32_t) * words));
     HIPCHK(c, hipMalloc(&F.state, sizeof(uint32_t) * 16));
+    if (imp) HIPCHK(c, hipMalloc(&F.stack, sizeof(uint32_t) * max_flows));
+    if (te) {
+        F.wstride = cap;
+        F.wmask = nb - 1;
+        F.te = te;
+        HIPCHK(c, hipMalloc(&F.lastseen, sizeof(uint32_t) * cap));
+        HIPCHK(c, hipMalloc(&F.wheel, sizeof(uint32_t) * (size_t)nb * cap));
+        HIPCHK(c, hipMalloc(&F.wheel_len, sizeof(uint32_t) * nb));
+        HIPCHK(c, hipMalloc(&c->flow_spare, sizeof(uint4) * slots));
+        HIPCHK(c, hipMalloc(&c->maint.qbsr, sizeof(uint32_t) * cap));
+        HIPCHK(c, hipMalloc(&c->maint.dead, sizeof(uint32_t) * cap));
+        HIPCHK(c, hipMalloc(&c->maint.rbuf, sizeof(uint16_t) * cap));
+        HIPCHK(c, hipMalloc(&c->maint.counts, sizeof(uint32_t) * (size_t)((cap + kMaintChunk - 1) / kMaintChunk) *
+                                                  (te + 1)));
+        c->maint.to_ms = fc->timeout_s * 1000u;
+        c->maint.ri_ms = fc->recycle_ms;
+        c->maint.eps = eps;
+    }
     HIPCHK(c, hipHostMalloc((void **)&c->flow_hint, sizeof(uint32_t), hipHostMallocMapped));
     for (auto &e : c->flow_order)
         if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -601,7 +668,72 @@ int fcgpu_flow_enable(fcgpu_ctx *c, uint32_t max_flows) {
     c->max_flows = max_flows;
     c->flow_slots = slots;
     c->flow_words = words;
+    c->flow_conf = *fc;
+    c->flow_conf.capacity = cap;
     return flow_clear(c);
+}
+
+int fcgpu_flow_enable(fcgpu_ctx *c, uint32_t max_flows) {
+    if (!c) return FCGPU_EINVAL;
+    if (max_flows > FCGPU_MAX_FLOWS) return fail(c, FCGPU_EINVAL, "max_flows above FCGPU_MAX_FLOWS");
+    fcgpu_flow_config fc{};
+    fc.manager = FCGPU_FLOW_MGR_HMP;
+    fc.capacity = max_flows;
+    return fcgpu_flow_configure(c, &fc);
+}
+
+int fcgpu_flow_set_time(fcgpu_ctx *c, uint32_t now_ms) {
+    if (!c) return FCGPU_EINVAL;
+    c->flow_now = now_ms;
+    return FCGPU_OK;
+}
+
+int fcgpu_flow_maintain(fcgpu_ctx *c, uint32_t now_ms, void *stream) {
+    if (!c) return FCGPU_EINVAL;
+    if (!c->fl.lastseen) return FCGPU_OK;           // no timeouts: nothing expires
+    HIPCHK(c, hipSetDevice(c->device));
+    // the stream the flow batches are ordered on
+    hipStream_t s = c->stream ? c->stream : (hipStream_t)stream;
+    if (++c->maint.seq == 0) {                        // run numbers mark released IDs; never 0
+        HIPCHK(c, hipMemsetAsync(c->maint.dead, 0, sizeof(uint32_t) * c->fl.wstride, s));
+        c->maint.seq = 1;
+    }
+    MaintArgs M = c->maint;
+    M.now = now_ms;
+    const uint32_t nch = (c->fl.wstride + kMaintChunk - 1) / kMaintChunk;
+    const uint32_t g = std::min(nch, 1024u);
+    hipLaunchKernelGGL(k_maint_count, dim3(g), dim3(kMaintChunk), 0, s, c->fl, M);
+    hipLaunchKernelGGL(k_maint_scan, dim3(c->fl.te + 1), dim3(kMaintChunk), 0, s, c->fl, M);
+    hipLaunchKernelGGL(k_maint_scatter, dim3(g), dim3(kMaintChunk), 0, s, c->fl, M);
+    hipLaunchKernelGGL(k_maint_finish, dim3(1), dim3(64), 0, s, c->fl);
+    HIPCHK(c, hipGetLastError());
+    const size_t bytes = sizeof(uint4) * c->flow_slots;
+    HIPCHK(c, hipMemsetAsync(c->flow_spare, 0, bytes, s));
+    const uint32_t gr = std::min((c->flow_slots + kFlowGridBlock - 1) / kFlowGridBlock, 4096u);
+    hipLaunchKernelGGL(k_flow_rebuild, dim3(gr), dim3(kFlowGridBlock), 0, s, c->fl.slots, c->flow_spare,
+                       c->fl.claim, c->fl.mask, c->maint.dead, c->maint.seq);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemsetAsync(c->fl.claim, 0, sizeof(uint32_t) * c->flow_slots, s));
+    std::swap(c->fl.slots, c->flow_spare);
+    return FCGPU_OK;
+}
+
+int fcgpu_flow_stats(fcgpu_ctx *c, fcgpu_flow_stat *st) {
+    if (!c || !st) return FCGPU_EINVAL;
+    *st = fcgpu_flow_stat{};
+    if (!c->fl.slots) return FCGPU_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());
+    uint32_t w[16];
+    HIPCHK(c, hipMemcpy(w, c->fl.state, sizeof w, hipMemcpyDeviceToHost));
+    st->manager = c->flow_conf.manager;
+    st->capacity = c->flow_conf.capacity;
+    const uint32_t q = c->fl.lastseen ? w[kFsQlen] : 0u;
+    st->count = w[kFsNext] - q;
+    st->free_ids = c->max_flows - w[kFsNext];
+    st->pending = q;
+    st->epochs = c->fl.lastseen ? w[kFsIndex] : 0u;
+    return FCGPU_OK;
 }
 
 int fcgpu_flow_reset(fcgpu_ctx *c) {
@@ -618,7 +750,9 @@ int fcgpu_flow_count(fcgpu_ctx *c, uint32_t *count) {
     if (!c->fl.slots) return FCGPU_OK;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipDeviceSynchronize());
-    HIPCHK(c, hipMemcpy(count, c->fl.state + kFsNext, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    uint32_t w[16];
+    HIPCHK(c, hipMemcpy(w, c->fl.state, sizeof w, hipMemcpyDeviceToHost));
+    *count = w[kFsNext] - (c->fl.lastseen ? w[kFsQlen] : 0u);
     return FCGPU_OK;
 }
 
@@ -834,6 +968,7 @@ static int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_d
     a.cfg = c->dcfg;
     a.fl = c->fl;
     a.fl.flowid = o->flowid;
+    a.fl.now = c->flow_now;
     if (a.fl.slots) {
         if (++c->flow_epoch == 0) ++c->flow_epoch;   // never 0 (the cleared state)
         a.fl.epoch = c->flow_epoch;

@@ -64,9 +64,11 @@ struct DevCfg {
 constexpr int32_t kProgUnmatched = 0x7fff;
 constexpr uint32_t kStepTable = 2u;       // in the flags (x >> 16)
 
-// Flow table state (fcgpu_flow_enable). Slot = {saddr, daddr, ports, tag} with
-// tag = proto | (flow id + 1) << 8; tag 0 = empty. Linear probing, never more
-// than half full (max_flows <= slots / 2), no deletions.
+// Flow table state (fcgpu_flow_configure). Slot = {saddr, daddr, ports, tag}
+// with tag = proto | (flow id + 1) << 8; tag 0 = empty. Linear probing, never
+// more than half full (max_flows <= slots / 2), no deletions between
+// maintainer runs (an IMP run with timeouts rebuilds the table without the
+// flows it expired, k_flow_rebuild).
 struct FlowArgs {
     uint4 *slots;
     uint32_t mask;           // slots - 1
@@ -84,11 +86,23 @@ struct FlowArgs {
     uint32_t *host_hint;     // mapped host word: size class of the last batch's misses (kHint*)
     uint32_t *flowid;        // [n] output (may be null)
     uint32_t epoch;          // this batch's number (never 0)
+    // IMP managers (fcgpu_flow.hh, "IMP"): null stack = HMP (IDs 0, 1, 2, ...)
+    uint32_t *stack;         // free IDs; [0, max_flows - state[kFsNext]) hold them, top last
+    uint32_t *lastseen;      // [wstride] ms of the last batch with a packet of the flow (null: no timeout)
+    uint32_t *wheel;         // [wmask + 1][wstride] timer-wheel buckets, IDs in scheduling order
+    uint32_t *wheel_len;     // [wmask + 1]
+    uint32_t wstride;        // the table's capacity (IDs 0 .. wstride - 1)
+    uint32_t wmask;          // wheel buckets - 1
+    uint32_t te;             // timeout in maintainer epochs
+    uint32_t now;            // this batch's time (ms, fcgpu_flow_set_time)
 };
-constexpr uint32_t kFsNext = 0;   // next flow ID
+constexpr uint32_t kFsNext = 0;   // HMP: next flow ID; IMP: IDs out of the stack (max_flows - stack size)
 constexpr uint32_t kFsBase = 1;   // the ID base of the batch being finished (grid-wide finish)
 constexpr uint32_t kFsMissed = 2; // epoch of the last batch with a miss
 constexpr uint32_t kFsHint = 3;   // the hint last published
+constexpr uint32_t kFsIndex = 4;  // IMP: timer-wheel index (maintainer runs so far)
+constexpr uint32_t kFsWBase = 5;  // IMP: the new-flow bucket's length when the batch began (grid-wide finish)
+constexpr uint32_t kFsQlen = 6;   // IMP: IDs the last maintainer run released (pushed back by the next)
 constexpr uint32_t kFlowMiss = 0xfffffffdu;
 constexpr uint32_t kSlotNone = 0xffffffffu;
 
@@ -929,6 +943,10 @@ __device__ __forceinline__ void flow_resolve(const FlowArgs &F, FlowProbe &q, bo
             q.pos = (q.pos + 1) & F.mask;
             q.sl = F.slots[q.pos];
         }
+        // IMP with timeouts: a flow with a packet in the batch is stamped with
+        // the batch's time (virtualflowmanager.hh:236-239,311-313); new flows
+        // are stamped by their first packet in the new-flow pass
+        if (F.lastseen && id < kTagFull) F.lastseen[id] = F.now;
     }
     // No miss list and no counter: a miss keeps its packet index (its record
     // lives at index i), the wave writes its 64-bit miss word, and a wave with

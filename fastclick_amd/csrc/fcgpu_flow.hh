@@ -61,19 +61,35 @@ __device__ __forceinline__ void publish_hint(const FlowArgs &F, uint32_t m) {
 // commits the slot (key + tag) and frees the claim. A flow the table had no
 // ID left for is committed as FULL too, so later lookups of keys that probe
 // past this slot still find their own.
+//   HMP: ID = base + rank. IMP: the (base + rank)-th pop of the free-ID stack
+//   (virtualflowmanager.hh:264), and with timeouts the first packet stamps the
+//   flow and schedules it TE epochs ahead (:293-296): appended, in rank order,
+//   to the wheel bucket `wb` whose length was `wbase` when the batch began.
 __device__ __forceinline__ void flow_commit(const FlowArgs &F, uint32_t i, uint32_t slot, uint32_t fp,
-                                            uint32_t base, uint32_t rank) {
+                                            uint32_t base, uint32_t rank, uint32_t wb, uint32_t wbase) {
     uint32_t id = FCGPU_FLOW_FULL;
     if (slot != kSlotNone) {
-        if (base + rank < F.max_flows) id = base + rank;
+        if (base + rank < F.max_flows) id = F.stack ? F.stack[F.max_flows - 1u - (base + rank)] : base + rank;
         if (i == fp) {
             const uint4 k = F.miss_key[i];
             F.slots[slot] = make_uint4(k.x, k.y, k.z, k.w | ((id != FCGPU_FLOW_FULL ? id + 1u : kTagFull) << 8));
             F.claim[slot] = 0;
             F.first[slot] = 0xffffffffu;
+            if (F.lastseen && id != FCGPU_FLOW_FULL) {
+                F.lastseen[id] = F.now;
+                F.wheel[(size_t)wb * F.wstride + wbase + rank] = id;
+            }
         }
     }
     if (F.flowid) F.flowid[i] = id;
+}
+
+// IMP with timeouts: the bucket new flows go to (schedule_after(fcb, TE),
+// timerwheel.hh: index + TE) and its length when the batch began.
+__device__ __forceinline__ uint2 flow_new_bucket(const FlowArgs &F) {
+    if (!F.lastseen) return make_uint2(0, 0);
+    const uint32_t wb = (F.state[kFsIndex] + F.te) & F.wmask;
+    return make_uint2(wb, F.wheel_len[wb]);
 }
 
 __device__ __forceinline__ uint32_t flow_next_after(const FlowArgs &F, uint32_t next, uint32_t total) {
@@ -100,7 +116,7 @@ __device__ __forceinline__ void flow_mark_wave(const FlowArgs &F, uint32_t i0) {
     if (lane == 0) F.firstmask[i0 >> 6] = fm;
 }
 
-__device__ __forceinline__ void flow_assign_wave(const FlowArgs &F, uint32_t i0, uint32_t base) {
+__device__ __forceinline__ void flow_assign_wave(const FlowArgs &F, uint32_t i0, uint32_t base, uint2 wb) {
     const uint32_t lane = threadIdx.x & 63, i = i0 + lane;
     const uint64_t mw = F.missmask[i0 >> 6];
     if ((mw >> lane) & 1u) {
@@ -110,7 +126,7 @@ __device__ __forceinline__ void flow_assign_wave(const FlowArgs &F, uint32_t i0,
             const uint32_t w = fp >> 6;
             rank = F.wordpre[w] + (uint32_t)__popcll(F.firstmask[w] & ((1ull << (fp & 63)) - 1ull));
         }
-        flow_commit(F, i, slot, fp, base, rank);
+        flow_commit(F, i, slot, fp, base, rank, wb.x, wb.y);
     }
 }
 
@@ -215,6 +231,7 @@ __global__ __launch_bounds__(kFinishBlock) void k_flow_finish(FlowArgs F, uint32
         return;
     }
     const uint32_t next = F.state[kFsNext];
+    const uint2 wb = flow_new_bucket(F);
     // miss words: word w = t + k * kFinishBlock stays in registers; its
     // popcount goes to LDS, becomes the word's first miss index (exclusive
     // prefix in word order, via thread-contiguous chunks of LDS)
@@ -314,14 +331,16 @@ __global__ __launch_bounds__(kFinishBlock) void k_flow_finish(FlowArgs F, uint32
                 }
                 rank = s_f[lo];
             }
-            flow_commit(F, pkt[q], slot[q], fp[q], next, rank);
+            flow_commit(F, pkt[q], slot[q], fp[q], next, rank, wb.x, wb.y);
         }
         nfirst_before += nf;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // commits done before the next chunk looks
         __syncthreads();                      // s_idx / s_f reused by the next chunk
     }
     if (t == 0) {
-        F.state[kFsNext] = flow_next_after(F, next, nfirst_before);
+        const uint32_t nx = flow_next_after(F, next, nfirst_before);
+        F.state[kFsNext] = nx;
+        if (F.lastseen) F.wheel_len[wb.x] = wb.y + (nx - next);
         publish_hint(F, m);
     }
 }
@@ -344,9 +363,14 @@ __global__ __launch_bounds__(kFinishBlock) void k_flow_scan(FlowArgs F, uint32_t
     }
     const uint2 tot = mask_prefix<kFinishBlock>(F, nw, s_w, s_pre);
     if (threadIdx.x == 0) {
-        const uint32_t next = F.state[kFsNext];
+        const uint32_t next = F.state[kFsNext], nx = flow_next_after(F, next, tot.x);
         F.state[kFsBase] = next;
-        F.state[kFsNext] = flow_next_after(F, next, tot.x);
+        F.state[kFsNext] = nx;
+        if (F.lastseen) {
+            const uint2 wb = flow_new_bucket(F);
+            F.state[kFsWBase] = wb.y;
+            F.wheel_len[wb.x] = wb.y + (nx - next);
+        }
         publish_hint(F, tot.y);
     }
 }
@@ -354,9 +378,201 @@ __global__ __launch_bounds__(kFinishBlock) void k_flow_scan(FlowArgs F, uint32_t
 __global__ __launch_bounds__(kFlowGridBlock) void k_flow_assign(FlowArgs F, uint32_t nw) {
     if (F.state[kFsMissed] != F.epoch) return;
     const uint32_t base = F.state[kFsBase];
+    const uint2 wb = F.lastseen ? make_uint2((F.state[kFsIndex] + F.te) & F.wmask, F.state[kFsWBase]) : make_uint2(0, 0);
     for (uint32_t i0 = blockIdx.x * kFlowGridBlock + (threadIdx.x & ~63u); i0 < nw * 64;
          i0 += gridDim.x * kFlowGridBlock)
-        flow_assign_wave(F, i0, base);
+        flow_assign_wave(F, i0, base, wb);
+}
+
+// ---- IMP maintainer run (VirtualFlowManagerIMP::maintainer,
+// include/click/flow/virtualflowmanager.hh:151-223) ---------------------------
+// The reference keeps each wheel bucket as a singly linked list through the
+// FCBs (prepend on schedule, walk from the head), and the IDs a run releases
+// as another such list pushed back onto the stack at the start of the next
+// run. Here a bucket is an array in scheduling order (so the walk is the array
+// backwards) and the released IDs an array in release order (pushed back last
+// first), which keeps the same order with coalesced accesses.
+//
+// An entry of the walked bucket goes to the released list (r = 0) or to the
+// bucket r epochs ahead (1 <= r <= TE), keeping its walk order within its
+// destination: a stable partition of the walk into TE + 1 destinations, done
+// grid-wide in 1024-entry chunks of the walk:
+//   k_maint_count   (grid) each entry's r (kept in rbuf); per chunk, the count
+//                   per destination; also pushes the previous run's releases
+//   k_maint_scan    (a block per destination) exclusive scan of its counts
+//                   over the chunks, from the destination's current length
+//   k_maint_scatter (grid) each entry to its place: the chunk's offset plus
+//                   its rank among the chunk's earlier entries of the same r
+//   k_maint_finish  the walked bucket emptied, the wheel index advanced
+// (One block walking the bucket took 4.1 ms for a 1M-flow bucket, one
+// memory latency per 1024 entries.)
+constexpr uint32_t kMaxWheel = 1u << 14;     // wheel buckets (LDS counters)
+constexpr uint32_t kMaintChunk = 1024;       // walk entries per chunk (= block)
+struct MaintArgs {
+    uint32_t *qbsr;          // [wstride] IDs released by the last run, in release order
+    uint32_t *dead;          // [wstride] run number that released the ID
+    uint32_t *counts;        // [chunks][te + 1] per-chunk counts, then offsets
+    uint16_t *rbuf;          // [wstride] each walk entry's destination
+    uint32_t now, to_ms, ri_ms, eps, seq;
+};
+
+// lastseen -> destination: 0 = release, else reschedule r epochs ahead
+__device__ __forceinline__ uint32_t maint_dest(const FlowArgs &F, const MaintArgs &M, uint32_t ls) {
+    const int32_t old = (int32_t)(M.now - ls);
+    if (old <= 0) return F.te;                                   // lastseen not in the past (:174-180)
+    if ((uint32_t)old + M.ri_ms >= M.to_ms) return 0;            // expire (:185-205)
+    return ((M.to_ms - (uint32_t)old) * M.eps) / 1000u;          // time left (:209-211)
+}
+
+// Stable rank of each valid lane among the chunk's earlier lanes with the
+// same destination, from the per-destination bases in s_off (advanced past the
+// chunk): the waves take turns; inside a wave each distinct r (few: r is the
+// flow's remaining idle time in epochs) is one group.
+__device__ __forceinline__ uint32_t maint_rank(uint32_t *s_off, bool valid, uint32_t r) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t pos = 0;
+    for (uint32_t w = 0; w < kMaintChunk / 64; ++w) {
+        if (wave == w) {
+            uint64_t rem = __ballot(valid);
+            while (rem) {
+                const uint32_t leader = (uint32_t)__builtin_ctzll(rem);
+                const uint32_t k = __shfl(r, leader);
+                const uint64_t m = __ballot(valid && r == k);
+                uint32_t b = 0;
+                if (lane == leader) {
+                    b = s_off[k];
+                    s_off[k] = b + (uint32_t)__popcll(m);
+                }
+                b = __shfl(b, leader);
+                if (valid && r == k) pos = b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                rem &= ~m;
+            }
+        }
+        __syncthreads();
+    }
+    return pos;
+}
+
+__global__ __launch_bounds__(kMaintChunk) void k_maint_count(FlowArgs F, MaintArgs M) {
+    __shared__ uint32_t s_cnt[kMaxWheel];
+    const uint32_t t = threadIdx.x;
+    const uint32_t idx = F.state[kFsIndex], q = F.state[kFsQlen];
+    // the previous run's releases back onto the stack, the list's head (the
+    // last released) first (:155-161); k_maint_scatter rewrites qbsr later
+    const uint32_t S = F.max_flows - F.state[kFsNext];
+    for (uint32_t j = blockIdx.x * kMaintChunk + t; j < q; j += gridDim.x * kMaintChunk)
+        F.stack[S + j] = M.qbsr[q - 1u - j];
+    const uint32_t cur = idx & F.wmask, n = F.wheel_len[cur], D = F.te + 1u;
+    const uint32_t *list = F.wheel + (size_t)cur * F.wstride;
+    for (uint32_t c = blockIdx.x; c * kMaintChunk < n; c += gridDim.x) {
+        for (uint32_t r = t; r < D; r += kMaintChunk) s_cnt[r] = 0;
+        __syncthreads();
+        const uint32_t j = c * kMaintChunk + t;
+        const bool valid = j < n;
+        uint32_t r = 0;
+        if (valid) {
+            r = maint_dest(F, M, F.lastseen[list[n - 1u - j]]);
+            M.rbuf[j] = (uint16_t)r;
+        }
+        // one LDS add per (wave, destination)
+        uint64_t rem = __ballot(valid);
+        while (rem) {
+            const uint32_t leader = (uint32_t)__builtin_ctzll(rem);
+            const uint32_t k = __shfl(r, leader);
+            const uint64_t m = __ballot(valid && r == k);
+            if ((t & 63) == leader) atomicAdd(&s_cnt[k], (uint32_t)__popcll(m));
+            rem &= ~m;
+        }
+        __syncthreads();
+        for (uint32_t d = t; d < D; d += kMaintChunk) M.counts[(size_t)c * D + d] = s_cnt[d];
+        __syncthreads();
+    }
+}
+
+// One block per destination r: its counts over the chunks become offsets
+// (its current length + the earlier chunks' counts); its new length written.
+__global__ __launch_bounds__(kMaintChunk) void k_maint_scan(FlowArgs F, MaintArgs M) {
+    __shared__ uint32_t s_w[kMaintChunk / 64];
+    const uint32_t t = threadIdx.x, r = blockIdx.x, D = F.te + 1u;
+    const uint32_t idx = F.state[kFsIndex], cur = idx & F.wmask;
+    const uint32_t n = F.wheel_len[cur], nch = (n + kMaintChunk - 1) / kMaintChunk;
+    const uint32_t dest = (idx + r) & F.wmask;
+    const uint32_t base = r ? F.wheel_len[dest] : 0u;
+    const uint32_t per = (nch + kMaintChunk - 1) / kMaintChunk, c0 = t * per;
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < per; ++k)
+        if (c0 + k < nch) sum += M.counts[(size_t)(c0 + k) * D + r];
+    uint32_t total;
+    uint32_t off = base + block_excl_scan<kMaintChunk>(sum, s_w, total);
+    for (uint32_t k = 0; k < per; ++k) {
+        if (c0 + k < nch) {
+            uint32_t *p = &M.counts[(size_t)(c0 + k) * D + r];
+            const uint32_t v = *p;
+            *p = off;
+            off += v;
+        }
+    }
+    if (t == 0) {
+        if (r) {
+            F.wheel_len[dest] = base + total;
+        } else {
+            F.state[kFsNext] -= F.state[kFsQlen];    // the releases pushed by k_maint_count
+            F.state[kFsQlen] = total;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kMaintChunk) void k_maint_scatter(FlowArgs F, MaintArgs M) {
+    __shared__ uint32_t s_off[kMaxWheel];
+    const uint32_t t = threadIdx.x, D = F.te + 1u;
+    const uint32_t idx = F.state[kFsIndex], cur = idx & F.wmask, n = F.wheel_len[cur];
+    const uint32_t *list = F.wheel + (size_t)cur * F.wstride;
+    for (uint32_t c = blockIdx.x; c * kMaintChunk < n; c += gridDim.x) {
+        for (uint32_t d = t; d < D; d += kMaintChunk) s_off[d] = M.counts[(size_t)c * D + d];
+        __syncthreads();
+        const uint32_t j = c * kMaintChunk + t;
+        const bool valid = j < n;
+        const uint32_t r = valid ? M.rbuf[j] : 0u;
+        const uint32_t id = valid ? list[n - 1u - j] : 0u;
+        const uint32_t pos = maint_rank(s_off, valid, r);
+        if (valid) {
+            if (r == 0) {
+                M.qbsr[pos] = id;
+                M.dead[id] = M.seq;
+            } else {
+                F.wheel[(size_t)((idx + r) & F.wmask) * F.wstride + pos] = id;
+            }
+        }
+    }
+}
+
+__global__ void k_maint_finish(FlowArgs F) {
+    if (threadIdx.x == 0) {
+        const uint32_t idx = F.state[kFsIndex];
+        F.wheel_len[idx & F.wmask] = 0;
+        F.state[kFsIndex] = idx + 1u;
+    }
+}
+
+// The table without the flows this run expired (and without FULL markers:
+// the flows they stood for retry when they next arrive, as IDs may be back):
+// every other entry re-inserted into the cleared spare slot array. Placement
+// differs from the old array's; IDs do not depend on it.
+__global__ __launch_bounds__(kFlowGridBlock) void k_flow_rebuild(const uint4 *old, uint4 *slots, uint32_t *claim,
+                                                                 uint32_t mask, const uint32_t *dead, uint32_t seq) {
+    for (uint32_t s = blockIdx.x * kFlowGridBlock + threadIdx.x; s <= mask; s += gridDim.x * kFlowGridBlock) {
+        const uint4 e = old[s];
+        const uint32_t tag = e.w >> 8;
+        if (e.w == 0 || tag == kTagFull || dead[tag - 1u] == seq) continue;
+        uint32_t pos = flow_slot_hash(make_uint4(e.x, e.y, e.z, e.w & 0xffu)) & mask;
+        for (uint32_t p = 0; p <= mask; ++p) {
+            if (atomicCAS(&claim[pos], 0u, 1u) == 0u) {
+                slots[pos] = e;
+                break;
+            }
+            pos = (pos + 1) & mask;
+        }
+    }
 }
 
 }  // namespace fcgpu

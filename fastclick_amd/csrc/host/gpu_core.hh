@@ -55,6 +55,12 @@
 //     order of first appearance, elements/research/flowipmanagerhmp.cc:96-126)
 //     in the 4-byte annotation at FLOWID_ANNO; a new flow beyond the capacity
 //     is killed (as the IMP managers do when their flow stack is empty).
+//   FLOW_MANAGER HMP|IMP, FLOW_TIMEOUT s, FLOW_RECYCLE_INTERVAL s (default 1)
+//                                            -- IMP: FlowIPManager_CuckooPP /
+//     FlowIPManagerIMP (CAPACITY, TIMEOUT, RECYCLE_INTERVAL): IDs from a free-ID
+//     stack, flows idle for TIMEOUT s expire (include/click/flow/
+//     virtualflowmanager.hh); the maintainer runs every RECYCLE_INTERVAL on the
+//     batches' clock (each submission first runs the runs that are due).
 //   DEC_TTL, TTL_MULTICAST (default true), SET_CHECKSUM
 //                                            -- DecIPTTL / SetIPChecksum after the
 //     classifier (IPv4): TTL-expired packets (DecIPTTL output 1) join output N,
@@ -228,6 +234,19 @@ class RxCore {
             } else if (k == "FLOW_CAPACITY") {
                 if (!parse_int(v, n) || n < 0 || n > (long)FCGPU_MAX_FLOWS) return err(errh, "bad FLOW_CAPACITY");
                 _flow_cap = (uint32_t)n;
+            } else if (k == "FLOW_MANAGER") {
+                if (v == "HMP") _flow_mgr = FCGPU_FLOW_MGR_HMP;
+                else if (v == "IMP") _flow_mgr = FCGPU_FLOW_MGR_IMP;
+                else return err(errh, "FLOW_MANAGER expects HMP or IMP");
+            } else if (k == "FLOW_TIMEOUT") {
+                if (!parse_int(v, n) || n < 0 || n > 86400) return err(errh, "bad FLOW_TIMEOUT");
+                _flow_timeout = (uint32_t)n;
+            } else if (k == "FLOW_RECYCLE_INTERVAL") {
+                // seconds, as RECYCLE_INTERVAL (virtualflowmanager.hh:68-71)
+                char *end = nullptr;
+                const double d = strtod(v.c_str(), &end);
+                if (v.empty() || *end || !(d >= 0.001 && d <= 65.535)) return err(errh, "bad FLOW_RECYCLE_INTERVAL");
+                _flow_recycle_ms = (uint32_t)(d * 1000);
             } else if (k == "FLOWID_ANNO") {
                 if (!parse_int(v, n) || n < 0 || n > P::kAnnoSize - 4) return err(errh, "bad FLOWID_ANNO");
                 _flow_anno = (int)n;
@@ -244,6 +263,7 @@ class RxCore {
         const bool ip4 = _cfg.check_mode == FCGPU_CHECK_IP4 || _cfg.check_mode == FCGPU_MARK_IP4;
         if (_cfg.l4_mode != FCGPU_L4_NONE && !ip4) return err(errh, "L4 needs MODE CHECK or MARK");
         if (_flow_cap && !ip4) return err(errh, "FLOW_CAPACITY needs MODE CHECK or MARK");
+        if (_flow_timeout && _flow_mgr != FCGPU_FLOW_MGR_IMP) return err(errh, "FLOW_TIMEOUT needs FLOW_MANAGER IMP");
         if (_cfg.rewrite && !ip4) return err(errh, "DEC_TTL / SET_CHECKSUM need MODE CHECK or MARK");
         if (_cfg.classify == FCGPU_CLS_LB_CRC && !ip4) return err(errh, "LB_MODE hash_crc needs MODE CHECK or MARK");
         if (_cfg.classify == FCGPU_CLS_PROGRAM) {
@@ -277,8 +297,9 @@ class RxCore {
             reach = fcgpu::program_reach(_prog_kind, _prog.steps.data(), (uint32_t)_prog.steps.size(), l3, l3 + 60);
         }
         if (_flow_cap) {
-            rc = fcgpu_flow_enable(_ctx, _flow_cap);
-            if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_flow_enable: ") + fcgpu_last_error(_ctx));
+            fcgpu_flow_config fc{_flow_mgr, _flow_cap, _flow_timeout, _flow_recycle_ms};
+            rc = fcgpu_flow_configure(_ctx, &fc);
+            if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_flow_configure: ") + fcgpu_last_error(_ctx));
         }
         _capture = fcgpu::capture_bytes(_cfg, reach);
         const size_t per = _capture == fcgpu::kCaptureWhole ? 1536 : _capture;
@@ -520,6 +541,7 @@ class RxCore {
     void submit(Emit &emit) {
         const uint32_t k = _cur;
         Slot &s = _slot[k];
+        if (_flow_cap && _flow_timeout) flow_clock();
         const int rc = fcgpu_span_submit_block(_ctx, k, s.in, s.frames_off + s.used, 0, s.frames_off, s.n, s.res,
                                                _outputs, _partition);
         if (rc != FCGPU_OK) {
@@ -529,6 +551,23 @@ class RxCore {
         }
         _cur = (_cur + 1) % kSlots;
         if (_slot[_cur].inflight) complete(_cur, emit);
+    }
+
+    // IMP timeouts: the maintainer runs due by now (every RECYCLE_INTERVAL from
+    // the first batch, virtualflowmanager.hh:118-124,134-144), then this
+    // batch's time stamp (Timestamp::recent_steady() at push_batch, :227-230).
+    // Queued on the context's stream ahead of the batch.
+    void flow_clock() {
+        const uint32_t now = (uint32_t)(P::now_ns() / 1000000ull);
+        if (!_maint_armed) {
+            _next_maint = now + _flow_recycle_ms;
+            _maint_armed = true;
+        }
+        while ((int32_t)(now - _next_maint) >= 0) {
+            if (fcgpu_flow_maintain(_ctx, _next_maint, nullptr) != FCGPU_OK) _error = fcgpu_last_error(_ctx);
+            _next_maint += _flow_recycle_ms;
+        }
+        fcgpu_flow_set_time(_ctx, now);
     }
 
     void fail_slot(Slot &s, const char *msg) {
@@ -694,6 +733,9 @@ class RxCore {
     uint32_t _prog_kind = FCGPU_PROG_IPFILTER;
     int _color = -1;
     uint32_t _flow_cap = 0;
+    uint32_t _flow_mgr = FCGPU_FLOW_MGR_HMP, _flow_timeout = 0, _flow_recycle_ms = 1000;
+    uint32_t _next_maint = 0;
+    bool _maint_armed = false;
     int _flow_anno = 28;
     uint64_t _flow_drops = 0;
     int _device = 0;

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 12
+#define FCGPU_ABI_VERSION 13
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -386,8 +386,65 @@ int  fcgpu_set_program(fcgpu_ctx *ctx, uint32_t kind, const fcgpu_step *steps, u
 int  fcgpu_flow_enable(fcgpu_ctx *ctx, uint32_t max_flows);
 /* Forget every flow (IDs restart at 0). */
 int  fcgpu_flow_reset(fcgpu_ctx *ctx);
-/* Flows assigned so far. Synchronises the context's device work. */
+/* HMP: flow IDs assigned so far; IMP: flows in the table (the managers'
+ * "count" handler, virtualflowmanager.hh:387-388). Synchronises the context's
+ * device work. */
 int  fcgpu_flow_count(fcgpu_ctx *ctx, uint32_t *count);
+
+/* Flow managers (the VirtualFlowManager family). One table per
+ * context, as the reference keeps one per thread (per_thread_oread<State>,
+ * virtualflowmanager.hh:410); fcgpu_flow_enable(ctx, n) is the HMP manager.
+ *   FCGPU_FLOW_MGR_HMP: FlowIPManagerHMP, IDs 0, 1, 2, ... (above); no timeout.
+ *   FCGPU_FLOW_MGR_IMP: VirtualFlowManagerIMP over FlowManagerIMPState, the
+ *     manager of FlowIPManager_CuckooPP / FlowIPManagerIMP
+ *     (elements/flow/flowipmanager_cuckoopp.cc:57-121):
+ *     - capacity is rounded up to a power of two (virtualflowmanager.hh:85);
+ *       IDs come from a free-ID stack filled with 0 .. cap-1 (:113-115), popped
+ *       from the top: cap-1, cap-2, ... A popped 0 means "full" (:264-268): a
+ *       new flow when only 0 is left gets FCGPU_FLOW_FULL (the element kills
+ *       it). (The reference then reads below its stack on the next pop; here
+ *       the table stays full until IDs come back.)
+ *     - timeout_s > 0 (TIMEOUT) with recycle_ms (RECYCLE_INTERVAL, 1 ..
+ *       65535 ms): every flow with a packet in a batch is stamped with the
+ *       batch's time (fcgpu_flow_set_time before the batch; :236-239,311-313);
+ *       a new flow is scheduled on a timer wheel timeout_s * eps epochs ahead
+ *       (eps = max(1, 1000 / recycle_ms); :72-74,293-296). Each
+ *       fcgpu_flow_maintain is one maintainer run (:151-223): the IDs the
+ *       previous run released go back onto the stack, then the wheel's current
+ *       bucket is walked: a flow idle for old ms with old + recycle_ms >=
+ *       timeout_s * 1000 is removed from the table and its ID released; others
+ *       are rescheduled. The caller runs it every recycle_ms (the reference's
+ *       maintain timer, :118-124,134-144), on the same clock.
+ *       Memory: next_pow2(TE + 2) * cap * 4 B of wheel (TE = timeout epochs,
+ *       at most 16382) and (cap / 1024) * (TE + 1) * 4 B of maintainer counts
+ *       (at most 2^26 words); a second slot array the run rebuilds into.
+ *   Times are ms on any clock that the caller uses consistently (32-bit,
+ *   differences below 2^31 ms). */
+#define FCGPU_FLOW_MGR_HMP 0u
+#define FCGPU_FLOW_MGR_IMP 1u
+typedef struct fcgpu_flow_config {
+    uint32_t manager;       /* FCGPU_FLOW_MGR_* */
+    uint32_t capacity;      /* HMP: max flows; IMP: CAPACITY (0 disables the table) */
+    uint32_t timeout_s;     /* IMP: TIMEOUT in seconds, 0 = flows never expire */
+    uint32_t recycle_ms;    /* IMP with timeout: RECYCLE_INTERVAL in ms (reference default 1000) */
+} fcgpu_flow_config;
+int  fcgpu_flow_configure(fcgpu_ctx *ctx, const fcgpu_flow_config *cfg);
+/* The time stamp of the batches submitted after this call
+ * (Timestamp::recent_steady() of push_batch, :227-230). */
+int  fcgpu_flow_set_time(fcgpu_ctx *ctx, uint32_t now_ms);
+/* One maintainer run at time now_ms, queued after the batches submitted
+ * before it (on the context's own stream when it has one -- span submissions
+ * -- else on `stream`, NULL = the null stream). No-op without timeouts. */
+int  fcgpu_flow_maintain(fcgpu_ctx *ctx, uint32_t now_ms, void *stream);
+typedef struct fcgpu_flow_stat {
+    uint32_t manager, capacity;
+    uint32_t count;         /* flows in the table ("count" handler) */
+    uint32_t free_ids;      /* IDs the stack can still give ("count_fids", :390-391) */
+    uint32_t pending;       /* IDs released by the last run, back on the stack at the next */
+    uint32_t epochs;        /* maintainer runs so far (the wheel index) */
+} fcgpu_flow_stat;
+/* Synchronises the context's device work. */
+int  fcgpu_flow_stats(fcgpu_ctx *ctx, fcgpu_flow_stat *st);
 
 /* Host threads the context may use for the gather / copy-out loops of
  * fcgpu_process_host (the caller's thread included; default 1). */

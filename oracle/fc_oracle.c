@@ -612,29 +612,41 @@ static void fco_flow_grow(fco_flowtab *t)
     free(old);
 }
 
+/* Packet i's IPFlow5ID, or 0 when it has no flow. The manager sits after the
+ * checks, before the classifier and the header rewrites: packets those drop
+ * still have a flow. */
+static int fco_flow_key(const uint8_t *arena, const uint32_t *desc, const uint16_t *verdict,
+                        const fcgpu_anno *anno, uint32_t i, uint32_t k[4])
+{
+    uint32_t reason = verdict[i] & 0xff;
+    if (anno[i].ipver != 4 || (reason != FCGPU_R_OK && reason != FCGPU_R_NO_MATCH &&
+                               reason != FCGPU_R_TTL_EXPIRED && reason != FCGPU_R_SETCKSUM_BAD))
+        return 0;
+    const uint8_t *nh = arena + desc[2 * i] + anno[i].nh;
+    const uint8_t *th = arena + desc[2 * i] + anno[i].th;
+    /* IPFlow5ID(p) (lib/ipflowid.cc:29-46, :91-94): a non-first fragment
+     * returns before assign(), so its addresses stay IPAddress() = 0
+     * (ipaddress.hh:21-22) and its ports unset (defined here as 0);
+     * only ip_p is filled in */
+    k[0] = k[1] = k[2] = 0;
+    k[3] = nh[9];
+    if (((((uint32_t)nh[6] << 8) | nh[7]) & 0x1fff) == 0) {   /* IP_FIRSTFRAG */
+        memcpy(&k[0], nh + 12, 4);
+        memcpy(&k[1], nh + 16, 4);
+        memcpy(&k[2], th, 4);
+    }
+    return 1;
+}
+
 void fco_flow_batch(fco_flowtab *t, const uint8_t *arena, const uint32_t *desc, uint32_t n,
                     const uint16_t *verdict, const fcgpu_anno *anno, uint32_t *flowid)
 {
     for (uint32_t i = 0; i < n; i++) {
-        uint32_t reason = verdict[i] & 0xff;
         flowid[i] = FCGPU_FLOW_NONE;
-        /* the manager sits after the checks, before the classifier and the
-         * header rewrites: packets those drop still have a flow */
-        if (anno[i].ipver != 4 || (reason != FCGPU_R_OK && reason != FCGPU_R_NO_MATCH &&
-                                   reason != FCGPU_R_TTL_EXPIRED && reason != FCGPU_R_SETCKSUM_BAD))
+        uint32_t k[4];
+        if (!fco_flow_key(arena, desc, verdict, anno, i, k))
             continue;
-        const uint8_t *nh = arena + desc[2 * i] + anno[i].nh;
-        const uint8_t *th = arena + desc[2 * i] + anno[i].th;
-        /* IPFlow5ID(p) (lib/ipflowid.cc:29-46, :91-94): a non-first fragment
-         * returns before assign(), so its addresses stay IPAddress() = 0
-         * (ipaddress.hh:21-22) and its ports unset (defined here as 0);
-         * only ip_p is filled in */
-        uint32_t s = 0, d = 0, p = 0, pr = nh[9];
-        if (((((uint32_t)nh[6] << 8) | nh[7]) & 0x1fff) == 0) {   /* IP_FIRSTFRAG */
-            memcpy(&s, nh + 12, 4);
-            memcpy(&d, nh + 16, 4);
-            memcpy(&p, th, 4);
-        }
+        const uint32_t s = k[0], d = k[1], p = k[2], pr = k[3];
         if (2 * (t->n + 1) > t->cap) fco_flow_grow(t);
         fco_flow_ent *e = fco_flow_slot(t, s, d, p, pr);
         if (!e->used) {
@@ -646,4 +658,176 @@ void fco_flow_batch(fco_flowtab *t, const uint8_t *arena, const uint32_t *desc, 
         }
         flowid[i] = e->id;
     }
+}
+
+/* ---- Flow table with timeouts: VirtualFlowManagerIMP over a FlowManagerIMPState
+ * (include/click/flow/virtualflowmanager.hh; FlowIPManager_CuckooPP,
+ * elements/flow/flowipmanager_cuckoopp.cc:57-110, is its table) ----
+ * Written the reference's way -- a LIFO free-ID stack, a timer wheel of
+ * singly linked lists, a released list pushed back one maintainer run later
+ * -- so that the device's array formulation is checked against the linked
+ * one. Time is the caller's, in ms (Timestamp::recent_steady at push_batch and
+ * at the maintainer run); only differences of at most 2^31 ms are meaningful.
+ *
+ *   stack: initialised by pushing 0 .. cap-1 (:113-115), pops from the top
+ *     (:36-38); the reference treats a popped 0 as "table full" (:264-268) and
+ *     then reads below the stack on the next pop -- here the table is full
+ *     while only 0 is left (the same until that point; defined after it).
+ *   process (:249-327): a hit refreshes lastseen; a new flow pops an ID, is
+ *     inserted, and is scheduled TE epochs ahead (:293-296). lastseen = the
+ *     batch's time for every flow with a packet in the batch (:236-239,311-313).
+ *   maintainer (:151-223): push the IDs released by the previous run (:155-161,
+ *     walking the list from its head), then run the wheel's current bucket
+ *     (timerwheel.hh run_timers: from the bucket's head, LIFO): lastseen not in
+ *     the past -> reschedule after TE; old + interval >= timeout -> remove the
+ *     key and prepend the ID to the released list; else reschedule after
+ *     (timeout - old) * eps / 1000 epochs. Then the wheel index advances. */
+#define FCO_NIL 0xffffffffu
+struct fco_imp {
+    uint32_t cap, hmask, nb;
+    uint32_t *stack; int64_t si;
+    uint32_t (*key)[4];
+    uint32_t *hhead, *hnext, *lastseen, *whead, *wnext, *qnext;
+    uint8_t *live;
+    uint32_t qhead, windex;
+    uint32_t to_ms, ri_ms, eps, te;
+    uint32_t count;
+};
+
+static uint32_t fco_next_pow2(uint32_t x)
+{
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+fco_imp *fco_imp_new(uint32_t capacity, uint32_t timeout_s, uint32_t recycle_ms)
+{
+    fco_imp *t = (fco_imp *)calloc(1, sizeof(*t));
+    t->cap = fco_next_pow2(capacity ? capacity : 1);
+    t->hmask = fco_next_pow2(2 * t->cap) - 1;
+    t->stack = (uint32_t *)malloc(sizeof(uint32_t) * (t->cap + 1));
+    t->si = -1;
+    for (uint32_t i = 0; i < t->cap; i++) t->stack[++t->si] = i;
+    t->key = (uint32_t (*)[4])calloc(t->cap, sizeof(uint32_t[4]));
+    t->hhead = (uint32_t *)malloc(sizeof(uint32_t) * (t->hmask + 1));
+    for (uint32_t i = 0; i <= t->hmask; i++) t->hhead[i] = FCO_NIL;
+    t->hnext = (uint32_t *)calloc(t->cap, sizeof(uint32_t));
+    t->lastseen = (uint32_t *)calloc(t->cap, sizeof(uint32_t));
+    t->wnext = (uint32_t *)calloc(t->cap, sizeof(uint32_t));
+    t->qnext = (uint32_t *)calloc(t->cap, sizeof(uint32_t));
+    t->live = (uint8_t *)calloc(t->cap, 1);
+    t->qhead = FCO_NIL;
+    /* parse (:58-79) */
+    t->ri_ms = recycle_ms;
+    t->eps = recycle_ms ? 1000 / recycle_ms : 1;
+    if (t->eps < 1) t->eps = 1;
+    t->to_ms = timeout_s * 1000;
+    t->te = timeout_s * t->eps;
+    t->nb = t->te ? fco_next_pow2(t->te + 2) : 1;   /* TimerWheel::initialize */
+    t->whead = (uint32_t *)malloc(sizeof(uint32_t) * t->nb);
+    for (uint32_t i = 0; i < t->nb; i++) t->whead[i] = FCO_NIL;
+    return t;
+}
+
+void fco_imp_free(fco_imp *t)
+{
+    if (!t) return;
+    free(t->stack); free(t->key); free(t->hhead); free(t->hnext); free(t->lastseen);
+    free(t->whead); free(t->wnext); free(t->qnext); free(t->live); free(t);
+}
+
+static uint32_t fco_imp_bucket(const fco_imp *t, const uint32_t k[4])
+{
+    return fco_flow_h(k[0], k[1], k[2], k[3]) & t->hmask;
+}
+
+static uint32_t fco_imp_find(const fco_imp *t, const uint32_t k[4])
+{
+    for (uint32_t id = t->hhead[fco_imp_bucket(t, k)]; id != FCO_NIL; id = t->hnext[id])
+        if (!memcmp(t->key[id], k, 16)) return id;
+    return FCO_NIL;
+}
+
+static void fco_imp_remove(fco_imp *t, uint32_t id)
+{
+    uint32_t *pp = &t->hhead[fco_imp_bucket(t, t->key[id])];
+    while (*pp != id) pp = &t->hnext[*pp];
+    *pp = t->hnext[id];
+    t->live[id] = 0;
+    t->count--;
+}
+
+/* TimerWheel::schedule_after: prepend to bucket (index + after) & mask */
+static void fco_imp_schedule(fco_imp *t, uint32_t id, uint32_t after)
+{
+    const uint32_t b = (t->windex + after) & (t->nb - 1);
+    t->wnext[id] = t->whead[b];
+    t->whead[b] = id;
+}
+
+void fco_imp_batch(fco_imp *t, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                   const uint16_t *verdict, const fcgpu_anno *anno, uint32_t now_ms, uint32_t *flowid)
+{
+    for (uint32_t i = 0; i < n; i++) {
+        flowid[i] = FCGPU_FLOW_NONE;
+        uint32_t k[4];
+        if (!fco_flow_key(arena, desc, verdict, anno, i, k))
+            continue;
+        uint32_t id = fco_imp_find(t, k);
+        if (id == FCO_NIL) {
+            if (t->si <= 0) { flowid[i] = FCGPU_FLOW_FULL; continue; }   /* only ID 0 left */
+            id = t->stack[t->si--];
+            memcpy(t->key[id], k, 16);
+            const uint32_t b = fco_imp_bucket(t, k);
+            t->hnext[id] = t->hhead[b];
+            t->hhead[b] = id;
+            t->live[id] = 1;
+            t->count++;
+            if (t->te) fco_imp_schedule(t, id, t->te);
+        }
+        t->lastseen[id] = now_ms;
+        flowid[i] = id;
+    }
+}
+
+uint32_t fco_imp_maintain(fco_imp *t, uint32_t now_ms)
+{
+    if (!t->te) return 0;
+    while (t->qhead != FCO_NIL) {               /* :155-161 */
+        const uint32_t next = t->qnext[t->qhead];
+        t->stack[++t->si] = t->qhead;
+        t->qhead = next;
+    }
+    uint32_t removed = 0;
+    const uint32_t cur = t->windex & (t->nb - 1);
+    uint32_t f = t->whead[cur];
+    while (f != FCO_NIL) {                      /* run_timers */
+        const uint32_t next = t->wnext[f];
+        const int32_t old = (int32_t)(now_ms - t->lastseen[f]);
+        if (old <= 0) {
+            fco_imp_schedule(t, f, t->te);      /* :174-180 */
+        } else if ((uint32_t)old + t->ri_ms >= t->to_ms) {
+            fco_imp_remove(t, f);               /* :185-205 */
+            t->qnext[f] = t->qhead;
+            t->qhead = f;
+            removed++;
+        } else {
+            const uint32_t r = ((t->to_ms - (uint32_t)old) * t->eps) / 1000u;   /* :209-211 */
+            fco_imp_schedule(t, f, r);
+        }
+        f = next;
+    }
+    t->whead[cur] = FCO_NIL;
+    t->windex++;
+    return removed;
+}
+
+void fco_imp_stats(const fco_imp *t, uint32_t *count, uint32_t *free_ids, uint32_t *pending)
+{
+    uint32_t q = 0;
+    for (uint32_t f = t->qhead; f != FCO_NIL; f = t->qnext[f]) q++;
+    *count = t->count;
+    *free_ids = t->si > 0 ? (uint32_t)t->si : 0;   /* IDs the stack can still give */
+    *pending = q;
 }

@@ -68,6 +68,18 @@ uint32_t fco_flow_count(const fco_flowtab *t);
 void fco_flow_batch(fco_flowtab *t, const uint8_t *arena, const uint32_t *desc, uint32_t n,
                     const uint16_t *verdict, const fcgpu_anno *anno, uint32_t *flowid);
 
+/* Flow table with timeouts (VirtualFlowManagerIMP + FlowManagerIMPState,
+ * include/click/flow/virtualflowmanager.hh): IDs from a LIFO free-ID stack,
+ * a timer wheel expiring idle flows, released IDs reused one maintainer run
+ * later. Times in ms. See fc_oracle.c for the rules. */
+typedef struct fco_imp fco_imp;
+fco_imp *fco_imp_new(uint32_t capacity, uint32_t timeout_s, uint32_t recycle_ms);
+void fco_imp_free(fco_imp *t);
+void fco_imp_batch(fco_imp *t, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                   const uint16_t *verdict, const fcgpu_anno *anno, uint32_t now_ms, uint32_t *flowid);
+uint32_t fco_imp_maintain(fco_imp *t, uint32_t now_ms);
+void fco_imp_stats(const fco_imp *t, uint32_t *count, uint32_t *free_ids, uint32_t *pending);
+
 /* Individual pieces, exposed for known-answer tests. */
 uint32_t fco_ipflowid_hash(uint32_t saddr_raw, uint16_t sport_net,
                            uint32_t daddr_raw, uint16_t dport_net);  /* A6 */

@@ -62,6 +62,17 @@ def load():
     lib.fco_flow_batch.restype = None
     lib.fco_flow_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
                                    C.c_void_p, C.c_void_p]
+    lib.fco_imp_new.restype = C.c_void_p
+    lib.fco_imp_new.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
+    lib.fco_imp_free.restype = None
+    lib.fco_imp_free.argtypes = [C.c_void_p]
+    lib.fco_imp_batch.restype = None
+    lib.fco_imp_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                  C.c_void_p, C.c_uint32, C.c_void_p]
+    lib.fco_imp_maintain.restype = C.c_uint32
+    lib.fco_imp_maintain.argtypes = [C.c_void_p, C.c_uint32]
+    lib.fco_imp_stats.restype = None
+    lib.fco_imp_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     _lib = lib
     return lib
 
@@ -130,6 +141,36 @@ class FlowTable:
     def __del__(self):
         if getattr(self, "t", None):
             self.lib.fco_flow_free(self.t)
+            self.t = None
+
+
+class ImpFlowTable:
+    """VirtualFlowManagerIMP restatement (fc_oracle.c fco_imp_*): IDs popped
+    from a free-ID stack, idle flows expired by a timer wheel. Times in ms."""
+
+    def __init__(self, capacity, timeout_s=0, recycle_ms=1000):
+        self.lib = load()
+        self.t = self.lib.fco_imp_new(capacity, timeout_s, recycle_ms)
+
+    def batch(self, batch, res, now_ms):
+        flowid = np.zeros(batch.n, np.uint32)
+        arena = np.ascontiguousarray(batch.arena)
+        desc = np.ascontiguousarray(batch.desc, dtype=np.uint32)
+        self.lib.fco_imp_batch(self.t, _p(arena), _p(desc), batch.n, _p(res["verdict"]),
+                               _p(np.ascontiguousarray(res["anno"])), now_ms & 0xFFFFFFFF, _p(flowid))
+        return flowid
+
+    def maintain(self, now_ms):
+        return self.lib.fco_imp_maintain(self.t, now_ms & 0xFFFFFFFF)
+
+    def stats(self):
+        v = (C.c_uint32 * 3)()
+        self.lib.fco_imp_stats(self.t, C.byref(v, 0), C.byref(v, 4), C.byref(v, 8))
+        return dict(count=v[0], free_ids=v[1], pending=v[2])
+
+    def __del__(self):
+        if getattr(self, "t", None):
+            self.lib.fco_imp_free(self.t)
             self.t = None
 
 
