@@ -89,6 +89,10 @@ def parse(argv=None):
                     help="> 0: the device flow table (FlowIPManagerHMP flow IDs, fcgpu_flow_enable) "
                          "behind the check, with this many IDs; its new-flow pass runs every step "
                          "(one stream: the table assigns IDs in batch order)")
+    ap.add_argument("--errors", type=float, default=0.0,
+                    help="c2/c4: corrupt this fraction of the packets per error kind (bad version, "
+                         "header length, ip_len, checksum, BADSRC source; SURVEY 8(d) 'with-errors "
+                         "mix', e.g. 0.01); the invalid ones leave on the drop output")
     ap.add_argument("--flow-manager", choices=["hmp", "imp"], default="hmp",
                     help="hmp: FlowIPManagerHMP IDs 0,1,2,...; imp: VirtualFlowManagerIMP (free-ID "
                          "stack; with --flow-timeout, every packet stamps its flow and the maintainer "
@@ -111,6 +115,8 @@ def parse(argv=None):
         a.workload = "c4" if a.shard == "strong" else "c2"
     if a.frame_bytes != 64 and a.workload not in ("c2", "c4"):
         ap.error("--frame-bytes applies to c2/c4")
+    if a.errors and (a.workload not in ("c2", "c4") or a.frame_bytes != 64 or not 0 < a.errors <= 0.2):
+        ap.error("--errors applies to 64-B c2/c4, with a rate in (0, 0.2]")
     if not 64 <= a.frame_bytes <= 1518:
         ap.error("--frame-bytes must be in [64, 1518]")
     if a.flow_capacity and a.streams > 1:
@@ -264,7 +270,25 @@ def shard_of(args, world, rank):
     return 0, args.packets
 
 
+# CheckIPHeader(BADSRC ..) of the with-errors mix (the addresses synth's
+# BADSRC errors use, plus the limited broadcast)
+ERROR_BADSRC = ("192.0.2.255", "255.255.255.255")
+
+
 def make_host_batch(args):
+    """The workload's host batch; with --errors also the number of packets
+    the mix leaves valid."""
+    from fastclick_amd import synth
+    b = _make_host_batch(args)
+    if not args.errors:
+        return b, b.n
+    kind = synth.inject_errors(b, args.errors, seed=41,
+                               kinds=(synth.ERR_VERSION, synth.ERR_HLEN, synth.ERR_IPLEN, synth.ERR_CKSUM,
+                                      synth.ERR_BADSRC))
+    return b, int((kind < 0).sum())
+
+
+def _make_host_batch(args):
     from fastclick_amd import synth
     n = args.packets
     if args.workload in ("c2", "c4") and args.frame_bytes != 64:
@@ -293,7 +317,7 @@ class DeviceProcessor:
         self.N, self.torch, self.args = N, torch, args
         dev = torch.device("cuda", gpu)
         self.dev = dev
-        host = make_host_batch(args)
+        host, self.valid_per_batch = make_host_batch(args)
         self.frame_meta = dict(slot=int(host.desc[1, 0] - host.desc[0, 0]) if host.n > 1 else 64,
                                captured=int(host.desc[0, 1]))
         n = hi - lo
@@ -313,7 +337,8 @@ class DeviceProcessor:
         classify = (N.CLS_PROGRAM if program is not None else
                     N.CLS_LB_CRC if args.classify == "lbcrc" else N.CLS_LB_HASH)
         cfg = N.make_cfg(check_mode=N.CHECK_AUTO if self.auto else N.CHECK_IP4, offset=0 if self.auto else 14,
-                         checksum=True, hash_mode=N.HASH_FLOWID, classify=classify, nports=args.nports)
+                         checksum=True, hash_mode=N.HASH_FLOWID, classify=classify, nports=args.nports,
+                         badsrc=[N.raw_addr(a) for a in ERROR_BADSRC] if args.errors else ())
         part = N.PART_TILE if args.partition == "tile" else N.PART_GLOBAL
         tile = part == N.PART_TILE
         self.ctx = N.Context(gpu, max(n, 1), cfg)
@@ -460,6 +485,10 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
     total_pkts = (args.packets if args.shard == "strong" else args.packets * world) * args.steps
     valid = int(gv[N.CTR_COUNT])
     expect_valid = total_pkts if args.workload in ("c2", "c4") else None
+    vpb = getattr(proc, "valid_per_batch", None)
+    if args.errors and vpb is not None:
+        # every rank builds the whole batch: the strong shards add up to it
+        expect_valid = vpb * args.steps * (1 if args.shard == "strong" else world)
     if expect_valid is not None and valid != expect_valid:
         raise AssertionError(f"valid count {valid} != {expect_valid}")
     if not np.array_equal(gtot, gv[N.CTR_PORT:N.CTR_PORT + nb].astype(np.int64)):
@@ -521,6 +550,8 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
             "workload": (wl
                          + ("; StripEtherVLANHeader + CheckIP6Header/CheckIPHeader(CHECKSUM true)"
                             if auto else "; CheckIPHeader(CHECKSUM true)")
+                         + (f" (with-errors mix: {args.errors:g} each of bad version, header length, "
+                            f"ip_len, checksum, BADSRC)" if args.errors else "")
                          + ((f" + FlowIPManagerHMP flow table ({args.flow_capacity} IDs)"
                              if args.flow_manager == "hmp" else
                              f" + VirtualFlowManagerIMP flow table (CAPACITY {args.flow_capacity}, "
@@ -535,6 +566,8 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                             if args.partition == "tile" else
                             " + stable per-port partition of the whole batch")),
             "classify": args.classify,
+            **({"errors_per_kind": args.errors,
+                "valid_fraction": round(valid / total_pkts, 4)} if args.errors else {}),
             "partition": "none" if args.no_perm else args.partition,
             "streams": max(1, args.streams),
             "frame_bytes": fb,

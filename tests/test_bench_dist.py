@@ -29,9 +29,10 @@ class OracleProcessor:
         import bench
         from fastclick_amd import synth, _native as N
         from oracle import oracle as O
-        b = bench.make_host_batch(args)
+        b, self.valid_per_batch = bench.make_host_batch(args)
         shard = synth.Batch(arena=b.arena, desc=np.ascontiguousarray(b.desc[lo:hi]))
-        cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=args.nports)
+        cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=args.nports,
+                         badsrc=[N.raw_addr(a) for a in bench.ERROR_BADSRC] if args.errors else ())
         self.per_step = O.process_batch(cfg, shard)["counters"].astype(np.int64)
         self.steps = args.steps
         self.ctr = torch.zeros(N.CTR_SHARDS, N.NCOUNTERS, dtype=torch.int64)
@@ -99,6 +100,17 @@ def test_bench_rank_main_strong_two_ranks(oracle):
     assert line["config"]["packets_per_step"] == 20000
     assert (res[0][2], res[0][3], res[1][2], res[1][3]) == (0, 10000, 10000, 20000)
     assert line["value"] > 0 and line["steps"] == 3
+
+
+@pytest.mark.timeout(300)
+def test_bench_rank_main_errors_two_ranks(oracle):
+    """--errors: the with-errors mix; rank_main checks the
+    all-reduced valid count against the packets the mix left valid."""
+    res = _run_two(["--gpus", "2", "--shard", "strong", "--packets", "20000", "--steps", "2",
+                    "--warmup", "1", "--no-cpu", "--nbuf", "1", "--errors", "0.01", "--workload", "c4"])
+    line = res[0][1]
+    assert line["config"]["errors_per_kind"] == 0.01
+    assert 0.93 < line["config"]["valid_fraction"] < 0.97
 
 
 @pytest.mark.timeout(300)
