@@ -10,11 +10,12 @@ step = one pass of the hot path over one batch:
 i.e. k_rx of libfcgpu.so (plus k_scan + k_part with --partition global).
 Steps rotate over --nbuf distinct batches placed in different HBM regions
 (default 16 x 72 MB of touched bytes = 1.15 GB > the 256 MB Infinity Cache),
-so every step reads its packets from HBM. Consecutive steps alternate over
---streams HIP streams (default 2: two rx queues feeding one GPU, each batch
-with its own outputs), so one batch's tail overlaps the next one's head. The
-timed steps are submitted by one fcgpu_process_jobs call (the C ABI loops
-over them; no per-step Python on the launch path).
+so every step reads its packets from HBM. The timed steps are submitted by
+one fcgpu_process_jobs call (no per-step Python on the launch path), each
+with its own output buffers, on one stream (--streams: more streams, as rx
+queues would); the library fuses a stream's queued batches into k_rx
+launches of up to 24 batches (--fuse), so the launch ramp and tail are paid
+once per launch, not once per batch.
 
 Multi-GPU: one process per GPU (torchrun, or `--gpus N` without WORLD_SIZE,
 which starts the N local rank processes itself). --shard weak (default):
@@ -63,15 +64,22 @@ def parse(argv=None):
     ap.add_argument("--partition", choices=["tile", "global"], default="tile",
                     help="tile: each 256-packet tile is one classified PacketBatch (1 launch); "
                          "global: the whole batch is one (3 launches)")
+    ap.add_argument("--fuse", type=int, default=24,
+                    help="batches one k_rx launch may carry (fcgpu_process_jobs fuses consecutive jobs of "
+                         "a stream whose outputs are disjoint, up to 24): each step gets its own output set "
+                         "among fuse x streams; 1 = one launch per batch")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
     ap.add_argument("--timing-every", type=int, default=0,
                     help="bracket every k-th timed launch with HIP events (hipExtLaunchKernelGGL "
                          "start/stop on the launch stream; created before the timed region). Each "
-                         "event idles the queue ~4 us, so the default samples sparsely: 8, or "
-                         "steps/2 below 64 steps")
-    ap.add_argument("--streams", type=int, default=2,
+                         "event idles the queue ~4 us, so the default samples sparsely: every 8th "
+                         "timed launch from 64 steps; below 64 steps the timed region carries no "
+                         "events and the kernel time comes from a pass of 64 launches after it, "
+                         "every 8th bracketed")
+    ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams the consecutive steps alternate over (each with its own output "
-                         "buffers), as batches of several rx queues would")
+                         "buffers), as batches of several rx queues would. Default 1: the steps are "
+                         "queued on one stream and fused into k_rx launches of up to --fuse batches")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse "
                          "several ranks on one GPU)")
@@ -353,14 +361,20 @@ class DeviceProcessor:
             else:
                 self.ctx.flow_enable(args.flow_capacity)
         self.streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
+        # one output set per step of a fused launch (fcgpu_process_jobs
+        # fuses only jobs whose outputs do not overlap)
+        nsets = len(self.streams) * max(1, min(args.fuse, 24))
         self.outs = [DeviceOutputs(max(n, 1), args.nports, device=dev, verdict=True, hash=True, anno=False,
                                    perm=(not args.no_perm) and not tile,
                                    tile_perm=(not args.no_perm) and tile, port_start=not args.no_perm,
                                    partition=part, flowid=args.flow_capacity > 0)
-                     for _ in self.streams]
+                     for _ in range(nsets)]
         self.ctr = torch.zeros(N.CTR_SHARDS, N.NCOUNTERS, dtype=torch.int64, device=dev)
-        self.timing_every = 0 if args.no_timing else (
-            args.timing_every or (8 if args.steps >= 64 else max(1, args.steps // 2)))
+        self.timing_every = 0 if args.no_timing else (args.timing_every or 8)
+        # a short timed region stays free of events; its kernel time is
+        # sampled by a pass of the same launches after it
+        self.post_timing = bool(self.timing_every) and not args.timing_every and args.steps < 64
+        self.warm_steps = 0
 
     def _jobs(self, first, count):
         specs = []
@@ -368,7 +382,8 @@ class DeviceProcessor:
         for k in range(first, first + count):
             a, d = self.bufs[k % len(self.bufs)]
             j = k % ns
-            specs.append((a.data_ptr(), d.data_ptr(), self.n, self.streams[j].cuda_stream, self.outs[j].ptrs()))
+            specs.append((a.data_ptr(), d.data_ptr(), self.n, self.streams[j].cuda_stream,
+                          self.outs[k % len(self.outs)].ptrs()))
         return self.ctx.jobs(specs)
 
     def warmup(self, steps):
@@ -382,6 +397,7 @@ class DeviceProcessor:
                 d.max()
             self.torch.cuda.synchronize()
         warm = self._jobs(0, steps)
+        self.warm_steps = steps
         self.timed = self._jobs(steps, self.args.steps)   # built before the warmup
         self.ctx.set_timing(self.timing_every)      # creates the event pool now
         self.ctx.run_jobs(warm)
@@ -389,7 +405,9 @@ class DeviceProcessor:
         self.ctx.read_timing()                      # drop warmup samples
         if self.args.flow_capacity and self.args.flow_manager == "imp" and self.args.flow_timeout:
             self._time_maintainer()
-        self.ctx.set_timing(self.timing_every)      # sample count restarts at the timed region
+        # sample count restarts at the timed region (no events in it when the
+        # timing pass follows it)
+        self.ctx.set_timing(0 if self.post_timing else self.timing_every)
         self.ctx.use_counters(self.ctr.data_ptr())  # timed steps count into the tensor
 
     def _time_maintainer(self):
@@ -422,6 +440,16 @@ class DeviceProcessor:
     def timing(self):
         if not self.timing_every:
             return None
+        if self.post_timing:
+            # after the timed region: the rotation continues for 64 launches,
+            # every 8th bracketed; counted into the context's own counters, not
+            # the timed region's
+            self.torch.cuda.synchronize()
+            self.ctx.use_counters(0)
+            post = self._jobs(self.warm_steps + self.args.steps, 64)
+            self.ctx.set_timing(self.timing_every)
+            self.ctx.run_jobs(post)
+            self.torch.cuda.synchronize()
         ms, cnt = self.ctx.read_timing()
         return dict(k_rx_ms=ms[0] / max(cnt[0], 1), k_scan_ms=ms[1] / max(cnt[1], 1),
                     k_part_ms=ms[2] / max(cnt[2], 1), launches=cnt)
@@ -521,10 +549,14 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
         roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, kernel="k_rx", basis=basis,
                     bytes_per_launch=PKT_BYTES_READ * per_gpu,
+                    per="batch (a k_rx launch carries up to config.batches_per_launch batches: "
+                        "kernel_ms = a launch's event time / its batches)",
                     kernel_ms=round(timing["k_rx_ms"], 5),
                     kernel_frac=round(PKT_BYTES_READ * per_gpu / kernel_s / 1e9 / HBM_PEAK_GBS, 4),
                     scan_ms=round(timing["k_scan_ms"], 5), part_ms=round(timing["k_part_ms"], 5),
-                    sampled_launches=timing["launches"][0])
+                    sampled_launches=timing["launches"][0],
+                    sampled_in=("a pass of 64 launches after the timed region" if getattr(proc, "post_timing", False)
+                                else "the timed region"))
     cpu = None
     if world == 1 and not args.no_cpu and args.workload in ("c2", "c3", "c4") and not args.flow_capacity:
         cpu = cpu_baseline(args.cpu_seconds, flows=dict(c2=1, c3=10000).get(args.workload, 4096),
@@ -570,6 +602,8 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                 "valid_fraction": round(valid / total_pkts, 4)} if args.errors else {}),
             "partition": "none" if args.no_perm else args.partition,
             "streams": max(1, args.streams),
+            "batches_per_launch": (1 if args.flow_capacity or args.partition == "global" else
+                                   max(1, min(args.fuse, 24, -(-args.steps // max(1, args.streams))))),
             "frame_bytes": fb,
             "packets_per_step_per_gpu": per_gpu,
             "packets_per_step": args.packets if args.shard == "strong" else args.packets * world,

@@ -44,6 +44,7 @@ constexpr uint32_t kArenaPad = 256;
 struct EvPair {
     hipEvent_t a, b;
     int stage;
+    uint32_t batches = 1;     // batches the bracketed launch processed (fused jobs)
 };
 
 constexpr size_t kTimingEvents = 6 * 64;     // pre-created by fcgpu_set_timing
@@ -289,56 +290,68 @@ static hipEvent_t take_event(fcgpu_ctx *c) {
 
 // ev0/ev1 non-null: hipExtLaunchKernelGGL records them around the dispatch
 // itself (timestamps of the kernel, not of the stream around it).
+// L: one batch (njobs 1, grid = its tiles) or several fused ones (grid =
+// their tiles end to end).
 template <int CM, bool CK, int PART, bool PROG, bool L4, bool FLOW = false>
-static void launch_rx(const RxArgs &a, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-    const size_t lds = prog_lds_bytes(a.cfg);   // program steps (PROG) or CRC tables (LB_CRC), else 0
+static void launch_rx(const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    const size_t lds = prog_lds_bytes(L.A.cfg);   // program steps (PROG) or CRC tables (LB_CRC), else 0
     if (ev0)
-        hipExtLaunchKernelGGL((k_rx<CM, CK, PART, PROG, L4, FLOW>), dim3(a.ntiles), dim3(kTile), lds, s, ev0, ev1,
-                              0, a);
+        hipExtLaunchKernelGGL((k_rx<CM, CK, PART, PROG, L4, FLOW>), dim3(grid), dim3(kTile), lds, s, ev0, ev1,
+                              0, L);
     else
-        hipLaunchKernelGGL((k_rx<CM, CK, PART, PROG, L4, FLOW>), dim3(a.ntiles), dim3(kTile), lds, s, a);
+        hipLaunchKernelGGL((k_rx<CM, CK, PART, PROG, L4, FLOW>), dim3(grid), dim3(kTile), lds, s, L);
 }
 
 // IPv4 check modes: L4 (CheckUDPHeader/CheckTCPHeader) and the flow table
 // exist only there (fcgpu_configure / fcgpu_process reject them with CHECK_AUTO).
 template <int CM, bool CK, int PART, bool PROG>
-static void launch_rx_ip4(const RxArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    const bool l4 = a.cfg.l4_mode != FCGPU_L4_NONE, flow = a.fl.slots != nullptr;
+static void launch_rx_ip4(const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    const bool l4 = L.A.cfg.l4_mode != FCGPU_L4_NONE, flow = L.A.fl.slots != nullptr;
     if (flow) {
-        if (l4) launch_rx<CM, CK, PART, PROG, true, true>(a, s, e0, e1);
-        else launch_rx<CM, CK, PART, PROG, false, true>(a, s, e0, e1);
+        if (l4) launch_rx<CM, CK, PART, PROG, true, true>(L, grid, s, e0, e1);
+        else launch_rx<CM, CK, PART, PROG, false, true>(L, grid, s, e0, e1);
     } else {
-        if (l4) launch_rx<CM, CK, PART, PROG, true>(a, s, e0, e1);
-        else launch_rx<CM, CK, PART, PROG, false>(a, s, e0, e1);
+        if (l4) launch_rx<CM, CK, PART, PROG, true>(L, grid, s, e0, e1);
+        else launch_rx<CM, CK, PART, PROG, false>(L, grid, s, e0, e1);
     }
 }
 
 template <int PART, bool PROG>
-static void launch_rx_part(uint32_t cm, bool ck, const RxArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+static void launch_rx_part(uint32_t cm, bool ck, const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     switch (cm * 2 + (ck ? 1 : 0)) {
-    case 0: launch_rx_ip4<FCGPU_CHECK_IP4, false, PART, PROG>(a, s, e0, e1); break;
-    case 1: launch_rx_ip4<FCGPU_CHECK_IP4, true, PART, PROG>(a, s, e0, e1); break;
-    case 2: case 3: launch_rx_ip4<FCGPU_MARK_IP4, false, PART, PROG>(a, s, e0, e1); break;
-    case 4: launch_rx<FCGPU_CHECK_AUTO, false, PART, PROG, false>(a, s, e0, e1); break;
-    case 6: case 7: launch_rx<FCGPU_MARK_IP6, false, PART, PROG, false>(a, s, e0, e1); break;
-    default: launch_rx<FCGPU_CHECK_AUTO, true, PART, PROG, false>(a, s, e0, e1); break;
+    case 0: launch_rx_ip4<FCGPU_CHECK_IP4, false, PART, PROG>(L, grid, s, e0, e1); break;
+    case 1: launch_rx_ip4<FCGPU_CHECK_IP4, true, PART, PROG>(L, grid, s, e0, e1); break;
+    case 2: case 3: launch_rx_ip4<FCGPU_MARK_IP4, false, PART, PROG>(L, grid, s, e0, e1); break;
+    case 4: launch_rx<FCGPU_CHECK_AUTO, false, PART, PROG, false>(L, grid, s, e0, e1); break;
+    case 6: case 7: launch_rx<FCGPU_MARK_IP6, false, PART, PROG, false>(L, grid, s, e0, e1); break;
+    default: launch_rx<FCGPU_CHECK_AUTO, true, PART, PROG, false>(L, grid, s, e0, e1); break;
     }
 }
 
 // PROG: the decision-program classifier is compiled only into the kernels
 // launched for FCGPU_CLS_PROGRAM, so the other modes keep their lean code.
 template <bool PROG>
-static void launch_rx_prog(int part, uint32_t cm, bool ck, const RxArgs &a, hipStream_t s, hipEvent_t e0,
+static void launch_rx_prog(int part, uint32_t cm, bool ck, const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_t e0,
                            hipEvent_t e1) {
-    if (part == kPartTile) launch_rx_part<kPartTile, PROG>(cm, ck, a, s, e0, e1);
-    else if (part == kPartGlobal) launch_rx_part<kPartGlobal, PROG>(cm, ck, a, s, e0, e1);
-    else launch_rx_part<kPartNone, PROG>(cm, ck, a, s, e0, e1);
+    if (part == kPartTile) launch_rx_part<kPartTile, PROG>(cm, ck, L, grid, s, e0, e1);
+    else if (part == kPartGlobal) launch_rx_part<kPartGlobal, PROG>(cm, ck, L, grid, s, e0, e1);
+    else launch_rx_part<kPartNone, PROG>(cm, ck, L, grid, s, e0, e1);
 }
 
-static void launch_rx_any(int part, uint32_t cm, bool ck, const RxArgs &a, hipStream_t s, hipEvent_t e0,
+static void launch_rx_any(int part, uint32_t cm, bool ck, const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_t e0,
                           hipEvent_t e1) {
-    if (a.cfg.classify == FCGPU_CLS_PROGRAM) launch_rx_prog<true>(part, cm, ck, a, s, e0, e1);
-    else launch_rx_prog<false>(part, cm, ck, a, s, e0, e1);
+    if (L.A.cfg.classify == FCGPU_CLS_PROGRAM) launch_rx_prog<true>(part, cm, ck, L, grid, s, e0, e1);
+    else launch_rx_prog<false>(part, cm, ck, L, grid, s, e0, e1);
+}
+
+// One batch: a.ntiles workgroups.
+static void launch_rx_one(int part, uint32_t cm, bool ck, const RxArgs &a, hipStream_t s, hipEvent_t e0,
+                          hipEvent_t e1) {
+    RxLaunch L;
+    L.A = a;
+    L.njobs = 1;
+    L.job_tiles = 0;
+    launch_rx_any(part, cm, ck, L, a.ntiles, s, e0, e1);
 }
 
 // Whole batch in one shot (FCGPU_PART_GLOBAL: the partition spans the batch).
@@ -991,7 +1004,7 @@ static int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_d
         HIPCHK(c, hipEventRecord(c->flow_order[0], c->stream));
         HIPCHK(c, hipStreamWaitEvent(s, c->flow_order[0], 0));
     }
-    launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, a, s, timed ? ev[0].a : nullptr,
+    launch_rx_one(part, c->cfg.check_mode, c->cfg.checksum != 0, a, s, timed ? ev[0].a : nullptr,
                   timed ? ev[0].b : nullptr);
     HIPCHK(c, hipGetLastError());
     if (a.fl.slots) {   // the batch's new flows get their IDs (fcgpu_flow.hh)
@@ -1042,6 +1055,86 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     return process_one(c, d_arena, d_desc, n, o, (hipStream_t)stream);   // NULL = the null stream
 }
 
+// The partition shape process_one launches k_rx with for these outputs.
+static int out_part(const fcgpu_out *o) {
+    const bool tile = o->partition == FCGPU_PART_TILE;
+    const bool want_global = !tile && (o->perm || o->port_start);
+    return tile && (o->perm || o->tile_perm) ? kPartTile : (want_global ? kPartGlobal : kPartNone);
+}
+
+// A job that may share a k_rx launch with others: no flow table (batch order
+// through the new-flow pass), no whole-batch partition (context scratch), no
+// in-place header rewrite (jobs may share an arena).
+static bool fusable(const fcgpu_ctx *c, const fcgpu_job &j) {
+    return j.n && !c->fl.slots && !c->cfg.rewrite && out_part(&j.out) != kPartGlobal;
+}
+
+static bool outputs_overlap(const fcgpu_out &x, const fcgpu_out &y) {
+    const void *a[] = {x.verdict, x.hash, x.anno, x.perm, x.tile_count, x.tile_perm};
+    const void *b[] = {y.verdict, y.hash, y.anno, y.perm, y.tile_count, y.tile_perm};
+    for (const void *p : a)
+        for (const void *q : b)
+            if (p && p == q) return true;
+    return false;
+}
+
+// Jobs grp[0..g) (fusable, one stream, one partition shape, disjoint outputs)
+// as one k_rx launch.
+static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, hipStream_t s) {
+    RxLaunch L;
+    const fcgpu_out &o0 = grp[0]->out;
+    const int part = out_part(&o0);
+    RxArgs &a = L.A;
+    a = RxArgs{};
+    a.tilecnt = c->d_tilecnt;
+    a.ctr = c->d_ctr;
+    a.cfg = c->dcfg;
+    a.fl = c->fl;
+    L.njobs = g;
+    uint32_t tiles = 0;
+    for (uint32_t k = 0; k < g; ++k) {
+        const fcgpu_job &j = *grp[k];
+        const bool tile = j.out.partition == FCGPU_PART_TILE;
+        RxJob &J = L.job[k];
+        J.arena = j.arena;
+        J.desc = reinterpret_cast<const uint2 *>(j.desc);
+        J.verdict = j.out.verdict;
+        J.hash = j.out.hash;
+        J.anno = j.out.anno;
+        J.perm = j.out.perm;
+        J.tile_count = j.out.tile_count;
+        J.tile_perm = tile ? j.out.tile_perm : nullptr;
+        J.n = j.n;
+        J.tile0 = tiles;
+        tiles += (j.n + kTile - 1) / kTile;
+    }
+    L.job_tiles = L.job[0].n ? (L.job[0].n + kTile - 1) / kTile : 0u;
+    for (uint32_t k = 1; k < g; ++k)
+        if (L.job[k].tile0 != k * L.job_tiles) L.job_tiles = 0;
+    if (tiles > g * L.job_tiles) L.job_tiles = 0;    // a last batch larger than the others
+    // the first job's pointers also fill A (a workgroup of a fused launch
+    // replaces them with its own job's)
+    a.arena = L.job[0].arena;
+    a.desc = L.job[0].desc;
+    a.n = L.job[0].n;
+    a.ntiles = (a.n + kTile - 1) / kTile;
+    // sampled timing counts batches: a fused launch is timed when it covers
+    // a multiple of timing_every
+    const uint64_t before = c->timing_seq;
+    bool timed = false;
+    if (c->timing_every) {
+        c->timing_seq += g;
+        timed = before / c->timing_every != c->timing_seq / c->timing_every;
+    }
+    EvPair ev;
+    if (timed) { ev.a = take_event(c); ev.b = take_event(c); ev.stage = 0; ev.batches = g; }
+    launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, L, tiles, s, timed ? ev.a : nullptr,
+                  timed ? ev.b : nullptr);
+    HIPCHK(c, hipGetLastError());
+    if (timed) c->pending.push_back(ev);
+    return FCGPU_OK;
+}
+
 int fcgpu_process_jobs(fcgpu_ctx *c, const fcgpu_job *jobs, uint32_t njobs, void *stream) {
     if (!c || (njobs && !jobs)) return FCGPU_EINVAL;
     // every job is checked before any is launched: a bad job launches nothing
@@ -1057,9 +1150,38 @@ int fcgpu_process_jobs(fcgpu_ctx *c, const fcgpu_job *jobs, uint32_t njobs, void
                                          "partition use context scratch (one stream only)");
     }
     HIPCHK(c, hipSetDevice(c->device));
+    auto eff = [&](const fcgpu_job &j) { return (hipStream_t)(j.stream ? j.stream : stream); };
+    // Per stream, in order: a fusable job and the stream's next fusable jobs
+    // (up to kMaxFuse, disjoint outputs, same partition shape, stopping at the
+    // stream's next non-fusable job) share one launch. Jobs on other streams
+    // are independent of them, so they are taken up in their own turn.
+    std::vector<uint8_t> done(njobs, 0);
+    std::vector<const fcgpu_job *> grp;
+    grp.reserve(kMaxFuse);
     for (uint32_t k = 0; k < njobs; ++k) {
+        if (done[k]) continue;
         const fcgpu_job &j = jobs[k];
-        int rc = process_one(c, j.arena, j.desc, j.n, &j.out, (hipStream_t)(j.stream ? j.stream : stream));
+        done[k] = 1;
+        if (!fusable(c, j)) {
+            int rc = process_one(c, j.arena, j.desc, j.n, &j.out, eff(j));
+            if (rc != FCGPU_OK) return rc;
+            continue;
+        }
+        const hipStream_t s = eff(j);
+        grp.assign(1, &j);
+        for (uint32_t m = k + 1; m < njobs && grp.size() < kMaxFuse; ++m) {
+            if (done[m] || eff(jobs[m]) != s) continue;
+            const fcgpu_job &x = jobs[m];
+            if (!fusable(c, x)) break;                  // the stream's order barrier
+            if (out_part(&x.out) != out_part(&j.out) || x.out.partition != j.out.partition) break;
+            bool clash = false;
+            for (const fcgpu_job *y : grp) clash = clash || outputs_overlap(x.out, y->out);
+            if (clash) break;
+            grp.push_back(&x);
+            done[m] = 1;
+        }
+        int rc = grp.size() == 1 ? process_one(c, j.arena, j.desc, j.n, &j.out, s)
+                                 : process_fused(c, grp.data(), (uint32_t)grp.size(), s);
         if (rc != FCGPU_OK) return rc;
     }
     return FCGPU_OK;
@@ -1638,7 +1760,7 @@ int fcgpu_read_timing(fcgpu_ctx *c, double *ms, uint32_t *launches, int nstages)
         float t = 0.f;
         HIPCHK(c, hipEventElapsedTime(&t, p.a, p.b));
         acc[p.stage] += t;
-        cnt[p.stage]++;
+        cnt[p.stage] += p.batches;
         c->free_ev.push_back(p.a);
         c->free_ev.push_back(p.b);
     }

@@ -1038,22 +1038,39 @@ __device__ __forceinline__ void rw_stage(const DevCfg &c, const FrameView &f, ui
     if (live && ip_rw) ip_rw[i] = changed ? w : 0u;
 }
 
+// The batch a workgroup works on: RxArgs' per-batch pointers, or (fused
+// launch) its job's. Plain scalars, so they stay in SGPRs.
+struct RxView {
+    const uint8_t *arena;
+    const uint2 *desc;
+    uint16_t *verdict;
+    uint32_t *hash;
+    fcgpu_anno *anno;
+    uint32_t *perm;
+    uint16_t *tile_count;
+    uint8_t *tile_perm;
+    uint32_t n;
+};
+__device__ __forceinline__ RxView rx_view(const RxArgs &A) {
+    return RxView{A.arena, A.desc, A.verdict, A.hash, A.anno, A.perm, A.tile_count, A.tile_perm, A.n};
+}
+
 // One 256-packet tile once its header window is in LDS: fused
 // [StripEtherVLANHeader ->] CheckIPHeader/CheckIP6Header -> AggregateHash ->
 // classify; per-wave histogram by ballots; counters by sharded atomics;
 // optionally the tile's stable per-output partition (CLASSIFY_EACH_PACKET on a
 // 256-packet PacketBatch).
 template <int CM, bool CK, int PART, bool PROG, bool L4, bool FAST, bool FLOW>
-__device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d, const uint8_t *wl,
+__device__ __forceinline__ void rx_tile(const RxArgs &A, const RxView &V, uint32_t tile, uint2 d, const uint8_t *wl,
                                         uint32_t (*s_cnt)[kMaxBins], const uint4 *sprog) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t i = tile * kTile + threadIdx.x;
-    const bool live = i < A.n;
+    const bool live = i < V.n;
     FrameView f;
     f.row = wl + lane * kWin;
     f.sw = (lane >> 2) & 3;
     f.shift = d.x & 15;
-    f.gwin = A.arena + (d.x & ~15u);
+    f.gwin = V.arena + (d.x & ~15u);
 
     PktResult r;
     r.an = fcgpu_anno{};
@@ -1079,15 +1096,15 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d,
     } else if (live) {
         process_packet<CM, CK, PROG>(A.cfg, f, d.y, r, sprog);
     }
-    if (L4) l4_stage(A.cfg, f, A.arena + d.x, live, r);
+    if (L4) l4_stage(A.cfg, f, V.arena + d.x, live, r);
     FlowProbe fq;
     if (FLOW) fq = flow_issue(A.fl, f, live, r);
     if (A.cfg.rewrite)   // launch-uniform
-        rw_stage(A.cfg, f, const_cast<uint8_t *>(A.arena) + d.x, live, r, A.ip_rw, i);
+        rw_stage(A.cfg, f, const_cast<uint8_t *>(V.arena) + d.x, live, r, A.ip_rw, i);
     if (live) {
-        if (A.verdict) A.verdict[i] = (uint16_t)(r.reason | (r.port << 8));
-        if (A.hash) A.hash[i] = r.hash;
-        if (A.anno) A.anno[i] = r.an;
+        if (V.verdict) V.verdict[i] = (uint16_t)(r.reason | (r.port << 8));
+        if (V.hash) V.hash[i] = r.hash;
+        if (V.anno) V.anno[i] = r.an;
         bin = r.port;
         if (r.reason != FCGPU_R_OK) rslot = reason_slot(r.reason);
     }
@@ -1115,7 +1132,7 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d,
     if (t < nbt) tot = s_cnt[0][t] + s_cnt[1][t] + s_cnt[2][t] + s_cnt[3][t];
     if (PART == kPartGlobal && t < nb) A.tilecnt[t * A.ntiles + tile] = tot;
     if (PART == kPartTile) {
-        if (t < nb) A.tile_count[(size_t)tile * nb + t] = (uint16_t)tot;
+        if (t < nb) V.tile_count[(size_t)tile * nb + t] = (uint16_t)tot;
         // every wave scans the tile's output totals in registers (lane = output,
         // nb <= 65: output 64 rides in lane 63's inclusive sum) and adds the
         // counts of the waves before it, then each lane fetches its output's
@@ -1143,8 +1160,8 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d,
         // measured 1 % slower, profiles/r01_kernel_experiments)
         if (live) {
             const size_t pos = (size_t)tile * kTile + mine + rank;
-            if (A.perm) A.perm[pos] = i;
-            if (A.tile_perm) A.tile_perm[pos] = (uint8_t)threadIdx.x;
+            if (V.perm) V.perm[pos] = i;
+            if (V.tile_perm) V.tile_perm[pos] = (uint8_t)threadIdx.x;
         }
     }
     if (FLOW) flow_resolve(A.fl, fq, live, i);
@@ -1165,20 +1182,67 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, uint32_t tile, uint2 d,
 // (Two tiles per workgroup with the second window prefetched into VGPRs
 // while the first is processed measured 10-15 % slower: one resident round
 // of workgroups instead of two loses the natural load/compute skew.)
+//
+// One launch may carry several batches (fcgpu_process_jobs on one stream,
+// RxLaunch::njobs > 1): the grid is the batches' tiles end to end and each
+// workgroup takes its batch's pointers from the launch arguments. A queue of
+// batches then pays one launch ramp and tail instead of one per batch; the
+// batches are independent (no flow table, no whole-batch partition, no
+// in-place rewrite: the host only fuses such jobs).
+constexpr uint32_t kMaxFuse = 24;
+struct RxJob {
+    const uint8_t *arena;
+    const uint2 *desc;
+    uint16_t *verdict;
+    uint32_t *hash;
+    fcgpu_anno *anno;
+    uint32_t *perm;
+    uint16_t *tile_count;
+    uint8_t *tile_perm;
+    uint32_t n, tile0;       // packets; first workgroup of the batch in the grid
+};
+struct RxLaunch {
+    RxArgs A;                // njobs == 1: the batch; else the shared configuration
+    uint32_t njobs;
+    uint32_t job_tiles;      // every job's tile count when they are all equal, else 0
+    RxJob job[kMaxFuse];
+};
+
 template <int CM, bool CK, int PART, bool PROG, bool L4, bool FLOW = false,
           bool FAST = (CM == FCGPU_CHECK_IP4 || CM == FCGPU_CHECK_AUTO)>
-__global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
+__global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4 * kWave * kWin];
     __shared__ uint32_t s_cnt[4][kMaxBins];
     extern __shared__ uint4 s_prog[];           // prog_lds_bytes(cfg) at launch: program steps or CRC tables
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t tile = blockIdx.x;
+    const RxArgs &A = L.A;
+    RxView V = rx_view(A);
+    uint32_t tile = blockIdx.x;
+    if (!FLOW && PART != kPartGlobal && L.njobs > 1) {   // workgroup-uniform
+        // equal batches: a division; ragged ones: a walk over the jobs' first
+        // tiles (kernel-argument loads the workgroup waits for)
+        uint32_t j = 0;
+        if (L.job_tiles) j = blockIdx.x / L.job_tiles;
+        else
+            for (uint32_t k = 1; k < L.njobs; ++k) j = blockIdx.x >= L.job[k].tile0 ? k : j;
+        const RxJob &J = L.job[j];
+        V.arena = J.arena;
+        V.desc = J.desc;
+        V.verdict = J.verdict;
+        V.hash = J.hash;
+        V.anno = J.anno;
+        V.perm = J.perm;
+        V.tile_count = J.tile_count;
+        V.tile_perm = J.tile_perm;
+        V.n = J.n;
+        tile = blockIdx.x - J.tile0;
+    }
     const uint32_t i = tile * kTile + threadIdx.x;
     uint2 d = make_uint2(0, 0);
-    if (i < A.n) d = A.desc[i];
+    if (i < V.n) d = V.desc[i];
     uint8_t *wl = s_win + wave * (kWave * kWin);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) glds16(win_src(A.arena, d.x, lane, k), wl + k * 1024);
+    for (int k = 0; k < 4; ++k) glds16(win_src(V.arena, d.x, lane, k), wl + k * 1024);
     // decision program: the block's LDS copy when it fits (block-uniform)
     const bool prog_lds = PROG && prog_in_lds(A.cfg);
     const bool crc_lds = !PROG && crc_in_lds(A.cfg);          // block-uniform
@@ -1186,7 +1250,7 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxArgs A) {
     if (crc_lds) s_prog[threadIdx.x] = A.cfg.crc_tab[threadIdx.x];   // kCrcTabQ == kTile
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (prog_lds || crc_lds) __syncthreads();
-    rx_tile<CM, CK, PART, PROG, L4, FAST, FLOW>(A, tile, d, wl, s_cnt, prog_lds || crc_lds ? s_prog : nullptr);
+    rx_tile<CM, CK, PART, PROG, L4, FAST, FLOW>(A, V, tile, d, wl, s_cnt, prog_lds || crc_lds ? s_prog : nullptr);
 }
 
 // Exclusive scan of one output's per-tile counts (in place) and its total.

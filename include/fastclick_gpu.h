@@ -254,7 +254,14 @@ int  fcgpu_process(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_des
  * different streams run concurrently (their outputs must not overlap); that
  * is rejected when the context has a flow table or a job asks for a
  * whole-batch partition (both use context scratch). Every job is checked
- * before the first is launched. */
+ * before the first is launched.
+ * Consecutive jobs of one stream whose outputs do not overlap share one
+ * receive-kernel launch (up to 24 batches: the grid is their tiles end to
+ * end), unless the context has a flow table or header rewrites or a job asks
+ * for a whole-batch partition; results are the same as one launch per job.
+ * Sampled timing (fcgpu_set_timing) then counts batches: a fused launch is
+ * timed when it covers a multiple of `every`, and fcgpu_read_timing reports
+ * its batches as launches (time per batch = ms / launches). */
 typedef struct fcgpu_job {
     const uint8_t  *arena;
     const uint32_t *desc;

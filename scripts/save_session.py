@@ -27,6 +27,8 @@ for d in sorted(glob.glob(os.path.join(src, "prof_*"))):
     if os.path.exists(tr):
         with open(os.path.join(out, "timeline.txt"), "w") as fh:
             subprocess.run([sys.executable, "scripts/trace_steps.py", tr, "20"], stdout=fh)
+        with open(os.path.join(out, "launches.txt"), "w") as fh:
+            subprocess.run([sys.executable, "scripts/launch_table.py", tr], stdout=fh)
     cc = os.path.join(d, "run_counter_collection.csv")
     if os.path.exists(cc):
         agg = collections.defaultdict(list)

@@ -30,11 +30,11 @@ for s in "${ST[@]}"; do
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 300 python bench.py $DRV ;;
-    bench_s1) step bench_s1 300 python bench.py $DRV --streams 1 --no-cpu ;;
+    bench_s1) step bench_s1 300 python bench.py $DRV --streams 1 --fuse 1 --no-cpu ;;
     bench_long) step bench_long 300 python bench.py --steps 200 --warmup 20 --no-cpu ;;
-    bench_long_s1) step bench_long_s1 300 python bench.py --steps 200 --warmup 20 --no-cpu --streams 1 ;;
+    bench_long_s1) step bench_long_s1 300 python bench.py --steps 200 --warmup 20 --no-cpu --streams 1 --fuse 1 ;;
     kt_drv) kt kt_drv 300 $DRV --no-cpu ;;
-    kt_drv_s1) kt kt_drv_s1 300 $DRV --no-cpu --streams 1 ;;
+    kt_drv_s1) kt kt_drv_s1 300 $DRV --no-cpu --streams 1 --fuse 1 ;;
     kt_long) kt kt_long 300 --steps 200 --warmup 20 --no-cpu ;;
     kt_w40) kt kt_w40 300 --gpus 1 --steps 20 --warmup 40 --no-cpu ;;
     kt_notime) kt kt_notime 300 $DRV --no-cpu --no-timing ;;
@@ -44,12 +44,16 @@ for s in "${ST[@]}"; do
     kt_w40_s1) kt kt_w40_s1 300 --gpus 1 --steps 20 --warmup 40 --no-cpu --streams 1 ;;
     bench2) step bench2 300 python bench.py $DRV --no-cpu ;;
     bench3) step bench3 300 python bench.py $DRV --no-cpu ;;
-    pmc) pmc pmc_fetch FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1
-         pmc pmc_write WRITE_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1
-         pmc pmc_ea TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1 ;;
-    pmc_var) pmc pmc_fetch_fb128 FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1 --frame-bytes 128
-             pmc pmc_fetch_fb1500 FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1 --frame-bytes 1500
-             pmc pmc_fetch_c3 FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1 --workload c3
+    # PMC per batch: one batch per launch (--fuse 1)
+    pmc) pmc pmc_fetch FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1 --fuse 1
+         pmc pmc_write WRITE_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1 --fuse 1
+         pmc pmc_ea TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1 --fuse 1 ;;
+    bench_s2) step bench_s2 300 python bench.py $DRV --streams 2 --fuse 1 --no-cpu ;;
+    bench_long_s2) step bench_long_s2 300 python bench.py --steps 200 --warmup 20 --no-cpu --streams 2 --fuse 1 ;;
+    kt_drv_s2) kt kt_drv_s2 300 $DRV --no-cpu --streams 2 --fuse 1 ;;
+    pmc_var) pmc pmc_fetch_fb128 FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1 --fuse 1 --frame-bytes 128
+             pmc pmc_fetch_fb1500 FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1 --fuse 1 --frame-bytes 1500
+             pmc pmc_fetch_c3 FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --streams 1 --fuse 1 --workload c3
              pmc pmc_fetch_c4flow FETCH_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --workload c4 --flow-capacity 2000000
              pmc pmc_ea_c4flow TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum -- --steps 40 --warmup 4 --no-cpu --no-timing --workload c4 --flow-capacity 2000000
              pmc pmc_write_c4flow WRITE_SIZE -- --steps 40 --warmup 4 --no-cpu --no-timing --workload c4 --flow-capacity 2000000 ;;

@@ -345,3 +345,68 @@ def test_process_jobs_two_streams(dev, oracle):
         assert np.array_equal(np.array(ctx.counters(), np.int64), before)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("partition", [N.PART_TILE, None])
+def test_process_jobs_fused(dev, oracle, partition):
+    """fcgpu_process_jobs fuses a stream's consecutive jobs with disjoint
+    outputs into one k_rx launch (up to 24 batches, the grid their tiles end
+    to end): 30 ragged batches (1 .. 30,001 packets, one empty) on one stream
+    -> two fused launches; every batch gets the oracle's results, the counters
+    sum over the batches. Two jobs sharing an output set are not fused: the
+    later one's results are what the set holds, as with one call per job."""
+    import torch
+    from fastclick_amd.device import DeviceBatch, DeviceOutputs
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16, badsrc=BADSRC)
+    sizes = [1, 255, 256, 257, 0, 30_001] + [1_000 + 997 * k for k in range(24)]
+    batches = []
+    for k, n in enumerate(sizes):
+        b = synth.c4(max(n, 1), seed=200 + k)
+        synth.inject_errors(b, 0.02, seed=300 + k)
+        if n == 0:
+            b = synth.Batch(arena=b.arena, desc=b.desc[:0].copy())
+        batches.append(b)
+    exps = [oracle.process_batch(cfg, b) for b in batches]
+    tile = partition == N.PART_TILE
+    ctx = N.Context(0, 40_000, cfg)
+    try:
+        dbs = [DeviceBatch.upload(b, device="cuda:0") for b in batches]
+        outs, specs = [], []
+        for b in dbs:
+            o = DeviceOutputs(max(b.n, 1), 16, device="cuda:0", perm=tile, anno=False,
+                              partition=N.PART_TILE if tile else N.PART_GLOBAL, port_start=False)
+            outs.append(o)
+            specs.append((b.arena.data_ptr(), b.desc.data_ptr(), b.n, None, o.ptrs()))
+        ctx.set_timing(1)
+        ctx.run_jobs(ctx.jobs(specs))
+        torch.cuda.synchronize()
+        ms, cnt = ctx.read_timing()
+        assert cnt[0] == sum(1 for n in sizes if n)          # timing counts batches
+        ctx.set_timing(0)
+        for k, (b, o) in enumerate(zip(batches, outs)):
+            if b.n == 0:
+                continue
+            got, exp = o.numpy(), exps[k]
+            assert np.array_equal(got["reason"][:b.n], exp["reason"]), k
+            assert np.array_equal(got["port"][:b.n], exp["port"]), k
+            ok = exp["reason"] == N.R_OK
+            assert np.array_equal(got["hash"][:b.n][ok], exp["hash"][ok]), k
+            if tile:
+                nt = (b.n + N.TILE - 1) // N.TILE
+                assert np.array_equal(got["tile_count"][:nt * 17], exp["tile_count"]), k
+                assert np.array_equal(got["perm_tile"][:b.n], exp["perm_tile"]), k
+        want = sum(e["counters"].astype(np.int64) for e, b in zip(exps, batches) if b.n)
+        assert np.array_equal(np.array(ctx.counters(), np.int64), want)
+        # two jobs on one output set: sequential semantics (the second wins)
+        shared = DeviceOutputs(40_000, 16, device="cuda:0", perm=tile, anno=False,
+                               partition=N.PART_TILE if tile else N.PART_GLOBAL, port_start=False)
+        pair = [(dbs[5].arena.data_ptr(), dbs[5].desc.data_ptr(), dbs[5].n, None, shared.ptrs()),
+                (dbs[29].arena.data_ptr(), dbs[29].desc.data_ptr(), dbs[29].n, None, shared.ptrs())]
+        ctx.run_jobs(ctx.jobs(pair))
+        torch.cuda.synchronize()
+        got = shared.numpy()
+        n29 = batches[29].n
+        assert np.array_equal(got["reason"][:n29], exps[29]["reason"])
+        assert np.array_equal(got["reason"][n29:batches[5].n], exps[5]["reason"][n29:])
+    finally:
+        ctx.close()
