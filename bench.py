@@ -70,12 +70,10 @@ def parse(argv=None):
                          "among fuse x streams; 1 = one launch per batch")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
     ap.add_argument("--timing-every", type=int, default=0,
-                    help="bracket every k-th timed launch with HIP events (hipExtLaunchKernelGGL "
-                         "start/stop on the launch stream; created before the timed region). Each "
-                         "event idles the queue ~4 us, so the default samples sparsely: every 8th "
-                         "timed launch from 64 steps; below 64 steps the timed region carries no "
-                         "events and the kernel time comes from a pass of 64 launches after it, "
-                         "every 8th bracketed")
+                    help="bracket the k_rx launch covering every k-th timed batch with HIP events "
+                         "(hipExtLaunchKernelGGL start/stop on the launch stream; created before the "
+                         "timed region). Each event idles the queue ~4 us, so the default samples "
+                         "sparsely: 8 (a fused launch of 20 batches is one bracketed launch)")
     ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams the consecutive steps alternate over (each with its own output "
                          "buffers), as batches of several rx queues would. Default 1: the steps are "
@@ -371,10 +369,6 @@ class DeviceProcessor:
                      for _ in range(nsets)]
         self.ctr = torch.zeros(N.CTR_SHARDS, N.NCOUNTERS, dtype=torch.int64, device=dev)
         self.timing_every = 0 if args.no_timing else (args.timing_every or 8)
-        # a short timed region stays free of events; its kernel time is
-        # sampled by a pass of the same launches after it
-        self.post_timing = bool(self.timing_every) and not args.timing_every and args.steps < 64
-        self.warm_steps = 0
 
     def _jobs(self, first, count):
         specs = []
@@ -397,7 +391,6 @@ class DeviceProcessor:
                 d.max()
             self.torch.cuda.synchronize()
         warm = self._jobs(0, steps)
-        self.warm_steps = steps
         self.timed = self._jobs(steps, self.args.steps)   # built before the warmup
         self.ctx.set_timing(self.timing_every)      # creates the event pool now
         self.ctx.run_jobs(warm)
@@ -405,9 +398,7 @@ class DeviceProcessor:
         self.ctx.read_timing()                      # drop warmup samples
         if self.args.flow_capacity and self.args.flow_manager == "imp" and self.args.flow_timeout:
             self._time_maintainer()
-        # sample count restarts at the timed region (no events in it when the
-        # timing pass follows it)
-        self.ctx.set_timing(0 if self.post_timing else self.timing_every)
+        self.ctx.set_timing(self.timing_every)      # sample count restarts at the timed region
         self.ctx.use_counters(self.ctr.data_ptr())  # timed steps count into the tensor
 
     def _time_maintainer(self):
@@ -440,16 +431,6 @@ class DeviceProcessor:
     def timing(self):
         if not self.timing_every:
             return None
-        if self.post_timing:
-            # after the timed region: the rotation continues for 64 launches,
-            # every 8th bracketed; counted into the context's own counters, not
-            # the timed region's
-            self.torch.cuda.synchronize()
-            self.ctx.use_counters(0)
-            post = self._jobs(self.warm_steps + self.args.steps, 64)
-            self.ctx.set_timing(self.timing_every)
-            self.ctx.run_jobs(post)
-            self.torch.cuda.synchronize()
         ms, cnt = self.ctx.read_timing()
         return dict(k_rx_ms=ms[0] / max(cnt[0], 1), k_scan_ms=ms[1] / max(cnt[1], 1),
                     k_part_ms=ms[2] / max(cnt[2], 1), launches=cnt)
@@ -550,13 +531,11 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, kernel="k_rx", basis=basis,
                     bytes_per_launch=PKT_BYTES_READ * per_gpu,
                     per="batch (a k_rx launch carries up to config.batches_per_launch batches: "
-                        "kernel_ms = a launch's event time / its batches)",
+                        "kernel_ms = the sampled launches' event time in the timed region / their batches)",
                     kernel_ms=round(timing["k_rx_ms"], 5),
                     kernel_frac=round(PKT_BYTES_READ * per_gpu / kernel_s / 1e9 / HBM_PEAK_GBS, 4),
                     scan_ms=round(timing["k_scan_ms"], 5), part_ms=round(timing["k_part_ms"], 5),
-                    sampled_launches=timing["launches"][0],
-                    sampled_in=("a pass of 64 launches after the timed region" if getattr(proc, "post_timing", False)
-                                else "the timed region"))
+                    sampled_batches=timing["launches"][0])
     cpu = None
     if world == 1 and not args.no_cpu and args.workload in ("c2", "c3", "c4") and not args.flow_capacity:
         cpu = cpu_baseline(args.cpu_seconds, flows=dict(c2=1, c3=10000).get(args.workload, 4096),
