@@ -68,7 +68,7 @@ for s in "${ST[@]}"; do
               done ;;
     sweep) for fb in 64 128 256 512 1024 1500; do
              step "sweep_$fb" 300 python bench.py --steps 200 --warmup 20 --no-cpu --frame-bytes $fb
-             step "sweep_s1_$fb" 300 python bench.py --steps 200 --warmup 20 --no-cpu --frame-bytes $fb --streams 1
+             step "sweep_s2_$fb" 300 python bench.py --steps 200 --warmup 20 --no-cpu --frame-bytes $fb --streams 2 --fuse 1
            done ;;
     variants) for v in "--workload c3" "--workload c4" "--workload c5" "--classify ipclass16" \
                        "--workload c4 --classify ipclass16" "--flow-capacity 1" "--workload c3 --flow-capacity 20000" \
