@@ -58,7 +58,10 @@ def parse(argv=None):
     ap.add_argument("--packets", type=int, default=1 << 20,
                     help="packets per step per GPU (weak) or per step in total (strong)")
     ap.add_argument("--shard", choices=["weak", "strong"], default="weak")
-    ap.add_argument("--nbuf", type=int, default=16)
+    ap.add_argument("--nbuf", type=int, default=0,
+                    help="distinct HBM copies of the batch the steps rotate over; 0 (default): enough "
+                         "for >= 1.15 GB of arenas, at least 4 and at most 16 (16 x 72 MB for 64-B "
+                         "frames; 4 x 420 MB for IMIX) -- beyond the 256 MB Infinity Cache either way")
     ap.add_argument("--nports", type=int, default=16)
     ap.add_argument("--no-perm", action="store_true", help="skip the partition")
     ap.add_argument("--partition", choices=["tile", "global"], default="tile",
@@ -332,6 +335,9 @@ class DeviceProcessor:
         desc = torch.from_numpy(np.ascontiguousarray(host.desc[lo:hi]).view(np.int32)).to(dev)
         del host
         # nbuf copies at distinct HBM addresses (device-side copies)
+        if not args.nbuf:
+            touched = int(arena.numel())
+            args.nbuf = max(4, min(16, -(-1_150_000_000 // max(touched, 1))))
         self.bufs = [(arena, desc)] + [(arena.clone(), desc.clone()) for _ in range(args.nbuf - 1)]
         program = None
         if args.classify == "ipclass16":

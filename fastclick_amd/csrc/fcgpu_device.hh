@@ -1221,10 +1221,14 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
     if (!FLOW && PART != kPartGlobal && L.njobs > 1) {   // workgroup-uniform
         // equal batches: a division; ragged ones: a walk over the jobs' first
         // tiles (kernel-argument loads the workgroup waits for)
-        uint32_t j = 0;
-        if (L.job_tiles) j = blockIdx.x / L.job_tiles;
-        else
+        uint32_t j = 0, t = 0;
+        if (L.job_tiles) {
+            j = blockIdx.x / L.job_tiles;
+            t = blockIdx.x - j * L.job_tiles;
+        } else {
             for (uint32_t k = 1; k < L.njobs; ++k) j = blockIdx.x >= L.job[k].tile0 ? k : j;
+            t = blockIdx.x - L.job[j].tile0;
+        }
         const RxJob &J = L.job[j];
         V.arena = J.arena;
         V.desc = J.desc;
@@ -1235,7 +1239,7 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
         V.tile_count = J.tile_count;
         V.tile_perm = J.tile_perm;
         V.n = J.n;
-        tile = blockIdx.x - J.tile0;
+        tile = t;
     }
     const uint32_t i = tile * kTile + threadIdx.x;
     uint2 d = make_uint2(0, 0);
