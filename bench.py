@@ -113,6 +113,9 @@ def parse(argv=None):
                          "(CRC32-C of the IPFlow5ID, DPDK builds); ipclass16: the survey's "
                          "IPClassifier with 15 UDP dst-port ranges + '-' (program printed by the "
                          "reference compiler, tests/golden/reftests.json)")
+    ap.add_argument("--program-jit", type=int, default=1,
+                    help="ipclass16: 1 = the program compiled to code (fcgpu_program_jit, hiprtc, before "
+                         "the warmup); 0 = the step interpreter")
     ap.add_argument("--prefault", type=int, default=1,
                     help="1: read every rotating batch once before the warmup (page translations "
                          "resident, GPU clocks up); 0: off")
@@ -356,6 +359,8 @@ class DeviceProcessor:
         self.ctx = N.Context(gpu, max(n, 1), cfg)
         if program is not None:
             self.ctx.set_program(*program)
+            if args.program_jit:
+                self.ctx.program_jit(True)
         self.maintain_ms = None
         if args.flow_capacity:
             if args.flow_manager == "imp":
@@ -374,7 +379,7 @@ class DeviceProcessor:
                                    partition=part, flowid=args.flow_capacity > 0)
                      for _ in range(nsets)]
         self.ctr = torch.zeros(N.CTR_SHARDS, N.NCOUNTERS, dtype=torch.int64, device=dev)
-        self.timing_every = 0 if args.no_timing else (args.timing_every or 8)
+        self.timing_every = 0 if args.no_timing else (args.timing_every or min(8, max(1, args.steps)))
 
     def _jobs(self, first, count):
         specs = []
@@ -514,7 +519,7 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
     ms_per_step = elapsed / args.steps * 1e3
     per_gpu = hi - lo
     roof = None
-    if timing:
+    if timing and timing["launches"][0] and timing["k_rx_ms"] > 0:
         kernel_s = timing["k_rx_ms"] * 1e-3
         step_s = ms_per_step * 1e-3
         nstreams = max(1, args.streams)
@@ -582,7 +587,8 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                             " + stable per-port partition of every 256-packet PacketBatch"
                             if args.partition == "tile" else
                             " + stable per-port partition of the whole batch")),
-            "classify": args.classify,
+            "classify": args.classify + (" (compiled program)" if args.classify == "ipclass16" and args.program_jit
+                                         else " (interpreted program)" if args.classify == "ipclass16" else ""),
             **({"errors_per_kind": args.errors,
                 "valid_fraction": round(valid / total_pkts, 4)} if args.errors else {}),
             "partition": "none" if args.no_perm else args.partition,

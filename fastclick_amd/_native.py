@@ -14,7 +14,7 @@ LIBFCGPU = os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 13
+ABI_VERSION = 14
 SPAN_SLOTS = 3
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
@@ -198,6 +198,8 @@ FCGPU_SYMBOLS = {
     "fcgpu_flow_reset": (C.c_int, [C.c_void_p]),
     "fcgpu_flow_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "fcgpu_flow_configure": (C.c_int, [C.c_void_p, C.POINTER(fcgpu_flow_config)]),
+    "fcgpu_program_jit": (C.c_int, [C.c_void_p, C.c_int]),
+    "fcgpu_program_jit_active": (C.c_int, [C.c_void_p]),
     "fcgpu_flow_set_time": (C.c_int, [C.c_void_p, C.c_uint32]),
     "fcgpu_flow_maintain": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "fcgpu_flow_stats": (C.c_int, [C.c_void_p, C.POINTER(fcgpu_flow_stat)]),
@@ -416,6 +418,13 @@ class Context:
             arr[i] = st if isinstance(st, fcgpu_step) else fcgpu_step(*[int(x) for x in st])
         self._chk(self.lib.fcgpu_set_program(self.h, kind, arr, len(steps), output_everything),
                   "fcgpu_set_program")
+
+    def program_jit(self, enable=True):
+        """Compile the installed (and later) decision programs to code (hiprtc)."""
+        self._chk(self.lib.fcgpu_program_jit(self.h, int(enable)), "fcgpu_program_jit")
+
+    def program_jit_active(self) -> bool:
+        return bool(self.lib.fcgpu_program_jit_active(self.h))
 
     def flow_enable(self, max_flows: int):
         """Device flow table (FlowIPManagerHMP semantics); 0 disables it."""

@@ -27,6 +27,8 @@
 #include "fcgpu_device.hh"
 #include "fcgpu_flow.hh"
 #include "capture.hh"
+#include "prog_jit.hh"
+#include "jit_sources.inc"   // kJitDeviceHh, kJitAbiH (fastclick_amd/build.py)
 
 #pragma clang diagnostic ignored "-Wunused-result"
 #pragma clang diagnostic ignored "-Wunused-value"
@@ -178,6 +180,12 @@ struct fcgpu_ctx {
     uint32_t prog_n = 0, prog_kind = 0, prog_q = 0, prog_tab = 0;
     int32_t prog_all = -1;
     std::vector<fcgpu_step> prog_host;   // the installed program (capture reach)
+    std::vector<uint4> prog_dev;         // ... in the device format (table steps, fallbacks, tables)
+    // fcgpu_program_jit: the program compiled to code (prog_jit.hh)
+    bool jit_on = false;
+    std::string jit_src;                 // generated program function ("" = interpreted)
+    std::vector<int> jit_keys;           // k_rx instantiations in the module
+    JitModule jit;
     uint16_t *d_verdict = nullptr;   // scratch verdicts when the caller wants perm only
     // host-resident staging
     uint8_t *h_arena = nullptr, *d_arena = nullptr;
@@ -292,8 +300,21 @@ static hipEvent_t take_event(fcgpu_ctx *c) {
 // itself (timestamps of the kernel, not of the stream around it).
 // L: one batch (njobs 1, grid = its tiles) or several fused ones (grid =
 // their tiles end to end).
+static hipFunction_t jit_function(fcgpu_ctx *c, int key);
+
 template <int CM, bool CK, int PART, bool PROG, bool L4, bool FLOW = false>
-static void launch_rx(const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+static void launch_rx(const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
+                      fcgpu_ctx *jc) {
+    if (PROG && jc) {   // the program compiled to code, when the context has it
+        if (hipFunction_t fn = jit_function(jc, jit_key(CM, CK, PART, L4, FLOW))) {
+            void *args[] = {const_cast<RxLaunch *>(&L)};
+            if (ev0)
+                hipExtModuleLaunchKernel(fn, grid * kTile, 1, 1, kTile, 1, 1, 0, s, args, nullptr, ev0, ev1, 0);
+            else
+                hipModuleLaunchKernel(fn, grid, 1, 1, kTile, 1, 1, 0, s, args, nullptr);
+            return;
+        }
+    }
     const size_t lds = prog_lds_bytes(L.A.cfg);   // program steps (PROG) or CRC tables (LB_CRC), else 0
     if (ev0)
         hipExtLaunchKernelGGL((k_rx<CM, CK, PART, PROG, L4, FLOW>), dim3(grid), dim3(kTile), lds, s, ev0, ev1,
@@ -305,26 +326,26 @@ static void launch_rx(const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_
 // IPv4 check modes: L4 (CheckUDPHeader/CheckTCPHeader) and the flow table
 // exist only there (fcgpu_configure / fcgpu_process reject them with CHECK_AUTO).
 template <int CM, bool CK, int PART, bool PROG>
-static void launch_rx_ip4(const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+static void launch_rx_ip4(const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1, fcgpu_ctx *jc) {
     const bool l4 = L.A.cfg.l4_mode != FCGPU_L4_NONE, flow = L.A.fl.slots != nullptr;
     if (flow) {
-        if (l4) launch_rx<CM, CK, PART, PROG, true, true>(L, grid, s, e0, e1);
-        else launch_rx<CM, CK, PART, PROG, false, true>(L, grid, s, e0, e1);
+        if (l4) launch_rx<CM, CK, PART, PROG, true, true>(L, grid, s, e0, e1, jc);
+        else launch_rx<CM, CK, PART, PROG, false, true>(L, grid, s, e0, e1, jc);
     } else {
-        if (l4) launch_rx<CM, CK, PART, PROG, true>(L, grid, s, e0, e1);
-        else launch_rx<CM, CK, PART, PROG, false>(L, grid, s, e0, e1);
+        if (l4) launch_rx<CM, CK, PART, PROG, true>(L, grid, s, e0, e1, jc);
+        else launch_rx<CM, CK, PART, PROG, false>(L, grid, s, e0, e1, jc);
     }
 }
 
 template <int PART, bool PROG>
-static void launch_rx_part(uint32_t cm, bool ck, const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+static void launch_rx_part(uint32_t cm, bool ck, const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1, fcgpu_ctx *jc) {
     switch (cm * 2 + (ck ? 1 : 0)) {
-    case 0: launch_rx_ip4<FCGPU_CHECK_IP4, false, PART, PROG>(L, grid, s, e0, e1); break;
-    case 1: launch_rx_ip4<FCGPU_CHECK_IP4, true, PART, PROG>(L, grid, s, e0, e1); break;
-    case 2: case 3: launch_rx_ip4<FCGPU_MARK_IP4, false, PART, PROG>(L, grid, s, e0, e1); break;
-    case 4: launch_rx<FCGPU_CHECK_AUTO, false, PART, PROG, false>(L, grid, s, e0, e1); break;
-    case 6: case 7: launch_rx<FCGPU_MARK_IP6, false, PART, PROG, false>(L, grid, s, e0, e1); break;
-    default: launch_rx<FCGPU_CHECK_AUTO, true, PART, PROG, false>(L, grid, s, e0, e1); break;
+    case 0: launch_rx_ip4<FCGPU_CHECK_IP4, false, PART, PROG>(L, grid, s, e0, e1, jc); break;
+    case 1: launch_rx_ip4<FCGPU_CHECK_IP4, true, PART, PROG>(L, grid, s, e0, e1, jc); break;
+    case 2: case 3: launch_rx_ip4<FCGPU_MARK_IP4, false, PART, PROG>(L, grid, s, e0, e1, jc); break;
+    case 4: launch_rx<FCGPU_CHECK_AUTO, false, PART, PROG, false>(L, grid, s, e0, e1, jc); break;
+    case 6: case 7: launch_rx<FCGPU_MARK_IP6, false, PART, PROG, false>(L, grid, s, e0, e1, jc); break;
+    default: launch_rx<FCGPU_CHECK_AUTO, true, PART, PROG, false>(L, grid, s, e0, e1, jc); break;
     }
 }
 
@@ -332,26 +353,26 @@ static void launch_rx_part(uint32_t cm, bool ck, const RxLaunch &L, uint32_t gri
 // launched for FCGPU_CLS_PROGRAM, so the other modes keep their lean code.
 template <bool PROG>
 static void launch_rx_prog(int part, uint32_t cm, bool ck, const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_t e0,
-                           hipEvent_t e1) {
-    if (part == kPartTile) launch_rx_part<kPartTile, PROG>(cm, ck, L, grid, s, e0, e1);
-    else if (part == kPartGlobal) launch_rx_part<kPartGlobal, PROG>(cm, ck, L, grid, s, e0, e1);
-    else launch_rx_part<kPartNone, PROG>(cm, ck, L, grid, s, e0, e1);
+                           hipEvent_t e1, fcgpu_ctx *jc) {
+    if (part == kPartTile) launch_rx_part<kPartTile, PROG>(cm, ck, L, grid, s, e0, e1, jc);
+    else if (part == kPartGlobal) launch_rx_part<kPartGlobal, PROG>(cm, ck, L, grid, s, e0, e1, jc);
+    else launch_rx_part<kPartNone, PROG>(cm, ck, L, grid, s, e0, e1, jc);
 }
 
 static void launch_rx_any(int part, uint32_t cm, bool ck, const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_t e0,
-                          hipEvent_t e1) {
-    if (L.A.cfg.classify == FCGPU_CLS_PROGRAM) launch_rx_prog<true>(part, cm, ck, L, grid, s, e0, e1);
-    else launch_rx_prog<false>(part, cm, ck, L, grid, s, e0, e1);
+                          hipEvent_t e1, fcgpu_ctx *jc) {
+    if (L.A.cfg.classify == FCGPU_CLS_PROGRAM) launch_rx_prog<true>(part, cm, ck, L, grid, s, e0, e1, jc);
+    else launch_rx_prog<false>(part, cm, ck, L, grid, s, e0, e1, jc);
 }
 
 // One batch: a.ntiles workgroups.
 static void launch_rx_one(int part, uint32_t cm, bool ck, const RxArgs &a, hipStream_t s, hipEvent_t e0,
-                          hipEvent_t e1) {
+                          hipEvent_t e1, fcgpu_ctx *jc) {
     RxLaunch L;
     L.A = a;
     L.njobs = 1;
     L.job_tiles = 0;
-    launch_rx_any(part, cm, ck, L, a.ntiles, s, e0, e1);
+    launch_rx_any(part, cm, ck, L, a.ntiles, s, e0, e1, jc);
 }
 
 // Whole batch in one shot (FCGPU_PART_GLOBAL: the partition spans the batch).
@@ -523,6 +544,58 @@ static uint32_t build_tables(std::vector<uint4> &dev, uint32_t nsteps, uint32_t 
         dev.push_back(q);
     }
     return nsteps + (uint32_t)copies.size();
+}
+
+// ---- compiled programs (fcgpu_program_jit, prog_jit.hh) ---------------------
+// The k_rx instantiations the context's configuration launches (as the
+// launch_rx_part dispatch normalises them), for every partition shape.
+static std::vector<int> jit_keys_for(const fcgpu_ctx *c) {
+    int cm = (int)c->cfg.check_mode;
+    bool ck = c->cfg.checksum != 0;
+    if (cm == FCGPU_MARK_IP4 || cm == FCGPU_MARK_IP6) ck = false;
+    const bool ip4 = cm == FCGPU_CHECK_IP4 || cm == FCGPU_MARK_IP4;
+    const bool l4 = ip4 && c->cfg.l4_mode != FCGPU_L4_NONE, flow = ip4 && c->fl.slots != nullptr;
+    std::vector<int> keys;
+    for (int part : {kPartTile, kPartNone, kPartGlobal}) keys.push_back(jit_key(cm, ck, part, l4, flow));
+    return keys;
+}
+
+// (Re)build the module for the installed program and `keys`.
+static int jit_build(fcgpu_ctx *c, const std::vector<int> &keys) {
+    std::string err;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!jit_compile(c->jit_src, keys, kJitDeviceHh, kJitAbiH, c->jit, err)) {
+        c->jit_src.clear();
+        c->jit_keys.clear();
+        return fail(c, FCGPU_ERUNTIME, "fcgpu_program_jit: " + err);
+    }
+    c->jit_keys = keys;
+    return FCGPU_OK;
+}
+
+// The installed program as code: generated and compiled for the current
+// configuration; a program with a cycle stays interpreted (error returned).
+static int jit_install(fcgpu_ctx *c) {
+    c->jit.unload();
+    c->jit_src.clear();
+    c->jit_keys.clear();
+    if (!c->jit_on || c->prog_all >= 0 || c->prog_dev.empty()) return FCGPU_OK;
+    std::string why;
+    c->jit_src = jit_program_source(c->prog_dev, c->prog_n, c->prog_tab, c->prog_kind, why);
+    if (c->jit_src.empty()) return fail(c, FCGPU_EINVAL, "fcgpu_program_jit: " + why);
+    return jit_build(c, jit_keys_for(c));
+}
+
+// The compiled kernel for an instantiation; one the module lacks (the
+// configuration changed since) is added by recompiling. nullptr: interpret.
+static hipFunction_t jit_function(fcgpu_ctx *c, int key) {
+    auto it = c->jit.fn.find(key);
+    if (it != c->jit.fn.end()) return it->second;
+    std::vector<int> keys = c->jit_keys;
+    keys.push_back(key);
+    if (jit_build(c, keys) != FCGPU_OK) return nullptr;
+    it = c->jit.fn.find(key);
+    return it == c->jit.fn.end() ? nullptr : it->second;
 }
 
 extern "C" {
@@ -774,6 +847,8 @@ void fcgpu_close(fcgpu_ctx *c) {
     if (c->device >= 0) {
         hipSetDevice(c->device);
         if (c->stream) hipStreamSynchronize(c->stream);
+        hipDeviceSynchronize();
+        c->jit.unload();
         for (auto &p : c->pending) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
         for (auto e : c->free_ev) hipEventDestroy(e);
         hipFree(c->d_tilecnt);
@@ -1005,7 +1080,7 @@ static int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_d
         HIPCHK(c, hipStreamWaitEvent(s, c->flow_order[0], 0));
     }
     launch_rx_one(part, c->cfg.check_mode, c->cfg.checksum != 0, a, s, timed ? ev[0].a : nullptr,
-                  timed ? ev[0].b : nullptr);
+                  timed ? ev[0].b : nullptr, c->jit_src.empty() ? nullptr : c);
     HIPCHK(c, hipGetLastError());
     if (a.fl.slots) {   // the batch's new flows get their IDs (fcgpu_flow.hh)
         const uint32_t nw = (n + 63) / 64;
@@ -1129,7 +1204,7 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
     EvPair ev;
     if (timed) { ev.a = take_event(c); ev.b = take_event(c); ev.stage = 0; ev.batches = g; }
     launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, L, tiles, s, timed ? ev.a : nullptr,
-                  timed ? ev.b : nullptr);
+                  timed ? ev.b : nullptr, c->jit_src.empty() ? nullptr : c);
     HIPCHK(c, hipGetLastError());
     if (timed) c->pending.push_back(ev);
     return FCGPU_OK;
@@ -1724,8 +1799,18 @@ int fcgpu_set_program(fcgpu_ctx *c, uint32_t kind, const fcgpu_step *steps, uint
     c->dcfg.prog_n = c->prog_n;
     c->dcfg.prog_kind = c->prog_kind;
     c->dcfg.prog_all = c->prog_all;
+    c->prog_dev = dev;
+    if (c->jit_on && jit_install(c) != FCGPU_OK) c->err.clear();   // a cycle: interpreted
     return FCGPU_OK;
 }
+
+int fcgpu_program_jit(fcgpu_ctx *c, int enable) {
+    if (!c) return FCGPU_EINVAL;
+    c->jit_on = enable != 0;
+    return jit_install(c);
+}
+
+int fcgpu_program_jit_active(fcgpu_ctx *c) { return c && !c->jit_src.empty() ? 1 : 0; }
 
 int fcgpu_use_counters(fcgpu_ctx *c, uint64_t *d) {
     if (!c) return FCGPU_EINVAL;

@@ -13,8 +13,10 @@
 // Integer/byte work only; no MFMA. The kernel is bound by HBM read bytes:
 // 8 B descriptor + 64 B window per packet.
 #pragma once
+#ifndef __HIPCC_RTC__   // hiprtc provides the HIP runtime declarations itself
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 #include "../../include/fastclick_gpu.h"
 
 namespace fcgpu {
@@ -305,7 +307,11 @@ __device__ __forceinline__ uint32_t run_program_on(const DevCfg &c, const FrameV
 // header windows and counts each) within a CU's 160 KB.
 constexpr uint32_t kProgLdsQ = 160;
 __host__ __device__ inline bool prog_in_lds(const DevCfg &c) {
+#ifdef FCGPU_JIT_PROGRAM
+    return false;                 // the program is code: no steps to cache
+#else
     return c.classify == FCGPU_CLS_PROGRAM && c.prog_all < 0 && c.prog_q <= kProgLdsQ;
+#endif
 }
 // dynamic LDS of a k_rx launch: only program mode pays for the step cache,
 // only LB_CRC for its 4-KB slicing tables
@@ -314,10 +320,19 @@ __host__ __device__ inline bool crc_in_lds(const DevCfg &c) { return c.classify 
 inline size_t prog_lds_bytes(const DevCfg &c) {
     return prog_in_lds(c) ? sizeof(uint4) * c.prog_q : crc_in_lds(c) ? sizeof(uint4) * kCrcTabQ : 0;
 }
+#ifdef FCGPU_JIT_PROGRAM
+// The installed program compiled to straight-line code (fcgpu_program_jit,
+// fcgpu_api.hip jit_source): defined by the generated source after this header.
+__device__ __forceinline__ uint32_t jit_program(const FrameView &f, const fcgpu_anno &an);
+#endif
 __device__ __forceinline__ uint32_t run_program(const DevCfg &c, const FrameView &f, const fcgpu_anno &an,
                                                 const uint4 *sprog) {
+#ifdef FCGPU_JIT_PROGRAM
+    return jit_program(f, an);
+#else
     if (sprog) return run_program_on(c, f, an, sprog);
     return run_program_on(c, f, an, c.prog);
+#endif
 }
 
 struct PktResult {

@@ -39,7 +39,8 @@
 //   BADADDRS, PROCESS_EH                     -- CheckIP6Header (IPv6, MODE AUTO)
 //   N / LB_MODE hash|hash_agg|hash_ip|hash_crc -- FlowSwitch / LoadBalancer
 //   HASHSWITCH "OFFSET LENGTH"               -- HashSwitch
-//   PROGRAM "<program text>", PROGRAM_KIND IPFILTER|CLASSIFIER
+//   PROGRAM "<program text>", PROGRAM_KIND IPFILTER|CLASSIFIER, PROGRAM_JIT (default
+//     true: the program compiled to code at initialize, fcgpu_program_jit)
 //                                            -- IPFilter / IPClassifier / Classifier:
 //     the compiled program as the reference's `program` handler prints it
 //     (lines separated by newlines or '|', program_text.hh); N is the
@@ -179,6 +180,8 @@ class RxCore {
                 std::string e = parse_program(text, _prog);
                 if (!e.empty()) return err(errh, "PROGRAM: " + e);
                 _cfg.classify = FCGPU_CLS_PROGRAM;
+            } else if (k == "PROGRAM_JIT") {
+                if (!parse_bool(v, _prog_jit)) return err(errh, "PROGRAM_JIT expects true/false");
             } else if (k == "PROGRAM_KIND") {
                 if (v == "IPFILTER") _prog_kind = FCGPU_PROG_IPFILTER;
                 else if (v == "CLASSIFIER") _prog_kind = FCGPU_PROG_CLASSIFIER;
@@ -290,6 +293,9 @@ class RxCore {
         if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_configure: ") + fcgpu_last_error(_ctx));
         uint32_t reach = 0;
         if (_cfg.classify == FCGPU_CLS_PROGRAM) {
+            // the program as code (fcgpu_program_jit) unless PROGRAM_JIT false;
+            // one with a cycle stays interpreted
+            if (_prog_jit) fcgpu_program_jit(_ctx, 1);
             rc = fcgpu_set_program(_ctx, _prog_kind, _prog.steps.data(), (uint32_t)_prog.steps.size(),
                                    _prog.output_everything);
             if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_set_program: ") + fcgpu_last_error(_ctx));
@@ -731,6 +737,7 @@ class RxCore {
     fcgpu_ctx *_ctx = nullptr;
     ParsedProgram _prog;
     uint32_t _prog_kind = FCGPU_PROG_IPFILTER;
+    bool _prog_jit = true;
     int _color = -1;
     uint32_t _flow_cap = 0;
     uint32_t _flow_mgr = FCGPU_FLOW_MGR_HMP, _flow_timeout = 0, _flow_recycle_ms = 1000;

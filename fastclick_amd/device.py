@@ -96,19 +96,20 @@ def run_device(ctx: N.Context, dbatch: DeviceBatch, outs: DeviceOutputs, stream=
 
 
 def process_batch(batch, cfg, *, anno=True, perm=True, device_index=0, partition=N.PART_GLOBAL,
-                  program=None):
+                  program=None, program_jit=False):
     """One batch on a fresh context (see process_batches)."""
     return process_batches([batch], cfg, anno=anno, perm=perm, device_index=device_index,
-                           partition=partition, program=program)[0]
+                           partition=partition, program=program, program_jit=program_jit)[0]
 
 
 def process_batches(batches, cfg, *, anno=True, perm=True, device_index=0, partition=N.PART_GLOBAL,
-                    program=None, max_flows=0):
+                    program=None, max_flows=0, program_jit=False):
     """Upload host Batches, run the device path over them in order on one
     context, return per-batch numpy results and the running counter vector.
     Convenience for tests and smoke(). program: optional (kind, steps,
-    output_everything) for CLS_PROGRAM (fcgpu_set_program); max_flows > 0
-    enables the flow table (its state carries across the batches)."""
+    output_everything) for CLS_PROGRAM (fcgpu_set_program), compiled to code
+    with program_jit (fcgpu_program_jit); max_flows > 0 enables the flow table
+    (its state carries across the batches)."""
     torch = _torch()
     res = []
     with torch.cuda.device(device_index):
@@ -116,6 +117,8 @@ def process_batches(batches, cfg, *, anno=True, perm=True, device_index=0, parti
         try:
             if program is not None:
                 ctx.set_program(*program)
+                if program_jit:
+                    ctx.program_jit(True)
             if max_flows:
                 ctx.flow_enable(max_flows)
             for batch in batches:

@@ -42,14 +42,16 @@
 #ifndef FASTCLICK_GPU_H
 #define FASTCLICK_GPU_H
 
+#ifndef __HIPCC_RTC__   /* hiprtc (fcgpu_set_program's compiled programs) has its own */
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 13
+#define FCGPU_ABI_VERSION 14
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -364,6 +366,18 @@ typedef struct fcgpu_step {
  * program is empty and every packet goes to that output ("all->[N]"). */
 int  fcgpu_set_program(fcgpu_ctx *ctx, uint32_t kind, const fcgpu_step *steps, uint32_t nsteps,
                        int32_t output_everything);
+/* Programs compiled to code (enable != 0): the installed program, and every
+ * program installed later, is also emitted as straight-line HIP (one block
+ * per step with its offset, mask and value as immediates; a jump table as
+ * compares over its runs) and compiled with hiprtc into the receive kernels
+ * the context launches (~1-5 s per program and configuration, at this call /
+ * fcgpu_set_program, or at the first launch of another configuration).
+ * Results are identical to the interpreter's. A program with a cycle stays
+ * interpreted (FCGPU_EINVAL here; fcgpu_set_program keeps it interpreted
+ * silently). enable 0: back to the interpreter. */
+int  fcgpu_program_jit(fcgpu_ctx *ctx, int enable);
+/* 1 when the installed program runs as compiled code. */
+int  fcgpu_program_jit_active(fcgpu_ctx *ctx);
 
 /* Flow table: the IPFlow5ID flow classification of
  * FlowIPManagerHMP (elements/research/flowipmanagerhmp.cc:96-126; the

@@ -212,15 +212,17 @@ def test_gpu_program_required(dev):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("jit", ["true", "false"])
 @pytest.mark.parametrize("name", ["ipc", "cls"])
-def test_element_program_golden(name):
-    """IPClassifier/Classifier through the element: packets leave on the rule's
-    output in input order, unmatched packets are killed, invalid ones leave on N."""
+def test_element_program_golden(name, jit):
+    """IPClassifier/Classifier through the element (program compiled to code,
+    or interpreted): packets leave on the rule's output in input order,
+    unmatched packets are killed, invalid ones leave on N."""
     from fastclick_amd import click
     g = load("prog")
     text, _, nout = _program(g, name)
     kind = "IPFILTER" if name == "ipc" else "CLASSIFIER"
-    conf = (f"GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N {nout}, PROGRAM_KIND {kind}, "
+    conf = (f"GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N {nout}, PROGRAM_KIND {kind}, PROGRAM_JIT {jit}, "
             f"PROGRAM \"{text.replace(chr(10), '|')}\")")
     res = click.run_element(conf, batch_of(g), nsinks=nout + 1)
     exp = g[f"{name}_out"].astype(np.int64)
@@ -357,3 +359,101 @@ def test_gpu_chain_programs_tables_vs_oracle(dev, oracle):
         assert np.array_equal(got["counters"], exp["counters"])
         outcomes |= set(np.unique(exp["port"]).tolist())
     assert len(outcomes) > 5
+
+
+# ---------------------------------------------------- programs compiled to code
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ipc", "cls"])
+def test_gpu_program_jit_golden(dev, name):
+    """fcgpu_program_jit: the reference-compiled programs as straight-line code
+    (hiprtc) give the reference's outputs, for both partition shapes."""
+    g = load("prog")
+    _, prog, nout = _program(g, name)
+    for part in (N.PART_GLOBAL, N.PART_TILE):
+        r = dev.process_batch(batch_of(g), _cfg(nout), partition=part, program=prog, program_jit=True)
+        got = _outputs(r)
+        exp = g[f"{name}_out"]
+        bad = np.nonzero(got != exp)[0]
+        assert len(bad) == 0, f"jit {name} part={part}: {len(bad)} differ, first {bad[:8]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["c4", "mix"])
+def test_gpu_random_programs_jit_vs_oracle(dev, oracle, mode):
+    """Random programs (table steps, short words, [X], outputs past N) as
+    code: the same outputs and counters as the oracle, program by program."""
+    import torch
+    from fastclick_amd.device import DeviceBatch, DeviceOutputs, run_device
+    rng = np.random.default_rng(700 + len(mode))
+    if mode == "mix":
+        b = synth.c5(20_000, seed=15)
+        base = dict(check_mode=N.CHECK_AUTO, checksum=True)
+    else:
+        b = synth.c4(20_000, seed=14)
+        synth.add_ip_options(b, 0.1, seed=16)
+        synth.inject_errors(b, 0.02, seed=17)
+        base = dict(offset=14, checksum=True)
+    for trial, kind in enumerate([N.PROG_IPFILTER, N.PROG_CLASSIFIER, N.PROG_IPFILTER]):
+        nout = int(rng.integers(2, 40))
+        prog = (kind, random_program(rng, b, kind, nout, int(rng.integers(20, 200))), -1)
+        cfg = N.make_cfg(classify=N.CLS_PROGRAM, nports=nout, **base)
+        exp = oracle.process_batch(cfg, b, program=prog)
+        ctx = N.Context(0, b.n, cfg)
+        try:
+            ctx.set_program(*prog)
+            ctx.program_jit(True)
+            assert ctx.program_jit_active()
+            db = DeviceBatch.upload(b, device="cuda:0")
+            for part in (N.PART_GLOBAL, N.PART_TILE):
+                outs = DeviceOutputs(b.n, nout, device="cuda:0", anno=True, perm=True, port_start=True,
+                                     partition=part)
+                run_device(ctx, db, outs)
+                torch.cuda.synchronize()
+                got = outs.numpy()
+                compare(got, exp, ctx=f"jit {mode} trial={trial} part={part}")
+        finally:
+            ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_program_jit_cycle_and_reconfigure(dev, oracle):
+    """A program with a backward jump stays interpreted (fcgpu_program_jit
+    refuses it, the interpreter's bounded walk still answers as the oracle);
+    an acyclic program installed afterwards is compiled; a later flow table
+    adds its kernels on first launch; switching JIT off goes back to the
+    interpreter -- all with the oracle's outputs."""
+    import torch
+    from fastclick_amd.device import DeviceBatch, DeviceOutputs, run_device
+    b = synth.c4(8_000, seed=21)
+    # step 1 -> 2 -> 1 for odd source ports: the walk gives up (unmatched)
+    cyc = [(256 + 9, 17, 0xff, 1, -1, 0), (512, 0, 0x1, -1, 2, 0), (256 + 12, 0, 0, 1, 1, 0)]
+    steps = [(256 + 9, 17, 0xff, 1, -1, 0), (512 + 2, 0, 0x100, -0, -2, 0)]
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_PROGRAM, nports=3)
+    ctx = N.Context(0, b.n, cfg)
+    try:
+        db = DeviceBatch.upload(b, device="cuda:0")
+
+        def run_check(prog, flow=False):
+            exp = oracle.process_batch(cfg, b, program=prog)
+            outs = DeviceOutputs(b.n, 3, device="cuda:0", perm=True, partition=N.PART_TILE, flowid=flow)
+            run_device(ctx, db, outs)
+            torch.cuda.synchronize()
+            got = outs.numpy()
+            assert np.array_equal(got["reason"], exp["reason"]) and np.array_equal(got["port"], exp["port"])
+
+        ctx.set_program(N.PROG_IPFILTER, cyc, -1)
+        with pytest.raises(RuntimeError, match="cycle"):
+            ctx.program_jit(True)
+        assert not ctx.program_jit_active()
+        run_check((N.PROG_IPFILTER, cyc, -1))
+        ctx.set_program(N.PROG_IPFILTER, steps, -1)
+        assert ctx.program_jit_active()
+        run_check((N.PROG_IPFILTER, steps, -1))
+        ctx.flow_enable(1 << 16)
+        run_check((N.PROG_IPFILTER, steps, -1), flow=True)
+        ctx.program_jit(False)
+        assert not ctx.program_jit_active()
+        run_check((N.PROG_IPFILTER, steps, -1), flow=True)
+    finally:
+        ctx.close()
