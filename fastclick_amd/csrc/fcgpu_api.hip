@@ -1087,6 +1087,7 @@ static int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_d
         // the last finish's class of misses (no sync: maybe older) predicts this one's
         if (*(volatile uint32_t *)c->flow_hint == kHintBig) {
             const uint32_t g = std::max(1u, std::min((n + kFlowGridBlock - 1) / kFlowGridBlock, 2048u));
+            hipLaunchKernelGGL(k_flow_claim, dim3(g), dim3(kFlowGridBlock), 0, s, a.fl, nw);
             hipLaunchKernelGGL(k_flow_mark, dim3(g), dim3(kFlowGridBlock), 0, s, a.fl, nw);
             hipLaunchKernelGGL(k_flow_scan, dim3(1), dim3(kFinishBlock), 0, s, a.fl, nw);
             hipLaunchKernelGGL(k_flow_assign, dim3(g), dim3(kFlowGridBlock), 0, s, a.fl, nw);

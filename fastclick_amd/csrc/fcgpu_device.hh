@@ -924,30 +924,6 @@ __device__ __forceinline__ FlowProbe flow_issue(const FlowArgs &F, const FrameVi
     }
     return q;
 }
-// A miss claims its key's slot right away (see fcgpu_flow.hh): its key is
-// published in the miss list before the CAS (flow_resolve), and a lane that
-// finds another miss's claim reads that key with agent-scope loads.
-__device__ __forceinline__ uint32_t flow_claim(const FlowArgs &F, uint4 k, uint32_t pos, uint32_t e) {
-    if (__hip_atomic_load(&F.state[kFsNext], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= F.max_flows)
-        return kSlotNone;                        // no IDs left: FCGPU_FLOW_FULL
-    for (uint32_t p = 0; p <= F.mask; ++p) {
-        const uint4 sl = F.slots[pos];
-        if (sl.w == 0) {
-            const uint32_t old = atomicCAS(&F.claim[pos], 0u, e + 1);
-            if (old == 0) return pos;
-            const uint32_t *ok = reinterpret_cast<const uint32_t *>(&F.miss_key[old - 1]);
-            uint4 o;
-            o.x = __hip_atomic_load(ok + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            o.y = __hip_atomic_load(ok + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            o.z = __hip_atomic_load(ok + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            o.w = __hip_atomic_load(ok + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (o.x == k.x && o.y == k.y && o.z == k.z && o.w == k.w) return pos;
-        }
-        pos = (pos + 1) & F.mask;
-    }
-    return kSlotNone;
-}
-
 __device__ __forceinline__ void flow_resolve(const FlowArgs &F, FlowProbe &q, bool live, uint32_t i) {
     uint32_t id = FCGPU_FLOW_NONE;
     if (q.want) {
@@ -963,33 +939,21 @@ __device__ __forceinline__ void flow_resolve(const FlowArgs &F, FlowProbe &q, bo
         // are stamped by their first packet in the new-flow pass
         if (F.lastseen && id < kTagFull) F.lastseen[id] = F.now;
     }
-    // No miss list and no counter: a miss keeps its packet index (its record
-    // lives at index i), the wave writes its 64-bit miss word, and a wave with
+    // The lookup only reads the table: a miss keeps its record (key, and the
+    // empty slot its probe stopped at) at its packet index for the new-flow
+    // pass, which looks it up again and places it in batch order
+    // (fcgpu_flow.hh). The wave writes its 64-bit miss word, and a wave with
     // misses stamps the batch's epoch -- plain stores: only the next launch
-    // reads them, and the XCD's L2 absorbs the repeated stamp. (An atomic on
-    // one miss counter per wave with misses, or a coherent store of the stamp
-    // that the wave then waits for, serialised at ~30 ns each at the memory:
-    // 10k misses cost 300 us.)
+    // reads them. (An atomic on one miss counter per wave with misses
+    // serialised at ~30 ns each at the memory: 10k misses cost 300 us.)
     const uint64_t mm = __ballot(id == kFlowMiss), lv = __ballot(live);
     if ((threadIdx.x & 63) == 0 && lv) {
         F.missmask[i >> 6] = mm;
         if (mm) F.state[kFsMissed] = F.epoch;
     }
     if (id == kFlowMiss) {
-        // publish the key to lanes that will find this miss's claim: agent-
-        // scope stores, acknowledged at the coherence point (vmcnt) before
-        // the CAS issues. (__threadfence would also write back and
-        // invalidate this XCD's whole L2 -- buffer_wbl2/inv sc1 -- once per
-        // wave with a miss.)
-        uint32_t *kp = reinterpret_cast<uint32_t *>(&F.miss_key[i]);
-        __hip_atomic_store(kp + 0, q.key.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(kp + 1, q.key.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(kp + 2, q.key.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(kp + 3, q.key.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t slot = flow_claim(F, q.key, q.pos, i);   // q.pos: first empty slot
-        F.miss_slot[i] = slot;
-        if (slot != kSlotNone) atomicMin(&F.first[slot], i);
+        F.miss_key[i] = q.key;
+        F.miss_slot[i] = q.pos;
     }
     if (live && F.flowid) F.flowid[i] = id;
 }

@@ -6,31 +6,39 @@
 // appearance. On the device that is split in two:
 //
 //   k_rx (flow_issue / flow_resolve, fcgpu_device.hh): every checked packet
-//     looks its IPFlow5ID up in the table. A miss -- a flow the table has not
-//     seen -- keeps its record (key, slot) at its packet index and claims a
-//     slot for its key: the first miss of a key to reach an empty slot claims
-//     it (CAS on `claim`), later misses of the same key find the claim and
-//     compare keys, so all misses of one key end on one slot; atomicMin leaves
-//     the flow's first packet index in `first`. Each wave writes its 64-bit
-//     miss word; a wave with a miss stamps the batch's epoch.
-//   the finish (this file, after k_rx on the same stream): the first packet of
+//     looks its IPFlow5ID up in the table -- reads only. A miss keeps its
+//     record (key, the empty slot its probe stopped at) at its packet index;
+//     each wave writes its 64-bit miss word; a wave with a miss stamps the
+//     batch's epoch.
+//   the new-flow pass (this file, after k_rx, in batch order): every miss
+//     looks its key up again from where its probe stopped -- a flow an earlier
+//     batch (or an earlier chunk of this one) added since is a hit now -- and
+//     otherwise claims a slot: the first miss of a key to reach an empty slot
+//     claims it (CAS on `claim`), later misses of the same key find the claim
+//     and compare keys, so all misses of one key end on one slot; atomicMin
+//     leaves the flow's first packet index in `first`. The first packet of
 //     each new flow gets rank = the number of first appearances before it;
-//     ID = next + rank. The first packet commits the slot (key + tag) and
-//     frees the claim; every miss gets its flow's ID; the counter advances.
+//     ID = next + rank. The first packet commits the slot (key + tag) and frees
+//     the claim; every miss gets its flow's ID; the counter advances.
+//   Because k_rx never writes the table, a batch's lookups need not wait for
+//   the previous batch's new-flow pass: a flow that pass adds is a miss the
+//   batch's own pass resolves.
 //
-// Two shapes of finish, chosen by the host from a hint the previous finish
+// Two shapes of pass, chosen by the host from a hint the previous pass
 // published in mapped host memory (the size class of its batch's misses):
 //
 //   k_flow_finish (one block): batch without misses (epoch not stamped) ->
 //     returns at its first load; otherwise the misses in packet order, 1024
 //     at a time (one chunk when the hint is right): compacted from the miss
-//     words into LDS, one per thread; a block scan ranks the first packets
-//     and every miss finds its flow's first packet by binary search.
-//   k_flow_mark / k_flow_scan / k_flow_assign (grid-wide, for batches with
-//     many misses): each wave marks the first packets among its 64 packets
-//     as a 64-bit word; an exclusive popcount prefix over those words (one
-//     block, coalesced loads transposed through LDS) ranks them; every miss
-//     takes its ID. Nothing needs clearing: every word is rewritten each batch.
+//     words into LDS, one per thread, placed, the first packets ranked by a
+//     block scan, every other miss finding its flow's first packet by binary
+//     search.
+//   k_flow_claim / k_flow_mark / k_flow_scan / k_flow_assign (grid-wide, for
+//     batches with many misses): every miss placed; each wave marks the first
+//     packets among its 64 packets as a 64-bit word; an exclusive popcount
+//     prefix over those words (one block, coalesced loads transposed through
+//     LDS) ranks them; every miss takes its ID. Nothing needs clearing: every
+//     word is rewritten each batch.
 #pragma once
 #include "fcgpu_device.hh"
 
@@ -97,6 +105,48 @@ __device__ __forceinline__ uint32_t flow_next_after(const FlowArgs &F, uint32_t 
     return next + (total < room ? total : room);
 }
 
+// Miss i of the batch placed in the table: its key looked up again from the
+// slot its k_rx probe stopped at (slots only fill between maintainer runs, so
+// the key cannot lie before it) -- found: kSlotHit, its ID stored; else the
+// empty slot it claims or shares with an earlier miss of the same key (the
+// claimant's key, written by k_rx, is compared), its first packet index
+// atomicMin'd into `first`. kSlotNone: no IDs left (FCGPU_FLOW_FULL).
+constexpr uint32_t kSlotHit = 0xfffffffeu;
+__device__ __forceinline__ uint32_t flow_place(const FlowArgs &F, uint32_t i) {
+    const uint4 k = F.miss_key[i];
+    uint32_t pos = F.miss_slot[i];
+    const bool full = __hip_atomic_load(&F.state[kFsNext], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= F.max_flows;
+    for (uint32_t p = 0; p <= F.mask; ++p) {
+        // agent scope: an earlier chunk of this pass may have committed it
+        const uint32_t *sp = reinterpret_cast<const uint32_t *>(&F.slots[pos]);
+        const uint32_t tag = __hip_atomic_load(sp + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tag != 0) {
+            if ((tag & 0xffu) == k.w && __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k.x &&
+                __hip_atomic_load(sp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k.y &&
+                __hip_atomic_load(sp + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k.z) {
+                const uint32_t id = flow_tag_id(tag);
+                if (F.lastseen && id < kTagFull) F.lastseen[id] = F.now;
+                if (F.flowid) F.flowid[i] = id;
+                return kSlotHit;
+            }
+        } else {
+            if (full) return kSlotNone;
+            const uint32_t old = atomicCAS(&F.claim[pos], 0u, i + 1);
+            if (old == 0) {
+                atomicMin(&F.first[pos], i);
+                return pos;
+            }
+            const uint4 o = F.miss_key[old - 1];
+            if (o.x == k.x && o.y == k.y && o.z == k.z && o.w == k.w) {
+                atomicMin(&F.first[pos], i);
+                return pos;
+            }
+        }
+        pos = (pos + 1) & F.mask;
+    }
+    return kSlotNone;
+}
+
 // The wave's 64 packets from i0 (a multiple of 64): the first packet of each
 // new flow sets its bit in the wave's first-packet word (written even when 0).
 __device__ __forceinline__ void flow_mark_wave(const FlowArgs &F, uint32_t i0) {
@@ -106,7 +156,7 @@ __device__ __forceinline__ void flow_mark_wave(const FlowArgs &F, uint32_t i0) {
     if ((mw >> lane) & 1u) {
         const uint32_t slot = F.miss_slot[i];
         uint32_t fp = kSlotNone;
-        if (slot != kSlotNone) {
+        if (slot != kSlotNone && slot != kSlotHit) {
             fp = F.first[slot];
             isfirst = fp == i;
         }
@@ -119,7 +169,7 @@ __device__ __forceinline__ void flow_mark_wave(const FlowArgs &F, uint32_t i0) {
 __device__ __forceinline__ void flow_assign_wave(const FlowArgs &F, uint32_t i0, uint32_t base, uint2 wb) {
     const uint32_t lane = threadIdx.x & 63, i = i0 + lane;
     const uint64_t mw = F.missmask[i0 >> 6];
-    if ((mw >> lane) & 1u) {
+    if ((mw >> lane) & 1u && F.miss_slot[i] != kSlotHit) {
         const uint32_t slot = F.miss_slot[i], fp = F.miss_first[i];
         uint32_t rank = 0;
         if (slot != kSlotNone) {
@@ -283,44 +333,38 @@ __global__ __launch_bounds__(kFinishBlock) void k_flow_finish(FlowArgs F, uint32
             }
         }
         __syncthreads();
-        // kQ consecutive entries per thread; loads from clamped indices and
-        // results selected, so all of them are in flight at once
+        // kQ consecutive entries per thread, each placed (found again, or a
+        // slot claimed / shared); then every claim and first[] update is in
         const uint32_t e0 = t * kQ;
         uint32_t pkt[kQ], slot[kQ], fp[kQ];
 #pragma unroll
         for (uint32_t q = 0; q < kQ; ++q) {
             pkt[q] = e0 + q < cn ? s_idx[e0 + q] : 0u;
-            const uint32_t sl = F.miss_slot[pkt[q]];
-            slot[q] = e0 + q < cn ? sl : kSlotNone;
+            slot[q] = e0 + q < cn ? flow_place(F, pkt[q]) : kSlotNone;
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         uint32_t nfirst = 0;
 #pragma unroll
         for (uint32_t q = 0; q < kQ; ++q) {
-            // agent-scope: a slot committed by an earlier chunk has first[] reset
-            const uint32_t f = __hip_atomic_load(&F.first[slot[q] != kSlotNone ? slot[q] : 0u], __ATOMIC_RELAXED,
+            const bool placed = slot[q] != kSlotNone && slot[q] != kSlotHit;
+            // agent scope: other waves' atomicMin
+            const uint32_t f = __hip_atomic_load(&F.first[placed ? slot[q] : 0u], __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
-            fp[q] = slot[q] != kSlotNone ? f : kSlotNone;
-            nfirst += slot[q] != kSlotNone && fp[q] == pkt[q];
+            fp[q] = placed ? f : kSlotNone;
+            nfirst += placed && fp[q] == pkt[q];
         }
         uint32_t nf;
         uint32_t r = nfirst_before + block_excl_scan<kFinishBlock>(nfirst, s_w, nf);
 #pragma unroll
         for (uint32_t q = 0; q < kQ; ++q) {
             if (e0 + q < cn) s_f[e0 + q] = r;
-            r += slot[q] != kSlotNone && fp[q] == pkt[q];
+            r += slot[q] != kSlotNone && slot[q] != kSlotHit && fp[q] == pkt[q];
         }
         __syncthreads();
 #pragma unroll
         for (uint32_t q = 0; q < kQ; ++q) {
-            if (e0 + q >= cn) continue;
-            if (slot[q] != kSlotNone && fp[q] == 0xffffffffu) {
-                // the flow's first packet was in an earlier chunk: its slot
-                // holds the ID already
-                const uint32_t tag = __hip_atomic_load(reinterpret_cast<const uint32_t *>(&F.slots[slot[q]]) + 3,
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (F.flowid) F.flowid[pkt[q]] = flow_tag_id(tag);
-                continue;
-            }
+            if (e0 + q >= cn || slot[q] == kSlotHit) continue;   // a hit has its ID
             uint32_t rank = 0;
             if (slot[q] != kSlotNone) {
                 uint32_t lo = 0, hi = cn;         // the entry of fp in this chunk
@@ -347,6 +391,16 @@ __global__ __launch_bounds__(kFinishBlock) void k_flow_finish(FlowArgs F, uint32
 
 // ---- grid-wide finish (the hint says many misses) ---------------------------
 constexpr int kFlowGridBlock = 256;
+
+// Every miss placed (flow_place); hits take their ID here.
+__global__ __launch_bounds__(kFlowGridBlock) void k_flow_claim(FlowArgs F, uint32_t nw) {
+    if (F.state[kFsMissed] != F.epoch) return;
+    for (uint32_t i0 = blockIdx.x * kFlowGridBlock + (threadIdx.x & ~63u); i0 < nw * 64;
+         i0 += gridDim.x * kFlowGridBlock) {
+        const uint32_t lane = threadIdx.x & 63, i = i0 + lane;
+        if ((F.missmask[i0 >> 6] >> lane) & 1u) F.miss_slot[i] = flow_place(F, i);
+    }
+}
 
 __global__ __launch_bounds__(kFlowGridBlock) void k_flow_mark(FlowArgs F, uint32_t nw) {
     if (F.state[kFsMissed] != F.epoch) return;
