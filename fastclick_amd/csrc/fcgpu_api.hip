@@ -210,6 +210,10 @@ struct fcgpu_ctx {
     uint32_t *flow_hint = nullptr;    // mapped: size class of the last finish's misses (kHint*)
     uint32_t flow_epoch = 0;          // batches through the table (FlowArgs::epoch)
     fcgpu_flow_config flow_conf{};    // the manager (fcgpu_flow_configure)
+    // fused launches with a flow table: miss records of up to kMaxFuseFlow batches
+    uint4 *fuse_key = nullptr;
+    uint32_t *fuse_slot = nullptr, *fuse_missed = nullptr;
+    uint64_t *fuse_mask = nullptr;
     uint4 *flow_spare = nullptr;      // IMP with timeouts: the slot array a maintainer run rebuilds into
     MaintArgs maint{};                // IMP with timeouts: released list, run numbers, timeout parameters
     uint32_t flow_now = 0;            // fcgpu_flow_set_time
@@ -633,11 +637,15 @@ static void flow_free(fcgpu_ctx *c) {
                     (void *)F.miss_first, (void *)F.missmask, (void *)F.firstmask, (void *)F.wordpre,
                     (void *)F.state, (void *)F.stack, (void *)F.lastseen, (void *)F.wheel, (void *)F.wheel_len,
                     (void *)c->flow_spare, (void *)c->maint.qbsr, (void *)c->maint.dead, (void *)c->maint.rbuf,
-                    (void *)c->maint.counts})
+                    (void *)c->maint.counts, (void *)c->fuse_key, (void *)c->fuse_slot, (void *)c->fuse_missed,
+                    (void *)c->fuse_mask})
         if (p) hipFree(p);
     if (c->flow_hint) hipHostFree(c->flow_hint);
     c->flow_hint = nullptr;
     c->flow_spare = nullptr;
+    c->fuse_key = nullptr;
+    c->fuse_slot = c->fuse_missed = nullptr;
+    c->fuse_mask = nullptr;
     F = FlowArgs{};
     c->maint = MaintArgs{};
     c->flow_conf = fcgpu_flow_config{};
@@ -727,6 +735,7 @@ int fcgpu_flow_configure(fcgpu_ctx *c, const fcgpu_flow_config *fc) {
     HIPCHK(c, hipMalloc(&F.firstmask, sizeof(uint64_t) * words));
     HIPCHK(c, hipMalloc(&F.wordpre, sizeof(uint32_t) * words));
     HIPCHK(c, hipMalloc(&F.state, sizeof(uint32_t) * 16));
+    F.missed = F.state + kFsMissed;
     if (imp) HIPCHK(c, hipMalloc(&F.stack, sizeof(uint32_t) * max_flows));
     if (te) {
         F.wstride = cap;
@@ -1024,6 +1033,22 @@ static int check_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d
     return FCGPU_OK;
 }
 
+// The new-flow pass of one batch of n packets (fcgpu_flow.hh), its shape
+// predicted by the last pass's class of misses (no sync: maybe older).
+static hipError_t flow_pass(fcgpu_ctx *c, const FlowArgs &F, uint32_t n, hipStream_t s) {
+    const uint32_t nw = (n + 63) / 64;
+    if (*(volatile uint32_t *)c->flow_hint == kHintBig) {
+        const uint32_t g = std::max(1u, std::min((n + kFlowGridBlock - 1) / kFlowGridBlock, 2048u));
+        hipLaunchKernelGGL(k_flow_claim, dim3(g), dim3(kFlowGridBlock), 0, s, F, nw);
+        hipLaunchKernelGGL(k_flow_mark, dim3(g), dim3(kFlowGridBlock), 0, s, F, nw);
+        hipLaunchKernelGGL(k_flow_scan, dim3(1), dim3(kFinishBlock), 0, s, F, nw);
+        hipLaunchKernelGGL(k_flow_assign, dim3(g), dim3(kFlowGridBlock), 0, s, F, nw);
+    } else {
+        hipLaunchKernelGGL(k_flow_finish, dim3(1), dim3(kFinishBlock), 0, s, F, nw);
+    }
+    return hipGetLastError();
+}
+
 // One batch's launches on stream s (arguments checked, device current).
 static int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, uint32_t n,
                        const fcgpu_out *o, hipStream_t s) {
@@ -1083,18 +1108,7 @@ static int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_d
                   timed ? ev[0].b : nullptr, c->jit_src.empty() ? nullptr : c);
     HIPCHK(c, hipGetLastError());
     if (a.fl.slots) {   // the batch's new flows get their IDs (fcgpu_flow.hh)
-        const uint32_t nw = (n + 63) / 64;
-        // the last finish's class of misses (no sync: maybe older) predicts this one's
-        if (*(volatile uint32_t *)c->flow_hint == kHintBig) {
-            const uint32_t g = std::max(1u, std::min((n + kFlowGridBlock - 1) / kFlowGridBlock, 2048u));
-            hipLaunchKernelGGL(k_flow_claim, dim3(g), dim3(kFlowGridBlock), 0, s, a.fl, nw);
-            hipLaunchKernelGGL(k_flow_mark, dim3(g), dim3(kFlowGridBlock), 0, s, a.fl, nw);
-            hipLaunchKernelGGL(k_flow_scan, dim3(1), dim3(kFinishBlock), 0, s, a.fl, nw);
-            hipLaunchKernelGGL(k_flow_assign, dim3(g), dim3(kFlowGridBlock), 0, s, a.fl, nw);
-        } else {
-            hipLaunchKernelGGL(k_flow_finish, dim3(1), dim3(kFinishBlock), 0, s, a.fl, nw);
-        }
-        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, flow_pass(c, a.fl, n, s));
         if (cross) {
             HIPCHK(c, hipEventRecord(c->flow_order[1], s));
             HIPCHK(c, hipStreamWaitEvent(c->stream, c->flow_order[1], 0));
@@ -1138,11 +1152,14 @@ static int out_part(const fcgpu_out *o) {
     return tile && (o->perm || o->tile_perm) ? kPartTile : (want_global ? kPartGlobal : kPartNone);
 }
 
-// A job that may share a k_rx launch with others: no flow table (batch order
-// through the new-flow pass), no whole-batch partition (context scratch), no
-// in-place header rewrite (jobs may share an arena).
+// A job that may share a k_rx launch with others: no whole-batch partition
+// (context scratch), no in-place header rewrite (jobs may share an arena).
+// With a flow table the lookups of the launch's batches only read the table
+// and each batch keeps its miss records apart (up to kMaxFuseFlow batches);
+// their new-flow passes then run in batch order after the launch.
+constexpr uint32_t kMaxFuseFlow = 8;
 static bool fusable(const fcgpu_ctx *c, const fcgpu_job &j) {
-    return j.n && !c->fl.slots && !c->cfg.rewrite && out_part(&j.out) != kPartGlobal;
+    return j.n && !c->cfg.rewrite && out_part(&j.out) != kPartGlobal;
 }
 
 static bool outputs_overlap(const fcgpu_out &x, const fcgpu_out &y) {
@@ -1167,11 +1184,38 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
     a.cfg = c->dcfg;
     a.fl = c->fl;
     L.njobs = g;
+    L.flow_stride = L.flow_words = 0;
+    const bool flow = c->fl.slots != nullptr;
+    uint32_t epoch0 = 0;
+    if (flow) {
+        // each batch's miss records apart; one epoch per batch, none 0
+        const size_t words = c->flow_words;
+        if (!c->fuse_key) {
+            HIPCHK(c, hipMalloc(&c->fuse_key, sizeof(uint4) * (size_t)kMaxFuseFlow * c->max_batch));
+            HIPCHK(c, hipMalloc(&c->fuse_slot, sizeof(uint32_t) * (size_t)kMaxFuseFlow * c->max_batch));
+            HIPCHK(c, hipMalloc(&c->fuse_mask, sizeof(uint64_t) * kMaxFuseFlow * words));
+            HIPCHK(c, hipMalloc(&c->fuse_missed, sizeof(uint32_t) * kMaxFuseFlow));
+            HIPCHK(c, memset_sync(c->fuse_mask, 0, sizeof(uint64_t) * kMaxFuseFlow * words));
+            HIPCHK(c, memset_sync(c->fuse_missed, 0, sizeof(uint32_t) * kMaxFuseFlow));
+        }
+        if (c->flow_epoch > 0xffffffffu - 2 * kMaxFuse) c->flow_epoch = 0;
+        epoch0 = c->flow_epoch + 1;
+        c->flow_epoch += g;
+        a.fl.miss_key = c->fuse_key;
+        a.fl.miss_slot = c->fuse_slot;
+        a.fl.missmask = c->fuse_mask;
+        a.fl.missed = c->fuse_missed;
+        a.fl.epoch = epoch0;
+        a.fl.now = c->flow_now;
+        L.flow_stride = c->max_batch;
+        L.flow_words = (uint32_t)words;
+    }
     uint32_t tiles = 0;
     for (uint32_t k = 0; k < g; ++k) {
         const fcgpu_job &j = *grp[k];
         const bool tile = j.out.partition == FCGPU_PART_TILE;
         RxJob &J = L.job[k];
+        J.flowid = j.out.flowid;
         J.arena = j.arena;
         J.desc = reinterpret_cast<const uint2 *>(j.desc);
         J.verdict = j.out.verdict;
@@ -1204,10 +1248,48 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
     }
     EvPair ev;
     if (timed) { ev.a = take_event(c); ev.b = take_event(c); ev.stage = 0; ev.batches = g; }
+    // the flow table's scratch is shared with the context's span stream (see process_one)
+    const bool cross = flow && c->stream && s != c->stream;
+    if (cross) {
+        HIPCHK(c, hipEventRecord(c->flow_order[0], c->stream));
+        HIPCHK(c, hipStreamWaitEvent(s, c->flow_order[0], 0));
+    }
     launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, L, tiles, s, timed ? ev.a : nullptr,
                   timed ? ev.b : nullptr, c->jit_src.empty() ? nullptr : c);
     HIPCHK(c, hipGetLastError());
     if (timed) c->pending.push_back(ev);
+    if (flow && *(volatile uint32_t *)c->flow_hint != kHintBig) {
+        // the batches' new-flow passes, in batch order, in one block
+        static_assert(kMaxFuseFlow <= kMaxFusePass, "k_flow_finish_multi");
+        FinishMulti M{};
+        M.g = g;
+        M.stride = L.flow_stride;
+        M.words = L.flow_words;
+        for (uint32_t k = 0; k < g; ++k) {
+            M.n[k] = grp[k]->n;
+            M.flowid[k] = grp[k]->out.flowid;
+        }
+        hipLaunchKernelGGL(k_flow_finish_multi, dim3(1), dim3(kFinishBlock), 0, s, a.fl, M);
+        HIPCHK(c, hipGetLastError());
+    } else if (flow) {
+        // many new flows: each batch's grid-wide pass, in batch order
+        for (uint32_t k = 0; k < g; ++k) {
+            FlowArgs F = a.fl;
+            F.miss_key += (size_t)k * L.flow_stride;
+            F.miss_slot += (size_t)k * L.flow_stride;
+            F.missmask += (size_t)k * L.flow_words;
+            F.missed += k;
+            F.epoch = epoch0 + k;
+            F.flowid = grp[k]->out.flowid;
+            HIPCHK(c, flow_pass(c, F, grp[k]->n, s));
+        }
+    }
+    if (flow) {
+        if (cross) {
+            HIPCHK(c, hipEventRecord(c->flow_order[1], s));
+            HIPCHK(c, hipStreamWaitEvent(c->stream, c->flow_order[1], 0));
+        }
+    }
     return FCGPU_OK;
 }
 
@@ -1245,7 +1327,8 @@ int fcgpu_process_jobs(fcgpu_ctx *c, const fcgpu_job *jobs, uint32_t njobs, void
         }
         const hipStream_t s = eff(j);
         grp.assign(1, &j);
-        for (uint32_t m = k + 1; m < njobs && grp.size() < kMaxFuse; ++m) {
+        const size_t gmax = c->fl.slots ? kMaxFuseFlow : kMaxFuse;
+        for (uint32_t m = k + 1; m < njobs && grp.size() < gmax; ++m) {
             if (done[m] || eff(jobs[m]) != s) continue;
             const fcgpu_job &x = jobs[m];
             if (!fusable(c, x)) break;                  // the stream's order barrier

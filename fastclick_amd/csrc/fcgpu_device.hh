@@ -87,6 +87,7 @@ struct FlowArgs {
     uint32_t *state;         // kFs* words below
     uint32_t *host_hint;     // mapped host word: size class of the last batch's misses (kHint*)
     uint32_t *flowid;        // [n] output (may be null)
+    uint32_t *missed;        // the word a wave with misses stamps with the epoch (state + kFsMissed)
     uint32_t epoch;          // this batch's number (never 0)
     // IMP managers (fcgpu_flow.hh, "IMP"): null stack = HMP (IDs 0, 1, 2, ...)
     uint32_t *stack;         // free IDs; [0, max_flows - state[kFsNext]) hold them, top last
@@ -100,7 +101,7 @@ struct FlowArgs {
 };
 constexpr uint32_t kFsNext = 0;   // HMP: next flow ID; IMP: IDs out of the stack (max_flows - stack size)
 constexpr uint32_t kFsBase = 1;   // the ID base of the batch being finished (grid-wide finish)
-constexpr uint32_t kFsMissed = 2; // epoch of the last batch with a miss
+constexpr uint32_t kFsMissed = 2; // epoch of the last batch with a miss (FlowArgs::missed, one batch per launch)
 constexpr uint32_t kFsHint = 3;   // the hint last published
 constexpr uint32_t kFsIndex = 4;  // IMP: timer-wheel index (maintainer runs so far)
 constexpr uint32_t kFsWBase = 5;  // IMP: the new-flow bucket's length when the batch began (grid-wide finish)
@@ -949,7 +950,7 @@ __device__ __forceinline__ void flow_resolve(const FlowArgs &F, FlowProbe &q, bo
     const uint64_t mm = __ballot(id == kFlowMiss), lv = __ballot(live);
     if ((threadIdx.x & 63) == 0 && lv) {
         F.missmask[i >> 6] = mm;
-        if (mm) F.state[kFsMissed] = F.epoch;
+        if (mm) *F.missed = F.epoch;
     }
     if (id == kFlowMiss) {
         F.miss_key[i] = q.key;
@@ -1040,7 +1041,8 @@ __device__ __forceinline__ RxView rx_view(const RxArgs &A) {
 // optionally the tile's stable per-output partition (CLASSIFY_EACH_PACKET on a
 // 256-packet PacketBatch).
 template <int CM, bool CK, int PART, bool PROG, bool L4, bool FAST, bool FLOW>
-__device__ __forceinline__ void rx_tile(const RxArgs &A, const RxView &V, uint32_t tile, uint2 d, const uint8_t *wl,
+__device__ __forceinline__ void rx_tile(const RxArgs &A, const RxView &V, const FlowArgs &FL, uint32_t tile, uint2 d,
+                                        const uint8_t *wl,
                                         uint32_t (*s_cnt)[kMaxBins], const uint4 *sprog) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t i = tile * kTile + threadIdx.x;
@@ -1077,7 +1079,7 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, const RxView &V, uint32
     }
     if (L4) l4_stage(A.cfg, f, V.arena + d.x, live, r);
     FlowProbe fq;
-    if (FLOW) fq = flow_issue(A.fl, f, live, r);
+    if (FLOW) fq = flow_issue(FL, f, live, r);
     if (A.cfg.rewrite)   // launch-uniform
         rw_stage(A.cfg, f, const_cast<uint8_t *>(V.arena) + d.x, live, r, A.ip_rw, i);
     if (live) {
@@ -1143,7 +1145,7 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, const RxView &V, uint32
             if (V.tile_perm) V.tile_perm[pos] = (uint8_t)threadIdx.x;
         }
     }
-    if (FLOW) flow_resolve(A.fl, fq, live, i);
+    if (FLOW) flow_resolve(FL, fq, live, i);
     // counters: one atomic per non-zero bin per tile, sharded by tile. "count"
     // and "drops" are not kept here: both follow from these bins on read
     // (fcgpu_counters_derive), which saves an atomic per tile (-0.4 us / 1M).
@@ -1178,12 +1180,16 @@ struct RxJob {
     uint32_t *perm;
     uint16_t *tile_count;
     uint8_t *tile_perm;
+    uint32_t *flowid;
     uint32_t n, tile0;       // packets; first workgroup of the batch in the grid
 };
 struct RxLaunch {
     RxArgs A;                // njobs == 1: the batch; else the shared configuration
     uint32_t njobs;
     uint32_t job_tiles;      // every job's tile count when they are all equal, else 0
+    // flow table, several batches: batch j's miss records at j x flow_stride
+    // packets (j x flow_words mask words, missed + j) past A.fl's
+    uint32_t flow_stride, flow_words;
     RxJob job[kMaxFuse];
 };
 
@@ -1196,8 +1202,9 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const RxArgs &A = L.A;
     RxView V = rx_view(A);
+    FlowArgs FL = A.fl;
     uint32_t tile = blockIdx.x;
-    if (!FLOW && PART != kPartGlobal && L.njobs > 1) {   // workgroup-uniform
+    if (PART != kPartGlobal && L.njobs > 1) {   // workgroup-uniform
         // equal batches: a division; ragged ones: a walk over the jobs' first
         // tiles (kernel-argument loads the workgroup waits for)
         uint32_t j = 0, t = 0;
@@ -1219,6 +1226,14 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
         V.tile_perm = J.tile_perm;
         V.n = J.n;
         tile = t;
+        if (FLOW) {
+            FL.miss_key += (size_t)j * L.flow_stride;
+            FL.miss_slot += (size_t)j * L.flow_stride;
+            FL.missmask += (size_t)j * L.flow_words;
+            FL.missed += j;
+            FL.flowid = J.flowid;
+            FL.epoch += j;
+        }
     }
     const uint32_t i = tile * kTile + threadIdx.x;
     uint2 d = make_uint2(0, 0);
@@ -1233,7 +1248,7 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
     if (crc_lds) s_prog[threadIdx.x] = A.cfg.crc_tab[threadIdx.x];   // kCrcTabQ == kTile
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (prog_lds || crc_lds) __syncthreads();
-    rx_tile<CM, CK, PART, PROG, L4, FAST, FLOW>(A, V, tile, d, wl, s_cnt, prog_lds || crc_lds ? s_prog : nullptr);
+    rx_tile<CM, CK, PART, PROG, L4, FAST, FLOW>(A, V, FL, tile, d, wl, s_cnt, prog_lds || crc_lds ? s_prog : nullptr);
 }
 
 // Exclusive scan of one output's per-tile counts (in place) and its total.

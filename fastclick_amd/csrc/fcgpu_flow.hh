@@ -270,18 +270,37 @@ __device__ uint2 mask_prefix(const FlowArgs &F, uint32_t nw, uint32_t *s_w, uint
 // the chunk by binary search -- or, when it lay in an earlier chunk, takes
 // the ID from the slot that chunk committed. Cost grows with the misses, not the
 // batch: one chunk for <= 1024 misses.
-__global__ __launch_bounds__(kFinishBlock) void k_flow_finish(FlowArgs F, uint32_t nw) {
+struct FinishLds {
+    uint32_t idx[kSmallFinish], f[kSmallFinish], pre[kLdsPadded];
+    uint32_t w[kFinishBlock / 64];
+    uint32_t bc[3];
+};
+
+// One batch's single-block pass (k_flow_finish, k_flow_finish_multi).
+__device__ __forceinline__ void flow_finish_body(const FlowArgs &F, uint32_t nw, FinishLds &L) {
     constexpr uint32_t kQ = kSmallFinish / kFinishBlock;     // misses per thread per chunk
     constexpr uint32_t kIt = (kLdsWords + kFinishBlock - 1) / kFinishBlock;
-    __shared__ uint32_t s_idx[kSmallFinish], s_f[kSmallFinish], s_pre[kLdsPadded];
-    __shared__ uint32_t s_w[kFinishBlock / 64];
+    uint32_t *s_idx = L.idx, *s_f = L.f, *s_pre = L.pre, *s_w = L.w;
     const uint32_t t = threadIdx.x;
-    if (F.state[kFsMissed] != F.epoch) {      // no misses in this batch
+    if (*F.missed != F.epoch) {      // no misses in this batch
         if (t == 0) publish_hint(F, 0);
         return;
     }
-    const uint32_t next = F.state[kFsNext];
-    const uint2 wb = flow_new_bucket(F);
+    // the table state as the previous pass left it (agent scope: in
+    // k_flow_finish_multi that pass ran in this block, its stores by thread 0)
+    if (t == 0) {
+        L.bc[0] = __hip_atomic_load(&F.state[kFsNext], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint2 b = make_uint2(0, 0);
+        if (F.lastseen) {
+            b.x = (__hip_atomic_load(&F.state[kFsIndex], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + F.te) & F.wmask;
+            b.y = __hip_atomic_load(&F.wheel_len[b.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        L.bc[1] = b.x;
+        L.bc[2] = b.y;
+    }
+    __syncthreads();
+    const uint32_t next = L.bc[0];
+    const uint2 wb = make_uint2(L.bc[1], L.bc[2]);
     // miss words: word w = t + k * kFinishBlock stays in registers; its
     // popcount goes to LDS, becomes the word's first miss index (exclusive
     // prefix in word order, via thread-contiguous chunks of LDS)
@@ -387,6 +406,37 @@ __global__ __launch_bounds__(kFinishBlock) void k_flow_finish(FlowArgs F, uint32
         if (F.lastseen) F.wheel_len[wb.x] = wb.y + (nx - next);
         publish_hint(F, m);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kFinishBlock) void k_flow_finish(FlowArgs F, uint32_t nw) {
+    __shared__ FinishLds L;
+    flow_finish_body(F, nw, L);
+}
+
+// The passes of the batches one fused k_rx launch looked up, in batch order,
+// in one block (batch j's miss records at j x stride packets / words past F's,
+// its epoch F.epoch + j): a queue of batches without new flows costs one
+// launch, not one per batch.
+constexpr uint32_t kMaxFusePass = 8;
+struct FinishMulti {
+    uint32_t g, stride, words;
+    uint32_t n[kMaxFusePass];
+    uint32_t *flowid[kMaxFusePass];
+};
+__global__ __launch_bounds__(kFinishBlock) void k_flow_finish_multi(FlowArgs F, FinishMulti M) {
+    __shared__ FinishLds L;
+    for (uint32_t j = 0; j < M.g; ++j) {
+        FlowArgs Fj = F;
+        Fj.miss_key += (size_t)j * M.stride;
+        Fj.miss_slot += (size_t)j * M.stride;
+        Fj.missmask += (size_t)j * M.words;
+        Fj.missed += j;
+        Fj.epoch += j;
+        Fj.flowid = M.flowid[j];
+        flow_finish_body(Fj, (M.n[j] + 63) / 64, L);
+    }
 }
 
 // ---- grid-wide finish (the hint says many misses) ---------------------------
@@ -394,7 +444,7 @@ constexpr int kFlowGridBlock = 256;
 
 // Every miss placed (flow_place); hits take their ID here.
 __global__ __launch_bounds__(kFlowGridBlock) void k_flow_claim(FlowArgs F, uint32_t nw) {
-    if (F.state[kFsMissed] != F.epoch) return;
+    if (*F.missed != F.epoch) return;
     for (uint32_t i0 = blockIdx.x * kFlowGridBlock + (threadIdx.x & ~63u); i0 < nw * 64;
          i0 += gridDim.x * kFlowGridBlock) {
         const uint32_t lane = threadIdx.x & 63, i = i0 + lane;
@@ -403,7 +453,7 @@ __global__ __launch_bounds__(kFlowGridBlock) void k_flow_claim(FlowArgs F, uint3
 }
 
 __global__ __launch_bounds__(kFlowGridBlock) void k_flow_mark(FlowArgs F, uint32_t nw) {
-    if (F.state[kFsMissed] != F.epoch) return;
+    if (*F.missed != F.epoch) return;
     for (uint32_t i0 = blockIdx.x * kFlowGridBlock + (threadIdx.x & ~63u); i0 < nw * 64;
          i0 += gridDim.x * kFlowGridBlock)
         flow_mark_wave(F, i0);
@@ -411,7 +461,7 @@ __global__ __launch_bounds__(kFlowGridBlock) void k_flow_mark(FlowArgs F, uint32
 
 __global__ __launch_bounds__(kFinishBlock) void k_flow_scan(FlowArgs F, uint32_t nw) {
     __shared__ uint32_t s_w[kFinishBlock / 64], s_pre[kLdsPadded];
-    if (F.state[kFsMissed] != F.epoch) {
+    if (*F.missed != F.epoch) {
         if (threadIdx.x == 0) publish_hint(F, 0);
         return;
     }
@@ -430,7 +480,7 @@ __global__ __launch_bounds__(kFinishBlock) void k_flow_scan(FlowArgs F, uint32_t
 }
 
 __global__ __launch_bounds__(kFlowGridBlock) void k_flow_assign(FlowArgs F, uint32_t nw) {
-    if (F.state[kFsMissed] != F.epoch) return;
+    if (*F.missed != F.epoch) return;
     const uint32_t base = F.state[kFsBase];
     const uint2 wb = F.lastseen ? make_uint2((F.state[kFsIndex] + F.te) & F.wmask, F.state[kFsWBase]) : make_uint2(0, 0);
     for (uint32_t i0 = blockIdx.x * kFlowGridBlock + (threadIdx.x & ~63u); i0 < nw * 64;

@@ -241,3 +241,47 @@ def test_gpu_nonfirst_fragments_flow(oracle):
     got = device.process_batches(batches, cfg, max_flows=1 << 16, anno=False, perm=False)
     assert np.array_equal(np.concatenate([g["flowid"] for g in got]), exp)
     assert got[-1]["flow_count"] == cnt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("manager", ["hmp", "imp"])
+def test_gpu_flow_fused_jobs(oracle, manager):
+    """fcgpu_process_jobs with a flow table fuses up to 8 batches per k_rx
+    launch (lookups only read the table; each batch keeps its miss records)
+    and runs the batches' new-flow passes after it in batch order: a stream
+    cut into 13 batches -- flows recurring across batches, new ones in every
+    batch, a table that fills -- gets the IDs of one batch at a time."""
+    import torch
+    from fastclick_amd.device import DeviceBatch, DeviceOutputs
+    b = _mixed(130_000, 6_000, 81)
+    bs = split(b, [10_000] * 13)
+    cfg = flow_cfg()
+    cap = 4_000
+    if manager == "hmp":
+        exp, ecnt = oracle_flows(oracle, cfg, bs, cap)
+    else:
+        t = oracle.ImpFlowTable(cap, 0, 1000)
+        exp = np.concatenate([t.batch(x, oracle.process_batch(cfg, x), 5) for x in bs])
+        ecnt = t.stats()["count"]
+    ctx = N.Context(0, 10_000, cfg)
+    try:
+        if manager == "hmp":
+            ctx.flow_enable(cap)
+        else:
+            ctx.flow_configure(N.FLOW_MGR_IMP, cap)
+            ctx.flow_set_time(5)
+        s = torch.cuda.current_stream()
+        dbs = [DeviceBatch.upload(x, device="cuda:0") for x in bs]
+        outs = [DeviceOutputs(x.n, cfg.nports, device="cuda:0", perm=True, partition=N.PART_TILE, flowid=True)
+                for x in bs]
+        specs = [(d.arena.data_ptr(), d.desc.data_ptr(), d.n, s.cuda_stream, o.ptrs()) for d, o in zip(dbs, outs)]
+        ctx.run_jobs(ctx.jobs(specs))
+        torch.cuda.synchronize()
+        got = np.concatenate([o.numpy()["flowid"] for o in outs])
+        if not np.array_equal(got, exp):
+            bad = np.nonzero(got != exp)[0]
+            raise AssertionError(f"{manager}: {len(bad)} IDs differ, first {bad[:6]}: {got[bad[:6]]} vs {exp[bad[:6]]}")
+        assert (got == FULL).any()
+        assert ctx.flow_count() == ecnt
+    finally:
+        ctx.close()
