@@ -694,6 +694,7 @@ int fcgpu_flow_configure(fcgpu_ctx *c, const fcgpu_flow_config *fc) {
         return fail(c, FCGPU_EINVAL, "flow manager: FCGPU_FLOW_MGR_HMP or FCGPU_FLOW_MGR_IMP");
     const bool imp = fc->manager == FCGPU_FLOW_MGR_IMP;
     if (!imp && fc->timeout_s) return fail(c, FCGPU_EINVAL, "flow timeouts need FCGPU_FLOW_MGR_IMP");
+    if (fc->capacity > FCGPU_MAX_FLOWS) return fail(c, FCGPU_EINVAL, "flow capacity above FCGPU_MAX_FLOWS");
     // IMP: CAPACITY rounded up to a power of two (virtualflowmanager.hh:85), IDs 1 .. cap-1
     const uint32_t cap = imp && fc->capacity ? pow2_at_least(std::max(fc->capacity, 2u)) : fc->capacity;
     const uint32_t max_flows = imp && cap ? cap - 1u : cap;
@@ -704,10 +705,10 @@ int fcgpu_flow_configure(fcgpu_ctx *c, const fcgpu_flow_config *fc) {
             return fail(c, FCGPU_EINVAL, "flow recycle interval must be 1 .. 65535 ms");
         // parse (:58-79): epochs per second, timeout in epochs; TimerWheel::initialize
         eps = std::max(1u, 1000u / fc->recycle_ms);
-        te = fc->timeout_s * eps;
-        nb = pow2_at_least(te + 2u);
         if ((uint64_t)fc->timeout_s * eps + 2u > kMaxWheel)
             return fail(c, FCGPU_EINVAL, "flow timeout too long for the recycle interval (timer wheel above 16384 epochs)");
+        te = fc->timeout_s * eps;
+        nb = pow2_at_least(te + 2u);
         // the maintainer's per-chunk counts: (cap / 1024) x (TE + 1) words
         if ((uint64_t)((cap + kMaintChunk - 1) / kMaintChunk) * (te + 1u) > (1ull << 26))
             return fail(c, FCGPU_EINVAL, "flow timeout in epochs x capacity too large for the maintainer (timer wheel)");
