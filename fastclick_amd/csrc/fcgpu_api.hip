@@ -568,6 +568,8 @@ static std::vector<int> jit_keys_for(const fcgpu_ctx *c) {
 static int jit_build(fcgpu_ctx *c, const std::vector<int> &keys) {
     std::string err;
     HIPCHK(c, hipSetDevice(c->device));
+    // launches of the module being replaced may still run
+    HIPCHK(c, hipDeviceSynchronize());
     if (!jit_compile(c->jit_src, keys, kJitDeviceHh, kJitAbiH, c->jit, err)) {
         c->jit_src.clear();
         c->jit_keys.clear();
@@ -580,6 +582,8 @@ static int jit_build(fcgpu_ctx *c, const std::vector<int> &keys) {
 // The installed program as code: generated and compiled for the current
 // configuration; a program with a cycle stays interpreted (error returned).
 static int jit_install(fcgpu_ctx *c) {
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());      // no launch of the old module still running
     c->jit.unload();
     c->jit_src.clear();
     c->jit_keys.clear();
