@@ -360,3 +360,34 @@ def test_element_imp_ids(oracle):
         assert (r["port"][~ok] == 0xFFFFFFFF).all()
         assert r["handlers"]["flow_count"] == "1023"
         assert r["handlers"]["flow_drops"] == str(int((~ok).sum()))
+
+
+@pytest.mark.gpu
+def test_gpu_imp_reset_and_stats():
+    """fcgpu_flow_reset on an IMP table: the stack is full again (IDs restart
+    at cap-1), the table and the wheel empty; fcgpu_flow_stats follows."""
+    import torch
+    from fastclick_amd import device
+    rng = np.random.default_rng(3)
+    pool = synth._rand_flows(rng, 500)
+    b = make_batch(pool, rng.integers(0, 500, 3000))
+    cfg = flow_cfg()
+    ctx = N.Context(0, b.n, cfg)
+    try:
+        ctx.flow_configure(N.FLOW_MGR_IMP, 1024, timeout_s=2, recycle_ms=500)
+        db = device.DeviceBatch.upload(b, device="cuda:0")
+        ids = []
+        for _ in range(2):
+            ctx.flow_set_time(100)
+            outs = device.DeviceOutputs(b.n, cfg.nports, device="cuda:0", flowid=True)
+            device.run_device(ctx, db, outs)
+            torch.cuda.synchronize()
+            ids.append(outs.numpy()["flowid"])
+            st = ctx.flow_stats()
+            nfl = len(np.unique(ids[-1]))
+            assert (st["count"], st["free_ids"], st["pending"], st["epochs"]) == (nfl, 1023 - nfl, 0, 0)
+            assert ids[-1].max() == 1023 and ids[-1].min() == 1024 - nfl
+            ctx.flow_reset()
+        assert np.array_equal(ids[0], ids[1])
+    finally:
+        ctx.close()
