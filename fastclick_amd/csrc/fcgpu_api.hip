@@ -9,6 +9,23 @@
 //   FCGPU_PART_GLOBAL only:
 //   k_scan per-output exclusive scan over tiles                 (grid = outputs)
 //   k_part dense stable partition scatter                       (grid = tiles)
+//   flow table only: the new-flow pass (fcgpu_flow.hh)
+// Queued batches of one stream share one k_rx launch (process_fused).
+//
+// Sections, in file order:
+//   context (struct fcgpu_ctx), error/event helpers
+//   k_rx launch dispatch (launch_rx*: template instance per configuration;
+//     compiled programs through jit_function)
+//   whole-batch host path (process_host_whole)
+//   decision programs: jump tables (build_tables), compiled programs (jit_*)
+//   flow table: configure / clear / maintain / stats (fcgpu_flow_*)
+//   open / configure / close
+//   device-resident batches: process_one, fcgpu_process, fused jobs
+//     (process_fused, fcgpu_process_jobs)
+//   host-resident batches: pipelined chunks (process_host_pipelined), spans
+//     and blocks (fcgpu_span_*), mbuf ingress (fcgpu_pool_register,
+//     fcgpu_process_mbufs)
+//   counters, programs, timing
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <stdint.h>
