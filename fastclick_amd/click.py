@@ -47,6 +47,9 @@ def load():
     lib.fcclick_run_ex.restype = C.c_int
     lib.fcclick_run_ex.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                    C.c_uint32, C.POINTER(fcclick_result), C.c_char_p, C.c_size_t]
+    lib.fcclick_run_clocked.restype = C.c_int
+    lib.fcclick_run_clocked.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                        C.c_void_p, C.POINTER(fcclick_result), C.c_char_p, C.c_size_t]
     lib.fcclick_bench.restype = C.c_int
     lib.fcclick_bench.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.POINTER(C.c_double), C.c_char_p, C.c_size_t]
@@ -85,7 +88,10 @@ PER_PACKET = 0xFFFFFFFF   # burst value: the source calls push(0, p) per packet 
 TIMER_FLUSH = 1           # fcclick_run_ex flag: end with the element's timer, not flush()
 
 
-def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1, timer_flush: bool = False):
+def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1, timer_flush: bool = False,
+                burst_ns=None):
+    """Source(batch, BURST) -> conf => sinks. burst_ns: the element's clock (ns)
+    at each burst (fcclick_run_clocked), for time-driven behaviour."""
     lib = load()
     n = batch.n
     arena = np.ascontiguousarray(batch.arena)
@@ -101,8 +107,14 @@ def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1, timer_flu
                          nb.ctypes.data, C.cast(hbuf, C.c_char_p), 4096, out["paint"].ctypes.data,
                          out["flow"].ctypes.data, out["ip8"].ctypes.data, parked.ctypes.data)
     err = C.create_string_buffer(512)
-    rc = lib.fcclick_run_ex(conf.encode(), arena.ctypes.data, desc.ctypes.data, n, burst, nsinks,
-                            TIMER_FLUSH if timer_flush else 0, C.byref(res), err, 512)
+    if burst_ns is not None:
+        clock = np.ascontiguousarray(burst_ns, dtype=np.uint64)
+        assert len(clock) >= -(-n // burst) and not timer_flush
+        rc = lib.fcclick_run_clocked(conf.encode(), arena.ctypes.data, desc.ctypes.data, n, burst, nsinks,
+                                     clock.ctypes.data, C.byref(res), err, 512)
+    else:
+        rc = lib.fcclick_run_ex(conf.encode(), arena.ctypes.data, desc.ctypes.data, n, burst, nsinks,
+                                TIMER_FLUSH if timer_flush else 0, C.byref(res), err, 512)
     if rc == -1:
         raise ConfigError(err.value.decode())
     if rc != 0:

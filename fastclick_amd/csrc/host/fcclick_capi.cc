@@ -144,9 +144,28 @@ extern "C" int fcclick_parse_program(const char *text, fcgpu_step *steps, uint32
     return 0;
 }
 
+static int run_graph(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n, uint32_t burst,
+                     uint32_t nsinks, uint32_t flags, const uint64_t *burst_ns, fcclick_result *res, char *err,
+                     size_t errcap);
+
 extern "C" int fcclick_run_ex(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
                               uint32_t burst, uint32_t nsinks, uint32_t flags, fcclick_result *res, char *err,
                               size_t errcap) {
+    return run_graph(conf, arena, desc, n, burst, nsinks, flags, nullptr, res, err, errcap);
+}
+
+extern "C" int fcclick_run_clocked(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                                   uint32_t burst, uint32_t nsinks, const uint64_t *burst_ns, fcclick_result *res,
+                                   char *err, size_t errcap) {
+    if (!burst_ns) return -1;
+    const int rc = run_graph(conf, arena, desc, n, burst, nsinks, 0, burst_ns, res, err, errcap);
+    ModelPolicy::virtual_ns.store(0);
+    return rc;
+}
+
+static int run_graph(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n, uint32_t burst,
+                     uint32_t nsinks, uint32_t flags, const uint64_t *burst_ns, fcclick_result *res, char *err,
+                     size_t errcap) {
     std::string e;
     auto el = make_element(conf, e);
     if (!el || el->initialize(e) < 0) {
@@ -173,6 +192,7 @@ extern "C" int fcclick_run_ex(const char *conf, const uint8_t *arena, const uint
     // FromDPDKDevice-style source: BURST packets per PacketBatch
     for (uint32_t i = 0; i < n; i += burst) {
         uint32_t m = n - i < burst ? n - i : burst;
+        if (burst_ns) ModelPolicy::virtual_ns.store(burst_ns[i / burst] ? burst_ns[i / burst] : 1);
         Packet *head = nullptr, *prev = nullptr;
         for (uint32_t j = 0; j < m; ++j) {
             Packet *p = pool.make(arena + desc[2 * (i + j)], desc[2 * (i + j) + 1]);

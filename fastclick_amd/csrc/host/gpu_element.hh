@@ -6,6 +6,7 @@
 // FastClick data model (include/click/packet.hh, packetbatch.hh). This class
 // is what libfcclick.so drives in the tests and the host-rate benchmark.
 #pragma once
+#include <atomic>
 #include <chrono>
 #include <string>
 #include <vector>
@@ -38,7 +39,12 @@ struct ModelPolicy {
         return p;
     }
     static Batch *make_batch(Packet *h, Packet *t, unsigned n) { return PacketBatch::make_from_list(h, t, n); }
+    // the harness's clock: steady_clock, or the virtual time a clocked run
+    // sets before each burst (fcclick_run_clocked)
+    static inline std::atomic<uint64_t> virtual_ns{0};
     static uint64_t now_ns() {
+        const uint64_t v = virtual_ns.load(std::memory_order_relaxed);
+        if (v) return v;
         return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
                    std::chrono::steady_clock::now().time_since_epoch()).count();
     }

@@ -74,6 +74,14 @@ int fcclick_run_ex(const char *conf, const uint8_t *arena, const uint32_t *desc,
                    uint32_t burst, uint32_t nsinks, uint32_t flags, fcclick_result *res, char *err,
                    size_t errcap);
 
+/* fcclick_run on a virtual clock: before burst b is pushed the element's clock
+ * (what it reads as Timestamp::recent_steady) is set to burst_ns[b]
+ * (ceil(n / burst) entries), so time-driven behaviour -- the flow managers'
+ * timeouts and maintainer runs -- is reproducible. Ends with flush(). */
+int fcclick_run_clocked(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                        uint32_t burst, uint32_t nsinks, const uint64_t *burst_ns, fcclick_result *res,
+                        char *err, size_t errcap);
+
 /* Host-resident rate: repeat the same run `reps` times (packets recycled
  * LIFO into a mempool sized to what the element can hold, sinks discard), return packets per second through the element
  * including gather, PCIe copies, kernels and relinking. */

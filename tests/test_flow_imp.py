@@ -391,3 +391,44 @@ def test_gpu_imp_reset_and_stats():
         assert np.array_equal(ids[0], ids[1])
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+def test_element_imp_timeouts_virtual_clock(oracle):
+    """The element's IMP glue end to end on the harness's virtual clock
+    (fcclick_run_clocked): bursts 150 ms apart, BATCH 0 (a device batch per
+    PacketBatch), FLOW_TIMEOUT 1 s, FLOW_RECYCLE_INTERVAL 0.1 s -- the
+    maintainer runs due before each batch run first (every 100 ms from the
+    first batch), flows drifting out of use expire and their IDs are reused,
+    exactly as the oracle replaying the same events says."""
+    from fastclick_amd import click as K
+    rng = np.random.default_rng(17)
+    pool = synth._rand_flows(rng, 3_000)
+    nb, burst, t0 = 40, 64, 5_000_000_000           # ns
+    idx = np.concatenate([(b * 40 + rng.integers(0, 300, burst)) % 3_000 for b in range(nb)])
+    b = make_batch(pool, idx)
+    clock = np.array([t0 + k * 150_000_000 for k in range(nb)], np.uint64)
+    conf = ("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4, FLOW_CAPACITY 256, FLOW_MANAGER IMP, "
+            "FLOW_TIMEOUT 1, FLOW_RECYCLE_INTERVAL 0.1, BATCH 0)")
+    r = K.run_element(conf, b, burst=burst, nsinks=5, burst_ns=clock)
+    # the oracle replays the element's events (gpu_core.hh flow_clock)
+    cfg = flow_cfg()
+    t = oracle.ImpFlowTable(256, 1, 100)
+    nxt = None
+    exp = []
+    for k in range(nb):
+        now = int(clock[k] // 1_000_000) & 0xFFFFFFFF
+        if nxt is None:
+            nxt = now + 100
+        while now - nxt >= 0:
+            t.maintain(nxt)
+            nxt += 100
+        part = synth.Batch(arena=b.arena, desc=np.ascontiguousarray(b.desc[k * burst:(k + 1) * burst]))
+        exp.append(t.batch(part, oracle.process_batch(cfg, part), now))
+    exp = np.concatenate(exp)
+    ok = exp != FULL
+    assert ok.sum() > 1000 and (~ok).sum() > 0          # some flows found the table full
+    assert np.array_equal(r["flow"][ok], exp[ok])
+    assert (r["port"][~ok] == 0xFFFFFFFF).all()
+    assert len(np.unique(exp[ok])) < len(np.unique(idx))  # IDs were reused
+    assert r["handlers"]["flow_drops"] == str(int((~ok).sum()))
