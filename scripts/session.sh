@@ -79,7 +79,7 @@ for s in "${ST[@]}"; do
     host) step host_rate 600 python scripts/host_rate.py ;;
     host_q16) GPU_MAX_HW_QUEUES=16 step host_rate_q16 600 python scripts/host_rate.py ;;
     kgather) step kgather 180 ./scripts/kgather 64 ;;
-    latency) step latency 120 python scripts/latency_probe.py && step latency_spin 120 python scripts/latency_probe.py --spin ;;
+    latency) step latency 120 python scripts/latency_probe.py ;;
     dist2) step dist2 300 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 --no-cpu ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
