@@ -112,7 +112,7 @@ __device__ __forceinline__ uint32_t flow_next_after(const FlowArgs &F, uint32_t 
 // claimant's key, written by k_rx, is compared), its first packet index
 // atomicMin'd into `first`. kSlotNone: no IDs left (FCGPU_FLOW_FULL).
 constexpr uint32_t kSlotHit = 0xfffffffeu;
-__device__ __forceinline__ uint32_t flow_place(const FlowArgs &F, uint32_t i) {
+__device__ __forceinline__ uint32_t flow_place(const FlowArgs &F, uint32_t i, uint32_t &hid) {
     const uint4 k = F.miss_key[i];
     uint32_t pos = F.miss_slot[i];
     const bool full = __hip_atomic_load(&F.state[kFsNext], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= F.max_flows;
@@ -127,6 +127,7 @@ __device__ __forceinline__ uint32_t flow_place(const FlowArgs &F, uint32_t i) {
                 const uint32_t id = flow_tag_id(tag);
                 if (F.lastseen && id < kTagFull) F.lastseen[id] = F.now;
                 if (F.flowid) F.flowid[i] = id;
+                hid = id;
                 return kSlotHit;
             }
         } else {
@@ -145,6 +146,33 @@ __device__ __forceinline__ uint32_t flow_place(const FlowArgs &F, uint32_t i) {
         pos = (pos + 1) & F.mask;
     }
     return kSlotNone;
+}
+
+// flow_place for the misses of a wave (`live` lanes; every lane of the wave
+// calls it). Misses of one key stop their k_rx probe at the same slot, so the
+// lanes sharing a stop slot and the key of the lowest such lane follow that
+// lane: it alone places the key (its index is the lowest, so its atomicMin on
+// `first` is theirs too) and they take its result. A batch whose misses are
+// mostly one new flow (an elephant's first batch) then costs one CAS + one
+// atomicMin per wave on the flow's slot, not per packet (1M packets of one new
+// flow: 17 ms of contended atomics on one address without this).
+__device__ __forceinline__ uint32_t flow_place_wave(const FlowArgs &F, uint32_t i, bool live) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t stop = live ? F.miss_slot[i] : 0u;
+    const uint4 k = live ? F.miss_key[i] : make_uint4(0, 0, 0, 0);
+    const uint64_t grp = match_any(stop, 32u - __clz(F.mask | 1u), __ballot(live));
+    const uint32_t lead = grp ? (uint32_t)__builtin_ctzll(grp) : lane;
+    const bool same = __shfl(k.x, (int)lead) == k.x && __shfl(k.y, (int)lead) == k.y &&
+                      __shfl(k.z, (int)lead) == k.z && __shfl(k.w, (int)lead) == k.w;
+    const bool follow = live && lead != lane && same;
+    uint32_t slot = kSlotNone, hid = 0;
+    if (live && !follow) slot = flow_place(F, i, hid);
+    const uint32_t ls = (uint32_t)__shfl((int)slot, (int)lead), lh = (uint32_t)__shfl((int)hid, (int)lead);
+    if (follow) {
+        slot = ls;
+        if (slot == kSlotHit && F.flowid) F.flowid[i] = lh;
+    }
+    return slot;
 }
 
 // The wave's 64 packets from i0 (a multiple of 64): the first packet of each
@@ -359,7 +387,7 @@ __device__ __forceinline__ void flow_finish_body(const FlowArgs &F, uint32_t nw,
 #pragma unroll
         for (uint32_t q = 0; q < kQ; ++q) {
             pkt[q] = e0 + q < cn ? s_idx[e0 + q] : 0u;
-            slot[q] = e0 + q < cn ? flow_place(F, pkt[q]) : kSlotNone;
+            slot[q] = flow_place_wave(F, pkt[q], e0 + q < cn);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -448,7 +476,9 @@ __global__ __launch_bounds__(kFlowGridBlock) void k_flow_claim(FlowArgs F, uint3
     for (uint32_t i0 = blockIdx.x * kFlowGridBlock + (threadIdx.x & ~63u); i0 < nw * 64;
          i0 += gridDim.x * kFlowGridBlock) {
         const uint32_t lane = threadIdx.x & 63, i = i0 + lane;
-        if ((F.missmask[i0 >> 6] >> lane) & 1u) F.miss_slot[i] = flow_place(F, i);
+        const bool live = (F.missmask[i0 >> 6] >> lane) & 1u;
+        const uint32_t slot = flow_place_wave(F, i, live);
+        if (live) F.miss_slot[i] = slot;
     }
 }
 

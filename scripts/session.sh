@@ -28,6 +28,7 @@ IFS=, read -ra ST <<< "${STEPS:-tests,smoke,bench}"
 for s in "${ST[@]}"; do
   case $s in
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    tests_flow) step pytest_flow 600 python -u -m pytest tests/test_flow.py tests/test_flow_imp.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 300 python bench.py $DRV ;;
     bench_s1) step bench_s1 300 python bench.py $DRV --streams 1 --fuse 1 --no-cpu ;;
@@ -79,6 +80,9 @@ for s in "${ST[@]}"; do
     host) step host_rate 600 python scripts/host_rate.py ;;
     host_q16) GPU_MAX_HW_QUEUES=16 step host_rate_q16 600 python scripts/host_rate.py ;;
     kgather) step kgather 180 ./scripts/kgather 64 ;;
+    kt_flow) kt kt_flow_c2 300 --steps 200 --warmup 20 --no-cpu --flow-capacity 1 &&
+             kt kt_flow_c3 300 --steps 200 --warmup 20 --no-cpu --workload c3 --flow-capacity 20000 &&
+             kt kt_flow_c4 300 --steps 200 --warmup 20 --no-cpu --workload c4 --flow-capacity 2000000 ;;
     latency) step latency 120 python scripts/latency_probe.py ;;
     dist2) step dist2 300 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 --no-cpu ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -285,3 +285,38 @@ def test_gpu_flow_fused_jobs(oracle, manager):
         assert ctx.flow_count() == ecnt
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_flows", [1 << 16, 1_985])
+def test_gpu_flow_elephants(oracle, max_flows):
+    """Batches whose misses are mostly a few new flows, interleaved packet by
+    packet: the lanes of a wave that share a flow follow one lane through the
+    placement (flow_place_wave). 150k packets of 3 new flows (grid-wide pass);
+    then 800 and 900 packets of 2 new flows each among 2,000 known flows (grid
+    pass, then the single-block pass after a small batch). With max_flows 1,985
+    (the 1,983 known flows + 2) the third elephant and every later new flow
+    find the table full, so followers of a lane that found
+    no ID take FCGPU_FLOW_FULL."""
+    base = synth.c3(10_000, nflows=2_000, seed=70)
+    eleph = synth.c3(150_000, nflows=3, seed=71)
+    rng = np.random.default_rng(72)
+
+    def few_new(k, seed):
+        frames = [base.frame(i) for i in range(base.n)]
+        new = synth.c3(k, nflows=2, seed=seed)
+        pos = np.sort(rng.integers(0, len(frames) + 1, k))
+        for j, p in enumerate(pos[::-1]):
+            frames.insert(int(p), new.frame(k - 1 - j))
+        return synth.from_frames(frames)
+
+    bs = [base, eleph, few_new(800, 73), few_new(900, 74)]
+    cfg = flow_cfg()
+    got, cnt, res = _dev_flows(cfg, bs, max_flows)
+    exp, ecnt = oracle_flows(oracle, cfg, bs, max_flows)
+    for j, (r, b) in enumerate(zip(res, bs)):
+        o = exp[sum(x.n for x in bs[:j]):][:b.n]
+        assert np.array_equal(r["flowid"], o), f"batch {j}: {np.count_nonzero(r['flowid'] != o)} IDs differ"
+    assert cnt == ecnt
+    if max_flows == 1_985:
+        assert (got == FULL).any()
