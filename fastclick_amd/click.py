@@ -24,7 +24,7 @@ class fcclick_result(C.Structure):
                 ("out_dst", C.c_void_p), ("out_len", C.c_void_p), ("out_nh", C.c_void_p),
                 ("out_batches", C.c_void_p), ("handlers", C.c_char_p), ("handlers_cap", C.c_size_t),
                 ("out_paint", C.c_void_p), ("out_flow", C.c_void_p), ("out_ip8", C.c_void_p),
-                ("out_parked", C.c_void_p)]
+                ("out_parked", C.c_void_p), ("out_batch", C.c_void_p)]
 
 
 def load():
@@ -98,14 +98,16 @@ def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1, timer_flu
     desc = np.ascontiguousarray(batch.desc, dtype=np.uint32)
     out = {k: np.zeros(n, dt) for k, dt in (("port", np.uint32), ("seq", np.uint32), ("agg", np.uint32),
                                             ("dst", np.uint32), ("len", np.uint32), ("nh", np.int32),
-                                            ("paint", np.uint8), ("flow", np.uint32), ("ip8", np.uint32))}
+                                            ("paint", np.uint8), ("flow", np.uint32), ("ip8", np.uint32),
+                                            ("batch", np.uint32))}
     nb = np.zeros(1, np.uint32)
     parked = np.zeros(1, np.uint32)
     hbuf = C.create_string_buffer(4096)
     res = fcclick_result(out["port"].ctypes.data, out["seq"].ctypes.data, out["agg"].ctypes.data,
                          out["dst"].ctypes.data, out["len"].ctypes.data, out["nh"].ctypes.data,
                          nb.ctypes.data, C.cast(hbuf, C.c_char_p), 4096, out["paint"].ctypes.data,
-                         out["flow"].ctypes.data, out["ip8"].ctypes.data, parked.ctypes.data)
+                         out["flow"].ctypes.data, out["ip8"].ctypes.data, parked.ctypes.data,
+                         out["batch"].ctypes.data)
     err = C.create_string_buffer(512)
     if burst_ns is not None:
         clock = np.ascontiguousarray(burst_ns, dtype=np.uint64)

@@ -22,7 +22,7 @@ class Sink : public Element {
     const char *class_name() const override { return "Sink"; }
     int configure(const std::vector<std::string> &, std::string &) override { return 0; }
     void push_batch(int, PacketBatch *b) override {
-        ++*_nbatch;
+        const uint32_t bi = (*_nbatch)++;
         unsigned cnt = 0;
         for (Packet *p = b->first(); p;) {
             Packet *nx = p->next();
@@ -30,6 +30,7 @@ class Sink : public Element {
             if (_r) {
                 if (_r->out_port) _r->out_port[i] = (uint32_t)_port;
                 if (_r->out_seq) _r->out_seq[i] = (*_seq);
+                if (_r->out_batch) _r->out_batch[i] = bi;
                 if (_r->out_agg) _r->out_agg[i] = p->anno_u32(AGGREGATE_ANNO_OFFSET);
                 if (_r->out_dst) _r->out_dst[i] = p->anno_u32(DST_IP_ANNO_OFFSET);
                 if (_r->out_len) _r->out_len[i] = p->length();
@@ -180,6 +181,7 @@ static int run_graph(const char *conf, const uint8_t *arena, const uint32_t *des
         for (uint32_t i = 0; i < n; ++i) {
             if (res->out_port) res->out_port[i] = 0xffffffffu;
             if (res->out_seq) res->out_seq[i] = 0xffffffffu;
+            if (res->out_batch) res->out_batch[i] = 0xffffffffu;
         }
     }
     std::vector<std::unique_ptr<Sink>> sinks;

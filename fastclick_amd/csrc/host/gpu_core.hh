@@ -56,6 +56,9 @@
 //     order of first appearance, elements/research/flowipmanagerhmp.cc:96-126)
 //     in the 4-byte annotation at FLOWID_ANNO; a new flow beyond the capacity
 //     is killed (as the IMP managers do when their flow stack is empty).
+//   FLOW_RUNS (default true): each output's packets leave in runs of one
+//     flow, a PacketBatch per run, as the flow managers' BatchBuilder pushes
+//     them (flowipmanagerhmp.cc:101-117); false: one batch per output run.
 //   FLOW_MANAGER HMP|IMP, FLOW_TIMEOUT s, FLOW_RECYCLE_INTERVAL s (default 1)
 //                                            -- IMP: FlowIPManager_CuckooPP /
 //     FlowIPManagerIMP (CAPACITY, TIMEOUT, RECYCLE_INTERVAL): IDs from a free-ID
@@ -250,6 +253,9 @@ class RxCore {
                 const double d = strtod(v.c_str(), &end);
                 if (v.empty() || *end || !(d >= 0.001 && d <= 65.535)) return err(errh, "bad FLOW_RECYCLE_INTERVAL");
                 _flow_recycle_ms = (uint32_t)(d * 1000);
+            } else if (k == "FLOW_RUNS") {
+                if (!parse_bool(v, b)) return err(errh, "FLOW_RUNS expects true/false");
+                _flow_runs = b;
             } else if (k == "FLOWID_ANNO") {
                 if (!parse_int(v, n) || n < 0 || n > P::kAnnoSize - 4) return err(errh, "bad FLOWID_ANNO");
                 _flow_anno = (int)n;
@@ -707,8 +713,19 @@ class RxCore {
                     s.keep[w++] = i;
                 }
             }
+            // FLOW_RUNS: consecutive packets of one flow leave as one batch
+            // (the BatchBuilder of FlowIPManagerHMP::process and
+            // VirtualFlowManagerIMP::process, flowipmanagerhmp.cc:101-117,
+            // virtualflowmanager.hh:304-326); killed packets do not end a run
+            const bool runs = _flow_runs && s.flowid && !last;
             for (uint32_t a = 0; a < w;) {
-                const uint32_t k = w - a < kMaxBatch ? w - a : kMaxBatch;
+                uint32_t k = w - a < kMaxBatch ? w - a : kMaxBatch;
+                if (runs) {
+                    const uint32_t f = s.flowid[s.keep[a]];
+                    uint32_t j = 1;
+                    while (j < k && s.flowid[s.keep[a + j]] == f) ++j;
+                    k = j;
+                }
                 Packet *head = s.pkts[s.keep[a]], *prev = head;
                 for (uint32_t j = 1; j < k; ++j) {
                     Packet *q = s.pkts[s.keep[a + j]];
@@ -744,6 +761,7 @@ class RxCore {
     uint32_t _next_maint = 0;
     bool _maint_armed = false;
     int _flow_anno = 28;
+    bool _flow_runs = true;
     uint64_t _flow_drops = 0;
     int _device = 0;
     uint32_t _batch = 16384;

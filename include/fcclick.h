@@ -50,6 +50,8 @@ typedef struct fcclick_result {
                                departure, little-endian (may be NULL)                  */
     uint32_t *out_parked;   /* [1] FCCLICK_TIMER_FLUSH: packets the element still held when
                                the source stopped (may be NULL)                          */
+    uint32_t *out_batch;    /* [n] index of the PacketBatch the packet arrived in at its
+                               sink, in arrival order over all sinks (may be NULL)    */
 } fcclick_result;
 
 /* burst value for a non-batch upstream: the source calls the element's

@@ -28,6 +28,7 @@ IFS=, read -ra ST <<< "${STEPS:-tests,smoke,bench}"
 for s in "${ST[@]}"; do
   case $s in
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    tests_sel) step pytest_sel 600 python -u -m pytest $SEL -m gpu -x -v --timeout 120 --timeout-method thread ;;
     tests_flow) step pytest_flow 600 python -u -m pytest tests/test_flow.py tests/test_flow_imp.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 300 python bench.py $DRV ;;

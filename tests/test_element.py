@@ -223,6 +223,38 @@ def test_element_flow_golden():
     assert r["handlers"]["flow_drops"] == str(int(full.sum()))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("runs", [True, False])
+def test_element_flow_runs(runs):
+    """FLOW_RUNS (default true): behind the flow table the packets of each
+    output leave as one PacketBatch per run of one flow, as the flow managers'
+    BatchBuilder pushes them (flowipmanagerhmp.cc:101-117,
+    virtualflowmanager.hh:304-326). Departures come per device batch (BATCH),
+    per 256-packet tile, per output; a new batch starts exactly where the
+    output, the tile or (with runs) the flow changes. Invalid packets (output
+    N) have no flow and leave as one batch per tile."""
+    from fastclick_amd import click as K
+    b = synth.c3(20_000, nflows=20, seed=80)
+    synth.inject_errors(b, 0.01, seed=81)
+    batch, nports = 4096, 4
+    conf = (f"GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N {nports}, FLOW_CAPACITY 1024, BATCH {batch}"
+            + ("" if runs else ", FLOW_RUNS false") + ")")
+    r = K.run_element(conf, b, nsinks=nports + 1)
+    left = np.nonzero(r["port"] != 0xFFFFFFFF)[0]
+    order = left[np.argsort(r["seq"][left])]
+    port = r["port"][order].astype(np.int64)
+    flow = np.where(port < nports, r["flow"][order].astype(np.int64), -1) if runs else np.zeros(len(order), np.int64)
+    key = np.stack([port, order // batch, (order % batch) // 256, flow], axis=1)
+    change = np.any(key[1:] != key[:-1], axis=1)
+    assert r["batches"] == int(change.sum()) + 1
+    bi = r["batch"][order]
+    assert np.array_equal(bi[1:] != bi[:-1], change)
+    if runs:   # every batch behind the table holds one flow
+        valid = port < nports
+        pairs = np.unique(np.stack([bi[valid], flow[valid]], axis=1), axis=0)
+        assert len(pairs) == len(np.unique(bi[valid]))
+
+
 def test_config_flow_keywords():
     from fastclick_amd import click as K
     K.check_config("GPUIPCheckClassify(OFFSET 14, FLOW_CAPACITY 65536, FLOWID_ANNO 32)")
@@ -230,6 +262,9 @@ def test_config_flow_keywords():
         K.check_config("GPUIPCheckClassify(MODE AUTO, FLOW_CAPACITY 10)")
     with pytest.raises(K.ConfigError, match="FLOWID_ANNO"):
         K.check_config("GPUIPCheckClassify(FLOWID_ANNO 46)")
+    K.check_config("GPUIPCheckClassify(OFFSET 14, FLOW_CAPACITY 64, FLOW_RUNS false)")
+    with pytest.raises(K.ConfigError, match="FLOW_RUNS"):
+        K.check_config("GPUIPCheckClassify(FLOW_RUNS maybe)")
 
 
 @pytest.mark.gpu
