@@ -74,7 +74,7 @@ def parse(argv=None):
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
     ap.add_argument("--timing-every", type=int, default=0,
                     help="bracket the k_rx launch covering every k-th timed batch with HIP events "
-                         "(hipExtLaunchKernelGGL start/stop on the launch stream; created before the "
+                         "(stream markers on the launch stream, hipEventRecord; created before the "
                          "timed region). Each event idles the queue ~4 us, so the default samples "
                          "sparsely: 8 (a fused launch of 20 batches is one bracketed launch)")
     ap.add_argument("--streams", type=int, default=1,
@@ -403,7 +403,11 @@ class DeviceProcessor:
             self.torch.cuda.synchronize()
         warm = self._jobs(0, steps)
         self.timed = self._jobs(steps, self.args.steps)   # built before the warmup
-        self.ctx.set_timing(self.timing_every)      # creates the event pool now
+        # creates the event pool now, and times every warmup launch: the first
+        # launch with timing events pays a one-time cost in HIP (~9 us of host
+        # enqueue, profiles/r02_s9/diag*.log) that belongs in the warmup, not
+        # in the timed region (the pool hands the same events out again)
+        self.ctx.set_timing(1 if self.timing_every else 0)
         self.ctx.run_jobs(warm)
         self.torch.cuda.synchronize()
         self.ctx.read_timing()                      # drop warmup samples
@@ -450,6 +454,28 @@ class DeviceProcessor:
         self.ctx.close()
 
 
+def _diag_regions(proc, elapsed, enq, timing, repeats=6):
+    """FCGPU_BENCH_DIAG=1 (diagnostics, stderr only; the JSON line is the
+    first region's): the timed region repeated in the same process on the
+    same jobs and output sets, so a first-region-only cost shows up."""
+    snap = proc.counters().clone()     # the repeats count too: restored below
+    regs = []
+    for _ in range(repeats):
+        proc.sync()
+        t0 = time.perf_counter()
+        proc.run_timed()
+        t1 = time.perf_counter()
+        proc.sync()
+        regs.append(((time.perf_counter() - t0) * 1e6, (t1 - t0) * 1e6))
+    print(json.dumps({"diag": {"region_us": round(elapsed * 1e6, 1), "enqueue_us": round(enq * 1e6, 1),
+                               "kernel_ms": timing and timing["k_rx_ms"],
+                               "repeat_region_us": [round(r, 1) for r, _ in regs],
+                               "repeat_enqueue_us": [round(e, 1) for _, e in regs]}}),
+          file=sys.stderr, flush=True)
+    proc.timing()   # drop the repeats' samples
+    proc.counters().copy_(snap)
+
+
 def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_collectives):
     """One rank of the benchmark: build, warm up, time exactly args.steps
     steps between barrier + device sync on both sides, take the max over
@@ -474,11 +500,14 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
         proc.sync()
         t0 = time.perf_counter()
         proc.run_timed()
+        t_enq = time.perf_counter()
         proc.sync()
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         timing = proc.timing()
+        if os.environ.get("FCGPU_BENCH_DIAG"):
+            _diag_regions(proc, elapsed, t_enq - t0, timing)
         maintain_ms = getattr(proc, "maintain_ms", None)
 
         # after the timed region: max time over ranks, counters summed over

@@ -1276,8 +1276,15 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
         HIPCHK(c, hipEventRecord(c->flow_order[0], c->stream));
         HIPCHK(c, hipStreamWaitEvent(s, c->flow_order[0], 0));
     }
-    launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, L, tiles, s, timed ? ev.a : nullptr,
-                  timed ? ev.b : nullptr, c->jit_src.empty() ? nullptr : c);
+    // a sampled launch is bracketed by two stream markers (hipEventRecord),
+    // not by hipExtLaunchKernelGGL's event pair: the pair cost ~4 us more of
+    // host enqueue and 5-10 us more per timed region on an idle queue
+    // (profiles/r02_s9/evt_ab.txt); the markers' interval adds only the
+    // launch's dispatch latency, shared by its batches
+    if (timed) HIPCHK(c, hipEventRecord(ev.a, s));
+    launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, L, tiles, s, nullptr, nullptr,
+                  c->jit_src.empty() ? nullptr : c);
+    if (timed) HIPCHK(c, hipEventRecord(ev.b, s));
     HIPCHK(c, hipGetLastError());
     if (timed) c->pending.push_back(ev);
     if (flow && *(volatile uint32_t *)c->flow_hint != kHintBig) {

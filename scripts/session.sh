@@ -44,6 +44,7 @@ for s in "${ST[@]}"; do
     kt_nopf_s1) kt kt_nopf_s1 300 $DRV --no-cpu --prefault 0 --streams 1 ;;
     kt_notime_s1) kt kt_notime_s1 300 $DRV --no-cpu --no-timing --streams 1 ;;
     kt_w40_s1) kt kt_w40_s1 300 --gpus 1 --steps 20 --warmup 40 --no-cpu --streams 1 ;;
+    diag) for k in 1 2 3; do FCGPU_BENCH_DIAG=1 step "diag$k" 300 python bench.py $DRV --no-cpu; done ;;
     bench2) step bench2 300 python bench.py $DRV --no-cpu ;;
     bench3) step bench3 300 python bench.py $DRV --no-cpu ;;
     # PMC per batch: one batch per launch (--fuse 1)
