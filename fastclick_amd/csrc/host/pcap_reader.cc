@@ -172,7 +172,7 @@ int fcpcap_read(fcpcap *r, uint8_t *buf, size_t cap, uint32_t *desc, uint32_t *w
     *used = 0;
     // the carried partial record first, then as much of the file as fits
     size_t have = r->carry.size() < cap ? r->carry.size() : cap;
-    memcpy(buf, r->carry.data(), have);
+    if (have) memcpy(buf, r->carry.data(), have);   // (an empty carry's data() may be null)
     r->carry.erase(r->carry.begin(), r->carry.begin() + have);
     if (!r->eof && have < cap && r->carry.empty()) {
         // the rest of the buffer from the file, as `threads` pread() pieces of

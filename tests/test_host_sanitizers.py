@@ -1,0 +1,60 @@
+"""Host code under AddressSanitizer + UndefinedBehaviorSanitizer (CPU only).
+
+SURVEY §5: the reference ships no sanitizer build; this repo runs its own
+host-side parsers (FromDump-compatible pcap reader, decision-program text,
+element keywords) and the oracle under ASan/UBSan on seeded random and
+mutated inputs (tests/host_fuzz.cc), and the pcap reader's parallel reads
+under ThreadSanitizer. The HIP kernels are not instrumented
+(GPU sanitizers are not available on the pool); libfcgpu.so is linked
+uninstrumented only for fcgpu_default_cfg and the element's symbols, and no
+HIP call is made.
+"""
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "fastclick_amd", "lib")
+
+
+def _build_and_run(tmp_path, sanitize, runs):
+    san = [f"-fsanitize={sanitize}", "-fno-omit-frame-pointer", "-g", "-O1"]
+    if sanitize != "thread":
+        san.append("-fno-sanitize-recover=all")
+    tag = sanitize.replace(",", "_")
+    obj = tmp_path / f"fc_oracle_{tag}.o"
+    subprocess.run(["gcc", *san, "-std=gnu11", "-I", os.path.join(ROOT, "include"), "-c",
+                    os.path.join(ROOT, "oracle", "fc_oracle.c"), "-o", str(obj)], check=True)
+    exe = tmp_path / f"host_fuzz_{tag}"
+    subprocess.run(["g++", *san, "-std=c++17", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "host_fuzz.cc"),
+                    os.path.join(ROOT, "fastclick_amd", "csrc", "host", "pcap_reader.cc"), str(obj),
+                    "-L", LIB, "-lfcgpu", f"-Wl,-rpath,{LIB}", "-lpthread", "-o", str(exe)], check=True)
+    with open(os.path.join(ROOT, "tests", "golden", "reftests.json")) as f:
+        progs = [p["program"].strip().replace("\n", "|") for p in json.load(f)["programs"]]
+    pf = tmp_path / "programs.txt"
+    pf.write_text("\n".join(progs) + "\n")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:halt_on_error=1:abort_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1", TSAN_OPTIONS="halt_on_error=1",
+               TMPDIR=str(tmp_path))
+    for seed, seconds in runs:
+        out = subprocess.run([str(exe), str(pf), str(seconds), str(seed)], capture_output=True, text=True,
+                             env=env, timeout=300)
+        assert out.returncode == 0, out.stderr[-4000:]
+        assert "host_fuzz ok" in out.stdout, out.stdout + out.stderr[-2000:]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None or shutil.which("gcc") is None, reason="no host compiler")
+@pytest.mark.skipif(not os.path.exists(os.path.join(LIB, "libfcgpu.so")), reason="libfcgpu.so not built")
+def test_host_code_under_asan_ubsan(tmp_path):
+    _build_and_run(tmp_path, "address,undefined", [(1, 4), (2, 4)])
+
+
+@pytest.mark.skipif(shutil.which("g++") is None or shutil.which("gcc") is None, reason="no host compiler")
+@pytest.mark.skipif(not os.path.exists(os.path.join(LIB, "libfcgpu.so")), reason="libfcgpu.so not built")
+def test_host_code_under_tsan(tmp_path):
+    """The pcap reader's parallel pread() pieces (fcpcap_set_threads)."""
+    _build_and_run(tmp_path, "thread", [(3, 3)])
