@@ -855,6 +855,18 @@ __device__ __forceinline__ uint64_t match_any(uint32_t key, uint32_t nbits, uint
     return m;
 }
 
+// A workgroup barrier for LDS data only: this wave's LDS operations complete,
+// then s_barrier. __syncthreads() is a workgroup release/acquire fence on all
+// memory, which on gfx9 means s_waitcnt vmcnt(0) before the barrier: every
+// wave of the tile would first wait for its outstanding global loads (the
+// flow-table probe k_rx issues early to hide its latency) and for its
+// verdict/hash stores to be acknowledged. Nothing after rx_tile's barrier
+// reads global memory another wave of the workgroup wrote, so the LDS
+// counters are all the barrier has to publish.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Partition modes of k_rx
 constexpr int kPartNone = 0;     // counters only
 constexpr int kPartGlobal = 1;   // + per-tile port histogram for k_scan/k_part (dense perm)
@@ -1106,7 +1118,7 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, const RxView &V, const 
         const uint64_t g2 = match_any(rslot, 4, mbad);
         if (rslot != 0xffffffffu && __popcll(g2 & lt) == 0) s_cnt[wave][nb + rslot] = (uint32_t)__popcll(g2);
     }
-    __syncthreads();
+    lds_barrier();
     const uint32_t nbt = nb + FCGPU_NREASON_SLOTS;
     const uint32_t t = threadIdx.x;
     uint32_t tot = 0;
