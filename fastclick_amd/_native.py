@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
-LIBFCGPU = os.path.join(LIB_DIR, "libfcgpu.so")
+# FCGPU_LIB: another build of the library (same-box A/B measurements only)
+LIBFCGPU = os.environ.get("FCGPU_LIB") or os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------

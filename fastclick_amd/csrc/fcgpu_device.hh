@@ -167,6 +167,16 @@ struct FrameView {
         const uint32_t x = b + shift;
         return (wdw(x & ~3u) >> (8 * (x & 3u))) & 0xff;
     }
+    // rd32 for a frame byte whose dword pair lies in the window (x + 8 <= kWin):
+    // LDS reads only. (wdw's choice between the LDS row and the arena compiles
+    // to flat loads, which go through the vector-memory path and wait on it.)
+    __device__ __forceinline__ uint32_t rd32_win(uint32_t b) const {
+        const uint32_t x = b + shift, a = x & ~3u;
+        const uint32_t lo = *reinterpret_cast<const uint32_t *>(row + ((((a >> 4) ^ sw) << 4) | (a & 15)));
+        const uint32_t a4 = a + 4;
+        const uint32_t hi = *reinterpret_cast<const uint32_t *>(row + ((((a4 >> 4) ^ sw) << 4) | (a4 & 15)));
+        return __builtin_amdgcn_alignbyte(hi, lo, x & 3u);
+    }
 };
 
 // click_in_cksum(hdr, hlen) == 0  <=>  the end-around-carry sum of the header's
@@ -901,14 +911,29 @@ __device__ __forceinline__ uint32_t flow_tag_id(uint32_t tag) {
 // (sport, dport), ip_p. A non-first fragment returns before assign(): its
 // addresses stay 0 (IPAddress(), ipaddress.hh:21-22) and its ports unset
 // (defined as 0), so it keys on ip_p alone.
-__device__ __forceinline__ uint4 flow_key(const FrameView &f, const fcgpu_anno &an) {
+__device__ __forceinline__ uint4 flow_key(const FrameView &f, const fcgpu_anno &an, bool live) {
     uint4 k;
-    const uint32_t w1 = f.rd32(an.nh + 4);          // id, frag offset
-    const uint32_t w2 = f.rd32(an.nh + 8);          // ttl, proto, sum
+    uint32_t w1, w2, sa, da, pt;
+    // the header and the first L4 word inside the window for every lane of
+    // the wave (the common case): LDS reads only; else the general reads
+    const bool inwin = an.th + f.shift + 8 <= (uint32_t)kWin && an.nh + f.shift + 24 <= (uint32_t)kWin;
+    if (!__ballot(live && !inwin)) {
+        w1 = f.rd32_win(an.nh + 4);
+        w2 = f.rd32_win(an.nh + 8);
+        sa = f.rd32_win(an.nh + 12);
+        da = f.rd32_win(an.nh + 16);
+        pt = f.rd32_win(an.th);
+    } else {
+        w1 = f.rd32(an.nh + 4);                     // id, frag offset
+        w2 = f.rd32(an.nh + 8);                     // ttl, proto, sum
+        sa = f.rd32(an.nh + 12);
+        da = f.rd32(an.nh + 16);
+        pt = f.rd32(an.th);
+    }
     const bool first = (bswap16(w1 >> 16) & 0x1fff) == 0;
-    k.x = first ? f.rd32(an.nh + 12) : 0u;
-    k.y = first ? f.rd32(an.nh + 16) : 0u;
-    k.z = first ? f.rd32(an.th) : 0u;
+    k.x = first ? sa : 0u;
+    k.y = first ? da : 0u;
+    k.z = first ? pt : 0u;
     k.w = (w2 >> 8) & 0xffu;
     return k;
 }
@@ -931,7 +956,7 @@ __device__ __forceinline__ FlowProbe flow_issue(const FlowArgs &F, const FrameVi
     q.sl = make_uint4(0, 0, 0, 0);
     q.pos = 0;
     if (q.want) {
-        q.key = flow_key(f, r.an);
+        q.key = flow_key(f, r.an, true);
         q.pos = flow_slot_hash(q.key) & F.mask;
         q.sl = F.slots[q.pos];
     }
