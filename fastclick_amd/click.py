@@ -37,6 +37,8 @@ def load():
     lib = C.CDLL(N.LIBFCCLICK)
     lib.fcclick_check_config.restype = C.c_int
     lib.fcclick_check_config.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t]
+    lib.fcclick_element_cfg.restype = C.c_int
+    lib.fcclick_element_cfg.argtypes = [C.c_char_p, C.POINTER(N.fcgpu_cfg), C.c_char_p, C.c_size_t]
     lib.fcclick_parse_program.restype = C.c_int
     lib.fcclick_parse_program.argtypes = [C.c_char_p, C.POINTER(N.fcgpu_step), C.c_uint32,
                                           C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.c_char_p,
@@ -69,6 +71,16 @@ def check_config(conf: str):
     err = C.create_string_buffer(512)
     if lib.fcclick_check_config(conf.encode(), err, 512) != 0:
         raise ConfigError(err.value.decode())
+
+
+def element_cfg(conf: str):
+    """The fcgpu_cfg a GPUIPCheckClassify configuration string produces (no GPU)."""
+    lib = load()
+    cfg = N.fcgpu_cfg()
+    err = C.create_string_buffer(512)
+    if lib.fcclick_element_cfg(conf.encode(), C.byref(cfg), err, 512) != 0:
+        raise ConfigError(err.value.decode())
+    return cfg
 
 
 def parse_program(text: str):

@@ -80,4 +80,50 @@ inline bool parse_ip4(const std::string &v, uint32_t &out) {
     return true;
 }
 
+// IPPrefixArg(true) (lib/ipaddress.cc:196-255): "a[.b[.c[.d]]]/len",
+// "a.b.c.d/m.m.m.m" or a bare address (mask 255.255.255.255); the mask may not
+// cover more bytes than the address gives. Raw network-order words.
+inline bool parse_ip4_prefix(const std::string &v, uint32_t &addr, uint32_t &mask) {
+    const size_t slash = v.rfind('/');
+    if (slash == std::string::npos) {
+        if (!parse_ip4(v, addr)) return false;
+        mask = 0xFFFFFFFFu;
+        return true;
+    }
+    const std::string a = v.substr(0, slash), m = v.substr(slash + 1);
+    uint8_t b[4] = {0, 0, 0, 0};
+    int nbytes = 0;
+    size_t pos = 0;
+    while (nbytes < 4) {
+        size_t e = pos;
+        unsigned val = 0;
+        while (e < a.size() && a[e] >= '0' && a[e] <= '9' && e - pos < 3) val = val * 10 + (unsigned)(a[e++] - '0');
+        if (e == pos || val > 255) return false;
+        b[nbytes++] = (uint8_t)val;
+        if (e == a.size()) { pos = e; break; }
+        if (a[e] != '.') return false;
+        pos = e + 1;
+    }
+    if (pos != a.size()) return false;
+    uint32_t mk;
+    char *end = nullptr;
+    const long l = strtol(m.c_str(), &end, 10);
+    if (!m.empty() && end && *end == 0 && l >= 0 && l <= 32) {
+        const uint32_t host = l == 0 ? 0u : 0xFFFFFFFFu << (32 - l);   // host-order prefix
+        const uint8_t mb[4] = {(uint8_t)(host >> 24), (uint8_t)(host >> 16), (uint8_t)(host >> 8), (uint8_t)host};
+        memcpy(&mk, mb, 4);
+    } else if (!parse_ip4(m, mk)) {
+        return false;
+    }
+    if (nbytes < 4) {   // the mask may not reach past the bytes given
+        uint8_t mb[4];
+        memcpy(mb, &mk, 4);
+        for (int j = nbytes; j < 4; ++j)
+            if (mb[j]) return false;
+    }
+    memcpy(&addr, b, 4);
+    mask = mk;
+    return true;
+}
+
 }  // namespace fcx

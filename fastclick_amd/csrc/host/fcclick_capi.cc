@@ -126,6 +126,26 @@ extern "C" int fcclick_check_config(const char *conf, char *err, size_t errcap) 
     return 0;
 }
 
+extern "C" int fcclick_element_cfg(const char *conf, fcgpu_cfg *cfg, char *err, size_t errcap) {
+    if (!conf || !cfg) {
+        copy_err("null argument", err, errcap);
+        return -1;
+    }
+    std::string e;
+    auto el = make_element(conf, e);
+    if (!el) {
+        copy_err(e, err, errcap);
+        return -1;
+    }
+    auto *g = dynamic_cast<GPUIPCheckClassify *>(el.get());
+    if (!g) {
+        copy_err("not a GPUIPCheckClassify", err, errcap);
+        return -1;
+    }
+    *cfg = g->device_cfg();
+    return 0;
+}
+
 extern "C" int fcclick_parse_program(const char *text, fcgpu_step *steps, uint32_t cap, uint32_t *nsteps,
                                      int32_t *output_everything, char *err, size_t errcap) {
     if (!text || !nsteps || !output_everything) {

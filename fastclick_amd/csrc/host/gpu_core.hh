@@ -32,7 +32,7 @@
 //
 // Keyword arguments mirror the replaced elements:
 //   OFFSET, CHECKSUM (default FALSE: checkipheader.cc:110), BADSRC, GOODDST,
-//   VERBOSE, DETAILS                         -- CheckIPHeader
+//   INTERFACES, VERBOSE, DETAILS             -- CheckIPHeader
 //   NATIVE_VLAN (default 0)                  -- StripEtherVLANHeader
 //   VLAN_ETHERTYPE (default 0x8100)          -- VLANDecap(ETHERTYPE) + Strip(14) (MODE AUTO)
 //   MODE MARK6                               -- MarkIP6Header(OFFSET)
@@ -113,6 +113,8 @@ class RxCore {
         fcgpu_default_cfg(&_cfg);
         _cfg.checksum = 0;
         bool strip_set = false;
+        bool have_if = false, badsrc_set = false, gooddst_set = false;
+        std::vector<uint32_t> if_bad, if_good;   // INTERFACES (raw network-order words)
         for (const auto &raw : conf) {
             ConfArg a = parse_arg(raw);
             const std::string &k = a.key, &v = a.value;
@@ -128,11 +130,30 @@ class RxCore {
                 if (!parse_bool(v, _verbose)) return err(errh, "VERBOSE expects true/false");
             } else if (k == "DETAILS") {
                 if (!parse_bool(v, _details)) return err(errh, "DETAILS expects true/false");
+            } else if (k == "INTERFACES") {
+                // CheckIPHeader::InterfacesArg (checkipheader.cc:56-80): per
+                // prefix, its broadcast address is a bad source and the address
+                // a good destination; then 0.0.0.0 and 255.255.255.255
+                std::istringstream ss(v);
+                std::string w;
+                if_bad.clear();
+                if_good.clear();
+                while (ss >> w) {
+                    uint32_t ip, mask;
+                    if (!parse_ip4_prefix(w, ip, mask)) return err(errh, "INTERFACES expects IP prefixes");
+                    if_bad.push_back((ip & mask) | ~mask);
+                    if_good.push_back(ip);
+                }
+                if_bad.push_back(0u);
+                if_bad.push_back(0xFFFFFFFFu);
+                if (if_bad.size() > FCGPU_MAX_ADDRS) return err(errh, "INTERFACES: too many addresses");
+                have_if = true;
             } else if (k == "BADSRC" || k == "GOODDST") {
                 std::istringstream ss(v);
                 std::string w;
                 uint32_t *dst = k == "BADSRC" ? _cfg.badsrc : _cfg.gooddst;
                 uint32_t &cnt = k == "BADSRC" ? _cfg.nbadsrc : _cfg.ngooddst;
+                (k == "BADSRC" ? badsrc_set : gooddst_set) = true;
                 cnt = 0;
                 while (ss >> w) {
                     uint32_t ip;
@@ -268,6 +289,16 @@ class RxCore {
                 return err(errh, "unknown keyword " + k);
             }
         }
+        // Args reads INTERFACES before BADSRC and GOODDST, which replace its
+        // lists (IPAddressArg's Vector parse swaps, lib/ipaddress.cc:174-193)
+        if (have_if && !badsrc_set) {
+            _cfg.nbadsrc = (uint32_t)if_bad.size();
+            for (size_t j = 0; j < if_bad.size(); ++j) _cfg.badsrc[j] = if_bad[j];
+        }
+        if (have_if && !gooddst_set) {
+            _cfg.ngooddst = (uint32_t)if_good.size();
+            for (size_t j = 0; j < if_good.size(); ++j) _cfg.gooddst[j] = if_good[j];
+        }
         if (!strip_set) _strip = (_cfg.check_mode == FCGPU_CHECK_AUTO);
         const bool ip4 = _cfg.check_mode == FCGPU_CHECK_IP4 || _cfg.check_mode == FCGPU_MARK_IP4;
         if (_cfg.l4_mode != FCGPU_L4_NONE && !ip4) return err(errh, "L4 needs MODE CHECK or MARK");
@@ -287,6 +318,7 @@ class RxCore {
     }
 
     int64_t timer_us() const { return _timer_us; }
+    const fcgpu_cfg &device_cfg() const { return _cfg; }
     uint32_t nports() const { return _cfg.nports; }
 
     // ---- device context and staging slots ----------------------------------

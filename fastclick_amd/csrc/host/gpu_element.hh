@@ -71,6 +71,7 @@ class GPUIPCheckClassify : public Element {
     uint32_t held() const override { return _core.held(); }
     uint32_t max_held() const override { return _core.max_held(); }
     std::string read_handler(const std::string &h) override { return _core.read_handler(h); }
+    const fcgpu_cfg &device_cfg() const { return _core.device_cfg(); }
 
   private:
     struct Emit {          // RxCore hands each output run here

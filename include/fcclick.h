@@ -23,6 +23,13 @@ extern "C" {
  * without touching a GPU. Returns 0, or -1 with the message in err. */
 int fcclick_check_config(const char *conf, char *err, size_t errcap);
 
+/* The device configuration (fcgpu_cfg) a GPUIPCheckClassify configuration
+ * string produces -- its keywords mapped as the element maps them, e.g.
+ * INTERFACES to the BADSRC / GOODDST lists -- without touching a GPU.
+ * Returns 0, or -1 with the message in err. */
+struct fcgpu_cfg;
+int fcclick_element_cfg(const char *conf, struct fcgpu_cfg *cfg, char *err, size_t errcap);
+
 /* Parse a decision program in the text form the reference's IPFilter /
  * IPClassifier / Classifier `program` read handler prints
  * (elements/standard/classification.cc:978-991, :1104-1140) into fcgpu_step

@@ -219,12 +219,15 @@ static void fuzz_keywords(Rng &rng) {
                                  "PROGRAM", "PROGRAM_KIND", "PROGRAM_JIT", "L4", "L4_CHECKSUM", "COLOR",
                                  "FLOW_CAPACITY", "FLOWID_ANNO", "FLOW_RUNS", "FLOW_MANAGER", "FLOW_TIMEOUT",
                                  "FLOW_RECYCLE_INTERVAL", "DEC_TTL", "TTL_MULTICAST", "SET_CHECKSUM", "HASH",
-                                 "STRIP", "DEVICE", "BATCH", "TIMER", "PARTITION", "BOGUS"};
+                                 "STRIP", "DEVICE", "BATCH", "TIMER", "PARTITION", "INTERFACES", "BOGUS"};
     static const char *vals[] = {"", "0", "1", "14", "-1", "65536", "4294967296", "true", "false", "yes", "0x10",
                                  "1.2.3.4", "1.2.3.4 5.6.7.8", "256.1.1.1", "hash", "hash_ip", "hash_crc", "hash_agg",
                                  "AUTO", "MARK", "MARK6", "CHECK", "UDP", "TCP", "IMP", "HMP", "TILE", "GLOBAL",
                                  "\"14 4\"", "14 4", "IPFILTER", "CLASSIFIER", "0.001", "65.536", "1e9", "x",
-                                 "\"0 12/00000000%00000000 yes->[0] no->[1]\"", "99999999999999999999"};
+                                 "\"0 12/00000000%00000000 yes->[0] no->[1]\"", "99999999999999999999",
+                                 "18.26.4.9/24 1.0.0.1/255.0.0.0", "18.26/24", "18.26.4/24", "1.2.3.4/", "/8",
+                                 "1.2.3.4/33", "1.2.3.4/255.0", "1.2.3.4 5.6.7.8 9.9.9.9 1.1.1.1 2.2.2.2 3.3.3.3 "
+                                 "4.4.4.4 5.5.5.5 6.6.6.6 7.7.7.7 8.8.8.8 9.9.9.8 1.1.1.2 1.1.1.3 1.1.1.4"};
     std::vector<std::string> conf;
     const int n = (int)(rng() % 8);
     for (int i = 0; i < n; ++i)

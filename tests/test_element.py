@@ -32,6 +32,65 @@ def test_config_errors():
             K.check_config(bad)
 
 
+def _addrs(words, n):
+    return [N.raw_addr(a) for a in words][:n]
+
+
+def test_interfaces_keyword():
+    """INTERFACES (CheckIPHeader::InterfacesArg, checkipheader.cc:56-80): each
+    prefix's broadcast address is a bad source and its address a good
+    destination, then 0.0.0.0 and 255.255.255.255; BADSRC / GOODDST, read
+    after it, replace those lists whatever the keyword order."""
+    from fastclick_amd import click as K
+    c = K.element_cfg("GPUIPCheckClassify(OFFSET 14, INTERFACES 18.26.4.9/24 1.0.0.1/255.0.0.0 10.0.0.5 "
+                      "18.26.7/24)")
+    bad = ["18.26.4.255", "1.255.255.255", "10.0.0.5", "18.26.7.255", "0.0.0.0", "255.255.255.255"]
+    good = ["18.26.4.9", "1.0.0.1", "10.0.0.5", "18.26.7.0"]
+    assert list(c.badsrc)[:c.nbadsrc] == _addrs(bad, 99)
+    assert list(c.gooddst)[:c.ngooddst] == _addrs(good, 99)
+    for conf in ("GPUIPCheckClassify(INTERFACES 18.26.4.9/24, BADSRC 192.0.2.1)",
+                 "GPUIPCheckClassify(BADSRC 192.0.2.1, INTERFACES 18.26.4.9/24)"):
+        c = K.element_cfg(conf)
+        assert list(c.badsrc)[:c.nbadsrc] == _addrs(["192.0.2.1"], 9)
+        assert list(c.gooddst)[:c.ngooddst] == _addrs(["18.26.4.9"], 9)
+    c = K.element_cfg("GPUIPCheckClassify(GOODDST 10.1.1.1, INTERFACES 18.26.4.9/24)")
+    assert list(c.badsrc)[:c.nbadsrc] == _addrs(["18.26.4.255", "0.0.0.0", "255.255.255.255"], 9)
+    assert list(c.gooddst)[:c.ngooddst] == _addrs(["10.1.1.1"], 9)
+    for bad_conf in ("GPUIPCheckClassify(INTERFACES 18.26/24)",       # mask past the bytes given
+                     "GPUIPCheckClassify(INTERFACES 18.26.4.9/33)",
+                     "GPUIPCheckClassify(INTERFACES 300.1.1.1/8)",
+                     "GPUIPCheckClassify(INTERFACES host.example/24)"):
+        with pytest.raises(K.ConfigError, match="INTERFACES"):
+            K.element_cfg(bad_conf)
+
+
+@pytest.mark.gpu
+def test_element_interfaces(oracle):
+    """INTERFACES end to end: sources on the interfaces' broadcast addresses
+    are dropped unless sent to an interface address (BAD_SADDR rule)."""
+    from fastclick_amd import click as K
+    rng = np.random.default_rng(520)
+    n = 6000
+    src = rng.integers(0, 2**32, n, dtype=np.uint64)
+    dst = rng.integers(0, 2**32, n, dtype=np.uint64)
+    cand_src = [synth.ip4(18, 26, 4, 255), synth.ip4(1, 255, 255, 255), synth.ip4(0, 0, 0, 0),
+                synth.ip4(255, 255, 255, 255)]
+    cand_dst = [synth.ip4(18, 26, 4, 9), synth.ip4(1, 0, 0, 1)]
+    pick = rng.random(n)
+    src = np.where(pick < 0.3, np.array(cand_src, np.uint64)[rng.integers(0, 4, n)], src)
+    dst = np.where(rng.random(n) < 0.3, np.array(cand_dst, np.uint64)[rng.integers(0, 2, n)], dst)
+    hdr = synth.build_headers(n, src=src, dst=dst, sport=rng.integers(0, 2**16, n, dtype=np.uint32),
+                              dport=rng.integers(0, 2**16, n, dtype=np.uint32), frame_len=60, width=64)
+    b = synth.pack(hdr, 60)
+    conf = "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4, LB_MODE hash, INTERFACES 18.26.4.9/24 1.0.0.1/8)"
+    cfg = K.element_cfg(conf)
+    e = oracle.process_batch(cfg, b)
+    assert 0 < int((e["reason"] == N.R_BAD_SADDR).sum()) < n
+    r = K.run_element(conf, b, nsinks=5)
+    assert np.array_equal(r["port"], e["port"].astype(np.uint32))
+    assert int(r["handlers"]["drops"]) == int((e["reason"] != N.R_OK).sum())
+
+
 def expected(batch, cfg, oracle):
     return oracle.process_batch(cfg, batch)
 
