@@ -117,8 +117,10 @@ def parse(argv=None):
                     help="ipclass16: 1 = the program compiled to code (fcgpu_program_jit, hiprtc, before "
                          "the warmup); 0 = the step interpreter")
     ap.add_argument("--prefault", type=int, default=1,
-                    help="1: read every rotating batch once before the warmup (page translations "
-                         "resident, GPU clocks up); 0: off")
+                    help="1: read every rotating batch before the warmup, repeatedly for at least "
+                         "--prefault-ms (page translations resident, GPU clocks up after the idle "
+                         "process start); 0: off")
+    ap.add_argument("--prefault-ms", type=float, default=250.0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -393,14 +395,22 @@ class DeviceProcessor:
 
     def warmup(self, steps):
         if self.args.prefault:
-            # touch every rotating batch once (a read-only reduction), so the
-            # timed steps meet resident page translations, as buffers a NIC
-            # keeps filling would be; the warmup steps that follow stream
-            # 72 MB each, so none of this is left in the Infinity Cache
-            for a, d in self.bufs:
-                a.max()
-                d.max()
-            self.torch.cuda.synchronize()
+            # read every rotating batch (a read-only reduction), so the timed
+            # steps meet resident page translations, as buffers a NIC keeps
+            # filling would be, and keep doing so for --prefault-ms so the
+            # GPU's clocks are up: after the idle process start (or a test
+            # run) a single pass left the first timed region up to 8 % slower
+            # in kernel time (profiles/r02_final/bench.log). The warmup steps
+            # that follow stream 72 MB each, so none of this is left in the
+            # Infinity Cache.
+            t_end = time.perf_counter() + self.args.prefault_ms * 1e-3
+            while True:
+                for a, d in self.bufs:
+                    a.max()
+                    d.max()
+                self.torch.cuda.synchronize()
+                if time.perf_counter() >= t_end:
+                    break
         warm = self._jobs(0, steps)
         self.timed = self._jobs(steps, self.args.steps)   # built before the warmup
         # creates the event pool now, and times every warmup launch: the first
