@@ -524,9 +524,12 @@ int  fcgpu_use_counters(fcgpu_ctx *ctx, uint64_t *d_counters);
 
 /* Per-kernel timing with HIP events on the launch stream (off by default).
  * fcgpu_set_timing(ctx, k): k > 0 brackets the k-th, 2k-th, ... launch of the
- * context after this call (1 = every launch) with start/stop events recorded
- * by the launch itself; the events are created by this call, not on the
- * launch path. 0 = off. (Each recorded event idles the queue for a few us,
+ * context after this call (1 = every launch) with start/stop events: the
+ * event pair of hipExtLaunchKernelGGL for a one-batch launch, two stream
+ * markers (hipEventRecord) around a fused launch of several batches (cheaper
+ * on an idle queue; the interval adds the launch's dispatch latency). A fused
+ * launch counts as its number of batches. The events are created by this
+ * call, not on the launch path. 0 = off. (Each recorded event idles the queue for a few us,
  * so sparse sampling keeps the measured region representative.)
  * fcgpu_read_timing returns, per stage (0 = fused check/hash/classify,
  * 1 = count scan, 2 = partition scatter), the summed milliseconds and launches
