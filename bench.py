@@ -632,8 +632,8 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                 "valid_fraction": round(valid / total_pkts, 4)} if args.errors else {}),
             "partition": "none" if args.no_perm else args.partition,
             "streams": max(1, args.streams),
-            "batches_per_launch": (1 if args.flow_capacity or args.partition == "global" else
-                                   max(1, min(args.fuse, 24, -(-args.steps // max(1, args.streams))))),
+            "batches_per_launch": max(1, min(args.fuse, 8 if args.flow_capacity else 24,
+                                             -(-args.steps // max(1, args.streams)))),
             "frame_bytes": fb,
             "packets_per_step_per_gpu": per_gpu,
             "packets_per_step": args.packets if args.shard == "strong" else args.packets * world,

@@ -190,6 +190,9 @@ struct fcgpu_ctx {
     bool configured = false;
     uint32_t *d_tilecnt = nullptr;
     uint32_t *d_totals = nullptr;
+    // fused whole-batch partitions: per-tile counts and totals of each batch
+    // of a launch (kMaxFuse x [FCGPU_MAX_PORTS+1][max_tiles], allocated on first use)
+    uint32_t *fuse_tilecnt = nullptr, *fuse_totals = nullptr;
     unsigned long long *d_ctr = nullptr;      // active counter vector
     unsigned long long *d_ctr_own = nullptr;  // context-owned vector
     uint4 *d_prog = nullptr;                  // decision program (FCGPU_CLS_PROGRAM)
@@ -884,6 +887,8 @@ void fcgpu_close(fcgpu_ctx *c) {
         for (auto e : c->free_ev) hipEventDestroy(e);
         hipFree(c->d_tilecnt);
         hipFree(c->d_totals);
+        hipFree(c->fuse_tilecnt);
+        hipFree(c->fuse_totals);
         hipFree(c->d_ctr_own);
         hipFree(c->d_prog);
         hipFree(c->d_crc);
@@ -1180,13 +1185,18 @@ static int out_part(const fcgpu_out *o) {
 // and each batch keeps its miss records apart (up to kMaxFuseFlow batches);
 // their new-flow passes then run in batch order after the launch.
 constexpr uint32_t kMaxFuseFlow = 8;
+constexpr uint32_t kFuseCntStride = FCGPU_MAX_PORTS + 2;   // per-batch rows of fuse_tilecnt / fuse_totals
 static bool fusable(const fcgpu_ctx *c, const fcgpu_job &j) {
-    return j.n && !c->cfg.rewrite && out_part(&j.out) != kPartGlobal;
+    // a whole-batch partition fuses with its per-batch counts in fuse_tilecnt
+    // (not with the flow table, and only with the caller's verdicts, which
+    // its scatter pass reads)
+    const bool global_ok = out_part(&j.out) != kPartGlobal || (!c->fl.slots && j.out.verdict);
+    return j.n && !c->cfg.rewrite && global_ok;
 }
 
 static bool outputs_overlap(const fcgpu_out &x, const fcgpu_out &y) {
-    const void *a[] = {x.verdict, x.hash, x.anno, x.perm, x.tile_count, x.tile_perm};
-    const void *b[] = {y.verdict, y.hash, y.anno, y.perm, y.tile_count, y.tile_perm};
+    const void *a[] = {x.verdict, x.hash, x.anno, x.perm, x.tile_count, x.tile_perm, x.port_start, x.flowid};
+    const void *b[] = {y.verdict, y.hash, y.anno, y.perm, y.tile_count, y.tile_perm, y.port_start, y.flowid};
     for (const void *p : a)
         for (const void *q : b)
             if (p && p == q) return true;
@@ -1232,6 +1242,10 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
         L.flow_stride = c->max_batch;
         L.flow_words = (uint32_t)words;
     }
+    if (part == kPartGlobal && !c->fuse_tilecnt) {
+        HIPCHK(c, hipMalloc(&c->fuse_tilecnt, sizeof(uint32_t) * (size_t)kMaxFuse * kFuseCntStride * c->max_tiles));
+        HIPCHK(c, hipMalloc(&c->fuse_totals, sizeof(uint32_t) * (size_t)kMaxFuse * kFuseCntStride));
+    }
     uint32_t tiles = 0;
     for (uint32_t k = 0; k < g; ++k) {
         const fcgpu_job &j = *grp[k];
@@ -1246,6 +1260,7 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
         J.perm = j.out.perm;
         J.tile_count = j.out.tile_count;
         J.tile_perm = tile ? j.out.tile_perm : nullptr;
+        J.tilecnt = part == kPartGlobal ? c->fuse_tilecnt + (size_t)k * kFuseCntStride * c->max_tiles : nullptr;
         J.n = j.n;
         J.tile0 = tiles;
         tiles += (j.n + kTile - 1) / kTile;
@@ -1260,6 +1275,7 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
     a.desc = L.job[0].desc;
     a.n = L.job[0].n;
     a.ntiles = (a.n + kTile - 1) / kTile;
+    if (part == kPartGlobal) a.tilecnt = L.job[0].tilecnt;
     // sampled timing counts batches: a fused launch is timed when it covers
     // a multiple of timing_every
     const uint64_t before = c->timing_seq;
@@ -1287,6 +1303,48 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
     if (timed) HIPCHK(c, hipEventRecord(ev.b, s));
     HIPCHK(c, hipGetLastError());
     if (timed) c->pending.push_back(ev);
+    if (part == kPartGlobal) {
+        // the batches' whole-batch partitions: one scan launch (block (b, j):
+        // output b of batch j) and one scatter launch over all their tiles
+        const uint32_t nb = c->cfg.nports + 1;
+        ScanMulti S{};
+        PartMulti P{};
+        uint32_t wg = 0;
+        for (uint32_t k = 0; k < g; ++k) {
+            const fcgpu_job &j = *grp[k];
+            const uint32_t nt = (j.n + kTile - 1) / kTile;
+            S.tilecnt[k] = L.job[k].tilecnt;
+            S.totals[k] = c->fuse_totals + (size_t)k * kFuseCntStride;
+            S.ntiles[k] = nt;
+            P.verdict[k] = j.out.verdict;
+            P.tileoff[k] = S.tilecnt[k];
+            P.totals[k] = S.totals[k];
+            P.perm[k] = j.out.perm;
+            P.port_start[k] = j.out.port_start;
+            P.n[k] = j.out.perm ? j.n : 0u;
+            P.ntiles[k] = nt;
+            P.wg0[k] = wg;
+            wg += j.out.perm ? nt : 1u;
+        }
+        P.g = g;
+        P.nports = c->cfg.nports;
+        EvPair e1, e2;
+        if (timed) {
+            e1.a = take_event(c); e1.b = take_event(c); e1.stage = 1; e1.batches = g;
+            e2.a = take_event(c); e2.b = take_event(c); e2.stage = 2; e2.batches = g;
+            HIPCHK(c, hipEventRecord(e1.a, s));
+        }
+        hipLaunchKernelGGL(k_scan_multi, dim3(nb, g), dim3(1024), 0, s, S);
+        HIPCHK(c, hipGetLastError());
+        if (timed) { HIPCHK(c, hipEventRecord(e1.b, s)); HIPCHK(c, hipEventRecord(e2.a, s)); }
+        hipLaunchKernelGGL(k_part_multi, dim3(wg), dim3(kTile), 0, s, P);
+        HIPCHK(c, hipGetLastError());
+        if (timed) {
+            HIPCHK(c, hipEventRecord(e2.b, s));
+            c->pending.push_back(e1);
+            c->pending.push_back(e2);
+        }
+    }
     if (flow && *(volatile uint32_t *)c->flow_hint != kHintBig) {
         // the batches' new-flow passes, in batch order, in one block
         static_assert(kMaxFuseFlow <= kMaxFusePass, "k_flow_finish_multi");

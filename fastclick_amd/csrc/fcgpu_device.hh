@@ -1066,10 +1066,12 @@ struct RxView {
     uint32_t *perm;
     uint16_t *tile_count;
     uint8_t *tile_perm;
-    uint32_t n;
+    uint32_t *tilecnt;       // kPartGlobal: [nports+1][ntiles]
+    uint32_t n, ntiles;
 };
 __device__ __forceinline__ RxView rx_view(const RxArgs &A) {
-    return RxView{A.arena, A.desc, A.verdict, A.hash, A.anno, A.perm, A.tile_count, A.tile_perm, A.n};
+    return RxView{A.arena, A.desc, A.verdict, A.hash, A.anno, A.perm, A.tile_count, A.tile_perm, A.tilecnt,
+                  A.n, A.ntiles};
 }
 
 // One 256-packet tile once its header window is in LDS: fused
@@ -1148,7 +1150,7 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, const RxView &V, const 
     const uint32_t t = threadIdx.x;
     uint32_t tot = 0;
     if (t < nbt) tot = s_cnt[0][t] + s_cnt[1][t] + s_cnt[2][t] + s_cnt[3][t];
-    if (PART == kPartGlobal && t < nb) A.tilecnt[t * A.ntiles + tile] = tot;
+    if (PART == kPartGlobal && t < nb) V.tilecnt[(size_t)t * V.ntiles + tile] = tot;
     if (PART == kPartTile) {
         if (t < nb) V.tile_count[(size_t)tile * nb + t] = (uint16_t)tot;
         // every wave scans the tile's output totals in registers (lane = output,
@@ -1208,6 +1210,7 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, const RxView &V, const 
 // batches are independent (no flow table, no whole-batch partition, no
 // in-place rewrite: the host only fuses such jobs).
 constexpr uint32_t kMaxFuse = 24;
+constexpr uint32_t kMaxFuseJobs = kMaxFuse;   // ScanMulti / PartMulti
 struct RxJob {
     const uint8_t *arena;
     const uint2 *desc;
@@ -1218,6 +1221,7 @@ struct RxJob {
     uint16_t *tile_count;
     uint8_t *tile_perm;
     uint32_t *flowid;
+    uint32_t *tilecnt;       // kPartGlobal: the batch's per-tile counts (its own scratch)
     uint32_t n, tile0;       // packets; first workgroup of the batch in the grid
 };
 struct RxLaunch {
@@ -1241,7 +1245,7 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
     RxView V = rx_view(A);
     FlowArgs FL = A.fl;
     uint32_t tile = blockIdx.x;
-    if (PART != kPartGlobal && L.njobs > 1) {   // workgroup-uniform
+    if (L.njobs > 1) {   // workgroup-uniform
         // equal batches: a division; ragged ones: a walk over the jobs' first
         // tiles (kernel-argument loads the workgroup waits for)
         uint32_t j = 0, t = 0;
@@ -1261,7 +1265,9 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
         V.perm = J.perm;
         V.tile_count = J.tile_count;
         V.tile_perm = J.tile_perm;
+        V.tilecnt = J.tilecnt;
         V.n = J.n;
+        V.ntiles = (J.n + kTile - 1) / kTile;
         tile = t;
         if (FLOW) {
             FL.miss_key += (size_t)j * L.flow_stride;
@@ -1290,9 +1296,8 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
 
 // Exclusive scan of one output's per-tile counts (in place) and its total.
 // grid = nports+1 blocks of 1024 threads.
-__global__ __launch_bounds__(1024) void k_scan(uint32_t *tilecnt, uint32_t ntiles, uint32_t *totals) {
+__device__ __forceinline__ void scan_column(uint32_t *tilecnt, uint32_t ntiles, uint32_t *totals, uint32_t b) {
     __shared__ uint32_t s_w[16];
-    const uint32_t b = blockIdx.x;
     uint32_t *col = tilecnt + (size_t)b * ntiles;
     const uint32_t per = (ntiles + 1023) / 1024;
     const uint32_t beg = threadIdx.x * per;
@@ -1327,24 +1332,37 @@ __global__ __launch_bounds__(1024) void k_scan(uint32_t *tilecnt, uint32_t ntile
     }
     if (threadIdx.x == 0) totals[b] = total;
 }
+__global__ __launch_bounds__(1024) void k_scan(uint32_t *tilecnt, uint32_t ntiles, uint32_t *totals) {
+    scan_column(tilecnt, ntiles, totals, blockIdx.x);
+}
+// The batches of a fused launch (fcgpu_process_jobs): block (b, j) scans
+// output b of batch j.
+struct ScanMulti {
+    uint32_t *tilecnt[kMaxFuseJobs];
+    uint32_t *totals[kMaxFuseJobs];
+    uint32_t ntiles[kMaxFuseJobs];
+};
+__global__ __launch_bounds__(1024) void k_scan_multi(ScanMulti M) {
+    const uint32_t j = blockIdx.y;
+    scan_column(M.tilecnt[j], M.ntiles[j], M.totals[j], blockIdx.x);
+}
 
 // Dense global stable partition (CLASSIFY_EACH_PACKET order over the whole
 // batch): perm[start[bin] + rank] = i.
-__global__ __launch_bounds__(kTile) void k_part(const uint16_t *verdict, uint32_t n, uint32_t ntiles,
-                                                uint32_t nports, const uint32_t *tileoff,
-                                                const uint32_t *totals, uint32_t *perm,
-                                                uint32_t *port_start) {
+__device__ __forceinline__ void part_tile(const uint16_t *verdict, uint32_t n, uint32_t ntiles, uint32_t nports,
+                                          const uint32_t *tileoff, const uint32_t *totals, uint32_t *perm,
+                                          uint32_t *port_start, uint32_t tile) {
     __shared__ uint32_t s_cnt[4][FCGPU_MAX_PORTS + 1];
     __shared__ uint32_t s_base[FCGPU_MAX_PORTS + 2];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t i = blockIdx.x * kTile + threadIdx.x;
+    const uint32_t i = tile * kTile + threadIdx.x;
     const uint32_t nb = nports + 1;
     if (threadIdx.x == 0) {
         uint32_t acc = 0;
         for (uint32_t b = 0; b < nb; ++b) { s_base[b] = acc; acc += totals[b]; }
         s_base[nb] = acc;
     }
-    if (blockIdx.x == 0 && port_start) {
+    if (tile == 0 && port_start) {
         __syncthreads();
         if (threadIdx.x <= nb) port_start[threadIdx.x] = s_base[threadIdx.x];
     }
@@ -1360,8 +1378,33 @@ __global__ __launch_bounds__(kTile) void k_part(const uint16_t *verdict, uint32_
     if (live) {
         uint32_t wpre = 0;
         for (uint32_t w = 0; w < wave; ++w) wpre += s_cnt[w][bin];
-        perm[s_base[bin] + tileoff[(size_t)bin * ntiles + blockIdx.x] + wpre + rank] = i;
+        perm[s_base[bin] + tileoff[(size_t)bin * ntiles + tile] + wpre + rank] = i;
     }
+}
+__global__ __launch_bounds__(kTile) void k_part(const uint16_t *verdict, uint32_t n, uint32_t ntiles,
+                                                uint32_t nports, const uint32_t *tileoff,
+                                                const uint32_t *totals, uint32_t *perm,
+                                                uint32_t *port_start) {
+    part_tile(verdict, n, ntiles, nports, tileoff, totals, perm, port_start, blockIdx.x);
+}
+// The batches of a fused launch: the grid is their partition tiles end to end
+// (a batch without perm has one workgroup, for its port_start).
+struct PartMulti {
+    const uint16_t *verdict[kMaxFuseJobs];
+    const uint32_t *tileoff[kMaxFuseJobs];
+    const uint32_t *totals[kMaxFuseJobs];
+    uint32_t *perm[kMaxFuseJobs];
+    uint32_t *port_start[kMaxFuseJobs];
+    uint32_t n[kMaxFuseJobs];        // 0 for a batch without perm
+    uint32_t ntiles[kMaxFuseJobs];   // the batch's tile count (its tileoff columns)
+    uint32_t wg0[kMaxFuseJobs];      // first workgroup of the batch
+    uint32_t g, nports;
+};
+__global__ __launch_bounds__(kTile) void k_part_multi(PartMulti M) {
+    uint32_t j = 0;
+    for (uint32_t k = 1; k < M.g; ++k) j = blockIdx.x >= M.wg0[k] ? k : j;   // workgroup-uniform
+    part_tile(M.verdict[j], M.n[j], M.ntiles[j], M.nports, M.tileoff[j], M.totals[j], M.perm[j],
+              M.port_start[j], blockIdx.x - M.wg0[j]);
 }
 
 // ---- mbuf ingress: descriptors from the mbufs themselves -------------------

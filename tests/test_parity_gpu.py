@@ -347,14 +347,17 @@ def test_process_jobs_two_streams(dev, oracle):
         ctx.close()
 
 
-@pytest.mark.parametrize("partition", [N.PART_TILE, None])
+@pytest.mark.parametrize("partition", [N.PART_TILE, N.PART_GLOBAL, None])
 def test_process_jobs_fused(dev, oracle, partition):
     """fcgpu_process_jobs fuses a stream's consecutive jobs with disjoint
     outputs into one k_rx launch (up to 24 batches, the grid their tiles end
     to end): 30 ragged batches (1 .. 30,001 packets, one empty) on one stream
     -> two fused launches; every batch gets the oracle's results, the counters
     sum over the batches. Two jobs sharing an output set are not fused: the
-    later one's results are what the set holds, as with one call per job."""
+    later one's results are what the set holds, as with one call per job.
+    PART_GLOBAL: the whole-batch partitions of a fused launch (one scan and
+    one scatter launch for all its batches); odd batches ask for port_start
+    only (one scatter workgroup each)."""
     import torch
     from fastclick_amd.device import DeviceBatch, DeviceOutputs
     cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16, badsrc=BADSRC)
@@ -368,13 +371,14 @@ def test_process_jobs_fused(dev, oracle, partition):
         batches.append(b)
     exps = [oracle.process_batch(cfg, b) for b in batches]
     tile = partition == N.PART_TILE
+    glob = partition == N.PART_GLOBAL
     ctx = N.Context(0, 40_000, cfg)
     try:
         dbs = [DeviceBatch.upload(b, device="cuda:0") for b in batches]
         outs, specs = [], []
-        for b in dbs:
-            o = DeviceOutputs(max(b.n, 1), 16, device="cuda:0", perm=tile, anno=False,
-                              partition=N.PART_TILE if tile else N.PART_GLOBAL, port_start=False)
+        for k, b in enumerate(dbs):
+            o = DeviceOutputs(max(b.n, 1), 16, device="cuda:0", perm=tile or (glob and k % 2 == 0), anno=False,
+                              partition=N.PART_TILE if tile else N.PART_GLOBAL, port_start=glob)
             outs.append(o)
             specs.append((b.arena.data_ptr(), b.desc.data_ptr(), b.n, None, o.ptrs()))
         ctx.set_timing(1)
@@ -395,6 +399,10 @@ def test_process_jobs_fused(dev, oracle, partition):
                 nt = (b.n + N.TILE - 1) // N.TILE
                 assert np.array_equal(got["tile_count"][:nt * 17], exp["tile_count"]), k
                 assert np.array_equal(got["perm_tile"][:b.n], exp["perm_tile"]), k
+            if glob:
+                assert np.array_equal(got["port_start"], exp["port_start"]), k
+                if k % 2 == 0:
+                    assert np.array_equal(got["perm"][:b.n], exp["perm"]), k
         want = sum(e["counters"].astype(np.int64) for e, b in zip(exps, batches) if b.n)
         assert np.array_equal(np.array(ctx.counters(), np.int64), want)
         # two jobs on one output set: sequential semantics (the second wins)
