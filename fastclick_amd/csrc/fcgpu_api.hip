@@ -1324,7 +1324,7 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
             P.n[k] = j.out.perm ? j.n : 0u;
             P.ntiles[k] = nt;
             P.wg0[k] = wg;
-            wg += j.out.perm ? nt : 1u;
+            wg += j.out.perm ? (nt + kPartTiles - 1) / kPartTiles : 1u;
         }
         P.g = g;
         P.nports = c->cfg.nports;

@@ -1357,9 +1357,14 @@ __device__ __forceinline__ void part_tile(const uint16_t *verdict, uint32_t n, u
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t i = tile * kTile + threadIdx.x;
     const uint32_t nb = nports + 1;
+    // the outputs' starts: the totals loaded in parallel, summed from LDS
+    // (one thread walking them in global memory waited on each load)
+    __shared__ uint32_t s_tot[FCGPU_MAX_PORTS + 1];
+    if (threadIdx.x < nb) s_tot[threadIdx.x] = totals[threadIdx.x];
+    __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t acc = 0;
-        for (uint32_t b = 0; b < nb; ++b) { s_base[b] = acc; acc += totals[b]; }
+        for (uint32_t b = 0; b < nb; ++b) { s_base[b] = acc; acc += s_tot[b]; }
         s_base[nb] = acc;
     }
     if (tile == 0 && port_start) {
@@ -1400,11 +1405,68 @@ struct PartMulti {
     uint32_t wg0[kMaxFuseJobs];      // first workgroup of the batch
     uint32_t g, nports;
 };
+// Each workgroup scatters kPartTiles consecutive tiles of its batch (one tile
+// per workgroup left the pass bound by the workgroup dispatch rate: 7 us per
+// 1M-packet batch for 6 MB of traffic), the next tile's verdicts and column
+// offsets loaded while the current one is ranked and scattered.
+constexpr uint32_t kPartTiles = 8;
 __global__ __launch_bounds__(kTile) void k_part_multi(PartMulti M) {
+    __shared__ uint32_t s_cnt[4][FCGPU_MAX_PORTS + 1];
+    __shared__ uint32_t s_base[FCGPU_MAX_PORTS + 2];
+    __shared__ uint32_t s_off[2][FCGPU_MAX_PORTS + 1];
     uint32_t j = 0;
     for (uint32_t k = 1; k < M.g; ++k) j = blockIdx.x >= M.wg0[k] ? k : j;   // workgroup-uniform
-    part_tile(M.verdict[j], M.n[j], M.ntiles[j], M.nports, M.tileoff[j], M.totals[j], M.perm[j],
-              M.port_start[j], blockIdx.x - M.wg0[j]);
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+    const uint32_t nb = M.nports + 1, n = M.n[j], ntiles = M.ntiles[j];
+    const uint32_t t0 = (blockIdx.x - M.wg0[j]) * kPartTiles;
+    const uint32_t nt = n ? ntiles : 1u;
+    const uint16_t *verdict = M.verdict[j];
+    const uint32_t *tileoff = M.tileoff[j];
+    // the outputs' starts, from the batch's totals
+    if (tid < nb) s_cnt[0][tid] = M.totals[j][tid];
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (uint32_t b = 0; b < nb; ++b) { s_base[b] = acc; acc += s_cnt[0][b]; }
+        s_base[nb] = acc;
+    }
+    __syncthreads();
+    if (t0 == 0 && M.port_start[j] && tid <= nb) M.port_start[j][tid] = s_base[tid];
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t nbits = 32 - __clz(nb - 1 | 1);
+    uint32_t v = 0xffffu, off = 0;
+    if (t0 < nt) {
+        const uint32_t i = t0 * kTile + tid;
+        if (i < n) v = verdict[i];
+        if (tid < nb && n) off = tileoff[(size_t)tid * ntiles + t0];
+    }
+    for (uint32_t u = 0; u < kPartTiles && t0 + u < nt; ++u) {
+        const uint32_t tile = t0 + u, i = tile * kTile + tid;
+        // the next tile's loads go out before this one's work
+        uint32_t vn = 0xffffu, offn = 0;
+        if (u + 1 < kPartTiles && tile + 1 < nt) {
+            const uint32_t in = i + kTile;
+            if (in < n) vn = verdict[in];
+            if (tid < nb && n) offn = tileoff[(size_t)tid * ntiles + tile + 1];
+        }
+        const bool live = i < n;
+        const uint32_t bin = live ? (v >> 8) : 0xffffffffu;
+        const uint64_t grp = match_any(bin, nbits, __ballot(live));
+        const uint32_t rank = (uint32_t)__popcll(grp & lt);
+        for (uint32_t b = lane; b < nb; b += 64) s_cnt[wave][b] = 0;
+        if (tid < nb) s_off[u & 1][tid] = off;
+        __builtin_amdgcn_wave_barrier();
+        if (live && rank == 0) s_cnt[wave][bin] = (uint32_t)__popcll(grp);
+        __syncthreads();
+        if (live) {
+            uint32_t wpre = 0;
+            for (uint32_t w = 0; w < wave; ++w) wpre += s_cnt[w][bin];
+            M.perm[j][s_base[bin] + s_off[u & 1][bin] + wpre + rank] = i;
+        }
+        __syncthreads();   // the counts are read before the next tile resets them
+        v = vn;
+        off = offn;
+    }
 }
 
 // ---- mbuf ingress: descriptors from the mbufs themselves -------------------
