@@ -8,7 +8,7 @@
 //          and (FCGPU_PART_TILE) each tile's stable partition  (grid = tiles)
 //   FCGPU_PART_GLOBAL only:
 //   k_scan per-output exclusive scan over tiles                 (grid = outputs)
-//   k_part dense stable partition scatter                       (grid = tiles)
+//   k_part_multi dense stable partition scatter  (grid = batches' tiles / 8)
 //   flow table only: the new-flow pass (fcgpu_flow.hh)
 // Queued batches of one stream share one k_rx launch (process_fused).
 //
@@ -1044,6 +1044,12 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     return FCGPU_OK;
 }
 
+// Tiles per k_part_multi workgroup: up to kPartTiles, while the grid keeps
+// ~2048 workgroups (8 per CU) to fill the machine.
+static uint32_t part_tiles_per_wg(uint32_t tiles) {
+    return std::max(1u, std::min(kPartTiles, tiles / 2048u));
+}
+
 // Argument checks shared by fcgpu_process and fcgpu_process_jobs.
 static int check_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, uint32_t n,
                          const fcgpu_out *o) {
@@ -1146,8 +1152,19 @@ static int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_d
         hipLaunchKernelGGL(k_scan, dim3(nports + 1), dim3(1024), 0, s, c->d_tilecnt, ntiles, c->d_totals);
         HIPCHK(c, hipGetLastError());
         if (timed) { hipEventRecord(ev[1].b, s); hipEventRecord(ev[2].a, s); }
-        hipLaunchKernelGGL(k_part, dim3(o->perm ? ntiles : 1), dim3(kTile), 0, s, verdict, o->perm ? n : 0u,
-                           ntiles, nports, c->d_tilecnt, c->d_totals, o->perm, o->port_start);
+        PartMulti P{};   // the scatter pass of one batch (k_part_multi with one job)
+        P.verdict[0] = verdict;
+        P.tileoff[0] = c->d_tilecnt;
+        P.totals[0] = c->d_totals;
+        P.perm[0] = o->perm;
+        P.port_start[0] = o->port_start;
+        P.n[0] = o->perm ? n : 0u;
+        P.ntiles[0] = ntiles;
+        P.wg0[0] = 0;
+        P.g = 1;
+        P.nports = nports;
+        P.tpw = part_tiles_per_wg(ntiles);
+        hipLaunchKernelGGL(k_part_multi, dim3(o->perm ? (ntiles + P.tpw - 1) / P.tpw : 1u), dim3(kTile), 0, s, P);
         HIPCHK(c, hipGetLastError());
         if (timed) hipEventRecord(ev[2].b, s);
     }
@@ -1309,7 +1326,9 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
         const uint32_t nb = c->cfg.nports + 1;
         ScanMulti S{};
         PartMulti P{};
-        uint32_t wg = 0;
+        uint32_t wg = 0, all_tiles = 0;
+        for (uint32_t k = 0; k < g; ++k) all_tiles += (grp[k]->n + kTile - 1) / kTile;
+        P.tpw = part_tiles_per_wg(all_tiles);
         for (uint32_t k = 0; k < g; ++k) {
             const fcgpu_job &j = *grp[k];
             const uint32_t nt = (j.n + kTile - 1) / kTile;
@@ -1324,7 +1343,7 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
             P.n[k] = j.out.perm ? j.n : 0u;
             P.ntiles[k] = nt;
             P.wg0[k] = wg;
-            wg += j.out.perm ? (nt + kPartTiles - 1) / kPartTiles : 1u;
+            wg += j.out.perm ? (nt + P.tpw - 1) / P.tpw : 1u;
         }
         P.g = g;
         P.nports = c->cfg.nports;

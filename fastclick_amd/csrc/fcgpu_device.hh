@@ -1347,53 +1347,10 @@ __global__ __launch_bounds__(1024) void k_scan_multi(ScanMulti M) {
     scan_column(M.tilecnt[j], M.ntiles[j], M.totals[j], blockIdx.x);
 }
 
-// Dense global stable partition (CLASSIFY_EACH_PACKET order over the whole
-// batch): perm[start[bin] + rank] = i.
-__device__ __forceinline__ void part_tile(const uint16_t *verdict, uint32_t n, uint32_t ntiles, uint32_t nports,
-                                          const uint32_t *tileoff, const uint32_t *totals, uint32_t *perm,
-                                          uint32_t *port_start, uint32_t tile) {
-    __shared__ uint32_t s_cnt[4][FCGPU_MAX_PORTS + 1];
-    __shared__ uint32_t s_base[FCGPU_MAX_PORTS + 2];
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t i = tile * kTile + threadIdx.x;
-    const uint32_t nb = nports + 1;
-    // the outputs' starts: the totals loaded in parallel, summed from LDS
-    // (one thread walking them in global memory waited on each load)
-    __shared__ uint32_t s_tot[FCGPU_MAX_PORTS + 1];
-    if (threadIdx.x < nb) s_tot[threadIdx.x] = totals[threadIdx.x];
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (uint32_t b = 0; b < nb; ++b) { s_base[b] = acc; acc += s_tot[b]; }
-        s_base[nb] = acc;
-    }
-    if (tile == 0 && port_start) {
-        __syncthreads();
-        if (threadIdx.x <= nb) port_start[threadIdx.x] = s_base[threadIdx.x];
-    }
-    const bool live = i < n;
-    const uint32_t bin = live ? (uint32_t)(verdict[i] >> 8) : 0xffffffffu;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    const uint64_t grp = match_any(bin, 32 - __clz(nb - 1 | 1), __ballot(live));
-    const uint32_t rank = (uint32_t)__popcll(grp & lt);
-    for (uint32_t b = lane; b < nb; b += 64) s_cnt[wave][b] = 0;
-    __builtin_amdgcn_wave_barrier();
-    if (live && rank == 0) s_cnt[wave][bin] = (uint32_t)__popcll(grp);
-    __syncthreads();
-    if (live) {
-        uint32_t wpre = 0;
-        for (uint32_t w = 0; w < wave; ++w) wpre += s_cnt[w][bin];
-        perm[s_base[bin] + tileoff[(size_t)bin * ntiles + tile] + wpre + rank] = i;
-    }
-}
-__global__ __launch_bounds__(kTile) void k_part(const uint16_t *verdict, uint32_t n, uint32_t ntiles,
-                                                uint32_t nports, const uint32_t *tileoff,
-                                                const uint32_t *totals, uint32_t *perm,
-                                                uint32_t *port_start) {
-    part_tile(verdict, n, ntiles, nports, tileoff, totals, perm, port_start, blockIdx.x);
-}
-// The batches of a fused launch: the grid is their partition tiles end to end
-// (a batch without perm has one workgroup, for its port_start).
+// The scatter pass of the dense whole-batch partition (CLASSIFY_EACH_PACKET
+// order over each batch): perm[start[bin] + tile offset + rank] = i, for one
+// batch or the batches of a fused launch; the grid is their tile groups end to
+// end (a batch without perm has one workgroup, for its port_start).
 struct PartMulti {
     const uint16_t *verdict[kMaxFuseJobs];
     const uint32_t *tileoff[kMaxFuseJobs];
@@ -1404,11 +1361,13 @@ struct PartMulti {
     uint32_t ntiles[kMaxFuseJobs];   // the batch's tile count (its tileoff columns)
     uint32_t wg0[kMaxFuseJobs];      // first workgroup of the batch
     uint32_t g, nports;
+    uint32_t tpw;                    // tiles per workgroup (1..kPartTiles)
 };
-// Each workgroup scatters kPartTiles consecutive tiles of its batch (one tile
-// per workgroup left the pass bound by the workgroup dispatch rate: 7 us per
-// 1M-packet batch for 6 MB of traffic), the next tile's verdicts and column
-// offsets loaded while the current one is ranked and scattered.
+// Each workgroup scatters tpw consecutive tiles of its batch (one tile per
+// workgroup left the pass bound by the workgroup dispatch rate: 7 us per
+// 1M-packet batch for 6 MB of traffic; the host picks tpw so the grid still
+// fills the machine), the next tile's verdicts and column offsets loaded while
+// the current one is ranked and scattered.
 constexpr uint32_t kPartTiles = 8;
 __global__ __launch_bounds__(kTile) void k_part_multi(PartMulti M) {
     __shared__ uint32_t s_cnt[4][FCGPU_MAX_PORTS + 1];
@@ -1418,7 +1377,7 @@ __global__ __launch_bounds__(kTile) void k_part_multi(PartMulti M) {
     for (uint32_t k = 1; k < M.g; ++k) j = blockIdx.x >= M.wg0[k] ? k : j;   // workgroup-uniform
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
     const uint32_t nb = M.nports + 1, n = M.n[j], ntiles = M.ntiles[j];
-    const uint32_t t0 = (blockIdx.x - M.wg0[j]) * kPartTiles;
+    const uint32_t t0 = (blockIdx.x - M.wg0[j]) * M.tpw;
     const uint32_t nt = n ? ntiles : 1u;
     const uint16_t *verdict = M.verdict[j];
     const uint32_t *tileoff = M.tileoff[j];
@@ -1440,11 +1399,11 @@ __global__ __launch_bounds__(kTile) void k_part_multi(PartMulti M) {
         if (i < n) v = verdict[i];
         if (tid < nb && n) off = tileoff[(size_t)tid * ntiles + t0];
     }
-    for (uint32_t u = 0; u < kPartTiles && t0 + u < nt; ++u) {
+    for (uint32_t u = 0; u < M.tpw && t0 + u < nt; ++u) {
         const uint32_t tile = t0 + u, i = tile * kTile + tid;
         // the next tile's loads go out before this one's work
         uint32_t vn = 0xffffu, offn = 0;
-        if (u + 1 < kPartTiles && tile + 1 < nt) {
+        if (u + 1 < M.tpw && tile + 1 < nt) {
             const uint32_t in = i + kTile;
             if (in < n) vn = verdict[in];
             if (tid < nb && n) offn = tileoff[(size_t)tid * ntiles + tile + 1];
