@@ -18,7 +18,7 @@ run() {  # name env... -- args...
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
 for k in ${AB_RUNS:-1 2 3}; do
   run base$k --
-  run evm1_$k FCGPU_EVT_MODE=1 --
+  run kdev0_$k HIP_FORCE_DEV_KERNARG=0 --
   run notime$k -- --no-timing
 done
 exit 0
