@@ -347,6 +347,37 @@ def test_process_jobs_two_streams(dev, oracle):
         ctx.close()
 
 
+def test_process_jobs_fused_global_large(dev, oracle):
+    """Fused whole-batch partitions large enough that each scatter workgroup
+    takes several tiles (5 ragged batches, 4.5M packets: 8 tiles per
+    workgroup), against the oracle's permutation and port starts."""
+    import torch
+    from fastclick_amd.device import DeviceBatch, DeviceOutputs
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16, badsrc=BADSRC)
+    sizes = [900_000, 899_937, 900_001, 913_131, 887_777]
+    ctx = N.Context(0, max(sizes), cfg)
+    try:
+        specs, keep = [], []
+        for k, n in enumerate(sizes):
+            b = synth.c4(n, seed=700 + k)
+            synth.inject_errors(b, 0.01, seed=710 + k)
+            db = DeviceBatch.upload(b, device="cuda:0")
+            o = DeviceOutputs(n, 16, device="cuda:0", perm=True, anno=False, partition=N.PART_GLOBAL,
+                              port_start=True)
+            keep.append((b, db, o))
+            specs.append((db.arena.data_ptr(), db.desc.data_ptr(), n, None, o.ptrs()))
+        ctx.run_jobs(ctx.jobs(specs))
+        torch.cuda.synchronize()
+        for k, (b, db, o) in enumerate(keep):
+            exp = oracle.process_batch(cfg, b)
+            got = o.numpy()
+            assert np.array_equal(got["port"][:b.n], exp["port"]), k
+            assert np.array_equal(got["port_start"], exp["port_start"]), k
+            assert np.array_equal(got["perm"][:b.n], exp["perm"]), k
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("partition", [N.PART_TILE, N.PART_GLOBAL, None])
 def test_process_jobs_fused(dev, oracle, partition):
     """fcgpu_process_jobs fuses a stream's consecutive jobs with disjoint
