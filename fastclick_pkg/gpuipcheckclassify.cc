@@ -196,3 +196,4 @@ CLICK_ENDDECLS
 ELEMENT_REQUIRES(batch)
 ELEMENT_LIBS(-lfcgpu)
 EXPORT_ELEMENT(GPUIPCheckClassify)
+ELEMENT_MT_SAFE(GPUIPCheckClassify)
