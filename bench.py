@@ -113,6 +113,13 @@ def parse(argv=None):
                          "(CRC32-C of the IPFlow5ID, DPDK builds); ipclass16: the survey's "
                          "IPClassifier with 15 UDP dst-port ranges + '-' (program printed by the "
                          "reference compiler, tests/golden/reftests.json)")
+    ap.add_argument("--l4", choices=["none", "udp", "tcp"], default="none",
+                    help="CheckUDPHeader / CheckTCPHeader behind the IPv4 check (pseudo-header checksum "
+                         "over the whole segment; the synthetic frames are UDP, so tcp sends them all to "
+                         "the drop output)")
+    ap.add_argument("--rewrite", action="store_true",
+                    help="DecIPTTL + SetIPChecksum behind the classifier; the rewritten header bytes go "
+                         "to an ip_rw output per batch (not in place: the rotating batches are reused)")
     ap.add_argument("--program-jit", type=int, default=1,
                     help="ipclass16: 1 = the program compiled to code (fcgpu_program_jit, hiprtc, before "
                          "the warmup); 0 = the step interpreter")
@@ -133,6 +140,8 @@ def parse(argv=None):
         ap.error("--errors applies to 64-B c2/c4, with a rate in (0, 0.2]")
     if not 64 <= a.frame_bytes <= 1518:
         ap.error("--frame-bytes must be in [64, 1518]")
+    if (a.l4 != "none" or a.rewrite) and a.workload == "c5":
+        ap.error("--l4 / --rewrite need an IPv4 workload (c2, c3, c4)")
     if a.flow_capacity and a.streams > 1:
         # one table per context, IDs in batch order: a second stream would
         # either race on the table's scratch or need a second table
@@ -355,7 +364,9 @@ class DeviceProcessor:
                     N.CLS_LB_CRC if args.classify == "lbcrc" else N.CLS_LB_HASH)
         cfg = N.make_cfg(check_mode=N.CHECK_AUTO if self.auto else N.CHECK_IP4, offset=0 if self.auto else 14,
                          checksum=True, hash_mode=N.HASH_FLOWID, classify=classify, nports=args.nports,
-                         badsrc=[N.raw_addr(a) for a in ERROR_BADSRC] if args.errors else ())
+                         badsrc=[N.raw_addr(a) for a in ERROR_BADSRC] if args.errors else (),
+                         l4_mode=dict(none=N.L4_NONE, udp=N.L4_UDP, tcp=N.L4_TCP)[args.l4],
+                         rewrite=(N.RW_DECTTL | N.RW_SETCKSUM) if args.rewrite else 0)
         part = N.PART_TILE if args.partition == "tile" else N.PART_GLOBAL
         tile = part == N.PART_TILE
         self.ctx = N.Context(gpu, max(n, 1), cfg)
@@ -378,7 +389,7 @@ class DeviceProcessor:
         self.outs = [DeviceOutputs(max(n, 1), args.nports, device=dev, verdict=True, hash=True, anno=False,
                                    perm=(not args.no_perm) and not tile,
                                    tile_perm=(not args.no_perm) and tile, port_start=not args.no_perm,
-                                   partition=part, flowid=args.flow_capacity > 0)
+                                   partition=part, flowid=args.flow_capacity > 0, ip_rw=args.rewrite)
                      for _ in range(nsets)]
         self.ctr = torch.zeros(N.CTR_SHARDS, N.NCOUNTERS, dtype=torch.int64, device=dev)
         self.timing_every = 0 if args.no_timing else (args.timing_every or min(8, max(1, args.steps)))
@@ -613,6 +624,7 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                             if auto else "; CheckIPHeader(CHECKSUM true)")
                          + (f" (with-errors mix: {args.errors:g} each of bad version, header length, "
                             f"ip_len, checksum, BADSRC)" if args.errors else "")
+                         + (f" + Check{args.l4.upper()}Header" if args.l4 != "none" else "")
                          + ((f" + FlowIPManagerHMP flow table ({args.flow_capacity} IDs)"
                              if args.flow_manager == "hmp" else
                              f" + VirtualFlowManagerIMP flow table (CAPACITY {args.flow_capacity}, "
@@ -625,7 +637,8 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                          + ("" if args.no_perm else
                             " + stable per-port partition of every 256-packet PacketBatch"
                             if args.partition == "tile" else
-                            " + stable per-port partition of the whole batch")),
+                            " + stable per-port partition of the whole batch")
+                         + (" + DecIPTTL + SetIPChecksum (rewritten bytes to ip_rw)" if args.rewrite else "")),
             "classify": args.classify + (" (compiled program)" if args.classify == "ipclass16" and args.program_jit
                                          else " (interpreted program)" if args.classify == "ipclass16" else ""),
             **({"errors_per_kind": args.errors,

@@ -1208,12 +1208,16 @@ static bool fusable(const fcgpu_ctx *c, const fcgpu_job &j) {
     // (not with the flow table, and only with the caller's verdicts, which
     // its scatter pass reads)
     const bool global_ok = out_part(&j.out) != kPartGlobal || (!c->fl.slots && j.out.verdict);
-    return j.n && !c->cfg.rewrite && global_ok;
+    // header rewrites into the arena do not fuse (jobs may share an arena);
+    // rewrites reported through ip_rw do
+    return j.n && !(c->cfg.rewrite & FCGPU_RW_INPLACE) && global_ok;
 }
 
 static bool outputs_overlap(const fcgpu_out &x, const fcgpu_out &y) {
-    const void *a[] = {x.verdict, x.hash, x.anno, x.perm, x.tile_count, x.tile_perm, x.port_start, x.flowid};
-    const void *b[] = {y.verdict, y.hash, y.anno, y.perm, y.tile_count, y.tile_perm, y.port_start, y.flowid};
+    const void *a[] = {x.verdict, x.hash, x.anno, x.perm, x.tile_count, x.tile_perm, x.port_start, x.flowid,
+                       x.ip_rw};
+    const void *b[] = {y.verdict, y.hash, y.anno, y.perm, y.tile_count, y.tile_perm, y.port_start, y.flowid,
+                       y.ip_rw};
     for (const void *p : a)
         for (const void *q : b)
             if (p && p == q) return true;
@@ -1278,6 +1282,7 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
         J.tile_count = j.out.tile_count;
         J.tile_perm = tile ? j.out.tile_perm : nullptr;
         J.tilecnt = part == kPartGlobal ? c->fuse_tilecnt + (size_t)k * kFuseCntStride * c->max_tiles : nullptr;
+        J.ip_rw = j.out.ip_rw;
         J.n = j.n;
         J.tile0 = tiles;
         tiles += (j.n + kTile - 1) / kTile;

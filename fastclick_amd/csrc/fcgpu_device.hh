@@ -1004,15 +1004,17 @@ __device__ __forceinline__ void flow_resolve(const FlowArgs &F, FlowProbe &q, bo
 // click_in_cksum of the header with ip_sum = 0; kills a packet whose header
 // does not fit (only reachable in MARK mode). The packet's IP header bytes
 // 8..11 after the rewrites go to ip_rw (and the arena with FCGPU_RW_INPLACE).
-__device__ __forceinline__ void rw_stage(const DevCfg &c, const FrameView &f, uint8_t *frame, bool live,
-                                         PktResult &r, uint32_t *ip_rw, uint32_t i) {
+template <bool WIN>
+__device__ __forceinline__ void rw_stage_t(const DevCfg &c, const FrameView &f, uint8_t *frame, bool live,
+                                           PktResult &r, uint32_t *ip_rw, uint32_t i) {
+    auto rd = [&](uint32_t b) { return WIN ? f.rd32_win(b) : f.rd32(b); };
     uint32_t w = 0;
     bool changed = false;
     if (live && r.reason == FCGPU_R_OK && r.an.ipver == 4) {
         const uint32_t nh = r.an.nh;
-        w = f.rd32(nh + 8);                         // ttl, proto, sum (network order)
+        w = rd(nh + 8);                         // ttl, proto, sum (network order)
         if (c.rewrite & FCGPU_RW_DECTTL) {
-            const bool mcast = (f.rd8(nh + 16) & 0xf0u) == 0xe0u;   // IPAddress::is_multicast
+            const bool mcast = (rd(nh + 16) & 0xf0u) == 0xe0u;   // IPAddress::is_multicast
             if (c.ttl_multicast || !mcast) {
                 const uint32_t ttl = w & 0xffu;
                 if (ttl <= 1) {
@@ -1028,13 +1030,13 @@ __device__ __forceinline__ void rw_stage(const DevCfg &c, const FrameView &f, ui
             }
         }
         if ((c.rewrite & FCGPU_RW_SETCKSUM) && r.reason == FCGPU_R_OK) {
-            const uint32_t plen = (uint32_t)r.an.length - nh, hl = (f.rd8(nh) & 15u) << 2;
+            const uint32_t plen = (uint32_t)r.an.length - nh, hl = (rd(nh) & 15u) << 2;
             if (plen < 20 || hl < 20 || hl > plen) {
                 r.reason = FCGPU_R_SETCKSUM_BAD;
                 r.port = c.nports;
             } else {
-                uint64_t s = (uint64_t)f.rd32(nh) + f.rd32(nh + 4) + (w & 0xffffu);
-                for (uint32_t j = 12; j < hl; j += 4) s += f.rd32(nh + j);
+                uint64_t s = (uint64_t)rd(nh) + rd(nh + 4) + (w & 0xffffu);
+                for (uint32_t j = 12; j < hl; j += 4) s += rd(nh + j);
                 s = (s & 0xffffffffu) + (s >> 32);
                 s = (s & 0xffffffffu) + (s >> 32);
                 uint32_t t = (uint32_t)s;
@@ -1054,6 +1056,24 @@ __device__ __forceinline__ void rw_stage(const DevCfg &c, const FrameView &f, ui
     }
     if (live && ip_rw) ip_rw[i] = changed ? w : 0u;
 }
+// The header reads from the LDS window when every rewriting lane of the wave
+// has its IP header there (the general reads compile to flat loads that wait
+// on the vector-memory path).
+__device__ __forceinline__ void rw_stage(const DevCfg &c, const FrameView &f, uint8_t *frame, bool live,
+                                         PktResult &r, uint32_t *ip_rw, uint32_t i) {
+    const bool elig = live && r.reason == FCGPU_R_OK && r.an.ipver == 4;
+    bool inw = true;
+    if (elig) {
+        const uint32_t x = r.an.nh + f.shift;
+        inw = x + 8 <= (uint32_t)kWin;
+        if (inw) {
+            const uint32_t hl = (f.rd32_win(r.an.nh) & 15u) << 2;
+            inw = x + (hl > 20u ? hl : 20u) + 4 <= (uint32_t)kWin;
+        }
+    }
+    if (!__ballot(elig && !inw)) rw_stage_t<true>(c, f, frame, live, r, ip_rw, i);
+    else rw_stage_t<false>(c, f, frame, live, r, ip_rw, i);
+}
 
 // The batch a workgroup works on: RxArgs' per-batch pointers, or (fused
 // launch) its job's. Plain scalars, so they stay in SGPRs.
@@ -1067,11 +1087,12 @@ struct RxView {
     uint16_t *tile_count;
     uint8_t *tile_perm;
     uint32_t *tilecnt;       // kPartGlobal: [nports+1][ntiles]
+    uint32_t *ip_rw;         // cfg.rewrite: the rewritten header bytes
     uint32_t n, ntiles;
 };
 __device__ __forceinline__ RxView rx_view(const RxArgs &A) {
     return RxView{A.arena, A.desc, A.verdict, A.hash, A.anno, A.perm, A.tile_count, A.tile_perm, A.tilecnt,
-                  A.n, A.ntiles};
+                  A.ip_rw, A.n, A.ntiles};
 }
 
 // One 256-packet tile once its header window is in LDS: fused
@@ -1120,7 +1141,7 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, const RxView &V, const 
     FlowProbe fq;
     if (FLOW) fq = flow_issue(FL, f, live, r);
     if (A.cfg.rewrite)   // launch-uniform
-        rw_stage(A.cfg, f, const_cast<uint8_t *>(V.arena) + d.x, live, r, A.ip_rw, i);
+        rw_stage(A.cfg, f, const_cast<uint8_t *>(V.arena) + d.x, live, r, V.ip_rw, i);
     if (live) {
         if (V.verdict) V.verdict[i] = (uint16_t)(r.reason | (r.port << 8));
         if (V.hash) V.hash[i] = r.hash;
@@ -1207,8 +1228,8 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, const RxView &V, const 
 // RxLaunch::njobs > 1): the grid is the batches' tiles end to end and each
 // workgroup takes its batch's pointers from the launch arguments. A queue of
 // batches then pays one launch ramp and tail instead of one per batch; the
-// batches are independent (no flow table, no whole-batch partition, no
-// in-place rewrite: the host only fuses such jobs).
+// batches are independent (no in-place rewrite: jobs may share an arena;
+// the flow table and the whole-batch partition keep per-batch scratch).
 constexpr uint32_t kMaxFuse = 24;
 constexpr uint32_t kMaxFuseJobs = kMaxFuse;   // ScanMulti / PartMulti
 struct RxJob {
@@ -1222,6 +1243,7 @@ struct RxJob {
     uint8_t *tile_perm;
     uint32_t *flowid;
     uint32_t *tilecnt;       // kPartGlobal: the batch's per-tile counts (its own scratch)
+    uint32_t *ip_rw;         // cfg.rewrite (not in place): the batch's rewritten header bytes
     uint32_t n, tile0;       // packets; first workgroup of the batch in the grid
 };
 struct RxLaunch {
@@ -1266,6 +1288,7 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
         V.tile_count = J.tile_count;
         V.tile_perm = J.tile_perm;
         V.tilecnt = J.tilecnt;
+        V.ip_rw = J.ip_rw;
         V.n = J.n;
         V.ntiles = (J.n + kTile - 1) / kTile;
         tile = t;

@@ -259,8 +259,11 @@ int  fcgpu_process(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_des
  * before the first is launched.
  * Consecutive jobs of one stream whose outputs do not overlap share one
  * receive-kernel launch (up to 24 batches: the grid is their tiles end to
- * end), unless the context has a flow table or header rewrites or a job asks
- * for a whole-batch partition; results are the same as one launch per job.
+ * end; 8 with a flow table, whose new-flow passes follow in batch order; a
+ * whole-batch partition adds one scan and one scatter launch for them all),
+ * unless the context rewrites headers in place (FCGPU_RW_INPLACE: jobs may
+ * share an arena) or a whole-batch partition comes without the caller's
+ * verdicts or with a flow table; results are the same as one launch per job.
  * Sampled timing (fcgpu_set_timing) then counts batches: a fused launch is
  * timed when it covers a multiple of `every`, and fcgpu_read_timing reports
  * its batches as launches (time per batch = ms / launches). */

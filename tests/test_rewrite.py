@@ -133,3 +133,44 @@ def test_gpu_rewrite_inplace():
     assert np.array_equal(after[changed], res["ip_rw"][changed])
     assert np.array_equal(after[changed], g["decset"][changed])
     assert np.array_equal(after[~changed], orig_bytes(b)[~changed])
+
+
+@pytest.mark.gpu
+def test_gpu_rewrite_fused_jobs(oracle):
+    """Rewrites reported through ip_rw (not in place) fuse across queued
+    batches (fcgpu_process_jobs): each batch's ip_rw, verdicts and tile
+    partition match the oracle; batches with TTL 0/1/2 packets and IP options."""
+    import torch
+    from fastclick_amd.device import DeviceBatch, DeviceOutputs
+    cfg = N.make_cfg(offset=14, checksum=True, rewrite=N.RW_DECTTL | N.RW_SETCKSUM, classify=N.CLS_LB_HASH,
+                     nports=8)
+    rng = np.random.default_rng(64)
+    batches = []
+    for k, n in enumerate([3000, 257, 40_000, 12_345, 1]):
+        b = synth.c4(n, seed=640 + k)
+        synth.add_ip_options(b, 0.1, seed=650 + k)
+        for i in np.nonzero(rng.random(b.n) < 0.2)[0]:
+            o = int(b.desc[i, 0]) + 14
+            b.arena[o + 8] = int(rng.integers(0, 3))
+            synth._refresh_cksum(b.arena, o)
+        batches.append(b)
+    ctx = N.Context(0, 40_000, cfg)
+    try:
+        dbs = [DeviceBatch.upload(b, device="cuda:0") for b in batches]
+        outs = [DeviceOutputs(b.n, 8, device="cuda:0", perm=True, anno=False, partition=N.PART_TILE,
+                              ip_rw=True) for b in batches]
+        ctx.set_timing(1)
+        ctx.run_jobs(ctx.jobs([(db.arena.data_ptr(), db.desc.data_ptr(), db.n, None, o.ptrs())
+                               for db, o in zip(dbs, outs)]))
+        torch.cuda.synchronize()
+        _, cnt = ctx.read_timing()
+        assert cnt[0] == len(batches)
+        for k, (b, o) in enumerate(zip(batches, outs)):
+            got, exp = o.numpy(), oracle.process_batch(cfg, b)
+            for key in ("reason", "port", "ip_rw"):
+                assert np.array_equal(got[key][:b.n], exp[key]), (k, key)
+            nt = (b.n + N.TILE - 1) // N.TILE
+            assert np.array_equal(got["perm_tile"][:b.n], exp["perm_tile"]), k
+            assert np.array_equal(got["tile_count"][:nt * 9], exp["tile_count"]), k
+    finally:
+        ctx.close()
