@@ -8,9 +8,10 @@ step = one pass of the hot path over one batch:
     -> FlowSwitch LB_MODE hash over 16 outputs -> stable per-port partition
 
 i.e. k_rx of libfcgpu.so (plus k_scan + k_part with --partition global).
-Steps rotate over --nbuf distinct batches placed in different HBM regions
-(default 16 x 72 MB of touched bytes = 1.15 GB > the 256 MB Infinity Cache),
-so every step reads its packets from HBM. The timed steps are submitted by
+Steps rotate over --nbuf distinct copies of the rank's batch placed in
+different HBM regions (default: >= 1.15 GB of touched bytes per GPU, e.g.
+16 x 72 MB at 1M 64-B packets, > 4x the 256 MB Infinity Cache), so every step
+reads its packets from HBM. The timed steps are submitted by
 one fcgpu_process_jobs call (no per-step Python on the launch path), each
 with its own output buffers, on one stream (--streams: more streams, as rx
 queues would); the library fuses a stream's queued batches into k_rx
@@ -23,7 +24,9 @@ every rank processes its own 1M-packet batches (scaling "weak", no data-path
 collective). --shard strong (configs[3], C4): one 1M-packet batch per step is
 split over the ranks with dist.shard_range (131,072 packets per GPU at N=8;
 every shard is a whole number of 256-packet PacketBatches, so no per-step
-exchange is needed either). After the timed region the per-port / per-reason
+exchange is needed either); each rank uploads only its shard's frames
+(shard_arrays) and rotates over enough copies of them to stay beyond the
+Infinity Cache (122 x 9.4 MB of frames + descriptors at N=8). After the timed region the per-port / per-reason
 counters are all-reduced over RCCL (the reference sums per-thread counters on
 read, include/click/sync.hh:384) and the per-output offsets all-gathered
 (dist.output_offsets); both are checked.
@@ -59,9 +62,10 @@ def parse(argv=None):
                     help="packets per step per GPU (weak) or per step in total (strong)")
     ap.add_argument("--shard", choices=["weak", "strong"], default="weak")
     ap.add_argument("--nbuf", type=int, default=0,
-                    help="distinct HBM copies of the batch the steps rotate over; 0 (default): enough "
-                         "for >= 1.15 GB of arenas, at least 4 and at most 16 (16 x 72 MB for 64-B "
-                         "frames; 4 x 420 MB for IMIX) -- beyond the 256 MB Infinity Cache either way")
+                    help="distinct HBM copies of this rank's batch (its shard with --shard strong) the "
+                         "steps rotate over; 0 (default): enough for >= 1.15 GB of touched bytes per GPU, "
+                         "at least 4 (16 x 72 MB for 1M 64-B frames, 122 x 9.4 MB for a 1/8 strong shard, "
+                         "4 x 420 MB for IMIX) -- beyond the 256 MB Infinity Cache at every N")
     ap.add_argument("--nports", type=int, default=16)
     ap.add_argument("--no-perm", action="store_true", help="skip the partition")
     ap.add_argument("--partition", choices=["tile", "global"], default="tile",
@@ -327,9 +331,61 @@ def _make_host_batch(args):
     return dict(c2=synth.c2, c3=synth.c3, c4=synth.c4, c5=synth.c5)[args.workload](n)
 
 
+ROTATION_BYTES = 1_150_000_000   # > 4 x the 256 MB Infinity Cache of one MI355X
+
+
+def shard_arrays(host, lo, hi, pad=256):
+    """The frames of desc[lo:hi] alone: (arena, desc) with the descriptors
+    rebased onto an arena that holds only this rank's bytes (plus `pad`
+    zero bytes, the header-window over-read include/fastclick_gpu.h allows).
+
+    The slice keeps every frame's offset modulo 256, so the shard's frames sit
+    in 128-B lines exactly as they did in the whole batch (two 64-B slots per
+    line for C2/C4). synth lays frames out in index order, so desc[lo:hi]'s
+    bytes are one contiguous range; the whole batch is returned as is."""
+    import numpy as np
+    desc = np.ascontiguousarray(host.desc[lo:hi])
+    if lo == 0 and hi == host.n:
+        return host.arena, desc
+    if hi <= lo:
+        return np.zeros(pad, np.uint8), desc.reshape(0, 2)
+    off = desc[:, 0].astype(np.int64)
+    end = int((off + desc[:, 1].astype(np.int64)).max()) + pad
+    base = int(off.min()) & ~255
+    arena = np.zeros(end - base, np.uint8)
+    src = host.arena[base:min(end, host.arena.size)]
+    arena[:src.size] = src
+    desc = desc.copy()
+    desc[:, 0] -= np.uint32(base)
+    return arena, desc
+
+
+def rotation_nbuf(touched: int, nbuf: int = 0) -> int:
+    """Distinct HBM copies of a rank's batch the steps rotate over: --nbuf, or
+    enough that the rotation (copies x the bytes one step touches: arena +
+    descriptors) is >= ROTATION_BYTES, and at least 4. Sized from the rank's
+    own shard, so a strong shard of 1/N of the batch gets N times the copies
+    (122 x 9.4 MB at N = 8) and every point of the curve reads HBM."""
+    if nbuf:
+        return nbuf
+    return max(4, -(-ROTATION_BYTES // max(int(touched), 1)))
+
+
+def check_devices(world: int, ndev: int, backend: str) -> None:
+    """One process per GPU: RCCL cannot run two ranks of one communicator on
+    one device, so an nccl world larger than the visible devices fails here,
+    at startup, instead of hanging inside the first collective."""
+    if ndev == 0:
+        raise SystemExit("bench.py: no HIP device visible")
+    if backend == "nccl" and world > ndev:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} ranks but {ndev} visible GPU(s): the nccl backend "
+                         "needs one GPU per rank (--backend gloo only rehearses several ranks on one GPU)")
+
+
 class DeviceProcessor:
-    """The hot path on this rank's GPU: nbuf HBM-resident copies of the
-    batch, one context, --streams output sets; steps submitted through
+    """The hot path on this rank's GPU: nbuf HBM-resident copies of this
+    rank's shard of the batch (one allocation, rows 4 KB aligned), one
+    context, --streams output sets; steps submitted through
     fcgpu_process_jobs."""
 
     def __init__(self, args, lo, hi, gpu):
@@ -345,14 +401,21 @@ class DeviceProcessor:
                                captured=int(host.desc[0, 1]))
         n = hi - lo
         self.n = n
-        arena = torch.from_numpy(np.ascontiguousarray(host.arena)).to(dev)
-        desc = torch.from_numpy(np.ascontiguousarray(host.desc[lo:hi]).view(np.int32)).to(dev)
+        arena_np, desc_np = shard_arrays(host, lo, hi)
         del host
-        # nbuf copies at distinct HBM addresses (device-side copies)
-        if not args.nbuf:
-            touched = int(arena.numel())
-            args.nbuf = max(4, min(16, -(-1_150_000_000 // max(touched, 1))))
-        self.bufs = [(arena, desc)] + [(arena.clone(), desc.clone()) for _ in range(args.nbuf - 1)]
+        touched = arena_np.nbytes + desc_np.nbytes
+        args.nbuf = rotation_nbuf(touched, args.nbuf)
+        self.rotation_bytes = args.nbuf * touched
+        # nbuf copies at distinct HBM addresses, filled by device-side copies
+        stride = -(-arena_np.size // 4096) * 4096
+        arena = torch.from_numpy(arena_np).to(dev)
+        desc = torch.from_numpy(desc_np.view(np.int32)).to(dev)
+        self.arena_all = torch.empty((args.nbuf, stride), dtype=torch.uint8, device=dev)
+        self.desc_all = torch.empty((args.nbuf,) + tuple(desc.shape), dtype=torch.int32, device=dev)
+        self.arena_all[:, :arena.numel()].copy_(arena.expand(args.nbuf, -1))
+        self.desc_all.copy_(desc.expand(args.nbuf, *desc.shape))
+        del arena, desc
+        self.bufs = [(self.arena_all[k], self.desc_all[k]) for k in range(args.nbuf)]
         program = None
         if args.classify == "ipclass16":
             from fastclick_amd import click
@@ -416,9 +479,8 @@ class DeviceProcessor:
             # Infinity Cache.
             t_end = time.perf_counter() + self.args.prefault_ms * 1e-3
             while True:
-                for a, d in self.bufs:
-                    a.max()
-                    d.max()
+                self.arena_all.max()
+                self.desc_all.max()
                 self.torch.cuda.synchronize()
                 if time.perf_counter() >= t_end:
                     break
@@ -651,6 +713,8 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
             "packets_per_step_per_gpu": per_gpu,
             "packets_per_step": args.packets if args.shard == "strong" else args.packets * world,
             "hbm_batches": args.nbuf,
+            **({"rotation_bytes_per_gpu": int(proc.rotation_bytes)}
+               if getattr(proc, "rotation_bytes", None) else {}),
             "nports": args.nports,
             **({"flow_maintain_ms": round(maintain_ms, 4)} if maintain_ms is not None else {}),
             "parallelism": (f"batch-sharded x{world}" if args.shard == "weak" else
@@ -678,8 +742,7 @@ def main():
     import torch
     import torch.distributed as dist
     ndev = torch.cuda.device_count()
-    if ndev == 0:
-        raise SystemExit("bench.py: no HIP device visible")
+    check_devices(world, ndev, args.backend)
     gpu = local % ndev
     if world > 1:
         if args.backend == "nccl":

@@ -150,7 +150,8 @@ def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1, timer_flu
 
 def bench_element(conf: str, batch, *, burst: int = 32, reps: int = 5, threads: int = 1) -> float:
     """Packets/s through the element (threads > 1: that many instances, one
-    per thread, each with its own GPU context; the sum of their rates)."""
+    per thread, each with its own GPU context, their timed loops started
+    together after every set-up; all packets over the union of the windows)."""
     lib = load()
     arena = np.ascontiguousarray(batch.arena)
     desc = np.ascontiguousarray(batch.desc, dtype=np.uint32)

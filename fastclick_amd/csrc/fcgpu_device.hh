@@ -1003,7 +1003,8 @@ __device__ __forceinline__ void flow_resolve(const FlowArgs &F, FlowProbe &q, bo
 // SetIPChecksum::simple_action (elements/ip/setipchecksum.cc:38-58): the full
 // click_in_cksum of the header with ip_sum = 0; kills a packet whose header
 // does not fit (only reachable in MARK mode). The packet's IP header bytes
-// 8..11 after the rewrites go to ip_rw (and the arena with FCGPU_RW_INPLACE).
+// 8..11 after the rewrites go to ip_rw for every packet that leaves with
+// R_OK (and, when changed, to the arena with FCGPU_RW_INPLACE).
 template <bool WIN>
 __device__ __forceinline__ void rw_stage_t(const DevCfg &c, const FrameView &f, uint8_t *frame, bool live,
                                            PktResult &r, uint32_t *ip_rw, uint32_t i) {
@@ -1054,7 +1055,10 @@ __device__ __forceinline__ void rw_stage_t(const DevCfg &c, const FrameView &f, 
             p[3] = (uint8_t)(w >> 24);
         }
     }
-    if (live && ip_rw) ip_rw[i] = changed ? w : 0u;
+    // every packet that leaves with R_OK reports its bytes 8..11 as they leave
+    // (rewritten or not), so a rewritten word of 0 (ttl 0, proto 0, sum 0 after
+    // SetIPChecksum) is told apart from "no rewrite"; the rest report 0
+    if (live && ip_rw) ip_rw[i] = r.reason == FCGPU_R_OK ? w : 0u;
 }
 // The header reads from the LDS window when every rewriting lane of the wave
 // has its IP header there (the general reads compile to flat loads that wait

@@ -555,7 +555,11 @@ __device__ __forceinline__ uint32_t maint_dest(const FlowArgs &F, const MaintArg
     const int32_t old = (int32_t)(M.now - ls);
     if (old <= 0) return F.te;                                   // lastseen not in the past (:174-180)
     if ((uint32_t)old + M.ri_ms >= M.to_ms) return 0;            // expire (:185-205)
-    return ((M.to_ms - (uint32_t)old) * M.eps) / 1000u;          // time left (:209-211)
+    // time left (:209-211); a flow with under one epoch left (eps floored,
+    // e.g. RECYCLE_INTERVAL 300 ms) goes one epoch ahead: r = 0 is the
+    // reference's "likely a bug" (timerwheel.hh:25 asserts timeout > 0)
+    const uint32_t r = ((M.to_ms - (uint32_t)old) * M.eps) / 1000u;
+    return r ? r : 1u;
 }
 
 // Stable rank of each valid lane among the chunk's earlier lanes with the

@@ -2,6 +2,8 @@
 #include <algorithm>
 #include <chrono>
 #include <thread>
+#include <condition_variable>
+#include <mutex>
 #include <memory>
 #include <string>
 #include <vector>
@@ -272,12 +274,32 @@ extern "C" int fcclick_run(const char *conf, const uint8_t *arena, const uint32_
 }
 
 namespace {
+// Every thread's timed loop starts together: after each has set up its
+// element (GPU context, pinned staging, possibly hiprtc) and run its warm-up.
+struct StartLine {
+    std::mutex mu;
+    std::condition_variable cv;
+    uint32_t waiting = 0, parties = 1;
+    void arrive() {
+        std::unique_lock<std::mutex> g(mu);
+        if (++waiting >= parties) cv.notify_all();
+        else cv.wait(g, [this] { return waiting >= parties; });
+    }
+};
+using Clock = std::chrono::steady_clock;
+
 // One element instance (its own GPU context, like one Click thread) pushed
-// `reps` times through the trace; returns packets per second, or < 0.
+// `reps` times through the trace; returns packets per second, or < 0. With a
+// start line, the timed loop begins once every thread has reached it (a
+// thread that fails still arrives), and [t_beg, t_end] is its timed window.
 double bench_one(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n, uint32_t burst,
-                 uint32_t reps, std::string &e) {
+                 uint32_t reps, std::string &e, StartLine *line = nullptr, Clock::time_point *t_beg = nullptr,
+                 Clock::time_point *t_end = nullptr) {
     auto el = make_element(conf, e);
-    if (!el || el->initialize(e) < 0) return -1.0;
+    if (!el || el->initialize(e) < 0) {
+        if (line) line->arrive();
+        return -1.0;
+    }
     const bool per_packet = burst == FCCLICK_PER_PACKET;
     if (burst == 0) burst = 32;
     if (per_packet) burst = 32;
@@ -316,9 +338,12 @@ double bench_one(const char *conf, const uint8_t *arena, const uint32_t *desc, u
         el->flush();
     };
     one();   // warm-up (allocations, first launch)
-    auto t0 = std::chrono::steady_clock::now();
+    if (line) line->arrive();
+    auto t0 = Clock::now();
     for (uint32_t r = 0; r < reps; ++r) one();
-    auto t1 = std::chrono::steady_clock::now();
+    auto t1 = Clock::now();
+    if (t_beg) *t_beg = t0;
+    if (t_end) *t_end = t1;
     const double s = std::chrono::duration<double>(t1 - t0).count();
     e = el->read_handler("error");
     el.reset();                      // before the pool its packets belong to
@@ -345,20 +370,26 @@ extern "C" int fcclick_bench_threads(const char *conf, const uint8_t *arena, con
     if (threads == 0) threads = 1;
     std::vector<double> r(threads, 0.0);
     std::vector<std::string> es(threads);
+    std::vector<Clock::time_point> beg(threads), end(threads);
     std::vector<std::thread> th;
-    auto t0 = std::chrono::steady_clock::now();
+    StartLine line;
+    line.parties = threads;
     for (uint32_t t = 0; t < threads; ++t)
-        th.emplace_back([&, t]() { r[t] = bench_one(conf, arena, desc, n, burst, reps, es[t]); });
+        th.emplace_back([&, t]() { r[t] = bench_one(conf, arena, desc, n, burst, reps, es[t], &line, &beg[t], &end[t]); });
     for (auto &x : th) x.join();
-    (void)t0;
-    double tot = 0;
-    for (uint32_t t = 0; t < threads; ++t) {
+    for (uint32_t t = 0; t < threads; ++t)
         if (r[t] < 0) {
             copy_err(es[t], err, errcap);
             return r[t] == -1.0 ? -1 : -2;
         }
-        tot += r[t];
+    // aggregate: every thread's packets over the union of the timed windows
+    // (earliest start to latest end), not the sum of per-thread rates
+    Clock::time_point b = beg[0], e = end[0];
+    for (uint32_t t = 1; t < threads; ++t) {
+        b = std::min(b, beg[t]);
+        e = std::max(e, end[t]);
     }
-    if (pps) *pps = tot;
+    const double s = std::chrono::duration<double>(e - b).count();
+    if (pps) *pps = s > 0 ? (double)n * reps * threads / s : 0.0;
     return 0;
 }

@@ -82,6 +82,8 @@
 #include <arpa/inet.h>
 #include <stdio.h>
 #include <string.h>
+#include <atomic>
+#include <mutex>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -362,6 +364,7 @@ class RxCore {
 
     // Kill whatever is still staged or in flight (router cleanup).
     void release() {
+        std::lock_guard<std::mutex> g(_mu);
         for (uint32_t k = 0; k < kSlots; ++k) {
             Slot &s = _slot[k];
             if (s.inflight && _ctx) fcgpu_span_wait(_ctx, k);
@@ -437,14 +440,22 @@ class RxCore {
     }
 
     // ---- handlers ------------------------------------------------------------
-    // This core's counters (fcgpu_read_counters), flow IDs issued, flows dropped.
-    void counters(uint64_t (&c)[FCGPU_NCOUNTERS], uint64_t &flows, uint64_t &flow_drops) {
+    // This core's counters (fcgpu_read_counters), flow IDs issued, flows
+    // dropped and last error. Safe from any thread (a handler reads every
+    // thread's core, ELEMENT_MT_SAFE): the context and the error string are
+    // only touched under _mu, which the owning data thread holds around its
+    // own context calls (submit, completion wait, maintainer, failure).
+    void counters(uint64_t (&c)[FCGPU_NCOUNTERS], uint64_t &flows, uint64_t &flow_drops, std::string *error = nullptr) {
         memset(c, 0, sizeof c);
-        if (_ctx) fcgpu_read_counters(_ctx, c, FCGPU_NCOUNTERS);
         uint32_t f = 0;
-        if (_ctx && _flow_cap) fcgpu_flow_count(_ctx, &f);
+        {
+            std::lock_guard<std::mutex> g(_mu);
+            if (_ctx) fcgpu_read_counters(_ctx, c, FCGPU_NCOUNTERS);
+            if (_ctx && _flow_cap) fcgpu_flow_count(_ctx, &f);
+            if (error) *error = _error;
+        }
         flows = f;
-        flow_drops = _flow_drops;
+        flow_drops = _flow_drops.load(std::memory_order_relaxed);
     }
     bool details() const { return _details; }
 
@@ -471,10 +482,14 @@ class RxCore {
     std::string read_handler(const std::string &h) {
         uint64_t c[FCGPU_NCOUNTERS];
         uint64_t flows, drops;
-        counters(c, flows, drops);
-        return format_handler(h, c, _cfg.nports, _details, flows, drops, _error);
+        std::string error;
+        counters(c, flows, drops, &error);
+        return format_handler(h, c, _cfg.nports, _details, flows, drops, error);
     }
-    const std::string &error() const { return _error; }
+    std::string error() const {
+        std::lock_guard<std::mutex> g(_mu);
+        return _error;
+    }
 
     // CheckIPHeader::reason_texts (elements/ip/checkipheader.cc:35-38)
     static constexpr const char *kReasonTexts[6] = {"tiny packet", "bad IPv4 version", "bad IPv4 header length",
@@ -585,13 +600,16 @@ class RxCore {
     void submit(Emit &emit) {
         const uint32_t k = _cur;
         Slot &s = _slot[k];
-        if (_flow_cap && _flow_timeout) flow_clock();
-        const int rc = fcgpu_span_submit_block(_ctx, k, s.in, s.frames_off + s.used, 0, s.frames_off, s.n, s.res,
-                                               _outputs, _partition);
-        if (rc != FCGPU_OK) {
-            fail_slot(s, fcgpu_last_error(_ctx));
-        } else {
-            s.inflight = true;
+        {
+            std::lock_guard<std::mutex> g(_mu);
+            if (_flow_cap && _flow_timeout) flow_clock();
+            const int rc = fcgpu_span_submit_block(_ctx, k, s.in, s.frames_off + s.used, 0, s.frames_off, s.n,
+                                                   s.res, _outputs, _partition);
+            if (rc != FCGPU_OK) {
+                fail_slot(s, fcgpu_last_error(_ctx));
+            } else {
+                s.inflight = true;
+            }
         }
         _cur = (_cur + 1) % kSlots;
         if (_slot[_cur].inflight) complete(_cur, emit);
@@ -600,7 +618,7 @@ class RxCore {
     // IMP timeouts: the maintainer runs due by now (every RECYCLE_INTERVAL from
     // the first batch, virtualflowmanager.hh:118-124,134-144), then this
     // batch's time stamp (Timestamp::recent_steady() at push_batch, :227-230).
-    // Queued on the context's stream ahead of the batch.
+    // Queued on the context's stream ahead of the batch. Called with _mu held.
     void flow_clock() {
         const uint32_t now = (uint32_t)(P::now_ns() / 1000000ull);
         if (!_maint_armed) {
@@ -614,6 +632,7 @@ class RxCore {
         fcgpu_flow_set_time(_ctx, now);
     }
 
+    // Called with _mu held.
     void fail_slot(Slot &s, const char *msg) {
         // no CPU fallback: report, drop the batch, keep running
         _error = msg ? msg : "GPU processing failed";
@@ -649,16 +668,19 @@ class RxCore {
     template <class Emit>
     void complete(uint32_t k, Emit &emit) {
         Slot &s = _slot[k];
-        const int rc = fcgpu_span_wait(_ctx, k);
-        s.inflight = false;
-        if (rc != FCGPU_OK) {
-            fail_slot(s, fcgpu_last_error(_ctx));
-            return;
-        }
         const uint32_t n = s.n;
-        s.holes = false;
         fcgpu_block_layout L;
-        fcgpu_block_layout_for(_ctx, n, _outputs, _partition, &L);
+        {
+            std::lock_guard<std::mutex> g(_mu);
+            const int rc = fcgpu_span_wait(_ctx, k);
+            s.inflight = false;
+            if (rc != FCGPU_OK) {
+                fail_slot(s, fcgpu_last_error(_ctx));
+                return;
+            }
+            fcgpu_block_layout_for(_ctx, n, _outputs, _partition, &L);
+        }
+        s.holes = false;
         s.map(L);
         const bool hashing = _cfg.hash_mode != FCGPU_HASH_NONE;
         const bool autom = _cfg.check_mode == FCGPU_CHECK_AUTO;
@@ -671,7 +693,9 @@ class RxCore {
             if (autom && reason != FCGPU_R_VLAN_REJECT)
                 P::set_anno_u16(p, P::kVlanTci, a.vlan_tci);                     // StripEtherVLANHeader
             if (reason == FCGPU_R_OK || reason >= FCGPU_R_NO_MATCH) {
-                if (s.iprw && s.iprw[i]) {                                       // DecIPTTL / SetIPChecksum
+                // DecIPTTL / SetIPChecksum: ip_rw holds every R_OK packet's bytes
+                // 8..11 as they leave; only a changed word is written back
+                if (s.iprw && reason == FCGPU_R_OK && memcmp(P::data(p) + a.nh + 8u, &s.iprw[i], 4) != 0) {
                     Packet *q = P::write_bytes(p, a.nh + 8u, &s.iprw[i], 4);
                     if (!q) {                                                    // uniqueify failed: freed
                         s.pkts[i] = nullptr;
@@ -739,7 +763,7 @@ class RxCore {
                 if ((nomatch && r == FCGPU_R_NO_MATCH) || (last && r == FCGPU_R_SETCKSUM_BAD)) {
                     P::kill(p);
                 } else if (s.flowid && s.flowid[i] == FCGPU_FLOW_FULL) {
-                    ++_flow_drops;
+                    _flow_drops.fetch_add(1, std::memory_order_relaxed);
                     P::kill(p);
                 } else {
                     s.keep[w++] = i;
@@ -794,7 +818,7 @@ class RxCore {
     bool _maint_armed = false;
     int _flow_anno = 28;
     bool _flow_runs = true;
-    uint64_t _flow_drops = 0;
+    std::atomic<uint64_t> _flow_drops{0};       // read by handlers on other threads
     int _device = 0;
     uint32_t _batch = 16384;
     int64_t _timer_us = 100;
@@ -803,7 +827,8 @@ class RxCore {
     uint32_t _partition = FCGPU_PART_TILE;
     uint32_t _outputs = 0;                       // FCGPU_OUT_* the element asks for
     bool _verbose = false, _details = false, _strip = false, _warned = false;
-    std::string _error;
+    std::string _error;                         // under _mu
+    mutable std::mutex _mu;                     // the context and _error (see counters())
     Slot _slot[kSlots];
     uint32_t _cur = 0;
 };

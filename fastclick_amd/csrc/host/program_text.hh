@@ -91,7 +91,7 @@ inline std::string parse_program(const std::string &text, ParsedProgram &out) {
         if (!strncmp(p, "alignment offset", 16)) { out.align_offset = atoi(p + 16); continue; }
         if (!strncmp(p, "all->", 5)) {
             const char *q = p + 5;
-            int32_t j;
+            int32_t j = 0;
             if (!parse_jump(q, j) || j > 0) return "bad all-> line " + std::to_string(lineno);
             out.output_everything = j <= -2147483647 ? 0x7fff : -j;
             continue;

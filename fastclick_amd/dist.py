@@ -37,22 +37,32 @@ def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
     return (n * rank) // world, (n * (rank + 1)) // world
 
 
-def reduce_counters(replicas, group=None):
+def _collective(group, force):
+    """Whether to issue the collective: a process group exists and has more
+    than one rank, or `force` (a world-1 group still runs the RCCL call, so
+    the N = 1 case exercises the same code as N = 8)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return force or dist.get_world_size(group) > 1
+
+
+def reduce_counters(replicas, group=None, force=False):
     """Sum a [replicas, NCOUNTERS] int64 tensor over replicas, then over ranks.
     Returns the global NCOUNTERS vector (same device as the input)."""
     import torch.distributed as dist
     local = replicas.sum(0) if replicas.dim() == 2 else replicas.clone()
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if _collective(group, force):
         dist.all_reduce(local, op=dist.ReduceOp.SUM, group=group)
     return local
 
 
-def output_offsets(local_counts, group=None):
+def output_offsets(local_counts, group=None, force=False):
     """All-gather every rank's per-output counts [nout] and return this rank's
     start offset within each output's global list, plus the global totals."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+    if not _collective(group, force):
         return torch.zeros_like(local_counts), local_counts.clone()
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)

@@ -153,7 +153,9 @@ GPUIPCheckClassify::read_handler(Element *e, void *thunk)
     static const char *const names[] = {"count", "drops", "drop_details", "port_counts",
                                         "flow_count", "flow_drops", "error"};
     // PER_THREAD_SUM (include/click/sync.hh:384): the per-thread cores'
-    // counters are summed on read
+    // counters are summed on read. Each core's counters and error are read
+    // under that core's own lock (RxCore::counters), never racing the thread
+    // that owns its GPU context.
     uint64_t sum[FCGPU_NCOUNTERS] = {0};
     uint64_t flows = 0, drops = 0;
     std::string error;
@@ -165,7 +167,8 @@ GPUIPCheckClassify::read_handler(Element *e, void *thunk)
             continue;
         uint64_t c[FCGPU_NCOUNTERS];
         uint64_t f, d;
-        s.core->counters(c, f, d);
+        std::string e;
+        s.core->counters(c, f, d, &e);
         for (int k = 0; k < FCGPU_NCOUNTERS; k++)
             sum[k] += c[k];
         flows += f;
@@ -173,7 +176,7 @@ GPUIPCheckClassify::read_handler(Element *e, void *thunk)
         nports = s.core->nports();
         details = s.core->details();
         if (error.empty())
-            error = s.core->error();
+            error = e;
     }
     const int h = (int)(uintptr_t)thunk;
     std::string out = Core::format_handler(names[h], sum, nports, details, flows, drops, error);

@@ -210,7 +210,9 @@ typedef struct fcgpu_out {
                                  FCGPU_FLOW_NONE for packets that reach no flow manager */
     uint32_t   *ip_rw;        /* [n] with cfg.rewrite: IP header bytes 8..11 after the rewrite
                                  (little-endian load: ttl | proto << 8 | checksum bytes << 16);
-                                 written for packets the rewrite stage changed, else 0  */
+                                 for every packet that leaves with FCGPU_R_OK, rewritten
+                                 or not (a rewritten word may be 0: compare it with the
+                                 packet's bytes to see a change); 0 for the rest        */
 } fcgpu_out;
 
 typedef struct fcgpu_ctx fcgpu_ctx;

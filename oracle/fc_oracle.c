@@ -415,7 +415,9 @@ static void rewrite_ip4(const fcgpu_cfg *c, const uint8_t *f, fco_result *r)
         memcpy(b + 2, &ck, 2);
         changed = 1;
     }
-    if (changed) r->ip_rw = (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 | (uint32_t)b[3] << 24;
+    /* the bytes as the packet leaves, changed or not (fastclick_gpu.h ip_rw) */
+    (void)changed;
+    r->ip_rw = (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 | (uint32_t)b[3] << 24;
 }
 
 void fco_process_packet(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, fco_result *r)
@@ -814,7 +816,7 @@ uint32_t fco_imp_maintain(fco_imp *t, uint32_t now_ms)
             removed++;
         } else {
             const uint32_t r = ((t->to_ms - (uint32_t)old) * t->eps) / 1000u;   /* :209-211 */
-            fco_imp_schedule(t, f, r);
+            fco_imp_schedule(t, f, r ? r : 1u);   /* timerwheel.hh:25: timeout > 0 */
         }
         f = next;
     }

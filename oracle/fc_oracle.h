@@ -28,7 +28,7 @@ typedef struct fco_result {
     uint8_t    port;     /* output index; nports for the invalid list */
     uint32_t   hash;
     fcgpu_anno anno;
-    uint32_t   ip_rw;    /* IP header bytes 8..11 after cfg.rewrite (0 if unchanged) */
+    uint32_t   ip_rw;    /* IP header bytes 8..11 as a packet that leaves with R_OK leaves (cfg.rewrite), else 0 */
 } fco_result;
 
 /* A2 (+A4/A13/A14): one packet through the configured check chain, then

@@ -182,5 +182,28 @@ def main():
     print(json.dumps(out))
 
 
+def thread_sweep():
+    """The element's host-side scaling: BATCH x threads (one element instance
+    and GPU context per thread, all timed loops started together, aggregate =
+    all packets over the union of the windows), beside the harness floor (a
+    pass-through element) at the same thread counts. One JSON line."""
+    b = synth.c2(1 << 16)
+    base = "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BATCH {})"
+    out = {"gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)"),
+           "affinity": len(os.sched_getaffinity(0))}
+    for t in (1, 2, 4, 8, 12, 16):
+        out[f"floor_t{t}"] = round(K.bench_element("Pass", b, burst=32, reps=40, threads=t) / 1e6, 1)
+    for batch in (4096, 8192, 16384):
+        for t in (1, 2, 4, 8, 12, 16):
+            out[f"el_b{batch}_t{t}"] = round(
+                K.bench_element(base.format(batch), b, burst=32, reps=40, threads=t) / 1e6, 1)
+            print(json.dumps({k: v for k, v in out.items() if k.startswith(f"el_b{batch}")}), file=sys.stderr,
+                  flush=True)
+    print(json.dumps(out), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "threads":
+        thread_sweep()
+    else:
+        main()

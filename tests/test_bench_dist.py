@@ -145,3 +145,43 @@ def test_gpu_bench_two_ranks():
         line = json.loads(r.stdout.strip().splitlines()[-1])
         assert line["n_gpus"] == 2 and line["scaling"] == shard
         assert line["config"]["packets_per_step"] == (131072 if shard == "weak" else 65536)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_strong_shards_rotate_beyond_the_infinity_cache(world):
+    """--shard strong (C4, 1M packets): every rank uploads only its own
+    frames (an arena of ~1/world of the batch, descriptors rebased onto it,
+    the frames' bytes unchanged) and rotates over enough copies of them that
+    the bytes its steps touch exceed 1.15 GB -- HBM, not the 256 MB Infinity
+    Cache, at every point of the strong curve."""
+    import bench
+    from fastclick_amd import synth
+    args = bench.parse(["--gpus", str(world), "--shard", "strong"])
+    host, _ = bench.make_host_batch(args)
+    assert host.n == 1 << 20
+    for rank in range(world):
+        lo, hi = bench.shard_of(args, world, rank)
+        arena, desc = bench.shard_arrays(host, lo, hi)
+        assert desc.shape == (hi - lo, 2)
+        assert arena.nbytes <= host.arena.nbytes // world + 4096
+        touched = arena.nbytes + desc.nbytes
+        nbuf = bench.rotation_nbuf(touched)
+        assert nbuf * touched >= 1.15e9 and (nbuf - 1) * touched < 1.15e9 or nbuf == 4
+        for i in (0, (hi - lo) // 2, hi - lo - 1):   # the frames travel unchanged
+            o, ln = (int(x) for x in desc[i])
+            oo, lln = (int(x) for x in host.desc[lo + i])
+            assert ln == lln and o % 256 == oo % 256
+            assert bytes(arena[o:o + ln]) == bytes(host.arena[oo:oo + ln])
+        shard = synth.Batch(arena=arena, desc=desc)
+        assert shard.frame(hi - lo - 1) == host.frame(hi - 1)
+    assert bench.rotation_nbuf(131072 * 64 + 256 + 131072 * 8) == 122   # 122 x 9.4 MB at N = 8
+
+
+def test_nccl_world_larger_than_devices_fails_at_startup():
+    import bench
+    with pytest.raises(SystemExit, match="one GPU per rank"):
+        bench.check_devices(8, 1, "nccl")
+    bench.check_devices(2, 1, "gloo")     # a rehearsal on one GPU
+    bench.check_devices(8, 8, "nccl")
+    with pytest.raises(SystemExit, match="no HIP device"):
+        bench.check_devices(1, 0, "nccl")

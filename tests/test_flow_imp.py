@@ -103,7 +103,8 @@ class ImpModel:
                 self.link[f] = self.qbsr
                 self.qbsr = f
             else:
-                self.schedule_after(f, ((self.timeout_ms - old) * self.eps) // 1000)   # :209-211
+                # :209-211; r >= 1 (timerwheel.hh:25 asserts timeout > 0)
+                self.schedule_after(f, max(1, ((self.timeout_ms - old) * self.eps) // 1000))
             f = nxt
         self.buckets[cur] = None
         self.index += 1
@@ -156,6 +157,12 @@ SCENARIOS = {
     "fills": dict(cap=512, timeout_s=1, recycle_ms=100,
                   sc=dict(seed=6, npool=5_000, nsteps=30, sizes=[700, 90, 1500], window=900,
                           drift=(50, 400), dt_ms=(30, 300), recycle_ms=100)),
+    # a RECYCLE_INTERVAL that does not divide 1000 ms (eps = 3 floored): flows
+    # idle 667-699 ms of a 1 s timeout have under one epoch left and are
+    # rescheduled one epoch ahead, not released early
+    "recycle300": dict(cap=8192, timeout_s=1, recycle_ms=300,
+                       sc=dict(seed=8, npool=20_000, nsteps=60, sizes=[500, 1800, 60], window=1200,
+                               drift=(50, 400), dt_ms=(10, 120), recycle_ms=300)),
     # no timeout: IDs cap-1, cap-2, ... and the table fills for good
     "no-timeout": dict(cap=1000, timeout_s=0, recycle_ms=1000,
                        sc=dict(seed=7, npool=3_000, nsteps=6, sizes=[400], window=3_000,

@@ -32,8 +32,9 @@ def orig_bytes(b, nh_off=14):
 
 
 def effective(r, b):
-    """Bytes 8..11 after the element: ip_rw when it changed them, else the input's."""
-    return np.where(r["ip_rw"] != 0, r["ip_rw"], orig_bytes(b))
+    """Bytes 8..11 after the element: ip_rw for a packet that leaves with R_OK
+    (rewritten or not), else the input's."""
+    return np.where(r["reason"] == N.R_OK, r["ip_rw"], orig_bytes(b))
 
 
 def check_rw(run, g):
@@ -128,9 +129,11 @@ def test_gpu_rewrite_inplace():
     finally:
         ctx.close()
     after = orig_bytes(synth.Batch(arena=arena, desc=b.desc))
-    changed = res["ip_rw"] != 0
+    ok = res["reason"] == N.R_OK
+    assert np.array_equal(res["ip_rw"][~ok], np.zeros((~ok).sum(), np.uint32))
+    changed = ok & (res["ip_rw"] != orig_bytes(b))
     assert changed.sum() > 2000
-    assert np.array_equal(after[changed], res["ip_rw"][changed])
+    assert np.array_equal(after[ok], res["ip_rw"][ok])
     assert np.array_equal(after[changed], g["decset"][changed])
     assert np.array_equal(after[~changed], orig_bytes(b)[~changed])
 
