@@ -76,6 +76,10 @@ def parse(argv=None):
                          "a stream whose outputs are disjoint, up to 24): each step gets its own output set "
                          "among fuse x streams; 1 = one launch per batch")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
+    ap.add_argument("--no-plan", action="store_true",
+                    help="submit the steps with fcgpu_process_jobs (each fused launch carries its batch table "
+                         "as ~2.7 KB of kernel arguments) instead of a plan (fcgpu_plan_jobs: the table "
+                         "uploaded once, the launch passes its pointer)")
     ap.add_argument("--timing-every", type=int, default=0,
                     help="bracket the k_rx launch covering every k-th timed batch with HIP events "
                          "(stream markers on the launch stream, hipEventRecord; created before the "
@@ -458,6 +462,8 @@ class DeviceProcessor:
         self.timing_every = 0 if args.no_timing else (args.timing_every or min(8, max(1, args.steps)))
 
     def _jobs(self, first, count):
+        """Steps first .. first+count-1 as one submission: a plan (default: an rx
+        ring's fixed slots, launches and tables decided once) or a job array."""
         specs = []
         ns = len(self.streams)
         for k in range(first, first + count):
@@ -465,7 +471,14 @@ class DeviceProcessor:
             j = k % ns
             specs.append((a.data_ptr(), d.data_ptr(), self.n, self.streams[j].cuda_stream,
                           self.outs[k % len(self.outs)].ptrs()))
-        return self.ctx.jobs(specs)
+        jobs = self.ctx.jobs(specs)
+        return jobs if self.args.no_plan else self.ctx.plan(jobs)
+
+    def _run(self, sub):
+        if self.args.no_plan:
+            self.ctx.run_jobs(sub)
+        else:
+            self.ctx.run_plan(sub)
 
     def warmup(self, steps):
         if self.args.prefault:
@@ -491,7 +504,7 @@ class DeviceProcessor:
         # enqueue, profiles/r02_s9/diag*.log) that belongs in the warmup, not
         # in the timed region (the pool hands the same events out again)
         self.ctx.set_timing(1 if self.timing_every else 0)
-        self.ctx.run_jobs(warm)
+        self._run(warm)
         self.torch.cuda.synchronize()
         self.ctx.read_timing()                      # drop warmup samples
         if self.args.flow_capacity and self.args.flow_manager == "imp" and self.args.flow_timeout:
@@ -518,7 +531,7 @@ class DeviceProcessor:
         self.maintain_ms = best
 
     def run_timed(self):
-        self.ctx.run_jobs(self.timed)
+        self._run(self.timed)
 
     def sync(self):
         self.torch.cuda.synchronize()
@@ -707,6 +720,7 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                 "valid_fraction": round(valid / total_pkts, 4)} if args.errors else {}),
             "partition": "none" if args.no_perm else args.partition,
             "streams": max(1, args.streams),
+            "submission": "fcgpu_process_jobs" if args.no_plan else "fcgpu_run_plan (device job table)",
             "batches_per_launch": max(1, min(args.fuse, 8 if args.flow_capacity else 24,
                                              -(-args.steps // max(1, args.streams)))),
             "frame_bytes": fb,

@@ -378,8 +378,9 @@ def test_process_jobs_fused_global_large(dev, oracle):
         ctx.close()
 
 
+@pytest.mark.parametrize("submit", ["jobs", "plan"])
 @pytest.mark.parametrize("partition", [N.PART_TILE, N.PART_GLOBAL, None])
-def test_process_jobs_fused(dev, oracle, partition):
+def test_process_jobs_fused(dev, oracle, partition, submit):
     """fcgpu_process_jobs fuses a stream's consecutive jobs with disjoint
     outputs into one k_rx launch (up to 24 batches, the grid their tiles end
     to end): 30 ragged batches (1 .. 30,001 packets, one empty) on one stream
@@ -388,7 +389,10 @@ def test_process_jobs_fused(dev, oracle, partition):
     later one's results are what the set holds, as with one call per job.
     PART_GLOBAL: the whole-batch partitions of a fused launch (one scan and
     one scatter launch for all its batches); odd batches ask for port_start
-    only (one scatter workgroup each)."""
+    only (one scatter workgroup each).
+    submit "plan": the same jobs planned once (fcgpu_plan_jobs: the fused
+    launches' tables in device memory; the whole-batch partition takes the
+    ordinary path) and run twice -- the same results, the counters twice."""
     import torch
     from fastclick_amd.device import DeviceBatch, DeviceOutputs
     cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16, badsrc=BADSRC)
@@ -413,10 +417,26 @@ def test_process_jobs_fused(dev, oracle, partition):
             outs.append(o)
             specs.append((b.arena.data_ptr(), b.desc.data_ptr(), b.n, None, o.ptrs()))
         ctx.set_timing(1)
-        ctx.run_jobs(ctx.jobs(specs))
+        runs = 1
+        if submit == "jobs":
+            ctx.run_jobs(ctx.jobs(specs))
+        else:
+            plan = ctx.plan(ctx.jobs(specs))
+            for o in outs:                      # the second run must rewrite every output
+                for t in (o.verdict, o.hash, o.tile_count, o.tile_perm, o.perm):
+                    if t is not None:
+                        t.fill_(-1)
+            ctx.run_plan(plan)
+            torch.cuda.synchronize()
+            for o in outs:
+                for t in (o.verdict, o.hash, o.tile_count, o.tile_perm, o.perm):
+                    if t is not None:
+                        t.fill_(-1)
+            ctx.run_plan(plan)
+            runs = 2
         torch.cuda.synchronize()
         ms, cnt = ctx.read_timing()
-        assert cnt[0] == sum(1 for n in sizes if n)          # timing counts batches
+        assert cnt[0] == runs * sum(1 for n in sizes if n)   # timing counts batches
         ctx.set_timing(0)
         for k, (b, o) in enumerate(zip(batches, outs)):
             if b.n == 0:
@@ -435,7 +455,7 @@ def test_process_jobs_fused(dev, oracle, partition):
                 if k % 2 == 0:
                     assert np.array_equal(got["perm"][:b.n], exp["perm"]), k
         want = sum(e["counters"].astype(np.int64) for e, b in zip(exps, batches) if b.n)
-        assert np.array_equal(np.array(ctx.counters(), np.int64), want)
+        assert np.array_equal(np.array(ctx.counters(), np.int64), runs * want)
         # two jobs on one output set: sequential semantics (the second wins)
         shared = DeviceOutputs(40_000, 16, device="cuda:0", perm=tile, anno=False,
                                partition=N.PART_TILE if tile else N.PART_GLOBAL, port_start=False)
@@ -447,5 +467,52 @@ def test_process_jobs_fused(dev, oracle, partition):
         n29 = batches[29].n
         assert np.array_equal(got["reason"][:n29], exps[29]["reason"])
         assert np.array_equal(got["reason"][n29:batches[5].n], exps[5]["reason"][n29:])
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("mode", ["c5_auto", "mark_crc", "ipclass_fallback"])
+def test_plan_equal_batches(dev, oracle, mode):
+    """fcgpu_run_plan over 24 equal batches (one launch, the table's
+    equal-tile division) and a ragged tail batch: C5's StripEtherVLANHeader +
+    IPv4/IPv6 dispatch, MarkIPHeader + LB_MODE hash_crc (LDS tables), and an
+    IPClassifier program (not table-eligible: the plan takes the
+    fcgpu_process_jobs path) -- every batch's results are the oracle's."""
+    import torch
+    from fastclick_amd import click
+    from fastclick_amd.device import DeviceBatch, DeviceOutputs
+    program = None
+    if mode == "c5_auto":
+        cfg = N.make_cfg(check_mode=N.CHECK_AUTO, offset=0, checksum=True, classify=N.CLS_LB_HASH, nports=16)
+        mk = lambda k, n: synth.c5(n, seed=500 + k)  # noqa: E731
+    elif mode == "mark_crc":
+        cfg = N.make_cfg(check_mode=N.MARK_IP4, offset=14, classify=N.CLS_LB_CRC, nports=16)
+        mk = lambda k, n: synth.c4(n, seed=600 + k)  # noqa: E731
+    else:
+        import bench
+        cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_PROGRAM, nports=16)
+        steps, oe = click.parse_program(bench.ipclass16_program())
+        program = (N.PROG_IPFILTER, steps, oe)
+        mk = lambda k, n: synth.c4(n, seed=700 + k)  # noqa: E731
+    sizes = [4096] * 24 + [777]
+    batches = [mk(k, n) for k, n in enumerate(sizes)]
+    ctx = N.Context(0, 4096, cfg)
+    try:
+        if program is not None:
+            ctx.set_program(*program)
+        dbs = [DeviceBatch.upload(b, device="cuda:0") for b in batches]
+        outs = [DeviceOutputs(b.n, 16, device="cuda:0", perm=True, anno=False, partition=N.PART_TILE)
+                for b in dbs]
+        specs = [(b.arena.data_ptr(), b.desc.data_ptr(), b.n, None, o.ptrs()) for b, o in zip(dbs, outs)]
+        plan = ctx.plan(ctx.jobs(specs))
+        ctx.run_plan(plan)
+        torch.cuda.synchronize()
+        for k, (b, o) in enumerate(zip(batches, outs)):
+            got = o.numpy()
+            exp = oracle.process_batch(cfg, b, program=program) if program else oracle.process_batch(cfg, b)
+            for key in ("reason", "port", "perm_tile"):
+                assert np.array_equal(got[key][:b.n], exp[key]), (mode, k, key)
+            ok = exp["reason"] == N.R_OK
+            assert np.array_equal(got["hash"][:b.n][ok], exp["hash"][ok]), (mode, k)
     finally:
         ctx.close()
