@@ -76,10 +76,6 @@ def parse(argv=None):
                          "a stream whose outputs are disjoint, up to 24): each step gets its own output set "
                          "among fuse x streams; 1 = one launch per batch")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
-    ap.add_argument("--no-plan", action="store_true",
-                    help="submit the steps with fcgpu_process_jobs (each fused launch carries its batch table "
-                         "as ~2.7 KB of kernel arguments) instead of a plan (fcgpu_plan_jobs: the table "
-                         "uploaded once, the launch passes its pointer)")
     ap.add_argument("--timing-every", type=int, default=0,
                     help="bracket the k_rx launch covering every k-th timed batch with HIP events "
                          "(stream markers on the launch stream, hipEventRecord; created before the "
@@ -462,8 +458,7 @@ class DeviceProcessor:
         self.timing_every = 0 if args.no_timing else (args.timing_every or min(8, max(1, args.steps)))
 
     def _jobs(self, first, count):
-        """Steps first .. first+count-1 as one submission: a plan (default: an rx
-        ring's fixed slots, launches and tables decided once) or a job array."""
+        """Steps first .. first+count-1 as one fcgpu_process_jobs submission."""
         specs = []
         ns = len(self.streams)
         for k in range(first, first + count):
@@ -471,14 +466,10 @@ class DeviceProcessor:
             j = k % ns
             specs.append((a.data_ptr(), d.data_ptr(), self.n, self.streams[j].cuda_stream,
                           self.outs[k % len(self.outs)].ptrs()))
-        jobs = self.ctx.jobs(specs)
-        return jobs if self.args.no_plan else self.ctx.plan(jobs)
+        return self.ctx.jobs(specs)
 
     def _run(self, sub):
-        if self.args.no_plan:
-            self.ctx.run_jobs(sub)
-        else:
-            self.ctx.run_plan(sub)
+        self.ctx.run_jobs(sub)
 
     def warmup(self, steps):
         if self.args.prefault:
@@ -720,7 +711,6 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                 "valid_fraction": round(valid / total_pkts, 4)} if args.errors else {}),
             "partition": "none" if args.no_perm else args.partition,
             "streams": max(1, args.streams),
-            "submission": "fcgpu_process_jobs" if args.no_plan else "fcgpu_run_plan (device job table)",
             "batches_per_launch": max(1, min(args.fuse, 8 if args.flow_capacity else 24,
                                              -(-args.steps // max(1, args.streams)))),
             "frame_bytes": fb,

@@ -183,10 +183,6 @@ FCGPU_SYMBOLS = {
     "fcgpu_process": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                 C.POINTER(fcgpu_out), C.c_void_p]),
     "fcgpu_process_jobs": (C.c_int, [C.c_void_p, C.POINTER(fcgpu_job), C.c_uint32, C.c_void_p]),
-    "fcgpu_plan_jobs": (C.c_int, [C.c_void_p, C.POINTER(fcgpu_job), C.c_uint32, C.c_void_p,
-                                  C.POINTER(C.c_void_p)]),
-    "fcgpu_run_plan": (C.c_int, [C.c_void_p, C.c_void_p]),
-    "fcgpu_plan_free": (None, [C.c_void_p, C.c_void_p]),
     "fcgpu_process_host": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_void_p, C.c_uint32,
                                      C.POINTER(fcgpu_out)]),
     "fcgpu_set_program": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(fcgpu_step), C.c_uint32,
@@ -382,28 +378,6 @@ class Context:
         arr, n = prepared
         self._chk(self.lib.fcgpu_process_jobs(self.h, arr, n, stream or None), "fcgpu_process_jobs")
 
-    def plan(self, prepared, stream=0):
-        """fcgpu_plan_jobs on a jobs() array: launches decided and fused
-        launches' tables uploaded once; run with run_plan (the plan is freed
-        with the context, or by free_plan)."""
-        arr, n = prepared
-        h = C.c_void_p()
-        self._chk(self.lib.fcgpu_plan_jobs(self.h, arr, n, stream or None, C.byref(h)), "fcgpu_plan_jobs")
-        self._plans = getattr(self, "_plans", [])
-        self._plans.append(h)
-        return h
-
-    def run_plan(self, plan):
-        self._chk(self.lib.fcgpu_run_plan(self.h, plan), "fcgpu_run_plan")
-
-    def free_plan(self, plan):
-        plans = getattr(self, "_plans", [])
-        for k, h in enumerate(plans):
-            if h is plan:
-                self.lib.fcgpu_plan_free(self.h, h)
-                del plans[k]
-                return
-
     def pool_register(self, base: int, nbytes: int):
         """Register a packet-buffer pool (mbuf headers + data rooms) for fcgpu_process_mbufs."""
         self._chk(self.lib.fcgpu_pool_register(self.h, base, nbytes), "fcgpu_pool_register")
@@ -513,9 +487,6 @@ class Context:
 
     def close(self):
         if getattr(self, "h", None):
-            for p in getattr(self, "_plans", []):
-                self.lib.fcgpu_plan_free(self.h, p)
-            self._plans = []
             self.lib.fcgpu_close(self.h)
             self.h = None
 

@@ -36,7 +36,6 @@
 #include <condition_variable>
 #include <functional>
 #include <map>
-#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -1405,12 +1404,7 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
     return FCGPU_OK;
 }
 
-// The checks and the launch grouping of fcgpu_process_jobs: every job
-// checked first, then fn(grp, g, stream) per launch group in submission
-// order (g == 1: process_one's shape; else a fused launch).
-extern "C++" {
-template <class Fn>
-static int group_jobs(fcgpu_ctx *c, const fcgpu_job *jobs, uint32_t njobs, void *stream, Fn &&fn) {
+int fcgpu_process_jobs(fcgpu_ctx *c, const fcgpu_job *jobs, uint32_t njobs, void *stream) {
     if (!c || (njobs && !jobs)) return FCGPU_EINVAL;
     // every job is checked before any is launched: a bad job launches nothing
     bool split = false;
@@ -1424,6 +1418,7 @@ static int group_jobs(fcgpu_ctx *c, const fcgpu_job *jobs, uint32_t njobs, void 
             return fail(c, FCGPU_EINVAL, "jobs on several streams: the flow table and the whole-batch "
                                          "partition use context scratch (one stream only)");
     }
+    HIPCHK(c, hipSetDevice(c->device));
     auto eff = [&](const fcgpu_job &j) { return (hipStream_t)(j.stream ? j.stream : stream); };
     // Per stream, in order: a fusable job and the stream's next fusable jobs
     // (up to kMaxFuse, disjoint outputs, same partition shape, stopping at the
@@ -1436,211 +1431,30 @@ static int group_jobs(fcgpu_ctx *c, const fcgpu_job *jobs, uint32_t njobs, void 
         if (done[k]) continue;
         const fcgpu_job &j = jobs[k];
         done[k] = 1;
+        if (!fusable(c, j)) {
+            int rc = process_one(c, j.arena, j.desc, j.n, &j.out, eff(j));
+            if (rc != FCGPU_OK) return rc;
+            continue;
+        }
         const hipStream_t s = eff(j);
         grp.assign(1, &j);
-        if (fusable(c, j)) {
-            const size_t gmax = c->fl.slots ? kMaxFuseFlow : kMaxFuse;
-            for (uint32_t m = k + 1; m < njobs && grp.size() < gmax; ++m) {
-                if (done[m] || eff(jobs[m]) != s) continue;
-                const fcgpu_job &x = jobs[m];
-                if (!fusable(c, x)) break;                  // the stream's order barrier
-                if (out_part(&x.out) != out_part(&j.out) || x.out.partition != j.out.partition) break;
-                bool clash = false;
-                for (const fcgpu_job *y : grp) clash = clash || outputs_overlap(x.out, y->out);
-                if (clash) break;
-                grp.push_back(&x);
-                done[m] = 1;
-            }
+        const size_t gmax = c->fl.slots ? kMaxFuseFlow : kMaxFuse;
+        for (uint32_t m = k + 1; m < njobs && grp.size() < gmax; ++m) {
+            if (done[m] || eff(jobs[m]) != s) continue;
+            const fcgpu_job &x = jobs[m];
+            if (!fusable(c, x)) break;                  // the stream's order barrier
+            if (out_part(&x.out) != out_part(&j.out) || x.out.partition != j.out.partition) break;
+            bool clash = false;
+            for (const fcgpu_job *y : grp) clash = clash || outputs_overlap(x.out, y->out);
+            if (clash) break;
+            grp.push_back(&x);
+            done[m] = 1;
         }
-        int rc = fn(grp.data(), (uint32_t)grp.size(), s);
+        int rc = grp.size() == 1 ? process_one(c, j.arena, j.desc, j.n, &j.out, s)
+                                 : process_fused(c, grp.data(), (uint32_t)grp.size(), s);
         if (rc != FCGPU_OK) return rc;
     }
     return FCGPU_OK;
-}
-}  // extern "C++"
-
-int fcgpu_process_jobs(fcgpu_ctx *c, const fcgpu_job *jobs, uint32_t njobs, void *stream) {
-    if (!c || (njobs && !jobs)) return FCGPU_EINVAL;
-    HIPCHK(c, hipSetDevice(c->device));
-    return group_jobs(c, jobs, njobs, stream, [c](const fcgpu_job *const *grp, uint32_t g, hipStream_t s) {
-        return g == 1 ? process_one(c, grp[0]->arena, grp[0]->desc, grp[0]->n, &grp[0]->out, s)
-                      : process_fused(c, grp, g, s);
-    });
-}
-
-// ---- plans: a fixed job list, its fused launches' tables in device memory --
-struct PlanGroup {
-    std::vector<fcgpu_job> jobs;
-    hipStream_t s = nullptr;
-    RxJob *d_tab = nullptr;      // fused, table-eligible: the batches' RxJob table
-    uint32_t tiles = 0, job_tiles = 0;
-};
-struct fcgpu_plan {
-    std::vector<PlanGroup> groups;
-};
-
-// A fused launch that can take its table from device memory: k_rx<..., RxLaunchTab>
-// is instantiated for the check modes without a decision program, an L4
-// check or a flow table, and without the whole-batch partition (its scratch
-// pointers are per launch).
-static bool tab_ok(const fcgpu_ctx *c, int part) {
-    return !c->fl.slots && c->cfg.classify != FCGPU_CLS_PROGRAM && c->cfg.l4_mode == FCGPU_L4_NONE &&
-           part != kPartGlobal;
-}
-
-int fcgpu_plan_jobs(fcgpu_ctx *c, const fcgpu_job *jobs, uint32_t njobs, void *stream, fcgpu_plan **out) {
-    if (!c || !out || (njobs && !jobs)) return FCGPU_EINVAL;
-    *out = nullptr;
-    HIPCHK(c, hipSetDevice(c->device));
-    std::unique_ptr<fcgpu_plan> P(new fcgpu_plan());
-    int rc = group_jobs(c, jobs, njobs, stream, [&](const fcgpu_job *const *grp, uint32_t g, hipStream_t s) {
-        PlanGroup G;
-        G.s = s;
-        for (uint32_t k = 0; k < g; ++k) G.jobs.push_back(*grp[k]);
-        if (g > 1 && tab_ok(c, out_part(&grp[0]->out))) {
-            std::vector<RxJob> t(g);
-            uint32_t tiles = 0;
-            for (uint32_t k = 0; k < g; ++k) {
-                const fcgpu_job &j = *grp[k];
-                RxJob &J = t[k];
-                J = RxJob{};
-                J.arena = j.arena;
-                J.desc = reinterpret_cast<const uint2 *>(j.desc);
-                J.verdict = j.out.verdict;
-                J.hash = j.out.hash;
-                J.anno = j.out.anno;
-                J.perm = j.out.perm;
-                J.tile_count = j.out.tile_count;
-                J.tile_perm = j.out.partition == FCGPU_PART_TILE ? j.out.tile_perm : nullptr;
-                J.flowid = j.out.flowid;
-                J.ip_rw = j.out.ip_rw;
-                J.n = j.n;
-                J.tile0 = tiles;
-                tiles += (j.n + kTile - 1) / kTile;
-            }
-            uint32_t jt = (t[0].n + kTile - 1) / kTile;
-            for (uint32_t k = 1; k < g; ++k)
-                if (t[k].tile0 != k * jt) jt = 0;
-            if (tiles > g * jt) jt = 0;
-            G.tiles = tiles;
-            G.job_tiles = jt;
-            HIPCHK(c, hipMalloc(&G.d_tab, sizeof(RxJob) * g));
-            HIPCHK(c, hipMemcpy(G.d_tab, t.data(), sizeof(RxJob) * g, hipMemcpyHostToDevice));
-        }
-        P->groups.push_back(std::move(G));
-        return FCGPU_OK;
-    });
-    if (rc != FCGPU_OK) {
-        fcgpu_plan_free(c, P.release());
-        return rc;
-    }
-    *out = P.release();
-    return FCGPU_OK;
-}
-
-extern "C++" {
-template <int CM, bool CK, int PART>
-static void launch_tab(const RxLaunchTab &L, uint32_t grid, hipStream_t s) {
-    const size_t lds = prog_lds_bytes(L.A.cfg);   // LB_CRC tables
-    hipLaunchKernelGGL((k_rx<CM, CK, PART, false, false, false, (CM == FCGPU_CHECK_IP4 || CM == FCGPU_CHECK_AUTO),
-                             RxLaunchTab>),
-                       dim3(grid), dim3(kTile), lds, s, L);
-}
-template <int PART>
-static void launch_tab_part(uint32_t cm, bool ck, const RxLaunchTab &L, uint32_t grid, hipStream_t s) {
-    switch (cm * 2 + (ck ? 1 : 0)) {
-    case 0: launch_tab<FCGPU_CHECK_IP4, false, PART>(L, grid, s); break;
-    case 1: launch_tab<FCGPU_CHECK_IP4, true, PART>(L, grid, s); break;
-    case 2: case 3: launch_tab<FCGPU_MARK_IP4, false, PART>(L, grid, s); break;
-    case 4: launch_tab<FCGPU_CHECK_AUTO, false, PART>(L, grid, s); break;
-    case 6: case 7: launch_tab<FCGPU_MARK_IP6, false, PART>(L, grid, s); break;
-    default: launch_tab<FCGPU_CHECK_AUTO, true, PART>(L, grid, s); break;
-    }
-}
-}  // extern "C++"
-
-// One planned fused launch from its device table: process_fused without the
-// flow table and whole-batch partition parts (tab_ok), same timing rules.
-static int run_tab(fcgpu_ctx *c, const PlanGroup &G) {
-    const uint32_t g = (uint32_t)G.jobs.size();
-    RxLaunchTab L;
-    RxArgs &a = L.A;
-    a = RxArgs{};
-    a.tilecnt = c->d_tilecnt;
-    a.ctr = c->d_ctr;
-    a.cfg = c->dcfg;
-    a.fl = c->fl;
-    a.arena = G.jobs[0].arena;
-    a.desc = reinterpret_cast<const uint2 *>(G.jobs[0].desc);
-    a.n = G.jobs[0].n;
-    a.ntiles = (a.n + kTile - 1) / kTile;
-    L.njobs = g;
-    L.job_tiles = G.job_tiles;
-    L.flow_stride = L.flow_words = 0;
-    L.tab = G.d_tab;
-    const uint64_t before = c->timing_seq;
-    bool timed = false;
-    if (c->timing_every) {
-        c->timing_seq += g;
-        timed = before / c->timing_every != c->timing_seq / c->timing_every;
-    }
-    EvPair ev;
-    if (timed) { ev.a = take_event(c); ev.b = take_event(c); ev.stage = 0; ev.batches = g; }
-    if (timed) HIPCHK(c, hipEventRecord(ev.a, G.s));
-    const int part = out_part(&G.jobs[0].out);
-    const uint32_t cm = c->cfg.check_mode;
-    const bool ck = c->cfg.checksum != 0;
-    if (part == kPartTile) launch_tab_part<kPartTile>(cm, ck, L, G.tiles, G.s);
-    else launch_tab_part<kPartNone>(cm, ck, L, G.tiles, G.s);
-    if (timed) HIPCHK(c, hipEventRecord(ev.b, G.s));
-    HIPCHK(c, hipGetLastError());
-    if (timed) c->pending.push_back(ev);
-    return FCGPU_OK;
-}
-
-int fcgpu_run_plan(fcgpu_ctx *c, fcgpu_plan *P) {
-    if (!c || !P) return FCGPU_EINVAL;
-    HIPCHK(c, hipSetDevice(c->device));
-    for (const PlanGroup &G : P->groups) {
-        const uint32_t g = (uint32_t)G.jobs.size();
-        int rc;
-        // the table holds only the jobs' pointers: it serves whatever the
-        // context's configuration is now, when that configuration is one
-        // the table launch covers
-        if (G.d_tab && tab_ok(c, out_part(&G.jobs[0].out))) {
-            rc = run_tab(c, G);
-        } else if (g == 1) {
-            const fcgpu_job &j = G.jobs[0];
-            rc = check_process(c, j.arena, j.desc, j.n, &j.out);
-            if (rc == FCGPU_OK) rc = process_one(c, j.arena, j.desc, j.n, &j.out, G.s);
-        } else {
-            // not table-eligible (now): the ordinary path, checked again
-            std::vector<const fcgpu_job *> grp;
-            for (const fcgpu_job &j : G.jobs) {
-                rc = check_process(c, j.arena, j.desc, j.n, &j.out);
-                if (rc != FCGPU_OK) return rc;
-                grp.push_back(&j);
-            }
-            rc = process_fused(c, grp.data(), g, G.s);
-        }
-        if (rc != FCGPU_OK) return rc;
-    }
-    return FCGPU_OK;
-}
-
-void fcgpu_plan_free(fcgpu_ctx *c, fcgpu_plan *P) {
-    if (!P) return;
-    if (c && c->device >= 0) hipSetDevice(c->device);
-    bool synced = false;
-    for (PlanGroup &G : P->groups)
-        if (G.d_tab) {
-            if (!synced) {              // a launch still reading the table finishes first
-                hipDeviceSynchronize();
-                synced = true;
-            }
-            hipFree(G.d_tab);
-        }
-    delete P;
 }
 
 static int slot_alloc(fcgpu_ctx *c, HostSlot &sl, uint32_t cap) {

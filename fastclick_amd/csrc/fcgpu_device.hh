@@ -1258,24 +1258,11 @@ struct RxLaunch {
     // packets (j x flow_words mask words, missed + j) past A.fl's
     uint32_t flow_stride, flow_words;
     RxJob job[kMaxFuse];
-    __device__ const RxJob &job_at(uint32_t j) const { return job[j]; }
-};
-// The same launch with the batches' table in device memory (a plan,
-// fcgpu_plan_jobs: a fixed set of rx-ring slots whose table is uploaded once):
-// ~0.4 KB of kernel arguments instead of ~2.7 KB; each workgroup reads its
-// batch's entry with scalar loads (no flow table: RxLaunch only).
-struct RxLaunchTab {
-    RxArgs A;
-    uint32_t njobs;
-    uint32_t job_tiles;
-    uint32_t flow_stride, flow_words;
-    const RxJob *tab;        // [njobs], device memory
-    __device__ const RxJob &job_at(uint32_t j) const { return tab[j]; }
 };
 
 template <int CM, bool CK, int PART, bool PROG, bool L4, bool FLOW = false,
-          bool FAST = (CM == FCGPU_CHECK_IP4 || CM == FCGPU_CHECK_AUTO), class LT = RxLaunch>
-__global__ __launch_bounds__(kTile, 8) void k_rx(LT L) {
+          bool FAST = (CM == FCGPU_CHECK_IP4 || CM == FCGPU_CHECK_AUTO)>
+__global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4 * kWave * kWin];
     __shared__ uint32_t s_cnt[4][kMaxBins];
     extern __shared__ uint4 s_prog[];           // prog_lds_bytes(cfg) at launch: program steps or CRC tables
@@ -1292,10 +1279,10 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(LT L) {
             j = blockIdx.x / L.job_tiles;
             t = blockIdx.x - j * L.job_tiles;
         } else {
-            for (uint32_t k = 1; k < L.njobs; ++k) j = blockIdx.x >= L.job_at(k).tile0 ? k : j;
-            t = blockIdx.x - L.job_at(j).tile0;
+            for (uint32_t k = 1; k < L.njobs; ++k) j = blockIdx.x >= L.job[k].tile0 ? k : j;
+            t = blockIdx.x - L.job[j].tile0;
         }
-        const RxJob &J = L.job_at(j);
+        const RxJob &J = L.job[j];
         V.arena = J.arena;
         V.desc = J.desc;
         V.verdict = J.verdict;

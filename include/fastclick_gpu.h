@@ -279,25 +279,6 @@ typedef struct fcgpu_job {
 } fcgpu_job;
 int  fcgpu_process_jobs(fcgpu_ctx *ctx, const fcgpu_job *jobs, uint32_t njobs, void *stream);
 
-/* A fixed job list submitted again and again -- an rx ring whose slots keep
- * their arena, descriptor and output buffers (FromDPDKDevice's ring,
- * elements/userlevel/fromdpdkdevice.cc:374-456): fcgpu_plan_jobs checks the
- * jobs and decides their launches once, as fcgpu_process_jobs would, and
- * uploads each fused launch's per-batch table to device memory, so that
- * fcgpu_run_plan passes one pointer where fcgpu_process_jobs passes the whole
- * table as kernel arguments (~0.4 KB instead of ~2.7 KB per launch; less host
- * enqueue per launch). Every fcgpu_run_plan is exactly
- * fcgpu_process_jobs(ctx, jobs, njobs, stream) on the jobs as they were
- * planned (the job array may be freed after planning; the buffers it points
- * at must stay). The device table is used for launches without a flow table,
- * a decision program, an L4 check or a whole-batch partition; the others
- * (and every launch after fcgpu_configure changes the context) take
- * fcgpu_process_jobs's path. */
-typedef struct fcgpu_plan fcgpu_plan;
-int  fcgpu_plan_jobs(fcgpu_ctx *ctx, const fcgpu_job *jobs, uint32_t njobs, void *stream, fcgpu_plan **out);
-int  fcgpu_run_plan(fcgpu_ctx *ctx, fcgpu_plan *plan);
-void fcgpu_plan_free(fcgpu_ctx *ctx, fcgpu_plan *plan);
-
 /* Host-resident batch: frames[i] points at packet i's data (length lens[i]).
  * The first min(len, 128) bytes of every frame are gathered into pinned
  * staging, copied H2D, processed, and the requested outputs copied D2H into the

@@ -378,9 +378,8 @@ def test_process_jobs_fused_global_large(dev, oracle):
         ctx.close()
 
 
-@pytest.mark.parametrize("submit", ["jobs", "plan"])
 @pytest.mark.parametrize("partition", [N.PART_TILE, N.PART_GLOBAL, None])
-def test_process_jobs_fused(dev, oracle, partition, submit):
+def test_process_jobs_fused(dev, oracle, partition):
     """fcgpu_process_jobs fuses a stream's consecutive jobs with disjoint
     outputs into one k_rx launch (up to 24 batches, the grid their tiles end
     to end): 30 ragged batches (1 .. 30,001 packets, one empty) on one stream
@@ -389,10 +388,7 @@ def test_process_jobs_fused(dev, oracle, partition, submit):
     later one's results are what the set holds, as with one call per job.
     PART_GLOBAL: the whole-batch partitions of a fused launch (one scan and
     one scatter launch for all its batches); odd batches ask for port_start
-    only (one scatter workgroup each).
-    submit "plan": the same jobs planned once (fcgpu_plan_jobs: the fused
-    launches' tables in device memory; the whole-batch partition takes the
-    ordinary path) and run twice -- the same results, the counters twice."""
+    only (one scatter workgroup each)."""
     import torch
     from fastclick_amd.device import DeviceBatch, DeviceOutputs
     cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16, badsrc=BADSRC)
@@ -417,26 +413,10 @@ def test_process_jobs_fused(dev, oracle, partition, submit):
             outs.append(o)
             specs.append((b.arena.data_ptr(), b.desc.data_ptr(), b.n, None, o.ptrs()))
         ctx.set_timing(1)
-        runs = 1
-        if submit == "jobs":
-            ctx.run_jobs(ctx.jobs(specs))
-        else:
-            plan = ctx.plan(ctx.jobs(specs))
-            for o in outs:                      # the second run must rewrite every output
-                for t in (o.verdict, o.hash, o.tile_count, o.tile_perm, o.perm):
-                    if t is not None:
-                        t.fill_(-1)
-            ctx.run_plan(plan)
-            torch.cuda.synchronize()
-            for o in outs:
-                for t in (o.verdict, o.hash, o.tile_count, o.tile_perm, o.perm):
-                    if t is not None:
-                        t.fill_(-1)
-            ctx.run_plan(plan)
-            runs = 2
+        ctx.run_jobs(ctx.jobs(specs))
         torch.cuda.synchronize()
         ms, cnt = ctx.read_timing()
-        assert cnt[0] == runs * sum(1 for n in sizes if n)   # timing counts batches
+        assert cnt[0] == sum(1 for n in sizes if n)          # timing counts batches
         ctx.set_timing(0)
         for k, (b, o) in enumerate(zip(batches, outs)):
             if b.n == 0:
@@ -455,7 +435,7 @@ def test_process_jobs_fused(dev, oracle, partition, submit):
                 if k % 2 == 0:
                     assert np.array_equal(got["perm"][:b.n], exp["perm"]), k
         want = sum(e["counters"].astype(np.int64) for e, b in zip(exps, batches) if b.n)
-        assert np.array_equal(np.array(ctx.counters(), np.int64), runs * want)
+        assert np.array_equal(np.array(ctx.counters(), np.int64), want)
         # two jobs on one output set: sequential semantics (the second wins)
         shared = DeviceOutputs(40_000, 16, device="cuda:0", perm=tile, anno=False,
                                partition=N.PART_TILE if tile else N.PART_GLOBAL, port_start=False)
@@ -471,13 +451,13 @@ def test_process_jobs_fused(dev, oracle, partition, submit):
         ctx.close()
 
 
-@pytest.mark.parametrize("mode", ["c5_auto", "mark_crc", "ipclass_fallback"])
-def test_plan_equal_batches(dev, oracle, mode):
-    """fcgpu_run_plan over 24 equal batches (one launch, the table's
-    equal-tile division) and a ragged tail batch: C5's StripEtherVLANHeader +
-    IPv4/IPv6 dispatch, MarkIPHeader + LB_MODE hash_crc (LDS tables), and an
-    IPClassifier program (not table-eligible: the plan takes the
-    fcgpu_process_jobs path) -- every batch's results are the oracle's."""
+@pytest.mark.parametrize("mode", ["c5_auto", "mark_crc", "ipclass"])
+def test_process_jobs_fused_equal_batches(dev, oracle, mode):
+    """One fused k_rx launch over 24 equal batches (the equal-tile division of
+    the grid) plus a ragged tail batch in another launch: C5's
+    StripEtherVLANHeader + IPv4/IPv6 dispatch, MarkIPHeader + LB_MODE
+    hash_crc (LDS tables), an IPClassifier program -- every batch's results
+    are the oracle's."""
     import torch
     from fastclick_amd import click
     from fastclick_amd.device import DeviceBatch, DeviceOutputs
@@ -504,12 +484,11 @@ def test_plan_equal_batches(dev, oracle, mode):
         outs = [DeviceOutputs(b.n, 16, device="cuda:0", perm=True, anno=False, partition=N.PART_TILE)
                 for b in dbs]
         specs = [(b.arena.data_ptr(), b.desc.data_ptr(), b.n, None, o.ptrs()) for b, o in zip(dbs, outs)]
-        plan = ctx.plan(ctx.jobs(specs))
-        ctx.run_plan(plan)
+        ctx.run_jobs(ctx.jobs(specs))
         torch.cuda.synchronize()
         for k, (b, o) in enumerate(zip(batches, outs)):
             got = o.numpy()
-            exp = oracle.process_batch(cfg, b, program=program) if program else oracle.process_batch(cfg, b)
+            exp = oracle.process_batch(cfg, b, program=program)
             for key in ("reason", "port", "perm_tile"):
                 assert np.array_equal(got[key][:b.n], exp[key]), (mode, k, key)
             ok = exp["reason"] == N.R_OK
