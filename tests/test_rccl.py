@@ -75,7 +75,8 @@ def test_gpu_rccl_world1_counter_allreduce_and_gather():
     r = subprocess.run([sys.executable, "-c", CHILD, ROOT], env=env, capture_output=True, text=True,
                        timeout=200)
     assert r.returncode == 0, r.stderr[-3000:]
-    out = json.loads(r.stdout.strip().splitlines()[-1])
+    # RCCL's log shares stdout: the child's result is its JSON line
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert out["backend"] == "nccl" and out["world"] == 1 and out["on_device"]
     assert out["tot"] == out["want"]
     assert out["before"] == [0] * len(out["counts"]) and out["gtot"] == out["counts"]
@@ -86,3 +87,6 @@ def test_gpu_rccl_world1_counter_allreduce_and_gather():
     for op in ("AllReduce", "AllGather"):
         assert op in log, f"no {op} in RCCL's log:\n" + log[-2000:]
     print(f"RCCL {out['rccl']}: world-1 communicator on cuda:0; AllReduce + AllGather issued")
+    for ln in log.splitlines():           # the evidence, in the test's own output (-v -s)
+        if "NCCL INFO" in ln and any(k in ln for k in ("AllReduce", "AllGather", "Init COMPLETE", "RCCL version")):
+            print(ln)
