@@ -165,6 +165,20 @@ WORKLOADS = {
 }
 
 
+KERNEL_SOURCES = ("fastclick_amd/csrc/fcgpu_device.hh", "fastclick_amd/csrc/fcgpu_api.hip")
+
+
+def kernel_source_sha() -> str:
+    """Hash of the k_rx sources: the stored PMC traffic (profiles/pmc_traffic.json)
+    counts only while the kernel it was measured on is the one running."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, p), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def ipclass16_program():
     """The survey's 16-output IPClassifier as compiled by the reference (text)."""
     with open(os.path.join(ROOT, "tests", "golden", "reftests.json")) as f:
@@ -645,17 +659,25 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
         basis = "kernel" if nstreams == 1 else "step"
         t_launch = kernel_s if basis == "kernel" else step_s
         achieved = PKT_BYTES_READ * per_gpu / t_launch / 1e9
-        traffic = None
+        traffic, traffic_src = None, None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
+            # the stored PMC figure (rocprofv3 cannot run inside the bench) counts
+            # only for this workload and only while the kernel sources are the
+            # ones it was measured on
             if tj.get("packets") == per_gpu and tj.get("workload", "c2") == args.workload \
                     and tj.get("frame_bytes", 64) == args.frame_bytes:
-                traffic = tj.get("hbm_bytes_per_launch")
+                if tj.get("source_sha16") == kernel_source_sha():
+                    traffic = tj.get("hbm_bytes_per_launch")
+                    traffic_src = tj.get("source")
+                else:
+                    traffic_src = "stale: profiles/pmc_traffic.json was measured on other kernel sources"
         except Exception:
             pass
         roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, kernel="k_rx", basis=basis,
+                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=traffic_src,
+                    kernel="k_rx", basis=basis,
                     bytes_per_launch=PKT_BYTES_READ * per_gpu,
                     per="batch (a k_rx launch carries up to config.batches_per_launch batches: "
                         "kernel_ms = the sampled launches' event time in the timed region / their batches)",
