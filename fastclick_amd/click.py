@@ -32,9 +32,10 @@ def load():
     if _lib is not None:
         return _lib
     N.load()   # libfcgpu.so first (same HIP runtime as torch), then the harness
-    if not os.path.exists(N.LIBFCCLICK):
-        raise N.NativeMissing(f"{N.LIBFCCLICK} not built (run __graft_entry__.build())")
-    lib = C.CDLL(N.LIBFCCLICK)
+    path = os.environ.get("FCCLICK_LIB", N.LIBFCCLICK)   # FCCLICK_LIB: an A/B build of the harness
+    if not os.path.exists(path):
+        raise N.NativeMissing(f"{path} not built (run __graft_entry__.build())")
+    lib = C.CDLL(path)
     lib.fcclick_check_config.restype = C.c_int
     lib.fcclick_check_config.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t]
     lib.fcclick_element_cfg.restype = C.c_int

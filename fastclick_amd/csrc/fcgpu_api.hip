@@ -165,6 +165,8 @@ struct SpanSlot {
     uint8_t *d_in = nullptr, *d_res = nullptr;   // block submissions
     size_t in_cap = 0, res_cap = 0;
     bool busy = false;
+    hipEvent_t done = nullptr;   // shared streams: the slot's last operation (else the stream is waited)
+    bool evt = false;            // the last submission recorded `done`
 };
 
 inline uint32_t span(uint32_t n, uint32_t part, uint32_t np) { return (uint32_t)((uint64_t)n * part / np); }
@@ -224,6 +226,7 @@ struct fcgpu_ctx {
     Pool pool;
     // fcgpu_span_submit slots
     SpanSlot span[FCGPU_SPAN_SLOTS];
+    int span_index = -1;              // FCGPU_SPAN_STREAMS=shared:N: this context's place in the pool
     // flow table (fcgpu_flow_enable)
     uint32_t max_flows = 0, flow_slots = 0, flow_words = 0;
     FlowArgs fl{};            // device pointers; fl.slots == nullptr: disabled
@@ -911,6 +914,7 @@ void fcgpu_close(fcgpu_ctx *c) {
                             (void *)sp.d_tp, (void *)sp.d_in, (void *)sp.d_res})
                 hipFree(p);
             if (sp.own) hipStreamDestroy(sp.own);
+            if (sp.done) hipEventDestroy(sp.done);
         }
         flow_free(c);
         hipFree(c->d_mptr);
@@ -1711,6 +1715,7 @@ int fcgpu_span_submit(fcgpu_ctx *c, uint32_t slot, const uint8_t *h_span, size_t
         (rc = back(h->tile_perm, sp.d_tp, n)) || (rc = back(h->flowid, sp.d_fl, sizeof(uint32_t) * n)) ||
         (rc = back(h->ip_rw, sp.d_rw, sizeof(uint32_t) * n)))
         return rc;
+    sp.evt = false;
     sp.busy = true;
     return FCGPU_OK;
 }
@@ -1719,7 +1724,7 @@ int fcgpu_span_poll(fcgpu_ctx *c, uint32_t slot) {
     if (!c || slot >= FCGPU_SPAN_SLOTS) return FCGPU_EINVAL;
     SpanSlot &sp = c->span[slot];
     if (!sp.busy) return 1;
-    const hipError_t e = hipStreamQuery(sp.s);
+    const hipError_t e = sp.evt ? hipEventQuery(sp.done) : hipStreamQuery(sp.s);
     if (e == hipSuccess) return 1;
     if (e == hipErrorNotReady) return 0;
     return fail(c, FCGPU_ERUNTIME, std::string("hipStreamQuery: ") + hipGetErrorString(e));
@@ -1749,6 +1754,56 @@ int fcgpu_block_layout_for(const fcgpu_ctx *c, uint32_t n, uint32_t outputs, uin
     return FCGPU_OK;
 }
 
+// The stream a span slot's copies and kernels go on. FCGPU_SPAN_STREAMS
+// (read once): "slot" (default) -- a stream per slot; "ctx" -- one per
+// context (its slots share it); "shared:N" -- N streams per device shared by
+// every context of the process, slot k of the i-th context on stream
+// (2i + k) mod N. Fewer streams are fewer hardware (compute and SDMA) queues
+// for the runtime to map; the context's own work still completes in order.
+static std::mutex g_span_mu;
+static std::map<int, std::vector<hipStream_t>> g_span_shared;
+static uint32_t g_span_ctx_seq = 0;
+static int span_stream_mode(uint32_t &nshared) {
+    static int mode = -1;
+    static uint32_t ns = 0;
+    if (mode < 0) {
+        const char *e = getenv("FCGPU_SPAN_STREAMS");
+        mode = 0;
+        if (e && !strcmp(e, "ctx")) mode = 1;
+        else if (e && !strncmp(e, "shared:", 7)) {
+            const long v = atol(e + 7);
+            if (v >= 1 && v <= 64) { mode = 2; ns = (uint32_t)v; }
+        }
+    }
+    nshared = ns;
+    return mode;
+}
+static hipError_t span_stream(fcgpu_ctx *c, uint32_t slot, hipStream_t *out) {
+    uint32_t ns = 0;
+    const int mode = span_stream_mode(ns);
+    SpanSlot &sp = c->span[slot];
+    if (mode == 0 || (mode == 1 && slot == 0)) {
+        if (!sp.own) {
+            hipError_t e = hipStreamCreateWithFlags(&sp.own, hipStreamNonBlocking);
+            if (e != hipSuccess) return e;
+        }
+        *out = sp.own;
+        return hipSuccess;
+    }
+    if (mode == 1) return span_stream(c, 0, out);
+    std::lock_guard<std::mutex> g(g_span_mu);
+    if (c->span_index < 0) c->span_index = (int)g_span_ctx_seq++;
+    auto &pool = g_span_shared[c->device];
+    while (pool.size() < ns) {
+        hipStream_t st = nullptr;
+        hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+        if (e != hipSuccess) return e;
+        pool.push_back(st);
+    }
+    *out = pool[((uint32_t)c->span_index * FCGPU_SPAN_SLOTS + slot) % ns];
+    return hipSuccess;
+}
+
 int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_t in_bytes, size_t desc_off,
                             size_t frames_off, uint32_t n, void *h_out, uint32_t outputs, uint32_t partition) {
     if (!c || slot >= FCGPU_SPAN_SLOTS || (n && (!h_in || !h_out))) return FCGPU_EINVAL;
@@ -1761,9 +1816,10 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
     fcgpu_block_layout L;
     if (fcgpu_block_layout_for(c, n, outputs, partition, &L) != FCGPU_OK) return fail(c, FCGPU_EINVAL, "bad block layout");
     HIPCHK(c, hipSetDevice(c->device));
-    if (!sp.own) HIPCHK(c, hipStreamCreateWithFlags(&sp.own, hipStreamNonBlocking));
+    hipStream_t ss = nullptr;
+    HIPCHK(c, span_stream(c, slot, &ss));
     if (in_bytes + kArenaPad > sp.in_cap) {
-        HIPCHK(c, hipStreamSynchronize(sp.own));
+        HIPCHK(c, hipStreamSynchronize(ss));
         hipFree(sp.d_in);
         sp.d_in = nullptr;
         sp.in_cap = 0;
@@ -1773,7 +1829,7 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
         sp.in_cap = cap;
     }
     if (L.bytes > sp.res_cap) {
-        HIPCHK(c, hipStreamSynchronize(sp.own));
+        HIPCHK(c, hipStreamSynchronize(ss));
         hipFree(sp.d_res);
         sp.d_res = nullptr;
         sp.res_cap = 0;
@@ -1784,7 +1840,7 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
         sp.res_cap = cap;
     }
     if (c->fl.slots && !c->stream) HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    sp.s = c->fl.slots ? c->stream : sp.own;
+    sp.s = c->fl.slots ? c->stream : ss;
     hipStream_t s = sp.s;
     if (n == 0) return FCGPU_OK;
     HIPCHK(c, hipMemcpyAsync(sp.d_in, h_in, in_bytes, hipMemcpyHostToDevice, s));
@@ -1803,6 +1859,15 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
     int rc = fcgpu_process(c, sp.d_in + frames_off, reinterpret_cast<const uint32_t *>(sp.d_in + desc_off), n, &d, s);
     if (rc != FCGPU_OK) return rc;
     HIPCHK(c, hipMemcpyAsync(h_out, sp.d_res, L.bytes, hipMemcpyDeviceToHost, s));
+    uint32_t ns = 0;
+    if (span_stream_mode(ns) != 0 && !c->fl.slots) {
+        // a stream other slots also use: wait for this slot's work alone
+        if (!sp.done) HIPCHK(c, hipEventCreateWithFlags(&sp.done, hipEventDisableTiming));
+        HIPCHK(c, hipEventRecord(sp.done, s));
+        sp.evt = true;
+    } else {
+        sp.evt = false;
+    }
     sp.busy = true;
     return FCGPU_OK;
 }
@@ -1813,7 +1878,8 @@ int fcgpu_span_wait(fcgpu_ctx *c, uint32_t slot) {
     if (!sp.busy) return FCGPU_OK;
     HIPCHK(c, hipSetDevice(c->device));
     sp.busy = false;
-    HIPCHK(c, hipStreamSynchronize(sp.s));
+    if (sp.evt) HIPCHK(c, hipEventSynchronize(sp.done));
+    else HIPCHK(c, hipStreamSynchronize(sp.s));
     return FCGPU_OK;
 }
 
