@@ -115,12 +115,16 @@ static double run(Kern k, const uint8_t *base, const uint32_t *doff, uint32_t n,
 
 int main(int argc, char **argv) {
     const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : (1u << 18);
-    const size_t stride = 2304;
+    // argv[2]: stride between pieces (2304 = rte_mbuf element; 64 = the
+    // element's packed staging records); argv[3] = 0: pieces in address order
+    const size_t stride = argc > 2 ? (size_t)atoi(argv[2]) : 2304;
+    const bool shuffled = argc > 3 ? atoi(argv[3]) != 0 : true;
     const size_t bytes = stride * n + 4096;
     std::vector<uint32_t> off(n);
-    for (uint32_t i = 0; i < n; ++i) off[i] = (uint32_t)(i * stride + 256);   // data after header + headroom
+    for (uint32_t i = 0; i < n; ++i) off[i] = (uint32_t)(i * stride + (stride >= 2304 ? 256 : 0));   // data after header + headroom
     std::mt19937 rng(1);
-    std::shuffle(off.begin(), off.end(), rng);
+    if (shuffled) std::shuffle(off.begin(), off.end(), rng);
+    printf("# %u pieces, stride %zu B, %s\n", n, stride, shuffled ? "shuffled" : "in address order");
     uint32_t *doff, *dout;
     CK(hipMalloc(&doff, 4ull * n));
     CK(hipMalloc(&dout, 4ull * n));
