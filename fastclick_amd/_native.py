@@ -15,8 +15,10 @@ LIBFCGPU = os.environ.get("FCGPU_LIB") or os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 15
+ABI_VERSION = 16
 SPAN_SLOTS = 3
+SPAN_COPY = 0
+SPAN_ZEROCOPY = 1
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
     R_BAD_IP6, R_VLAN_REJECT, R_NO_MATCH, R_L4_PROTO, R_L4_LENGTH, R_L4_CKSUM, \
@@ -192,6 +194,7 @@ FCGPU_SYMBOLS = {
                                     C.POINTER(fcgpu_out)]),
     "fcgpu_span_wait": (C.c_int, [C.c_void_p, C.c_uint32]),
     "fcgpu_span_poll": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "fcgpu_span_mode": (C.c_int, [C.c_void_p, C.c_uint32]),
     "fcgpu_block_layout_for": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]),
     "fcgpu_span_submit_block": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t,
                                           C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32]),

@@ -164,6 +164,9 @@ struct SpanSlot {
     uint8_t *d_tp = nullptr;
     uint8_t *d_in = nullptr, *d_res = nullptr;   // block submissions
     size_t in_cap = 0, res_cap = 0;
+    // zero-copy block submissions: the device addresses of the last h_in / h_out
+    const void *zc_hin = nullptr, *zc_hout = nullptr;
+    uint8_t *zc_din = nullptr, *zc_dout = nullptr;
     bool busy = false;
     hipEvent_t done = nullptr;   // shared streams: the slot's last operation (else the stream is waited)
     bool evt = false;            // the last submission recorded `done`
@@ -227,6 +230,7 @@ struct fcgpu_ctx {
     // fcgpu_span_submit slots
     SpanSlot span[FCGPU_SPAN_SLOTS];
     int span_index = -1;              // FCGPU_SPAN_STREAMS=shared:N: this context's place in the pool
+    uint32_t span_mode = FCGPU_SPAN_COPY;   // fcgpu_span_mode: block submissions copied or read in place
     // flow table (fcgpu_flow_enable)
     uint32_t max_flows = 0, flow_slots = 0, flow_words = 0;
     FlowArgs fl{};            // device pointers; fl.slots == nullptr: disabled
@@ -1720,6 +1724,14 @@ int fcgpu_span_submit(fcgpu_ctx *c, uint32_t slot, const uint8_t *h_span, size_t
     return FCGPU_OK;
 }
 
+int fcgpu_span_mode(fcgpu_ctx *c, uint32_t mode) {
+    if (!c || mode > FCGPU_SPAN_ZEROCOPY) return FCGPU_EINVAL;
+    for (const SpanSlot &sp : c->span)
+        if (sp.busy) return fail(c, FCGPU_EINVAL, "fcgpu_span_mode: a span slot is in flight");
+    c->span_mode = mode;
+    return FCGPU_OK;
+}
+
 int fcgpu_span_poll(fcgpu_ctx *c, uint32_t slot) {
     if (!c || slot >= FCGPU_SPAN_SLOTS) return FCGPU_EINVAL;
     SpanSlot &sp = c->span[slot];
@@ -1818,7 +1830,29 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t ss = nullptr;
     HIPCHK(c, span_stream(c, slot, &ss));
-    if (in_bytes + kArenaPad > sp.in_cap) {
+    const bool zc = c->span_mode == FCGPU_SPAN_ZEROCOPY;
+    if (zc) {
+        // the kernels read h_in and write h_out where they lie (page-locked
+        // memory mapped into the device's address space): no copy engine
+        if (h_in != sp.zc_hin) {
+            void *d = nullptr;
+            if (hipHostGetDevicePointer(&d, const_cast<void *>(h_in), 0) != hipSuccess || !d) {
+                (void)hipGetLastError();
+                return fail(c, FCGPU_EINVAL, "zero-copy block: h_in is not page-locked host memory (fcgpu_host_alloc)");
+            }
+            sp.zc_hin = h_in;
+            sp.zc_din = static_cast<uint8_t *>(d);
+        }
+        if (h_out != sp.zc_hout) {
+            void *d = nullptr;
+            if (hipHostGetDevicePointer(&d, h_out, 0) != hipSuccess || !d) {
+                (void)hipGetLastError();
+                return fail(c, FCGPU_EINVAL, "zero-copy block: h_out is not page-locked host memory (fcgpu_host_alloc)");
+            }
+            sp.zc_hout = h_out;
+            sp.zc_dout = static_cast<uint8_t *>(d);
+        }
+    } else if (in_bytes + kArenaPad > sp.in_cap) {
         HIPCHK(c, hipStreamSynchronize(ss));
         hipFree(sp.d_in);
         sp.d_in = nullptr;
@@ -1828,7 +1862,7 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
         HIPCHK(c, memset_sync(sp.d_in, 0, cap));
         sp.in_cap = cap;
     }
-    if (L.bytes > sp.res_cap) {
+    if (!zc && L.bytes > sp.res_cap) {
         HIPCHK(c, hipStreamSynchronize(ss));
         hipFree(sp.d_res);
         sp.d_res = nullptr;
@@ -1843,8 +1877,9 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
     sp.s = c->fl.slots ? c->stream : ss;
     hipStream_t s = sp.s;
     if (n == 0) return FCGPU_OK;
-    HIPCHK(c, hipMemcpyAsync(sp.d_in, h_in, in_bytes, hipMemcpyHostToDevice, s));
-    auto at = [&](size_t o) -> void * { return o == FCGPU_OUT_ABSENT ? nullptr : sp.d_res + o; };
+    uint8_t *din = zc ? sp.zc_din : sp.d_in, *dres = zc ? sp.zc_dout : sp.d_res;
+    if (!zc) HIPCHK(c, hipMemcpyAsync(sp.d_in, h_in, in_bytes, hipMemcpyHostToDevice, s));
+    auto at = [&](size_t o) -> void * { return o == FCGPU_OUT_ABSENT ? nullptr : dres + o; };
     fcgpu_out d{};
     d.verdict = (uint16_t *)at(L.verdict);
     d.hash = (uint32_t *)at(L.hash);
@@ -1856,9 +1891,9 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
     d.tile_perm = (uint8_t *)at(L.tile_perm);
     d.flowid = (uint32_t *)at(L.flowid);
     d.ip_rw = (uint32_t *)at(L.ip_rw);
-    int rc = fcgpu_process(c, sp.d_in + frames_off, reinterpret_cast<const uint32_t *>(sp.d_in + desc_off), n, &d, s);
+    int rc = fcgpu_process(c, din + frames_off, reinterpret_cast<const uint32_t *>(din + desc_off), n, &d, s);
     if (rc != FCGPU_OK) return rc;
-    HIPCHK(c, hipMemcpyAsync(h_out, sp.d_res, L.bytes, hipMemcpyDeviceToHost, s));
+    if (!zc) HIPCHK(c, hipMemcpyAsync(h_out, sp.d_res, L.bytes, hipMemcpyDeviceToHost, s));
     uint32_t ns = 0;
     if (span_stream_mode(ns) != 0 && !c->fl.slots) {
         // a stream other slots also use: wait for this slot's work alone

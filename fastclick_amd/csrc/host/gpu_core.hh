@@ -73,6 +73,9 @@
 //   MODE CHECK|MARK|AUTO, HASH NONE|FLOWID|FLOW5ID, STRIP, DEVICE,
 //   BATCH (packets per device batch, default 16384; 0: each incoming
 //   PacketBatch is one), TIMER (us, default 100; -1 none),
+//   ZEROCOPY (default false): the device reads each slot's staged block and
+//   writes its results in pinned host memory, where they lie (fcgpu_span_mode
+//   FCGPU_SPAN_ZEROCOPY), instead of one H2D and one D2H copy per batch,
 //   PARTITION TILE (default: each 256-packet tile classified as one batch,
 //   one fused launch) | GLOBAL (the whole device batch as one, three launches)
 // Handlers: count, drops, drop_details (DETAILS true), port_counts,
@@ -235,6 +238,8 @@ class RxCore {
             } else if (k == "DEVICE") {
                 if (!parse_int(v, n) || n < 0) return err(errh, "bad DEVICE");
                 _device = (int)n;
+            } else if (k == "ZEROCOPY") {
+                if (!parse_bool(v, _zerocopy)) return err(errh, "ZEROCOPY expects true/false");
             } else if (k == "PARTITION") {
                 if (v == "TILE") _partition = FCGPU_PART_TILE;
                 else if (v == "GLOBAL") _partition = FCGPU_PART_GLOBAL;
@@ -331,6 +336,8 @@ class RxCore {
         if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_open: ") + fcgpu_last_error(nullptr));
         rc = fcgpu_configure(_ctx, &_cfg);
         if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_configure: ") + fcgpu_last_error(_ctx));
+        rc = fcgpu_span_mode(_ctx, _zerocopy ? FCGPU_SPAN_ZEROCOPY : FCGPU_SPAN_COPY);
+        if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_span_mode: ") + fcgpu_last_error(_ctx));
         uint32_t reach = 0;
         if (_cfg.classify == FCGPU_CLS_PROGRAM) {
             // the program as code (fcgpu_program_jit) unless PROGRAM_JIT false;
@@ -847,6 +854,7 @@ class RxCore {
     uint32_t _cap = 0;
     uint32_t _capture = fcgpu::kCaptureMin;
     uint32_t _partition = FCGPU_PART_TILE;
+    bool _zerocopy = false;                      // ZEROCOPY: the kernels read/write the pinned slots in place
     uint32_t _outputs = 0;                       // FCGPU_OUT_* the element asks for
     bool _verbose = false, _details = false, _strip = false, _warned = false;
     std::string _error;                         // under _mu

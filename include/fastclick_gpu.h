@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 15
+#define FCGPU_ABI_VERSION 16
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -339,6 +339,24 @@ int  fcgpu_block_layout_for(const fcgpu_ctx *ctx, uint32_t n, uint32_t outputs, 
 int  fcgpu_span_submit_block(fcgpu_ctx *ctx, uint32_t slot, const void *h_in, size_t in_bytes,
                              size_t desc_off, size_t frames_off, uint32_t n, void *h_out, uint32_t outputs,
                              uint32_t partition);
+
+/* How block submissions reach the device (per context, default COPY):
+ *   FCGPU_SPAN_COPY     -- one H2D copy of h_in and one D2H copy of the
+ *                          results per batch, through the copy engine (the
+ *                          device copy is padded for the header-window reads);
+ *   FCGPU_SPAN_ZEROCOPY -- no copies: the kernels read the descriptors and
+ *                          frames from h_in and write the results into h_out
+ *                          over PCIe, where they lie. Both must be page-locked
+ *                          (fcgpu_host_alloc), and h_in readable 256 bytes past
+ *                          in_bytes (the header-window over-read; those bytes
+ *                          are never part of a verdict). Many contexts
+ *                          submitting small batches share one copy engine;
+ *                          zero-copy batches only queue kernels.
+ * Results are identical in both modes. Returns FCGPU_EINVAL for another mode
+ * or while a slot is in flight. */
+#define FCGPU_SPAN_COPY     0u
+#define FCGPU_SPAN_ZEROCOPY 1u
+int  fcgpu_span_mode(fcgpu_ctx *ctx, uint32_t mode);
 
 /* Decision programs. A program is the step list the
  * reference's own compiler produces and prints through the `program` handler

@@ -1,0 +1,18 @@
+#!/bin/bash
+# round 3, session 9: line-request sizes -- klines (64-B pieces packed vs
+# alone in their 128-B line, five cache policies) timed and under a PMC pass
+# (EA read requests by size); C2/C3/C5 k_rx request sizes; the 1/8 strong
+# shard (131,072 packets, 122 rotating copies) with FETCH_SIZE.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 120 ./scripts/klines > gpurun_out/klines.log 2>&1 || exit $?
+timeout -s KILL 60 rocprofv3 --pmc TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum -f csv -d gpurun_out/pmc_klines -o run -- ./scripts/klines 262144 > gpurun_out/pmc_klines.log 2>&1 || exit $?
+P="--steps 20 --warmup 2 --no-cpu --no-timing --streams 1 --fuse 1"
+for w in c2 c3 c5; do
+  timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --kernel-include-regex k_rx -f csv -d gpurun_out/pmc_rq_$w -o run -- python3 bench.py $P --workload $w > gpurun_out/pmc_rq_$w.log 2>&1 || exit $?
+done
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --workload c4 --shard strong --packets 131072 > gpurun_out/strong131k.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --gpus 1 --steps 200 --warmup 5 --no-cpu --workload c4 --shard strong --packets 131072 > gpurun_out/strong131k_200.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_rx -f csv -d gpurun_out/pmc_strong131k -o run -- python3 bench.py --steps 40 --warmup 2 --no-cpu --no-timing --workload c4 --shard strong --packets 131072 > gpurun_out/pmc_strong131k.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_rx -f csv -d gpurun_out/pmc_strong131k_w -o run -- python3 bench.py --steps 40 --warmup 2 --no-cpu --no-timing --workload c4 --shard strong --packets 131072 > gpurun_out/pmc_strong131k_w.log 2>&1 || exit $?

@@ -377,3 +377,36 @@ def test_element_drop_chatter_text(capfd):
     err = capfd.readouterr().err
     assert "GPUIPCheckClassify: IP header check failed: bad IPv4 checksum" in err
     assert err.count("IP header check failed") == 1      # once, not VERBOSE
+
+
+ZC_CONFS = [
+    ("c4", CONF[:-1] + ", BATCH 4096)", 17),
+    ("c4", CONF[:-1] + ", BATCH 4096, PARTITION GLOBAL)", 17),
+    ("c5", "GPUIPCheckClassify(MODE AUTO, CHECKSUM true, N 8, LB_MODE hash, BATCH 2048)", 9),
+    ("c3", "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4, L4 UDP, BATCH 3000)", 5),
+    ("c4", "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 8, DEC_TTL true, SET_CHECKSUM true, BATCH 4096)", 9),
+    ("c4", "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4, FLOW_CAPACITY 5000, BATCH 4096)", 5),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wl,conf,nsinks", ZC_CONFS)
+def test_element_zerocopy_matches_copy(oracle, wl, conf, nsinks):
+    """ZEROCOPY true (fcgpu_span_mode FCGPU_SPAN_ZEROCOPY: the kernels read the
+    pinned staging block and write the results over PCIe, no copy engine)
+    gives the element's outputs, annotations, rewritten bytes, flow IDs and
+    handlers exactly as the copy mode does, and the oracle's ports."""
+    from fastclick_amd import click as K
+    b = getattr(synth, wl)(12_345, seed=530)
+    if wl != "c5":
+        synth.inject_errors(b, 0.02, seed=531)
+    a = K.run_element(conf, b, burst=32, nsinks=nsinks)
+    z = K.run_element(conf[:-1] + ", ZEROCOPY true)", b, burst=32, nsinks=nsinks)
+    for k in ("port", "seq", "agg", "dst", "len", "nh", "flow", "ip8"):
+        assert np.array_equal(a[k], z[k]), k
+    assert a["handlers"] == z["handlers"]
+    if "FLOW" not in conf and "DEC_TTL" not in conf and "L4" not in conf:
+        cfg = K.element_cfg(conf)
+        e = oracle.process_batch(cfg, b)
+        port = e["port"].astype(np.uint32)
+        assert np.array_equal(z["port"], np.where(port < nsinks, port, 0xFFFFFFFF))
