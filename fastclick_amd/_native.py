@@ -19,6 +19,7 @@ ABI_VERSION = 16
 SPAN_SLOTS = 3
 SPAN_COPY = 0
 SPAN_ZEROCOPY = 1
+SPAN_AUTO = 2
 OK, EINVAL, ENODEV, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4
 R_MINISCULE, R_BAD_VERSION, R_BAD_HLEN, R_BAD_IP_LEN, R_BAD_CKSUM, R_BAD_SADDR, R_OK, \
     R_BAD_IP6, R_VLAN_REJECT, R_NO_MATCH, R_L4_PROTO, R_L4_LENGTH, R_L4_CKSUM, \

@@ -281,6 +281,7 @@ static hipError_t memset_sync(void *p, int v, size_t bytes) {
 }
 
 static std::string g_open_err;
+static void span_auto_count(fcgpu_ctx *c, uint32_t new_mode);
 
 // Pools registered by fcgpu_pool_register, with the number of contexts using each.
 static std::mutex g_pool_mu;
@@ -885,6 +886,7 @@ int fcgpu_flow_count(fcgpu_ctx *c, uint32_t *count) {
 
 void fcgpu_close(fcgpu_ctx *c) {
     if (!c) return;
+    span_auto_count(c, FCGPU_SPAN_COPY);
     if (c->device >= 0) {
         hipSetDevice(c->device);
         if (c->stream) hipStreamSynchronize(c->stream);
@@ -1724,10 +1726,32 @@ int fcgpu_span_submit(fcgpu_ctx *c, uint32_t slot, const uint8_t *h_span, size_t
     return FCGPU_OK;
 }
 
+// FCGPU_SPAN_AUTO: contexts per device in that mode; block submissions go
+// zero-copy while at least kZeroCopyAuto of them exist (one or two threads
+// submit few enough copies for the copy engine, and copies are faster there:
+// profiles/r03_s8/el_zc.log)
+constexpr uint32_t kZeroCopyAuto = 4;
+static std::mutex g_auto_mu;
+static std::map<int, uint32_t> g_auto_ctx;
+static void span_auto_count(fcgpu_ctx *c, uint32_t new_mode) {
+    const bool was = c->span_mode == FCGPU_SPAN_AUTO, now = new_mode == FCGPU_SPAN_AUTO;
+    if (was == now) return;
+    std::lock_guard<std::mutex> g(g_auto_mu);
+    uint32_t &n = g_auto_ctx[c->device];
+    n = now ? n + 1 : (n ? n - 1 : 0);
+}
+static bool span_zerocopy(const fcgpu_ctx *c) {
+    if (c->span_mode != FCGPU_SPAN_AUTO) return c->span_mode == FCGPU_SPAN_ZEROCOPY;
+    std::lock_guard<std::mutex> g(g_auto_mu);
+    auto it = g_auto_ctx.find(c->device);
+    return it != g_auto_ctx.end() && it->second >= kZeroCopyAuto;
+}
+
 int fcgpu_span_mode(fcgpu_ctx *c, uint32_t mode) {
-    if (!c || mode > FCGPU_SPAN_ZEROCOPY) return FCGPU_EINVAL;
+    if (!c || mode > FCGPU_SPAN_AUTO) return FCGPU_EINVAL;
     for (const SpanSlot &sp : c->span)
         if (sp.busy) return fail(c, FCGPU_EINVAL, "fcgpu_span_mode: a span slot is in flight");
+    span_auto_count(c, mode);
     c->span_mode = mode;
     return FCGPU_OK;
 }
@@ -1830,7 +1854,7 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t ss = nullptr;
     HIPCHK(c, span_stream(c, slot, &ss));
-    const bool zc = c->span_mode == FCGPU_SPAN_ZEROCOPY;
+    const bool zc = span_zerocopy(c);
     if (zc) {
         // the kernels read h_in and write h_out where they lie (page-locked
         // memory mapped into the device's address space): no copy engine

@@ -73,9 +73,13 @@
 //   MODE CHECK|MARK|AUTO, HASH NONE|FLOWID|FLOW5ID, STRIP, DEVICE,
 //   BATCH (packets per device batch, default 16384; 0: each incoming
 //   PacketBatch is one), TIMER (us, default 100; -1 none),
-//   ZEROCOPY (default false): the device reads each slot's staged block and
-//   writes its results in pinned host memory, where they lie (fcgpu_span_mode
-//   FCGPU_SPAN_ZEROCOPY), instead of one H2D and one D2H copy per batch,
+//   SLOTS (default 2): device batches a thread stages or has in flight
+//   (double or triple buffering),
+//   ZEROCOPY true|false|auto (default auto): true -- the device reads each
+//   slot's staged block and writes its results in pinned host memory, where
+//   they lie (fcgpu_span_mode FCGPU_SPAN_ZEROCOPY), instead of one H2D and one
+//   D2H copy per batch; auto -- zero-copy while >= 4 element threads share
+//   the GPU (their copies would queue on one copy engine), else copies,
 //   PARTITION TILE (default: each 256-packet tile classified as one batch,
 //   one fused launch) | GLOBAL (the whole device batch as one, three launches)
 // Handlers: count, drops, drop_details (DETAILS true), port_counts,
@@ -103,7 +107,7 @@ class RxCore {
   public:
     using Packet = typename P::Packet;
     using Batch = typename P::Batch;
-    static constexpr uint32_t kSlots = 2;          // batches staged / in flight
+    static constexpr uint32_t kMaxSlots = FCGPU_SPAN_SLOTS;   // batches staged / in flight: SLOTS (2..3)
     static constexpr uint32_t kMaxBatch = 8192;    // MAX_BATCH_SIZE (packetbatch.hh:416)
 
     RxCore() { fcgpu_default_cfg(&_cfg); }
@@ -238,8 +242,13 @@ class RxCore {
             } else if (k == "DEVICE") {
                 if (!parse_int(v, n) || n < 0) return err(errh, "bad DEVICE");
                 _device = (int)n;
+            } else if (k == "SLOTS") {
+                if (!parse_int(v, n) || n < 2 || n > (long)kMaxSlots) return err(errh, "SLOTS expects 2 or 3");
+                _nslots = (uint32_t)n;
             } else if (k == "ZEROCOPY") {
-                if (!parse_bool(v, _zerocopy)) return err(errh, "ZEROCOPY expects true/false");
+                if (v == "auto" || v == "AUTO") _span_mode = FCGPU_SPAN_AUTO;
+                else if (parse_bool(v, b)) _span_mode = b ? FCGPU_SPAN_ZEROCOPY : FCGPU_SPAN_COPY;
+                else return err(errh, "ZEROCOPY expects true, false or auto");
             } else if (k == "PARTITION") {
                 if (v == "TILE") _partition = FCGPU_PART_TILE;
                 else if (v == "GLOBAL") _partition = FCGPU_PART_GLOBAL;
@@ -336,7 +345,7 @@ class RxCore {
         if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_open: ") + fcgpu_last_error(nullptr));
         rc = fcgpu_configure(_ctx, &_cfg);
         if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_configure: ") + fcgpu_last_error(_ctx));
-        rc = fcgpu_span_mode(_ctx, _zerocopy ? FCGPU_SPAN_ZEROCOPY : FCGPU_SPAN_COPY);
+        rc = fcgpu_span_mode(_ctx, _span_mode);
         if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_span_mode: ") + fcgpu_last_error(_ctx));
         uint32_t reach = 0;
         if (_cfg.classify == FCGPU_CLS_PROGRAM) {
@@ -363,8 +372,8 @@ class RxCore {
         fcgpu_block_layout L;
         if (fcgpu_block_layout_for(_ctx, _cap, _outputs, _partition, &L) != FCGPU_OK)
             return err(errh, "fcgpu_block_layout_for failed");
-        for (Slot &s : _slot)
-            if (!s.alloc(_cap, (size_t)_cap * per + 65536, L.bytes))
+        for (uint32_t k = 0; k < _nslots; ++k)
+            if (!_slot[k].alloc(_cap, (size_t)_cap * per + 65536, L.bytes))
                 return err(errh, "cannot allocate pinned staging (fcgpu_host_alloc)");
         return 0;
     }
@@ -372,7 +381,7 @@ class RxCore {
     // Kill whatever is still staged or in flight (router cleanup).
     void release() {
         std::lock_guard<std::mutex> g(_mu);
-        for (uint32_t k = 0; k < kSlots; ++k) {
+        for (uint32_t k = 0; k < _nslots; ++k) {
             Slot &s = _slot[k];
             if (s.inflight && _ctx) fcgpu_span_wait(_ctx, k);
             s.inflight = false;
@@ -407,8 +416,8 @@ class RxCore {
     template <class Emit>
     void flush(Emit &&emit) {
         if (_slot[_cur].n) submit(emit);
-        for (uint32_t k = 0; k < kSlots; ++k) {
-            const uint32_t j = (_cur + k) % kSlots;      // oldest first
+        for (uint32_t k = 0; k < _nslots; ++k) {
+            const uint32_t j = (_cur + k) % _nslots;      // oldest first
             if (_slot[j].inflight) complete(j, emit);
         }
     }
@@ -425,8 +434,8 @@ class RxCore {
             flush(emit);
             return false;
         }
-        for (uint32_t k = 1; k < kSlots; ++k) {
-            const uint32_t j = (_cur + k) % kSlots;      // oldest first
+        for (uint32_t k = 1; k < _nslots; ++k) {
+            const uint32_t j = (_cur + k) % _nslots;      // oldest first
             if (_slot[j].inflight) complete(j, emit);
         }
         return s.n != 0;
@@ -439,7 +448,7 @@ class RxCore {
         for (const Slot &s : _slot) h += s.n;
         return h;
     }
-    uint32_t max_held() const { return kSlots * (_cap ? _cap : (_batch ? _batch : 65536)); }
+    uint32_t max_held() const { return _nslots * (_cap ? _cap : (_batch ? _batch : 65536)); }
     bool idle() const {
         for (const Slot &s : _slot)
             if (s.n || s.inflight) return false;
@@ -618,7 +627,7 @@ class RxCore {
                 s.inflight = true;
             }
         }
-        _cur = (_cur + 1) % kSlots;
+        _cur = (_cur + 1) % _nslots;
         if (_slot[_cur].inflight) complete(_cur, emit);
     }
 
@@ -854,12 +863,13 @@ class RxCore {
     uint32_t _cap = 0;
     uint32_t _capture = fcgpu::kCaptureMin;
     uint32_t _partition = FCGPU_PART_TILE;
-    bool _zerocopy = false;                      // ZEROCOPY: the kernels read/write the pinned slots in place
+    uint32_t _span_mode = FCGPU_SPAN_AUTO;       // ZEROCOPY: the kernels read/write the pinned slots in place
     uint32_t _outputs = 0;                       // FCGPU_OUT_* the element asks for
     bool _verbose = false, _details = false, _strip = false, _warned = false;
     std::string _error;                         // under _mu
     mutable std::mutex _mu;                     // the context and _error (see counters())
-    Slot _slot[kSlots];
+    Slot _slot[kMaxSlots];
+    uint32_t _nslots = 2;
     uint32_t _cur = 0;
 };
 

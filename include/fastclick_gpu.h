@@ -352,10 +352,14 @@ int  fcgpu_span_submit_block(fcgpu_ctx *ctx, uint32_t slot, const void *h_in, si
  *                          are never part of a verdict). Many contexts
  *                          submitting small batches share one copy engine;
  *                          zero-copy batches only queue kernels.
- * Results are identical in both modes. Returns FCGPU_EINVAL for another mode
+ *   FCGPU_SPAN_AUTO     -- ZEROCOPY while at least 4 contexts of the process
+ *                          are in AUTO mode on this device (one per element
+ *                          thread), else COPY; decided at each submission.
+ * Results are identical in every mode. Returns FCGPU_EINVAL for another mode
  * or while a slot is in flight. */
 #define FCGPU_SPAN_COPY     0u
 #define FCGPU_SPAN_ZEROCOPY 1u
+#define FCGPU_SPAN_AUTO     2u
 int  fcgpu_span_mode(fcgpu_ctx *ctx, uint32_t mode);
 
 /* Decision programs. A program is the step list the

@@ -381,6 +381,7 @@ def test_element_drop_chatter_text(capfd):
 
 ZC_CONFS = [
     ("c4", CONF[:-1] + ", BATCH 4096)", 17),
+    ("c4", CONF[:-1] + ", BATCH 1000, SLOTS 3)", 17),
     ("c4", CONF[:-1] + ", BATCH 4096, PARTITION GLOBAL)", 17),
     ("c5", "GPUIPCheckClassify(MODE AUTO, CHECKSUM true, N 8, LB_MODE hash, BATCH 2048)", 9),
     ("c3", "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4, L4 UDP, BATCH 3000)", 5),
