@@ -1,0 +1,116 @@
+"""Block submissions in every span mode (fcgpu_span_mode): COPY, ZEROCOPY and
+AUTO (zero-copy while >= 4 AUTO contexts share the device) give the same
+result blocks, equal to the oracle's verdicts, hashes and tile partition.
+
+The element path (fcgpu_span_submit_block) of include/fastclick_gpu.h, driven
+through ctypes with pinned blocks from fcgpu_host_alloc, as RxCore stages
+them: [descriptors: cap x 8 B][64-B records] in, the fcgpu_block_layout_for
+arrays out.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from fastclick_amd import synth
+from fastclick_amd import _native as N
+
+OUTS = 0x1 | 0x2 | 0x20 | 0x40          # verdict, hash, tile_count, tile_perm
+
+
+def _cfg():
+    return N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16,
+                      badsrc=[N.raw_addr("192.0.2.255")])
+
+
+class Block:
+    """A pinned input block holding batch b as 64-B records, and a result block."""
+
+    def __init__(self, lib, ctx, b, cap):
+        self.lib = lib
+        n = b.n
+        self.n = n
+        self.frames_off = (cap * 8 + 255) & ~255
+        rec = 64
+        self.in_bytes = self.frames_off + n * rec
+        self.pin = lib.fcgpu_host_alloc(self.in_bytes + 65536)
+        assert self.pin
+        buf = np.ctypeslib.as_array(C.cast(self.pin, C.POINTER(C.c_uint8)), shape=(self.in_bytes + 65536,))
+        buf[:] = 0
+        desc = buf[:cap * 8].view(np.uint32).reshape(cap, 2)
+        for i in range(n):
+            off, ln = int(b.desc[i, 0]), int(b.desc[i, 1])
+            cp = min(ln, 64)
+            buf[self.frames_off + i * rec:self.frames_off + i * rec + cp] = b.arena[off:off + cp]
+            desc[i] = (i * rec, ln)
+        self.L = N.fcgpu_block_layout()
+        assert lib.fcgpu_block_layout_for(ctx, n, OUTS, N.PART_TILE, C.byref(self.L)) == N.OK
+        self.out = lib.fcgpu_host_alloc(self.L.bytes)
+        assert self.out
+        self.res = np.ctypeslib.as_array(C.cast(self.out, C.POINTER(C.c_uint8)), shape=(self.L.bytes,))
+
+    def run(self, ctx, slot=0):
+        self.res[:] = 0xEE
+        rc = self.lib.fcgpu_span_submit_block(ctx, slot, self.pin, self.in_bytes, 0, self.frames_off, self.n,
+                                              self.out, OUTS, N.PART_TILE)
+        assert rc == N.OK, self.lib.fcgpu_last_error(ctx)
+        assert self.lib.fcgpu_span_wait(ctx, slot) == N.OK
+        n = self.n
+        return {"verdict": self.res[self.L.verdict:self.L.verdict + 2 * n].view(np.uint16).copy(),
+                "hash": self.res[self.L.hash:self.L.hash + 4 * n].view(np.uint32).copy(),
+                "tile_perm": self.res[self.L.tile_perm:self.L.tile_perm + n].copy()}
+
+    def free(self):
+        self.lib.fcgpu_host_free(self.pin)
+        self.lib.fcgpu_host_free(self.out)
+
+
+def test_span_mode_arguments():
+    """Mode values beyond AUTO are rejected without a device call."""
+    lib = N.load()
+    assert lib.fcgpu_span_mode(None, N.SPAN_COPY) == N.EINVAL
+    assert N.SPAN_AUTO == 2
+
+
+@pytest.mark.gpu
+def test_gpu_span_modes_copy_zerocopy_auto(oracle):
+    lib = N.load()
+    b = synth.c4(5000 + 37, seed=601)
+    synth.inject_errors(b, 0.03, seed=602)
+    cfg = _cfg()
+    exp = oracle.process_batch(cfg, b)
+    cap = 8192
+    ctxs = []
+    for _ in range(4):
+        h = C.c_void_p()
+        assert lib.fcgpu_open(0, cap, C.byref(h)) == N.OK
+        assert lib.fcgpu_configure(h, C.byref(cfg)) == N.OK
+        ctxs.append(h)
+    blk = Block(lib, ctxs[0], b, cap)
+    try:
+        def check(got):
+            assert np.array_equal(got["verdict"] & 0xff, exp["reason"].astype(np.uint16))
+            ok = exp["reason"] == N.R_OK
+            assert np.array_equal(got["hash"][ok], exp["hash"][ok])
+            return got
+        assert lib.fcgpu_span_mode(ctxs[0], 7) == N.EINVAL
+        copy = check(blk.run(ctxs[0]))                       # COPY (default)
+        assert lib.fcgpu_span_mode(ctxs[0], N.SPAN_ZEROCOPY) == N.OK
+        zc = check(blk.run(ctxs[0], slot=1))
+        for k in copy:
+            assert np.array_equal(copy[k], zc[k]), k
+        # AUTO: three AUTO contexts -> copies; a fourth -> zero-copy; back to three -> copies
+        for h in ctxs[:3]:
+            assert lib.fcgpu_span_mode(h, N.SPAN_AUTO) == N.OK
+        a3 = check(blk.run(ctxs[0], slot=2))
+        assert lib.fcgpu_span_mode(ctxs[3], N.SPAN_AUTO) == N.OK
+        a4 = check(blk.run(ctxs[0]))
+        lib.fcgpu_close(ctxs.pop())
+        a3b = check(blk.run(ctxs[0], slot=1))
+        for got in (a3, a4, a3b):
+            for k in copy:
+                assert np.array_equal(copy[k], got[k]), k
+    finally:
+        blk.free()
+        for h in ctxs:
+            lib.fcgpu_close(h)
