@@ -282,6 +282,7 @@ static hipError_t memset_sync(void *p, int v, size_t bytes) {
 
 static std::string g_open_err;
 static void span_auto_count(fcgpu_ctx *c, uint32_t new_mode);
+static bool span_zerocopy(const fcgpu_ctx *c);
 
 // Pools registered by fcgpu_pool_register, with the number of contexts using each.
 static std::mutex g_pool_mu;
@@ -1678,7 +1679,8 @@ int fcgpu_span_submit(fcgpu_ctx *c, uint32_t slot, const uint8_t *h_span, size_t
         HIPCHK(c, hipMalloc(&sp.d_fl, sizeof(uint32_t) * m));
         HIPCHK(c, hipMalloc(&sp.d_rw, sizeof(uint32_t) * m));
     }
-    if (bytes + kArenaPad > sp.span_cap) {
+    const bool zc = span_zerocopy(c);
+    if (!zc && bytes + kArenaPad > sp.span_cap) {
         HIPCHK(c, hipStreamSynchronize(sp.own));
         hipFree(sp.d_span);
         sp.d_span = nullptr;
@@ -1694,6 +1696,37 @@ int fcgpu_span_submit(fcgpu_ctx *c, uint32_t slot, const uint8_t *h_span, size_t
     sp.s = c->fl.slots ? c->stream : sp.own;
     hipStream_t s = sp.s;
     if (n == 0) return FCGPU_OK;
+    if (zc) {
+        // in place: the kernels read the caller's page-locked span and
+        // descriptors and write its page-locked output arrays over PCIe
+        auto dev = [&](const void *p, const char *what, void **out) -> int {
+            *out = nullptr;
+            if (!p) return FCGPU_OK;
+            if (hipHostGetDevicePointer(out, const_cast<void *>(p), 0) != hipSuccess || !*out) {
+                (void)hipGetLastError();
+                return fail(c, FCGPU_EINVAL, std::string("zero-copy span: ") + what +
+                                                 " is not page-locked host memory (fcgpu_host_alloc / fcgpu_host_register)");
+            }
+            return FCGPU_OK;
+        };
+        void *dspan, *ddesc;
+        fcgpu_out d{};
+        d.partition = h->partition;
+        int rc;
+        if ((rc = dev(h_span, "h_span", &dspan)) || (rc = dev(h_desc, "h_desc", &ddesc)) ||
+            (rc = dev(h->verdict, "verdict", (void **)&d.verdict)) || (rc = dev(h->hash, "hash", (void **)&d.hash)) ||
+            (rc = dev(h->anno, "anno", (void **)&d.anno)) || (rc = dev(h->perm, "perm", (void **)&d.perm)) ||
+            (rc = dev(h->port_start, "port_start", (void **)&d.port_start)) ||
+            (rc = dev(h->tile_count, "tile_count", (void **)&d.tile_count)) ||
+            (rc = dev(h->tile_perm, "tile_perm", (void **)&d.tile_perm)) ||
+            (rc = dev(h->flowid, "flowid", (void **)&d.flowid)) || (rc = dev(h->ip_rw, "ip_rw", (void **)&d.ip_rw)))
+            return rc;
+        rc = fcgpu_process(c, static_cast<const uint8_t *>(dspan), static_cast<const uint32_t *>(ddesc), n, &d, s);
+        if (rc != FCGPU_OK) return rc;
+        sp.evt = false;
+        sp.busy = true;
+        return FCGPU_OK;
+    }
     HIPCHK(c, hipMemcpyAsync(sp.d_span, h_span, bytes, hipMemcpyHostToDevice, s));
     HIPCHK(c, hipMemcpyAsync(sp.d_desc, h_desc, sizeof(uint32_t) * 2 * n, hipMemcpyHostToDevice, s));
     fcgpu_out d{};

@@ -340,16 +340,19 @@ int  fcgpu_span_submit_block(fcgpu_ctx *ctx, uint32_t slot, const void *h_in, si
                              size_t desc_off, size_t frames_off, uint32_t n, void *h_out, uint32_t outputs,
                              uint32_t partition);
 
-/* How block submissions reach the device (per context, default COPY):
+/* How span and block submissions reach the device (per context, default COPY):
  *   FCGPU_SPAN_COPY     -- one H2D copy of h_in and one D2H copy of the
  *                          results per batch, through the copy engine (the
  *                          device copy is padded for the header-window reads);
  *   FCGPU_SPAN_ZEROCOPY -- no copies: the kernels read the descriptors and
- *                          frames from h_in and write the results into h_out
- *                          over PCIe, where they lie. Both must be page-locked
- *                          (fcgpu_host_alloc), and h_in readable 256 bytes past
- *                          in_bytes (the header-window over-read; those bytes
- *                          are never part of a verdict). Many contexts
+ *                          frames from h_in (fcgpu_span_submit: h_span,
+ *                          h_desc) and write the results into h_out (the
+ *                          h_out arrays) over PCIe, where they lie. All must
+ *                          be page-locked (fcgpu_host_alloc, or
+ *                          fcgpu_host_register / hipHostRegister), and the
+ *                          frames readable 256 bytes past in_bytes /
+ *                          span_bytes (the header-window over-read; those
+ *                          bytes are never part of a verdict). Many contexts
  *                          submitting small batches share one copy engine;
  *                          zero-copy batches only queue kernels.
  *   FCGPU_SPAN_AUTO     -- ZEROCOPY while at least 4 contexts of the process

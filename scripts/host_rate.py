@@ -5,7 +5,9 @@
 2. The GPUIPCheckClassify element behind a BURST-32 source (Click-shaped
    packets, linked-list batches, annotation scatter, per-port relinking) at
    several BATCH (accumulation) sizes.
-Prints one JSON line.
+Prints one JSON line. `host_rate.py threads`: the element's thread sweep;
+`host_rate.py span`: a host-resident ring through fcgpu_span_submit, copies
+vs zero-copy (span_mpps).
 """
 import ctypes as C
 import json
@@ -107,6 +109,71 @@ def pcap_mpps(n=1 << 22, chunk_pkts=1 << 18, threads=1, mapped=False):
     return best if not mapped else (best, reg)
 
 
+def span_mpps(n=1 << 20, mode="copy", slots=3, reps=24):
+    """A host-resident ring: n C2 frames already contiguous in pinned memory
+    (64-B slots) and their descriptors, submitted with fcgpu_span_submit over
+    `slots` slots (a stream each) with no per-packet host work -- the
+    end-to-end host-resident rate of SURVEY 8(d): H2D of descriptors +
+    headers, the kernels and the D2H of verdict, hash and tile partition,
+    overlapped across streams (mode "copy"), or the kernels reading the span
+    and writing the outputs in place over PCIe (mode "zerocopy"). Every
+    submission's counters are checked at the end."""
+    lib = N.load()
+    b = synth.c2(n)
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=16)
+    ctx = N.Context(0, n, cfg)
+    ptrs = []
+
+    def pinned(nbytes, dtype):
+        p = lib.fcgpu_host_alloc(nbytes)
+        assert p
+        ptrs.append(p)
+        return p, np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(nbytes,)).view(dtype)
+    try:
+        ps, span = pinned(b.arena.size + 4096, np.uint8)
+        span[:b.arena.size] = b.arena
+        pd, desc = pinned(8 * n, np.uint32)
+        desc[:] = np.ascontiguousarray(b.desc, dtype=np.uint32).reshape(-1)
+        outs = []
+        for _ in range(slots):
+            pv, _ = pinned(2 * n, np.uint16)
+            ph, _ = pinned(4 * n, np.uint32)
+            ptc, _ = pinned(2 * 17 * (n // 256 + 1), np.uint16)
+            ptp, _ = pinned(n + 256, np.uint8)
+            outs.append(dict(verdict=pv, hash=ph, tile_count=ptc, tile_perm=ptp, partition=N.PART_TILE))
+        assert lib.fcgpu_span_mode(ctx.h, N.SPAN_ZEROCOPY if mode == "zerocopy" else N.SPAN_COPY) == N.OK
+        ctx.reset_counters()
+
+        def run(k):
+            for r in range(k):
+                s = r % slots
+                if r >= slots:
+                    ctx.span_wait(s)
+                ctx.span_submit(s, ps, b.arena.size, pd, n, **outs[s])
+            for s in range(min(k, slots)):
+                ctx.span_wait(s)
+        run(slots)                      # warm-up: allocations, first launches
+        t0 = time.perf_counter()
+        run(reps)
+        dt = time.perf_counter() - t0
+        assert int(ctx.counters()[N.CTR_COUNT]) == n * (reps + slots)
+        return n * reps / dt / 1e6
+    finally:
+        for p in ptrs:
+            lib.fcgpu_host_free(p)
+        ctx.close()
+
+
+def span_sweep():
+    """span_mpps for both modes at 1M / 256K / 64K packets per submission: one JSON line."""
+    out = {}
+    for n in (1 << 20, 1 << 18, 1 << 16):
+        for mode in ("copy", "zerocopy"):
+            out[f"span_{mode}_{n}"] = round(span_mpps(n, mode, reps=max(24, (24 << 20) // n)), 1)
+            print(json.dumps(out), file=sys.stderr, flush=True)
+    print(json.dumps(out))
+
+
 def mbuf_mpps(n=1 << 18, reps=48, order="shuffled", streams=1):
     """mbuf ingress (fcgpu_process_mbufs): n C2 frames in a DPDK-style
     mempool in page-locked host memory (128-B header, 128-B headroom,
@@ -205,5 +272,7 @@ def thread_sweep():
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "threads":
         thread_sweep()
+    elif len(sys.argv) > 1 and sys.argv[1] == "span":
+        span_sweep()
     else:
         main()

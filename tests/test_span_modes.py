@@ -114,3 +114,62 @@ def test_gpu_span_modes_copy_zerocopy_auto(oracle):
         blk.free()
         for h in ctxs:
             lib.fcgpu_close(h)
+
+
+def _pinned(lib, nbytes, dtype):
+    p = lib.fcgpu_host_alloc(nbytes)
+    assert p
+    arr = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(nbytes,)).view(dtype)
+    return p, arr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["copy", "zerocopy"])
+def test_gpu_span_submit_modes(oracle, mode):
+    """fcgpu_span_submit (frames already contiguous in host memory: the pcap
+    ingress, a host-resident ring) in COPY and ZEROCOPY mode: verdicts, hashes,
+    annotations and the tile partition equal the oracle's; ZEROCOPY reads the
+    pinned span in place and writes the pinned output arrays."""
+    lib = N.load()
+    b = synth.c3(20_000 + 11, seed=611)
+    synth.inject_errors(b, 0.02, seed=612)
+    cfg = _cfg()
+    exp = oracle.process_batch(cfg, b)
+    n = b.n
+    ctx = N.Context(0, 32768, cfg)
+    ptrs = []
+    try:
+        span_bytes = b.arena.size
+        ps, span = _pinned(lib, span_bytes + 4096, np.uint8)
+        span[:] = 0
+        span[:span_bytes] = b.arena
+        pd, desc = _pinned(lib, 8 * n, np.uint32)
+        desc[:] = np.ascontiguousarray(b.desc, dtype=np.uint32).reshape(-1)
+        pv, verdict = _pinned(lib, 2 * n, np.uint16)
+        ph, hsh = _pinned(lib, 4 * n, np.uint32)
+        pa, anno = _pinned(lib, 16 * n, np.uint8)
+        ntiles = -(-n // 256)
+        ptc, tc = _pinned(lib, 2 * 17 * ntiles, np.uint16)
+        ptp, tp = _pinned(lib, n + 256, np.uint8)
+        ptrs = [ps, pd, pv, ph, pa, ptc, ptp]
+        want = N.SPAN_ZEROCOPY if mode == "zerocopy" else N.SPAN_COPY
+        assert lib.fcgpu_span_mode(ctx.h, want) == N.OK
+        for slot in range(2):
+            verdict[:] = 0xEEEE
+            ctx.span_submit(slot, ps, span_bytes, pd, n, verdict=pv, hash=ph, anno=pa, tile_count=ptc,
+                            tile_perm=ptp, partition=N.PART_TILE)
+            ctx.span_wait(slot)
+            assert np.array_equal(verdict & 0xff, exp["reason"].astype(np.uint16))
+            assert np.array_equal(verdict >> 8, exp["port"].astype(np.uint16))
+            ok = exp["reason"] == N.R_OK
+            assert np.array_equal(hsh[ok], exp["hash"][ok])
+            # the tile partition: each tile's packets in output order, input order within an output
+            port = exp["port"].astype(np.int64)
+            for t in (0, ntiles // 2, ntiles - 1):
+                lo, hi = t * 256, min(n, t * 256 + 256)
+                order = lo + tp[lo:hi].astype(np.int64)
+                assert np.array_equal(order, lo + np.argsort(port[lo:hi], kind="stable"))
+    finally:
+        for p in ptrs:
+            lib.fcgpu_host_free(p)
+        ctx.close()
