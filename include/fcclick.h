@@ -99,7 +99,8 @@ int fcclick_bench(const char *conf, const uint8_t *arena, const uint32_t *desc, 
 
 /* The same with `threads` element instances, one per thread (each with its
  * own GPU context and packet pool, as Click threads with their own rx queue
- * would be); *pps = the sum of the threads' rates. */
+ * would be), their timed loops started together after every thread's set-up;
+ * *pps = all threads' packets over the union of their timed windows. */
 int fcclick_bench_threads(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
                           uint32_t burst, uint32_t reps, uint32_t threads, double *pps, char *err,
                           size_t errcap);
