@@ -64,7 +64,8 @@ for s in "${ST[@]}"; do
          pmc pmc_ea_c4flow TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_DRAM_sum -- \
              --steps 40 --warmup 4 --no-cpu --no-timing --workload c4 --flow-capacity 2000000 ;;
     host) step host_rate 600 python scripts/host_rate.py
-          step host_threads 600 python scripts/host_rate.py threads ;;
+          step host_threads 600 python scripts/host_rate.py threads
+          step host_span 300 python scripts/host_rate.py span ;;
     dist) step dist2 300 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 --no-cpu
           step dist2_strong 300 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 --no-cpu --shard strong ;;
     latency) step latency 120 python scripts/latency_probe.py
