@@ -167,6 +167,10 @@ struct SpanSlot {
     // zero-copy block submissions: the device addresses of the last h_in / h_out
     const void *zc_hin = nullptr, *zc_hout = nullptr;
     uint8_t *zc_din = nullptr, *zc_dout = nullptr;
+    // zero-copy span submissions: the last host -> device translation of each
+    // pointer argument (span, descriptors, the nine output arrays)
+    const void *zc_key[11] = {};
+    void *zc_val[11] = {};
     bool busy = false;
     hipEvent_t done = nullptr;   // shared streams: the slot's last operation (else the stream is waited)
     bool evt = false;            // the last submission recorded `done`
@@ -1699,14 +1703,23 @@ int fcgpu_span_submit(fcgpu_ctx *c, uint32_t slot, const uint8_t *h_span, size_t
     if (zc) {
         // in place: the kernels read the caller's page-locked span and
         // descriptors and write its page-locked output arrays over PCIe
+        int k = 0;
         auto dev = [&](const void *p, const char *what, void **out) -> int {
+            const int slot_k = k++;
             *out = nullptr;
             if (!p) return FCGPU_OK;
+            if (p == sp.zc_key[slot_k]) {        // the caller's buffers are usually reused
+                *out = sp.zc_val[slot_k];
+                return FCGPU_OK;
+            }
+            sp.zc_key[slot_k] = nullptr;
             if (hipHostGetDevicePointer(out, const_cast<void *>(p), 0) != hipSuccess || !*out) {
                 (void)hipGetLastError();
                 return fail(c, FCGPU_EINVAL, std::string("zero-copy span: ") + what +
                                                  " is not page-locked host memory (fcgpu_host_alloc / fcgpu_host_register)");
             }
+            sp.zc_key[slot_k] = p;
+            sp.zc_val[slot_k] = *out;
             return FCGPU_OK;
         };
         void *dspan, *ddesc;
@@ -1786,6 +1799,10 @@ int fcgpu_span_mode(fcgpu_ctx *c, uint32_t mode) {
         if (sp.busy) return fail(c, FCGPU_EINVAL, "fcgpu_span_mode: a span slot is in flight");
     span_auto_count(c, mode);
     c->span_mode = mode;
+    for (SpanSlot &sp : c->span) {      // forget the zero-copy address translations
+        sp.zc_hin = sp.zc_hout = nullptr;
+        for (auto &k : sp.zc_key) k = nullptr;
+    }
     return FCGPU_OK;
 }
 

@@ -352,7 +352,11 @@ int  fcgpu_span_submit_block(fcgpu_ctx *ctx, uint32_t slot, const void *h_in, si
  *                          fcgpu_host_register / hipHostRegister), and the
  *                          frames readable 256 bytes past in_bytes /
  *                          span_bytes (the header-window over-read; those
- *                          bytes are never part of a verdict). Many contexts
+ *                          bytes are never part of a verdict). The context
+ *                          remembers each buffer address's device translation
+ *                          until the next fcgpu_span_mode call, so a buffer
+ *                          freed and replaced at the same address must be
+ *                          page-locked as well. Many contexts
  *                          submitting small batches share one copy engine;
  *                          zero-copy batches only queue kernels.
  *   FCGPU_SPAN_AUTO     -- ZEROCOPY while at least 4 contexts of the process
