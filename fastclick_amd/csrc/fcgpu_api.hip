@@ -1905,7 +1905,7 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
     hipStream_t ss = nullptr;
     HIPCHK(c, span_stream(c, slot, &ss));
     const bool zc = span_zerocopy(c);
-    if (zc) {
+    if (zc && n) {
         // the kernels read h_in and write h_out where they lie (page-locked
         // memory mapped into the device's address space): no copy engine
         if (h_in != sp.zc_hin) {

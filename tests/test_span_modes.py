@@ -97,6 +97,9 @@ def test_gpu_span_modes_copy_zerocopy_auto(oracle):
         copy = check(blk.run(ctxs[0]))                       # COPY (default)
         assert lib.fcgpu_span_mode(ctxs[0], N.SPAN_ZEROCOPY) == N.OK
         zc = check(blk.run(ctxs[0], slot=1))
+        # an empty batch in zero-copy mode: no buffers needed, nothing queued
+        assert lib.fcgpu_span_submit_block(ctxs[0], 0, None, 0, 0, 0, 0, None, OUTS, N.PART_TILE) == N.OK
+        assert lib.fcgpu_span_wait(ctxs[0], 0) == N.OK
         for k in copy:
             assert np.array_equal(copy[k], zc[k]), k
         # AUTO: three AUTO contexts -> copies; a fourth -> zero-copy; back to three -> copies
