@@ -26,7 +26,10 @@ def _cfg():
 class Block:
     """A pinned input block holding batch b as 64-B records, and a result block."""
 
-    def __init__(self, lib, ctx, b, cap):
+    def __init__(self, lib, ctx, b, cap, place=None):
+        """place[i]: the 64-B record slot packet i is staged in (default i, as
+        RxCore stages: the zero-copy kernel's speculative strided gather then
+        always hits; another permutation makes it fall back per wave)."""
         self.lib = lib
         n = b.n
         self.n = n
@@ -38,11 +41,13 @@ class Block:
         buf = np.ctypeslib.as_array(C.cast(self.pin, C.POINTER(C.c_uint8)), shape=(self.in_bytes + 65536,))
         buf[:] = 0
         desc = buf[:cap * 8].view(np.uint32).reshape(cap, 2)
+        place = np.arange(n) if place is None else place
         for i in range(n):
             off, ln = int(b.desc[i, 0]), int(b.desc[i, 1])
             cp = min(ln, 64)
-            buf[self.frames_off + i * rec:self.frames_off + i * rec + cp] = b.arena[off:off + cp]
-            desc[i] = (i * rec, ln)
+            r = int(place[i]) * rec
+            buf[self.frames_off + r:self.frames_off + r + cp] = b.arena[off:off + cp]
+            desc[i] = (r, ln)
         self.L = N.fcgpu_block_layout()
         assert lib.fcgpu_block_layout_for(ctx, n, OUTS, N.PART_TILE, C.byref(self.L)) == N.OK
         self.out = lib.fcgpu_host_alloc(self.L.bytes)
@@ -172,6 +177,77 @@ def test_gpu_span_submit_modes(oracle, mode):
                 lo, hi = t * 256, min(n, t * 256 + 256)
                 order = lo + tp[lo:hi].astype(np.int64)
                 assert np.array_equal(order, lo + np.argsort(port[lo:hi], kind="stable"))
+    finally:
+        for p in ptrs:
+            lib.fcgpu_host_free(p)
+        ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["reversed", "few_swapped"])
+def test_gpu_zerocopy_records_out_of_order(oracle, layout):
+    """Zero-copy blocks whose 64-B records fill the block end to end but are not
+    in packet order: the kernel's speculative strided window gather misses (in
+    every wave, or in a few) and gathers again from the descriptors -- the
+    results stay the oracle's and the copy mode's."""
+    lib = N.load()
+    b = synth.c4(3000 + 5, seed=621)
+    synth.inject_errors(b, 0.03, seed=622)
+    cfg = _cfg()
+    exp = oracle.process_batch(cfg, b)
+    n = b.n
+    place = np.arange(n)[::-1].copy() if layout == "reversed" else np.arange(n)
+    if layout == "few_swapped":
+        rng = np.random.default_rng(623)
+        for a, c in rng.integers(0, n, (5, 2)):
+            place[[a, c]] = place[[c, a]]
+    h = C.c_void_p()
+    assert lib.fcgpu_open(0, 4096, C.byref(h)) == N.OK
+    assert lib.fcgpu_configure(h, C.byref(cfg)) == N.OK
+    blk = Block(lib, h, b, 4096, place=place)
+    try:
+        copy = blk.run(h)
+        assert lib.fcgpu_span_mode(h, N.SPAN_ZEROCOPY) == N.OK
+        zc = blk.run(h, slot=1)
+        for got in (copy, zc):
+            assert np.array_equal(got["verdict"] & 0xff, exp["reason"].astype(np.uint16))
+            ok = exp["reason"] == N.R_OK
+            assert np.array_equal(got["hash"][ok], exp["hash"][ok])
+        for k in copy:
+            assert np.array_equal(copy[k], zc[k]), k
+    finally:
+        blk.free()
+        lib.fcgpu_close(h)
+
+
+@pytest.mark.gpu
+def test_gpu_span_zerocopy_strided_slots(oracle):
+    """A ring of 64-B slots end to end (span bytes = 64 n: the speculative
+    strided gather of fcgpu_span_submit's zero-copy mode) against the oracle."""
+    lib = N.load()
+    b = synth.c4(8192 + 64, seed=631)
+    synth.inject_errors(b, 0.02, seed=632)
+    cfg = _cfg()
+    exp = oracle.process_batch(cfg, b)
+    n = b.n
+    assert np.array_equal(b.desc[:, 0].astype(np.int64), 64 * np.arange(n))
+    ctx = N.Context(0, 16384, cfg)
+    ptrs = []
+    try:
+        ps, span = _pinned(lib, 64 * n + 4096, np.uint8)
+        span[:] = 0
+        span[:64 * n] = b.arena[:64 * n]
+        pd, desc = _pinned(lib, 8 * n, np.uint32)
+        desc[:] = np.ascontiguousarray(b.desc, dtype=np.uint32).reshape(-1)
+        pv, verdict = _pinned(lib, 2 * n, np.uint16)
+        ph, hsh = _pinned(lib, 4 * n, np.uint32)
+        ptrs = [ps, pd, pv, ph]
+        assert lib.fcgpu_span_mode(ctx.h, N.SPAN_ZEROCOPY) == N.OK
+        ctx.span_submit(0, ps, 64 * n, pd, n, verdict=pv, hash=ph, partition=N.PART_TILE)
+        ctx.span_wait(0)
+        assert np.array_equal(verdict & 0xff, exp["reason"].astype(np.uint16))
+        ok = exp["reason"] == N.R_OK
+        assert np.array_equal(hsh[ok], exp["hash"][ok])
     finally:
         for p in ptrs:
             lib.fcgpu_host_free(p)
