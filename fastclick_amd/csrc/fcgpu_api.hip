@@ -235,7 +235,6 @@ struct fcgpu_ctx {
     SpanSlot span[FCGPU_SPAN_SLOTS];
     int span_index = -1;              // FCGPU_SPAN_STREAMS=shared:N: this context's place in the pool
     uint32_t span_mode = FCGPU_SPAN_COPY;   // fcgpu_span_mode: block submissions copied or read in place
-    uint32_t next_stride64 = 0;       // RxArgs::stride64 of the next process_one (zero-copy submissions)
     // flow table (fcgpu_flow_enable)
     uint32_t max_flows = 0, flow_slots = 0, flow_words = 0;
     FlowArgs fl{};            // device pointers; fl.slots == nullptr: disabled
@@ -1118,7 +1117,6 @@ static int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_d
     a.desc = reinterpret_cast<const uint2 *>(d_desc);
     a.n = n;
     a.ntiles = ntiles;
-    a.stride64 = c->next_stride64;
     a.verdict = verdict;
     a.hash = o->hash;
     a.anno = o->anno;
@@ -1736,11 +1734,7 @@ int fcgpu_span_submit(fcgpu_ctx *c, uint32_t slot, const uint8_t *h_span, size_t
             (rc = dev(h->tile_perm, "tile_perm", (void **)&d.tile_perm)) ||
             (rc = dev(h->flowid, "flowid", (void **)&d.flowid)) || (rc = dev(h->ip_rw, "ip_rw", (void **)&d.ip_rw)))
             return rc;
-        // 64-B slots end to end: the window gather need not wait for the
-        // descriptors' PCIe round trip (RxArgs::stride64)
-        c->next_stride64 = bytes == 64ull * n;
         rc = fcgpu_process(c, static_cast<const uint8_t *>(dspan), static_cast<const uint32_t *>(ddesc), n, &d, s);
-        c->next_stride64 = 0;
         if (rc != FCGPU_OK) return rc;
         sp.evt = false;
         sp.busy = true;
@@ -1971,11 +1965,7 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
     d.tile_perm = (uint8_t *)at(L.tile_perm);
     d.flowid = (uint32_t *)at(L.flowid);
     d.ip_rw = (uint32_t *)at(L.ip_rw);
-    // zero-copy with 64-B records end to end (frames of up to 64 captured
-    // bytes, the element's common case): speculative window gather
-    c->next_stride64 = zc && in_bytes - frames_off == 64ull * n;
     int rc = fcgpu_process(c, din + frames_off, reinterpret_cast<const uint32_t *>(din + desc_off), n, &d, s);
-    c->next_stride64 = 0;
     if (rc != FCGPU_OK) return rc;
     if (!zc) HIPCHK(c, hipMemcpyAsync(h_out, sp.d_res, L.bytes, hipMemcpyDeviceToHost, s));
     uint32_t ns = 0;

@@ -114,12 +114,6 @@ struct RxArgs {
     const uint2 *desc;
     uint32_t n;
     uint32_t ntiles;
-    // nonzero: the records are most likely 64-B strided (record i at arena +
-    // 64 i), so the window gather is issued before the descriptor arrives and
-    // redone from the descriptors only where a record lies elsewhere. For
-    // arenas read over PCIe (zero-copy), where the descriptor load is a round
-    // trip of its own.
-    uint32_t stride64;
     uint16_t *verdict;
     uint32_t *hash;
     fcgpu_anno *anno;
@@ -1313,23 +1307,10 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
     }
     const uint32_t i = tile * kTile + threadIdx.x;
     uint2 d = make_uint2(0, 0);
+    if (i < V.n) d = V.desc[i];
     uint8_t *wl = s_win + wave * (kWave * kWin);
-    if (L.njobs == 1 && A.stride64) {   // launch-uniform
-        const uint32_t g = i < V.n ? i * 64u : 0u;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) glds16(win_src(V.arena, g, lane, k), wl + k * 1024);
-        if (i < V.n) d = V.desc[i];
-        // waiting for d waited for the gathers too (one in-order counter):
-        // a wave with a record elsewhere gathers again from the descriptors
-        if (__any(i < V.n && d.x != g)) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) glds16(win_src(V.arena, d.x, lane, k), wl + k * 1024);
-        }
-    } else {
-        if (i < V.n) d = V.desc[i];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) glds16(win_src(V.arena, d.x, lane, k), wl + k * 1024);
-    }
+    for (int k = 0; k < 4; ++k) glds16(win_src(V.arena, d.x, lane, k), wl + k * 1024);
     // decision program: the block's LDS copy when it fits (block-uniform)
     const bool prog_lds = PROG && prog_in_lds(A.cfg);
     const bool crc_lds = !PROG && crc_in_lds(A.cfg);          // block-uniform

@@ -28,8 +28,7 @@ class Block:
 
     def __init__(self, lib, ctx, b, cap, place=None):
         """place[i]: the 64-B record slot packet i is staged in (default i, as
-        RxCore stages: the zero-copy kernel's speculative strided gather then
-        always hits; another permutation makes it fall back per wave)."""
+        RxCore stages; the ABI allows any placement)."""
         self.lib = lib
         n = b.n
         self.n = n
@@ -187,9 +186,8 @@ def test_gpu_span_submit_modes(oracle, mode):
 @pytest.mark.parametrize("layout", ["reversed", "few_swapped"])
 def test_gpu_zerocopy_records_out_of_order(oracle, layout):
     """Zero-copy blocks whose 64-B records fill the block end to end but are not
-    in packet order: the kernel's speculative strided window gather misses (in
-    every wave, or in a few) and gathers again from the descriptors -- the
-    results stay the oracle's and the copy mode's."""
+    in packet order (all of them, or a few swapped): the descriptors place
+    every window, in both modes -- the oracle's results and the copy mode's."""
     lib = N.load()
     b = synth.c4(3000 + 5, seed=621)
     synth.inject_errors(b, 0.03, seed=622)
@@ -222,8 +220,9 @@ def test_gpu_zerocopy_records_out_of_order(oracle, layout):
 
 @pytest.mark.gpu
 def test_gpu_span_zerocopy_strided_slots(oracle):
-    """A ring of 64-B slots end to end (span bytes = 64 n: the speculative
-    strided gather of fcgpu_span_submit's zero-copy mode) against the oracle."""
+    """A ring of 64-B slots end to end (span bytes = 64 n, nothing past the
+    last frame but the pinned allocation's slack) read in place, against the
+    oracle."""
     lib = N.load()
     b = synth.c4(8192 + 64, seed=631)
     synth.inject_errors(b, 0.02, seed=632)
