@@ -153,6 +153,12 @@ struct HostSlot {
 
 // One in-flight fcgpu_span_submit: device copy of the span and descriptors,
 // device outputs, the stream it runs on.
+// one launch of the shared zero-copy queue (FCGPU_SPAN_AUTO, agg_launch_locked)
+struct AggLaunch {
+    hipEvent_t ev = nullptr;
+    uint32_t refs = 0;        // submissions it carries that have not been waited for
+};
+
 struct SpanSlot {
     hipStream_t own = nullptr, s = nullptr;
     uint8_t *d_span = nullptr;
@@ -171,6 +177,10 @@ struct SpanSlot {
     // pointer argument (span, descriptors, the nine output arrays)
     const void *zc_key[11] = {};
     void *zc_val[11] = {};
+    // FCGPU_SPAN_AUTO with many contexts: the submission went to the device's
+    // shared queue (agg); al = the launch carrying it (nullptr while pending)
+    bool agg = false, agg_err = false;
+    AggLaunch *al = nullptr;
     bool busy = false;
     hipEvent_t done = nullptr;   // shared streams: the slot's last operation (else the stream is waited)
     bool evt = false;            // the last submission recorded `done`
@@ -287,6 +297,7 @@ static hipError_t memset_sync(void *p, int v, size_t bytes) {
 static std::string g_open_err;
 static void span_auto_count(fcgpu_ctx *c, uint32_t new_mode);
 static bool span_zerocopy(const fcgpu_ctx *c);
+int fcgpu_span_wait(fcgpu_ctx *c, uint32_t slot);
 
 // Pools registered by fcgpu_pool_register, with the number of contexts using each.
 static std::mutex g_pool_mu;
@@ -891,6 +902,8 @@ int fcgpu_flow_count(fcgpu_ctx *c, uint32_t *count) {
 
 void fcgpu_close(fcgpu_ctx *c) {
     if (!c) return;
+    for (uint32_t k = 0; k < FCGPU_SPAN_SLOTS; ++k)      // submissions in the shared queue
+        if (c->span[k].agg) fcgpu_span_wait(c, k);
     span_auto_count(c, FCGPU_SPAN_COPY);
     if (c->device >= 0) {
         hipSetDevice(c->device);
@@ -1298,6 +1311,7 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
         J.tile_perm = tile ? j.out.tile_perm : nullptr;
         J.tilecnt = part == kPartGlobal ? c->fuse_tilecnt + (size_t)k * kFuseCntStride * c->max_tiles : nullptr;
         J.ip_rw = j.out.ip_rw;
+        J.ctr = c->d_ctr;
         J.n = j.n;
         J.tile0 = tiles;
         tiles += (j.n + kTile - 1) / kTile;
@@ -1793,6 +1807,188 @@ static bool span_zerocopy(const fcgpu_ctx *c) {
     return it != g_auto_ctx.end() && it->second >= kZeroCopyAuto;
 }
 
+// ---- the shared zero-copy queue of FCGPU_SPAN_AUTO --------------------------
+// With many element contexts on one device, each zero-copy batch is a small
+// kernel (16-64 workgroups, latency-bound over PCIe) that waits behind other
+// contexts' kernels in the few HW queues their streams map to (4 on the box:
+// the HW queues ran ~2 kernels at a time, profiles/r03_s10/kt_el16). So in
+// AUTO mode, once kZeroCopyAuto contexts share the device, block submissions
+// go to one queue per device, and a submitter that finds kAggLaunch of them
+// pending -- or a context waiting for one of its own still pending --
+// launches them together: one k_rx launch carries the batches of several
+// contexts with one configuration (RxJob::ctr keeps each context's counters),
+// on one of kAggStreams streams. Flow tables (batch order), whole-batch
+// partitions and in-place rewrites (context scratch) keep their own launches.
+struct AggItem {
+    fcgpu_ctx *c;
+    uint32_t slot;
+    fcgpu_job job;            // device (mapped) addresses
+};
+struct AggQueue {
+    std::mutex mu;
+    int device = -1;
+    std::vector<AggItem> pending;
+    hipStream_t st[4] = {};
+    uint32_t rr = 0;
+    std::vector<AggLaunch *> spare;
+};
+constexpr uint32_t kAggLaunch = 4;
+static std::mutex g_agg_mu;
+static std::map<int, AggQueue *> g_agg;
+static AggQueue &agg_queue(int device) {
+    std::lock_guard<std::mutex> g(g_agg_mu);
+    AggQueue *&q = g_agg[device];
+    if (!q) {
+        q = new AggQueue();
+        q->device = device;
+    }
+    return *q;
+}
+static bool agg_eligible(const fcgpu_ctx *c, const fcgpu_out &o) {
+    return c->span_mode == FCGPU_SPAN_AUTO && !c->fl.slots && out_part(&o) != kPartGlobal &&
+           !(c->cfg.rewrite & FCGPU_RW_INPLACE) && !c->timing_every;
+}
+static bool agg_compatible(const AggItem &a, const AggItem &b) {
+    return memcmp(&a.c->dcfg, &b.c->dcfg, sizeof(DevCfg)) == 0 && out_part(&a.job.out) == out_part(&b.job.out) &&
+           a.job.out.partition == b.job.out.partition && a.c->jit_src == b.c->jit_src;
+}
+// Launch every pending submission (q.mu held): the first one with the next
+// ones of its configuration, up to kMaxFuse per launch, until none is left.
+static int agg_launch_locked(AggQueue &q) {
+    if (q.pending.empty()) return FCGPU_OK;
+    if (hipSetDevice(q.device) != hipSuccess) return FCGPU_ERUNTIME;
+    while (!q.pending.empty()) {
+        std::vector<size_t> grp{0};
+        for (size_t m = 1; m < q.pending.size() && grp.size() < kMaxFuse; ++m)
+            if (agg_compatible(q.pending[0], q.pending[m])) grp.push_back(m);
+        fcgpu_ctx *c0 = q.pending[0].c;
+        const fcgpu_out &o0 = q.pending[0].job.out;
+        const int part = out_part(&o0);
+        RxLaunch L;
+        RxArgs &a = L.A;
+        a = RxArgs{};
+        a.tilecnt = c0->d_tilecnt;
+        a.ctr = c0->d_ctr;
+        a.cfg = c0->dcfg;
+        a.fl = c0->fl;
+        L.njobs = (uint32_t)grp.size();
+        L.flow_stride = L.flow_words = 0;
+        uint32_t tiles = 0;
+        for (size_t k = 0; k < grp.size(); ++k) {
+            const AggItem &it = q.pending[grp[k]];
+            const fcgpu_job &j = it.job;
+            RxJob &J = L.job[k];
+            J = RxJob{};
+            J.arena = j.arena;
+            J.desc = reinterpret_cast<const uint2 *>(j.desc);
+            J.verdict = j.out.verdict;
+            J.hash = j.out.hash;
+            J.anno = j.out.anno;
+            J.perm = j.out.perm;
+            J.tile_count = j.out.tile_count;
+            J.tile_perm = j.out.partition == FCGPU_PART_TILE ? j.out.tile_perm : nullptr;
+            J.flowid = nullptr;
+            J.ip_rw = j.out.ip_rw;
+            J.ctr = it.c->d_ctr;
+            J.n = j.n;
+            J.tile0 = tiles;
+            tiles += (j.n + kTile - 1) / kTile;
+        }
+        L.job_tiles = (L.job[0].n + kTile - 1) / kTile;
+        for (uint32_t k = 1; k < L.njobs; ++k)
+            if (L.job[k].tile0 != k * L.job_tiles) L.job_tiles = 0;
+        if (tiles > L.njobs * L.job_tiles) L.job_tiles = 0;
+        a.arena = L.job[0].arena;
+        a.desc = L.job[0].desc;
+        a.n = L.job[0].n;
+        a.ntiles = (a.n + kTile - 1) / kTile;
+        const uint32_t si = q.rr++ % 4;
+        hipError_t e = q.st[si] ? hipSuccess : hipStreamCreateWithFlags(&q.st[si], hipStreamNonBlocking);
+        AggLaunch *al = nullptr;
+        if (!q.spare.empty()) {
+            al = q.spare.back();
+            q.spare.pop_back();
+        } else {
+            al = new AggLaunch();
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&al->ev, hipEventDisableTiming);
+        }
+        if (e == hipSuccess) {
+            launch_rx_any(part, c0->cfg.check_mode, c0->cfg.checksum != 0, L, tiles, q.st[si], nullptr, nullptr,
+                          c0->jit_src.empty() ? nullptr : c0);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipEventRecord(al->ev, q.st[si]);
+        al->refs = (uint32_t)grp.size();
+        for (size_t k : grp) {
+            AggItem &it = q.pending[k];
+            SpanSlot &sp = it.c->span[it.slot];
+            if (e == hipSuccess) {
+                sp.al = al;
+            } else {
+                sp.agg_err = true;     // its owner's wait reports the failure
+            }
+        }
+        if (e != hipSuccess) {
+            al->refs = 0;
+            q.spare.push_back(al);
+        }
+        // the launched submissions leave the queue, the rest keep their order
+        std::vector<AggItem> rest;
+        rest.reserve(q.pending.size() - grp.size());
+        size_t g = 0;
+        for (size_t m = 0; m < q.pending.size(); ++m) {
+            if (g < grp.size() && grp[g] == m) { ++g; continue; }
+            rest.push_back(q.pending[m]);
+        }
+        q.pending.swap(rest);
+        if (e != hipSuccess) return FCGPU_ERUNTIME;
+    }
+    return FCGPU_OK;
+}
+// Queue one zero-copy block submission (device addresses in j).
+static int agg_submit(fcgpu_ctx *c, uint32_t slot, const fcgpu_job &j) {
+    AggQueue &q = agg_queue(c->device);
+    SpanSlot &sp = c->span[slot];
+    std::lock_guard<std::mutex> g(q.mu);
+    q.pending.push_back(AggItem{c, slot, j});
+    sp.agg = true;
+    sp.agg_err = false;
+    sp.al = nullptr;
+    sp.busy = true;
+    if (q.pending.size() >= kAggLaunch) return agg_launch_locked(q) == FCGPU_OK ? FCGPU_OK : FCGPU_ERUNTIME;
+    return FCGPU_OK;
+}
+// Wait for (block = true) or poll a queued submission: launched first if
+// still pending. Returns 1 done, 0 running, < 0 error.
+static int agg_finish(fcgpu_ctx *c, uint32_t slot, bool block) {
+    AggQueue &q = agg_queue(c->device);
+    SpanSlot &sp = c->span[slot];
+    AggLaunch *al = nullptr;
+    {
+        std::lock_guard<std::mutex> g(q.mu);
+        if (!sp.al && !sp.agg_err) agg_launch_locked(q);
+        al = sp.al;
+    }
+    hipError_t e = hipSuccess;
+    if (al) {
+        e = block ? hipEventSynchronize(al->ev) : hipEventQuery(al->ev);
+        if (!block && e == hipErrorNotReady) return 0;
+    }
+    {
+        std::lock_guard<std::mutex> g(q.mu);
+        if (al && --al->refs == 0) q.spare.push_back(al);
+        sp.al = nullptr;
+        sp.agg = false;
+        sp.busy = false;
+    }
+    if (!al) return fail(c, FCGPU_ERUNTIME, "shared zero-copy launch failed");
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(c, FCGPU_ERUNTIME, std::string("shared zero-copy batch: ") + hipGetErrorString(e));
+    }
+    return 1;
+}
+
 int fcgpu_span_mode(fcgpu_ctx *c, uint32_t mode) {
     if (!c || mode > FCGPU_SPAN_AUTO) return FCGPU_EINVAL;
     for (const SpanSlot &sp : c->span)
@@ -1810,6 +2006,7 @@ int fcgpu_span_poll(fcgpu_ctx *c, uint32_t slot) {
     if (!c || slot >= FCGPU_SPAN_SLOTS) return FCGPU_EINVAL;
     SpanSlot &sp = c->span[slot];
     if (!sp.busy) return 1;
+    if (sp.agg) return agg_finish(c, slot, false);
     const hipError_t e = sp.evt ? hipEventQuery(sp.done) : hipStreamQuery(sp.s);
     if (e == hipSuccess) return 1;
     if (e == hipErrorNotReady) return 0;
@@ -1965,6 +2162,16 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
     d.tile_perm = (uint8_t *)at(L.tile_perm);
     d.flowid = (uint32_t *)at(L.flowid);
     d.ip_rw = (uint32_t *)at(L.ip_rw);
+    if (zc && agg_eligible(c, d)) {   // AUTO chose zero-copy: >= kZeroCopyAuto contexts share the device
+        fcgpu_job j{};
+        j.arena = din + frames_off;
+        j.desc = reinterpret_cast<const uint32_t *>(din + desc_off);
+        j.n = n;
+        j.out = d;
+        int rc = check_process(c, j.arena, j.desc, n, &j.out);
+        if (rc != FCGPU_OK) return rc;
+        return agg_submit(c, slot, j);
+    }
     int rc = fcgpu_process(c, din + frames_off, reinterpret_cast<const uint32_t *>(din + desc_off), n, &d, s);
     if (rc != FCGPU_OK) return rc;
     if (!zc) HIPCHK(c, hipMemcpyAsync(h_out, sp.d_res, L.bytes, hipMemcpyDeviceToHost, s));
@@ -1985,6 +2192,10 @@ int fcgpu_span_wait(fcgpu_ctx *c, uint32_t slot) {
     if (!c || slot >= FCGPU_SPAN_SLOTS) return FCGPU_EINVAL;
     SpanSlot &sp = c->span[slot];
     if (!sp.busy) return FCGPU_OK;
+    if (sp.agg) {
+        const int r = agg_finish(c, slot, true);
+        return r < 0 ? r : FCGPU_OK;
+    }
     HIPCHK(c, hipSetDevice(c->device));
     sp.busy = false;
     if (sp.evt) HIPCHK(c, hipEventSynchronize(sp.done));

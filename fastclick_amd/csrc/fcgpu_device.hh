@@ -1092,11 +1092,12 @@ struct RxView {
     uint8_t *tile_perm;
     uint32_t *tilecnt;       // kPartGlobal: [nports+1][ntiles]
     uint32_t *ip_rw;         // cfg.rewrite: the rewritten header bytes
+    unsigned long long *ctr; // the batch's context's counter replicas
     uint32_t n, ntiles;
 };
 __device__ __forceinline__ RxView rx_view(const RxArgs &A) {
     return RxView{A.arena, A.desc, A.verdict, A.hash, A.anno, A.perm, A.tile_count, A.tile_perm, A.tilecnt,
-                  A.ip_rw, A.n, A.ntiles};
+                  A.ip_rw, A.ctr, A.n, A.ntiles};
 }
 
 // One 256-packet tile once its header window is in LDS: fused
@@ -1214,7 +1215,7 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, const RxView &V, const 
     // and "drops" are not kept here: both follow from these bins on read
     // (fcgpu_counters_derive), which saves an atomic per tile (-0.4 us / 1M).
     if (t < nbt) {
-        unsigned long long *ctr = A.ctr + (size_t)(tile & (FCGPU_CTR_SHARDS - 1)) * FCGPU_NCOUNTERS;
+        unsigned long long *ctr = V.ctr + (size_t)(tile & (FCGPU_CTR_SHARDS - 1)) * FCGPU_NCOUNTERS;
         if (tot) {
             if (t < nb) atomicAdd(&ctr[FCGPU_CTR_PORT + t], (unsigned long long)tot);
             else atomicAdd(&ctr[FCGPU_CTR_REASON + (t - nb)], (unsigned long long)tot);
@@ -1248,6 +1249,8 @@ struct RxJob {
     uint32_t *flowid;
     uint32_t *tilecnt;       // kPartGlobal: the batch's per-tile counts (its own scratch)
     uint32_t *ip_rw;         // cfg.rewrite (not in place): the batch's rewritten header bytes
+    unsigned long long *ctr; // the counter replicas of the batch's context (a launch may carry
+                             // the batches of several contexts with one configuration)
     uint32_t n, tile0;       // packets; first workgroup of the batch in the grid
 };
 struct RxLaunch {
@@ -1293,6 +1296,7 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
         V.tile_perm = J.tile_perm;
         V.tilecnt = J.tilecnt;
         V.ip_rw = J.ip_rw;
+        V.ctr = J.ctr;
         V.n = J.n;
         V.ntiles = (J.n + kTile - 1) / kTile;
         tile = t;

@@ -251,3 +251,121 @@ def test_gpu_span_zerocopy_strided_slots(oracle):
         for p in ptrs:
             lib.fcgpu_host_free(p)
         ctx.close()
+
+
+def _counters(lib, h):
+    v = (C.c_uint64 * N.NCOUNTERS)()
+    assert lib.fcgpu_read_counters(h, v, N.NCOUNTERS) == N.OK
+    return list(v)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nsub", [4, 3, 9])
+def test_gpu_auto_shared_queue_fuses_contexts(oracle, nsub):
+    """FCGPU_SPAN_AUTO with >= 4 contexts: zero-copy block submissions go to the
+    device's shared queue and are launched together (one k_rx launch carrying
+    several contexts' batches; launched by the 4th pending submission, or by a
+    wait on one still pending). Every batch gets the oracle's verdicts and
+    hashes, and every context's counters count its own batches only."""
+    lib = N.load()
+    cfg = _cfg()
+    nctx = 5
+    ctxs, blks, exps = [], [], []
+    try:
+        for k in range(nctx):
+            h = C.c_void_p()
+            assert lib.fcgpu_open(0, 8192, C.byref(h)) == N.OK
+            assert lib.fcgpu_configure(h, C.byref(cfg)) == N.OK
+            assert lib.fcgpu_span_mode(h, N.SPAN_AUTO) == N.OK
+            ctxs.append(h)
+        for k in range(nsub):
+            b = synth.c4(1000 + 300 * k, seed=700 + k)
+            synth.inject_errors(b, 0.05, seed=800 + k)
+            blks.append(Block(lib, ctxs[k % nctx], b, 8192))
+            exps.append(oracle.process_batch(cfg, b))
+        # submit everything (slot = round of the context), then wait in reverse
+        subs = []
+        for k in range(nsub):
+            h, slot = ctxs[k % nctx], k // nctx
+            blks[k].res[:] = 0xEE
+            rc = lib.fcgpu_span_submit_block(h, slot, blks[k].pin, blks[k].in_bytes, 0, blks[k].frames_off,
+                                             blks[k].n, blks[k].out, OUTS, N.PART_TILE)
+            assert rc == N.OK, lib.fcgpu_last_error(h)
+            subs.append((h, slot))
+        for k in reversed(range(nsub)):
+            h, slot = subs[k]
+            assert lib.fcgpu_span_wait(h, slot) == N.OK, lib.fcgpu_last_error(h)
+        valid = [0] * nctx
+        for k in range(nsub):
+            L, n, e = blks[k].L, blks[k].n, exps[k]
+            v = blks[k].res[L.verdict:L.verdict + 2 * n].view(np.uint16)
+            hs = blks[k].res[L.hash:L.hash + 4 * n].view(np.uint32)
+            assert np.array_equal(v & 0xff, e["reason"].astype(np.uint16)), k
+            ok = e["reason"] == N.R_OK
+            assert np.array_equal(hs[ok], e["hash"][ok]), k
+            valid[k % nctx] += int(ok.sum())
+        for k in range(nctx):
+            assert _counters(lib, ctxs[k])[N.CTR_COUNT] == valid[k], k
+    finally:
+        for blk in blks:
+            blk.free()
+        for h in ctxs:
+            lib.fcgpu_close(h)
+
+
+@pytest.mark.gpu
+def test_gpu_auto_shared_queue_threads(oracle):
+    """Eight threads, each with its own AUTO context and two slots, submitting
+    and waiting concurrently through the shared queue (ctypes releases the
+    GIL around the calls): every batch's results are the oracle's."""
+    import threading
+    lib = N.load()
+    cfg = _cfg()
+    nthr, rounds = 8, 12
+    batches = []
+    for k in range(4):
+        b = synth.c4(2048 + 256 * k, seed=900 + k)
+        synth.inject_errors(b, 0.05, seed=950 + k)
+        batches.append((b, oracle.process_batch(cfg, b)))
+    errors = []
+
+    def worker(t):
+        h = C.c_void_p()
+        blk = []
+        try:
+            assert lib.fcgpu_open(0, 8192, C.byref(h)) == N.OK
+            assert lib.fcgpu_configure(h, C.byref(cfg)) == N.OK
+            assert lib.fcgpu_span_mode(h, N.SPAN_AUTO) == N.OK
+            blk = [Block(lib, h, batches[(t + s) % 4][0], 8192) for s in range(2)]
+            barrier.wait()
+            for r in range(rounds):
+                s = r % 2
+                if r >= 2:
+                    assert lib.fcgpu_span_wait(h, s) == N.OK, lib.fcgpu_last_error(h)
+                    e = batches[(t + s) % 4][1]
+                    L, n = blk[s].L, blk[s].n
+                    v = blk[s].res[L.verdict:L.verdict + 2 * n].view(np.uint16)
+                    assert np.array_equal(v & 0xff, e["reason"].astype(np.uint16))
+                    blk[s].res[:] = 0xEE
+                rc = lib.fcgpu_span_submit_block(h, s, blk[s].pin, blk[s].in_bytes, 0, blk[s].frames_off, blk[s].n,
+                                                 blk[s].out, OUTS, N.PART_TILE)
+                assert rc == N.OK, lib.fcgpu_last_error(h)
+            for s in range(2):
+                assert lib.fcgpu_span_wait(h, s) == N.OK
+        except Exception as ex:  # noqa: BLE001 -- reported by the main thread
+            errors.append(f"thread {t}: {ex!r}")
+            barrier.abort()
+        finally:
+            for x in blk:
+                x.free()
+            if h:
+                lib.fcgpu_close(h)
+
+    barrier = threading.Barrier(nthr)
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(nthr)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=60)
+    assert not any(th.is_alive() for th in ths), "a thread did not finish"
+    assert not errors, errors
