@@ -1968,6 +1968,12 @@ static int agg_finish(fcgpu_ctx *c, uint32_t slot, bool block) {
         std::lock_guard<std::mutex> g(q.mu);
         if (!sp.al && !sp.agg_err) agg_launch_locked(q);
         al = sp.al;
+        if (!al)    // not launched (a launch failed): it leaves the queue unrun
+            for (size_t m = 0; m < q.pending.size(); ++m)
+                if (q.pending[m].c == c && q.pending[m].slot == slot) {
+                    q.pending.erase(q.pending.begin() + (long)m);
+                    break;
+                }
     }
     hipError_t e = hipSuccess;
     if (al) {
