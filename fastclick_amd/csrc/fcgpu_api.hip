@@ -1868,9 +1868,9 @@ static int agg_launch_locked(AggQueue &q) {
         RxArgs &a = L.A;
         a = RxArgs{};
         a.tilecnt = c0->d_tilecnt;
-        a.ctr = c0->d_ctr;
         a.cfg = c0->dcfg;
         a.fl = c0->fl;
+        a.fl.flowid = nullptr;
         L.njobs = (uint32_t)grp.size();
         L.flow_stride = L.flow_words = 0;
         uint32_t tiles = 0;
@@ -1898,10 +1898,20 @@ static int agg_launch_locked(AggQueue &q) {
         for (uint32_t k = 1; k < L.njobs; ++k)
             if (L.job[k].tile0 != k * L.job_tiles) L.job_tiles = 0;
         if (tiles > L.njobs * L.job_tiles) L.job_tiles = 0;
-        a.arena = L.job[0].arena;
-        a.desc = L.job[0].desc;
-        a.n = L.job[0].n;
+        // the first batch also fills A: a launch of one batch reads A alone
+        const RxJob &J0 = L.job[0];
+        a.arena = J0.arena;
+        a.desc = J0.desc;
+        a.n = J0.n;
         a.ntiles = (a.n + kTile - 1) / kTile;
+        a.verdict = J0.verdict;
+        a.hash = J0.hash;
+        a.anno = J0.anno;
+        a.perm = J0.perm;
+        a.tile_count = J0.tile_count;
+        a.tile_perm = J0.tile_perm;
+        a.ip_rw = J0.ip_rw;
+        a.ctr = J0.ctr;
         const uint32_t si = q.rr++ % 4;
         hipError_t e = q.st[si] ? hipSuccess : hipStreamCreateWithFlags(&q.st[si], hipStreamNonBlocking);
         AggLaunch *al = nullptr;

@@ -362,6 +362,15 @@ int  fcgpu_span_submit_block(fcgpu_ctx *ctx, uint32_t slot, const void *h_in, si
  *   FCGPU_SPAN_AUTO     -- ZEROCOPY while at least 4 contexts of the process
  *                          are in AUTO mode on this device (one per element
  *                          thread), else COPY; decided at each submission.
+ *                          Zero-copy block submissions of AUTO contexts then
+ *                          share one queue per device: the 4th pending one, or
+ *                          a wait/poll on one still pending, launches the
+ *                          pending batches together (one kernel launch carries
+ *                          several contexts' batches of one configuration, each
+ *                          counted in its own context). Flow tables, whole-batch
+ *                          partitions and in-place rewrites keep their own
+ *                          launches. fcgpu_span_wait / fcgpu_span_poll of a slot
+ *                          is how its batch is guaranteed to start.
  * Results are identical in every mode. Returns FCGPU_EINVAL for another mode
  * or while a slot is in flight. */
 #define FCGPU_SPAN_COPY     0u
