@@ -407,20 +407,47 @@ static void launch_rx_prog(int part, uint32_t cm, bool ck, const RxLaunch &L, ui
     else launch_rx_part<kPartNone, PROG>(cm, ck, L, grid, s, e0, e1, jc);
 }
 
-static void launch_rx_any(int part, uint32_t cm, bool ck, const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_t e0,
+// The outputs a k_rx launch stores through without a null check, for the
+// partition shape it is instantiated with (rx_tile: tile_count for
+// kPartTile, tilecnt for kPartGlobal), and the inputs every batch reads: a
+// launch missing one is refused on the host instead of faulting the device.
+static bool rx_launch_ok(int part, const RxLaunch &L, uint32_t grid) {
+    auto batch_ok = [part](const uint8_t *arena, const uint2 *desc, uint32_t n, const uint16_t *tile_count,
+                           const uint32_t *tilecnt) {
+        if (n && (!arena || !desc)) return false;
+        if (part == kPartTile && n && !tile_count) return false;
+        if (part == kPartGlobal && n && !tilecnt) return false;
+        return true;
+    };
+    if (L.njobs <= 1)
+        return batch_ok(L.A.arena, L.A.desc, L.A.n, L.A.tile_count, L.A.tilecnt) && L.A.ctr &&
+               grid <= (L.A.n + kTile - 1) / kTile;
+    if (L.njobs > kMaxFuse) return false;
+    uint32_t tiles = 0;
+    for (uint32_t k = 0; k < L.njobs; ++k) {
+        const RxJob &J = L.job[k];
+        if (!batch_ok(J.arena, J.desc, J.n, J.tile_count, J.tilecnt) || !J.ctr || J.tile0 != tiles) return false;
+        tiles += (J.n + kTile - 1) / kTile;
+    }
+    return grid <= tiles;
+}
+
+static hipError_t launch_rx_any(int part, uint32_t cm, bool ck, const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_t e0,
                           hipEvent_t e1, fcgpu_ctx *jc) {
+    if (!rx_launch_ok(part, L, grid)) return hipErrorInvalidValue;
     if (L.A.cfg.classify == FCGPU_CLS_PROGRAM) launch_rx_prog<true>(part, cm, ck, L, grid, s, e0, e1, jc);
     else launch_rx_prog<false>(part, cm, ck, L, grid, s, e0, e1, jc);
+    return hipSuccess;
 }
 
 // One batch: a.ntiles workgroups.
-static void launch_rx_one(int part, uint32_t cm, bool ck, const RxArgs &a, hipStream_t s, hipEvent_t e0,
+static hipError_t launch_rx_one(int part, uint32_t cm, bool ck, const RxArgs &a, hipStream_t s, hipEvent_t e0,
                           hipEvent_t e1, fcgpu_ctx *jc) {
     RxLaunch L;
     L.A = a;
     L.njobs = 1;
     L.job_tiles = 0;
-    launch_rx_any(part, cm, ck, L, a.ntiles, s, e0, e1, jc);
+    return launch_rx_any(part, cm, ck, L, a.ntiles, s, e0, e1, jc);
 }
 
 // Whole batch in one shot (FCGPU_PART_GLOBAL: the partition spans the batch).
@@ -1165,8 +1192,8 @@ static int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_d
         HIPCHK(c, hipEventRecord(c->flow_order[0], c->stream));
         HIPCHK(c, hipStreamWaitEvent(s, c->flow_order[0], 0));
     }
-    launch_rx_one(part, c->cfg.check_mode, c->cfg.checksum != 0, a, s, timed ? ev[0].a : nullptr,
-                  timed ? ev[0].b : nullptr, c->jit_src.empty() ? nullptr : c);
+    HIPCHK(c, launch_rx_one(part, c->cfg.check_mode, c->cfg.checksum != 0, a, s, timed ? ev[0].a : nullptr,
+                            timed ? ev[0].b : nullptr, c->jit_src.empty() ? nullptr : c));
     HIPCHK(c, hipGetLastError());
     if (a.fl.slots) {   // the batch's new flows get their IDs (fcgpu_flow.hh)
         HIPCHK(c, flow_pass(c, a.fl, n, s));
@@ -1349,8 +1376,8 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
     // (profiles/r02_s9/evt_ab.txt); the markers' interval adds only the
     // launch's dispatch latency, shared by its batches
     if (timed) HIPCHK(c, hipEventRecord(ev.a, s));
-    launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, L, tiles, s, nullptr, nullptr,
-                  c->jit_src.empty() ? nullptr : c);
+    HIPCHK(c, launch_rx_any(part, c->cfg.check_mode, c->cfg.checksum != 0, L, tiles, s, nullptr, nullptr,
+                            c->jit_src.empty() ? nullptr : c));
     if (timed) HIPCHK(c, hipEventRecord(ev.b, s));
     HIPCHK(c, hipGetLastError());
     if (timed) c->pending.push_back(ev);
@@ -1923,9 +1950,9 @@ static int agg_launch_locked(AggQueue &q) {
             if (e == hipSuccess) e = hipEventCreateWithFlags(&al->ev, hipEventDisableTiming);
         }
         if (e == hipSuccess) {
-            launch_rx_any(part, c0->cfg.check_mode, c0->cfg.checksum != 0, L, tiles, q.st[si], nullptr, nullptr,
-                          c0->jit_src.empty() ? nullptr : c0);
-            e = hipGetLastError();
+            e = launch_rx_any(part, c0->cfg.check_mode, c0->cfg.checksum != 0, L, tiles, q.st[si], nullptr,
+                              nullptr, c0->jit_src.empty() ? nullptr : c0);
+            if (e == hipSuccess) e = hipGetLastError();
         }
         if (e == hipSuccess) e = hipEventRecord(al->ev, q.st[si]);
         al->refs = (uint32_t)grp.size();
