@@ -122,44 +122,146 @@ int fcpcap_map(fcpcap *r, const uint8_t **base, size_t *bytes) {
     return 0;
 }
 
+// One record header at pos of the mapped file, by FromDump::read_packet's
+// rules (fromdump.cc:446-466, as fcpcap_read): 1 parsed, 0 the record does not
+// fit in the file (a truncated final record), -1 a bad header.
+namespace {
+struct Rec {
+    uint32_t len, caplen;
+    size_t size;                 // header + captured bytes (+ bytes past len)
+    uint64_t ts_ns;
+};
+inline int parse_rec(const fcpcap *r, size_t pos, Rec &o) {
+    if (pos + 16 > r->map_bytes) return 0;
+    uint32_t h[4];
+    memcpy(h, r->map + pos, 16);
+    if (r->swapped)
+        for (auto &x : h) x = sw32(x);
+    uint32_t len, caplen, skip = 0;
+    if (r->minor > 3 || (r->minor == 3 && h[2] <= h[3])) {
+        len = h[3];
+        caplen = h[2];
+    } else {
+        len = h[2];
+        caplen = h[3];
+    }
+    if (caplen > 65535) return -1;
+    if (caplen > len) {
+        skip = caplen - len;
+        caplen = len;
+    }
+    o.len = len;
+    o.caplen = caplen;
+    o.size = (size_t)16 + r->extra + caplen + skip;
+    o.ts_ns = (uint64_t)h[0] * 1000000000ull + (uint64_t)h[1] * (r->nano ? 1ull : 1000ull);
+    if (pos + o.size > r->map_bytes) return 0;
+    return 1;
+}
+// Could a record header start at pos? For the parallel walk's speculative
+// starts only: a sub-second field in range and a sane length, for 16
+// consecutive records (or to the end of the range). A wrong guess is caught
+// when the walks are stitched.
+inline bool plausible_chain(const fcpcap *r, size_t pos, size_t end) {
+    for (int k = 0; k < 16 && pos < end; ++k) {
+        Rec q;
+        if (parse_rec(r, pos, q) != 1) return false;
+        uint32_t frac;
+        memcpy(&frac, r->map + pos + 4, 4);
+        if (r->swapped) frac = sw32(frac);
+        if (frac >= (r->nano ? 1000000000u : 1000000u) || q.len > (1u << 24)) return false;
+        pos += q.size;
+    }
+    return true;
+}
+struct Walk {
+    size_t from = 0, end = 0;    // first record start; the position after the walk's last record
+    size_t bad = (size_t)-1;     // position of a bad header the walk stopped at
+    std::vector<size_t> pos;     // record starts
+    std::vector<Rec> rec;
+};
+// Records from `from` while their starts are below `stop` (and fit the file).
+void walk(const fcpcap *r, size_t from, size_t stop, Walk &w) {
+    w.from = from;
+    w.pos.clear();
+    w.rec.clear();
+    w.bad = (size_t)-1;
+    size_t pos = from;
+    while (pos < stop) {
+        Rec q;
+        const int k = parse_rec(r, pos, q);
+        if (k < 0) { w.bad = pos; break; }
+        if (k == 0) break;
+        w.pos.push_back(pos);
+        w.rec.push_back(q);
+        pos += q.size;
+    }
+    w.end = pos;
+}
+}  // namespace
+
 int fcpcap_index(fcpcap *r, uint32_t max, size_t max_bytes, size_t *chunk_off, size_t *chunk_bytes, uint32_t *desc,
                  uint32_t *wire, uint64_t *ts_ns) {
     if (!r || !r->map || !chunk_off || !chunk_bytes || !desc) return -1;
     const uint32_t hdr = 16 + r->extra;
-    size_t pos = (size_t)r->fpos;
-    const size_t start = pos;
-    uint32_t n = 0;
-    while (n < max && pos + 16 <= r->map_bytes) {
-        uint32_t h[4];
-        memcpy(h, r->map + pos, 16);
-        if (r->swapped)
-            for (auto &x : h) x = sw32(x);
-        uint32_t len, caplen, skip = 0;     // as in fcpcap_read (fromdump.cc:446-466)
-        if (r->minor > 3 || (r->minor == 3 && h[2] <= h[3])) {
-            len = h[3];
-            caplen = h[2];
-        } else {
-            len = h[2];
-            caplen = h[3];
+    const size_t start = (size_t)r->fpos;
+    const size_t lim = std::min(r->map_bytes, start + max_bytes);   // record starts of this chunk lie below
+    // the walk over [start, lim): in T pieces on T threads when the chunk is
+    // large -- piece 0 from the exact start, the others from the first
+    // plausible record header at or after their piece's start, each until
+    // its records start in the next piece; stitched in order, a piece whose
+    // guessed start is not where the walk before it ended is walked again
+    // from there. The result is the sequential walk's, record for record.
+    const size_t span = lim > start ? lim - start : 0;
+    const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>(r->threads, span >> 22));   // >= 4 MiB each
+    std::vector<Walk> w(T);
+    std::vector<size_t> b(T + 1);
+    for (unsigned t = 0; t <= T; ++t) b[t] = start + span * t / T;
+    auto piece = [&](unsigned t) {
+        size_t from = b[t];
+        if (t) {
+            const size_t last = std::min(b[t + 1], b[t] + (size_t)hdr + 65535 * 2);
+            while (from < last && !plausible_chain(r, from, lim)) ++from;
+            if (from >= last) { w[t].from = (size_t)-1; return; }
         }
-        if (caplen > 65535) {
+        walk(r, from, b[t + 1], w[t]);
+    };
+    if (T > 1) {
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < T; ++t) th.emplace_back(piece, t);
+        piece(0);
+        for (auto &x : th) x.join();
+        for (unsigned t = 1; t < T; ++t)
+            if (w[t].from != w[t - 1].end || w[t - 1].bad != (size_t)-1) {
+                if (w[t - 1].bad != (size_t)-1) { w.resize(t); break; }   // the bad header ends the walk
+                walk(r, w[t - 1].end, b[t + 1], w[t]);
+            }
+    } else {
+        walk(r, start, lim, w[0]);
+    }
+    // the chunk: up to max records, the last ending within max_bytes of the start
+    uint32_t n = 0;
+    size_t pos = start;
+    for (const Walk &x : w) {
+        for (size_t k = 0; k < x.pos.size() && n < max; ++k) {
+            const Rec &q = x.rec[k];
+            if (x.pos[k] + q.size - start > max_bytes && n) goto done;
+            desc[2 * n] = (uint32_t)(x.pos[k] + hdr - start);
+            desc[2 * n + 1] = q.caplen;
+            if (wire) wire[n] = q.len;
+            if (ts_ns) ts_ns[n] = q.ts_ns;
+            ++n;
+            pos = x.pos[k] + q.size;
+        }
+        if (n >= max) break;
+        if (x.bad != (size_t)-1) {
+            // reached: the records before it leave now, and the next call
+            // starts at the bad header and fails (FromDump stops there too)
+            if (n) goto done;
             r->err = "bad packet header; giving up";
             return -1;
         }
-        if (caplen > len) {
-            skip = caplen - len;
-            caplen = len;
-        }
-        const size_t rec = (size_t)hdr + caplen + skip;
-        if (pos + rec > r->map_bytes) break;          // truncated final record
-        if (pos + rec - start > max_bytes && n) break;
-        desc[2 * n] = (uint32_t)(pos + hdr - start);
-        desc[2 * n + 1] = caplen;
-        if (wire) wire[n] = len;
-        if (ts_ns) ts_ns[n] = (uint64_t)h[0] * 1000000000ull + (uint64_t)h[1] * (r->nano ? 1ull : 1000ull);
-        ++n;
-        pos += rec;
     }
+done:
     *chunk_off = start;
     *chunk_bytes = pos - start;
     r->fpos = (off_t)pos;

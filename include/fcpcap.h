@@ -44,8 +44,11 @@ int  fcpcap_read(fcpcap *r, uint8_t *buf, size_t cap, uint32_t *desc, uint32_t *
 int  fcpcap_map(fcpcap *r, const uint8_t **base, size_t *bytes);
 /* Index the next records of the mapped file (up to max packets / max_bytes):
  * the chunk is [base + *chunk_off, + *chunk_bytes); desc offsets are relative
- * to its start. Returns the count (0 at the end), -1 on a bad record. Do not
- * mix with fcpcap_read on one reader. */
+ * to its start. Returns the count (0 at the end), -1 on a bad record header
+ * (the records before it came with this call or the previous one). With
+ * fcpcap_set_threads(T > 1) a chunk of >= 8 MiB is walked in up to T pieces
+ * in parallel and stitched; the records are exactly the one-thread walk's.
+ * Do not mix with fcpcap_read on one reader. */
 int  fcpcap_index(fcpcap *r, uint32_t max, size_t max_bytes, size_t *chunk_off, size_t *chunk_bytes,
                   uint32_t *desc, uint32_t *wire, uint64_t *ts_ns);
 const char *fcpcap_error(const fcpcap *r);

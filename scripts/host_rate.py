@@ -83,6 +83,8 @@ def gather_only_mpps(n=1 << 20, reps=10):
 
 
 def pcap_mpps(n=1 << 22, chunk_pkts=1 << 18, threads=1, mapped=False):
+    # (chunk_pkts 256K records of 76 B = ~20 MB per chunk: walked in pieces of
+    # >= 4 MiB when threads > 1 and mapped)
     """pcap ingress (fcpcap + fcgpu_span_submit): a C2 trace written as a pcap
     (16-B record header + 60-B frame per packet), read from the page cache
     into pinned chunks and copied as-is; verdict + hash come back. The file is
@@ -221,6 +223,8 @@ def main():
     m, reg = pcap_mpps(mapped=True)
     out["pcap_ingress_mpps_4M_mapped"] = round(m, 2)
     out["pcap_mapped_registered"] = bool(reg)
+    for t in (4, 8):    # the record-header walk in parallel pieces (fcpcap_index)
+        out[f"pcap_ingress_mpps_4M_mapped_t{t}"] = round(pcap_mpps(mapped=True, threads=t)[0], 2)
     out["mbuf_ingress_mpps_256k_shuffled"] = round(mbuf_mpps(), 2)
     out["mbuf_ingress_mpps_256k_sequential"] = round(mbuf_mpps(order="sequential"), 2)
     out["mbuf_ingress_mpps_256k_shuffled_2streams"] = round(mbuf_mpps(streams=2), 2)

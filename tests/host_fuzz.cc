@@ -185,6 +185,56 @@ static void fuzz_pcap(Rng &rng) {
     }
 }
 
+// The mapped index of one file, one call at a time: every call's outcome.
+static std::vector<std::vector<uint64_t>> index_calls(const std::string &path, unsigned threads, uint32_t max,
+                                                      size_t max_bytes) {
+    std::vector<std::vector<uint64_t>> calls;
+    fcpcap *r = nullptr;
+    char err[256];
+    if (fcpcap_open(path.c_str(), &r, err, sizeof err) != 0) return calls;
+    fcpcap_set_threads(r, threads);
+    const uint8_t *base = nullptr;
+    size_t bytes = 0;
+    CHECK(fcpcap_map(r, &base, &bytes) == 0);
+    std::vector<uint32_t> desc(2ull * max), wire(max);
+    std::vector<uint64_t> ts(max);
+    for (int it = 0; it < 100000; ++it) {
+        size_t off = 0, cb = 0;
+        const int n = fcpcap_index(r, max, max_bytes, &off, &cb, desc.data(), wire.data(), ts.data());
+        std::vector<uint64_t> c{(uint64_t)(int64_t)n, off, cb};
+        for (int i = 0; i < n; ++i) {
+            CHECK((size_t)desc[2 * i] + desc[2 * i + 1] <= cb && off + cb <= bytes);
+            c.insert(c.end(), {desc[2 * i], desc[2 * i + 1], wire[i], ts[i]});
+        }
+        calls.push_back(c);
+        if (n <= 0) break;
+    }
+    fcpcap_close(r);
+    return calls;
+}
+
+// The parallel mapped index (fcpcap_set_threads > 1, chunks of >= 8 MiB) is
+// the one-thread walk, call for call -- on a ~20 MB file and on copies with
+// flipped bits and forced huge caplens. Once per run (under ThreadSanitizer
+// this is the check that its threads share nothing but the read-only map).
+static void check_parallel_index(Rng &rng) {
+    for (int v = 0; v < 3; ++v) {
+        PcapSpec sp{v == 1 ? 0xa1b23c4du : 0xa1b2c3d4u, v == 2, 4};
+        uint32_t expect = 0;
+        auto f = make_pcap(rng, sp, 26000, expect);
+        if (v) {
+            for (int k = 0; k < 40; ++k) f[24 + rng() % (f.size() - 24)] ^= (uint8_t)(1u << (rng() % 8));
+            if (v == 2) f[f.size() / 2] = 0xff;
+        }
+        const std::string p = write_tmp(f);
+        for (size_t mb : {(size_t)9 << 20, (size_t)16 << 20}) {
+            const auto ref = index_calls(p, 1, 1u << 20, mb);
+            for (unsigned t : {2u, 4u, 7u}) CHECK(index_calls(p, t, 1u << 20, mb) == ref);
+        }
+        unlink(p.c_str());
+    }
+}
+
 // ---- 2. decision-program text -------------------------------------------------
 static void fuzz_program(Rng &rng, const std::vector<std::string> &progs) {
     if (progs.empty()) return;
@@ -355,6 +405,7 @@ int main(int argc, char **argv) {
     const double budget = argc > 2 ? atof(argv[2]) : 5.0;
     Rng rng(argc > 3 ? strtoull(argv[3], nullptr, 10) : 12345);
     const auto t0 = std::chrono::steady_clock::now();
+    check_parallel_index(rng);
     long it = 0;
     for (;; ++it) {
         fuzz_pcap(rng);

@@ -180,3 +180,71 @@ def test_gpu_pcap_ingress_flows(tmp_path):
                              max_flows=1 << 16)
     assert np.array_equal(out["flowid"], g["flowid"])
     assert out["flow_count"] == int(g["flowid"][g["flowid"] != N.FLOW_NONE].max()) + 1
+
+
+def _fake_chain_frame(rng, nrec):
+    """A frame whose payload is itself a run of nrec tiny, plausible pcap
+    records: a parallel walk that starts inside it syncs on a false chain."""
+    body = b"".join(struct.pack("<IIII", 5, int(rng.integers(0, 999_999)), 8, 8) + bytes(8) for _ in range(nrec))
+    return bytes(14) + body
+
+
+def _index_all(path, threads, max_pkts, max_bytes):
+    from fastclick_amd.pcap import PcapReader
+    rd = PcapReader(path, threads)
+    rd.map()
+    desc = np.zeros(2 * max_pkts, np.uint32)
+    wire = np.zeros(max_pkts, np.uint32)
+    tsn = np.zeros(max_pkts, np.uint64)
+    calls = []
+    try:
+        while True:
+            try:
+                n, off, nb = rd.index(max_pkts, max_bytes, desc.ctypes.data, wire.ctypes.data, tsn.ctypes.data)
+            except OSError as e:
+                calls.append(("error", str(e)))
+                break
+            calls.append((n, off, nb, desc[:2 * n].tobytes(), wire[:n].tobytes(), tsn[:n].tobytes()))
+            if n == 0:
+                break
+    finally:
+        rd.close()
+    return calls
+
+
+@pytest.mark.parametrize("variant", ["plain", "fake_chains", "truncated", "bad_mid", "nano_swapped"])
+def test_reader_parallel_index_is_the_sequential_walk(tmp_path, variant):
+    """fcpcap_index with 2-8 threads (chunks of >= 8 MiB walked in pieces,
+    speculative piece starts, stitched) gives exactly the one-thread walk's
+    calls: counts, chunk offsets and sizes, descriptors, wire lengths and
+    time stamps -- also when frame payloads hold false record chains, the last
+    record is cut, or a bad header (caplen > 65535) sits mid-file."""
+    rng = np.random.default_rng(41)
+    frames, total = [], 0
+    noise = rng.integers(0, 256, 1 << 21, dtype=np.uint8).tobytes()
+    while total < (26 << 20):
+        if variant == "fake_chains" and rng.random() < 0.4:
+            fr = _fake_chain_frame(rng, int(rng.integers(18, 60)))
+        else:
+            a = int(rng.integers(0, len(noise) - 1600))
+            fr = noise[a:a + int(rng.integers(40, 1600))]
+        frames.append(fr)
+        total += len(fr) + 16
+    p = str(tmp_path / "big.pcap")
+    kw = {}
+    if variant == "nano_swapped":
+        kw = dict(magic=0xA1B23C4D, swapped=True)
+    write_pcap(p, frames, cut_last=7 if variant == "truncated" else 0, **kw)
+    if variant == "bad_mid":
+        # frame 20000's header: caplen 70000 (FromDump: "bad packet header")
+        off = 24 + sum(len(f) + 16 for f in frames[:20000])
+        with open(p, "r+b") as f:
+            f.seek(off + 8)
+            f.write(struct.pack("<II", 70000, 70000))
+    for max_pkts, max_bytes in ((1 << 20, 24 << 20), (40_000, 16 << 20), (1 << 20, 9 << 20)):
+        ref = _index_all(p, 1, max_pkts, max_bytes)
+        assert sum(c[0] for c in ref if c[0] != "error") > 0
+        if variant == "bad_mid":
+            assert ref[-1][0] == "error"
+        for t in (2, 4, 8):
+            assert _index_all(p, t, max_pkts, max_bytes) == ref, (t, max_pkts, max_bytes)
