@@ -83,12 +83,11 @@ def gather_only_mpps(n=1 << 20, reps=10):
 
 
 def pcap_mpps(n=1 << 22, chunk_pkts=1 << 18, threads=1, mapped=False):
-    # (chunk_pkts 256K records of 76 B = ~20 MB per chunk: walked in pieces of
-    # >= 4 MiB when threads > 1 and mapped)
     """pcap ingress (fcpcap + fcgpu_span_submit): a C2 trace written as a pcap
     (16-B record header + 60-B frame per packet), read from the page cache
     into pinned chunks and copied as-is; verdict + hash come back. The file is
-    read once untimed so it is in the page cache."""
+    read once untimed so it is in the page cache. (A chunk of 256K records of
+    76 B is ~20 MB: walked in pieces of >= 4 MiB when threads > 1 and mapped.)"""
     import tempfile
     from fastclick_amd.pcap import process_pcap
     b = synth.c2(1 << 16)
