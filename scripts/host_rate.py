@@ -277,5 +277,14 @@ if __name__ == "__main__":
         thread_sweep()
     elif len(sys.argv) > 1 and sys.argv[1] == "span":
         span_sweep()
+    elif len(sys.argv) > 1 and sys.argv[1] == "pcap":
+        out = {}
+        for rep in range(2):
+            for t in (1, 4):
+                out[f"pcap_copy_t{t}_{rep}"] = round(pcap_mpps(threads=t), 1)
+            for t in (1, 2, 4, 8):
+                out[f"pcap_mapped_t{t}_{rep}"] = round(pcap_mpps(mapped=True, threads=t)[0], 1)
+            print(json.dumps(out), file=sys.stderr, flush=True)
+        print(json.dumps(out))
     else:
         main()
