@@ -158,23 +158,17 @@ inline int parse_rec(const fcpcap *r, size_t pos, Rec &o) {
     return 1;
 }
 // Could a record header start at pos? For the parallel walk's speculative
-// starts only: for 16 consecutive records (or to the end of the range), a
-// sub-second field in range, seconds within a day of the first record's, and
-// at least an Ethernet header captured of a sane length (runs of zero bytes
-// would otherwise parse as empty records). A wrong guess is caught when the
-// walks are stitched; a file of tiny records is just walked again in order.
+// starts only: a sub-second field in range and a sane length, for 16
+// consecutive records (or to the end of the range). A wrong guess is caught
+// when the walks are stitched.
 inline bool plausible_chain(const fcpcap *r, size_t pos, size_t end) {
-    uint32_t sec0 = 0;
     for (int k = 0; k < 16 && pos < end; ++k) {
         Rec q;
         if (parse_rec(r, pos, q) != 1) return false;
-        uint32_t t[2];
-        memcpy(t, r->map + pos, 8);
-        if (r->swapped) { t[0] = sw32(t[0]); t[1] = sw32(t[1]); }
-        if (!k) sec0 = t[0];
-        const uint32_t dsec = t[0] > sec0 ? t[0] - sec0 : sec0 - t[0];
-        if (t[1] >= (r->nano ? 1000000000u : 1000000u) || dsec > 86400 || q.caplen < 14 || q.len > (1u << 24))
-            return false;
+        uint32_t frac;
+        memcpy(&frac, r->map + pos + 4, 4);
+        if (r->swapped) frac = sw32(frac);
+        if (frac >= (r->nano ? 1000000000u : 1000000u) || q.len > (1u << 24)) return false;
         pos += q.size;
     }
     return true;

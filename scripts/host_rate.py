@@ -86,8 +86,7 @@ def pcap_mpps(n=1 << 22, chunk_pkts=1 << 18, threads=1, mapped=False):
     """pcap ingress (fcpcap + fcgpu_span_submit): a C2 trace written as a pcap
     (16-B record header + 60-B frame per packet), read from the page cache
     into pinned chunks and copied as-is; verdict + hash come back. The file is
-    read once untimed so it is in the page cache. (A chunk of 256K records of
-    76 B is ~20 MB: walked in pieces of >= 4 MiB when threads > 1 and mapped.)"""
+    read once untimed so it is in the page cache."""
     import tempfile
     from fastclick_amd.pcap import process_pcap
     b = synth.c2(1 << 16)
@@ -222,8 +221,6 @@ def main():
     m, reg = pcap_mpps(mapped=True)
     out["pcap_ingress_mpps_4M_mapped"] = round(m, 2)
     out["pcap_mapped_registered"] = bool(reg)
-    for t in (4, 8):    # the record-header walk in parallel pieces (fcpcap_index)
-        out[f"pcap_ingress_mpps_4M_mapped_t{t}"] = round(pcap_mpps(mapped=True, threads=t)[0], 2)
     out["mbuf_ingress_mpps_256k_shuffled"] = round(mbuf_mpps(), 2)
     out["mbuf_ingress_mpps_256k_sequential"] = round(mbuf_mpps(order="sequential"), 2)
     out["mbuf_ingress_mpps_256k_shuffled_2streams"] = round(mbuf_mpps(streams=2), 2)
@@ -282,8 +279,7 @@ if __name__ == "__main__":
         for rep in range(2):
             for t in (1, 4):
                 out[f"pcap_copy_t{t}_{rep}"] = round(pcap_mpps(threads=t), 1)
-            for t in (1, 2, 4, 8):
-                out[f"pcap_mapped_t{t}_{rep}"] = round(pcap_mpps(mapped=True, threads=t)[0], 1)
+            out[f"pcap_mapped_{rep}"] = round(pcap_mpps(mapped=True)[0], 1)
             print(json.dumps(out), file=sys.stderr, flush=True)
         print(json.dumps(out))
     else:
