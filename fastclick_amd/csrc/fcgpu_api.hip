@@ -1820,12 +1820,18 @@ int fcgpu_span_submit(fcgpu_ctx *c, uint32_t slot, const uint8_t *h_span, size_t
 constexpr uint32_t kZeroCopyAuto = 4;
 static std::mutex g_auto_mu;
 static std::map<int, uint32_t> g_auto_ctx;
+static void agg_release(int device);
 static void span_auto_count(fcgpu_ctx *c, uint32_t new_mode) {
     const bool was = c->span_mode == FCGPU_SPAN_AUTO, now = new_mode == FCGPU_SPAN_AUTO;
     if (was == now) return;
-    std::lock_guard<std::mutex> g(g_auto_mu);
-    uint32_t &n = g_auto_ctx[c->device];
-    n = now ? n + 1 : (n ? n - 1 : 0);
+    bool last = false;
+    {
+        std::lock_guard<std::mutex> g(g_auto_mu);
+        uint32_t &n = g_auto_ctx[c->device];
+        n = now ? n + 1 : (n ? n - 1 : 0);
+        last = n == 0;
+    }
+    if (last) agg_release(c->device);
 }
 static bool span_zerocopy(const fcgpu_ctx *c) {
     if (c->span_mode != FCGPU_SPAN_AUTO) return c->span_mode == FCGPU_SPAN_ZEROCOPY;
@@ -1982,6 +1988,31 @@ static int agg_launch_locked(AggQueue &q) {
     }
     return FCGPU_OK;
 }
+// The last AUTO context of a device is gone: every submission it queued was
+// waited for (fcgpu_close / fcgpu_span_mode wait or refuse busy slots), so
+// the queue's streams and events are idle and go.
+static void agg_release(int device) {
+    AggQueue *q = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_agg_mu);
+        auto it = g_agg.find(device);
+        if (it == g_agg.end()) return;
+        q = it->second;
+    }
+    std::lock_guard<std::mutex> g(q->mu);
+    if (!q->pending.empty()) return;
+    for (AggLaunch *al : q->spare) {
+        if (al->ev) hipEventDestroy(al->ev);
+        delete al;
+    }
+    q->spare.clear();
+    for (hipStream_t &st : q->st)
+        if (st) {
+            hipStreamDestroy(st);
+            st = nullptr;
+        }
+}
+
 // Queue one zero-copy block submission (device addresses in j).
 static int agg_submit(fcgpu_ctx *c, uint32_t slot, const fcgpu_job &j) {
     AggQueue &q = agg_queue(c->device);
