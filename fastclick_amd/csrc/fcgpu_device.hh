@@ -1424,21 +1424,25 @@ __global__ __launch_bounds__(kTile) void k_part_multi(PartMulti M) {
     if (t0 == 0 && M.port_start[j] && tid <= nb) M.port_start[j][tid] = s_base[tid];
     const uint64_t lt = (1ull << lane) - 1ull;
     const uint32_t nbits = 32 - __clz(nb - 1 | 1);
-    uint32_t v = 0xffffu, off = 0;
-    if (t0 < nt) {
-        const uint32_t i = t0 * kTile + tid;
-        if (i < n) v = verdict[i];
-        if (tid < nb && n) off = tileoff[(size_t)tid * ntiles + t0];
-    }
-    for (uint32_t u = 0; u < M.tpw && t0 + u < nt; ++u) {
-        const uint32_t tile = t0 + u, i = tile * kTile + tid;
-        // the next tile's loads go out before this one's work
-        uint32_t vn = 0xffffu, offn = 0;
-        if (u + 1 < M.tpw && tile + 1 < nt) {
-            const uint32_t in = i + kTile;
-            if (in < n) vn = verdict[in];
-            if (tid < nb && n) offn = tileoff[(size_t)tid * ntiles + tile + 1];
+    // every tile's verdicts and offsets are loaded up front (registers, the
+    // loops unrolled over kPartTiles): the tiles' work then waits for memory
+    // once, not once per tile
+    uint32_t vv[kPartTiles], oo[kPartTiles];
+#pragma unroll
+    for (uint32_t u = 0; u < kPartTiles; ++u) {
+        vv[u] = 0xffffu;
+        oo[u] = 0;
+        if (u < M.tpw && t0 + u < nt) {
+            const uint32_t i = (t0 + u) * kTile + tid;
+            if (i < n) vv[u] = verdict[i];
+            if (tid < nb && n) oo[u] = tileoff[(size_t)tid * ntiles + t0 + u];
         }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kPartTiles; ++u) {
+        if (u >= M.tpw || t0 + u >= nt) break;   // workgroup-uniform
+        const uint32_t tile = t0 + u, i = tile * kTile + tid;
+        const uint32_t v = vv[u], off = oo[u];
         const bool live = i < n;
         const uint32_t bin = live ? (v >> 8) : 0xffffffffu;
         const uint64_t grp = match_any(bin, nbits, __ballot(live));
@@ -1454,8 +1458,6 @@ __global__ __launch_bounds__(kTile) void k_part_multi(PartMulti M) {
             M.perm[j][s_base[bin] + s_off[u & 1][bin] + wpre + rank] = i;
         }
         __syncthreads();   // the counts are read before the next tile resets them
-        v = vn;
-        off = offn;
     }
 }
 
