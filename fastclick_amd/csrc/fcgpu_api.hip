@@ -2063,6 +2063,8 @@ static int agg_finish(fcgpu_ctx *c, uint32_t slot, bool block) {
     return 1;
 }
 
+int fcgpu_span_zerocopy_active(const fcgpu_ctx *c) { return c && span_zerocopy(c) ? 1 : 0; }
+
 int fcgpu_span_mode(fcgpu_ctx *c, uint32_t mode) {
     if (!c || mode > FCGPU_SPAN_AUTO) return FCGPU_EINVAL;
     for (const SpanSlot &sp : c->span)

@@ -71,8 +71,11 @@
 //     headers SetIPChecksum rejects are killed; the rewritten ttl/checksum
 //     bytes are written back into each packet.
 //   MODE CHECK|MARK|AUTO, HASH NONE|FLOWID|FLOW5ID, STRIP, DEVICE,
-//   BATCH (packets per device batch, default 16384; 0: each incoming
-//   PacketBatch is one), TIMER (us, default 100; -1 none),
+//   BATCH (packets per device batch; 0: each incoming PacketBatch is one;
+//   default auto: 16384 while the batches are copied, 4096 while they are
+//   zero-copy -- many threads' batches then share the PCIe-read path, and
+//   smaller ones keep each thread's round trip short: profiles/r03_s24),
+//   TIMER (us, default 100; -1 none),
 //   SLOTS (default 2): device batches a thread stages or has in flight
 //   (double or triple buffering),
 //   ZEROCOPY true|false|auto (default auto): true -- the device reads each
@@ -234,8 +237,14 @@ class RxCore {
                 if (!parse_bool(v, _strip)) return err(errh, "STRIP expects true/false");
                 strip_set = true;
             } else if (k == "BATCH") {
-                if (!parse_int(v, n) || n < 0 || n > (1L << 24)) return err(errh, "bad BATCH");
-                _batch = (uint32_t)n;                  // 0: every incoming PacketBatch is one device batch
+                if (v == "auto" || v == "AUTO") {
+                    _batch = kBatchCopy;
+                    _batch_auto = true;
+                } else {
+                    if (!parse_int(v, n) || n < 0 || n > (1L << 24)) return err(errh, "bad BATCH");
+                    _batch = (uint32_t)n;              // 0: every incoming PacketBatch is one device batch
+                    _batch_auto = false;
+                }
             } else if (k == "TIMER") {
                 if (!parse_int(v, n) || n < -1 || n > 10000000) return err(errh, "TIMER expects microseconds (-1: none)");
                 _timer_us = n;
@@ -316,6 +325,7 @@ class RxCore {
             for (size_t j = 0; j < if_good.size(); ++j) _cfg.gooddst[j] = if_good[j];
         }
         if (!strip_set) _strip = (_cfg.check_mode == FCGPU_CHECK_AUTO);
+        _eff_batch = _batch;
         const bool ip4 = _cfg.check_mode == FCGPU_CHECK_IP4 || _cfg.check_mode == FCGPU_MARK_IP4;
         if (_cfg.l4_mode != FCGPU_L4_NONE && !ip4) return err(errh, "L4 needs MODE CHECK or MARK");
         if (_flow_cap && !ip4) return err(errh, "FLOW_CAPACITY needs MODE CHECK or MARK");
@@ -607,7 +617,7 @@ class RxCore {
         s->desc[2 * s->n + 1] = len;
         s->pkts[s->n++] = p;
         s->used += rec;
-        if (s->n == _cap || (_batch && s->n >= _batch)) submit(emit);
+        if (s->n == _cap || (_batch && s->n >= _eff_batch)) submit(emit);
     }
 
     // The current slot goes to the device (asynchronous); the next slot is
@@ -621,6 +631,8 @@ class RxCore {
             if (_flow_cap && _flow_timeout) flow_clock();
             const int rc = fcgpu_span_submit_block(_ctx, k, s.in, s.frames_off + s.used, 0, s.frames_off, s.n,
                                                    s.res, _outputs, _partition);
+            // BATCH auto: the next batches' size for the path they now take
+            _eff_batch = _batch_auto && fcgpu_span_zerocopy_active(_ctx) ? kBatchZeroCopy : _batch;
             if (rc != FCGPU_OK) {
                 fail_slot(s, fcgpu_last_error(_ctx));
             } else {
@@ -858,7 +870,10 @@ class RxCore {
     bool _flow_runs = true;
     std::atomic<uint64_t> _flow_drops{0};       // read by handlers on other threads
     int _device = 0;
-    uint32_t _batch = 16384;
+    static constexpr uint32_t kBatchCopy = 16384, kBatchZeroCopy = 4096;
+    uint32_t _batch = kBatchCopy;
+    bool _batch_auto = true;                     // BATCH auto (the default)
+    uint32_t _eff_batch = kBatchCopy;            // packets per device batch now (BATCH auto: by the span path)
     int64_t _timer_us = 100;
     uint32_t _cap = 0;
     uint32_t _capture = fcgpu::kCaptureMin;

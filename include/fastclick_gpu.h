@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 16
+#define FCGPU_ABI_VERSION 17
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -377,6 +377,10 @@ int  fcgpu_span_submit_block(fcgpu_ctx *ctx, uint32_t slot, const void *h_in, si
 #define FCGPU_SPAN_ZEROCOPY 1u
 #define FCGPU_SPAN_AUTO     2u
 int  fcgpu_span_mode(fcgpu_ctx *ctx, uint32_t mode);
+/* 1 if the context's next block submission would be zero-copy (ZEROCOPY, or
+ * AUTO with enough contexts), else 0 -- e.g. for an element that stages
+ * smaller batches when its batches share the PCIe-read path with others. */
+int  fcgpu_span_zerocopy_active(const fcgpu_ctx *ctx);
 
 /* Decision programs. A program is the step list the
  * reference's own compiler produces and prints through the `program` handler

@@ -411,3 +411,36 @@ def test_element_zerocopy_matches_copy(oracle, wl, conf, nsinks):
         e = oracle.process_batch(cfg, b)
         port = e["port"].astype(np.uint32)
         assert np.array_equal(z["port"], np.where(port < nsinks, port, 0xFFFFFFFF))
+
+
+@pytest.mark.gpu
+def test_element_default_with_many_contexts(oracle):
+    """The element's defaults (ZEROCOPY auto, BATCH auto) when four more AUTO
+    contexts share the GPU, as in a 5-thread configuration: its batches go
+    zero-copy through the shared queue, 4096 packets each -- outputs, order,
+    annotations and handlers as the oracle says."""
+    import ctypes as C
+    from fastclick_amd import click as K
+    lib = N.load()
+    others = []
+    try:
+        for _ in range(4):
+            h = C.c_void_p()
+            assert lib.fcgpu_open(0, 4096, C.byref(h)) == N.OK
+            assert lib.fcgpu_span_mode(h, N.SPAN_AUTO) == N.OK
+            others.append(h)
+        b = synth.c4(30_000, seed=540)
+        synth.inject_errors(b, 0.02, seed=541)
+        r = K.run_element(CONF, b, burst=32, nsinks=17)
+        e = expected(b, _cfg_for_conf(), oracle)
+        assert np.array_equal(r["port"], e["port"].astype(np.uint32))
+        ok = e["reason"] == N.R_OK
+        assert np.array_equal(r["agg"][ok], e["hash"][ok])
+        assert np.array_equal(r["dst"][ok], e["anno"]["dst_ip"][ok])
+        for p in range(17):
+            idx = np.nonzero(r["port"] == p)[0]
+            assert (np.diff(r["seq"][idx].astype(np.int64)) > 0).all()
+        assert int(r["handlers"]["count"]) == int(ok.sum())
+    finally:
+        for h in others:
+            lib.fcgpu_close(h)
