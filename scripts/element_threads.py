@@ -10,12 +10,12 @@ import torch  # noqa: E402,F401
 from fastclick_amd import synth, click as K  # noqa: E402
 
 t = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-batch = int(sys.argv[2]) if len(sys.argv) > 2 else 16384
+batch = int(sys.argv[2]) if len(sys.argv) > 2 else 0      # 0: the element's default (BATCH auto)
 zc = {"1": "true", "true": "true", "0": "false", "false": "false"}.get(sys.argv[3].lower(), "auto") \
     if len(sys.argv) > 3 else "auto"
 slots = int(sys.argv[4]) if len(sys.argv) > 4 else 2
 b = synth.c2(1 << 16)
-conf = f"GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BATCH {batch}, ZEROCOPY {zc}, SLOTS {slots})"
+conf = f"GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BATCH {batch or 'auto'}, ZEROCOPY {zc}, SLOTS {slots})"
 mpps = K.bench_element(conf, b, burst=32, reps=40, threads=t) / 1e6
-print(json.dumps({"threads": t, "batch": batch, "zerocopy": zc, "slots": slots, "mpps": round(mpps, 1),
+print(json.dumps({"threads": t, "batch": batch or "auto", "zerocopy": zc, "slots": slots, "mpps": round(mpps, 1),
                   "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default")}), flush=True)
