@@ -369,3 +369,61 @@ def test_gpu_auto_shared_queue_threads(oracle):
         th.join(timeout=60)
     assert not any(th.is_alive() for th in ths), "a thread did not finish"
     assert not errors, errors
+
+
+@pytest.mark.gpu
+def test_gpu_auto_shared_queue_programs_and_flows(oracle):
+    """The shared queue with configurations that carry per-context device state:
+    decision programs (two contexts compiled to code, two interpreted -- each
+    launch only fuses contexts with one configuration) and a context with a
+    flow table among them (ordered: its batches keep their own launches).
+    Verdicts and output ports as the oracle says for every batch."""
+    from tests.test_program import random_program
+    lib = N.load()
+    rng = np.random.default_rng(641)
+    b = synth.c4(6000 + 13, seed=642)
+    synth.inject_errors(b, 0.02, seed=643)
+    nout = 7
+    prog = (N.PROG_IPFILTER, random_program(rng, b, N.PROG_IPFILTER, nout, 60), -1)
+    pcfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_PROGRAM, nports=nout)
+    pexp = oracle.process_batch(pcfg, b, program=prog)
+    fcfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=4)
+    ctxs, blks = [], []
+    try:
+        for k in range(4):
+            c = N.Context(0, 8192, pcfg)
+            c.set_program(*prog)
+            c.program_jit(k < 2)
+            assert lib.fcgpu_span_mode(c.h, N.SPAN_AUTO) == N.OK
+            ctxs.append(c)
+        fc = N.Context(0, 8192, fcfg)
+        assert lib.fcgpu_flow_enable(fc.h, 1 << 15) == N.OK
+        assert lib.fcgpu_span_mode(fc.h, N.SPAN_AUTO) == N.OK
+        ctxs.append(fc)
+        for c in ctxs:
+            blks.append([Block(lib, c.h, b, 8192), Block(lib, c.h, b, 8192)])
+        for s in range(2):
+            for c, bl in zip(ctxs, blks):
+                bl[s].res[:] = 0xEE
+                rc = lib.fcgpu_span_submit_block(c.h, s, bl[s].pin, bl[s].in_bytes, 0, bl[s].frames_off, bl[s].n,
+                                                 bl[s].out, OUTS, N.PART_TILE)
+                assert rc == N.OK, lib.fcgpu_last_error(c.h)
+        for s in range(2):
+            for c in ctxs:
+                assert lib.fcgpu_span_wait(c.h, s) == N.OK, lib.fcgpu_last_error(c.h)
+        for k, (c, bl) in enumerate(zip(ctxs, blks)):
+            for s in range(2):
+                L, n = bl[s].L, bl[s].n
+                v = bl[s].res[L.verdict:L.verdict + 2 * n].view(np.uint16)
+                if k < 4:
+                    assert np.array_equal(v & 0xff, pexp["reason"].astype(np.uint16)), (k, s)
+                    assert np.array_equal(v >> 8, pexp["port"].astype(np.uint16)), (k, s)
+                else:
+                    fexp = oracle.process_batch(fcfg, b)
+                    assert np.array_equal(v & 0xff, fexp["reason"].astype(np.uint16)), (k, s)
+    finally:
+        for bl in blks:
+            for x in bl:
+                x.free()
+        for c in ctxs:
+            c.close()
