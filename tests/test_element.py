@@ -444,3 +444,16 @@ def test_element_default_with_many_contexts(oracle):
     finally:
         for h in others:
             lib.fcgpu_close(h)
+
+
+def test_config_span_keywords():
+    """ZEROCOPY true|false|auto, BATCH <n>|auto, SLOTS 2|3 (host-side parsing;
+    the GPU tests above run each mode)."""
+    from fastclick_amd import click as K
+    for ok in ("ZEROCOPY auto", "ZEROCOPY true", "ZEROCOPY false", "BATCH auto", "BATCH 0", "BATCH 4096",
+               "SLOTS 2", "SLOTS 3", "ZEROCOPY AUTO, BATCH AUTO, SLOTS 3"):
+        K.check_config(f"GPUIPCheckClassify(OFFSET 14, {ok})")
+    for bad, msg in (("ZEROCOPY maybe", "ZEROCOPY"), ("SLOTS 1", "SLOTS"), ("SLOTS 4", "SLOTS"),
+                     ("BATCH -1", "BATCH"), ("BATCH many", "BATCH")):
+        with pytest.raises(K.ConfigError, match=msg):
+            K.check_config(f"GPUIPCheckClassify(OFFSET 14, {bad})")
