@@ -266,7 +266,25 @@ def cpu_baseline(seconds: float, flows: int = 1, program: str | None = None):
                 sample=main["sample"], mpps_1core=round(main.get("mpps_1core", 0.0), 3),
                 c1_value=round(c1["mpps"], 3), c1_mpps_1core=round(c1.get("mpps_1core", 0.0), 3),
                 c1_sample=c1["sample"], nproc=info["nproc"], affinity=info["affinity"],
-                cgroup_quota=info["cgroup_quota"], cores_basis=info["threads_basis"], cpu_model=info["model"])
+                cgroup_quota=info["cgroup_quota"], cores_basis=info["threads_basis"], cpu_model=info["model"],
+                calibration=CPU_CALIBRATION)
+
+
+# The port against the reference binary (within +-20 % per stage,
+# or the ratio stated). Measured once in the survey container, where the
+# reference was built (it cannot run on the GPU box): 1 thread, the same trace.
+CPU_CALIBRATION = {
+    "source": "DESIGN.md section 5.5 (survey container, reference click binary vs oracle/cpu_baseline.cc, "
+              "1 thread, same trace)",
+    "ns_per_pkt": {"CheckIPHeader(CHECKSUM true)": {"port": 10.5, "reference": 12.7},
+                   "AggregateHash": {"port": 3.8, "reference": 3.1}},
+    "harness_floor_mpps": {"port": 121.0, "reference": 22.5},
+    "end_to_end_port_over_reference": 2.0,
+    "note": "the port's per-element costs are within -17 %/+23 % of the reference's, but its replay "
+            "harness is ~5x lighter than Click's FromDump/ReplayUnqueue -> Discard, so the port's "
+            "end-to-end Mpps is ~2x what the reference itself would reach on these cores: "
+            "value is an upper bound for the reference, not the reference",
+}
 
 
 # ---- launching the local ranks ---------------------------------------------
@@ -615,6 +633,7 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
         # after the timed region: max time over ranks, counters summed over
         # ranks (RCCL all-reduce of the device vector), per-output offsets
         t_red = time.perf_counter()
+        collective = world > 1 and dist.is_available() and dist.is_initialized()
         ctr = proc.counters()
         glob = reduce_counters(ctr if backend == "nccl" else ctr.cpu())
         if backend == "nccl":
@@ -744,10 +763,13 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                if getattr(proc, "rotation_bytes", None) else {}),
             "nports": args.nports,
             **({"flow_maintain_ms": round(maintain_ms, 4)} if maintain_ms is not None else {}),
-            "parallelism": (f"batch-sharded x{world}" if args.shard == "weak" else
-                            f"one batch split x{world} (dist.shard_range)")
-                           + f", counters all-reduced after the timed region "
-                             f"({'RCCL' if backend == 'nccl' else 'gloo'}, {red_ms:.3f} ms)",
+            "parallelism": ((f"batch-sharded x{world}" if args.shard == "weak" else
+                             f"one batch split x{world} (dist.shard_range)")
+                            + f", counters all-reduced after the timed region "
+                              f"({'RCCL' if backend == 'nccl' else 'gloo'}, {red_ms:.3f} ms)"
+                            if collective else
+                            f"one GPU: no collective (world 1); counter replicas summed on the device "
+                            f"after the timed region ({red_ms:.3f} ms)"),
         },
         "roofline": roof,
         "cpu_baseline": cpu,

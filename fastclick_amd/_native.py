@@ -15,7 +15,7 @@ LIBFCGPU = os.environ.get("FCGPU_LIB") or os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 17
+ABI_VERSION = 18
 SPAN_SLOTS = 3
 SPAN_COPY = 0
 SPAN_ZEROCOPY = 1
@@ -46,6 +46,8 @@ CTR_SHARDS = 64
 PART_GLOBAL, PART_TILE = 0, 1
 OUT_VERDICT, OUT_HASH, OUT_ANNO, OUT_PERM, OUT_PORT_START, OUT_TILE_COUNT, OUT_TILE_PERM, OUT_FLOWID, \
     OUT_IP_RW = (1 << k for k in range(9))
+SUBMIT_COPY = 1 << 31
+FAULT_SUBMIT, FAULT_WAIT, FAULT_LAUNCH = 0, 1, 2
 OUT_ABSENT = (1 << 64) - 1
 TILE = 256
 
@@ -197,6 +199,8 @@ FCGPU_SYMBOLS = {
     "fcgpu_span_poll": (C.c_int, [C.c_void_p, C.c_uint32]),
     "fcgpu_span_mode": (C.c_int, [C.c_void_p, C.c_uint32]),
     "fcgpu_span_zerocopy_active": (C.c_int, [C.c_void_p]),
+    "fcgpu_inject_fault": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32]),
+    "fcgpu_launch_guard_selftest": (C.c_int, []),
     "fcgpu_block_layout_for": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]),
     "fcgpu_span_submit_block": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t,
                                           C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32]),

@@ -102,9 +102,12 @@ TIMER_FLUSH = 1           # fcclick_run_ex flag: end with the element's timer, n
 
 
 def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1, timer_flush: bool = False,
-                burst_ns=None):
+                burst_ns=None, allow_error: bool = False):
     """Source(batch, BURST) -> conf => sinks. burst_ns: the element's clock (ns)
-    at each burst (fcclick_run_clocked), for time-driven behaviour."""
+    at each burst (fcclick_run_clocked), for time-driven behaviour.
+    allow_error: a run whose element reported a GPU runtime error (packets a
+    failed batch cost) returns its results with the message in out["error"]
+    instead of raising."""
     lib = load()
     n = batch.n
     arena = np.ascontiguousarray(batch.arena)
@@ -132,13 +135,15 @@ def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1, timer_flu
                                 TIMER_FLUSH if timer_flush else 0, C.byref(res), err, 512)
     if rc == -1:
         raise ConfigError(err.value.decode())
-    if rc != 0:
+    if rc != 0 and not allow_error:
         raise RuntimeError(f"element runtime error: {err.value.decode()}")
+    out["error"] = err.value.decode() if rc != 0 else ""
     handlers = {}
     name = None
     for line in hbuf.value.decode().splitlines():
         if "=" in line and line.split("=", 1)[0] in ("count", "drops", "drop_details", "port_counts",
-                                                                "flow_count", "flow_drops", "error"):
+                                                                "flow_count", "flow_drops", "gpu_errors",
+                                                                "gpu_retries", "error"):
             name, val = line.split("=", 1)
             handlers[name] = val
         elif name is not None:

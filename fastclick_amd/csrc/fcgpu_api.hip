@@ -33,6 +33,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <map>
@@ -182,6 +183,7 @@ struct SpanSlot {
     bool agg = false, agg_err = false;
     AggLaunch *al = nullptr;
     bool busy = false;
+    bool doomed = false;         // fcgpu_inject_fault(FCGPU_FAULT_WAIT): accepted, nothing ran, the wait fails
     hipEvent_t done = nullptr;   // shared streams: the slot's last operation (else the stream is waited)
     bool evt = false;            // the last submission recorded `done`
 };
@@ -295,6 +297,7 @@ static hipError_t memset_sync(void *p, int v, size_t bytes) {
 }
 
 static std::string g_open_err;
+static bool fault_take(uint32_t where);
 static void span_auto_count(fcgpu_ctx *c, uint32_t new_mode);
 static bool span_zerocopy(const fcgpu_ctx *c);
 int fcgpu_span_wait(fcgpu_ctx *c, uint32_t slot);
@@ -1024,8 +1027,10 @@ int fcgpu_open(int device, uint32_t max_batch, fcgpu_ctx **out) {
     return FCGPU_OK;
 }
 
+static bool agg_queued(const fcgpu_ctx *c);
 int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     if (!c || !cfg) return FCGPU_EINVAL;
+    if (agg_queued(c)) return fail(c, FCGPU_EINVAL, "fcgpu_configure: a queued span submission is not waited for");
     if (cfg->size != sizeof(fcgpu_cfg)) return fail(c, FCGPU_EINVAL, "fcgpu_cfg size mismatch (ABI)");
     if (cfg->check_mode > FCGPU_MARK_IP6) return fail(c, FCGPU_EINVAL, "bad check_mode");
     const bool ip4mode = cfg->check_mode == FCGPU_CHECK_IP4 || cfg->check_mode == FCGPU_MARK_IP4;
@@ -1709,6 +1714,11 @@ int fcgpu_span_submit(fcgpu_ctx *c, uint32_t slot, const uint8_t *h_span, size_t
     if (bytes > 0xffffffffull - kArenaPad) return fail(c, FCGPU_EINVAL, "span larger than 4 GiB");
     SpanSlot &sp = c->span[slot];
     if (sp.busy) return fail(c, FCGPU_EINVAL, "span slot busy: fcgpu_span_wait it first");
+    if (fault_take(FCGPU_FAULT_SUBMIT)) return fail(c, FCGPU_ERUNTIME, "injected fault: submission failed");
+    if (fault_take(FCGPU_FAULT_WAIT)) {
+        sp.doomed = sp.busy = true;
+        return FCGPU_OK;
+    }
     HIPCHK(c, hipSetDevice(c->device));
     if (!sp.own) {
         const size_t m = c->max_batch, tiles = (m + kTile - 1) / kTile;
@@ -1840,6 +1850,23 @@ static bool span_zerocopy(const fcgpu_ctx *c) {
     return it != g_auto_ctx.end() && it->second >= kZeroCopyAuto;
 }
 
+// ---- fault injection (fcgpu_inject_fault) ------------------------------------
+static std::atomic<uint32_t> g_fault_armed{0};     // bit k: kind k has events to skip or fail
+static std::mutex g_fault_mu;
+static uint32_t g_fault_skip[3], g_fault_count[3];
+static bool fault_take(uint32_t where) {
+    if (!(g_fault_armed.load(std::memory_order_relaxed) & (1u << where))) return false;
+    std::lock_guard<std::mutex> g(g_fault_mu);
+    bool hit = false;
+    if (g_fault_skip[where]) --g_fault_skip[where];
+    else if (g_fault_count[where]) {
+        --g_fault_count[where];
+        hit = true;
+    }
+    if (!g_fault_count[where]) g_fault_armed.fetch_and(~(1u << where), std::memory_order_relaxed);
+    return hit;
+}
+
 // ---- the shared zero-copy queue of FCGPU_SPAN_AUTO --------------------------
 // With many element contexts on one device, each zero-copy batch is a small
 // kernel (16-64 workgroups, latency-bound over PCIe) that waits behind other
@@ -1856,6 +1883,13 @@ struct AggItem {
     fcgpu_ctx *c;
     uint32_t slot;
     fcgpu_job job;            // device (mapped) addresses
+    // the launch inputs, taken on the owner's thread at submit time: the
+    // launch may happen on another context's thread, later
+    DevCfg dcfg;
+    uint32_t cm;              // k_rx check mode / checksum as launch_rx_part normalises them
+    bool ck;
+    unsigned long long *ctr;  // the counter vector in use at submit
+    hipFunction_t fn;         // the compiled program's k_rx (nullptr: the built-in kernel)
 };
 struct AggQueue {
     std::mutex mu;
@@ -1881,9 +1915,24 @@ static bool agg_eligible(const fcgpu_ctx *c, const fcgpu_out &o) {
     return c->span_mode == FCGPU_SPAN_AUTO && !c->fl.slots && out_part(&o) != kPartGlobal &&
            !(c->cfg.rewrite & FCGPU_RW_INPLACE) && !c->timing_every;
 }
+// One launch takes its configuration from its first item: the others must
+// have the same one (everything agg_launch_locked reads from it).
 static bool agg_compatible(const AggItem &a, const AggItem &b) {
-    return memcmp(&a.c->dcfg, &b.c->dcfg, sizeof(DevCfg)) == 0 && out_part(&a.job.out) == out_part(&b.job.out) &&
-           a.job.out.partition == b.job.out.partition && a.c->jit_src == b.c->jit_src;
+    return memcmp(&a.dcfg, &b.dcfg, sizeof(DevCfg)) == 0 && a.cm == b.cm && a.ck == b.ck && a.fn == b.fn &&
+           out_part(&a.job.out) == out_part(&b.job.out) && a.job.out.partition == b.job.out.partition;
+}
+// A context with a queued submission keeps the configuration, program and
+// compiled module that submission was taken with (fcgpu_configure,
+// fcgpu_set_program and fcgpu_program_jit refuse until it is waited for).
+static bool agg_queued(const fcgpu_ctx *c) {
+    for (const SpanSlot &sp : c->span)
+        if (sp.busy && sp.agg) return true;
+    return false;
+}
+static hipError_t launch_rx_fn(hipFunction_t fn, int part, const RxLaunch &L, uint32_t grid, hipStream_t s) {
+    if (!rx_launch_ok(part, L, grid)) return hipErrorInvalidValue;
+    void *args[] = {const_cast<RxLaunch *>(&L)};
+    return hipModuleLaunchKernel(fn, grid, 1, 1, kTile, 1, 1, 0, s, args, nullptr);
 }
 // Launch every pending submission (q.mu held): the first one with the next
 // ones of its configuration, up to kMaxFuse per launch, until none is left.
@@ -1894,16 +1943,12 @@ static int agg_launch_locked(AggQueue &q) {
         std::vector<size_t> grp{0};
         for (size_t m = 1; m < q.pending.size() && grp.size() < kMaxFuse; ++m)
             if (agg_compatible(q.pending[0], q.pending[m])) grp.push_back(m);
-        fcgpu_ctx *c0 = q.pending[0].c;
-        const fcgpu_out &o0 = q.pending[0].job.out;
-        const int part = out_part(&o0);
+        const AggItem &i0 = q.pending[0];
+        const int part = out_part(&i0.job.out);
         RxLaunch L;
         RxArgs &a = L.A;
-        a = RxArgs{};
-        a.tilecnt = c0->d_tilecnt;
-        a.cfg = c0->dcfg;
-        a.fl = c0->fl;
-        a.fl.flowid = nullptr;
+        a = RxArgs{};    // no whole-batch partition or flow table here (agg_eligible)
+        a.cfg = i0.dcfg;
         L.njobs = (uint32_t)grp.size();
         L.flow_stride = L.flow_words = 0;
         uint32_t tiles = 0;
@@ -1922,7 +1967,7 @@ static int agg_launch_locked(AggQueue &q) {
             J.tile_perm = j.out.partition == FCGPU_PART_TILE ? j.out.tile_perm : nullptr;
             J.flowid = nullptr;
             J.ip_rw = j.out.ip_rw;
-            J.ctr = it.c->d_ctr;
+            J.ctr = it.ctr;
             J.n = j.n;
             J.tile0 = tiles;
             tiles += (j.n + kTile - 1) / kTile;
@@ -1955,10 +2000,14 @@ static int agg_launch_locked(AggQueue &q) {
             al = new AggLaunch();
             if (e == hipSuccess) e = hipEventCreateWithFlags(&al->ev, hipEventDisableTiming);
         }
+        if (e == hipSuccess && fault_take(FCGPU_FAULT_LAUNCH)) e = hipErrorLaunchFailure;
         if (e == hipSuccess) {
-            e = launch_rx_any(part, c0->cfg.check_mode, c0->cfg.checksum != 0, L, tiles, q.st[si], nullptr,
-                              nullptr, c0->jit_src.empty() ? nullptr : c0);
-            if (e == hipSuccess) e = hipGetLastError();
+            if (i0.fn) {
+                e = launch_rx_fn(i0.fn, part, L, tiles, q.st[si]);
+            } else {
+                e = launch_rx_any(part, i0.cm, i0.ck, L, tiles, q.st[si], nullptr, nullptr, nullptr);
+                if (e == hipSuccess) e = hipGetLastError();
+            }
         }
         if (e == hipSuccess) e = hipEventRecord(al->ev, q.st[si]);
         al->refs = (uint32_t)grp.size();
@@ -2013,17 +2062,34 @@ static void agg_release(int device) {
         }
 }
 
-// Queue one zero-copy block submission (device addresses in j).
+// Queue one zero-copy block submission (device addresses in j). Once queued
+// the submission is the owner's to wait for: a failed launch (of its group or
+// another) is reported by that wait (agg_err), never by this call.
 static int agg_submit(fcgpu_ctx *c, uint32_t slot, const fcgpu_job &j) {
+    AggItem it{};
+    it.c = c;
+    it.slot = slot;
+    it.job = j;
+    it.dcfg = c->dcfg;
+    it.cm = c->cfg.check_mode;
+    it.ck = c->cfg.checksum != 0;
+    if (it.cm == FCGPU_MARK_IP4 || it.cm == FCGPU_MARK_IP6) it.ck = false;
+    it.ctr = c->d_ctr;
+    it.fn = nullptr;
+    if (c->cfg.classify == FCGPU_CLS_PROGRAM && !c->jit_src.empty()) {
+        const bool ip4 = it.cm == FCGPU_CHECK_IP4 || it.cm == FCGPU_MARK_IP4;
+        it.fn = jit_function(c, jit_key((int)it.cm, it.ck, out_part(&j.out), ip4 && c->cfg.l4_mode != FCGPU_L4_NONE,
+                                        false));
+    }
     AggQueue &q = agg_queue(c->device);
     SpanSlot &sp = c->span[slot];
     std::lock_guard<std::mutex> g(q.mu);
-    q.pending.push_back(AggItem{c, slot, j});
+    q.pending.push_back(it);
     sp.agg = true;
     sp.agg_err = false;
     sp.al = nullptr;
     sp.busy = true;
-    if (q.pending.size() >= kAggLaunch) return agg_launch_locked(q) == FCGPU_OK ? FCGPU_OK : FCGPU_ERUNTIME;
+    if (q.pending.size() >= kAggLaunch) (void)agg_launch_locked(q);
     return FCGPU_OK;
 }
 // Wait for (block = true) or poll a queued submission: launched first if
@@ -2082,6 +2148,10 @@ int fcgpu_span_poll(fcgpu_ctx *c, uint32_t slot) {
     if (!c || slot >= FCGPU_SPAN_SLOTS) return FCGPU_EINVAL;
     SpanSlot &sp = c->span[slot];
     if (!sp.busy) return 1;
+    if (sp.doomed) {
+        sp.doomed = sp.busy = false;
+        return fail(c, FCGPU_ERUNTIME, "injected fault: batch failed on the device");
+    }
     if (sp.agg) return agg_finish(c, slot, false);
     const hipError_t e = sp.evt ? hipEventQuery(sp.done) : hipStreamQuery(sp.s);
     if (e == hipSuccess) return 1;
@@ -2123,19 +2193,22 @@ static std::mutex g_span_mu;
 static std::map<int, std::vector<hipStream_t>> g_span_shared;
 static uint32_t g_span_ctx_seq = 0;
 static int span_stream_mode(uint32_t &nshared) {
-    static int mode = -1;
-    static uint32_t ns = 0;
-    if (mode < 0) {
+    struct Mode {
+        int mode = 0;
+        uint32_t ns = 0;
+    };
+    static const Mode m = [] {      // initialised once, thread-safe
+        Mode r;
         const char *e = getenv("FCGPU_SPAN_STREAMS");
-        mode = 0;
-        if (e && !strcmp(e, "ctx")) mode = 1;
+        if (e && !strcmp(e, "ctx")) r.mode = 1;
         else if (e && !strncmp(e, "shared:", 7)) {
             const long v = atol(e + 7);
-            if (v >= 1 && v <= 64) { mode = 2; ns = (uint32_t)v; }
+            if (v >= 1 && v <= 64) { r.mode = 2; r.ns = (uint32_t)v; }
         }
-    }
-    nshared = ns;
-    return mode;
+        return r;
+    }();
+    nshared = m.ns;
+    return m.mode;
 }
 static hipError_t span_stream(fcgpu_ctx *c, uint32_t slot, hipStream_t *out) {
     uint32_t ns = 0;
@@ -2166,18 +2239,25 @@ static hipError_t span_stream(fcgpu_ctx *c, uint32_t slot, hipStream_t *out) {
 int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_t in_bytes, size_t desc_off,
                             size_t frames_off, uint32_t n, void *h_out, uint32_t outputs, uint32_t partition) {
     if (!c || slot >= FCGPU_SPAN_SLOTS || (n && (!h_in || !h_out))) return FCGPU_EINVAL;
+    const bool force_copy = (outputs & FCGPU_SUBMIT_COPY) != 0;
+    outputs &= ~FCGPU_SUBMIT_COPY;
     if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "batch larger than max_batch");
     if (desc_off + 8ull * n > in_bytes || frames_off > in_bytes || (desc_off & 7))
         return fail(c, FCGPU_EINVAL, "block: descriptors (8-B aligned) or frames outside in_bytes");
     if (in_bytes - frames_off > 0xffffffffull - kArenaPad) return fail(c, FCGPU_EINVAL, "frames larger than 4 GiB");
     SpanSlot &sp = c->span[slot];
     if (sp.busy) return fail(c, FCGPU_EINVAL, "span slot busy: fcgpu_span_wait it first");
+    if (fault_take(FCGPU_FAULT_SUBMIT)) return fail(c, FCGPU_ERUNTIME, "injected fault: submission failed");
+    if (fault_take(FCGPU_FAULT_WAIT)) {
+        sp.doomed = sp.busy = true;
+        return FCGPU_OK;
+    }
     fcgpu_block_layout L;
     if (fcgpu_block_layout_for(c, n, outputs, partition, &L) != FCGPU_OK) return fail(c, FCGPU_EINVAL, "bad block layout");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t ss = nullptr;
     HIPCHK(c, span_stream(c, slot, &ss));
-    const bool zc = span_zerocopy(c);
+    const bool zc = !force_copy && span_zerocopy(c);
     if (zc && n) {
         // the kernels read h_in and write h_out where they lie (page-locked
         // memory mapped into the device's address space): no copy engine
@@ -2268,6 +2348,10 @@ int fcgpu_span_wait(fcgpu_ctx *c, uint32_t slot) {
     if (!c || slot >= FCGPU_SPAN_SLOTS) return FCGPU_EINVAL;
     SpanSlot &sp = c->span[slot];
     if (!sp.busy) return FCGPU_OK;
+    if (sp.doomed) {
+        sp.doomed = sp.busy = false;
+        return fail(c, FCGPU_ERUNTIME, "injected fault: batch failed on the device");
+    }
     if (sp.agg) {
         const int r = agg_finish(c, slot, true);
         return r < 0 ? r : FCGPU_OK;
@@ -2276,6 +2360,90 @@ int fcgpu_span_wait(fcgpu_ctx *c, uint32_t slot) {
     sp.busy = false;
     if (sp.evt) HIPCHK(c, hipEventSynchronize(sp.done));
     else HIPCHK(c, hipStreamSynchronize(sp.s));
+    return FCGPU_OK;
+}
+
+int fcgpu_launch_guard_selftest(void) {
+    // host-only: rx_launch_ok decides before any HIP call
+    static uint8_t arena[64];
+    static uint2 desc[1];
+    static uint16_t tc[FCGPU_MAX_PORTS + 1];
+    static uint32_t tcnt[FCGPU_MAX_PORTS + 1];
+    static unsigned long long ctr[1];
+    auto one = [](uint32_t n) {
+        RxLaunch L;
+        L.A = RxArgs{};
+        L.A.arena = arena;
+        L.A.desc = desc;
+        L.A.n = n;
+        L.A.ctr = ctr;
+        L.A.tile_count = tc;
+        L.A.tilecnt = tcnt;
+        L.njobs = 1;
+        L.job_tiles = 0;
+        return L;
+    };
+    auto fused = [](uint32_t njobs, uint32_t n) {
+        RxLaunch L;
+        L.A = RxArgs{};
+        L.njobs = njobs;
+        L.job_tiles = 0;
+        for (uint32_t k = 0; k < njobs && k < kMaxFuse; ++k) {
+            RxJob &J = L.job[k];
+            J = RxJob{};
+            J.arena = arena;
+            J.desc = desc;
+            J.n = n;
+            J.ctr = ctr;
+            J.tile_count = tc;
+            J.tilecnt = tcnt;
+            J.tile0 = k * ((n + kTile - 1) / kTile);
+        }
+        return L;
+    };
+    const uint32_t n = 1000, t = (n + kTile - 1) / kTile;
+    // well-formed launches must pass, or the checks below prove nothing
+    if (!rx_launch_ok(kPartTile, one(n), t) || !rx_launch_ok(kPartGlobal, one(n), t) ||
+        !rx_launch_ok(kPartTile, fused(3, n), 3 * t))
+        return -1;
+    int accepted = 0;
+    RxLaunch L = one(n);
+    L.A.tile_count = nullptr;                           // the r03_s17 fault: TILE stores through tile_count
+    accepted += rx_launch_ok(kPartTile, L, t);
+    L = one(n);
+    L.A.tilecnt = nullptr;                              // GLOBAL stores per-tile counts
+    accepted += rx_launch_ok(kPartGlobal, L, t);
+    L = one(n);
+    L.A.arena = nullptr;
+    accepted += rx_launch_ok(kPartNone, L, t);
+    L = one(n);
+    L.A.desc = nullptr;
+    accepted += rx_launch_ok(kPartNone, L, t);
+    L = one(n);
+    L.A.ctr = nullptr;
+    accepted += rx_launch_ok(kPartNone, L, t);
+    accepted += rx_launch_ok(kPartNone, one(n), t + 1);       // more workgroups than tiles
+    L = fused(3, n);
+    L.job[1].tile_count = nullptr;
+    accepted += rx_launch_ok(kPartTile, L, 3 * t);
+    L = fused(3, n);
+    L.job[2].tile0 += 1;                                // tiles not end to end
+    accepted += rx_launch_ok(kPartTile, L, 3 * t);
+    L = fused(3, n);
+    accepted += rx_launch_ok(kPartTile, L, 3 * t + 1);
+    L = fused(kMaxFuse, n);
+    L.njobs = kMaxFuse + 1;
+    accepted += rx_launch_ok(kPartTile, L, kMaxFuse * t);
+    return accepted;
+}
+
+int fcgpu_inject_fault(uint32_t where, uint32_t skip, uint32_t count) {
+    if (where > FCGPU_FAULT_LAUNCH) return FCGPU_EINVAL;
+    std::lock_guard<std::mutex> g(g_fault_mu);
+    g_fault_skip[where] = count ? skip : 0;
+    g_fault_count[where] = count;
+    if (count) g_fault_armed.fetch_or(1u << where, std::memory_order_relaxed);
+    else g_fault_armed.fetch_and(~(1u << where), std::memory_order_relaxed);
     return FCGPU_OK;
 }
 
@@ -2421,6 +2589,7 @@ int fcgpu_set_program(fcgpu_ctx *c, uint32_t kind, const fcgpu_step *steps, uint
     if (kind > FCGPU_PROG_CLASSIFIER) return fail(c, FCGPU_EINVAL, "bad program kind");
     if (nsteps > FCGPU_MAX_STEPS || (nsteps && !steps)) return fail(c, FCGPU_EINVAL, "bad program size");
     if (nsteps == 0 && output_everything < 0) return fail(c, FCGPU_EINVAL, "empty program without output");
+    if (agg_queued(c)) return fail(c, FCGPU_EINVAL, "fcgpu_set_program: a queued span submission is not waited for");
     std::vector<uint4> dev(nsteps ? nsteps : 1);
     auto jump = [](int32_t j) -> int32_t {       // [X] (drop) and out-of-range -> unmatched
         if (j <= -32767 || j > 32767) return -kProgUnmatched;
@@ -2463,6 +2632,7 @@ int fcgpu_set_program(fcgpu_ctx *c, uint32_t kind, const fcgpu_step *steps, uint
 
 int fcgpu_program_jit(fcgpu_ctx *c, int enable) {
     if (!c) return FCGPU_EINVAL;
+    if (agg_queued(c)) return fail(c, FCGPU_EINVAL, "fcgpu_program_jit: a queued span submission is not waited for");
     c->jit_on = enable != 0;
     return jit_install(c);
 }

@@ -252,7 +252,7 @@ static int run_graph(const char *conf, const uint8_t *arena, const uint32_t *des
         if (res->handlers && res->handlers_cap) {
             std::string h;
             for (const char *name : {"count", "drops", "drop_details", "port_counts", "flow_count", "flow_drops",
-                                     "error"})
+                                     "gpu_errors", "gpu_retries", "error"})
                 h += std::string(name) + "=" + el->read_handler(name) + "\n";
             snprintf(res->handlers, res->handlers_cap, "%s", h.c_str());
         }

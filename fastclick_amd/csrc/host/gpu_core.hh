@@ -27,8 +27,12 @@
 // batch leaves when BATCH packets are staged or TIMER microseconds after its
 // first packet, whichever comes first (TIMER -1: only on BATCH or flush()).
 // Every packet the element receives leaves exactly once: pushed on one
-// output, or killed (GPU/runtime errors kill the batch and are reported
-// through the `error` handler -- there is no CPU fallback).
+// output, or killed. A batch the GPU fails (a submission or its completion
+// returns an error, SURVEY 8(b) "Errors") is re-submitted once through copies
+// (FCGPU_SUBMIT_COPY: no zero-copy, no shared queue); if that fails too its
+// packets leave unprocessed on ERROR_OUTPUT, or are killed (the default), and
+// are counted (gpu_errors, drop_details) -- never dropped silently. There is
+// no CPU fallback.
 //
 // Keyword arguments mirror the replaced elements:
 //   OFFSET, CHECKSUM (default FALSE: checkipheader.cc:110), BADSRC, GOODDST,
@@ -85,8 +89,12 @@
 //   the GPU (their copies would queue on one copy engine), else copies,
 //   PARTITION TILE (default: each 256-packet tile classified as one batch,
 //   one fused launch) | GLOBAL (the whole device batch as one, three launches)
+//   ERROR_OUTPUT p (default -1: kill)          -- where the packets of a batch the
+//     GPU failed twice leave, unprocessed and in input order
 // Handlers: count, drops, drop_details (DETAILS true), port_counts,
-// flow_count, flow_drops, error.
+// flow_count, flow_drops, gpu_errors (packets of batches the GPU failed twice),
+// gpu_retries (batches re-submitted through copies), error (the last failure
+// that cost packets).
 #pragma once
 #include <inttypes.h>
 #include <arpa/inet.h>
@@ -305,6 +313,9 @@ class RxCore {
             } else if (k == "FLOWID_ANNO") {
                 if (!parse_int(v, n) || n < 0 || n > P::kAnnoSize - 4) return err(errh, "bad FLOWID_ANNO");
                 _flow_anno = (int)n;
+            } else if (k == "ERROR_OUTPUT") {
+                if (!parse_int(v, n) || n < -1 || n > FCGPU_MAX_PORTS + 1) return err(errh, "bad ERROR_OUTPUT");
+                _error_output = (int)n;
             } else if (k == "PROCESS_EH") {
                 if (!parse_bool(v, b)) return err(errh, "PROCESS_EH expects true/false");
                 _cfg.process_eh = b;
@@ -466,12 +477,29 @@ class RxCore {
     }
 
     // ---- handlers ------------------------------------------------------------
-    // This core's counters (fcgpu_read_counters), flow IDs issued, flows
-    // dropped and last error. Safe from any thread (a handler reads every
-    // thread's core, ELEMENT_MT_SAFE): the context and the error string are
-    // only touched under _mu, which the owning data thread holds around its
-    // own context calls (submit, completion wait, maintainer, failure).
-    void counters(uint64_t (&c)[FCGPU_NCOUNTERS], uint64_t &flows, uint64_t &flow_drops, std::string *error = nullptr) {
+    // What the host side counts besides the device counters (summed over
+    // threads on read like them).
+    struct HostStats {
+        uint64_t flows = 0;        // flow IDs issued (flow table)
+        uint64_t flow_drops = 0;   // new flows killed, table full
+        uint64_t gpu_errors = 0;   // packets of batches the GPU failed twice (killed or on ERROR_OUTPUT)
+        uint64_t gpu_killed = 0;   // ... of which killed (no ERROR_OUTPUT)
+        uint64_t gpu_retries = 0;  // batches re-submitted through copies after a failure
+        HostStats &operator+=(const HostStats &o) {
+            flows += o.flows;
+            flow_drops += o.flow_drops;
+            gpu_errors += o.gpu_errors;
+            gpu_killed += o.gpu_killed;
+            gpu_retries += o.gpu_retries;
+            return *this;
+        }
+    };
+    // This core's counters (fcgpu_read_counters), host-side counts and last
+    // error. Safe from any thread (a handler reads every thread's core,
+    // ELEMENT_MT_SAFE): the context and the error string are only touched
+    // under _mu, which the owning data thread holds around its own context
+    // calls (submit, completion wait, maintainer, failure).
+    void counters(uint64_t (&c)[FCGPU_NCOUNTERS], HostStats &hs, std::string *error = nullptr) {
         memset(c, 0, sizeof c);
         uint32_t f = 0;
         {
@@ -480,17 +508,23 @@ class RxCore {
             if (_ctx && _flow_cap) fcgpu_flow_count(_ctx, &f);
             if (error) *error = _error;
         }
-        flows = f;
-        flow_drops = _flow_drops.load(std::memory_order_relaxed);
+        hs.flows = f;
+        hs.flow_drops = _flow_drops.load(std::memory_order_relaxed);
+        hs.gpu_errors = _gpu_errors.load(std::memory_order_relaxed);
+        hs.gpu_killed = _gpu_killed.load(std::memory_order_relaxed);
+        hs.gpu_retries = _gpu_retries.load(std::memory_order_relaxed);
     }
     bool details() const { return _details; }
 
     // Handler text from (summed) counters, in the replaced elements' formats.
+    // Packets a GPU failure killed count as drops; drop_details gives them a
+    // line of their own once there are any (the six CheckIPHeader lines
+    // otherwise, exactly).
     static std::string format_handler(const std::string &h, const uint64_t (&c)[FCGPU_NCOUNTERS], uint32_t nports,
-                                      bool details, uint64_t flows, uint64_t flow_drops, const std::string &error) {
+                                      bool details, const HostStats &hs, const std::string &error) {
         std::ostringstream s;
         if (h == "count") s << c[FCGPU_CTR_COUNT];
-        else if (h == "drops") s << c[FCGPU_CTR_DROPS];
+        else if (h == "drops") s << c[FCGPU_CTR_DROPS] + hs.gpu_killed;
         else if (h == "drop_details" && details) {
             char line[96];
             for (int i = 0; i < 6; ++i) {     // checkipheader.cc:247-256 format
@@ -498,19 +532,25 @@ class RxCore {
                          kReasonTexts[i]);
                 s << line;
             }
+            if (hs.gpu_errors) {
+                snprintf(line, sizeof line, "%15" PRIu64 " packets due to: %24s\n", hs.gpu_errors, "GPU failure");
+                s << line;
+            }
         } else if (h == "port_counts") {
             for (uint32_t p = 0; p <= nports; ++p) s << (p ? " " : "") << c[FCGPU_CTR_PORT + p];
-        } else if (h == "flow_count") s << flows;
-        else if (h == "flow_drops") s << flow_drops;
+        } else if (h == "flow_count") s << hs.flows;
+        else if (h == "flow_drops") s << hs.flow_drops;
+        else if (h == "gpu_errors") s << hs.gpu_errors;
+        else if (h == "gpu_retries") s << hs.gpu_retries;
         else if (h == "error") s << error;
         return s.str();
     }
     std::string read_handler(const std::string &h) {
         uint64_t c[FCGPU_NCOUNTERS];
-        uint64_t flows, drops;
+        HostStats hs;
         std::string error;
-        counters(c, flows, drops, &error);
-        return format_handler(h, c, _cfg.nports, _details, flows, drops, error);
+        counters(c, hs, &error);
+        return format_handler(h, c, _cfg.nports, _details, hs, error);
     }
     std::string error() const {
         std::lock_guard<std::mutex> g(_mu);
@@ -626,21 +666,34 @@ class RxCore {
     void submit(Emit &emit) {
         const uint32_t k = _cur;
         Slot &s = _slot[k];
+        bool failed = false;
         {
             std::lock_guard<std::mutex> g(_mu);
             if (_flow_cap && _flow_timeout) flow_clock();
-            const int rc = fcgpu_span_submit_block(_ctx, k, s.in, s.frames_off + s.used, 0, s.frames_off, s.n,
-                                                   s.res, _outputs, _partition);
+            int rc = fcgpu_span_submit_block(_ctx, k, s.in, s.frames_off + s.used, 0, s.frames_off, s.n, s.res,
+                                             _outputs, _partition);
             // BATCH auto: the next batches' size for the path they now take
             _eff_batch = _batch_auto && fcgpu_span_zerocopy_active(_ctx) ? kBatchZeroCopy : _batch;
-            if (rc != FCGPU_OK) {
-                fail_slot(s, fcgpu_last_error(_ctx));
-            } else {
-                s.inflight = true;
-            }
+            if (rc != FCGPU_OK) rc = resubmit(k);
+            if (rc == FCGPU_OK) s.inflight = true;
+            else failed = true;
         }
+        if (failed) fail_slot(s, emit);
         _cur = (_cur + 1) % _nslots;
         if (_slot[_cur].inflight) complete(_cur, emit);
+    }
+
+    // Slot k's batch failed (submission or completion): once more, through
+    // copies (FCGPU_SUBMIT_COPY). The staged block is intact -- nothing the
+    // failed attempt ran writes it. Called with _mu held; returns the
+    // re-submission's code.
+    int resubmit(uint32_t k) {
+        Slot &s = _slot[k];
+        _gpu_retries.fetch_add(1, std::memory_order_relaxed);
+        P::chatter(name + ": GPU batch failed (" + std::string(fcgpu_last_error(_ctx)) + "), re-submitting it");
+        _fail_msg = fcgpu_last_error(_ctx);
+        return fcgpu_span_submit_block(_ctx, k, s.in, s.frames_off + s.used, 0, s.frames_off, s.n, s.res,
+                                       _outputs | FCGPU_SUBMIT_COPY, _partition);
     }
 
     // IMP timeouts: the maintainer runs due by now (every RECYCLE_INTERVAL from
@@ -660,15 +713,41 @@ class RxCore {
         fcgpu_flow_set_time(_ctx, now);
     }
 
-    // Called with _mu held.
-    void fail_slot(Slot &s, const char *msg) {
-        // no CPU fallback: report, drop the batch, keep running
-        _error = msg ? msg : "GPU processing failed";
-        P::chatter(name + ": GPU processing failed: " + _error);
-        for (uint32_t i = 0; i < s.n; ++i) P::kill(s.pkts[i]);
+    // The batch failed twice (no CPU fallback): its packets leave
+    // unprocessed, in input order, on ERROR_OUTPUT, or are killed; either way
+    // they are counted (gpu_errors; killed ones also in drops).
+    template <class Emit>
+    void fail_slot(Slot &s, Emit &emit) {
+        const uint32_t n = s.n;
+        std::string msg;
+        {
+            std::lock_guard<std::mutex> g(_mu);
+            const char *m = _ctx ? fcgpu_last_error(_ctx) : nullptr;
+            _error = m && *m ? m : (_fail_msg.empty() ? "GPU processing failed" : _fail_msg);
+            msg = _error;
+        }
+        _gpu_errors.fetch_add(n, std::memory_order_relaxed);
         s.n = 0;
         s.used = 0;
         s.inflight = false;
+        if (_error_output >= 0) {
+            P::chatter(name + ": GPU processing failed twice: " + msg + "; " + std::to_string(n) +
+                       " packets to output " + std::to_string(_error_output));
+            for (uint32_t a = 0; a < n;) {
+                const uint32_t k = n - a < kMaxBatch ? n - a : kMaxBatch;
+                Packet *head = s.pkts[a], *prev = head;
+                for (uint32_t j = 1; j < k; ++j) {
+                    P::set_next(prev, s.pkts[a + j]);
+                    prev = s.pkts[a + j];
+                }
+                emit(_error_output, P::make_batch(head, prev, k));
+                a += k;
+            }
+        } else {
+            P::chatter(name + ": GPU processing failed twice: " + msg + "; " + std::to_string(n) + " packets killed");
+            _gpu_killed.fetch_add(n, std::memory_order_relaxed);
+            for (uint32_t i = 0; i < n; ++i) P::kill(s.pkts[i]);
+        }
     }
 
     // The first drop's chatter, as the replaced checker prints it
@@ -752,15 +831,21 @@ class RxCore {
         Slot &s = _slot[k];
         const uint32_t n = s.n;
         fcgpu_block_layout L;
+        bool failed = false;
         {
             std::lock_guard<std::mutex> g(_mu);
-            const int rc = fcgpu_span_wait(_ctx, k);
+            int rc = fcgpu_span_wait(_ctx, k);
             s.inflight = false;
             if (rc != FCGPU_OK) {
-                fail_slot(s, fcgpu_last_error(_ctx));
-                return;
+                rc = resubmit(k);
+                if (rc == FCGPU_OK) rc = fcgpu_span_wait(_ctx, k);
             }
-            fcgpu_block_layout_for(_ctx, n, _outputs, _partition, &L);
+            if (rc == FCGPU_OK) fcgpu_block_layout_for(_ctx, n, _outputs, _partition, &L);
+            else failed = true;
+        }
+        if (failed) {
+            fail_slot(s, emit);
+            return;
         }
         s.holes = false;
         s.map(L);
@@ -869,6 +954,9 @@ class RxCore {
     int _flow_anno = 28;
     bool _flow_runs = true;
     std::atomic<uint64_t> _flow_drops{0};       // read by handlers on other threads
+    std::atomic<uint64_t> _gpu_errors{0}, _gpu_killed{0}, _gpu_retries{0};
+    int _error_output = -1;                      // ERROR_OUTPUT (-1: kill)
+    std::string _fail_msg;                       // the failure that caused the last re-submission (under _mu)
     int _device = 0;
     static constexpr uint32_t kBatchCopy = 16384, kBatchZeroCopy = 4096;
     uint32_t _batch = kBatchCopy;

@@ -11,7 +11,8 @@
 #include <click/bitvector.hh>
 CLICK_DECLS
 
-enum { h_count, h_drops, h_drop_details, h_port_counts, h_flow_count, h_flow_drops, h_error };
+enum { h_count, h_drops, h_drop_details, h_port_counts, h_flow_count, h_flow_drops, h_gpu_errors, h_gpu_retries,
+       h_error };
 
 GPUIPCheckClassify::GPUIPCheckClassify() : _timer_us(100)
 {
@@ -151,13 +152,13 @@ GPUIPCheckClassify::read_handler(Element *e, void *thunk)
 {
     GPUIPCheckClassify *g = static_cast<GPUIPCheckClassify *>(e);
     static const char *const names[] = {"count", "drops", "drop_details", "port_counts",
-                                        "flow_count", "flow_drops", "error"};
+                                        "flow_count", "flow_drops", "gpu_errors", "gpu_retries", "error"};
     // PER_THREAD_SUM (include/click/sync.hh:384): the per-thread cores'
     // counters are summed on read. Each core's counters and error are read
     // under that core's own lock (RxCore::counters), never racing the thread
     // that owns its GPU context.
     uint64_t sum[FCGPU_NCOUNTERS] = {0};
-    uint64_t flows = 0, drops = 0;
+    Core::HostStats hsum;
     std::string error;
     uint32_t nports = 1;
     bool details = false;
@@ -166,20 +167,19 @@ GPUIPCheckClassify::read_handler(Element *e, void *thunk)
         if (!s.core)
             continue;
         uint64_t c[FCGPU_NCOUNTERS];
-        uint64_t f, d;
+        Core::HostStats hs;
         std::string e;
-        s.core->counters(c, f, d, &e);
+        s.core->counters(c, hs, &e);
         for (int k = 0; k < FCGPU_NCOUNTERS; k++)
             sum[k] += c[k];
-        flows += f;
-        drops += d;
+        hsum += hs;
         nports = s.core->nports();
         details = s.core->details();
         if (error.empty())
             error = e;
     }
     const int h = (int)(uintptr_t)thunk;
-    std::string out = Core::format_handler(names[h], sum, nports, details, flows, drops, error);
+    std::string out = Core::format_handler(names[h], sum, nports, details, hsum, error);
     return String(out.c_str());
 }
 
@@ -192,6 +192,8 @@ GPUIPCheckClassify::add_handlers()
     add_read_handler("port_counts", read_handler, h_port_counts);
     add_read_handler("flow_count", read_handler, h_flow_count);
     add_read_handler("flow_drops", read_handler, h_flow_drops);
+    add_read_handler("gpu_errors", read_handler, h_gpu_errors);
+    add_read_handler("gpu_retries", read_handler, h_gpu_retries);
     add_read_handler("error", read_handler, h_error);
 }
 

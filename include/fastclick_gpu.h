@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 17
+#define FCGPU_ABI_VERSION 18
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -329,6 +329,10 @@ int  fcgpu_span_poll(fcgpu_ctx *ctx, uint32_t slot);
 #define FCGPU_OUT_TILE_PERM  (1u << 6)   /* TILE                                         */
 #define FCGPU_OUT_FLOWID     (1u << 7)
 #define FCGPU_OUT_IP_RW      (1u << 8)
+/* Not an output: this one submission goes through copies (H2D of h_in, D2H
+ * of the results) whatever the span mode -- never zero-copy, never the shared
+ * queue. What an element re-submits a failed batch with (SURVEY 8(b) Errors). */
+#define FCGPU_SUBMIT_COPY    (1u << 31)
 #define FCGPU_OUT_ABSENT     ((size_t)-1)
 typedef struct fcgpu_block_layout {
     size_t verdict, hash, anno, perm, port_start, tile_count, tile_perm, flowid, ip_rw;  /* byte offsets */
@@ -377,6 +381,35 @@ int  fcgpu_span_submit_block(fcgpu_ctx *ctx, uint32_t slot, const void *h_in, si
 #define FCGPU_SPAN_ZEROCOPY 1u
 #define FCGPU_SPAN_AUTO     2u
 int  fcgpu_span_mode(fcgpu_ctx *ctx, uint32_t mode);
+/* Fault injection (tests of the callers' error paths; process-wide, every
+ * context): after `skip` events of kind `where` pass, the next `count` fail
+ * as a HIP failure would, with FCGPU_ERUNTIME and a message:
+ *   FCGPU_FAULT_SUBMIT -- fcgpu_span_submit / fcgpu_span_submit_block return
+ *                         the error; nothing was queued, the slot stays free;
+ *   FCGPU_FAULT_WAIT   -- fcgpu_span_submit / fcgpu_span_submit_block accept
+ *                         the batch but nothing runs (an asynchronous launch
+ *                         failure): its fcgpu_span_wait / fcgpu_span_poll
+ *                         returns the error and frees the slot;
+ *   FCGPU_FAULT_LAUNCH -- the next shared-queue launch (FCGPU_SPAN_AUTO) fails:
+ *                         every batch it carried reports the error through its
+ *                         owner's wait or poll.
+ * Events: submissions for SUBMIT and WAIT (an element's re-submission is
+ * one), shared launches for LAUNCH. count 0 clears the kind. Returns
+ * FCGPU_EINVAL for another kind. */
+#define FCGPU_FAULT_SUBMIT 0u
+#define FCGPU_FAULT_WAIT   1u
+#define FCGPU_FAULT_LAUNCH 2u
+int  fcgpu_inject_fault(uint32_t where, uint32_t skip, uint32_t count);
+
+/* Host-only self-test of the launch guard every kernel launch passes (no
+ * device needed): a set of malformed launches -- a partition output the
+ * kernel stores through left null (tile_count under a tile partition, the
+ * per-tile counts under a whole-batch one), null frames, descriptors or
+ * counters, more workgroups than tiles, fused batches not end to end or too
+ * many -- must all be refused. Returns how many were accepted (0 = all
+ * refused), or -1 if a well-formed launch was refused. */
+int  fcgpu_launch_guard_selftest(void);
+
 /* 1 if the context's next block submission would be zero-copy (ZEROCOPY, or
  * AUTO with enough contexts), else 0 -- e.g. for an element that stages
  * smaller batches when its batches share the PCIe-read path with others. */

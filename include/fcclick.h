@@ -49,7 +49,7 @@ typedef struct fcclick_result {
     int32_t  *out_nh;       /* [n] network header offset from data() (-1 unset)          */
     uint32_t *out_batches;  /* [1] number of PacketBatches the sinks received             */
     char     *handlers;     /* "name=value\n" for count, drops, drop_details, port_counts,
-                               flow_count, flow_drops, error                              */
+                               flow_count, flow_drops, gpu_errors, gpu_retries, error     */
     size_t    handlers_cap;
     uint8_t  *out_paint;    /* [n] PAINT_ANNO (anno u8 @17) on departure (may be NULL)     */
     uint32_t *out_flow;     /* [n] anno u32 @28 (FLOWID_ANNO default) on departure (may be NULL) */

@@ -7,8 +7,10 @@ build oracle/_ref/fcref from the reference's own lib/in_cksum.c and headers
 tests/golden/gen_golden.py run_kat() does (same seeds) and compare them with
 the committed tests/golden/kat.npz array by array. Without that tree the
 harness cannot be built here (this pipeline does not run the reference's
-configure), so the script says so and exits 0: the committed fixtures stay
-the pin. Exit 1 on any mismatch.
+configure, and writing a stand-in config.h is not allowed): the script says so
+and exits 3 (FROZEN) -- tests/test_golden.py::test_reference_harness_kat turns
+that into a visible pytest skip, so the frozen pin shows in every run. Exit 1
+on any mismatch, 0 when every array was re-derived identically.
 """
 import os
 import subprocess
@@ -17,15 +19,16 @@ import sys
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+FROZEN = 3
 ROOT = os.path.dirname(os.path.dirname(HERE))
 
 
 def main():
     fcbuild = os.environ.get("FCBUILD", "/tmp/fcbuild")
     if not os.path.exists(os.path.join(fcbuild, "include", "click", "config.h")):
-        print(f"check_kat: no {fcbuild}/include/click/config.h -- reference harness not buildable here; "
-              "tests/golden/kat.npz stays the pin")
-        return 0
+        print(f"check_kat: FROZEN -- no {fcbuild}/include/click/config.h, so the reference harness is not "
+              "buildable here; tests/golden/kat.npz is not re-derived (last derived round 1)")
+        return FROZEN
     subprocess.check_call(["make", "-s", "-C", HERE, f"FCBUILD={fcbuild}"])
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     import gen_golden
