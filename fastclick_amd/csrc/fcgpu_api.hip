@@ -222,6 +222,7 @@ struct fcgpu_ctx {
     int32_t prog_all = -1;
     std::vector<fcgpu_step> prog_host;   // the installed program (capture reach)
     std::vector<uint4> prog_dev;         // ... in the device format (table steps, fallbacks, tables)
+    uint64_t prog_key = 0;               // hash of the installed program's contents (0: none)
     // fcgpu_program_jit: the program compiled to code (prog_jit.hh)
     bool jit_on = false;
     std::string jit_src;                 // generated program function ("" = interpreted)
@@ -1890,6 +1891,7 @@ struct AggItem {
     bool ck;
     unsigned long long *ctr;  // the counter vector in use at submit
     hipFunction_t fn;         // the compiled program's k_rx (nullptr: the built-in kernel)
+    uint64_t prog_key;        // the program's contents (dcfg.prog is this context's copy of it)
 };
 struct AggQueue {
     std::mutex mu;
@@ -1917,9 +1919,17 @@ static bool agg_eligible(const fcgpu_ctx *c, const fcgpu_out &o) {
 }
 // One launch takes its configuration from its first item: the others must
 // have the same one (everything agg_launch_locked reads from it).
+// Device copies of equal contents (the program, the CRC tables) do not
+// matter: the launch reads the first item's, which its owner keeps until
+// its own wait (and fcgpu_set_program synchronises before freeing one).
 static bool agg_compatible(const AggItem &a, const AggItem &b) {
-    return memcmp(&a.dcfg, &b.dcfg, sizeof(DevCfg)) == 0 && a.cm == b.cm && a.ck == b.ck && a.fn == b.fn &&
-           out_part(&a.job.out) == out_part(&b.job.out) && a.job.out.partition == b.job.out.partition;
+    DevCfg x = a.dcfg, y = b.dcfg;
+    x.prog = y.prog = nullptr;
+    x.crc_tab = y.crc_tab = nullptr;
+    return memcmp(&x, &y, sizeof(DevCfg)) == 0 && a.prog_key == b.prog_key &&
+           (a.dcfg.crc_tab != nullptr) == (b.dcfg.crc_tab != nullptr) && a.cm == b.cm && a.ck == b.ck &&
+           (a.fn != nullptr) == (b.fn != nullptr) && out_part(&a.job.out) == out_part(&b.job.out) &&
+           a.job.out.partition == b.job.out.partition;
 }
 // A context with a queued submission keeps the configuration, program and
 // compiled module that submission was taken with (fcgpu_configure,
@@ -2076,6 +2086,7 @@ static int agg_submit(fcgpu_ctx *c, uint32_t slot, const fcgpu_job &j) {
     if (it.cm == FCGPU_MARK_IP4 || it.cm == FCGPU_MARK_IP6) it.ck = false;
     it.ctr = c->d_ctr;
     it.fn = nullptr;
+    it.prog_key = c->cfg.classify == FCGPU_CLS_PROGRAM ? c->prog_key : 0;
     if (c->cfg.classify == FCGPU_CLS_PROGRAM && !c->jit_src.empty()) {
         const bool ip4 = it.cm == FCGPU_CHECK_IP4 || it.cm == FCGPU_MARK_IP4;
         it.fn = jit_function(c, jit_key((int)it.cm, it.ck, out_part(&j.out), ip4 && c->cfg.l4_mode != FCGPU_L4_NONE,
@@ -2626,6 +2637,19 @@ int fcgpu_set_program(fcgpu_ctx *c, uint32_t kind, const fcgpu_step *steps, uint
     c->dcfg.prog_kind = c->prog_kind;
     c->dcfg.prog_all = c->prog_all;
     c->prog_dev = dev;
+    // contents, not the device copy: contexts with one program share launches
+    uint64_t key = 1469598103934665603ull;
+    auto mix = [&key](uint32_t v) {
+        for (int b = 0; b < 4; ++b) key = (key ^ ((v >> (8 * b)) & 0xff)) * 1099511628211ull;
+    };
+    for (const uint4 &q : dev) {
+        mix(q.x);
+        mix(q.y);
+        mix(q.z);
+        mix(q.w);
+    }
+    for (uint32_t v : {c->prog_n, c->prog_q, c->prog_tab, c->prog_kind, (uint32_t)c->prog_all}) mix(v);
+    c->prog_key = key | 1;
     if (c->jit_on && jit_install(c) != FCGPU_OK) c->err.clear();   // a cycle: interpreted
     return FCGPU_OK;
 }

@@ -774,6 +774,26 @@ __device__ __forceinline__ uint32_t wave_l4_sum(const uint8_t *seg, uint32_t len
     return mine;
 }
 
+// The same 16-bit sum for a segment inside the lane's LDS window (frame bytes
+// [b, b + len) with b + len + shift <= kWin): the window's aligned dwords,
+// bytes outside the segment masked. Window byte 0 is 16-B aligned in the
+// arena, so the segment's address parity is that of its window byte. Reading
+// the window instead of the arena matters when the arena is host memory read
+// over PCIe (zero-copy): the datagram of a small frame is already in LDS.
+__device__ __forceinline__ uint32_t win_l4_sum(const FrameView &f, uint32_t b, uint32_t len) {
+    const uint32_t x0 = b + f.shift, x1 = x0 + len;
+    uint64_t acc = 0;
+    for (uint32_t a = x0 & ~3u; a < x1; a += 4) {
+        const uint32_t w = *reinterpret_cast<const uint32_t *>(f.row + ((((a >> 4) ^ f.sw) << 4) | (a & 15)));
+        acc += dw_masked(w, a, x0, x1);
+    }
+    uint32_t t = (uint32_t)acc + (uint32_t)(acc >> 32);
+    t += (t < (uint32_t)acc) ? 1u : 0u;
+    t = (t & 0xffff) + (t >> 16);
+    t = (t & 0xffff) + (t >> 16);
+    return (x0 & 1) ? bswap16(t) : t;
+}
+
 // click_in_cksum_pseudohdr (include/clicknet/ip.h:156-163, lib/in_cksum.c:53-111):
 // the final destination of an SSRR/LSRR option replaces ip_dst. True = bad.
 __device__ __forceinline__ bool l4_cksum_bad(const FrameView &f, const fcgpu_anno &an, uint32_t dsum,
@@ -818,9 +838,12 @@ __device__ __forceinline__ void l4_stage(const DevCfg &c, const FrameView &f, co
             r.hash = 0;
         }
     }
-    const uint64_t need = __ballot(want);
-    if (need) {
-        const uint32_t dsum = wave_l4_sum(frame + r.an.th, l4len, need);
+    // segments inside the LDS window are summed there, the rest by the wave
+    const bool inwin = want && r.an.th + l4len + f.shift <= (uint32_t)kWin;
+    const uint64_t need = __ballot(want && !inwin);
+    if (need || __ballot(inwin)) {
+        uint32_t dsum = need ? wave_l4_sum(frame + r.an.th, l4len, need) : 0u;
+        if (inwin) dsum = win_l4_sum(f, r.an.th, l4len);
         if (want && l4_cksum_bad(f, r.an, dsum, l4len)) {
             r.reason = FCGPU_R_L4_CKSUM;
             r.port = c.nports;

@@ -56,6 +56,12 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     return FCGPU_OK;
 }
 int fcgpu_span_mode(fcgpu_ctx *, uint32_t) { return FCGPU_OK; }
+// MOCK_ZEROCOPY=1: report zero-copy (the element's BATCH auto then stages
+// 4096-packet batches, as with >= 4 threads on a real GPU)
+int fcgpu_span_zerocopy_active(const fcgpu_ctx *) {
+    const char *e = getenv("MOCK_ZEROCOPY");
+    return e && *e == '1';
+}
 void *fcgpu_host_alloc(size_t bytes) { return aligned_alloc(4096, (bytes + 4095) & ~(size_t)4095); }
 void fcgpu_host_free(void *p) { free(p); }
 int fcgpu_block_layout_for(const fcgpu_ctx *c, uint32_t n, uint32_t outputs, uint32_t, fcgpu_block_layout *L) {

@@ -8,9 +8,10 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() {  # name timeout cmd...
   local name=$1 t=$2; shift 2
-  echo "== $name $(date +%T)"; timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  echo "== $name $(date +%T)"; local t0=$SECONDS
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
-  echo "== $name rc=$rc"; tail -n 3 "gpurun_out/$name.log" | cut -c1-1500
+  echo "== $name rc=$rc wall=$((SECONDS - t0))s"; tail -n 3 "gpurun_out/$name.log" | cut -c1-1500
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
 kt() {  # name timeout bench-args...: kernel trace + stats of a bench command
@@ -86,7 +87,13 @@ for s in "${ST[@]}"; do
              kt kt_flow_c3 300 --steps 200 --warmup 20 --no-cpu --workload c3 --flow-capacity 20000 &&
              kt kt_flow_c4 300 --steps 200 --warmup 20 --no-cpu --workload c4 --flow-capacity 2000000 ;;
     latency) step latency 120 python scripts/latency_probe.py ;;
+    crossover) step crossover 1100 python -u scripts/crossover.py ;;
+    crossover16) step crossover16 600 python -u scripts/crossover.py --threads 8,16 --no-cpu ;;
+    mock_ab) step mock_ab 600 bash scripts/mock_ab_box.sh ;;
     dist2) step dist2 300 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 --no-cpu ;;
+    # the driver's 8-rank command shape, rehearsed on one GPU (gloo: RCCL needs a GPU per rank)
+    dist8) step dist8_weak 900 python bench.py --gpus 8 --backend gloo --steps 20 --warmup 5 --no-cpu &&
+           step dist8_strong 900 python bench.py --gpus 8 --backend gloo --shard strong --steps 20 --warmup 5 --no-cpu ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
