@@ -57,4 +57,50 @@ inline uint32_t capture_bytes(const fcgpu_cfg &c, uint32_t prog_reach) {
     return need < kCaptureMin ? kCaptureMin : need;
 }
 
+// Compact staging (the element's block records). For the IPv4 chains whose
+// reads all fall in [start, o + hl + tail) of each frame -- CheckIPHeader /
+// MarkIPHeader at OFFSET o (header, options, addresses), the ports IPFlowID /
+// IPFlow5ID read at th = o + hl (AggregateHash, FlowSwitch LB hash / hash_crc,
+// the flow table), CheckUDPHeader / CheckTCPHeader's length words without
+// their checksum (tail 16), DecIPTTL / SetIPChecksum (header), LB hash_ip's
+// bytes 26..33 and HashSwitch's range -- a record holds only those bytes: the
+// descriptor points `start` bytes before the record, so the device finds
+// every byte it reads at its frame offset, and bytes outside the range (the
+// neighbouring records) are never part of a decision. A 60-B UDP frame then
+// stages 32 B instead of 64. Chains that read more (AUTO with VLAN / IPv6,
+// decision programs, L4 checksums over the datagram) keep whole captures.
+struct StagePlan {
+    bool compact = false;
+    uint32_t start = 0;       // first frame byte any stage reads
+    uint32_t fixed_end = 0;   // frame bytes every packet needs up to (hash_ip, HashSwitch)
+    uint32_t tail = 4;        // bytes past th: ports (4) or the L4 length checks' words (16)
+};
+inline StagePlan stage_plan(const fcgpu_cfg &c) {
+    StagePlan p;
+    const bool ip4 = c.check_mode == FCGPU_CHECK_IP4 || c.check_mode == FCGPU_MARK_IP4;
+    if (!ip4 || c.classify == FCGPU_CLS_PROGRAM || (c.l4_mode != FCGPU_L4_NONE && c.l4_checksum)) return p;
+    p.compact = true;
+    p.start = (uint32_t)c.offset;
+    p.tail = c.l4_mode != FCGPU_L4_NONE ? 16u : 4u;
+    if (c.classify == FCGPU_CLS_HASH_IP) {
+        p.start = p.start < 26u ? p.start : 26u;
+        p.fixed_end = 34;
+    } else if (c.classify == FCGPU_CLS_HASHSWITCH) {
+        const uint32_t o = (uint32_t)c.hs_offset, e = o + (uint32_t)c.hs_length;
+        p.start = p.start < o ? p.start : o;
+        p.fixed_end = e;
+    }
+    return p;
+}
+// The frame bytes [plan.start, end) a packet's record must hold.
+inline uint32_t stage_end(const StagePlan &p, uint32_t offset, const uint8_t *frame, uint32_t len) {
+    uint32_t end = p.fixed_end;
+    if (len > offset) {
+        const uint32_t e = offset + ((uint32_t)(frame[offset] & 15) << 2) + p.tail;   // th + tail
+        end = e > end ? e : end;
+    }
+    return end < len ? end : len;
+}
+constexpr uint32_t kStageLead = 256;   // records start this far into the block (descriptor offsets >= 0)
+
 }  // namespace fcgpu

@@ -89,6 +89,10 @@
 //   the GPU (their copies would queue on one copy engine), else copies,
 //   PARTITION TILE (default: each 256-packet tile classified as one batch,
 //   one fused launch) | GLOBAL (the whole device batch as one, three launches)
+//   COMPACT true|false (default true): for IPv4 chains that read only the
+//     header, the ports and fixed byte ranges, each packet stages just those
+//     bytes in a 16-B record (capture.hh stage_plan): 32 B for a 60-B UDP
+//     frame instead of a 64-B slot -- the bytes a batch moves over PCIe
 //   ERROR_OUTPUT p (default -1: kill)          -- where the packets of a batch the
 //     GPU failed twice leave, unprocessed and in input order
 // Handlers: count, drops, drop_details (DETAILS true), port_counts,
@@ -313,6 +317,8 @@ class RxCore {
             } else if (k == "FLOWID_ANNO") {
                 if (!parse_int(v, n) || n < 0 || n > P::kAnnoSize - 4) return err(errh, "bad FLOWID_ANNO");
                 _flow_anno = (int)n;
+            } else if (k == "COMPACT") {
+                if (!parse_bool(v, _compact)) return err(errh, "COMPACT expects true/false");
             } else if (k == "ERROR_OUTPUT") {
                 if (!parse_int(v, n) || n < -1 || n > FCGPU_MAX_PORTS + 1) return err(errh, "bad ERROR_OUTPUT");
                 _error_output = (int)n;
@@ -385,6 +391,9 @@ class RxCore {
             if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_flow_configure: ") + fcgpu_last_error(_ctx));
         }
         _capture = fcgpu::capture_bytes(_cfg, reach);
+        _plan = fcgpu::stage_plan(_cfg);
+        _plan.compact = _plan.compact && _compact;
+        _lead = _plan.compact ? fcgpu::kStageLead : 0u;
         const size_t per = _capture == fcgpu::kCaptureWhole ? 1536 : _capture;
         _outputs = FCGPU_OUT_VERDICT | FCGPU_OUT_HASH | FCGPU_OUT_ANNO |
                    (_partition == FCGPU_PART_TILE ? FCGPU_OUT_TILE_PERM | FCGPU_OUT_TILE_COUNT
@@ -394,7 +403,7 @@ class RxCore {
         if (fcgpu_block_layout_for(_ctx, _cap, _outputs, _partition, &L) != FCGPU_OK)
             return err(errh, "fcgpu_block_layout_for failed");
         for (uint32_t k = 0; k < _nslots; ++k)
-            if (!_slot[k].alloc(_cap, (size_t)_cap * per + 65536, L.bytes))
+            if (!_slot[k].alloc(_cap, (size_t)_cap * per + 65536 + _lead, L.bytes))
                 return err(errh, "cannot allocate pinned staging (fcgpu_host_alloc)");
         return 0;
     }
@@ -639,9 +648,20 @@ class RxCore {
     inline void stage(Packet *p, Emit &emit) {
         Slot *s = &_slot[_cur];
         const uint32_t len = P::length(p);
-        const uint32_t cp = len < _capture ? len : _capture;
-        const size_t rec = cp ? ((size_t)cp + 63) & ~(size_t)63 : 64;
-        if (s->n && s->frames_off + s->used + rec > s->in_cap) {   // whole frames overflowing the block
+        const uint8_t *src = P::data(p);
+        uint32_t cp;
+        size_t rec;
+        if (_plan.compact) {
+            // the frame bytes [start, end) the chain reads, in 16-B records
+            const uint32_t end = fcgpu::stage_end(_plan, (uint32_t)_cfg.offset, src, len);
+            cp = end > _plan.start ? end - _plan.start : 0u;
+            src += cp ? _plan.start : 0u;
+            rec = cp ? ((size_t)cp + 15) & ~(size_t)15 : 16;
+        } else {
+            cp = len < _capture ? len : _capture;
+            rec = cp ? ((size_t)cp + 63) & ~(size_t)63 : 64;
+        }
+        if (s->n && s->frames_off + _lead + s->used + rec > s->in_cap) {   // whole frames overflowing the block
             submit(emit);
             s = &_slot[_cur];
         }
@@ -652,8 +672,9 @@ class RxCore {
             }
             s->t_first = _timer_us >= 0 ? P::now_ns() : 0;
         }
-        copy_head(s->span + s->used, P::data(p), cp);
-        s->desc[2 * s->n] = (uint32_t)s->used;
+        copy_head(s->span + _lead + s->used, src, cp);
+        // compact: frame byte b of the packet is at record + b - start
+        s->desc[2 * s->n] = (uint32_t)(_lead + s->used) - (_plan.compact ? _plan.start : 0u);
         s->desc[2 * s->n + 1] = len;
         s->pkts[s->n++] = p;
         s->used += rec;
@@ -670,7 +691,7 @@ class RxCore {
         {
             std::lock_guard<std::mutex> g(_mu);
             if (_flow_cap && _flow_timeout) flow_clock();
-            int rc = fcgpu_span_submit_block(_ctx, k, s.in, s.frames_off + s.used, 0, s.frames_off, s.n, s.res,
+            int rc = fcgpu_span_submit_block(_ctx, k, s.in, s.frames_off + _lead + s.used, 0, s.frames_off, s.n, s.res,
                                              _outputs, _partition);
             // BATCH auto: the next batches' size for the path they now take
             _eff_batch = _batch_auto && fcgpu_span_zerocopy_active(_ctx) ? kBatchZeroCopy : _batch;
@@ -692,7 +713,7 @@ class RxCore {
         _gpu_retries.fetch_add(1, std::memory_order_relaxed);
         P::chatter(name + ": GPU batch failed (" + std::string(fcgpu_last_error(_ctx)) + "), re-submitting it");
         _fail_msg = fcgpu_last_error(_ctx);
-        return fcgpu_span_submit_block(_ctx, k, s.in, s.frames_off + s.used, 0, s.frames_off, s.n, s.res,
+        return fcgpu_span_submit_block(_ctx, k, s.in, s.frames_off + _lead + s.used, 0, s.frames_off, s.n, s.res,
                                        _outputs | FCGPU_SUBMIT_COPY, _partition);
     }
 
@@ -965,6 +986,9 @@ class RxCore {
     int64_t _timer_us = 100;
     uint32_t _cap = 0;
     uint32_t _capture = fcgpu::kCaptureMin;
+    fcgpu::StagePlan _plan;                      // compact records (capture.hh) when the chain allows them
+    bool _compact = true;                        // COMPACT
+    uint32_t _lead = 0;                          // compact: records start this far into the block
     uint32_t _partition = FCGPU_PART_TILE;
     uint32_t _span_mode = FCGPU_SPAN_AUTO;       // ZEROCOPY: the kernels read/write the pinned slots in place
     uint32_t _outputs = 0;                       // FCGPU_OUT_* the element asks for

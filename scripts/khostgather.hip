@@ -119,19 +119,25 @@ int main(int argc, char **argv) {
     // element's packed staging records); argv[3] = 0: pieces in address order
     const size_t stride = argc > 2 ? (size_t)atoi(argv[2]) : 2304;
     const bool shuffled = argc > 3 ? atoi(argv[3]) != 0 : true;
-    const size_t bytes = stride * n + 4096;
+    // argv[4]: bytes each 64-B read starts before its piece (16: a window
+    // that starts 16 B early, as k_rx's does for a record staged from frame
+    // byte 14 at a 16-B aligned address -- neighbouring windows overlap when
+    // the stride is < 64)
+    const uint32_t lead = argc > 4 ? (uint32_t)atoi(argv[4]) : 0u;
+    const size_t bytes = stride * n + 4096 + 128;
     std::vector<uint32_t> off(n);
-    for (uint32_t i = 0; i < n; ++i) off[i] = (uint32_t)(i * stride + (stride >= 2304 ? 256 : 0));   // data after header + headroom
+    for (uint32_t i = 0; i < n; ++i) off[i] = (uint32_t)(i * stride + (stride >= 2304 ? 256 : 0) + 64 - lead);
     std::mt19937 rng(1);
     if (shuffled) std::shuffle(off.begin(), off.end(), rng);
-    printf("# %u pieces, stride %zu B, %s\n", n, stride, shuffled ? "shuffled" : "in address order");
+    printf("# %u pieces, stride %zu B, %s, reads start %u B before each piece\n", n, stride,
+           shuffled ? "shuffled" : "in address order", lead);
     uint32_t *doff, *dout;
     CK(hipMalloc(&doff, 4ull * n));
     CK(hipMalloc(&dout, 4ull * n));
     CK(hipMemcpy(doff, off.data(), 4ull * n, hipMemcpyHostToDevice));
     struct M { const char *name; Kern k; } ms[] = {
         {"glds", k_glds}, {"vec4", k_vec4}, {"lane64", k_lane64}, {"lane16", k_lane16}, {"w8x8", k_w8x8}};
-    for (int mem = 0; mem < 2; ++mem) {
+    for (int mem = 0; mem < 3; ++mem) {
         uint8_t *host = nullptr, *dev = nullptr;
         if (mem == 0) {
             host = static_cast<uint8_t *>(aligned_alloc(4096, (bytes + 4095) / 4096 * 4096));
@@ -139,19 +145,22 @@ int main(int argc, char **argv) {
             CK(hipHostRegister(host, (bytes + 4095) / 4096 * 4096, hipHostRegisterMapped));
             CK(hipHostGetDevicePointer((void **)&dev, host, 0));
         } else {
-            CK(hipHostMalloc((void **)&host, bytes, hipHostMallocDefault));
+            // 1: coherent (hipHostMallocDefault); 2: non-coherent -- the GPU's
+            // L2 may keep its lines within a kernel (written by the host
+            // before the launch, read by the kernel only)
+            CK(hipHostMalloc((void **)&host, bytes, mem == 1 ? hipHostMallocDefault : hipHostMallocNonCoherent));
             for (size_t j = 0; j < bytes; j += 4096) host[j] = (uint8_t)j;
             CK(hipHostGetDevicePointer((void **)&dev, host, 0));
         }
         for (auto &m : ms) {
             const double us = run(m.k, dev, doff, n, dout, 10);
-            printf("%s %-7s %8.1f us  %7.1f M pieces/s\n", mem == 0 ? "registered" : "hostmalloc", m.name, us,
-                   n / us);
+            printf("%s %-7s %8.1f us  %7.1f M pieces/s\n",
+                   mem == 0 ? "registered" : mem == 1 ? "hostmalloc" : "noncoherent", m.name, us, n / us);
         }
         if (mem == 0) {
             CK(hipHostUnregister(host));
             free(host);
-        } else {
+        } else {  // 1, 2
             CK(hipHostFree(host));
         }
     }

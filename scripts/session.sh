@@ -83,6 +83,10 @@ for s in "${ST[@]}"; do
     host) step host_rate 600 python scripts/host_rate.py ;;
     host_q16) GPU_MAX_HW_QUEUES=16 step host_rate_q16 600 python scripts/host_rate.py ;;
     kgather) step kgather 180 ./scripts/kgather 64 ;;
+    khg) for a in "16384 64 0 0" "16384 32 0 16" "16384 48 0 16" "262144 64 0 0" "262144 32 0 16" "262144 48 0 16"; do
+           n=$(echo "$a" | tr ' ' _)
+           step "khg_$n" 120 ./scripts/khostgather $a
+         done ;;
     kt_flow) kt kt_flow_c2 300 --steps 200 --warmup 20 --no-cpu --flow-capacity 1 &&
              kt kt_flow_c3 300 --steps 200 --warmup 20 --no-cpu --workload c3 --flow-capacity 20000 &&
              kt kt_flow_c4 300 --steps 200 --warmup 20 --no-cpu --workload c4 --flow-capacity 2000000 ;;
@@ -90,6 +94,13 @@ for s in "${ST[@]}"; do
     crossover) step crossover 1100 python -u scripts/crossover.py ;;
     crossover16) step crossover16 600 python -u scripts/crossover.py --threads 8,16 --no-cpu ;;
     mock_ab) step mock_ab 600 bash scripts/mock_ab_box.sh ;;
+    el_sweep) step el_sweep 900 bash scripts/el_sweep.sh 3 ;;
+    # the element at 16 threads (default BATCH/ZEROCOPY/SLOTS): rate, then a kernel trace
+    el16) step el16 300 python scripts/element_threads.py 16 &&
+          step el16_s3 300 python scripts/element_threads.py 16 0 auto 3 &&
+          step el16_b8k 300 python scripts/element_threads.py 16 8192 auto 2 &&
+          step el8 300 python scripts/element_threads.py 8 &&
+          step kt_el16 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_kt_el16 -o run -- python3 scripts/element_threads.py 16 ;;
     dist2) step dist2 300 python bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 --no-cpu ;;
     # the driver's 8-rank command shape, rehearsed on one GPU (gloo: RCCL needs a GPU per rank)
     dist8) step dist8_weak 900 python bench.py --gpus 8 --backend gloo --steps 20 --warmup 5 --no-cpu &&

@@ -457,3 +457,62 @@ def test_config_span_keywords():
                      ("BATCH -1", "BATCH"), ("BATCH many", "BATCH")):
         with pytest.raises(K.ConfigError, match=msg):
             K.check_config(f"GPUIPCheckClassify(OFFSET 14, {bad})")
+
+
+COMPACT_CONFS = [
+    ("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, DETAILS true)", 17),
+    ("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 8, LB_MODE hash_crc)", 9),
+    ("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 5, LB_MODE hash_ip)", 6),
+    ("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, HASHSWITCH 6 8, N 7)", 8),
+    ("GPUIPCheckClassify(OFFSET 14, MODE MARK, N 4, LB_MODE hash, HASH FLOW5ID)", 5),
+    ("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4, L4 TCP, L4_CHECKSUM false)", 5),
+    ("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 8, DEC_TTL true, SET_CHECKSUM true)", 9),
+    ("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4, FLOW_CAPACITY 5000)", 5),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("conf,nsinks", COMPACT_CONFS)
+@pytest.mark.parametrize("zc", ["false", "true"])
+def test_element_compact_records_match_full(oracle, conf, nsinks, zc):
+    """COMPACT true (the default: each packet stages only the frame bytes the
+    chain reads -- header, options, ports / L4 length words, hash_ip's and
+    HashSwitch's ranges -- in 16-B records whose neighbours are other
+    packets' bytes) against COMPACT false (whole 64-B-slot captures): the same
+    outputs, order, annotations, rewritten bytes, flow IDs and handlers, on
+    packets with IP options, every header error, non-first fragments, TCP
+    frames and truncated ones, in copy and zero-copy mode."""
+    from fastclick_amd import click as K
+    from tests.helpers import set_fragment
+    b = synth.c4(10_000 + 7, seed=560)
+    synth.add_ip_options(b, 0.2, seed=561)
+    synth.inject_errors(b, 0.03, seed=562)
+    set_fragment(b, 0.05, seed=563)
+    rng = np.random.default_rng(564)
+    off = b.desc[:, 0].astype(np.int64) + 14
+    tcp = rng.random(b.n) < 0.2
+    b.arena[off[tcp] + 9] = 6                          # protocol TCP: CheckTCPHeader's words differ
+    for i in np.nonzero(tcp)[0]:
+        synth._refresh_cksum(b.arena, int(off[i]))
+    short = rng.random(b.n) < 0.02
+    b.desc[short, 1] = rng.integers(0, 40, int(short.sum()))   # truncated frames
+    base = conf[:-1] + f", BATCH 4096, ZEROCOPY {zc}"
+    full = K.run_element(base + ", COMPACT false)", b, burst=32, nsinks=nsinks)
+    comp = K.run_element(base + ")", b, burst=32, nsinks=nsinks)
+    e = oracle.process_batch(K.element_cfg(conf), b)
+    if "MARK" in conf:
+        # MarkIPHeader checks nothing: ports past a truncated packet's end are
+        # whatever follows it in memory, for the reference as for either
+        # staging (undefined, DESIGN section 4); compared where defined
+        defined = e["anno"]["th"].astype(np.int64) + 4 <= b.desc[:, 1].astype(np.int64)
+        assert defined.sum() > 0.9 * b.n
+        for k in ("port", "agg", "dst", "len", "nh"):
+            assert np.array_equal(full[k][defined], comp[k][defined]), k
+    else:
+        for k in ("port", "seq", "agg", "dst", "len", "nh", "flow", "ip8", "batch"):
+            assert np.array_equal(full[k], comp[k]), k
+        assert full["handlers"] == comp["handlers"]
+    if "FLOW" not in conf and "DEC_TTL" not in conf and "L4" not in conf:
+        port = e["port"].astype(np.uint32)
+        inside = (e["anno"]["th"].astype(np.int64) + 4 <= b.desc[:, 1].astype(np.int64)) | ("MARK" not in conf)
+        assert np.array_equal(comp["port"][inside], np.where(port < nsinks, port, 0xFFFFFFFF)[inside])
