@@ -58,7 +58,7 @@ inline uint32_t capture_bytes(const fcgpu_cfg &c, uint32_t prog_reach) {
 }
 
 // Compact staging (the element's block records). For the IPv4 chains whose
-// reads all fall in [start, o + hl + tail) of each frame -- CheckIPHeader /
+// reads all fall in [start, o + max(hl, 20) + tail) of each frame -- CheckIPHeader /
 // MarkIPHeader at OFFSET o (header, options, addresses), the ports IPFlowID /
 // IPFlow5ID read at th = o + hl (AggregateHash, FlowSwitch LB hash / hash_crc,
 // the flow table), CheckUDPHeader / CheckTCPHeader's length words without
@@ -96,8 +96,13 @@ inline StagePlan stage_plan(const fcgpu_cfg &c) {
 inline uint32_t stage_end(const StagePlan &p, uint32_t offset, const uint8_t *frame, uint32_t len) {
     uint32_t end = p.fixed_end;
     if (len > offset) {
-        const uint32_t e = offset + ((uint32_t)(frame[offset] & 15) << 2) + p.tail;   // th + tail
+        // th + tail, and never less than the 20-B header: MarkIPHeader takes
+        // any hl, and IPFlowID / DST_IP read the addresses at o + 12..19
+        const uint32_t hl = (uint32_t)(frame[offset] & 15) << 2;
+        const uint32_t e = offset + (hl > 20u ? hl : 20u) + (hl >= 20u ? p.tail : 0u);
+        const uint32_t ep = offset + hl + p.tail;
         end = e > end ? e : end;
+        end = ep > end ? ep : end;
     }
     return end < len ? end : len;
 }

@@ -95,6 +95,8 @@ for s in "${ST[@]}"; do
     crossover16) step crossover16 600 python -u scripts/crossover.py --threads 8,16 --no-cpu ;;
     mock_ab) step mock_ab 600 bash scripts/mock_ab_box.sh ;;
     el_sweep) step el_sweep 900 bash scripts/el_sweep.sh 3 ;;
+    el_sweep2) BATCHES="4096 8192 16384" SLOTS_LIST=2 step el_sweep2 900 bash scripts/el_sweep.sh 3 16 8 4 ;;
+    el_spin) step el_spin 900 bash scripts/el_spin.sh 3 ;;
     # the element at 16 threads (default BATCH/ZEROCOPY/SLOTS): rate, then a kernel trace
     el16) step el16 300 python scripts/element_threads.py 16 &&
           step el16_s3 300 python scripts/element_threads.py 16 0 auto 3 &&
