@@ -154,11 +154,15 @@ struct HostSlot {
 
 // One in-flight fcgpu_span_submit: device copy of the span and descriptors,
 // device outputs, the stream it runs on.
-// one launch of the shared zero-copy queue (FCGPU_SPAN_AUTO, agg_launch_locked)
+// one launch of the shared zero-copy queue (FCGPU_SPAN_AUTO, agg_take_locked / agg_issue)
 struct AggLaunch {
     hipEvent_t ev = nullptr;
     uint32_t refs = 0;        // submissions it carries that have not been waited for
+    // kAggIssuing until the thread that took the group from the queue has
+    // issued it (outside the queue's lock), then kAggIssued or kAggFailed
+    std::atomic<int> state{0};
 };
+constexpr int kAggIssuing = 0, kAggIssued = 1, kAggFailed = 2;
 
 struct SpanSlot {
     hipStream_t own = nullptr, s = nullptr;
@@ -180,7 +184,7 @@ struct SpanSlot {
     void *zc_val[11] = {};
     // FCGPU_SPAN_AUTO with many contexts: the submission went to the device's
     // shared queue (agg); al = the launch carrying it (nullptr while pending)
-    bool agg = false, agg_err = false;
+    bool agg = false;
     AggLaunch *al = nullptr;
     bool busy = false;
     bool doomed = false;         // fcgpu_inject_fault(FCGPU_FAULT_WAIT): accepted, nothing ran, the wait fails
@@ -248,6 +252,7 @@ struct fcgpu_ctx {
     SpanSlot span[FCGPU_SPAN_SLOTS];
     int span_index = -1;              // FCGPU_SPAN_STREAMS=shared:N: this context's place in the pool
     uint32_t span_mode = FCGPU_SPAN_COPY;   // fcgpu_span_mode: block submissions copied or read in place
+    struct AggQueue *aq = nullptr;          // the device's shared queue (FCGPU_SPAN_AUTO), once used
     // flow table (fcgpu_flow_enable)
     uint32_t max_flows = 0, flow_slots = 0, flow_words = 0;
     FlowArgs fl{};            // device pointers; fl.slots == nullptr: disabled
@@ -1829,26 +1834,22 @@ int fcgpu_span_submit(fcgpu_ctx *c, uint32_t slot, const uint8_t *h_span, size_t
 // submit few enough copies for the copy engine, and copies are faster there:
 // profiles/r03_s8/el_zc.log)
 constexpr uint32_t kZeroCopyAuto = 4;
-static std::mutex g_auto_mu;
-static std::map<int, uint32_t> g_auto_ctx;
+constexpr int kMaxDevices = 64;
+static std::atomic<uint32_t> g_auto_n[kMaxDevices];   // AUTO contexts per device (read on every submission)
 static void agg_release(int device);
 static void span_auto_count(fcgpu_ctx *c, uint32_t new_mode) {
     const bool was = c->span_mode == FCGPU_SPAN_AUTO, now = new_mode == FCGPU_SPAN_AUTO;
-    if (was == now) return;
-    bool last = false;
-    {
-        std::lock_guard<std::mutex> g(g_auto_mu);
-        uint32_t &n = g_auto_ctx[c->device];
-        n = now ? n + 1 : (n ? n - 1 : 0);
-        last = n == 0;
+    if (was == now || c->device < 0 || c->device >= kMaxDevices) return;
+    if (now) {
+        g_auto_n[c->device].fetch_add(1, std::memory_order_relaxed);
+    } else if (g_auto_n[c->device].fetch_sub(1, std::memory_order_acq_rel) == 1) {
+        agg_release(c->device);
     }
-    if (last) agg_release(c->device);
 }
 static bool span_zerocopy(const fcgpu_ctx *c) {
     if (c->span_mode != FCGPU_SPAN_AUTO) return c->span_mode == FCGPU_SPAN_ZEROCOPY;
-    std::lock_guard<std::mutex> g(g_auto_mu);
-    auto it = g_auto_ctx.find(c->device);
-    return it != g_auto_ctx.end() && it->second >= kZeroCopyAuto;
+    return c->device >= 0 && c->device < kMaxDevices &&
+           g_auto_n[c->device].load(std::memory_order_relaxed) >= kZeroCopyAuto;
 }
 
 // ---- waiting for a span slot ---------------------------------------------------
@@ -1930,13 +1931,15 @@ struct AggQueue {
 constexpr uint32_t kAggLaunch = 4;
 static std::mutex g_agg_mu;
 static std::map<int, AggQueue *> g_agg;
-static AggQueue &agg_queue(int device) {
+static AggQueue &agg_queue(fcgpu_ctx *c) {
+    if (c->aq) return *c->aq;
     std::lock_guard<std::mutex> g(g_agg_mu);
-    AggQueue *&q = g_agg[device];
+    AggQueue *&q = g_agg[c->device];
     if (!q) {
         q = new AggQueue();
-        q->device = device;
+        q->device = c->device;
     }
+    c->aq = q;
     return *q;
 }
 static bool agg_eligible(const fcgpu_ctx *c, const fcgpu_out &o) {
@@ -1944,7 +1947,7 @@ static bool agg_eligible(const fcgpu_ctx *c, const fcgpu_out &o) {
            !(c->cfg.rewrite & FCGPU_RW_INPLACE) && !c->timing_every;
 }
 // One launch takes its configuration from its first item: the others must
-// have the same one (everything agg_launch_locked reads from it).
+// have the same one (everything agg_take_locked reads from it).
 // Device copies of equal contents (the program, the CRC tables) do not
 // matter: the launch reads the first item's, which its owner keeps until
 // its own wait (and fcgpu_set_program synchronises before freeing one).
@@ -1970,18 +1973,35 @@ static hipError_t launch_rx_fn(hipFunction_t fn, int part, const RxLaunch &L, ui
     void *args[] = {const_cast<RxLaunch *>(&L)};
     return hipModuleLaunchKernel(fn, grid, 1, 1, kTile, 1, 1, 0, s, args, nullptr);
 }
-// Launch every pending submission (q.mu held): the first one with the next
-// ones of its configuration, up to kMaxFuse per launch, until none is left.
-static int agg_launch_locked(AggQueue &q) {
-    if (q.pending.empty()) return FCGPU_OK;
-    if (hipSetDevice(q.device) != hipSuccess) return FCGPU_ERUNTIME;
+// A group of pending submissions taken from the queue, to be issued by the
+// thread that took it, outside the queue's lock (a kernel launch from 16
+// threads contending for the lock serialised their submissions).
+struct AggIssue {
+    RxLaunch L;
+    int part;
+    uint32_t cm, tiles;
+    bool ck;
+    hipFunction_t fn;
+    hipStream_t st;
+    AggLaunch *al;
+};
+// Take every pending submission (q.mu held) as launches: the first one with
+// the next ones of its configuration, up to kMaxFuse per launch, until none
+// is left. Each taken submission's slot points at its launch (state
+// kAggIssuing) before the lock is released.
+static void agg_take_locked(AggQueue &q, std::vector<AggIssue> &out) {
     while (!q.pending.empty()) {
         std::vector<size_t> grp{0};
         for (size_t m = 1; m < q.pending.size() && grp.size() < kMaxFuse; ++m)
             if (agg_compatible(q.pending[0], q.pending[m])) grp.push_back(m);
         const AggItem &i0 = q.pending[0];
-        const int part = out_part(&i0.job.out);
-        RxLaunch L;
+        out.emplace_back();
+        AggIssue &is = out.back();
+        is.part = out_part(&i0.job.out);
+        is.cm = i0.cm;
+        is.ck = i0.ck;
+        is.fn = i0.fn;
+        RxLaunch &L = is.L;
         RxArgs &a = L.A;
         a = RxArgs{};    // no whole-batch partition or flow table here (agg_eligible)
         a.cfg = i0.dcfg;
@@ -2008,6 +2028,7 @@ static int agg_launch_locked(AggQueue &q) {
             J.tile0 = tiles;
             tiles += (j.n + kTile - 1) / kTile;
         }
+        is.tiles = tiles;
         L.job_tiles = (L.job[0].n + kTile - 1) / kTile;
         for (uint32_t k = 1; k < L.njobs; ++k)
             if (L.job[k].tile0 != k * L.job_tiles) L.job_tiles = 0;
@@ -2027,40 +2048,30 @@ static int agg_launch_locked(AggQueue &q) {
         a.ip_rw = J0.ip_rw;
         a.ctr = J0.ctr;
         const uint32_t si = q.rr++ % 4;
-        hipError_t e = q.st[si] ? hipSuccess : hipStreamCreateWithFlags(&q.st[si], hipStreamNonBlocking);
+        if (!q.st[si] && hipStreamCreateWithFlags(&q.st[si], hipStreamNonBlocking) != hipSuccess) {
+            (void)hipGetLastError();
+            q.st[si] = nullptr;
+        }
+        is.st = q.st[si];
         AggLaunch *al = nullptr;
         if (!q.spare.empty()) {
             al = q.spare.back();
             q.spare.pop_back();
         } else {
             al = new AggLaunch();
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&al->ev, hipEventDisableTiming);
-        }
-        if (e == hipSuccess && fault_take(FCGPU_FAULT_LAUNCH)) e = hipErrorLaunchFailure;
-        if (e == hipSuccess) {
-            if (i0.fn) {
-                e = launch_rx_fn(i0.fn, part, L, tiles, q.st[si]);
-            } else {
-                e = launch_rx_any(part, i0.cm, i0.ck, L, tiles, q.st[si], nullptr, nullptr, nullptr);
-                if (e == hipSuccess) e = hipGetLastError();
+            if (hipEventCreateWithFlags(&al->ev, hipEventDisableTiming) != hipSuccess) {
+                (void)hipGetLastError();
+                al->ev = nullptr;
             }
         }
-        if (e == hipSuccess) e = hipEventRecord(al->ev, q.st[si]);
+        al->state.store(kAggIssuing, std::memory_order_relaxed);
         al->refs = (uint32_t)grp.size();
+        is.al = al;
         for (size_t k : grp) {
             AggItem &it = q.pending[k];
-            SpanSlot &sp = it.c->span[it.slot];
-            if (e == hipSuccess) {
-                sp.al = al;
-            } else {
-                sp.agg_err = true;     // its owner's wait reports the failure
-            }
+            it.c->span[it.slot].al = al;
         }
-        if (e != hipSuccess) {
-            al->refs = 0;
-            q.spare.push_back(al);
-        }
-        // the launched submissions leave the queue, the rest keep their order
+        // the taken submissions leave the queue, the rest keep their order
         std::vector<AggItem> rest;
         rest.reserve(q.pending.size() - grp.size());
         size_t g = 0;
@@ -2069,9 +2080,28 @@ static int agg_launch_locked(AggQueue &q) {
             rest.push_back(q.pending[m]);
         }
         q.pending.swap(rest);
-        if (e != hipSuccess) return FCGPU_ERUNTIME;
     }
-    return FCGPU_OK;
+}
+// Issue taken launches (no lock held); their owners' waits see the outcome.
+static void agg_issue(int device, std::vector<AggIssue> &iss) {
+    if (iss.empty()) return;
+    const bool dev_ok = hipSetDevice(device) == hipSuccess;
+    for (AggIssue &is : iss) {
+        hipError_t e = dev_ok && is.st && is.al->ev ? hipSuccess : hipErrorInvalidValue;
+        if (e == hipSuccess && fault_take(FCGPU_FAULT_LAUNCH)) e = hipErrorLaunchFailure;
+        if (e == hipSuccess) {
+            if (is.fn) {
+                e = launch_rx_fn(is.fn, is.part, is.L, is.tiles, is.st);
+            } else {
+                e = launch_rx_any(is.part, is.cm, is.ck, is.L, is.tiles, is.st, nullptr, nullptr, nullptr);
+                if (e == hipSuccess) e = hipGetLastError();
+            }
+        }
+        if (e == hipSuccess) e = hipEventRecord(is.al->ev, is.st);
+        if (e != hipSuccess) (void)hipGetLastError();
+        is.al->state.store(e == hipSuccess ? kAggIssued : kAggFailed, std::memory_order_release);
+    }
+    iss.clear();
 }
 // The last AUTO context of a device is gone: every submission it queued was
 // waited for (fcgpu_close / fcgpu_span_mode wait or refuse busy slots), so
@@ -2100,7 +2130,7 @@ static void agg_release(int device) {
 
 // Queue one zero-copy block submission (device addresses in j). Once queued
 // the submission is the owner's to wait for: a failed launch (of its group or
-// another) is reported by that wait (agg_err), never by this call.
+// another) is reported by that wait (AggLaunch::state), never by this call.
 static int agg_submit(fcgpu_ctx *c, uint32_t slot, const fcgpu_job &j) {
     AggItem it{};
     it.c = c;
@@ -2118,47 +2148,52 @@ static int agg_submit(fcgpu_ctx *c, uint32_t slot, const fcgpu_job &j) {
         it.fn = jit_function(c, jit_key((int)it.cm, it.ck, out_part(&j.out), ip4 && c->cfg.l4_mode != FCGPU_L4_NONE,
                                         false));
     }
-    AggQueue &q = agg_queue(c->device);
+    AggQueue &q = agg_queue(c);
     SpanSlot &sp = c->span[slot];
-    std::lock_guard<std::mutex> g(q.mu);
-    q.pending.push_back(it);
-    sp.agg = true;
-    sp.agg_err = false;
-    sp.al = nullptr;
-    sp.busy = true;
-    if (q.pending.size() >= kAggLaunch) (void)agg_launch_locked(q);
+    std::vector<AggIssue> iss;
+    {
+        std::lock_guard<std::mutex> g(q.mu);
+        q.pending.push_back(it);
+        sp.agg = true;
+        sp.al = nullptr;
+        sp.busy = true;
+        if (q.pending.size() >= kAggLaunch) agg_take_locked(q, iss);
+    }
+    agg_issue(q.device, iss);
     return FCGPU_OK;
 }
 // Wait for (block = true) or poll a queued submission: launched first if
 // still pending. Returns 1 done, 0 running, < 0 error.
 static int agg_finish(fcgpu_ctx *c, uint32_t slot, bool block) {
-    AggQueue &q = agg_queue(c->device);
+    AggQueue &q = agg_queue(c);
     SpanSlot &sp = c->span[slot];
     AggLaunch *al = nullptr;
+    std::vector<AggIssue> iss;
     {
         std::lock_guard<std::mutex> g(q.mu);
-        if (!sp.al && !sp.agg_err) agg_launch_locked(q);
+        if (!sp.al) agg_take_locked(q, iss);     // still pending: it (and every other) goes now
         al = sp.al;
-        if (!al)    // not launched (a launch failed): it leaves the queue unrun
-            for (size_t m = 0; m < q.pending.size(); ++m)
-                if (q.pending[m].c == c && q.pending[m].slot == slot) {
-                    q.pending.erase(q.pending.begin() + (long)m);
-                    break;
-                }
+    }
+    agg_issue(q.device, iss);
+    // the thread that took its group issues it outside the lock
+    int st;
+    while ((st = al->state.load(std::memory_order_acquire)) == kAggIssuing) {
+        if (!block) return 0;
+        std::this_thread::yield();
     }
     hipError_t e = hipSuccess;
-    if (al) {
+    if (st == kAggIssued) {
         e = block ? wait_event(al->ev) : hipEventQuery(al->ev);
         if (!block && e == hipErrorNotReady) return 0;
     }
     {
         std::lock_guard<std::mutex> g(q.mu);
-        if (al && --al->refs == 0) q.spare.push_back(al);
+        if (--al->refs == 0) q.spare.push_back(al);
         sp.al = nullptr;
         sp.agg = false;
         sp.busy = false;
     }
-    if (!al) return fail(c, FCGPU_ERUNTIME, "shared zero-copy launch failed");
+    if (st == kAggFailed) return fail(c, FCGPU_ERUNTIME, "shared zero-copy launch failed");
     if (e != hipSuccess) {
         (void)hipGetLastError();
         return fail(c, FCGPU_ERUNTIME, std::string("shared zero-copy batch: ") + hipGetErrorString(e));

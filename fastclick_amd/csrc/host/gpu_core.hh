@@ -78,7 +78,9 @@
 //   BATCH (packets per device batch; 0: each incoming PacketBatch is one;
 //   default auto: 16384 while the batches are copied, 4096 while they are
 //   zero-copy -- many threads' batches then share the PCIe-read path, and
-//   smaller ones keep each thread's round trip short: profiles/r03_s24),
+//   smaller ones keep each thread's round trip short: profiles/archive/r03_s24.txt
+//   -- and 8192 zero-copy with COMPACT records, half the bytes per packet:
+//   profiles/r04_crossover/el_sweep2_compact.log),
 //   TIMER (us, default 100; -1 none),
 //   SLOTS (default 2): device batches a thread stages or has in flight
 //   (double or triple buffering),
@@ -694,7 +696,9 @@ class RxCore {
             int rc = fcgpu_span_submit_block(_ctx, k, s.in, s.frames_off + _lead + s.used, 0, s.frames_off, s.n, s.res,
                                              _outputs, _partition);
             // BATCH auto: the next batches' size for the path they now take
-            _eff_batch = _batch_auto && fcgpu_span_zerocopy_active(_ctx) ? kBatchZeroCopy : _batch;
+            _eff_batch = _batch_auto && fcgpu_span_zerocopy_active(_ctx)
+                             ? (_plan.compact ? kBatchZeroCopyCompact : kBatchZeroCopy)
+                             : _batch;
             if (rc != FCGPU_OK) rc = resubmit(k);
             if (rc == FCGPU_OK) s.inflight = true;
             else failed = true;
@@ -979,7 +983,10 @@ class RxCore {
     int _error_output = -1;                      // ERROR_OUTPUT (-1: kill)
     std::string _fail_msg;                       // the failure that caused the last re-submission (under _mu)
     int _device = 0;
-    static constexpr uint32_t kBatchCopy = 16384, kBatchZeroCopy = 4096;
+    // BATCH auto: packets per batch while batches are copied, while they go
+    // zero-copy, and zero-copy with compact records (half the PCIe bytes per
+    // packet: bigger batches amortise the round trip; profiles/r04_crossover)
+    static constexpr uint32_t kBatchCopy = 16384, kBatchZeroCopy = 4096, kBatchZeroCopyCompact = 8192;
     uint32_t _batch = kBatchCopy;
     bool _batch_auto = true;                     // BATCH auto (the default)
     uint32_t _eff_batch = kBatchCopy;            // packets per device batch now (BATCH auto: by the span path)
