@@ -53,6 +53,9 @@ def load():
     lib.fcclick_run_clocked.restype = C.c_int
     lib.fcclick_run_clocked.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                         C.c_void_p, C.POINTER(fcclick_result), C.c_char_p, C.c_size_t]
+    lib.fcclick_stage_compact.restype = C.c_int
+    lib.fcclick_stage_compact.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t,
+                                          C.c_void_p, C.POINTER(C.c_size_t), C.c_char_p, C.c_size_t]
     lib.fcclick_bench.restype = C.c_int
     lib.fcclick_bench.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.POINTER(C.c_double), C.c_char_p, C.c_size_t]
@@ -95,6 +98,32 @@ def parse_program(text: str):
     if lib.fcclick_parse_program(text.encode(), steps, cap, C.byref(n), C.byref(oe), err, 512) != 0:
         raise ConfigError(err.value.decode())
     return [steps[i] for i in range(n.value)], oe.value
+
+
+def stage_compact(conf: str, batch, fill=None):
+    """The element's compact staging of `batch` (include/fcclick.h
+    fcclick_stage_compact) as a Batch: frame byte b of packet i at
+    arena[desc[i, 0] + b] for every byte the chain reads; the rest of the
+    arena is `fill` (default zeros), e.g. random bytes to make sure nothing
+    outside the staged range decides anything. None when the chain stages
+    whole captures."""
+    from . import synth
+    lib = load()
+    n = batch.n
+    cap = 256 + 128 * n + synth.ARENA_PAD
+    out = np.zeros(cap, np.uint8) if fill is None else np.ascontiguousarray(fill[:cap], dtype=np.uint8).copy()
+    desc = np.zeros((n, 2), np.uint32)
+    used = C.c_size_t()
+    err = C.create_string_buffer(512)
+    arena = np.ascontiguousarray(batch.arena)
+    src = np.ascontiguousarray(batch.desc, dtype=np.uint32)
+    rc = lib.fcclick_stage_compact(conf.encode(), arena.ctypes.data, src.ctypes.data, n, out.ctypes.data, cap,
+                                   desc.ctypes.data, C.byref(used), err, 512)
+    if rc == -2:
+        return None
+    if rc != 0:
+        raise ConfigError(err.value.decode())
+    return synth.Batch(arena=out, desc=desc)
 
 
 PER_PACKET = 0xFFFFFFFF   # burst value: the source calls push(0, p) per packet (fcclick.h)

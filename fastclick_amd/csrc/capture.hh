@@ -108,4 +108,15 @@ inline uint32_t stage_end(const StagePlan &p, uint32_t offset, const uint8_t *fr
 }
 constexpr uint32_t kStageLead = 256;   // records start this far into the block (descriptor offsets >= 0)
 
+// One packet's compact record: copy cp bytes from frame + src_off; the record
+// takes the returned size (a multiple of 16, at least 16) and the packet's
+// descriptor offset is the record's offset minus p.start.
+inline uint32_t stage_record_size(const StagePlan &p, uint32_t offset, const uint8_t *frame, uint32_t len,
+                                  uint32_t &src_off, uint32_t &cp) {
+    const uint32_t end = stage_end(p, offset, frame, len);
+    cp = end > p.start ? end - p.start : 0u;
+    src_off = cp ? p.start : 0u;
+    return cp ? (cp + 15) & ~15u : 16u;
+}
+
 }  // namespace fcgpu

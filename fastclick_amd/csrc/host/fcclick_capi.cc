@@ -268,6 +268,48 @@ static int run_graph(const char *conf, const uint8_t *arena, const uint32_t *des
     return 0;
 }
 
+// The element's compact staging of a batch (capture.hh), for tests: records
+// of the bytes the configured chain reads, as RxCore stages them.
+extern "C" int fcclick_stage_compact(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                                     uint8_t *out_arena, size_t out_cap, uint32_t *out_desc, size_t *out_bytes,
+                                     char *err, size_t errcap) {
+    std::string e;
+    std::string cls;
+    std::vector<std::string> args;
+    if (!parse_element(conf, cls, args, e) || cls != "GPUIPCheckClassify") {
+        copy_err(e.empty() ? "not a GPUIPCheckClassify configuration" : e, err, errcap);
+        return -1;
+    }
+    RxCore<ModelPolicy> core;
+    if (core.configure(args, e) < 0) {
+        copy_err(e, err, errcap);
+        return -1;
+    }
+    const fcgpu_cfg &cfg = core.device_cfg();
+    const fcgpu::StagePlan plan = fcgpu::stage_plan(cfg);
+    if (!plan.compact) {
+        copy_err("this chain stages whole captures (no compact records)", err, errcap);
+        return -2;
+    }
+    size_t used = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t *f = arena + desc[2 * i];
+        const uint32_t len = desc[2 * i + 1];
+        uint32_t so, cp;
+        const uint32_t rec = fcgpu::stage_record_size(plan, (uint32_t)cfg.offset, f, len, so, cp);
+        if (fcgpu::kStageLead + used + rec > out_cap) {
+            copy_err("out_arena too small", err, errcap);
+            return -1;
+        }
+        memcpy(out_arena + fcgpu::kStageLead + used, f + so, cp);
+        out_desc[2 * i] = (uint32_t)(fcgpu::kStageLead + used) - plan.start;
+        out_desc[2 * i + 1] = len;
+        used += rec;
+    }
+    if (out_bytes) *out_bytes = fcgpu::kStageLead + used;
+    return 0;
+}
+
 extern "C" int fcclick_run(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
                            uint32_t burst, uint32_t nsinks, fcclick_result *res, char *err, size_t errcap) {
     return fcclick_run_ex(conf, arena, desc, n, burst, nsinks, 0, res, err, errcap);

@@ -655,10 +655,9 @@ class RxCore {
         size_t rec;
         if (_plan.compact) {
             // the frame bytes [start, end) the chain reads, in 16-B records
-            const uint32_t end = fcgpu::stage_end(_plan, (uint32_t)_cfg.offset, src, len);
-            cp = end > _plan.start ? end - _plan.start : 0u;
-            src += cp ? _plan.start : 0u;
-            rec = cp ? ((size_t)cp + 15) & ~(size_t)15 : 16;
+            uint32_t so;
+            rec = fcgpu::stage_record_size(_plan, (uint32_t)_cfg.offset, src, len, so, cp);
+            src += so;
         } else {
             cp = len < _capture ? len : _capture;
             rec = cp ? ((size_t)cp + 63) & ~(size_t)63 : 64;

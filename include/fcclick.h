@@ -40,6 +40,17 @@ struct fcgpu_step;
 int fcclick_parse_program(const char *text, struct fcgpu_step *steps, uint32_t cap, uint32_t *nsteps,
                           int32_t *output_everything, char *err, size_t errcap);
 
+/* The element's compact staging (COMPACT true, fastclick_amd/csrc/capture.hh)
+ * of n frames for a configuration: each frame's record holds only the bytes
+ * the chain reads, in 16-B records from out_arena + 256; out_desc[i] = (record
+ * offset - the chain's first byte, length), so frame byte b of packet i is at
+ * out_arena + out_desc[2i] + b for every byte the chain reads. For tests (the
+ * oracle on the compact layout must agree with the oracle on the frames).
+ * Returns 0, -2 when the chain stages whole captures, -1 on error. */
+int fcclick_stage_compact(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                          uint8_t *out_arena, size_t out_cap, uint32_t *out_desc, size_t *out_bytes,
+                          char *err, size_t errcap);
+
 typedef struct fcclick_result {
     uint32_t *out_port;     /* [n] output the packet left on; 0xffffffff = killed        */
     uint32_t *out_seq;      /* [n] global departure order (0..), 0xffffffff = killed     */

@@ -20,3 +20,6 @@ lib = K.load()
 mpps = K.bench_element(conf, b, burst=32, reps=40, threads=t) / 1e6
 print(json.dumps({"threads": t, "batch": batch, "mpps": round(mpps, 1)}), flush=True)
 lib.fcclick_print_cycles()
+if os.environ.get("FCGPU_LIB"):
+    from fastclick_amd import _native as N
+    N.load().fcgpu_print_cycles()

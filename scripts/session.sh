@@ -97,7 +97,10 @@ for s in "${ST[@]}"; do
     el_sweep) step el_sweep 900 bash scripts/el_sweep.sh 3 ;;
     el_sweep2) BATCHES="4096 8192 16384" SLOTS_LIST=2 step el_sweep2 900 bash scripts/el_sweep.sh 3 16 8 4 ;;
     el_spin) step el_spin 900 bash scripts/el_spin.sh 3 ;;
+    # the job's 16-CPU cgroup quota is shared with the HIP runtime's own threads
+    el_quota) step el_quota 900 bash -c 'for r in 1 2 3; do for t in 16 15 14 12; do timeout -k 5 120 python scripts/element_threads.py $t || exit $?; done; done' ;;
     el_cyc) for t in 16 8 1; do FCCLICK_LIB=scripts/mock/cyc/libfcclick.so step el_cyc$t 300 python scripts/el_cycles.py $t; done ;;
+    el_cycgpu) for t in 16 8 4 1; do FCGPU_LIB=scripts/mock/cycgpu/libfcgpu.so FCCLICK_LIB=scripts/mock/cycgpu/libfcclick.so step el_cycgpu$t 300 python scripts/el_cycles.py $t; done ;;
     el_issue) ALT=scripts/mock/old/libfcclick.so ALT_FCGPU=scripts/mock/old/libfcgpu.so step el_issue 900 bash scripts/el_ab_lib.sh 3 ;;
     el_nt) ALT=scripts/mock/nt_real/libfcclick.so step el_nt 900 bash scripts/el_ab_lib.sh 3 ;;
     # the element at 16 threads (default BATCH/ZEROCOPY/SLOTS): rate, then a kernel trace

@@ -483,19 +483,7 @@ def test_element_compact_records_match_full(oracle, conf, nsinks, zc):
     packets with IP options, every header error, non-first fragments, TCP
     frames and truncated ones, in copy and zero-copy mode."""
     from fastclick_amd import click as K
-    from tests.helpers import set_fragment
-    b = synth.c4(10_000 + 7, seed=560)
-    synth.add_ip_options(b, 0.2, seed=561)
-    synth.inject_errors(b, 0.03, seed=562)
-    set_fragment(b, 0.05, seed=563)
-    rng = np.random.default_rng(564)
-    off = b.desc[:, 0].astype(np.int64) + 14
-    tcp = rng.random(b.n) < 0.2
-    b.arena[off[tcp] + 9] = 6                          # protocol TCP: CheckTCPHeader's words differ
-    for i in np.nonzero(tcp)[0]:
-        synth._refresh_cksum(b.arena, int(off[i]))
-    short = rng.random(b.n) < 0.02
-    b.desc[short, 1] = rng.integers(0, 40, int(short.sum()))   # truncated frames
+    b = _hostile_batch(560)
     base = conf[:-1] + f", BATCH 4096, ZEROCOPY {zc}"
     full = K.run_element(base + ", COMPACT false)", b, burst=32, nsinks=nsinks)
     comp = K.run_element(base + ")", b, burst=32, nsinks=nsinks)
@@ -517,3 +505,75 @@ def test_element_compact_records_match_full(oracle, conf, nsinks, zc):
         port = e["port"].astype(np.uint32)
         inside = (e["anno"]["th"].astype(np.int64) + 4 <= b.desc[:, 1].astype(np.int64)) | ("MARK" not in conf)
         assert np.array_equal(comp["port"][inside], np.where(port < nsinks, port, 0xFFFFFFFF)[inside])
+
+
+def _hostile_batch(seed):
+    from tests.helpers import set_fragment
+    b = synth.c4(6000 + 11, seed=seed)
+    synth.add_ip_options(b, 0.2, seed=seed + 1)
+    synth.inject_errors(b, 0.03, seed=seed + 2)
+    set_fragment(b, 0.05, seed=seed + 3)
+    rng = np.random.default_rng(seed + 4)
+    off = b.desc[:, 0].astype(np.int64) + 14
+    tcp = rng.random(b.n) < 0.2
+    b.arena[off[tcp] + 9] = 6
+    for i in np.nonzero(tcp)[0]:
+        o = int(off[i])
+        th = o + (int(b.arena[o]) & 15) * 4
+        if th + 13 <= int(b.desc[i, 0]) + int(b.desc[i, 1]):
+            b.arena[th + 12] = 0x50                    # th_off 5: a well-formed TCP header
+        synth._refresh_cksum(b.arena, o)
+    short = rng.random(b.n) < 0.02
+    b.desc[short, 1] = rng.integers(0, 40, int(short.sum()))
+    return b
+
+
+@pytest.mark.parametrize("conf", [c for c, _ in COMPACT_CONFS] + [
+    "GPUIPCheckClassify(OFFSET 30, CHECKSUM true, N 5, LB_MODE hash_ip)",
+    "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, HASHSWITCH 40 30, N 3)",
+    "GPUIPCheckClassify(OFFSET 0, CHECKSUM true, N 8, LB_MODE hash)"])
+def test_compact_layout_decides_nothing_else(oracle, conf):
+    """The compact staging rule (capture.hh stage_plan / stage_end, exported
+    as fcclick_stage_compact) against the oracle on the CPU: the oracle run
+    on the compact layout -- only the bytes the chain reads, every other
+    arena byte random -- gives the verdicts, ports, hashes and annotations it
+    gives on the frames themselves, on packets with IP options, header
+    errors, fragments, TCP and truncated frames."""
+    from fastclick_amd import click as K
+    b = _hostile_batch(580)
+    if "OFFSET 0" in conf:     # IP packets without an Ethernet header
+        b = synth.from_frames([f[14:] for f in b.frames()])
+    if "OFFSET 30" in conf:    # 16 more bytes ahead of the IP header
+        b = synth.from_frames([bytes(16) + f for f in b.frames()])
+    rng = np.random.default_rng(581)
+    comp = K.stage_compact(conf, b, fill=rng.integers(0, 256, 256 + 128 * b.n + 4096, dtype=np.uint8))
+    assert comp is not None
+    cfg = K.element_cfg(conf)
+    ref = oracle.process_batch(cfg, b)
+    got = oracle.process_batch(cfg, comp)
+    ok = ref["reason"] == N.R_OK
+    defined = np.ones(b.n, bool)
+    if "MARK" in conf:       # ports / addresses past a truncated packet's end: undefined
+        ln = b.desc[:, 1].astype(np.int64)
+        defined = (ref["anno"]["th"].astype(np.int64) + 4 <= ln) & (14 + 20 <= ln)
+    assert ok.sum() > (200 if "L4" in conf else 1000)
+    for k in ("reason", "port"):
+        assert np.array_equal(got[k][defined], ref[k][defined]), k
+    both = ok & defined
+    assert np.array_equal(got["hash"][both], ref["hash"][both])
+    for f in ("dst_ip", "length", "nh", "th"):
+        assert np.array_equal(got["anno"][f][both], ref["anno"][f][both]), f
+    if cfg.rewrite:
+        assert np.array_equal(got["ip_rw"][ok], ref["ip_rw"][ok])
+    # and the layout is compact: 16-B records, far below the 64-B slots
+    steps = np.diff(np.sort(comp.desc[:, 0].astype(np.int64)))
+    assert (steps % 16 == 0).all() and np.median(steps) <= 48
+
+
+def test_compact_layout_not_for_whole_captures():
+    from fastclick_amd import click as K
+    b = synth.c4(100, seed=590)
+    for conf in ("GPUIPCheckClassify(MODE AUTO, N 2, LB_MODE hash)",
+                 "GPUIPCheckClassify(OFFSET 14, N 2, L4 UDP)",
+                 "GPUIPCheckClassify(OFFSET 14, N 2, PROGRAM \" 0 265/11000000%ff000000  yes->[0]  no->[1]\")"):
+        assert K.stage_compact(conf, b) is None
