@@ -53,9 +53,10 @@ def load():
     lib.fcclick_run_clocked.restype = C.c_int
     lib.fcclick_run_clocked.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                         C.c_void_p, C.POINTER(fcclick_result), C.c_char_p, C.c_size_t]
-    lib.fcclick_stage_compact.restype = C.c_int
-    lib.fcclick_stage_compact.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t,
-                                          C.c_void_p, C.POINTER(C.c_size_t), C.c_char_p, C.c_size_t]
+    if hasattr(lib, "fcclick_stage_compact"):      # absent from older A/B builds of the harness
+        lib.fcclick_stage_compact.restype = C.c_int
+        lib.fcclick_stage_compact.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                              C.c_size_t, C.c_void_p, C.POINTER(C.c_size_t), C.c_char_p, C.c_size_t]
     lib.fcclick_bench.restype = C.c_int
     lib.fcclick_bench.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.POINTER(C.c_double), C.c_char_p, C.c_size_t]
