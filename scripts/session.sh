@@ -91,7 +91,7 @@ for s in "${ST[@]}"; do
              kt kt_flow_c3 300 --steps 200 --warmup 20 --no-cpu --workload c3 --flow-capacity 20000 &&
              kt kt_flow_c4 300 --steps 200 --warmup 20 --no-cpu --workload c4 --flow-capacity 2000000 ;;
     latency) step latency 120 python scripts/latency_probe.py ;;
-    crossover) step crossover 1100 python -u scripts/crossover.py ;;
+    crossover) step crossover 1000 python -u scripts/crossover.py ;;
     crossover16) step crossover16 600 python -u scripts/crossover.py --threads 8,16 --no-cpu ;;
     mock_ab) step mock_ab 600 bash scripts/mock_ab_box.sh ;;
     el_sweep) step el_sweep 900 bash scripts/el_sweep.sh 3 ;;
@@ -99,6 +99,8 @@ for s in "${ST[@]}"; do
     el_spin) step el_spin 900 bash scripts/el_spin.sh 3 ;;
     # the job's 16-CPU cgroup quota is shared with the HIP runtime's own threads
     el_quota) step el_quota 900 bash -c 'for r in 1 2 3; do for t in 16 15 14 12; do timeout -k 5 120 python scripts/element_threads.py $t || exit $?; done; done' ;;
+    # the element's defaults at 1-16 threads, two interleaved rounds
+    el_default) step el_default 600 bash -c 'for r in 1 2; do for t in 1 2 4 8 12 16; do timeout -k 5 120 python scripts/element_threads.py $t || exit $?; done; done' ;;
     el_cyc) for t in 16 8 1; do FCCLICK_LIB=scripts/mock/cyc/libfcclick.so step el_cyc$t 300 python scripts/el_cycles.py $t; done ;;
     el_cycgpu) for t in 16 8 4 1; do FCGPU_LIB=scripts/mock/cycgpu/libfcgpu.so FCCLICK_LIB=scripts/mock/cycgpu/libfcclick.so step el_cycgpu$t 300 python scripts/el_cycles.py $t; done ;;
     el_issue) ALT=scripts/mock/old/libfcclick.so ALT_FCGPU=scripts/mock/old/libfcgpu.so step el_issue 900 bash scripts/el_ab_lib.sh 3 ;;
