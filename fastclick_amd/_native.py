@@ -15,7 +15,7 @@ LIBFCGPU = os.environ.get("FCGPU_LIB") or os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 18
+ABI_VERSION = 19
 SPAN_SLOTS = 3
 SPAN_COPY = 0
 SPAN_ZEROCOPY = 1
@@ -228,6 +228,12 @@ FCGPU_SYMBOLS = {
     "fcgpu_set_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "fcgpu_read_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint32),
                                     C.c_int]),
+    "fcgpu_exchange_plan": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                      C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "fcgpu_exchange_pack": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p]),
+    "fcgpu_exchange_unpack": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64), C.c_uint32,
+                                        C.c_void_p, C.c_void_p]),
     "fcgpu_last_error": (C.c_char_p, [C.c_void_p]),
 }
 
@@ -493,6 +499,22 @@ class Context:
         cnt = (C.c_uint32 * 3)()
         self._chk(self.lib.fcgpu_read_timing(self.h, ms, cnt, 3), "fcgpu_read_timing")
         return list(ms), list(cnt)
+
+    def exchange_plan(self, desc, perm, port_start, n, world, rank, meta, seg_bytes, stream=0):
+        """fcgpu_exchange_plan on device pointers (flow re-shard, one record per leaving packet)."""
+        self._chk(self.lib.fcgpu_exchange_plan(self.h, desc, perm, port_start, n, world, rank, meta, seg_bytes,
+                                               stream or None), "fcgpu_exchange_plan")
+
+    def exchange_pack(self, arena, desc, port_start, meta, seg_bytes, n, world, send, send_cap, stream=0):
+        """fcgpu_exchange_pack: the leaving frames into their owners' segments of send."""
+        self._chk(self.lib.fcgpu_exchange_pack(self.h, arena, desc, port_start, meta, seg_bytes, n, world,
+                                               send or None, send_cap, stream or None), "fcgpu_exchange_pack")
+
+    def exchange_unpack(self, meta, n, src_displ, desc, stream=0):
+        """fcgpu_exchange_unpack: received records -> descriptors (src_displ: per-source segment starts)."""
+        arr = (C.c_uint64 * max(len(src_displ), 1))(*[int(x) for x in src_displ])
+        self._chk(self.lib.fcgpu_exchange_unpack(self.h, meta, n, arr, len(src_displ), desc, stream or None),
+                  "fcgpu_exchange_unpack")
 
     def close(self):
         if getattr(self, "h", None):

@@ -44,6 +44,7 @@
 
 #include "fcgpu_device.hh"
 #include "fcgpu_flow.hh"
+#include "fcgpu_exchange.hh"
 #include "capture.hh"
 #include "prog_jit.hh"
 #include "jit_sources.inc"   // kJitDeviceHh, kJitAbiH (fastclick_amd/build.py)
@@ -278,6 +279,8 @@ struct fcgpu_ctx {
     uint64_t timing_seq = 0;
     std::vector<EvPair> pending;
     std::vector<hipEvent_t> free_ev;
+    // flow re-shard plan (fcgpu_exchange_plan): block sums and segment starts
+    unsigned long long *x_bsum = nullptr, *x_base = nullptr;
     std::string err;
 };
 
@@ -979,6 +982,8 @@ void fcgpu_close(fcgpu_ctx *c) {
         flow_free(c);
         hipFree(c->d_mptr);
         hipFree(c->d_mdesc);
+        hipFree(c->x_bsum);
+        hipFree(c->x_base);
         pool_release(c);
         for (auto e : c->flow_order)
             if (e) hipEventDestroy(e);
@@ -2766,6 +2771,85 @@ int fcgpu_read_timing(fcgpu_ctx *c, double *ms, uint32_t *launches, int nstages)
         if (ms) ms[k] = acc[k];
         if (launches) launches[k] = cnt[k];
     }
+    return FCGPU_OK;
+}
+
+// ---- flow re-shard across GPUs (fcgpu_exchange.hh) ---------------------------
+int fcgpu_exchange_plan(fcgpu_ctx *c, const uint32_t *d_desc, const uint32_t *d_perm, const uint32_t *d_port_start,
+                        uint32_t n, uint32_t world, uint32_t rank, fcgpu_xmeta *d_meta, uint64_t *d_seg_bytes,
+                        void *stream) {
+    if (!c) return FCGPU_EINVAL;
+    if (world == 0 || world > FCGPU_MAX_PORTS) return fail(c, FCGPU_EINVAL, "fcgpu_exchange_plan: world must be 1..64");
+    if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "fcgpu_exchange_plan: batch larger than the context's max_batch");
+    if (!d_port_start || !d_seg_bytes || (n && (!d_desc || !d_perm || !d_meta)))
+        return fail(c, FCGPU_EINVAL, "fcgpu_exchange_plan: null buffer");
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint32_t nblk_max = (c->max_batch + kXItems - 1) / kXItems;
+    if (!c->x_bsum) {
+        HIPCHK(c, hipMalloc(&c->x_bsum, sizeof(unsigned long long) * (nblk_max + 1)));
+        HIPCHK(c, hipMalloc(&c->x_base, sizeof(unsigned long long) * (FCGPU_MAX_PORTS + 1)));
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    XPlan P{};
+    P.desc = d_desc;
+    P.perm = d_perm;
+    P.port_start = d_port_start;
+    P.n = n;
+    P.world = world;
+    P.rank = rank;
+    P.nblk = (n + kXItems - 1) / kXItems;
+    P.meta = reinterpret_cast<uint4 *>(d_meta);
+    P.bsum = c->x_bsum;
+    P.base = c->x_base;
+    P.seg_bytes = reinterpret_cast<unsigned long long *>(d_seg_bytes);
+    if (P.nblk) hipLaunchKernelGGL(k_xsum, dim3(P.nblk), dim3(kXThreads), 0, s, P);
+    hipLaunchKernelGGL(k_xscan, dim3(1), dim3(1024), 0, s, P);
+    if (P.nblk) hipLaunchKernelGGL(k_xmeta, dim3(P.nblk), dim3(kXThreads), 0, s, P);
+    HIPCHK(c, hipGetLastError());
+    return FCGPU_OK;
+}
+
+int fcgpu_exchange_pack(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, const uint32_t *d_port_start,
+                        const fcgpu_xmeta *d_meta, const uint64_t *d_seg_bytes, uint32_t n, uint32_t world,
+                        uint8_t *d_send, uint64_t send_cap, void *stream) {
+    if (!c) return FCGPU_EINVAL;
+    if (world == 0 || world > FCGPU_MAX_PORTS) return fail(c, FCGPU_EINVAL, "fcgpu_exchange_pack: world must be 1..64");
+    if (!d_port_start || !d_seg_bytes || (n && (!d_arena || !d_desc || !d_meta || (send_cap && !d_send))))
+        return fail(c, FCGPU_EINVAL, "fcgpu_exchange_pack: null buffer");
+    if (n == 0) return FCGPU_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    XPack X{};
+    X.arena = d_arena;
+    X.desc = d_desc;
+    X.port_start = d_port_start;
+    X.meta = reinterpret_cast<const uint4 *>(d_meta);
+    X.seg_bytes = reinterpret_cast<const unsigned long long *>(d_seg_bytes);
+    X.send = d_send;
+    X.send_cap = send_cap;
+    X.n = n;
+    X.world = world;
+    hipLaunchKernelGGL(k_xpack, dim3((n + kXFramesPerBlock - 1) / kXFramesPerBlock), dim3(kXThreads), 0,
+                       static_cast<hipStream_t>(stream), X);
+    HIPCHK(c, hipGetLastError());
+    return FCGPU_OK;
+}
+
+int fcgpu_exchange_unpack(fcgpu_ctx *c, const fcgpu_xmeta *d_meta, uint32_t n, const uint64_t *src_displ,
+                          uint32_t world, uint32_t *d_desc, void *stream) {
+    if (!c) return FCGPU_EINVAL;
+    if (world == 0 || world > FCGPU_MAX_PORTS) return fail(c, FCGPU_EINVAL, "fcgpu_exchange_unpack: world must be 1..64");
+    if (!src_displ || (n && (!d_meta || !d_desc))) return fail(c, FCGPU_EINVAL, "fcgpu_exchange_unpack: null buffer");
+    if (n == 0) return FCGPU_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    XUnpack U{};
+    U.meta = reinterpret_cast<const uint4 *>(d_meta);
+    U.desc = d_desc;
+    U.n = n;
+    U.world = world;
+    for (uint32_t r = 0; r < world; ++r) U.displ[r] = src_displ[r];
+    hipLaunchKernelGGL(k_xunpack, dim3((n + kXThreads - 1) / kXThreads), dim3(kXThreads), 0,
+                       static_cast<hipStream_t>(stream), U);
+    HIPCHK(c, hipGetLastError());
     return FCGPU_OK;
 }
 

@@ -136,3 +136,48 @@ def process_batches(batches, cfg, *, anno=True, perm=True, device_index=0, parti
         finally:
             ctx.close()
     return res
+
+
+def exchange_pack(ctx: N.Context, arena, desc, perm, port_start, world, rank, stream=None):
+    """The send side of the flow re-shard (fcgpu_exchange_plan + _pack, HIP):
+    perm / port_start from a device pass with LB_MODE hash over `world`
+    outputs and the whole-batch partition. Returns (send, meta, seg_n,
+    seg_bytes): the send buffer (followed by ARENA_PAD zero bytes, so at world
+    1 it is the received arena as is), the int32 [m, 4] fcgpu_xmeta records of
+    the m leaving packets in owner order, and per owner its packet and byte
+    counts (host lists: the all-to-all's split sizes). One host sync, for
+    those counts."""
+    torch = _torch()
+    from .dist import ARENA_PAD
+    n = int(desc.shape[0])
+    dev = desc.device
+    s = stream if stream is not None else torch.cuda.current_stream()
+    meta = torch.empty((max(n, 1), 4), dtype=torch.int32, device=dev)
+    seg = torch.empty(world, dtype=torch.int64, device=dev)
+    ctx.exchange_plan(desc.data_ptr(), perm.data_ptr(), port_start.data_ptr(), n, world, rank,
+                      meta.data_ptr(), seg.data_ptr(), stream=s.cuda_stream)
+    with torch.cuda.stream(s):
+        host = torch.cat([port_start[:world + 1].to(torch.int64), seg]).cpu()
+    ps = host[:world + 1].tolist()
+    seg_bytes = host[world + 1:].tolist()
+    m = min(ps[world], n)
+    seg_n = [min(ps[d + 1], m) - min(ps[d], m) for d in range(world)]
+    total = int(sum(seg_bytes))
+    send = torch.empty(total + ARENA_PAD, dtype=torch.uint8, device=dev)
+    with torch.cuda.stream(s):
+        send[total:].zero_()
+    ctx.exchange_pack(arena.data_ptr(), desc.data_ptr(), port_start.data_ptr(), meta.data_ptr(), seg.data_ptr(),
+                      n, world, send.data_ptr(), total, stream=s.cuda_stream)
+    return send, meta[:m], seg_n, seg_bytes
+
+
+def exchange_unpack(ctx: N.Context, meta, src_displ, stream=None):
+    """The receive side (fcgpu_exchange_unpack, HIP): records -> int32 [k, 2]
+    descriptors (uint32 bit patterns) into the received buffer, whose source r
+    segment starts at src_displ[r]."""
+    torch = _torch()
+    k = int(meta.shape[0])
+    s = stream if stream is not None else torch.cuda.current_stream()
+    desc = torch.empty((max(k, 1), 2), dtype=torch.int32, device=meta.device)
+    ctx.exchange_unpack(meta.data_ptr() if k else 0, k, src_displ, desc.data_ptr(), stream=s.cuda_stream)
+    return desc[:k]

@@ -15,8 +15,11 @@ With a flow table (fcgpu_flow_enable) the path is stateful per flow. FastClick
 keeps one flow table per core and relies on the NIC's RSS hash to send every
 packet of a flow to the same core. The GPU analogue:
 batches whose packets arrive on any GPU are re-sharded by flow first.
-`exchange_by_flow` moves each packet to the rank its flow hash names, with one
-RCCL all-to-all of counts and one of frame bytes over xGMI. Every flow then
+`exchange_by_flow` moves each packet to the rank its flow hash names: HIP
+kernels pack the leaving frames by owner and write a 16-B record per packet
+(fcgpu_exchange_plan / _pack), RCCL all-to-alls move the counts, the records
+and the frame bytes over xGMI, and a HIP kernel turns the received records
+into descriptors (fcgpu_exchange_unpack). Every flow then
 lives in exactly one rank's table. The owner of a packet is the device
 classifier's output with LB_MODE hash over `world` outputs: the
 FlowSwitch/LoadBalancer formula on the IPFlowID hash, a function of the
@@ -73,85 +76,67 @@ def output_offsets(local_counts, group=None, force=False):
     return before, stacked.sum(0)
 
 
-def exchange_by_flow(arena, desc, owner, group=None):
-    """Re-shard one rank's packets by owner rank (an all-to-all over `group`).
-
-    arena: uint8 tensor of frame bytes; desc: int32 [n, 2] (offset, length)
-    into it; owner: int64 [n], the destination rank of each packet (-1 keeps
-    nothing: the packet is dropped here, e.g. one that failed the checks).
-    Returns (arena_recv, desc_recv, src): the frames this rank now owns,
-    packed back to back in (source rank, source index) order and followed by
-    ARENA_PAD zero bytes (the header-window over-read the ABI allows), their
-    descriptors (uint32 offset/length bit patterns in int32), and
-    src = source_rank << 32 | source_index per packet. The frames keep their
-    bytes and lengths exactly.
-    """
+def exchange_segments(send, meta, seg_n, seg_bytes, group=None):
+    """The all-to-all of the flow re-shard: every rank sends owner d's records
+    (meta rows) and frame bytes (its segment of `send`) to rank d. send ends
+    with ARENA_PAD zero bytes; meta is an int32 [m, 4] tensor of fcgpu_xmeta
+    records; seg_n / seg_bytes are host lists of per-owner packet and byte
+    counts. Returns (buffer, meta, src_displ): the received segments
+    concatenated in source-rank order and followed by ARENA_PAD zero bytes
+    (the ABI's header-window over-read), their records, and where each
+    source's segment starts. Plumbing only (torch.distributed: RCCL over xGMI
+    on GPUs, gloo in CPU tests); the records and bytes are built and read by
+    the HIP kernels (fastclick_amd.device.exchange_pack / exchange_unpack)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
-    rank = dist.get_rank(group) if world > 1 else 0
-    dev = arena.device
-    owner = owner.to(torch.int64)
-    if owner.numel() and int(owner.max()) >= world:
-        raise ValueError(f"owner rank {int(owner.max())} outside a world of {world}")
-    keep = owner >= 0
-    idx = torch.nonzero(keep).flatten()
-    dst = owner[idx]
-    order = idx[torch.argsort(dst, stable=True)]             # packets grouped by destination
-    off = desc[order, 0].to(torch.int64) & 0xFFFFFFFF
-    ln = desc[order, 1].to(torch.int64) & 0xFFFFFFFF
-    send_n = torch.bincount(owner[order], minlength=world)
-    payload = _gather_frames(arena, off, ln)
-    send_b = torch.zeros(world, dtype=torch.int64, device=dev).index_add_(0, owner[order], ln)
-    meta = torch.stack([ln, (rank << 32) | order], 1)        # [m, 2] length, source tag
+    if len(seg_n) != world or len(seg_bytes) != world:
+        raise ValueError(f"{len(seg_n)} segments for a world of {world}")
     if world == 1:
-        recv_n, recv_b, rmeta, rpay = send_n, send_b, meta, payload
-    else:
-        cnt = torch.stack([send_n, send_b], 1).contiguous()
-        rcnt = torch.empty_like(cnt)
-        dist.all_to_all_single(rcnt, cnt, group=group)       # [world, 2] from every rank
-        recv_n, recv_b = rcnt[:, 0], rcnt[:, 1]
-        sn, rn = send_n.tolist(), recv_n.tolist()
-        rmeta = torch.empty(int(sum(rn)), 2, dtype=torch.int64, device=dev)
-        dist.all_to_all_single(rmeta, meta.contiguous(), rn, sn, group=group)
-        rpay = torch.empty(int(recv_b.sum()), dtype=torch.uint8, device=dev)
-        dist.all_to_all_single(rpay, payload.contiguous(), recv_b.tolist(), send_b.tolist(), group=group)
-    rlen = rmeta[:, 0]
-    roff = torch.cumsum(rlen, 0) - rlen
-    if rpay.numel() >= (1 << 32) - ARENA_PAD:
+        return send, meta, [0]
+    dev = send.device
+    cnt = torch.tensor([[int(a), int(b)] for a, b in zip(seg_n, seg_bytes)], dtype=torch.int64, device=dev)
+    rcnt = torch.empty_like(cnt)
+    dist.all_to_all_single(rcnt, cnt, group=group)           # [world, 2] from every rank
+    rc = rcnt.cpu().tolist()
+    rn, rb = [r[0] for r in rc], [r[1] for r in rc]
+    total = int(sum(rb))
+    if total + ARENA_PAD >= 1 << 32:
         raise ValueError("received frames exceed the 4 GiB a uint32 descriptor offset addresses")
-    # the ABI's over-read contract (include/fastclick_gpu.h): the arena stays
-    # readable 128 B past every frame start and 16 B past every frame end
-    arena_recv = torch.zeros(rpay.numel() + ARENA_PAD, dtype=torch.uint8, device=dev)
-    arena_recv[:rpay.numel()] = rpay
-    # offsets/lengths are uint32 bit patterns in an int32 tensor (DeviceBatch layout)
-    desc_recv = torch.stack([roff, rlen], 1).to(torch.int64)
-    desc_recv = torch.where(desc_recv >= (1 << 31), desc_recv - (1 << 32), desc_recv).to(torch.int32)
-    return arena_recv, desc_recv, rmeta[:, 1]
+    rmeta = torch.empty((int(sum(rn)), 4), dtype=torch.int32, device=dev)
+    dist.all_to_all_single(rmeta, meta.contiguous(), rn, [int(x) for x in seg_n], group=group)
+    buf = torch.empty(total + ARENA_PAD, dtype=torch.uint8, device=dev)
+    buf[total:].zero_()
+    sent = int(sum(seg_bytes))
+    dist.all_to_all_single(buf[:total], send[:sent], rb, [int(x) for x in seg_bytes], group=group)
+    displ, at = [], 0
+    for b in rb:
+        displ.append(at)
+        at += b
+    return buf, rmeta, displ
 
 
-def _gather_frames(arena, off, ln, chunk_bytes=1 << 24):
-    """Frames [off[k], off[k] + ln[k]) of arena, back to back. Gathers in
-    chunks of whole frames of about chunk_bytes, so the int64 byte index
-    never exceeds ~8 x chunk_bytes of temporary memory."""
+def exchange_by_flow(ctx, arena, desc, perm, port_start, group=None):
+    """Re-shard this rank's device batch by owner rank (one all-to-all).
+
+    ctx: a fastclick_amd._native.Context on this rank's GPU; arena / desc: the
+    batch (uint8 tensor; int32 [n, 2] uint32 bit patterns); perm / port_start:
+    the whole-batch partition of the device pass that named every packet's
+    owner (LB_MODE hash over `world` outputs; the invalid list, output
+    `world`, stays here). Returns (arena_recv, desc_recv, src): the frames this
+    rank now owns, in (source rank, source index) order, each at a 4-B aligned
+    offset with its bytes and length exact, the buffer followed by ARENA_PAD
+    zero bytes; their descriptors; src = source_rank << 32 | source_index.
+    Pack and unpack are HIP kernels (fcgpu_exchange_*); there is no CPU path."""
     import torch
-    total = int(ln.sum()) if ln.numel() else 0
-    out = torch.empty(total, dtype=torch.uint8, device=arena.device)
-    if total == 0:
-        return out
-    ends = torch.cumsum(ln, 0)
-    starts = ends - ln
-    bounds = [0]
-    if total > chunk_bytes:
-        cut = torch.searchsorted(ends, torch.arange(chunk_bytes, total, chunk_bytes, device=ln.device))
-        bounds += sorted(set(int(c) + 1 for c in cut.tolist()))
-    if bounds[-1] != ln.numel():
-        bounds.append(ln.numel())
-    for a, b in zip(bounds[:-1], bounds[1:]):
-        if b <= a:
-            continue
-        o, l, s0 = off[a:b], ln[a:b], int(starts[a])
-        m = int(l.sum())
-        pos = torch.arange(m, device=arena.device) - torch.repeat_interleave(starts[a:b] - s0, l)
-        out[s0:s0 + m] = arena[torch.repeat_interleave(o, l) + pos]
-    return out
+    import torch.distributed as dist
+    from . import device as DV
+    if not arena.is_cuda:
+        raise RuntimeError("exchange_by_flow runs on device tensors (fcgpu_exchange_*)")
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    rank = dist.get_rank(group) if world > 1 else 0
+    send, meta, seg_n, seg_bytes = DV.exchange_pack(ctx, arena, desc, perm, port_start, world, rank)
+    buf, rmeta, displ = exchange_segments(send, meta, seg_n, seg_bytes, group=group)
+    desc_recv = DV.exchange_unpack(ctx, rmeta, displ)
+    src = rmeta[:, 2:4].contiguous().view(torch.int64).flatten()
+    return buf, desc_recv, src

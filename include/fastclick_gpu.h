@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 18
+#define FCGPU_ABI_VERSION 19
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -616,6 +616,54 @@ int  fcgpu_use_counters(fcgpu_ctx *ctx, uint64_t *d_counters);
  * since the last read, and resets them. Synchronises the context stream. */
 int  fcgpu_set_timing(fcgpu_ctx *ctx, int every);
 int  fcgpu_read_timing(fcgpu_ctx *ctx, double *ms, uint32_t *launches, int nstages);
+
+/* Flow re-shard across GPUs (SURVEY 8(f) #1 over 8(e)). FastClick keeps one
+ * flow table per core and relies on the NIC's RSS hash to send every packet
+ * of a flow to one core (VirtualFlowManagerIMP::process,
+ * include/click/flow/virtualflowmanager.hh:249-330; FlowIPManagerHMP,
+ * elements/flow/flowipmanagerhmp.cc:101-117). When packets reach the GPUs
+ * unsharded, each rank's device pass (fcgpu_process with FCGPU_CLS_LB_HASH
+ * over nports = world outputs and FCGPU_PART_GLOBAL: perm + port_start) names
+ * every packet's owner rank, and these calls build and read the buffers of
+ * one all-to-all (RCCL over xGMI) that moves each packet to its owner:
+ *
+ *   fcgpu_exchange_plan   perm[0 .. port_start[world]) -- the packets that
+ *       leave (output `world`, the invalid list, stays) -- gets one
+ *       fcgpu_xmeta record each, in perm order; d_seg_bytes[d] = the bytes of
+ *       owner d's segment of the send buffer. Each frame takes a 4-B aligned
+ *       slot of (length + 3) & ~3 bytes. Segments follow in owner order.
+ *   fcgpu_exchange_pack   the frames into d_send (at least the sum of
+ *       d_seg_bytes; nothing is written past send_cap): owner d's segment
+ *       holds its packets in input order; slot bytes past a frame's length
+ *       are zero.
+ *   (the caller's all-to-all: records and segments; a receiver concatenates
+ *    the segments it gets in source-rank order)
+ *   fcgpu_exchange_unpack the received records -> descriptors into the
+ *       received buffer: desc[2j] = src_displ[record.src_rank] + record.off,
+ *       desc[2j+1] = record.length, where src_displ[r] is where source r's
+ *       segment starts in that buffer (host array of `world` values). The
+ *       offsets must fit in 32 bits; the receiver keeps the ABI's over-read
+ *       slack (128 B past every frame start, 16 B past every frame end)
+ *       readable after its buffer.
+ * The frames keep their bytes and lengths exactly; the records carry each
+ * packet's source (rank, index), so the receiver's order is (source rank,
+ * source index). world <= FCGPU_MAX_PORTS; n <= the context's max_batch for
+ * the plan. Asynchronous on `stream` (plan needs the context's scratch: one
+ * plan at a time per context). */
+typedef struct fcgpu_xmeta {
+    uint32_t off;             /* the frame's slot within its owner's segment             */
+    uint32_t length;          /* frame length                                            */
+    uint32_t src_index;       /* index in the source rank's batch                        */
+    uint32_t src_rank;        /* source rank (bytes 8..15 = src_rank << 32 | src_index)  */
+} fcgpu_xmeta;
+int  fcgpu_exchange_plan(fcgpu_ctx *ctx, const uint32_t *d_desc, const uint32_t *d_perm,
+                         const uint32_t *d_port_start, uint32_t n, uint32_t world, uint32_t rank,
+                         fcgpu_xmeta *d_meta, uint64_t *d_seg_bytes, void *stream);
+int  fcgpu_exchange_pack(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_desc,
+                         const uint32_t *d_port_start, const fcgpu_xmeta *d_meta, const uint64_t *d_seg_bytes,
+                         uint32_t n, uint32_t world, uint8_t *d_send, uint64_t send_cap, void *stream);
+int  fcgpu_exchange_unpack(fcgpu_ctx *ctx, const fcgpu_xmeta *d_meta, uint32_t n, const uint64_t *src_displ,
+                           uint32_t world, uint32_t *d_desc, void *stream);
 
 const char *fcgpu_last_error(fcgpu_ctx *ctx);   /* ctx may be NULL (open errors) */
 

@@ -99,6 +99,10 @@ for s in "${ST[@]}"; do
     el_spin) step el_spin 900 bash scripts/el_spin.sh 3 ;;
     # the job's 16-CPU cgroup quota is shared with the HIP runtime's own threads
     el_quota) step el_quota 900 bash -c 'for r in 1 2 3; do for t in 16 15 14 12; do timeout -k 5 120 python scripts/element_threads.py $t || exit $?; done; done' ;;
+    # the flow re-shard kernels: GPU tests, rates, kernel trace
+    exchange) step pytest_exchange 600 python -u -m pytest tests/test_exchange.py tests/test_dist.py -m gpu -x -v --timeout 120 --timeout-method thread &&
+              step exchange_rate 300 python scripts/exchange_rate.py &&
+              step kt_exchange 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_kt_exchange -o run -- python3 scripts/exchange_rate.py --reps 20 ;;
     # the element's defaults at 1-16 threads, two interleaved rounds
     el_default) step el_default 600 bash -c 'for r in 1 2; do for t in 1 2 4 8 12 16; do timeout -k 5 120 python scripts/element_threads.py $t || exit $?; done; done' ;;
     el_cyc) for t in 16 8 1; do FCCLICK_LIB=scripts/mock/cyc/libfcclick.so step el_cyc$t 300 python scripts/el_cycles.py $t; done ;;

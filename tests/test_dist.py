@@ -101,18 +101,25 @@ def _flow_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from oracle import oracle as O
+        from oracle import exchange as X
         b = _flow_batch()
         lo, hi = D.shard_range(b.n, world, rank)
         shard = synth.Batch(arena=b.arena, desc=np.ascontiguousarray(b.desc[lo:hi]))
         r = O.process_batch(_owner_cfg(world), shard)      # stands in for the device pass
-        owner = torch.from_numpy(np.where(r["reason"] == N.R_OK, r["port"].astype(np.int64), -1))
-        arena, desc, src = D.exchange_by_flow(torch.from_numpy(shard.arena), torch.from_numpy(
-            shard.desc.view(np.int32)), owner)
+        perm, ps = X.partition(np.where(r["reason"] == N.R_OK, r["port"].astype(np.int64), -1), world)
+        meta, seg = X.plan(shard.desc, perm, ps, world, rank)   # ... and for the HIP pack
+        send = np.concatenate([X.pack(shard.arena, shard.desc, meta, ps, seg, world),
+                               np.zeros(D.ARENA_PAD, np.uint8)])
+        seg_n = [int(ps[d + 1]) - int(ps[d]) for d in range(world)]
+        buf, rmeta, displ = D.exchange_segments(torch.from_numpy(send), torch.from_numpy(meta.view(np.int32)),
+                                                seg_n, [int(x) for x in seg], group=None)
+        rmeta = rmeta.numpy().view(np.uint32)
+        desc = X.unpack(rmeta, displ)
+        src = rmeta[:, 2:4].copy().view(np.int64).ravel()
         # the global packet index of each received packet: its source shard's lo + index
-        src = src.numpy()
         g = np.array([D.shard_range(b.n, world, int(s >> 32))[0] + int(s & 0xFFFFFFFF) for s in src],
                      dtype=np.int64)
-        q.put((rank, arena.numpy(), desc.numpy().view(np.uint32), g))
+        q.put((rank, buf.numpy(), desc, g))
     finally:
         dist.destroy_process_group()
 
@@ -120,7 +127,9 @@ def _flow_worker(rank, world, port, q):
 @pytest.mark.timeout(300)
 def test_two_rank_exchange_by_flow(oracle):
     """Packets of one 6k-packet batch, split over 2 ranks, are re-sharded by
-    the flow hash with fastclick_amd.dist.exchange_by_flow (gloo all-to-all):
+    the flow hash: the records and send buffers the HIP kernels build (their
+numpy restatement, oracle/exchange.py, stands in on the CPU) go through
+fastclick_amd.dist.exchange_segments (gloo all-to-all):
     every valid packet lands exactly once, on the rank its flow hash names,
     with its frame bytes intact and in source order; each rank's flow table
     then sees whole flows (IDs from per-rank tables are in order of first
@@ -161,48 +170,70 @@ def test_two_rank_exchange_by_flow(oracle):
 
 @pytest.mark.gpu
 def test_gpu_exchange_pack_and_flow_table(oracle):
-    """The device half of the flow re-sharding at world size 1: the owner pass
-    (LB_MODE hash over 2 ranks on the IPFlowID hash) runs on the GPU and
-    matches the oracle; exchange_by_flow packs rank 0's packets from CUDA
-    tensors (the all-to-all itself is covered by the 2-rank gloo test); the
-    flow table over the packed batch gives the oracle's IDs."""
+    """The device path of the flow re-sharding at world size 1: the owner pass
+    (LB_MODE hash over 2 ranks on the IPFlowID hash, whole-batch partition)
+    runs on the GPU and matches the oracle; exchange_by_flow packs the packets
+    owned by rank 0 with the HIP kernels; the flow table over the received
+    batch gives the oracle's IDs."""
     from fastclick_amd import device
-    from fastclick_amd.device import DeviceBatch
+    from fastclick_amd.device import DeviceBatch, DeviceOutputs
     b = _flow_batch()
-    cfg = _owner_cfg(2)
-    got = device.process_batch(b, cfg, anno=False, perm=False, partition=N.PART_TILE)
-    exp = oracle.process_batch(cfg, b)
-    assert np.array_equal(got["port"], exp["port"])
-    db = DeviceBatch.upload(b, device="cuda:0")
-    port = torch.from_numpy(got["port"].astype(np.int64)).cuda()
-    ok = torch.from_numpy(got["reason"] == N.R_OK).cuda()
-    owner = torch.where(ok & (port == 0), torch.zeros_like(port), torch.full_like(port, -1))
-    arena, desc, src = D.exchange_by_flow(db.arena, db.desc, owner)
-    g = src.cpu().numpy() & 0xFFFFFFFF
-    want = np.nonzero((exp["reason"] == N.R_OK) & (exp["port"] == 0))[0]
-    assert np.array_equal(g, want)
+    cfg = N.make_cfg(offset=14, checksum=True, hash_mode=N.HASH_FLOWID, classify=N.CLS_LB_HASH, nports=1)
+    exp2 = oracle.process_batch(_owner_cfg(2), b)
+    # world 1: the owner pass names output 0 for every valid packet
+    ctx = N.Context(0, b.n, cfg)
+    try:
+        db = DeviceBatch.upload(b, device="cuda:0")
+        outs = DeviceOutputs(b.n, 1, device="cuda:0", perm=True, port_start=True, partition=N.PART_GLOBAL)
+        device.run_device(ctx, db, outs)
+        arena, desc, src = D.exchange_by_flow(ctx, db.arena, db.desc, outs.perm, outs.port_start)
+        torch.cuda.synchronize()
+    finally:
+        ctx.close()
+    g = src.cpu().numpy()
+    want = np.nonzero(exp2["reason"] == N.R_OK)[0]
+    assert np.array_equal(g & 0xFFFFFFFF, want) and np.all(g >> 32 == 0)
     rb = synth.Batch(arena=arena.cpu().numpy(), desc=desc.cpu().numpy().view(np.uint32))
-    for k in range(0, len(g), 97):
+    assert np.all(rb.arena[-D.ARENA_PAD:] == 0)
+    for k in range(len(g)):
         o, n_ = int(rb.desc[k, 0]), int(rb.desc[k, 1])
-        assert bytes(rb.arena[o:o + n_]) == b.frame(int(g[k]))
+        assert o % 4 == 0 and bytes(rb.arena[o:o + n_]) == b.frame(int(g[k]))
     fcfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=4)
     res = device.process_batches([rb], fcfg, max_flows=1 << 16, anno=False, perm=False)
     ids = oracle.FlowTable(1 << 16).batch(rb, oracle.process_batch(fcfg, rb))
     assert np.array_equal(res[0]["flowid"], ids)
 
 
-def test_gather_frames_chunked_matches_whole():
-    """_gather_frames in small chunks equals a per-frame concatenation, and
-    exchange_by_flow's received arena carries the ABI's zeroed tail."""
+def test_exchange_format_round_trip():
+    """The re-shard format (oracle/exchange.py, the HIP kernels' checker):
+    three ranks' ragged frames at unaligned offsets, packed by owner, moved by
+    a simulated all-to-all and unpacked, land on their owners exactly once
+    with their bytes, in (source rank, source index) order, 4-B aligned, the
+    slot padding zero."""
+    from oracle import exchange as X
     rng = np.random.default_rng(5)
-    arena = torch.from_numpy(rng.integers(0, 256, 50_000, dtype=np.uint8))
-    ln = torch.from_numpy(rng.integers(0, 300, 200)).to(torch.int64)
-    off = torch.from_numpy(rng.integers(0, 49_000 - 300, 200)).to(torch.int64)
-    want = np.concatenate([arena.numpy()[o:o + n] for o, n in zip(off.tolist(), ln.tolist())])
-    for chunk in (1, 97, 1000, 1 << 24):
-        got = D._gather_frames(arena, off, ln, chunk_bytes=chunk)
-        assert np.array_equal(got.numpy(), want)
-    desc = torch.stack([off, ln], 1).to(torch.int32)
-    ra, rd, _ = D.exchange_by_flow(arena, desc, torch.zeros(200, dtype=torch.int64))
-    assert ra.numel() == int(ln.sum()) + D.ARENA_PAD and int(ra[-D.ARENA_PAD:].sum()) == 0
-    assert np.array_equal(ra[:int(ln.sum())].numpy(), want)
+    world = 3
+    arena = rng.integers(0, 256, 200_000, dtype=np.uint8)
+    parts, srcs = [], []
+    for rank in range(world):
+        n = int(rng.integers(0, 400))
+        ln = rng.integers(0, 300, n).astype(np.uint32)
+        off = rng.integers(0, 190_000, n).astype(np.uint32)
+        desc = np.stack([off, ln], 1)
+        owner = rng.integers(-1, world, n)
+        perm, ps = X.partition(owner, world)
+        meta, seg = X.plan(desc, perm, ps, world, rank)
+        assert np.all(np.diff(meta[:, 2].astype(np.int64)[ps[0]:ps[1]]) > 0)
+        send = X.pack(arena, desc, meta, ps, seg, world)
+        assert len(send) == int(sum(seg)) and len(send) == int(((ln[owner >= 0].astype(np.int64) + 3) // 4 * 4).sum())
+        parts.append((send, meta, ps, seg))
+        srcs.append((desc, owner))
+    for r, (buf, meta, displ) in enumerate(X.all_to_all(parts, world)):
+        d = X.unpack(meta, displ)
+        want = [(s, i) for s, (desc, owner) in enumerate(srcs) for i in np.nonzero(owner == r)[0]]
+        assert [(int(a), int(b)) for a, b in zip(meta[:, 3], meta[:, 2])] == want
+        for (o, n_), (s, i) in zip(d.tolist(), want):
+            so, sn = srcs[s][0][i].tolist()
+            assert n_ == sn and o % 4 == 0
+            assert np.array_equal(buf[o:o + n_], arena[so:so + sn])
+            assert np.all(buf[o + n_:o + ((n_ + 3) & ~3)] == 0)

@@ -1,0 +1,177 @@
+"""Flow re-shard across GPUs (fcgpu_exchange_plan / _pack / _unpack,
+fastclick_amd/csrc/fcgpu_exchange.hh) against its numpy restatement
+(oracle/exchange.py): records, segment sizes and send buffers bit-exact
+(slot padding included), on ragged frames at unaligned offsets, empty
+batches, all-invalid batches, 1 to 64 owners and a 1M-packet batch; the
+receive side through a simulated all-to-all. The 2-rank gloo exchange itself
+is tests/test_dist.py."""
+import numpy as np
+import pytest
+
+from fastclick_amd import _native as N
+from fastclick_amd import dist as D
+from fastclick_amd import synth
+from oracle import exchange as X
+
+torch = pytest.importorskip("torch")
+
+
+def _ragged(n, seed, max_len=1600):
+    """n frames of 0..max_len bytes at random (unaligned) offsets of a random
+    arena, with the ABI's slack after it."""
+    rng = np.random.default_rng(seed)
+    size = 1 << 21
+    arena = rng.integers(0, 256, size + 256, dtype=np.uint8)
+    ln = rng.integers(0, max_len + 1, n).astype(np.uint32)
+    off = (rng.integers(0, size - max_len, n)).astype(np.uint32)
+    return arena, np.stack([off, ln], 1) if n else np.zeros((0, 2), np.uint32)
+
+
+def _dev(a, dt):
+    return torch.from_numpy(np.ascontiguousarray(a).view(dt)).cuda()
+
+
+def _pack_gpu(ctx, arena, desc, perm, ps, world, rank):
+    from fastclick_amd import device
+    send, meta, seg_n, seg_b = device.exchange_pack(ctx, _dev(arena, np.uint8), _dev(desc, np.int32),
+                                                    _dev(perm.astype(np.uint32), np.int32),
+                                                    _dev(ps.astype(np.uint32), np.int32), world, rank)
+    torch.cuda.synchronize()
+    return (send.cpu().numpy(), meta.cpu().numpy().view(np.uint32).reshape(-1, 4), seg_n,
+            np.array(seg_b, dtype=np.uint64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n,seed", [(1, 5000, 1), (3, 5000, 2), (8, 20000, 3), (64, 20000, 4),
+                                          (5, 1, 5), (2, 2047, 6), (2, 2049, 7)])
+def test_gpu_exchange_pack_matches_oracle(world, n, seed):
+    arena, desc = _ragged(n, seed)
+    rng = np.random.default_rng(seed + 100)
+    owner = rng.integers(-1, world, n)
+    perm, ps = X.partition(owner, world)
+    ctx = N.Context(0, max(n, 1))
+    try:
+        send, meta, seg_n, seg_b = _pack_gpu(ctx, arena, desc, perm, ps, world, rank=7)
+    finally:
+        ctx.close()
+    emeta, eseg = X.plan(desc, perm, ps, world, 7)
+    esend = X.pack(arena, desc, emeta, ps, eseg, world)
+    assert np.array_equal(seg_b, eseg)
+    assert seg_n == [int(ps[d + 1] - ps[d]) for d in range(world)]
+    assert np.array_equal(meta, emeta)
+    total = int(eseg.sum())
+    assert np.array_equal(send[:total], esend)
+    assert len(send) == total + D.ARENA_PAD and not send[total:].any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["empty", "all_invalid", "zero_lengths"])
+def test_gpu_exchange_edges(case):
+    world = 4
+    n = {"empty": 0, "all_invalid": 3000, "zero_lengths": 3000}[case]
+    arena, desc = _ragged(n, 11)
+    owner = np.full(n, -1) if case == "all_invalid" else np.arange(n) % world
+    if case == "zero_lengths":
+        desc[::2, 1] = 0
+    perm, ps = X.partition(owner, world)
+    ctx = N.Context(0, max(n, 1))
+    try:
+        send, meta, seg_n, seg_b = _pack_gpu(ctx, arena, desc, perm, ps, world, rank=0)
+    finally:
+        ctx.close()
+    emeta, eseg = X.plan(desc, perm, ps, world, 0)
+    assert np.array_equal(seg_b, eseg) and np.array_equal(meta, emeta)
+    assert np.array_equal(send[:int(eseg.sum())], X.pack(arena, desc, emeta, ps, eseg, world))
+    if case != "zero_lengths":
+        assert len(meta) == 0 and int(seg_b.sum()) == 0
+
+
+@pytest.mark.gpu
+def test_gpu_exchange_owner_pass_and_simulated_all_to_all(oracle):
+    """Four ranks' shards of a C3 IMIX batch with errors: the owner pass
+    (LB_MODE hash over 4 outputs, whole-batch partition) and the pack on the
+    GPU, the segments moved as an all-to-all would, the descriptors unpacked
+    on the GPU: every valid packet lands once, on the rank its flow hash
+    names, with its bytes, in (source rank, source index) order."""
+    from fastclick_amd import device
+    from fastclick_amd.device import DeviceBatch, DeviceOutputs
+    world = 4
+    b = synth.c3(40_000, nflows=3000, seed=21)
+    synth.inject_errors(b, 0.03, seed=22)
+    cfg = N.make_cfg(offset=14, checksum=True, hash_mode=N.HASH_FLOWID, classify=N.CLS_LB_HASH, nports=world)
+    full = oracle.process_batch(cfg, b)
+    parts, shards = [], []
+    ctx = N.Context(0, b.n, cfg)
+    try:
+        for rank in range(world):
+            lo, hi = D.shard_range(b.n, world, rank)
+            shard = synth.Batch(arena=b.arena, desc=np.ascontiguousarray(b.desc[lo:hi]))
+            db = DeviceBatch.upload(shard, device="cuda:0")
+            outs = DeviceOutputs(shard.n, world, device="cuda:0", perm=True, port_start=True,
+                                 partition=N.PART_GLOBAL)
+            device.run_device(ctx, db, outs)
+            send, meta, seg_n, seg_b = device.exchange_pack(ctx, db.arena, db.desc, outs.perm, outs.port_start,
+                                                            world, rank)
+            torch.cuda.synchronize()
+            ps = outs.port_start.cpu().numpy().view(np.uint32)
+            exp_perm, exp_ps = X.partition(np.where(full["reason"][lo:hi] == N.R_OK,
+                                                    full["port"][lo:hi].astype(np.int64), -1), world)
+            assert np.array_equal(ps[:world + 1], exp_ps[:world + 1])
+            emeta, eseg = X.plan(shard.desc, exp_perm, exp_ps, world, rank)
+            assert np.array_equal(meta.cpu().numpy().view(np.uint32), emeta)
+            assert seg_b == [int(x) for x in eseg]
+            parts.append((send, meta, seg_n, seg_b))
+            shards.append(lo)
+        # the all-to-all, as RCCL would deliver it: receiver r gets source s's
+        # segment r, sources in rank order
+        for r in range(world):
+            bufs, metas, displ, at = [], [], [], 0
+            for send, meta, seg_n, seg_b in parts:
+                b0 = sum(seg_b[:r])
+                m0 = sum(seg_n[:r])
+                bufs.append(send[b0:b0 + seg_b[r]])
+                metas.append(meta[m0:m0 + seg_n[r]])
+                displ.append(at)
+                at += seg_b[r]
+            buf = torch.cat(bufs + [torch.zeros(D.ARENA_PAD, dtype=torch.uint8, device="cuda:0")])
+            rmeta = torch.cat(metas)
+            rdesc = device.exchange_unpack(ctx, rmeta, displ)
+            torch.cuda.synchronize()
+            rm = rmeta.cpu().numpy().view(np.uint32)
+            assert np.array_equal(rdesc.cpu().numpy().view(np.uint32), X.unpack(rm, displ))
+            g = np.array([shards[s] + i for i, s in zip(rm[:, 2], rm[:, 3])], dtype=np.int64)
+            want = np.nonzero((full["reason"] == N.R_OK) & (full["port"] == r))[0]
+            assert np.array_equal(g, want)
+            hb = buf.cpu().numpy()
+            for k, (o, n_) in enumerate(rdesc.cpu().numpy().view(np.uint32).tolist()):
+                assert bytes(hb[o:o + n_]) == b.frame(int(g[k]))
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_exchange_1m_batch():
+    """The full-size batch: 1M C4 packets (uniform 5-tuples) to 8 owners,
+    records and send buffer bit-exact against the restatement."""
+    world, n = 8, 1 << 20
+    b = synth.c4(n, seed=31)
+    owner = np.random.default_rng(32).integers(-1, world, n)
+    perm, ps = X.partition(owner, world)
+    arena = np.concatenate([b.arena, np.zeros(256, np.uint8)])
+    ctx = N.Context(0, n)
+    try:
+        send, meta, seg_n, seg_b = _pack_gpu(ctx, arena, b.desc, perm, ps, world, rank=3)
+    finally:
+        ctx.close()
+    emeta, eseg = X.plan(b.desc, perm, ps, world, 3)
+    assert np.array_equal(seg_b, eseg) and np.array_equal(meta, emeta)
+    assert np.array_equal(send[:int(eseg.sum())], X.pack(arena, b.desc, emeta, ps, eseg, world))
+
+
+def test_exchange_rejects_bad_arguments():
+    """Argument checks need no device: a null context, world 0 or > 64."""
+    lib = N.load()
+    assert lib.fcgpu_exchange_plan(None, None, None, None, 0, 1, 0, None, None, None) == N.EINVAL
+    assert lib.fcgpu_exchange_pack(None, None, None, None, None, None, 0, 1, None, 0, None) == N.EINVAL
+    arr = (N.C.c_uint64 * 1)()
+    assert lib.fcgpu_exchange_unpack(None, None, 0, arr, 1, None, None) == N.EINVAL
