@@ -63,6 +63,10 @@ def load():
     lib.fcclick_bench_threads.restype = C.c_int
     lib.fcclick_bench_threads.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
                                           C.c_uint32, C.c_uint32, C.POINTER(C.c_double), C.c_char_p, C.c_size_t]
+    if hasattr(lib, "fcclick_bench_timed"):        # absent from older A/B builds of the harness
+        lib.fcclick_bench_timed.restype = C.c_int
+        lib.fcclick_bench_timed.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                            C.c_double, C.c_uint32, C.POINTER(C.c_double), C.c_char_p, C.c_size_t]
     _lib = lib
     return lib
 
@@ -184,17 +188,23 @@ def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1, timer_flu
     return out
 
 
-def bench_element(conf: str, batch, *, burst: int = 32, reps: int = 5, threads: int = 1) -> float:
+def bench_element(conf: str, batch, *, burst: int = 32, reps: int = 5, threads: int = 1,
+                  seconds: float | None = None) -> float:
     """Packets/s through the element (threads > 1: that many instances, one
     per thread, each with its own GPU context, their timed loops started
-    together after every set-up; all packets over the union of the windows)."""
+    together after every set-up; all packets over the union of the windows).
+    seconds: push for that long instead of `reps` passes (fcclick_bench_timed)."""
     lib = load()
     arena = np.ascontiguousarray(batch.arena)
     desc = np.ascontiguousarray(batch.desc, dtype=np.uint32)
     pps = C.c_double()
     err = C.create_string_buffer(512)
-    rc = lib.fcclick_bench_threads(conf.encode(), arena.ctypes.data, desc.ctypes.data, batch.n, burst, reps,
-                                   threads, C.byref(pps), err, 512)
+    if seconds is not None:
+        rc = lib.fcclick_bench_timed(conf.encode(), arena.ctypes.data, desc.ctypes.data, batch.n, burst,
+                                     float(seconds), threads, C.byref(pps), err, 512)
+    else:
+        rc = lib.fcclick_bench_threads(conf.encode(), arena.ctypes.data, desc.ctypes.data, batch.n, burst, reps,
+                                       threads, C.byref(pps), err, 512)
     if rc != 0:
         raise RuntimeError(err.value.decode())
     return pps.value

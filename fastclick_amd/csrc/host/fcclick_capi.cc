@@ -334,9 +334,13 @@ using Clock = std::chrono::steady_clock;
 // `reps` times through the trace; returns packets per second, or < 0. With a
 // start line, the timed loop begins once every thread has reached it (a
 // thread that fails still arrives), and [t_beg, t_end] is its timed window.
+// With `stop`, the timed loop runs whole passes over the trace until *stop is
+// set (reps ignored) and *done gets the packets pushed -- a source that keeps
+// pushing for a fixed time, as the CPU baseline's threads do.
 double bench_one(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n, uint32_t burst,
                  uint32_t reps, std::string &e, StartLine *line = nullptr, Clock::time_point *t_beg = nullptr,
-                 Clock::time_point *t_end = nullptr) {
+                 Clock::time_point *t_end = nullptr, const std::atomic<bool> *stop = nullptr,
+                 uint64_t *done = nullptr) {
     auto el = make_element(conf, e);
     if (!el || el->initialize(e) < 0) {
         if (line) line->arrive();
@@ -384,16 +388,26 @@ double bench_one(const char *conf, const uint8_t *arena, const uint32_t *desc, u
     el->flush();
     if (line) line->arrive();
     auto t0 = Clock::now();
-    for (uint32_t r = 0; r < reps; ++r) one();
+    uint64_t passes = 0;
+    if (stop) {
+        while (!stop->load(std::memory_order_relaxed)) {
+            one();
+            ++passes;
+        }
+    } else {
+        for (uint32_t r = 0; r < reps; ++r) one();
+        passes = reps;
+    }
     el->flush();
     auto t1 = Clock::now();
     if (t_beg) *t_beg = t0;
     if (t_end) *t_end = t1;
+    if (done) *done = passes * n;
     const double s = std::chrono::duration<double>(t1 - t0).count();
     e = el->read_handler("error");
     el.reset();                      // before the pool its packets belong to
     if (!e.empty()) return -2.0;
-    return (double)n * reps / s;
+    return (double)n * passes / s;
 }
 }  // namespace
 
@@ -406,6 +420,50 @@ extern "C" int fcclick_bench(const char *conf, const uint8_t *arena, const uint3
         return r == -1.0 ? -1 : -2;
     }
     if (pps) *pps = r;
+    return 0;
+}
+
+// T element threads pushing for `seconds` (every thread set up and warmed up
+// first): packets of all threads over the union of their windows, each window
+// ending at the first pass boundary after the stop plus the final flush.
+extern "C" int fcclick_bench_timed(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                                   uint32_t burst, double seconds, uint32_t threads, double *pps, char *err,
+                                   size_t errcap) {
+    if (threads == 0) threads = 1;
+    if (!(seconds > 0)) {
+        copy_err("seconds must be > 0", err, errcap);
+        return -1;
+    }
+    std::vector<double> r(threads, 0.0);
+    std::vector<std::string> es(threads);
+    std::vector<Clock::time_point> beg(threads), end(threads);
+    std::vector<uint64_t> cnt(threads, 0);
+    std::atomic<bool> stop{false};
+    std::vector<std::thread> th;
+    StartLine line;
+    line.parties = threads + 1;                   // the threads and this timer
+    for (uint32_t t = 0; t < threads; ++t)
+        th.emplace_back([&, t]() {
+            r[t] = bench_one(conf, arena, desc, n, burst, 0, es[t], &line, &beg[t], &end[t], &stop, &cnt[t]);
+        });
+    line.arrive();
+    std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
+    stop.store(true, std::memory_order_relaxed);
+    for (auto &x : th) x.join();
+    for (uint32_t t = 0; t < threads; ++t)
+        if (r[t] < 0) {
+            copy_err(es[t], err, errcap);
+            return r[t] == -1.0 ? -1 : -2;
+        }
+    Clock::time_point b = beg[0], e = end[0];
+    uint64_t total = 0;
+    for (uint32_t t = 0; t < threads; ++t) {
+        b = std::min(b, beg[t]);
+        e = std::max(e, end[t]);
+        total += cnt[t];
+    }
+    const double s = std::chrono::duration<double>(e - b).count();
+    if (pps) *pps = s > 0 ? (double)total / s : 0.0;
     return 0;
 }
 

@@ -116,6 +116,15 @@ int fcclick_bench_threads(const char *conf, const uint8_t *arena, const uint32_t
                           uint32_t burst, uint32_t reps, uint32_t threads, double *pps, char *err,
                           size_t errcap);
 
+/* `threads` element instances pushing whole passes over the trace for
+ * `seconds` (a source that keeps pushing, as the CPU baseline's threads do:
+ * no thread's tail of a fixed packet count stretches the window): *pps = all
+ * threads' packets over the union of their windows, each ending at its first
+ * pass boundary after the stop plus its final flush. */
+int fcclick_bench_timed(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                        uint32_t burst, double seconds, uint32_t threads, double *pps, char *err,
+                        size_t errcap);
+
 #ifdef __cplusplus
 }
 #endif

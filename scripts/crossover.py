@@ -83,7 +83,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--chains", default="prog16,flow20k,udp,base")
     ap.add_argument("--threads", default="1,8,16")
-    ap.add_argument("--seconds", type=float, default=4.0)
+    ap.add_argument("--seconds", type=float, default=2.0)
     ap.add_argument("--reps", type=int, default=40)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-gpu", action="store_true")
@@ -104,9 +104,11 @@ def main():
         if not a.no_gpu:
             b = c["batch"]()
             for t in ths:
-                mpps = K.bench_element(c["gpu"], b, burst=32, reps=a.reps, threads=t) / 1e6
+                # pushed for --seconds, as the CPU side is; and the fixed-count run of earlier rounds
+                mpps = K.bench_element(c["gpu"], b, burst=32, threads=t, seconds=a.seconds) / 1e6
+                reps = K.bench_element(c["gpu"], b, burst=32, reps=a.reps, threads=t) / 1e6
                 print(json.dumps({"chain": name, "side": "gpu", "threads": t, "mpps": round(mpps, 1),
-                                  "conf": c["gpu"][:160]}), flush=True)
+                                  "mpps_reps": round(reps, 1), "conf": c["gpu"][:160]}), flush=True)
 
 
 if __name__ == "__main__":

@@ -577,3 +577,19 @@ def test_compact_layout_not_for_whole_captures():
                  "GPUIPCheckClassify(OFFSET 14, N 2, L4 UDP)",
                  "GPUIPCheckClassify(OFFSET 14, N 2, PROGRAM \" 0 265/11000000%ff000000  yes->[0]  no->[1]\")"):
         assert K.stage_compact(conf, b) is None
+
+
+@pytest.mark.gpu
+def test_element_bench_timed_runs_and_checks():
+    """fcclick_bench_timed (the element pushed for a fixed time, as the CPU
+    baseline's threads are): 2 threads for 0.3 s give a rate; the element's
+    errors and a non-positive duration are reported, not timed."""
+    from fastclick_amd import click as K
+    b = synth.c2(1 << 14)
+    conf = "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash)"
+    pps = K.bench_element(conf, b, threads=2, seconds=0.3)
+    assert pps > 1e6
+    with pytest.raises(RuntimeError, match="seconds"):
+        K.bench_element(conf, b, threads=1, seconds=0.0)
+    with pytest.raises(RuntimeError):
+        K.bench_element("GPUIPCheckClassify(OFFSET 14, N 0)", b, threads=1, seconds=0.1)
