@@ -230,7 +230,7 @@ FCGPU_SYMBOLS = {
                                     C.c_int]),
     "fcgpu_exchange_plan": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
                                       C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
-    "fcgpu_exchange_pack": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+    "fcgpu_exchange_pack": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p]),
     "fcgpu_exchange_unpack": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64), C.c_uint32,
                                         C.c_void_p, C.c_void_p]),
@@ -505,9 +505,10 @@ class Context:
         self._chk(self.lib.fcgpu_exchange_plan(self.h, desc, perm, port_start, n, world, rank, meta, seg_bytes,
                                                stream or None), "fcgpu_exchange_plan")
 
-    def exchange_pack(self, arena, desc, port_start, meta, seg_bytes, n, world, send, send_cap, stream=0):
-        """fcgpu_exchange_pack: the leaving frames into their owners' segments of send."""
-        self._chk(self.lib.fcgpu_exchange_pack(self.h, arena, desc, port_start, meta, seg_bytes, n, world,
+    def exchange_pack(self, arena, port_start, meta, seg_bytes, n, world, send, send_cap, stream=0):
+        """fcgpu_exchange_pack: the leaving frames into their owners' segments of send
+        (after exchange_plan of the same batch on this context)."""
+        self._chk(self.lib.fcgpu_exchange_pack(self.h, arena, port_start, meta, seg_bytes, n, world,
                                                send or None, send_cap, stream or None), "fcgpu_exchange_pack")
 
     def exchange_unpack(self, meta, n, src_displ, desc, stream=0):

@@ -280,7 +280,8 @@ struct fcgpu_ctx {
     std::vector<EvPair> pending;
     std::vector<hipEvent_t> free_ev;
     // flow re-shard plan (fcgpu_exchange_plan): block sums and segment starts
-    unsigned long long *x_bsum = nullptr, *x_base = nullptr;
+    unsigned long long *x_bsum = nullptr, *x_base = nullptr, *x_part = nullptr;
+    uint32_t *x_src = nullptr;   // arena offset of each leaving frame (plan -> pack)
     std::string err;
 };
 
@@ -984,6 +985,8 @@ void fcgpu_close(fcgpu_ctx *c) {
         hipFree(c->d_mdesc);
         hipFree(c->x_bsum);
         hipFree(c->x_base);
+        hipFree(c->x_part);
+        hipFree(c->x_src);
         pool_release(c);
         for (auto e : c->flow_order)
             if (e) hipEventDestroy(e);
@@ -2788,6 +2791,8 @@ int fcgpu_exchange_plan(fcgpu_ctx *c, const uint32_t *d_desc, const uint32_t *d_
     if (!c->x_bsum) {
         HIPCHK(c, hipMalloc(&c->x_bsum, sizeof(unsigned long long) * (nblk_max + 1)));
         HIPCHK(c, hipMalloc(&c->x_base, sizeof(unsigned long long) * (FCGPU_MAX_PORTS + 1)));
+        HIPCHK(c, hipMalloc(&c->x_part, sizeof(unsigned long long) * (FCGPU_MAX_PORTS + 1)));
+        HIPCHK(c, hipMalloc(&c->x_src, sizeof(uint32_t) * ((size_t)c->max_batch + 1)));
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
     XPlan P{};
@@ -2801,6 +2806,8 @@ int fcgpu_exchange_plan(fcgpu_ctx *c, const uint32_t *d_desc, const uint32_t *d_
     P.meta = reinterpret_cast<uint4 *>(d_meta);
     P.bsum = c->x_bsum;
     P.base = c->x_base;
+    P.part = c->x_part;
+    P.src = c->x_src;
     P.seg_bytes = reinterpret_cast<unsigned long long *>(d_seg_bytes);
     if (P.nblk) hipLaunchKernelGGL(k_xsum, dim3(P.nblk), dim3(kXThreads), 0, s, P);
     hipLaunchKernelGGL(k_xscan, dim3(1), dim3(1024), 0, s, P);
@@ -2809,18 +2816,20 @@ int fcgpu_exchange_plan(fcgpu_ctx *c, const uint32_t *d_desc, const uint32_t *d_
     return FCGPU_OK;
 }
 
-int fcgpu_exchange_pack(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, const uint32_t *d_port_start,
+int fcgpu_exchange_pack(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_port_start,
                         const fcgpu_xmeta *d_meta, const uint64_t *d_seg_bytes, uint32_t n, uint32_t world,
                         uint8_t *d_send, uint64_t send_cap, void *stream) {
     if (!c) return FCGPU_EINVAL;
     if (world == 0 || world > FCGPU_MAX_PORTS) return fail(c, FCGPU_EINVAL, "fcgpu_exchange_pack: world must be 1..64");
-    if (!d_port_start || !d_seg_bytes || (n && (!d_arena || !d_desc || !d_meta || (send_cap && !d_send))))
+    if (!d_port_start || !d_seg_bytes || (n && (!d_arena || !d_meta || (send_cap && !d_send))))
         return fail(c, FCGPU_EINVAL, "fcgpu_exchange_pack: null buffer");
+    if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "fcgpu_exchange_pack: batch larger than the context's max_batch");
     if (n == 0) return FCGPU_OK;
+    if (!c->x_src) return fail(c, FCGPU_EINVAL, "fcgpu_exchange_pack: no fcgpu_exchange_plan on this context");
     HIPCHK(c, hipSetDevice(c->device));
     XPack X{};
     X.arena = d_arena;
-    X.desc = d_desc;
+    X.src = c->x_src;
     X.port_start = d_port_start;
     X.meta = reinterpret_cast<const uint4 *>(d_meta);
     X.seg_bytes = reinterpret_cast<const unsigned long long *>(d_seg_bytes);
@@ -2828,8 +2837,15 @@ int fcgpu_exchange_pack(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_
     X.send_cap = send_cap;
     X.n = n;
     X.world = world;
-    hipLaunchKernelGGL(k_xpack, dim3((n + kXFramesPerBlock - 1) / kXFramesPerBlock), dim3(kXThreads), 0,
-                       static_cast<hipStream_t>(stream), X);
+    // lanes per frame by the mean slot (send_cap / n): 16 B per lane per step
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint64_t mean = send_cap / n;
+    if (mean <= 64)
+        hipLaunchKernelGGL(k_xpack<4>, dim3((n + kXThreads / 4 - 1) / (kXThreads / 4)), dim3(kXThreads), 0, s, X);
+    else if (mean <= 512)
+        hipLaunchKernelGGL(k_xpack<16>, dim3((n + kXThreads / 16 - 1) / (kXThreads / 16)), dim3(kXThreads), 0, s, X);
+    else
+        hipLaunchKernelGGL(k_xpack<64>, dim3((n + kXThreads / 64 - 1) / (kXThreads / 64)), dim3(kXThreads), 0, s, X);
     HIPCHK(c, hipGetLastError());
     return FCGPU_OK;
 }

@@ -166,7 +166,7 @@ def exchange_pack(ctx: N.Context, arena, desc, perm, port_start, world, rank, st
     send = torch.empty(total + ARENA_PAD, dtype=torch.uint8, device=dev)
     with torch.cuda.stream(s):
         send[total:].zero_()
-    ctx.exchange_pack(arena.data_ptr(), desc.data_ptr(), port_start.data_ptr(), meta.data_ptr(), seg.data_ptr(),
+    ctx.exchange_pack(arena.data_ptr(), port_start.data_ptr(), meta.data_ptr(), seg.data_ptr(),
                       n, world, send.data_ptr(), total, stream=s.cuda_stream)
     return send, meta[:m], seg_n, seg_bytes
 

@@ -635,7 +635,9 @@ int  fcgpu_read_timing(fcgpu_ctx *ctx, double *ms, uint32_t *launches, int nstag
  *   fcgpu_exchange_pack   the frames into d_send (at least the sum of
  *       d_seg_bytes; nothing is written past send_cap): owner d's segment
  *       holds its packets in input order; slot bytes past a frame's length
- *       are zero.
+ *       are zero. It reads the frames' arena offsets the plan left in the
+ *       context: call it after fcgpu_exchange_plan of the same batch on the
+ *       same context and stream, before the next plan.
  *   (the caller's all-to-all: records and segments; a receiver concatenates
  *    the segments it gets in source-rank order)
  *   fcgpu_exchange_unpack the received records -> descriptors into the
@@ -659,9 +661,9 @@ typedef struct fcgpu_xmeta {
 int  fcgpu_exchange_plan(fcgpu_ctx *ctx, const uint32_t *d_desc, const uint32_t *d_perm,
                          const uint32_t *d_port_start, uint32_t n, uint32_t world, uint32_t rank,
                          fcgpu_xmeta *d_meta, uint64_t *d_seg_bytes, void *stream);
-int  fcgpu_exchange_pack(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_desc,
-                         const uint32_t *d_port_start, const fcgpu_xmeta *d_meta, const uint64_t *d_seg_bytes,
-                         uint32_t n, uint32_t world, uint8_t *d_send, uint64_t send_cap, void *stream);
+int  fcgpu_exchange_pack(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_port_start,
+                         const fcgpu_xmeta *d_meta, const uint64_t *d_seg_bytes, uint32_t n, uint32_t world,
+                         uint8_t *d_send, uint64_t send_cap, void *stream);
 int  fcgpu_exchange_unpack(fcgpu_ctx *ctx, const fcgpu_xmeta *d_meta, uint32_t n, const uint64_t *src_displ,
                            uint32_t world, uint32_t *d_desc, void *stream);
 

@@ -5,8 +5,9 @@ plan (3 kernels), the pack and the unpack timed with HIP events on the launch
 stream, median of --reps. Prints one JSON line per workload with the per-kernel
 times, Mpps and the algorithmic HBM bytes per packet:
 
-  plan    perm 4 + desc 8 (twice: block sums, records) + record 16 written = 36 B
-  pack    record 16 + desc 8 + frame L read + slot (L+3)&~3 written
+  plan    perm 4 + desc 8 (twice: block sums, records) + record 16 + arena
+          offset 4 written = 40 B
+  pack    record 16 + arena offset 4 + frame L read + slot (L+3)&~3 written
   unpack  record 16 read + descriptor 8 written = 24 B
 
 python scripts/exchange_rate.py [--reps 50]
@@ -54,7 +55,7 @@ def main():
             ev[0].record()
             ctx.exchange_plan(*args, stream=s)
             ev[1].record()
-            ctx.exchange_pack(db.arena.data_ptr(), db.desc.data_ptr(), outs.port_start.data_ptr(), meta.data_ptr(),
+            ctx.exchange_pack(db.arena.data_ptr(), outs.port_start.data_ptr(), meta.data_ptr(),
                               seg.data_ptr(), n, world, send.data_ptr(), total, stream=s)
             ev[2].record()
             ctx.exchange_unpack(meta.data_ptr(), m, displ, rdesc.data_ptr(), stream=s)
@@ -64,7 +65,7 @@ def main():
                 for k, key in enumerate(("plan", "pack", "unpack")):
                     t[key].append(ev[k].elapsed_time(ev[k + 1]) * 1e3)
         med = {k: statistics.median(v) for k, v in t.items()}
-        byt = {"plan": 36 * m, "pack": 24 * m + frame_bytes + total, "unpack": 24 * m}
+        byt = {"plan": 40 * m, "pack": 20 * m + frame_bytes + total, "unpack": 24 * m}
         out = {"workload": name, "packets": n, "sent": m, "world": world, "frame_bytes": frame_bytes,
                "send_bytes": total, "us": {k: round(v, 2) for k, v in med.items()},
                "mpps": round(m / sum(med.values()), 1),

@@ -14,8 +14,8 @@
 
 int main(int argc, char **argv) {
     const uint32_t threads = argc > 1 ? (uint32_t)atoi(argv[1]) : 1;
-    const uint32_t batch = argc > 2 ? (uint32_t)atoi(argv[2]) : 16384;
-    const uint32_t reps = argc > 3 ? (uint32_t)atoi(argv[3]) : 40;
+    const std::string batch = argc > 2 ? argv[2] : "16384";     // a number or "auto"
+    const uint32_t reps = argc > 3 ? (uint32_t)atoi(argv[3]) : 40;   // 0: pushed for 2 s (fcclick_bench_timed)
     const uint32_t n = 1u << 16;
     std::vector<uint8_t> arena((size_t)n * 64 + 256, 0);
     std::vector<uint32_t> desc(2ull * n);
@@ -29,18 +29,22 @@ int main(int argc, char **argv) {
         desc[2 * i] = i * 64;
         desc[2 * i + 1] = 60;
     }
-    std::string conf = "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BATCH " + std::to_string(batch) + ")";
+    std::string conf = "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BATCH " + batch + ")";
+    auto run = [&](const char *c, double *pps, char *err) {
+        return reps ? fcclick_bench_threads(c, arena.data(), desc.data(), n, 32, reps, threads, pps, err, 512)
+                    : fcclick_bench_timed(c, arena.data(), desc.data(), n, 32, 2.0, threads, pps, err, 512);
+    };
     double pps = 0;
     char err[512] = {0};
-    const int rc = fcclick_bench_threads(conf.c_str(), arena.data(), desc.data(), n, 32, reps, threads, &pps, err,
-                                         sizeof err);
+    const int rc = run(conf.c_str(), &pps, err);
     if (rc) {
         fprintf(stderr, "error %d: %s\n", rc, err);
         return 1;
     }
     double floor = 0;
-    fcclick_bench_threads("Pass", arena.data(), desc.data(), n, 32, reps, threads, &floor, err, sizeof err);
-    printf("{\"threads\": %u, \"batch\": %u, \"element_mpps\": %.1f, \"floor_mpps\": %.1f, \"element_ns_per_pkt_per_thread\": %.2f}\n",
-           threads, batch, pps / 1e6, floor / 1e6, threads * 1e9 / pps);
+    run("Pass", &floor, err);
+    printf("{\"threads\": %u, \"batch\": \"%s\", \"method\": \"%s\", \"element_mpps\": %.1f, \"floor_mpps\": %.1f, "
+           "\"element_ns_per_pkt_per_thread\": %.2f}\n",
+           threads, batch.c_str(), reps ? "passes" : "timed 2 s", pps / 1e6, floor / 1e6, threads * 1e9 / pps);
     return 0;
 }

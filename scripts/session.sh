@@ -94,6 +94,9 @@ for s in "${ST[@]}"; do
     crossover) step crossover 1000 python -u scripts/crossover.py ;;
     crossover16) step crossover16 600 python -u scripts/crossover.py --threads 8,16 --no-cpu ;;
     mock_ab) step mock_ab 600 bash scripts/mock_ab_box.sh ;;
+    # the element's host-side ceiling (mock GPU library, zero-copy staging as on
+    # the box at >= 4 threads), pushed for 2 s, beside the real element
+    mock_timed) step mock_timed 600 bash -c 'for r in 1 2; do for t in 1 8 12 16; do MOCK_ZEROCOPY=1 timeout -k 5 60 scripts/mock/base/element_bench $t auto 0 || exit $?; timeout -k 5 120 python scripts/element_threads.py $t || exit $?; done; done' ;;
     el_sweep) step el_sweep 900 bash scripts/el_sweep.sh 3 ;;
     el_sweep2) BATCHES="4096 8192 16384" SLOTS_LIST=2 step el_sweep2 900 bash scripts/el_sweep.sh 3 16 8 4 ;;
     el_spin) step el_spin 900 bash scripts/el_spin.sh 3 ;;
@@ -105,10 +108,6 @@ for s in "${ST[@]}"; do
               step kt_exchange 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_kt_exchange -o run -- python3 scripts/exchange_rate.py --reps 20 ;;
     # the element's defaults at 1-16 threads, two interleaved rounds
     el_default) step el_default 600 bash -c 'for r in 1 2; do for t in 1 2 4 8 12 16; do timeout -k 5 120 python scripts/element_threads.py $t || exit $?; done; done' ;;
-    el_cyc) for t in 16 8 1; do FCCLICK_LIB=scripts/mock/cyc/libfcclick.so step el_cyc$t 300 python scripts/el_cycles.py $t; done ;;
-    el_cycgpu) for t in 16 8 4 1; do FCGPU_LIB=scripts/mock/cycgpu/libfcgpu.so FCCLICK_LIB=scripts/mock/cycgpu/libfcclick.so step el_cycgpu$t 300 python scripts/el_cycles.py $t; done ;;
-    el_issue) ALT=scripts/mock/old/libfcclick.so ALT_FCGPU=scripts/mock/old/libfcgpu.so step el_issue 900 bash scripts/el_ab_lib.sh 3 ;;
-    el_nt) ALT=scripts/mock/nt_real/libfcclick.so step el_nt 900 bash scripts/el_ab_lib.sh 3 ;;
     # the element at 16 threads (default BATCH/ZEROCOPY/SLOTS): rate, then a kernel trace
     el16) step el16 300 python scripts/element_threads.py 16 &&
           step el16_s3 300 python scripts/element_threads.py 16 0 auto 3 &&

@@ -43,7 +43,7 @@ def _pack_gpu(ctx, arena, desc, perm, ps, world, rank):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,n,seed", [(1, 5000, 1), (3, 5000, 2), (8, 20000, 3), (64, 20000, 4),
-                                          (5, 1, 5), (2, 2047, 6), (2, 2049, 7)])
+                                          (5, 1, 5), (2, 1023, 6), (2, 1025, 7), (2, 2049, 8)])
 def test_gpu_exchange_pack_matches_oracle(world, n, seed):
     arena, desc = _ragged(n, seed)
     rng = np.random.default_rng(seed + 100)
@@ -172,6 +172,6 @@ def test_exchange_rejects_bad_arguments():
     """Argument checks need no device: a null context, world 0 or > 64."""
     lib = N.load()
     assert lib.fcgpu_exchange_plan(None, None, None, None, 0, 1, 0, None, None, None) == N.EINVAL
-    assert lib.fcgpu_exchange_pack(None, None, None, None, None, None, 0, 1, None, 0, None) == N.EINVAL
+    assert lib.fcgpu_exchange_pack(None, None, None, None, None, 0, 1, None, 0, None) == N.EINVAL
     arr = (N.C.c_uint64 * 1)()
     assert lib.fcgpu_exchange_unpack(None, None, 0, arr, 1, None, None) == N.EINVAL
