@@ -106,6 +106,11 @@ for s in "${ST[@]}"; do
     exchange) step pytest_exchange 600 python -u -m pytest tests/test_exchange.py tests/test_dist.py -m gpu -x -v --timeout 120 --timeout-method thread &&
               step exchange_rate 300 python scripts/exchange_rate.py &&
               step kt_exchange 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_kt_exchange -o run -- python3 scripts/exchange_rate.py --reps 20 ;;
+    # CPU time the element's process takes (user + sys vs wall) and the job
+    # cgroup's CFS throttling around 8- and 16-thread runs
+    el_cpu) step el_cpu 600 bash -c 'cat /sys/fs/cgroup/cpu.max 2>/dev/null; for t in 8 12 16; do cat /sys/fs/cgroup/cpu.stat 2>/dev/null | tr "\n" " "; echo; timeout -k 5 120 python scripts/element_threads.py $t || exit $?; done; cat /sys/fs/cgroup/cpu.stat 2>/dev/null | tr "\n" " "; echo' ;;
+    # SLOTS 2 vs 3 at 12 / 16 threads, pushed for 2 s, three interleaved rounds
+    el_slots) step el_slots 900 bash -c 'for r in 1 2 3; do for t in 12 16; do for sl in 2 3; do timeout -k 5 120 python scripts/element_threads.py $t 0 auto $sl || exit $?; done; done; done' ;;
     # the element's defaults at 1-16 threads, two interleaved rounds
     el_default) step el_default 600 bash -c 'for r in 1 2; do for t in 1 2 4 8 12 16; do timeout -k 5 120 python scripts/element_threads.py $t || exit $?; done; done' ;;
     # the element at 16 threads (default BATCH/ZEROCOPY/SLOTS): rate, then a kernel trace
