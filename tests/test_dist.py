@@ -237,3 +237,57 @@ def test_exchange_format_round_trip():
             assert n_ == sn and o % 4 == 0
             assert np.array_equal(buf[o:o + n_], arena[so:so + sn])
             assert np.all(buf[o + n_:o + ((n_ + 3) & ~3)] == 0)
+
+
+def _segments_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import exchange as X
+        rng = np.random.default_rng(100 + rank)
+        n = 0 if rank == 2 else 300                     # rank 2 sends nothing
+        arena = rng.integers(0, 256, 50_000, dtype=np.uint8)
+        desc = np.stack([rng.integers(0, 49_000, n), rng.integers(0, 200, n)], 1).astype(np.uint32) \
+            if n else np.zeros((0, 2), np.uint32)
+        owner = rng.choice([0, 2, -1], n)               # nobody sends to rank 1
+        perm, ps = X.partition(owner, world)
+        meta, seg = X.plan(desc, perm, ps, world, rank)
+        send = np.concatenate([X.pack(arena, desc, meta, ps, seg, world), np.zeros(D.ARENA_PAD, np.uint8)])
+        seg_n = [int(ps[d + 1]) - int(ps[d]) for d in range(world)]
+        buf, rmeta, displ = D.exchange_segments(torch.from_numpy(send), torch.from_numpy(meta.view(np.int32)),
+                                                seg_n, [int(x) for x in seg])
+        q.put((rank, arena, desc, owner, buf.numpy(), rmeta.numpy().view(np.uint32), displ))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_three_rank_exchange_segments_with_empty_segments():
+    """exchange_segments over gloo with 3 ranks where one rank sends nothing
+    and one receives nothing: every rank gets exactly the frames addressed to
+    it, in (source rank, source index) order, its buffer ending in the ABI's
+    zero pad."""
+    from oracle import exchange as X
+    world = 3
+    port = 29500 + ((os.getpid() + 700) % 1000)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_segments_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r[0]: r[1:] for r in (q.get(timeout=240) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        _, _, _, buf, rmeta, displ = res[r]
+        assert not buf[len(buf) - D.ARENA_PAD:].any()
+        want = [(s, i) for s in range(world) for i in np.nonzero(res[s][2] == r)[0]]
+        assert [(int(a), int(b)) for a, b in zip(rmeta[:, 3], rmeta[:, 2])] == want
+        if r == 1:
+            assert len(rmeta) == 0 and len(buf) == D.ARENA_PAD
+        d = X.unpack(rmeta, displ)
+        for (o, n_), (s, i) in zip(d.tolist(), want):
+            so, sn = res[s][1][i].tolist()
+            assert n_ == sn and np.array_equal(buf[o:o + n_], res[s][0][so:so + sn])
