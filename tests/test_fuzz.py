@@ -112,3 +112,30 @@ def test_gpu_fuzz_flows_vs_oracle(oracle, mode):
         assert np.array_equal(r["reason"], e["reason"])
         assert np.array_equal(r["flowid"], t.batch(b, e))
     assert res[-1]["flow_count"] == t.count()
+
+
+ELEMENT_CONFS = [
+    "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BADSRC 192.0.2.255)",
+    "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4, LB_MODE hash_ip, L4 UDP)",
+    "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 8, DEC_TTL true, SET_CHECKSUM true, HASH FLOW5ID)",
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("conf", ELEMENT_CONFS)
+def test_gpu_fuzz_element_compact_vs_full(oracle, conf):
+    """The fuzzed frames through the drop-in element: compact staging (the
+    default, zero-copy through the shared path) against whole-capture
+    staging, and the verdict-derived outputs against the oracle."""
+    from fastclick_amd import click as K
+    b = fuzz_batch(12_000, 404)
+    base = conf[:-1] + ", BATCH 4096, ZEROCOPY true"
+    full = K.run_element(base + ", COMPACT false)", b, burst=32, nsinks=17)
+    comp = K.run_element(base + ")", b, burst=32, nsinks=17)
+    for k in ("port", "seq", "agg", "dst", "len", "nh", "ip8", "batch"):
+        assert np.array_equal(full[k], comp[k]), k
+    assert full["handlers"] == comp["handlers"]
+    e = oracle.process_batch(K.element_cfg(conf), b)
+    ok = e["reason"] == N.R_OK
+    assert int(comp["handlers"]["drops"]) == int((e["reason"] < N.R_OK).sum())
+    assert np.array_equal(comp["agg"][ok], e["hash"][ok])
