@@ -67,10 +67,13 @@ inline uint32_t capture_bytes(const fcgpu_cfg &c, uint32_t prog_reach) {
 // descriptor points `start` bytes before the record, so the device finds
 // every byte it reads at its frame offset, and bytes outside the range (the
 // neighbouring records) are never part of a decision. A 60-B UDP frame then
-// stages 32 B instead of 64. Chains that read more (AUTO with VLAN / IPv6,
-// decision programs, L4 checksums over the datagram) keep whole captures.
+// stages 24 B instead of 64. With CheckUDPHeader / CheckTCPHeader's checksum
+// (the datagram, whatever its length) a record holds the frame from OFFSET to
+// its end: 46 of a 60-B frame's bytes. Chains that read anywhere in the frame
+// (AUTO with VLAN / IPv6, decision programs) keep whole captures.
 struct StagePlan {
     bool compact = false;
+    bool rest = false;        // the record runs to the frame's end (L4 checksums)
     uint32_t start = 0;       // first frame byte any stage reads
     uint32_t fixed_end = 0;   // frame bytes every packet needs up to (hash_ip, HashSwitch)
     uint32_t tail = 4;        // bytes past th: ports (4) or the L4 length checks' words (16)
@@ -78,8 +81,9 @@ struct StagePlan {
 inline StagePlan stage_plan(const fcgpu_cfg &c) {
     StagePlan p;
     const bool ip4 = c.check_mode == FCGPU_CHECK_IP4 || c.check_mode == FCGPU_MARK_IP4;
-    if (!ip4 || c.classify == FCGPU_CLS_PROGRAM || (c.l4_mode != FCGPU_L4_NONE && c.l4_checksum)) return p;
+    if (!ip4 || c.classify == FCGPU_CLS_PROGRAM) return p;
     p.compact = true;
+    p.rest = c.l4_mode != FCGPU_L4_NONE && c.l4_checksum;
     p.start = (uint32_t)c.offset;
     p.tail = c.l4_mode != FCGPU_L4_NONE ? 16u : 4u;
     if (c.classify == FCGPU_CLS_HASH_IP) {
@@ -94,6 +98,7 @@ inline StagePlan stage_plan(const fcgpu_cfg &c) {
 }
 // The frame bytes [plan.start, end) a packet's record must hold.
 inline uint32_t stage_end(const StagePlan &p, uint32_t offset, const uint8_t *frame, uint32_t len) {
+    if (p.rest) return len;
     uint32_t end = p.fixed_end;
     if (len > offset) {
         // th + tail, and never less than the 20-B header: MarkIPHeader takes
@@ -108,15 +113,22 @@ inline uint32_t stage_end(const StagePlan &p, uint32_t offset, const uint8_t *fr
 }
 constexpr uint32_t kStageLead = 256;   // records start this far into the block (descriptor offsets >= 0)
 
+// Records start on kStageAlign-byte boundaries: the device reads a record
+// through 16-B aligned windows wherever it starts, and the PCIe bytes per
+// packet are the records' bytes (neighbouring records share the window
+// lines), so the finer the packing, the fewer bytes cross (C2: 24-B records
+// instead of 32).
+constexpr uint32_t kStageAlign = 8;
+
 // One packet's compact record: copy cp bytes from frame + src_off; the record
-// takes the returned size (a multiple of 16, at least 16) and the packet's
-// descriptor offset is the record's offset minus p.start.
+// takes the returned size (a multiple of kStageAlign, at least kStageAlign)
+// and the packet's descriptor offset is the record's offset minus p.start.
 inline uint32_t stage_record_size(const StagePlan &p, uint32_t offset, const uint8_t *frame, uint32_t len,
                                   uint32_t &src_off, uint32_t &cp) {
     const uint32_t end = stage_end(p, offset, frame, len);
     cp = end > p.start ? end - p.start : 0u;
     src_off = cp ? p.start : 0u;
-    return cp ? (cp + 15) & ~15u : 16u;
+    return cp ? (cp + kStageAlign - 1) & ~(kStageAlign - 1) : kStageAlign;
 }
 
 }  // namespace fcgpu

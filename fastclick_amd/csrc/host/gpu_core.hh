@@ -654,7 +654,7 @@ class RxCore {
         uint32_t cp;
         size_t rec;
         if (_plan.compact) {
-            // the frame bytes [start, end) the chain reads, in 16-B records
+            // the frame bytes [start, end) the chain reads, in records packed kStageAlign (8) bytes apart
             uint32_t so;
             rec = fcgpu::stage_record_size(_plan, (uint32_t)_cfg.offset, src, len, so, cp);
             src += so;

@@ -42,7 +42,7 @@ int fcclick_parse_program(const char *text, struct fcgpu_step *steps, uint32_t c
 
 /* The element's compact staging (COMPACT true, fastclick_amd/csrc/capture.hh)
  * of n frames for a configuration: each frame's record holds only the bytes
- * the chain reads, in 16-B records from out_arena + 256; out_desc[i] = (record
+ * the chain reads, in records packed 8 B apart from out_arena + 256; out_desc[i] = (record
  * offset - the chain's first byte, length), so frame byte b of packet i is at
  * out_arena + out_desc[2i] + b for every byte the chain reads. For tests (the
  * oracle on the compact layout must agree with the oracle on the frames).
