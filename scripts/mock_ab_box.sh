@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 for rep in 1 2; do
   for t in 1 8 16; do
     b=4096; [ $t = 1 ] && b=16384
-    for v in ${VARIANTS:-base nt}; do
+    for v in ${VARIANTS:-base}; do
       echo "{\"variant\": \"$v\", \"rep\": $rep, \"r\": $(timeout -k 5 120 scripts/mock/$v/element_bench $t $b 40)}"
     done
   done
