@@ -595,3 +595,25 @@ def test_element_bench_timed_runs_and_checks():
         K.bench_element(conf, b, threads=1, seconds=0.0)
     with pytest.raises(RuntimeError):
         K.bench_element("GPUIPCheckClassify(OFFSET 14, N 0)", b, threads=1, seconds=0.1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("zc", ["false", "true"])
+def test_element_compact_rest_of_frame_imix(oracle, zc):
+    """CheckUDPHeader's checksum over IMIX datagrams (64 / 570 / 1500-B
+    frames, valid non-zero checksums, 3 % header errors): records holding the
+    frame from OFFSET to its end (COMPACT true) against whole captures."""
+    from fastclick_amd import click as K
+    b = synth.c3(9000, nflows=500, seed=610)
+    synth.set_udp_checksums(b)
+    synth.inject_errors(b, 0.03, seed=611)
+    conf = f"GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 8, LB_MODE hash, L4 UDP, BATCH 4096, ZEROCOPY {zc}"
+    full = K.run_element(conf + ", COMPACT false)", b, burst=32, nsinks=9)
+    comp = K.run_element(conf + ")", b, burst=32, nsinks=9)
+    for k in ("port", "seq", "agg", "dst", "len", "nh", "batch"):
+        assert np.array_equal(full[k], comp[k]), k
+    assert full["handlers"] == comp["handlers"]
+    e = oracle.process_batch(K.element_cfg(conf + ")"), b)
+    ok = e["reason"] == N.R_OK
+    assert ok.sum() > 0.75 * b.n
+    assert np.array_equal(comp["agg"][ok], e["hash"][ok])
