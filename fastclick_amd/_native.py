@@ -15,7 +15,7 @@ LIBFCGPU = os.environ.get("FCGPU_LIB") or os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 19
+ABI_VERSION = 20
 SPAN_SLOTS = 3
 SPAN_COPY = 0
 SPAN_ZEROCOPY = 1
@@ -47,6 +47,7 @@ PART_GLOBAL, PART_TILE = 0, 1
 OUT_VERDICT, OUT_HASH, OUT_ANNO, OUT_PERM, OUT_PORT_START, OUT_TILE_COUNT, OUT_TILE_PERM, OUT_FLOWID, \
     OUT_IP_RW = (1 << k for k in range(9))
 SUBMIT_COPY = 1 << 31
+SUBMIT_DESC32 = 1 << 30
 FAULT_SUBMIT, FAULT_WAIT, FAULT_LAUNCH = 0, 1, 2
 OUT_ABSENT = (1 << 64) - 1
 TILE = 256

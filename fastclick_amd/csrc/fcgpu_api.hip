@@ -2320,10 +2320,16 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
                             size_t frames_off, uint32_t n, void *h_out, uint32_t outputs, uint32_t partition) {
     if (!c || slot >= FCGPU_SPAN_SLOTS || (n && (!h_in || !h_out))) return FCGPU_EINVAL;
     const bool force_copy = (outputs & FCGPU_SUBMIT_COPY) != 0;
-    outputs &= ~FCGPU_SUBMIT_COPY;
+    const bool desc32 = (outputs & FCGPU_SUBMIT_DESC32) != 0;
+    outputs &= ~(FCGPU_SUBMIT_COPY | FCGPU_SUBMIT_DESC32);
     if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "batch larger than max_batch");
-    if (desc_off + 8ull * n > in_bytes || frames_off > in_bytes || (desc_off & 7))
-        return fail(c, FCGPU_EINVAL, "block: descriptors (8-B aligned) or frames outside in_bytes");
+    const size_t dsz = desc32 ? 4 : 8;
+    if (desc_off + dsz * n > in_bytes || frames_off > in_bytes || (desc_off & (dsz - 1)))
+        return fail(c, FCGPU_EINVAL, "block: descriptors (aligned to their size) or frames outside in_bytes");
+    // the kernels read DESC32 descriptors through a pointer tagged in its low bit
+    auto descp = [desc32, desc_off](uint8_t *base) {
+        return reinterpret_cast<const uint32_t *>(reinterpret_cast<uintptr_t>(base + desc_off) | (desc32 ? 1u : 0u));
+    };
     if (in_bytes - frames_off > 0xffffffffull - kArenaPad) return fail(c, FCGPU_EINVAL, "frames larger than 4 GiB");
     SpanSlot &sp = c->span[slot];
     if (sp.busy) return fail(c, FCGPU_EINVAL, "span slot busy: fcgpu_span_wait it first");
@@ -2401,14 +2407,14 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
     if (zc && agg_eligible(c, d)) {   // AUTO chose zero-copy: >= kZeroCopyAuto contexts share the device
         fcgpu_job j{};
         j.arena = din + frames_off;
-        j.desc = reinterpret_cast<const uint32_t *>(din + desc_off);
+        j.desc = descp(din);
         j.n = n;
         j.out = d;
         int rc = check_process(c, j.arena, j.desc, n, &j.out);
         if (rc != FCGPU_OK) return rc;
         return agg_submit(c, slot, j);
     }
-    int rc = fcgpu_process(c, din + frames_off, reinterpret_cast<const uint32_t *>(din + desc_off), n, &d, s);
+    int rc = fcgpu_process(c, din + frames_off, descp(din), n, &d, s);
     if (rc != FCGPU_OK) return rc;
     if (!zc) HIPCHK(c, hipMemcpyAsync(h_out, sp.d_res, L.bytes, hipMemcpyDeviceToHost, s));
     uint32_t ns = 0;

@@ -861,6 +861,18 @@ __device__ __forceinline__ void glds16(const uint8_t *src, uint8_t *lds) {
                                      (__attribute__((address_space(3))) void *)lds, 16, 0, kWinCpol);
 }
 
+// Packet i's (offset, length) descriptor. A pointer with its low bit set
+// marks FCGPU_SUBMIT_DESC32 descriptors: one uint32 per packet, offset / 8 in
+// bits 0-15 and length in bits 16-31 (the bit is uniform over a batch).
+__device__ __forceinline__ uint2 load_desc(const uint2 *desc, uint32_t i) {
+    const uintptr_t p = reinterpret_cast<uintptr_t>(desc);
+    if (p & 1u) {
+        const uint32_t w = reinterpret_cast<const uint32_t *>(p - 1u)[i];
+        return make_uint2((w & 0xffffu) << 3, w >> 16);
+    }
+    return desc[i];
+}
+
 // Inclusive prefix sum over the 64 lanes of a wave by DPP (gfx9 row shifts
 // within 16-lane rows, then row_bcast:15 / row_bcast:31 across rows): six
 // VALU ops instead of six ds_bpermute round trips.
@@ -1334,7 +1346,7 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
     }
     const uint32_t i = tile * kTile + threadIdx.x;
     uint2 d = make_uint2(0, 0);
-    if (i < V.n) d = V.desc[i];
+    if (i < V.n) d = load_desc(V.desc, i);
     uint8_t *wl = s_win + wave * (kWave * kWin);
 #pragma unroll
     for (int k = 0; k < 4; ++k) glds16(win_src(V.arena, d.x, lane, k), wl + k * 1024);

@@ -395,7 +395,11 @@ class RxCore {
         _capture = fcgpu::capture_bytes(_cfg, reach);
         _plan = fcgpu::stage_plan(_cfg);
         _plan.compact = _plan.compact && _compact;
-        _lead = _plan.compact ? fcgpu::kStageLead : 0u;
+        // compact records with bounded size go with 4-B descriptors
+        // (FCGPU_SUBMIT_DESC32): each frame's start (record - start) then
+        // falls on an 8-B boundary
+        _desc32 = _plan.compact && !_plan.rest;
+        _lead = _plan.compact ? fcgpu::kStageLead + (_desc32 ? (_plan.start & 7u) : 0u) : 0u;
         const size_t per = _capture == fcgpu::kCaptureWhole ? 1536 : _capture;
         _outputs = FCGPU_OUT_VERDICT | FCGPU_OUT_HASH | FCGPU_OUT_ANNO |
                    (_partition == FCGPU_PART_TILE ? FCGPU_OUT_TILE_PERM | FCGPU_OUT_TILE_COUNT
@@ -587,6 +591,7 @@ class RxCore {
         std::vector<uint32_t> keep;
         uint32_t n = 0;
         bool inflight = false;
+        bool desc32 = false;       // descriptors as FCGPU_SUBMIT_DESC32 words (compact records)
         bool holes = false;        // a packet freed while its results were applied
         uint64_t t_first = 0;
         // the result arrays of the completed batch (inside res)
@@ -644,6 +649,17 @@ class RxCore {
         }
     }
 
+    // The slot's DESC32 words so far back to (offset, length) pairs, in place
+    // from the last (a frame longer than 65535 B arrived).
+    static void widen_desc(Slot &s) {
+        for (uint32_t i = s.n; i-- > 0;) {
+            const uint32_t w = s.desc[i];
+            s.desc[2 * i + 1] = w >> 16;
+            s.desc[2 * i] = (w & 0xffffu) << 3;
+        }
+        s.desc32 = false;
+    }
+
     // Copy the packet's leading bytes into the current slot (64-B aligned
     // records), remember the packet; a full slot goes to the device.
     template <class Emit>
@@ -662,7 +678,9 @@ class RxCore {
             cp = len < _capture ? len : _capture;
             rec = cp ? ((size_t)cp + 63) & ~(size_t)63 : 64;
         }
-        if (s->n && s->frames_off + _lead + s->used + rec > s->in_cap) {   // whole frames overflowing the block
+        // whole frames overflowing the block, or DESC32 offsets past their reach
+        if (s->n && (s->frames_off + _lead + s->used + rec > s->in_cap ||
+                     (s->desc32 && _lead + s->used + rec > kDesc32Reach))) {
             submit(emit);
             s = &_slot[_cur];
         }
@@ -672,11 +690,18 @@ class RxCore {
                 return;
             }
             s->t_first = _timer_us >= 0 ? P::now_ns() : 0;
+            s->desc32 = _desc32;
         }
         copy_head(s->span + _lead + s->used, src, cp);
         // compact: frame byte b of the packet is at record + b - start
-        s->desc[2 * s->n] = (uint32_t)(_lead + s->used) - (_plan.compact ? _plan.start : 0u);
-        s->desc[2 * s->n + 1] = len;
+        const uint32_t fo = (uint32_t)(_lead + s->used) - (_plan.compact ? _plan.start : 0u);
+        if (s->desc32 && len > 0xffffu) widen_desc(*s);   // a length DESC32 cannot carry
+        if (s->desc32) {
+            s->desc[s->n] = (fo >> 3) | (len << 16);
+        } else {
+            s->desc[2 * s->n] = fo;
+            s->desc[2 * s->n + 1] = len;
+        }
         s->pkts[s->n++] = p;
         s->used += rec;
         if (s->n == _cap || (_batch && s->n >= _eff_batch)) submit(emit);
@@ -693,7 +718,7 @@ class RxCore {
             std::lock_guard<std::mutex> g(_mu);
             if (_flow_cap && _flow_timeout) flow_clock();
             int rc = fcgpu_span_submit_block(_ctx, k, s.in, s.frames_off + _lead + s.used, 0, s.frames_off, s.n, s.res,
-                                             _outputs, _partition);
+                                             _outputs | (s.desc32 ? FCGPU_SUBMIT_DESC32 : 0u), _partition);
             // BATCH auto: the next batches' size for the path they now take
             _eff_batch = _batch_auto && fcgpu_span_zerocopy_active(_ctx)
                              ? (_plan.compact ? kBatchZeroCopyCompact : kBatchZeroCopy)
@@ -717,7 +742,8 @@ class RxCore {
         P::chatter(name + ": GPU batch failed (" + std::string(fcgpu_last_error(_ctx)) + "), re-submitting it");
         _fail_msg = fcgpu_last_error(_ctx);
         return fcgpu_span_submit_block(_ctx, k, s.in, s.frames_off + _lead + s.used, 0, s.frames_off, s.n, s.res,
-                                       _outputs | FCGPU_SUBMIT_COPY, _partition);
+                                       _outputs | FCGPU_SUBMIT_COPY | (s.desc32 ? FCGPU_SUBMIT_DESC32 : 0u),
+                                       _partition);
     }
 
     // IMP timeouts: the maintainer runs due by now (every RECYCLE_INTERVAL from
@@ -995,6 +1021,9 @@ class RxCore {
     fcgpu::StagePlan _plan;                      // compact records (capture.hh) when the chain allows them
     bool _compact = true;                        // COMPACT
     uint32_t _lead = 0;                          // compact: records start this far into the block
+    bool _desc32 = false;                        // compact records of bounded size: 4-B descriptors
+    // DESC32 frame offsets reach 65535 x 8 B; a slot stops short of it
+    static constexpr size_t kDesc32Reach = 0xffffu * 8u;
     uint32_t _partition = FCGPU_PART_TILE;
     uint32_t _span_mode = FCGPU_SPAN_AUTO;       // ZEROCOPY: the kernels read/write the pinned slots in place
     uint32_t _outputs = 0;                       // FCGPU_OUT_* the element asks for

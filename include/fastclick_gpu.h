@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 19
+#define FCGPU_ABI_VERSION 20
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -333,6 +333,12 @@ int  fcgpu_span_poll(fcgpu_ctx *ctx, uint32_t slot);
  * of the results) whatever the span mode -- never zero-copy, never the shared
  * queue. What an element re-submits a failed batch with (SURVEY 8(b) Errors). */
 #define FCGPU_SUBMIT_COPY    (1u << 31)
+/* Not an output either: the block's descriptors are one uint32 per packet
+ * (n x 4 B at a 4-B aligned desc_off) -- bits 0-15 the frame's offset from
+ * frames_off in 8-B units (frames start on 8-B boundaries below 512 KiB),
+ * bits 16-31 its length (< 65536) -- half the bytes a zero-copy batch reads
+ * for them over PCIe. */
+#define FCGPU_SUBMIT_DESC32  (1u << 30)
 #define FCGPU_OUT_ABSENT     ((size_t)-1)
 typedef struct fcgpu_block_layout {
     size_t verdict, hash, anno, perm, port_start, tile_count, tile_perm, flowid, ip_rw;  /* byte offsets */

@@ -617,3 +617,26 @@ def test_element_compact_rest_of_frame_imix(oracle, zc):
     ok = e["reason"] == N.R_OK
     assert ok.sum() > 0.75 * b.n
     assert np.array_equal(comp["agg"][ok], e["hash"][ok])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("zc", ["false", "true"])
+def test_element_desc32_widens_for_giant_frames(oracle, zc):
+    """Compact records go to the device with 4-B descriptors (16-bit
+    lengths); a frame longer than 65535 B in the middle of a batch turns the
+    slot's descriptors back into (offset, length) pairs: every output the
+    same as whole-capture staging."""
+    from fastclick_amd import click as K
+    b = synth.c4(3000, seed=620)
+    frames = [b.frame(i) for i in range(b.n)]
+    giant = bytearray(frames[7]) + bytes(65_600 - len(frames[7]))    # ip_len 46: take() trims it
+    frames[1500] = bytes(giant)
+    g = synth.from_frames(frames)
+    conf = f"GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 8, LB_MODE hash, BATCH 1024, ZEROCOPY {zc}"
+    full = K.run_element(conf + ", COMPACT false)", g, burst=32, nsinks=9)
+    comp = K.run_element(conf + ")", g, burst=32, nsinks=9)
+    for k in ("port", "seq", "agg", "dst", "len", "nh", "batch"):
+        assert np.array_equal(full[k], comp[k]), k
+    assert full["handlers"] == comp["handlers"]
+    e = oracle.process_batch(K.element_cfg(conf + ")"), g)
+    assert e["reason"][1500] == N.R_OK and comp["len"][1500] == 60
