@@ -865,9 +865,9 @@ __device__ __forceinline__ void glds16(const uint8_t *src, uint8_t *lds) {
 // marks FCGPU_SUBMIT_DESC32 descriptors: one uint32 per packet, offset / 8 in
 // bits 0-15 and length in bits 16-31 (the bit is uniform over a batch).
 __device__ __forceinline__ uint2 load_desc(const uint2 *desc, uint32_t i) {
-    const uintptr_t p = reinterpret_cast<uintptr_t>(desc);
+    const unsigned long long p = reinterpret_cast<unsigned long long>(desc);   // (hiprtc: no uintptr_t)
     if (p & 1u) {
-        const uint32_t w = reinterpret_cast<const uint32_t *>(p - 1u)[i];
+        const uint32_t w = reinterpret_cast<const uint32_t *>(p - 1ull)[i];
         return make_uint2((w & 0xffffu) << 3, w >> 16);
     }
     return desc[i];
