@@ -92,6 +92,9 @@ for s in "${ST[@]}"; do
              kt kt_flow_c4 300 --steps 200 --warmup 20 --no-cpu --workload c4 --flow-capacity 2000000 ;;
     latency) step latency 120 python scripts/latency_probe.py ;;
     crossover) step crossover 1000 python -u scripts/crossover.py ;;
+    crossover3) step crossover 600 python -u scripts/crossover.py --threads 8,16 &&
+                step crossover_b 600 python -u scripts/crossover.py --threads 8,16 &&
+                step crossover_c 600 python -u scripts/crossover.py --threads 8,16 ;;
     crossover2) step crossover_b 600 python -u scripts/crossover.py --threads 8,16 &&
                 step crossover_c 600 python -u scripts/crossover.py --threads 8,16 ;;
     crossover16) step crossover16 600 python -u scripts/crossover.py --threads 8,16 --no-cpu ;;
