@@ -395,10 +395,9 @@ class RxCore {
         _capture = fcgpu::capture_bytes(_cfg, reach);
         _plan = fcgpu::stage_plan(_cfg);
         _plan.compact = _plan.compact && _compact;
-        // compact records with bounded size go with 4-B descriptors
-        // (FCGPU_SUBMIT_DESC32): each frame's start (record - start) then
-        // falls on an 8-B boundary
-        _desc32 = _plan.compact && !_plan.rest;
+        // compact records go with 4-B descriptors (FCGPU_SUBMIT_DESC32): each
+        // frame's start (record - start) then falls on an 8-B boundary
+        _desc32 = _plan.compact;
         _lead = _plan.compact ? fcgpu::kStageLead + (_desc32 ? (_plan.start & 7u) : 0u) : 0u;
         const size_t per = _capture == fcgpu::kCaptureWhole ? 1536 : _capture;
         _outputs = FCGPU_OUT_VERDICT | FCGPU_OUT_HASH | FCGPU_OUT_ANNO |
@@ -650,7 +649,7 @@ class RxCore {
     }
 
     // The slot's DESC32 words so far back to (offset, length) pairs, in place
-    // from the last (a frame longer than 65535 B arrived).
+    // from the last (a frame longer than 65535 B, or records past 512 KiB).
     static void widen_desc(Slot &s) {
         for (uint32_t i = s.n; i-- > 0;) {
             const uint32_t w = s.desc[i];
@@ -678,9 +677,7 @@ class RxCore {
             cp = len < _capture ? len : _capture;
             rec = cp ? ((size_t)cp + 63) & ~(size_t)63 : 64;
         }
-        // whole frames overflowing the block, or DESC32 offsets past their reach
-        if (s->n && (s->frames_off + _lead + s->used + rec > s->in_cap ||
-                     (s->desc32 && _lead + s->used + rec > kDesc32Reach))) {
+        if (s->n && s->frames_off + _lead + s->used + rec > s->in_cap) {   // whole frames overflowing the block
             submit(emit);
             s = &_slot[_cur];
         }
@@ -695,7 +692,8 @@ class RxCore {
         copy_head(s->span + _lead + s->used, src, cp);
         // compact: frame byte b of the packet is at record + b - start
         const uint32_t fo = (uint32_t)(_lead + s->used) - (_plan.compact ? _plan.start : 0u);
-        if (s->desc32 && len > 0xffffu) widen_desc(*s);   // a length DESC32 cannot carry
+        // a length or an offset DESC32 cannot carry: (offset, length) pairs from here
+        if (s->desc32 && (len > 0xffffu || _lead + s->used + rec > kDesc32Reach)) widen_desc(*s);
         if (s->desc32) {
             s->desc[s->n] = (fo >> 3) | (len << 16);
         } else {
@@ -1021,8 +1019,8 @@ class RxCore {
     fcgpu::StagePlan _plan;                      // compact records (capture.hh) when the chain allows them
     bool _compact = true;                        // COMPACT
     uint32_t _lead = 0;                          // compact: records start this far into the block
-    bool _desc32 = false;                        // compact records of bounded size: 4-B descriptors
-    // DESC32 frame offsets reach 65535 x 8 B; a slot stops short of it
+    bool _desc32 = false;                        // compact records: 4-B descriptors while they fit
+    // DESC32 frame offsets reach 65535 x 8 B
     static constexpr size_t kDesc32Reach = 0xffffu * 8u;
     uint32_t _partition = FCGPU_PART_TILE;
     uint32_t _span_mode = FCGPU_SPAN_AUTO;       // ZEROCOPY: the kernels read/write the pinned slots in place
