@@ -57,6 +57,16 @@ inline uint32_t capture_bytes(const fcgpu_cfg &c, uint32_t prog_reach) {
     return need < kCaptureMin ? kCaptureMin : need;
 }
 
+// Records start on kStageAlign-byte boundaries: the device reads a record
+// through 16-B aligned windows wherever it starts, and the PCIe bytes per
+// packet are the records' bytes (neighbouring records share the window
+// lines), so the finer the packing, the fewer bytes cross (C2: 24-B records
+// instead of 32). Rest-of-frame records (L4 checksums) keep 16-B packing:
+// with every frame then at the same place in its 16-B aligned window, a small
+// datagram lies inside the window the device loads and is summed there
+// instead of read again (k_rx win_l4_sum).
+constexpr uint32_t kStageAlign = 8;
+
 // Compact staging (the element's block records). For the IPv4 chains whose
 // reads all fall in [start, o + max(hl, 20) + tail) of each frame -- CheckIPHeader /
 // MarkIPHeader at OFFSET o (header, options, addresses), the ports IPFlowID /
@@ -74,6 +84,7 @@ inline uint32_t capture_bytes(const fcgpu_cfg &c, uint32_t prog_reach) {
 struct StagePlan {
     bool compact = false;
     bool rest = false;        // the record runs to the frame's end (L4 checksums)
+    uint32_t align = 8;       // record packing (rest-of-frame records: 16, see stage_record_size)
     uint32_t start = 0;       // first frame byte any stage reads
     uint32_t fixed_end = 0;   // frame bytes every packet needs up to (hash_ip, HashSwitch)
     uint32_t tail = 4;        // bytes past th: ports (4) or the L4 length checks' words (16)
@@ -84,6 +95,7 @@ inline StagePlan stage_plan(const fcgpu_cfg &c) {
     if (!ip4 || c.classify == FCGPU_CLS_PROGRAM) return p;
     p.compact = true;
     p.rest = c.l4_mode != FCGPU_L4_NONE && c.l4_checksum;
+    p.align = p.rest ? 16u : kStageAlign;
     p.start = (uint32_t)c.offset;
     p.tail = c.l4_mode != FCGPU_L4_NONE ? 16u : 4u;
     if (c.classify == FCGPU_CLS_HASH_IP) {
@@ -113,22 +125,16 @@ inline uint32_t stage_end(const StagePlan &p, uint32_t offset, const uint8_t *fr
 }
 constexpr uint32_t kStageLead = 256;   // records start this far into the block (descriptor offsets >= 0)
 
-// Records start on kStageAlign-byte boundaries: the device reads a record
-// through 16-B aligned windows wherever it starts, and the PCIe bytes per
-// packet are the records' bytes (neighbouring records share the window
-// lines), so the finer the packing, the fewer bytes cross (C2: 24-B records
-// instead of 32).
-constexpr uint32_t kStageAlign = 8;
 
 // One packet's compact record: copy cp bytes from frame + src_off; the record
-// takes the returned size (a multiple of kStageAlign, at least kStageAlign)
+// takes the returned size (a multiple of p.align, at least p.align)
 // and the packet's descriptor offset is the record's offset minus p.start.
 inline uint32_t stage_record_size(const StagePlan &p, uint32_t offset, const uint8_t *frame, uint32_t len,
                                   uint32_t &src_off, uint32_t &cp) {
     const uint32_t end = stage_end(p, offset, frame, len);
     cp = end > p.start ? end - p.start : 0u;
     src_off = cp ? p.start : 0u;
-    return cp ? (cp + kStageAlign - 1) & ~(kStageAlign - 1) : kStageAlign;
+    return cp ? (cp + p.align - 1) & ~(p.align - 1) : p.align;
 }
 
 }  // namespace fcgpu

@@ -396,9 +396,11 @@ class RxCore {
         _plan = fcgpu::stage_plan(_cfg);
         _plan.compact = _plan.compact && _compact;
         // compact records go with 4-B descriptors (FCGPU_SUBMIT_DESC32): each
-        // frame's start (record - start) then falls on an 8-B boundary
+        // frame's start (record - start) falls on an 8-B boundary, and on a
+        // 16-B one while the records so far add up to 16-B multiples (always,
+        // for rest-of-frame records)
         _desc32 = _plan.compact;
-        _lead = _plan.compact ? fcgpu::kStageLead + (_desc32 ? (_plan.start & 7u) : 0u) : 0u;
+        _lead = _plan.compact ? fcgpu::kStageLead + (_plan.start & 15u) : 0u;
         const size_t per = _capture == fcgpu::kCaptureWhole ? 1536 : _capture;
         _outputs = FCGPU_OUT_VERDICT | FCGPU_OUT_HASH | FCGPU_OUT_ANNO |
                    (_partition == FCGPU_PART_TILE ? FCGPU_OUT_TILE_PERM | FCGPU_OUT_TILE_COUNT
