@@ -1860,32 +1860,6 @@ static bool span_zerocopy(const fcgpu_ctx *c) {
            g_auto_n[c->device].load(std::memory_order_relaxed) >= kZeroCopyAuto;
 }
 
-// ---- waiting for a span slot ---------------------------------------------------
-// FCGPU_SPAN_WAIT (read once): "block" (default) -- hipEventSynchronize /
-// hipStreamSynchronize, the runtime's wait; "spin" -- poll the event or
-// stream until it completes (the element's thread has nothing else to do
-// while its slot is still on the device; a sleeping wait adds the wake-up to
-// every round trip).
-static bool span_wait_spin() {
-    static const bool spin = [] {
-        const char *e = getenv("FCGPU_SPAN_WAIT");
-        return e && !strcmp(e, "spin");
-    }();
-    return spin;
-}
-static hipError_t wait_event(hipEvent_t ev) {
-    if (!span_wait_spin()) return hipEventSynchronize(ev);
-    hipError_t e;
-    while ((e = hipEventQuery(ev)) == hipErrorNotReady) __builtin_ia32_pause();
-    return e;
-}
-static hipError_t wait_stream(hipStream_t st) {
-    if (!span_wait_spin()) return hipStreamSynchronize(st);
-    hipError_t e;
-    while ((e = hipStreamQuery(st)) == hipErrorNotReady) __builtin_ia32_pause();
-    return e;
-}
-
 // ---- fault injection (fcgpu_inject_fault) ------------------------------------
 static std::atomic<uint32_t> g_fault_armed{0};     // bit k: kind k has events to skip or fail
 static std::mutex g_fault_mu;
@@ -2191,7 +2165,7 @@ static int agg_finish(fcgpu_ctx *c, uint32_t slot, bool block) {
     }
     hipError_t e = hipSuccess;
     if (st == kAggIssued) {
-        e = block ? wait_event(al->ev) : hipEventQuery(al->ev);
+        e = block ? hipEventSynchronize(al->ev) : hipEventQuery(al->ev);
         if (!block && e == hipErrorNotReady) return 0;
     }
     {
@@ -2444,8 +2418,8 @@ int fcgpu_span_wait(fcgpu_ctx *c, uint32_t slot) {
     }
     HIPCHK(c, hipSetDevice(c->device));
     sp.busy = false;
-    if (sp.evt) HIPCHK(c, wait_event(sp.done));
-    else HIPCHK(c, wait_stream(sp.s));
+    if (sp.evt) HIPCHK(c, hipEventSynchronize(sp.done));
+    else HIPCHK(c, hipStreamSynchronize(sp.s));
     return FCGPU_OK;
 }
 

@@ -104,7 +104,6 @@ for s in "${ST[@]}"; do
     mock_timed) step mock_timed 600 bash -c 'for r in 1 2; do for t in 1 8 12 16; do MOCK_ZEROCOPY=1 timeout -k 5 60 scripts/mock/base/element_bench $t auto 0 || exit $?; timeout -k 5 120 python scripts/element_threads.py $t || exit $?; done; done' ;;
     el_sweep) step el_sweep 900 bash scripts/el_sweep.sh 3 ;;
     el_sweep2) BATCHES="4096 8192 16384" SLOTS_LIST=2 step el_sweep2 900 bash scripts/el_sweep.sh 3 16 8 4 ;;
-    el_spin) step el_spin 900 bash scripts/el_spin.sh 3 ;;
     # the job's 16-CPU cgroup quota is shared with the HIP runtime's own threads
     el_quota) step el_quota 900 bash -c 'for r in 1 2 3; do for t in 16 15 14 12; do timeout -k 5 120 python scripts/element_threads.py $t || exit $?; done; done' ;;
     # the flow re-shard kernels: GPU tests, rates, kernel trace
