@@ -15,7 +15,7 @@ LIBFCGPU = os.environ.get("FCGPU_LIB") or os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 20
+ABI_VERSION = 21
 SPAN_SLOTS = 3
 SPAN_COPY = 0
 SPAN_ZEROCOPY = 1
@@ -45,7 +45,7 @@ NCOUNTERS = CTR_PORT + MAX_PORTS + 1
 CTR_SHARDS = 64
 PART_GLOBAL, PART_TILE = 0, 1
 OUT_VERDICT, OUT_HASH, OUT_ANNO, OUT_PERM, OUT_PORT_START, OUT_TILE_COUNT, OUT_TILE_PERM, OUT_FLOWID, \
-    OUT_IP_RW = (1 << k for k in range(9))
+    OUT_IP_RW, OUT_ANNO8 = (1 << k for k in range(10))
 SUBMIT_COPY = 1 << 31
 SUBMIT_DESC32 = 1 << 30
 FAULT_SUBMIT, FAULT_WAIT, FAULT_LAUNCH = 0, 1, 2

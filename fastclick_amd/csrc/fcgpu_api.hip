@@ -2226,7 +2226,8 @@ int fcgpu_block_layout_for(const fcgpu_ctx *c, uint32_t n, uint32_t outputs, uin
     };
     put(L->verdict, FCGPU_OUT_VERDICT, 2ull * n);
     put(L->hash, FCGPU_OUT_HASH, 4ull * n);
-    put(L->anno, FCGPU_OUT_ANNO, sizeof(fcgpu_anno) * n);
+    if (outputs & FCGPU_OUT_ANNO8) put(L->anno, FCGPU_OUT_ANNO8, sizeof(fcgpu_anno8) * n);
+    else put(L->anno, FCGPU_OUT_ANNO, sizeof(fcgpu_anno) * n);
     put(L->perm, FCGPU_OUT_PERM, 4ull * n);
     put(L->port_start, FCGPU_OUT_PORT_START, 4ull * (FCGPU_MAX_PORTS + 2));
     put(L->tile_count, FCGPU_OUT_TILE_COUNT, 2ull * nb * tiles);
@@ -2312,6 +2313,11 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
         sp.doomed = sp.busy = true;
         return FCGPU_OK;
     }
+    if (outputs & FCGPU_OUT_ANNO8) {
+        const bool ip4 = c->cfg.check_mode == FCGPU_CHECK_IP4 || c->cfg.check_mode == FCGPU_MARK_IP4;
+        if ((outputs & FCGPU_OUT_ANNO) || !ip4 || c->cfg.offset > 255)
+            return fail(c, FCGPU_EINVAL, "FCGPU_OUT_ANNO8: IPv4 check modes with OFFSET < 256, without FCGPU_OUT_ANNO");
+    }
     fcgpu_block_layout L;
     if (fcgpu_block_layout_for(c, n, outputs, partition, &L) != FCGPU_OK) return fail(c, FCGPU_EINVAL, "bad block layout");
     HIPCHK(c, hipSetDevice(c->device));
@@ -2371,6 +2377,8 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
     d.verdict = (uint16_t *)at(L.verdict);
     d.hash = (uint32_t *)at(L.hash);
     d.anno = (fcgpu_anno *)at(L.anno);
+    if (d.anno && (outputs & FCGPU_OUT_ANNO8))    // the kernels store fcgpu_anno8 through a tagged pointer
+        d.anno = reinterpret_cast<fcgpu_anno *>(reinterpret_cast<uintptr_t>(d.anno) | 1u);
     d.perm = (uint32_t *)at(L.perm);
     d.port_start = (uint32_t *)at(L.port_start);
     d.tile_count = (uint16_t *)at(L.tile_count);

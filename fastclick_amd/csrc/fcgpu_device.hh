@@ -873,6 +873,19 @@ __device__ __forceinline__ uint2 load_desc(const uint2 *desc, uint32_t i) {
     return desc[i];
 }
 
+// Packet i's annotation: fcgpu_anno, or -- the pointer's low bit set
+// (FCGPU_OUT_ANNO8, IPv4 check modes) -- the 8-B fcgpu_anno8.
+__device__ __forceinline__ void store_anno(fcgpu_anno *a, uint32_t i, const fcgpu_anno &an) {
+    const unsigned long long p = reinterpret_cast<unsigned long long>(a);
+    if (p & 1u) {
+        reinterpret_cast<uint2 *>(p - 1ull)[i] =
+            make_uint2(an.dst_ip, (uint32_t)an.length | ((uint32_t)(an.nh & 0xffu) << 16) |
+                                      ((uint32_t)((an.th - an.nh) & 0xffu) << 24));
+        return;
+    }
+    a[i] = an;
+}
+
 // Inclusive prefix sum over the 64 lanes of a wave by DPP (gfx9 row shifts
 // within 16-lane rows, then row_bcast:15 / row_bcast:31 across rows): six
 // VALU ops instead of six ds_bpermute round trips.
@@ -1185,7 +1198,7 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, const RxView &V, const 
     if (live) {
         if (V.verdict) V.verdict[i] = (uint16_t)(r.reason | (r.port << 8));
         if (V.hash) V.hash[i] = r.hash;
-        if (V.anno) V.anno[i] = r.an;
+        if (V.anno) store_anno(V.anno, i, r.an);
         bin = r.port;
         if (r.reason != FCGPU_R_OK) rslot = reason_slot(r.reason);
     }

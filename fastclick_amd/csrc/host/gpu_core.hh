@@ -402,7 +402,10 @@ class RxCore {
         _desc32 = _plan.compact;
         _lead = _plan.compact ? fcgpu::kStageLead + (_plan.start & 15u) : 0u;
         const size_t per = _capture == fcgpu::kCaptureWhole ? 1536 : _capture;
-        _outputs = FCGPU_OUT_VERDICT | FCGPU_OUT_HASH | FCGPU_OUT_ANNO |
+        // IPv4 chains: 8-B annotations (half the bytes written back per packet)
+        const bool a8 = (_cfg.check_mode == FCGPU_CHECK_IP4 || _cfg.check_mode == FCGPU_MARK_IP4) &&
+                        _cfg.offset >= 0 && _cfg.offset <= 255;
+        _outputs = FCGPU_OUT_VERDICT | FCGPU_OUT_HASH | (a8 ? FCGPU_OUT_ANNO8 : FCGPU_OUT_ANNO) |
                    (_partition == FCGPU_PART_TILE ? FCGPU_OUT_TILE_PERM | FCGPU_OUT_TILE_COUNT
                                                   : FCGPU_OUT_PERM | FCGPU_OUT_PORT_START) |
                    (_flow_cap ? FCGPU_OUT_FLOWID : 0u) | (_cfg.rewrite ? FCGPU_OUT_IP_RW : 0u);
@@ -599,6 +602,7 @@ class RxCore {
         uint16_t *verdict = nullptr, *tile_count = nullptr;
         uint32_t *hash = nullptr, *perm = nullptr, *start = nullptr, *flowid = nullptr, *iprw = nullptr;
         fcgpu_anno *anno = nullptr;
+        const fcgpu_anno8 *anno8 = nullptr;    // FCGPU_OUT_ANNO8 (IPv4 chains) instead of anno
         uint8_t *tperm = nullptr;
 
         bool alloc(uint32_t cap, size_t frame_bytes, size_t res_bytes) {
@@ -619,11 +623,12 @@ class RxCore {
             desc = nullptr;
         }
         // point the result arrays at their place in res for an n-packet batch
-        void map(const fcgpu_block_layout &L) {
+        void map(const fcgpu_block_layout &L, bool a8) {
             auto at = [this](size_t o) -> void * { return o == FCGPU_OUT_ABSENT ? nullptr : res + o; };
             verdict = (uint16_t *)at(L.verdict);
             hash = (uint32_t *)at(L.hash);
-            anno = (fcgpu_anno *)at(L.anno);
+            anno = a8 ? nullptr : (fcgpu_anno *)at(L.anno);
+            anno8 = a8 ? (const fcgpu_anno8 *)at(L.anno) : nullptr;
             perm = (uint32_t *)at(L.perm);
             start = (uint32_t *)at(L.port_start);
             tile_count = (uint16_t *)at(L.tile_count);
@@ -832,7 +837,12 @@ class RxCore {
         for (uint32_t i = b; i < e; ++i) {
             Packet *p = s.pkts[i];
             if (i + kAhead < s.n) prefetch_packet(s.pkts[i + kAhead]);
-            const fcgpu_anno &a = s.anno[i];
+            fcgpu_anno a8v;
+            if (s.anno8) {                                // IPv4 chain: the 8-B form
+                const fcgpu_anno8 &q = s.anno8[i];
+                a8v = fcgpu_anno{q.dst_ip, q.length, 0, q.nh, (uint16_t)(q.nh + q.thl), 0, 4, 0};
+            }
+            const fcgpu_anno &a = s.anno8 ? a8v : s.anno[i];
             const uint32_t reason = s.verdict[i] & 0xff;
             if (_color >= 0) P::set_anno_u8(p, P::kPaint, (uint8_t)_color);     // SET_PAINT_ANNO
             if (autom && reason != FCGPU_R_VLAN_REJECT)
@@ -898,7 +908,7 @@ class RxCore {
             return;
         }
         s.holes = false;
-        s.map(L);
+        s.map(L, (_outputs & FCGPU_OUT_ANNO8) != 0);
         const uint32_t nb = _cfg.nports + 1;
         if (_partition == FCGPU_PART_GLOBAL) {
             annotate(s, 0, n);

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 20
+#define FCGPU_ABI_VERSION 21
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -329,6 +329,17 @@ int  fcgpu_span_poll(fcgpu_ctx *ctx, uint32_t slot);
 #define FCGPU_OUT_TILE_PERM  (1u << 6)   /* TILE                                         */
 #define FCGPU_OUT_FLOWID     (1u << 7)
 #define FCGPU_OUT_IP_RW      (1u << 8)
+/* Instead of FCGPU_OUT_ANNO, for the IPv4 check modes (CHECK_IP4 / MARK_IP4,
+ * OFFSET < 256): 8-B annotations (fcgpu_anno8) at the layout's `anno`
+ * offset -- half the bytes written back per packet. ipver is 4, vlan_tci and
+ * ip6_nxt 0 for these modes; th = nh + thl. */
+#define FCGPU_OUT_ANNO8      (1u << 9)
+typedef struct fcgpu_anno8 {
+    uint32_t dst_ip;          /* as fcgpu_anno                                            */
+    uint16_t length;          /* as fcgpu_anno                                            */
+    uint8_t  nh;              /* as fcgpu_anno (< 256)                                    */
+    uint8_t  thl;             /* th - nh                                                  */
+} fcgpu_anno8;
 /* Not an output: this one submission goes through copies (H2D of h_in, D2H
  * of the results) whatever the span mode -- never zero-copy, never the shared
  * queue. What an element re-submits a failed batch with (SURVEY 8(b) Errors). */

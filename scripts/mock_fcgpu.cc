@@ -76,7 +76,8 @@ int fcgpu_block_layout_for(const fcgpu_ctx *c, uint32_t n, uint32_t outputs, uin
     };
     put(L->verdict, FCGPU_OUT_VERDICT, 2ull * n);
     put(L->hash, FCGPU_OUT_HASH, 4ull * n);
-    put(L->anno, FCGPU_OUT_ANNO, sizeof(fcgpu_anno) * n);
+    if (outputs & FCGPU_OUT_ANNO8) put(L->anno, FCGPU_OUT_ANNO8, sizeof(fcgpu_anno8) * n);
+    else put(L->anno, FCGPU_OUT_ANNO, sizeof(fcgpu_anno) * n);
     put(L->perm, FCGPU_OUT_PERM, 4ull * n);
     put(L->port_start, FCGPU_OUT_PORT_START, 4ull * (FCGPU_MAX_PORTS + 2));
     put(L->tile_count, FCGPU_OUT_TILE_COUNT, 2ull * nb * tiles);
@@ -109,11 +110,18 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t, const void *h_in, size_t, si
     for (uint32_t i = 0; i < n; ++i) {
         if (L.verdict != FCGPU_OUT_ABSENT) ((uint16_t *)(o + L.verdict))[i] = FCGPU_R_OK;
         if (L.hash != FCGPU_OUT_ABSENT) ((uint32_t *)(o + L.hash))[i] = 0x9e3779b1u * (i + 1);
-        if (L.anno != FCGPU_OUT_ABSENT) {
+        const uint32_t len = (outputs & FCGPU_SUBMIT_DESC32) ? desc[i] >> 16 : desc[2 * i + 1];
+        if (L.anno != FCGPU_OUT_ABSENT && (outputs & FCGPU_OUT_ANNO8)) {
+            fcgpu_anno8 &a = ((fcgpu_anno8 *)(o + L.anno))[i];
+            a.dst_ip = 0x0200000au;
+            a.length = (uint16_t)len;
+            a.nh = (uint8_t)c->cfg.offset;
+            a.thl = 20;
+        } else if (L.anno != FCGPU_OUT_ABSENT) {
             fcgpu_anno &a = ((fcgpu_anno *)(o + L.anno))[i];
             memset(&a, 0, sizeof a);
             a.dst_ip = 0x0200000au;
-            a.length = desc[2 * i + 1];
+            a.length = (uint16_t)len;
             a.nh = (uint16_t)c->cfg.offset;
             a.th = (uint16_t)(c->cfg.offset + 20);
             a.ipver = 4;

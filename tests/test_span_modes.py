@@ -427,3 +427,55 @@ def test_gpu_auto_shared_queue_programs_and_flows(oracle):
                 x.free()
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [N.SPAN_COPY, N.SPAN_ZEROCOPY])
+def test_gpu_block_anno8_matches_anno(oracle, mode):
+    """FCGPU_OUT_ANNO8 (IPv4 check modes): the 8-B annotations decode to the
+    fields of the 16-B ones (dst_ip, length, nh, th) for every packet, IP
+    options and header errors included; refused for other check modes."""
+    lib = N.load()
+    b = synth.c4(5000, seed=660)
+    synth.add_ip_options(b, 0.2, seed=661)
+    synth.inject_errors(b, 0.03, seed=662)
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=8)
+    c = N.Context(0, 8192, cfg)
+    try:
+        assert lib.fcgpu_span_mode(c.h, mode) == N.OK
+        blk = Block(lib, c.h, b, 8192)
+        got = {}
+        for name, outs in (("a16", OUTS | N.OUT_ANNO), ("a8", OUTS | N.OUT_ANNO8)):
+            L = N.fcgpu_block_layout()
+            assert lib.fcgpu_block_layout_for(c.h, b.n, outs, N.PART_TILE, C.byref(L)) == N.OK
+            out = lib.fcgpu_host_alloc(L.bytes)
+            res = np.ctypeslib.as_array(C.cast(out, C.POINTER(C.c_uint8)), shape=(L.bytes,))
+            res[:] = 0xEE
+            rc = lib.fcgpu_span_submit_block(c.h, 0, blk.pin, blk.in_bytes, 0, blk.frames_off, b.n, out, outs,
+                                             N.PART_TILE)
+            assert rc == N.OK, lib.fcgpu_last_error(c.h)
+            assert lib.fcgpu_span_wait(c.h, 0) == N.OK
+            width = 16 if name == "a16" else 8
+            got[name] = res[L.anno:L.anno + width * b.n].copy()
+            got[name + "_v"] = res[L.verdict:L.verdict + 2 * b.n].view(np.uint16).copy()
+            lib.fcgpu_host_free(out)
+        a16 = got["a16"].view(N.anno_dtype())
+        a8 = got["a8"].view(np.dtype([("dst_ip", "<u4"), ("length", "<u2"), ("nh", "u1"), ("thl", "u1")]))
+        ok = (got["a16_v"] & 0xFF) == N.R_OK
+        assert ok.sum() > 0.8 * b.n and np.array_equal(got["a16_v"], got["a8_v"])
+        assert np.array_equal(a8["dst_ip"][ok], a16["dst_ip"][ok])
+        assert np.array_equal(a8["length"][ok], a16["length"][ok])
+        assert np.array_equal(a8["nh"][ok].astype(np.uint16), a16["nh"][ok])
+        assert np.array_equal(a8["nh"][ok].astype(np.uint16) + a8["thl"][ok], a16["th"][ok])
+        exp = oracle.process_batch(cfg, b)
+        assert np.array_equal(a8["dst_ip"][ok], exp["anno"]["dst_ip"][ok])
+    finally:
+        c.close()
+    a = N.Context(0, 8192, N.make_cfg(check_mode=N.CHECK_AUTO, offset=0, classify=N.CLS_LB_HASH, nports=4))
+    try:
+        blk = Block(lib, a.h, b, 8192)
+        rc = lib.fcgpu_span_submit_block(a.h, 0, blk.pin, blk.in_bytes, 0, blk.frames_off, b.n, blk.out,
+                                         OUTS | N.OUT_ANNO8, N.PART_TILE)
+        assert rc == N.EINVAL
+    finally:
+        a.close()
