@@ -119,6 +119,8 @@ for s in "${ST[@]}"; do
     el_align) ALT=scripts/mock/align16/libfcclick.so step el_align 900 bash scripts/el_ab_lib.sh 3 ;;
     # 4-B descriptors (in-tree) against 8-B (scripts/mock/desc8)
     el_desc) ALT=scripts/mock/desc8/libfcclick.so step el_desc 900 bash scripts/el_ab_lib.sh 3 ;;
+    # 8-B IPv4 annotations (in-tree) against 16-B (scripts/mock/anno16)
+    el_anno) ALT=scripts/mock/anno16/libfcclick.so step el_anno 900 bash scripts/el_ab_lib.sh 3 ;;
     # the element's defaults at 1-16 threads, two interleaved rounds
     el_default) step el_default 600 bash -c 'for r in 1 2; do for t in 1 2 4 8 12 16; do timeout -k 5 120 python scripts/element_threads.py $t || exit $?; done; done' ;;
     # the element at 16 threads (default BATCH/ZEROCOPY/SLOTS): rate, then a kernel trace
