@@ -96,6 +96,14 @@ class fcgpu_anno(C.Structure):
     ]
 
 
+class fcgpu_anno8(C.Structure):
+    _fields_ = [("dst_ip", C.c_uint32), ("length", C.c_uint16), ("nh", C.c_uint8), ("thl", C.c_uint8)]
+
+
+class fcgpu_xmeta(C.Structure):
+    _fields_ = [("off", C.c_uint32), ("length", C.c_uint32), ("src_index", C.c_uint32), ("src_rank", C.c_uint32)]
+
+
 ANNO_DTYPE = None   # numpy structured dtype, set lazily (numpy import is optional here)
 
 

@@ -48,7 +48,7 @@ def test_field_offsets_match_c_compiler(tmp_path):
     structs = {"fcgpu_cfg": N.fcgpu_cfg, "fcgpu_anno": N.fcgpu_anno, "fcgpu_out": N.fcgpu_out,
                "fcgpu_step": N.fcgpu_step, "fcgpu_job": N.fcgpu_job, "fcgpu_block_layout": N.fcgpu_block_layout,
                "fcgpu_mbuf_layout": N.fcgpu_mbuf_layout, "fcgpu_flow_config": N.fcgpu_flow_config,
-               "fcgpu_flow_stat": N.fcgpu_flow_stat}
+               "fcgpu_flow_stat": N.fcgpu_flow_stat, "fcgpu_anno8": N.fcgpu_anno8, "fcgpu_xmeta": N.fcgpu_xmeta}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "fastclick_gpu.h"', "int main(void) {"]
     for sname, st in structs.items():
         lines.append(f'printf("{sname} sizeof %zu\\n", sizeof({sname}));')
