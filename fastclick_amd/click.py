@@ -19,6 +19,15 @@ from . import _native as N
 _lib = None
 
 
+class fcclick_event(C.Structure):
+    _fields_ = [("t_ns", C.c_uint64), ("kind", C.c_uint32), ("count", C.c_uint32)]
+
+
+EV_BURST, EV_READ = 0, 1
+HANDLERS = ("count", "drops", "drop_details", "port_counts", "flow_count", "flow_count_fids", "flow_drops",
+            "gpu_errors", "gpu_retries", "error")
+
+
 class fcclick_result(C.Structure):
     _fields_ = [("out_port", C.c_void_p), ("out_seq", C.c_void_p), ("out_agg", C.c_void_p),
                 ("out_dst", C.c_void_p), ("out_len", C.c_void_p), ("out_nh", C.c_void_p),
@@ -53,6 +62,11 @@ def load():
     lib.fcclick_run_clocked.restype = C.c_int
     lib.fcclick_run_clocked.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                         C.c_void_p, C.POINTER(fcclick_result), C.c_char_p, C.c_size_t]
+    if hasattr(lib, "fcclick_run_events"):         # absent from older A/B builds of the harness
+        lib.fcclick_run_events.restype = C.c_int
+        lib.fcclick_run_events.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                           C.POINTER(fcclick_event), C.c_uint32, C.POINTER(fcclick_result),
+                                           C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
     if hasattr(lib, "fcclick_stage_compact"):      # absent from older A/B builds of the harness
         lib.fcclick_stage_compact.restype = C.c_int
         lib.fcclick_stage_compact.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
@@ -115,14 +129,21 @@ def stage_compact(conf: str, batch, fill=None):
     from . import synth
     lib = load()
     n = batch.n
-    cap = 256 + 128 * n + synth.ARENA_PAD
-    out = np.zeros(cap, np.uint8) if fill is None else np.ascontiguousarray(fill[:cap], dtype=np.uint8).copy()
+    # a record holds at most max(frame, OFFSET + 60-B header + 16-B L4 tail)
+    # bytes plus its 16-B packing slack (capture.hh stage_record_size): room
+    # for every frame whatever the chain (OFFSET < 300 here)
+    lens = np.asarray(batch.desc[:, 1], dtype=np.int64) if n else np.zeros(0, np.int64)
+    cap = 256 + int((np.maximum(lens, 384) + 32).sum()) + synth.ARENA_PAD
+    out = np.zeros(cap, np.uint8)
+    if fill is not None:
+        f = np.asarray(fill, dtype=np.uint8).ravel()[:cap]
+        out[:len(f)] = f
     desc = np.zeros((n, 2), np.uint32)
     used = C.c_size_t()
     err = C.create_string_buffer(512)
     arena = np.ascontiguousarray(batch.arena)
     src = np.ascontiguousarray(batch.desc, dtype=np.uint32)
-    rc = lib.fcclick_stage_compact(conf.encode(), arena.ctypes.data, src.ctypes.data, n, out.ctypes.data, cap,
+    rc = lib.fcclick_stage_compact(conf.encode(), arena.ctypes.data, src.ctypes.data, n, out.ctypes.data, out.size,
                                    desc.ctypes.data, C.byref(used), err, 512)
     if rc == -2:
         return None
@@ -135,6 +156,55 @@ PER_PACKET = 0xFFFFFFFF   # burst value: the source calls push(0, p) per packet 
 TIMER_FLUSH = 1           # fcclick_run_ex flag: end with the element's timer, not flush()
 
 
+def parse_handlers(text: str) -> dict:
+    """"name=value" lines (a value may span lines) -> {name: value}."""
+    handlers = {}
+    name = None
+    for line in text.splitlines():
+        if "=" in line and line.split("=", 1)[0] in HANDLERS:
+            name, val = line.split("=", 1)
+            handlers[name] = val
+        elif name is not None:
+            handlers[name] += "\n" + line
+    return handlers
+
+
+class _Run:
+    """The per-packet result arrays one harness run fills (fcclick_result)."""
+
+    def __init__(self, batch):
+        n = batch.n
+        self.n = n
+        self.arena = np.ascontiguousarray(batch.arena)
+        self.desc = np.ascontiguousarray(batch.desc, dtype=np.uint32)
+        self.out = {k: np.zeros(n, dt) for k, dt in (("port", np.uint32), ("seq", np.uint32), ("agg", np.uint32),
+                                                     ("dst", np.uint32), ("len", np.uint32), ("nh", np.int32),
+                                                     ("paint", np.uint8), ("flow", np.uint32),
+                                                     ("ip8", np.uint32), ("batch", np.uint32))}
+        self.nb = np.zeros(1, np.uint32)
+        self.parked = np.zeros(1, np.uint32)
+        self.hbuf = C.create_string_buffer(4096)
+        o = self.out
+        self.res = fcclick_result(o["port"].ctypes.data, o["seq"].ctypes.data, o["agg"].ctypes.data,
+                                  o["dst"].ctypes.data, o["len"].ctypes.data, o["nh"].ctypes.data,
+                                  self.nb.ctypes.data, C.cast(self.hbuf, C.c_char_p), 4096,
+                                  o["paint"].ctypes.data, o["flow"].ctypes.data, o["ip8"].ctypes.data,
+                                  self.parked.ctypes.data, o["batch"].ctypes.data)
+        self.err = C.create_string_buffer(512)
+
+    def finish(self, rc: int, allow_error: bool) -> dict:
+        if rc == -1:
+            raise ConfigError(self.err.value.decode())
+        if rc != 0 and not allow_error:
+            raise RuntimeError(f"element runtime error: {self.err.value.decode()}")
+        out = self.out
+        out["error"] = self.err.value.decode() if rc != 0 else ""
+        out["batches"] = int(self.nb[0])
+        out["parked"] = int(self.parked[0])
+        out["handlers"] = parse_handlers(self.hbuf.value.decode())
+        return out
+
+
 def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1, timer_flush: bool = False,
                 burst_ns=None, allow_error: bool = False):
     """Source(batch, BURST) -> conf => sinks. burst_ns: the element's clock (ns)
@@ -143,48 +213,40 @@ def run_element(conf: str, batch, *, burst: int = 32, nsinks: int = 1, timer_flu
     failed batch cost) returns its results with the message in out["error"]
     instead of raising."""
     lib = load()
-    n = batch.n
-    arena = np.ascontiguousarray(batch.arena)
-    desc = np.ascontiguousarray(batch.desc, dtype=np.uint32)
-    out = {k: np.zeros(n, dt) for k, dt in (("port", np.uint32), ("seq", np.uint32), ("agg", np.uint32),
-                                            ("dst", np.uint32), ("len", np.uint32), ("nh", np.int32),
-                                            ("paint", np.uint8), ("flow", np.uint32), ("ip8", np.uint32),
-                                            ("batch", np.uint32))}
-    nb = np.zeros(1, np.uint32)
-    parked = np.zeros(1, np.uint32)
-    hbuf = C.create_string_buffer(4096)
-    res = fcclick_result(out["port"].ctypes.data, out["seq"].ctypes.data, out["agg"].ctypes.data,
-                         out["dst"].ctypes.data, out["len"].ctypes.data, out["nh"].ctypes.data,
-                         nb.ctypes.data, C.cast(hbuf, C.c_char_p), 4096, out["paint"].ctypes.data,
-                         out["flow"].ctypes.data, out["ip8"].ctypes.data, parked.ctypes.data,
-                         out["batch"].ctypes.data)
-    err = C.create_string_buffer(512)
+    r = _Run(batch)
     if burst_ns is not None:
         clock = np.ascontiguousarray(burst_ns, dtype=np.uint64)
-        assert len(clock) >= -(-n // burst) and not timer_flush
-        rc = lib.fcclick_run_clocked(conf.encode(), arena.ctypes.data, desc.ctypes.data, n, burst, nsinks,
-                                     clock.ctypes.data, C.byref(res), err, 512)
+        assert len(clock) >= -(-r.n // burst) and not timer_flush
+        rc = lib.fcclick_run_clocked(conf.encode(), r.arena.ctypes.data, r.desc.ctypes.data, r.n, burst, nsinks,
+                                     clock.ctypes.data, C.byref(r.res), r.err, 512)
     else:
-        rc = lib.fcclick_run_ex(conf.encode(), arena.ctypes.data, desc.ctypes.data, n, burst, nsinks,
-                                TIMER_FLUSH if timer_flush else 0, C.byref(res), err, 512)
-    if rc == -1:
-        raise ConfigError(err.value.decode())
-    if rc != 0 and not allow_error:
-        raise RuntimeError(f"element runtime error: {err.value.decode()}")
-    out["error"] = err.value.decode() if rc != 0 else ""
-    handlers = {}
-    name = None
-    for line in hbuf.value.decode().splitlines():
-        if "=" in line and line.split("=", 1)[0] in ("count", "drops", "drop_details", "port_counts",
-                                                                "flow_count", "flow_drops", "gpu_errors",
-                                                                "gpu_retries", "error"):
-            name, val = line.split("=", 1)
-            handlers[name] = val
-        elif name is not None:
-            handlers[name] += "\n" + line
-    out["batches"] = int(nb[0])
-    out["parked"] = int(parked[0])
-    out["handlers"] = handlers
+        rc = lib.fcclick_run_ex(conf.encode(), r.arena.ctypes.data, r.desc.ctypes.data, r.n, burst, nsinks,
+                                TIMER_FLUSH if timer_flush else 0, C.byref(r.res), r.err, 512)
+    return r.finish(rc, allow_error)
+
+
+def run_element_events(conf: str, batch, events, *, nsinks: int = 1, allow_error: bool = False):
+    """A scripted run on a virtual clock (fcclick_run_events): `events` is a
+    list of ("burst", t_ns, count) -- the next `count` packets as one
+    PacketBatch at time t_ns -- and ("read", t_ns) -- the element's Timer fires
+    at t_ns, then every handler is read. Returns run_element's dict plus
+    out["reads"]: one {handler: value} dict per read, in order."""
+    lib = load()
+    r = _Run(batch)
+    ev = (fcclick_event * len(events))()
+    for k, e in enumerate(events):
+        if e[0] == "burst":
+            ev[k] = fcclick_event(int(e[1]), EV_BURST, int(e[2]))
+        elif e[0] == "read":
+            ev[k] = fcclick_event(int(e[1]), EV_READ, 0)
+        else:
+            raise ValueError(f"unknown event {e!r}")
+    cap = 4096 * (1 + sum(1 for e in events if e[0] == "read"))
+    rbuf = C.create_string_buffer(cap)
+    rc = lib.fcclick_run_events(conf.encode(), r.arena.ctypes.data, r.desc.ctypes.data, r.n, nsinks, ev,
+                                len(events), C.byref(r.res), rbuf, cap, r.err, 512)
+    out = r.finish(rc, allow_error)
+    out["reads"] = [parse_handlers(block) for block in rbuf.value.decode().split("--\n")[:-1]]
     return out
 
 

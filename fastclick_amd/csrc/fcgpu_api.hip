@@ -434,12 +434,14 @@ static bool rx_launch_ok(int part, const RxLaunch &L, uint32_t grid) {
     };
     if (L.njobs <= 1)
         return batch_ok(L.A.arena, L.A.desc, L.A.n, L.A.tile_count, L.A.tilecnt) && L.A.ctr &&
-               grid <= (L.A.n + kTile - 1) / kTile;
+               !(L.A.layout & ~kLayKnown) && grid <= (L.A.n + kTile - 1) / kTile;
     if (L.njobs > kMaxFuse) return false;
     uint32_t tiles = 0;
     for (uint32_t k = 0; k < L.njobs; ++k) {
         const RxJob &J = L.job[k];
-        if (!batch_ok(J.arena, J.desc, J.n, J.tile_count, J.tilecnt) || !J.ctr || J.tile0 != tiles) return false;
+        if (!batch_ok(J.arena, J.desc, J.n, J.tile_count, J.tilecnt) || !J.ctr || J.tile0 != tiles ||
+            (J.layout & ~kLayKnown))
+            return false;
         tiles += (J.n + kTile - 1) / kTile;
     }
     return grid <= tiles;
@@ -680,9 +682,14 @@ static int jit_install(fcgpu_ctx *c) {
 
 // The compiled kernel for an instantiation; one the module lacks (the
 // configuration changed since) is added by recompiling. nullptr: interpret.
+static bool agg_queued(const fcgpu_ctx *c);
 static hipFunction_t jit_function(fcgpu_ctx *c, int key) {
     auto it = c->jit.fn.find(key);
     if (it != c->jit.fn.end()) return it->second;
+    // a rebuild replaces the module, whose functions this context's queued
+    // shared-queue submissions hold until they launch: interpret instead
+    // (identical results) while one is queued
+    if (agg_queued(c)) return nullptr;
     std::vector<int> keys = c->jit_keys;
     keys.push_back(key);
     if (jit_build(c, keys) != FCGPU_OK) return nullptr;
@@ -1157,8 +1164,10 @@ static hipError_t flow_pass(fcgpu_ctx *c, const FlowArgs &F, uint32_t n, hipStre
 }
 
 // One batch's launches on stream s (arguments checked, device current).
+// layout: kLay* bits of the batch's descriptors and annotations (0 through
+// the public entry points: {off, len} descriptors, fcgpu_anno).
 static int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, uint32_t n,
-                       const fcgpu_out *o, hipStream_t s) {
+                       const fcgpu_out *o, hipStream_t s, uint32_t layout = 0) {
     if (n == 0) return FCGPU_OK;
     const uint32_t ntiles = (n + kTile - 1) / kTile;
     const uint32_t nports = c->cfg.nports;
@@ -1194,6 +1203,7 @@ static int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_d
         a.fl.epoch = c->flow_epoch;
     }
     a.ip_rw = o->ip_rw;
+    a.layout = layout;
 
     // sampled timing: the timing_every-th, 2*timing_every-th, ... launch since
     // fcgpu_set_timing (not the first: a start event ahead of an idle queue's
@@ -1300,7 +1310,9 @@ static bool outputs_overlap(const fcgpu_out &x, const fcgpu_out &y) {
 
 // Jobs grp[0..g) (fusable, one stream, one partition shape, disjoint outputs)
 // as one k_rx launch.
-static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, hipStream_t s) {
+// lay: each job's kLay* bits (nullptr: all 0, the public layouts).
+static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, hipStream_t s,
+                         const uint32_t *lay = nullptr) {
     RxLaunch L;
     const fcgpu_out &o0 = grp[0]->out;
     const int part = out_part(&o0);
@@ -1360,6 +1372,7 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
         J.ctr = c->d_ctr;
         J.n = j.n;
         J.tile0 = tiles;
+        J.layout = lay ? lay[k] : 0u;
         tiles += (j.n + kTile - 1) / kTile;
     }
     L.job_tiles = L.job[0].n ? (L.job[0].n + kTile - 1) / kTile : 0u;
@@ -1372,6 +1385,7 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
     a.desc = L.job[0].desc;
     a.n = L.job[0].n;
     a.ntiles = (a.n + kTile - 1) / kTile;
+    a.layout = L.job[0].layout;
     if (part == kPartGlobal) a.tilecnt = L.job[0].tilecnt;
     // sampled timing counts batches: a fused launch is timed when it covers
     // a multiple of timing_every
@@ -1893,6 +1907,7 @@ struct AggItem {
     fcgpu_ctx *c;
     uint32_t slot;
     fcgpu_job job;            // device (mapped) addresses
+    uint32_t layout;          // kLay* bits of job's descriptors and annotations
     // the launch inputs, taken on the owner's thread at submit time: the
     // launch may happen on another context's thread, later
     DevCfg dcfg;
@@ -2008,6 +2023,7 @@ static void agg_take_locked(AggQueue &q, std::vector<AggIssue> &out) {
             J.ctr = it.ctr;
             J.n = j.n;
             J.tile0 = tiles;
+            J.layout = it.layout;
             tiles += (j.n + kTile - 1) / kTile;
         }
         is.tiles = tiles;
@@ -2029,6 +2045,7 @@ static void agg_take_locked(AggQueue &q, std::vector<AggIssue> &out) {
         a.tile_perm = J0.tile_perm;
         a.ip_rw = J0.ip_rw;
         a.ctr = J0.ctr;
+        a.layout = J0.layout;
         const uint32_t si = q.rr++ % 4;
         if (!q.st[si] && hipStreamCreateWithFlags(&q.st[si], hipStreamNonBlocking) != hipSuccess) {
             (void)hipGetLastError();
@@ -2113,11 +2130,12 @@ static void agg_release(int device) {
 // Queue one zero-copy block submission (device addresses in j). Once queued
 // the submission is the owner's to wait for: a failed launch (of its group or
 // another) is reported by that wait (AggLaunch::state), never by this call.
-static int agg_submit(fcgpu_ctx *c, uint32_t slot, const fcgpu_job &j) {
+static int agg_submit(fcgpu_ctx *c, uint32_t slot, const fcgpu_job &j, uint32_t layout) {
     AggItem it{};
     it.c = c;
     it.slot = slot;
     it.job = j;
+    it.layout = layout;
     it.dcfg = c->dcfg;
     it.cm = c->cfg.check_mode;
     it.ck = c->cfg.checksum != 0;
@@ -2301,10 +2319,10 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
     const size_t dsz = desc32 ? 4 : 8;
     if (desc_off + dsz * n > in_bytes || frames_off > in_bytes || (desc_off & (dsz - 1)))
         return fail(c, FCGPU_EINVAL, "block: descriptors (aligned to their size) or frames outside in_bytes");
-    // the kernels read DESC32 descriptors through a pointer tagged in its low bit
-    auto descp = [desc32, desc_off](uint8_t *base) {
-        return reinterpret_cast<const uint32_t *>(reinterpret_cast<uintptr_t>(base + desc_off) | (desc32 ? 1u : 0u));
-    };
+    // the kernels read the descriptors and store the annotations in the layout
+    // these bits name (RxJob::layout), never through tagged pointers
+    const uint32_t layout = (desc32 ? kLayDesc32 : 0u) | ((outputs & FCGPU_OUT_ANNO8) ? kLayAnno8 : 0u);
+    auto descp = [desc_off](uint8_t *base) { return reinterpret_cast<const uint32_t *>(base + desc_off); };
     if (in_bytes - frames_off > 0xffffffffull - kArenaPad) return fail(c, FCGPU_EINVAL, "frames larger than 4 GiB");
     SpanSlot &sp = c->span[slot];
     if (sp.busy) return fail(c, FCGPU_EINVAL, "span slot busy: fcgpu_span_wait it first");
@@ -2376,9 +2394,7 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
     fcgpu_out d{};
     d.verdict = (uint16_t *)at(L.verdict);
     d.hash = (uint32_t *)at(L.hash);
-    d.anno = (fcgpu_anno *)at(L.anno);
-    if (d.anno && (outputs & FCGPU_OUT_ANNO8))    // the kernels store fcgpu_anno8 through a tagged pointer
-        d.anno = reinterpret_cast<fcgpu_anno *>(reinterpret_cast<uintptr_t>(d.anno) | 1u);
+    d.anno = (fcgpu_anno *)at(L.anno);     // fcgpu_anno8 entries with kLayAnno8
     d.perm = (uint32_t *)at(L.perm);
     d.port_start = (uint32_t *)at(L.port_start);
     d.tile_count = (uint16_t *)at(L.tile_count);
@@ -2394,9 +2410,10 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
         j.out = d;
         int rc = check_process(c, j.arena, j.desc, n, &j.out);
         if (rc != FCGPU_OK) return rc;
-        return agg_submit(c, slot, j);
+        return agg_submit(c, slot, j, layout);
     }
-    int rc = fcgpu_process(c, din + frames_off, descp(din), n, &d, s);
+    int rc = check_process(c, din + frames_off, descp(din), n, &d);
+    if (rc == FCGPU_OK) rc = process_one(c, din + frames_off, descp(din), n, &d, s, layout);
     if (rc != FCGPU_OK) return rc;
     if (!zc) HIPCHK(c, hipMemcpyAsync(h_out, sp.d_res, L.bytes, hipMemcpyDeviceToHost, s));
     uint32_t ns = 0;
@@ -2474,6 +2491,15 @@ int fcgpu_launch_guard_selftest(void) {
     if (!rx_launch_ok(kPartTile, one(n), t) || !rx_launch_ok(kPartGlobal, one(n), t) ||
         !rx_launch_ok(kPartTile, fused(3, n), 3 * t))
         return -1;
+    {   // every known layout passes, alone and mixed within a launch
+        RxLaunch K = one(n);
+        K.A.layout = kLayKnown;
+        RxLaunch F = fused(3, n);
+        F.job[0].layout = kLayDesc32;
+        F.job[1].layout = kLayAnno8;
+        F.job[2].layout = kLayKnown;
+        if (!rx_launch_ok(kPartTile, K, t) || !rx_launch_ok(kPartTile, F, 3 * t)) return -1;
+    }
     int accepted = 0;
     RxLaunch L = one(n);
     L.A.tile_count = nullptr;                           // the r03_s17 fault: TILE stores through tile_count
@@ -2502,6 +2528,15 @@ int fcgpu_launch_guard_selftest(void) {
     L = fused(kMaxFuse, n);
     L.njobs = kMaxFuse + 1;
     accepted += rx_launch_ok(kPartTile, L, kMaxFuse * t);
+    L = one(n);
+    L.A.layout = kLayKnown + 1;                         // a layout bit no kernel knows
+    accepted += rx_launch_ok(kPartTile, L, t);
+    L = one(n);
+    L.A.layout = 0x80000000u;
+    accepted += rx_launch_ok(kPartTile, L, t);
+    L = fused(3, n);
+    L.job[2].layout = 4u;
+    accepted += rx_launch_ok(kPartTile, L, 3 * t);
     return accepted;
 }
 

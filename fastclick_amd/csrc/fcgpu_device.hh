@@ -109,6 +109,15 @@ constexpr uint32_t kFsQlen = 6;   // IMP: IDs the last maintainer run released (
 constexpr uint32_t kFlowMiss = 0xfffffffdu;
 constexpr uint32_t kSlotNone = 0xffffffffu;
 
+// A batch's descriptor and annotation layouts (RxArgs::layout, RxJob::layout):
+// kLayDesc32 -- FCGPU_SUBMIT_DESC32 descriptors, one uint32 per packet (offset
+// / 8 in bits 0-15, length in bits 16-31) instead of {u32 off, u32 len};
+// kLayAnno8 -- FCGPU_OUT_ANNO8 annotations, the 8-B fcgpu_anno8 instead of
+// fcgpu_anno. Any other bit is refused by the host launch guard.
+constexpr uint32_t kLayDesc32 = 1u;
+constexpr uint32_t kLayAnno8 = 2u;
+constexpr uint32_t kLayKnown = kLayDesc32 | kLayAnno8;
+
 struct RxArgs {
     const uint8_t *arena;
     const uint2 *desc;
@@ -124,6 +133,7 @@ struct RxArgs {
     unsigned long long *ctr;   // [FCGPU_CTR_SHARDS][FCGPU_NCOUNTERS]
     FlowArgs fl;               // FLOW instances only
     uint32_t *ip_rw;           // [n] rewritten IP header bytes 8..11 (cfg.rewrite)
+    uint32_t layout;           // kLay* bits: how desc and anno are laid out
     DevCfg cfg;
 };
 
@@ -861,24 +871,21 @@ __device__ __forceinline__ void glds16(const uint8_t *src, uint8_t *lds) {
                                      (__attribute__((address_space(3))) void *)lds, 16, 0, kWinCpol);
 }
 
-// Packet i's (offset, length) descriptor. A pointer with its low bit set
-// marks FCGPU_SUBMIT_DESC32 descriptors: one uint32 per packet, offset / 8 in
-// bits 0-15 and length in bits 16-31 (the bit is uniform over a batch).
-__device__ __forceinline__ uint2 load_desc(const uint2 *desc, uint32_t i) {
-    const unsigned long long p = reinterpret_cast<unsigned long long>(desc);   // (hiprtc: no uintptr_t)
-    if (p & 1u) {
-        const uint32_t w = reinterpret_cast<const uint32_t *>(p - 1ull)[i];
+// Packet i's (offset, length) descriptor, read in the batch's layout
+// (kLayDesc32: one uint32 per packet; the layout is uniform over a batch).
+__device__ __forceinline__ uint2 load_desc(const uint2 *desc, uint32_t i, uint32_t layout) {
+    if (layout & kLayDesc32) {
+        const uint32_t w = reinterpret_cast<const uint32_t *>(desc)[i];
         return make_uint2((w & 0xffffu) << 3, w >> 16);
     }
     return desc[i];
 }
 
-// Packet i's annotation: fcgpu_anno, or -- the pointer's low bit set
-// (FCGPU_OUT_ANNO8, IPv4 check modes) -- the 8-B fcgpu_anno8.
-__device__ __forceinline__ void store_anno(fcgpu_anno *a, uint32_t i, const fcgpu_anno &an) {
-    const unsigned long long p = reinterpret_cast<unsigned long long>(a);
-    if (p & 1u) {
-        reinterpret_cast<uint2 *>(p - 1ull)[i] =
+// Packet i's annotation: fcgpu_anno, or (kLayAnno8, IPv4 check modes) the
+// 8-B fcgpu_anno8.
+__device__ __forceinline__ void store_anno(fcgpu_anno *a, uint32_t i, const fcgpu_anno &an, uint32_t layout) {
+    if (layout & kLayAnno8) {
+        reinterpret_cast<uint2 *>(a)[i] =
             make_uint2(an.dst_ip, (uint32_t)an.length | ((uint32_t)(an.nh & 0xffu) << 16) |
                                       ((uint32_t)((an.th - an.nh) & 0xffu) << 24));
         return;
@@ -1142,10 +1149,11 @@ struct RxView {
     uint32_t *ip_rw;         // cfg.rewrite: the rewritten header bytes
     unsigned long long *ctr; // the batch's context's counter replicas
     uint32_t n, ntiles;
+    uint32_t layout;         // kLay* bits
 };
 __device__ __forceinline__ RxView rx_view(const RxArgs &A) {
     return RxView{A.arena, A.desc, A.verdict, A.hash, A.anno, A.perm, A.tile_count, A.tile_perm, A.tilecnt,
-                  A.ip_rw, A.ctr, A.n, A.ntiles};
+                  A.ip_rw, A.ctr, A.n, A.ntiles, A.layout};
 }
 
 // One 256-packet tile once its header window is in LDS: fused
@@ -1198,7 +1206,7 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, const RxView &V, const 
     if (live) {
         if (V.verdict) V.verdict[i] = (uint16_t)(r.reason | (r.port << 8));
         if (V.hash) V.hash[i] = r.hash;
-        if (V.anno) store_anno(V.anno, i, r.an);
+        if (V.anno) store_anno(V.anno, i, r.an, V.layout);
         bin = r.port;
         if (r.reason != FCGPU_R_OK) rslot = reason_slot(r.reason);
     }
@@ -1300,6 +1308,7 @@ struct RxJob {
     unsigned long long *ctr; // the counter replicas of the batch's context (a launch may carry
                              // the batches of several contexts with one configuration)
     uint32_t n, tile0;       // packets; first workgroup of the batch in the grid
+    uint32_t layout;         // kLay* bits of this batch (batches of one launch may differ)
 };
 struct RxLaunch {
     RxArgs A;                // njobs == 1: the batch; else the shared configuration
@@ -1347,6 +1356,7 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
         V.ctr = J.ctr;
         V.n = J.n;
         V.ntiles = (J.n + kTile - 1) / kTile;
+        V.layout = J.layout;
         tile = t;
         if (FLOW) {
             FL.miss_key += (size_t)j * L.flow_stride;
@@ -1359,7 +1369,7 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
     }
     const uint32_t i = tile * kTile + threadIdx.x;
     uint2 d = make_uint2(0, 0);
-    if (i < V.n) d = load_desc(V.desc, i);
+    if (i < V.n) d = load_desc(V.desc, i, V.layout);
     uint8_t *wl = s_win + wave * (kWave * kWin);
 #pragma unroll
     for (int k = 0; k < 4; ++k) glds16(win_src(V.arena, d.x, lane, k), wl + k * 1024);

@@ -273,6 +273,7 @@ template <uint32_t LPF>
 __global__ __launch_bounds__(kXThreads) void k_xpack(XPack X) {
     __shared__ uint32_t s_ps[FCGPU_MAX_PORTS + 1];
     __shared__ unsigned long long s_base[FCGPU_MAX_PORTS + 1];
+    __shared__ unsigned long long s_big;     // owners whose segment is 4 GiB or more
     uint32_t m = X.port_start[X.world];
     m = m < X.n ? m : X.n;
     const uint32_t j = blockIdx.x * (kXThreads / LPF) + threadIdx.x / LPF;
@@ -284,19 +285,28 @@ __global__ __launch_bounds__(kXThreads) void k_xpack(XPack X) {
         so = X.src[j];
     }
     if (threadIdx.x == 0) {
-        unsigned long long b = 0;
+        unsigned long long b = 0, big = 0;
         for (uint32_t d = 0; d <= X.world; ++d) {
             const uint32_t ps = X.port_start[d];
             s_ps[d] = ps < m ? ps : m;
             s_base[d] = b;
-            if (d < X.world) b += X.seg_bytes[d];
+            if (d < X.world) {
+                b += X.seg_bytes[d];
+                if (X.seg_bytes[d] > 0xffffffffull) big |= 1ull << d;
+            }
         }
+        s_big = big;
     }
     __syncthreads();
     if (j >= m) return;
     const uint32_t len = r.y;
     const uint64_t slot = xslot(len);
-    const uint64_t dst = s_base[xowner(s_ps, X.world, j)] + r.x;
+    const uint32_t own = xowner(s_ps, X.world, j);
+    // the record's 32-bit offset within a segment past 4 GiB is truncated:
+    // such a segment is not packed at all (the caller checks the plan's
+    // segment sizes, fastclick_amd/device.py exchange_pack)
+    if ((s_big >> own) & 1ull) return;
+    const uint64_t dst = s_base[own] + r.x;
     if (dst + slot > X.send_cap) return;           // a send buffer smaller than the plan: nothing past it
     const uintptr_t sa = reinterpret_cast<uintptr_t>(X.arena + so);
     const uint32_t sh = (uint32_t)(sa & 3u);

@@ -169,7 +169,17 @@ extern "C" int fcclick_parse_program(const char *text, fcgpu_step *steps, uint32
 
 static int run_graph(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n, uint32_t burst,
                      uint32_t nsinks, uint32_t flags, const uint64_t *burst_ns, fcclick_result *res, char *err,
-                     size_t errcap);
+                     size_t errcap, const fcclick_event *ev = nullptr, uint32_t nev = 0, char *reads = nullptr,
+                     size_t reads_cap = 0);
+
+static const char *const kHandlerNames[] = {"count",      "drops",           "drop_details", "port_counts",
+                                            "flow_count", "flow_count_fids", "flow_drops",   "gpu_errors",
+                                            "gpu_retries", "error"};
+static std::string read_all(Element *el) {
+    std::string h;
+    for (const char *name : kHandlerNames) h += std::string(name) + "=" + el->read_handler(name) + "\n";
+    return h;
+}
 
 extern "C" int fcclick_run_ex(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
                               uint32_t burst, uint32_t nsinks, uint32_t flags, fcclick_result *res, char *err,
@@ -186,9 +196,39 @@ extern "C" int fcclick_run_clocked(const char *conf, const uint8_t *arena, const
     return rc;
 }
 
+extern "C" int fcclick_run_events(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                                  uint32_t nsinks, const fcclick_event *ev, uint32_t nev, fcclick_result *res,
+                                  char *reads, size_t reads_cap, char *err, size_t errcap) {
+    if (!ev || !nev) {
+        copy_err("no events", err, errcap);
+        return -1;
+    }
+    uint64_t total = 0;
+    for (uint32_t k = 0; k < nev; ++k) {
+        if (ev[k].kind != FCCLICK_EV_BURST && ev[k].kind != FCCLICK_EV_READ) {
+            copy_err("unknown event kind", err, errcap);
+            return -1;
+        }
+        if (ev[k].kind == FCCLICK_EV_BURST) {
+            if (!ev[k].count) {
+                copy_err("an empty burst", err, errcap);
+                return -1;
+            }
+            total += ev[k].count;
+        }
+    }
+    if (total != n) {
+        copy_err("the bursts do not cover the n packets exactly", err, errcap);
+        return -1;
+    }
+    const int rc = run_graph(conf, arena, desc, n, 0, nsinks, 0, nullptr, res, err, errcap, ev, nev, reads, reads_cap);
+    ModelPolicy::virtual_ns.store(0);
+    return rc;
+}
+
 static int run_graph(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n, uint32_t burst,
                      uint32_t nsinks, uint32_t flags, const uint64_t *burst_ns, fcclick_result *res, char *err,
-                     size_t errcap) {
+                     size_t errcap, const fcclick_event *ev, uint32_t nev, char *reads, size_t reads_cap) {
     std::string e;
     auto el = make_element(conf, e);
     if (!el || el->initialize(e) < 0) {
@@ -213,10 +253,29 @@ static int run_graph(const char *conf, const uint8_t *arena, const uint32_t *des
     }
     const uint32_t headroom = 128;
     PacketPool pool(n ? n : 1, headroom + max_len(desc, n) + 64, headroom);
-    // FromDPDKDevice-style source: BURST packets per PacketBatch
-    for (uint32_t i = 0; i < n; i += burst) {
-        uint32_t m = n - i < burst ? n - i : burst;
-        if (burst_ns) ModelPolicy::virtual_ns.store(burst_ns[i / burst] ? burst_ns[i / burst] : 1);
+    // FromDPDKDevice-style source: BURST packets per PacketBatch -- or the
+    // events' bursts, with handler reads between them
+    std::vector<fcclick_event> evs;
+    if (ev) {
+        evs.assign(ev, ev + nev);
+    } else {
+        for (uint32_t i = 0; i < n; i += burst)
+            evs.push_back(fcclick_event{burst_ns ? burst_ns[i / burst] : 0, FCCLICK_EV_BURST,
+                                        n - i < burst ? n - i : burst});
+    }
+    std::string rd;
+    uint32_t i = 0;
+    for (const fcclick_event &e : evs) {
+        if (ev && e.t_ns) ModelPolicy::virtual_ns.store(e.t_ns);
+        else if (burst_ns) ModelPolicy::virtual_ns.store(e.t_ns ? e.t_ns : 1);
+        if (e.kind == FCCLICK_EV_READ) {
+            // the element's Timer fires at this time (the maintainer runs due,
+            // a partial batch due), then every handler is read
+            el->run_timer(ModelPolicy::now_ns());
+            rd += read_all(el.get()) + "--\n";
+            continue;
+        }
+        const uint32_t m = e.count;
         Packet *head = nullptr, *prev = nullptr;
         for (uint32_t j = 0; j < m; ++j) {
             Packet *p = pool.make(arena + desc[2 * (i + j)], desc[2 * (i + j) + 1]);
@@ -233,7 +292,9 @@ static int run_graph(const char *conf, const uint8_t *arena, const uint32_t *des
             }
         else
             el->push_batch(0, PacketBatch::make_from_list(head, prev, m));
+        i += m;
     }
+    if (reads && reads_cap) snprintf(reads, reads_cap, "%s", rd.c_str());
     if (flags & FCCLICK_TIMER_FLUSH) {
         // the source has stopped: only the element's Timer can release what it
         // still holds (MinBatch's timer, minbatch.cc:35,57-76)
@@ -249,13 +310,8 @@ static int run_graph(const char *conf, const uint8_t *arena, const uint32_t *des
     }
     if (res) {
         if (res->out_batches) *res->out_batches = nbatch;
-        if (res->handlers && res->handlers_cap) {
-            std::string h;
-            for (const char *name : {"count", "drops", "drop_details", "port_counts", "flow_count", "flow_drops",
-                                     "gpu_errors", "gpu_retries", "error"})
-                h += std::string(name) + "=" + el->read_handler(name) + "\n";
-            snprintf(res->handlers, res->handlers_cap, "%s", h.c_str());
-        }
+        if (res->handlers && res->handlers_cap)
+            snprintf(res->handlers, res->handlers_cap, "%s", read_all(el.get()).c_str());
     }
     std::string er = el->read_handler("error");
     // what the element still holds (TIMER -1 and no flush) is killed back into

@@ -67,8 +67,10 @@
 //                                            -- IMP: FlowIPManager_CuckooPP /
 //     FlowIPManagerIMP (CAPACITY, TIMEOUT, RECYCLE_INTERVAL): IDs from a free-ID
 //     stack, flows idle for TIMEOUT s expire (include/click/flow/
-//     virtualflowmanager.hh); the maintainer runs every RECYCLE_INTERVAL on the
-//     batches' clock (each submission first runs the runs that are due).
+//     virtualflowmanager.hh); the maintainer runs every RECYCLE_INTERVAL from
+//     the first batch on the element's clock: each submission first runs the
+//     runs that are due, and so does the element's Timer, which fires for
+//     them with no traffic as the reference's maintain_timer does.
 //   DEC_TTL, TTL_MULTICAST (default true), SET_CHECKSUM
 //                                            -- DecIPTTL / SetIPChecksum after the
 //     classifier (IPv4): TTL-expired packets (DecIPTTL output 1) join output N,
@@ -98,7 +100,8 @@
 //   ERROR_OUTPUT p (default -1: kill)          -- where the packets of a batch the
 //     GPU failed twice leave, unprocessed and in input order
 // Handlers: count, drops, drop_details (DETAILS true), port_counts,
-// flow_count, flow_drops, gpu_errors (packets of batches the GPU failed twice),
+// flow_count, flow_count_fids (IMP: the free-ID stack's entries, the
+// reference's count_fids), flow_drops, gpu_errors (packets of batches the GPU failed twice),
 // gpu_retries (batches re-submitted through copies), error (the last failure
 // that cost packets).
 #pragma once
@@ -363,6 +366,7 @@ class RxCore {
     }
 
     int64_t timer_us() const { return _timer_us; }
+    int error_output() const { return _error_output; }
     const fcgpu_cfg &device_cfg() const { return _cfg; }
     uint32_t nports() const { return _cfg.nports; }
 
@@ -466,8 +470,17 @@ class RxCore {
     // staged), and a partial batch staged at least TIMER us ago goes to the
     // device and completes too. Returns true while packets remain staged:
     // the caller reschedules the timer for due_ns().
+    // With IMP timeouts the Timer also runs the maintainer runs due by now,
+    // with no packet needed -- the reference's maintain_timer fires every
+    // RECYCLE_INTERVAL whether or not packets arrive
+    // (virtualflowmanager.hh:118-124,134-144), so idle flows expire and the
+    // handlers see it.
     template <class Emit>
     bool run_timer(uint64_t now_ns, Emit &&emit) {
+        if (_flow_cap && _flow_timeout) {
+            std::lock_guard<std::mutex> g(_mu);
+            if (_ctx) flow_catch_up(now_ns / 1000000ull);
+        }
         if (_timer_us < 0) return false;                  // TIMER -1: no timer
         Slot &s = _slot[_cur];
         if (s.n && now_ns >= due_ns()) {
@@ -482,6 +495,15 @@ class RxCore {
     }
     // ns at which the staged partial batch is due (valid while staged() > 0)
     uint64_t due_ns() const { return _slot[_cur].t_first + (uint64_t)(_timer_us < 0 ? 0 : _timer_us) * 1000ull; }
+    // IMP timeouts configured: the Timer also serves the maintainer
+    bool flow_timeouts() const { return _flow_cap && _flow_timeout; }
+    // The next maintainer run (IMP timeouts, once the first batch armed them):
+    // true and its time in *ns, for the Timer that must also fire for it.
+    bool maint_due_ns(uint64_t *ns) const {
+        if (!(_flow_cap && _flow_timeout && _maint_armed)) return false;
+        *ns = _next_maint_ms * 1000000ull;
+        return true;
+    }
     uint32_t staged() const { return _slot[_cur].n; }
     uint32_t held() const {
         uint32_t h = 0;
@@ -500,12 +522,14 @@ class RxCore {
     // threads on read like them).
     struct HostStats {
         uint64_t flows = 0;        // flow IDs issued (flow table)
+        uint64_t flow_fids = 0;    // IMP: entries on the free-ID stack, ID 0 included (count_fids)
         uint64_t flow_drops = 0;   // new flows killed, table full
         uint64_t gpu_errors = 0;   // packets of batches the GPU failed twice (killed or on ERROR_OUTPUT)
         uint64_t gpu_killed = 0;   // ... of which killed (no ERROR_OUTPUT)
         uint64_t gpu_retries = 0;  // batches re-submitted through copies after a failure
         HostStats &operator+=(const HostStats &o) {
             flows += o.flows;
+            flow_fids += o.flow_fids;
             flow_drops += o.flow_drops;
             gpu_errors += o.gpu_errors;
             gpu_killed += o.gpu_killed;
@@ -521,13 +545,19 @@ class RxCore {
     void counters(uint64_t (&c)[FCGPU_NCOUNTERS], HostStats &hs, std::string *error = nullptr) {
         memset(c, 0, sizeof c);
         uint32_t f = 0;
+        fcgpu_flow_stat st{};
         {
             std::lock_guard<std::mutex> g(_mu);
             if (_ctx) fcgpu_read_counters(_ctx, c, FCGPU_NCOUNTERS);
             if (_ctx && _flow_cap) fcgpu_flow_count(_ctx, &f);
+            if (_ctx && _flow_cap && _flow_mgr == FCGPU_FLOW_MGR_IMP) fcgpu_flow_stats(_ctx, &st);
             if (error) *error = _error;
         }
         hs.flows = f;
+        // flows_stack_i (virtualflowmanager.hh:33,389-391): the stack holds
+        // 0 .. cap-1 after initialization (:113-115), so it reads cap; ID 0 is
+        // on it but never handed out
+        hs.flow_fids = st.capacity ? (uint64_t)st.free_ids + 1 : 0;
         hs.flow_drops = _flow_drops.load(std::memory_order_relaxed);
         hs.gpu_errors = _gpu_errors.load(std::memory_order_relaxed);
         hs.gpu_killed = _gpu_killed.load(std::memory_order_relaxed);
@@ -558,6 +588,7 @@ class RxCore {
         } else if (h == "port_counts") {
             for (uint32_t p = 0; p <= nports; ++p) s << (p ? " " : "") << c[FCGPU_CTR_PORT + p];
         } else if (h == "flow_count") s << hs.flows;
+        else if (h == "flow_count_fids") s << hs.flow_fids;
         else if (h == "flow_drops") s << hs.flow_drops;
         else if (h == "gpu_errors") s << hs.gpu_errors;
         else if (h == "gpu_retries") s << hs.gpu_retries;
@@ -756,16 +787,22 @@ class RxCore {
     // batch's time stamp (Timestamp::recent_steady() at push_batch, :227-230).
     // Queued on the context's stream ahead of the batch. Called with _mu held.
     void flow_clock() {
-        const uint32_t now = (uint32_t)(P::now_ns() / 1000000ull);
+        const uint64_t now = P::now_ns() / 1000000ull;
         if (!_maint_armed) {
-            _next_maint = now + _flow_recycle_ms;
+            _next_maint_ms = now + _flow_recycle_ms;
             _maint_armed = true;
         }
-        while ((int32_t)(now - _next_maint) >= 0) {
-            if (fcgpu_flow_maintain(_ctx, _next_maint, nullptr) != FCGPU_OK) _error = fcgpu_last_error(_ctx);
-            _next_maint += _flow_recycle_ms;
+        flow_catch_up(now);
+        fcgpu_flow_set_time(_ctx, (uint32_t)now);
+    }
+    // The maintainer runs due by now_ms (ms on the element's clock; the
+    // device takes times mod 2^32). Called with _mu held.
+    void flow_catch_up(uint64_t now_ms) {
+        while (_maint_armed && now_ms >= _next_maint_ms) {
+            if (fcgpu_flow_maintain(_ctx, (uint32_t)_next_maint_ms, nullptr) != FCGPU_OK)
+                _error = fcgpu_last_error(_ctx);
+            _next_maint_ms += _flow_recycle_ms;
         }
-        fcgpu_flow_set_time(_ctx, now);
     }
 
     // The batch failed twice (no CPU fallback): its packets leave
@@ -785,7 +822,10 @@ class RxCore {
         s.n = 0;
         s.used = 0;
         s.inflight = false;
-        if (_error_output >= 0) {
+        // an ERROR_OUTPUT the element does not have (the harness connects its
+        // outputs after initialize) would kill them in checked_output_push_batch:
+        // they are killed and counted here instead
+        if (_error_output >= 0 && _error_output < emit.noutputs()) {
             P::chatter(name + ": GPU processing failed twice: " + msg + "; " + std::to_string(n) +
                        " packets to output " + std::to_string(_error_output));
             for (uint32_t a = 0; a < n;) {
@@ -1009,7 +1049,7 @@ class RxCore {
     int _color = -1;
     uint32_t _flow_cap = 0;
     uint32_t _flow_mgr = FCGPU_FLOW_MGR_HMP, _flow_timeout = 0, _flow_recycle_ms = 1000;
-    uint32_t _next_maint = 0;
+    uint64_t _next_maint_ms = 0;     // the next maintainer run, ms on the element's clock
     bool _maint_armed = false;
     int _flow_anno = 28;
     bool _flow_runs = true;

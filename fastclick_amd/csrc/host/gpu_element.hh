@@ -77,6 +77,7 @@ class GPUIPCheckClassify : public Element {
     struct Emit {          // RxCore hands each output run here
         GPUIPCheckClassify *e;
         void operator()(int port, PacketBatch *b) const { e->checked_output_push_batch(port, b); }
+        int noutputs() const { return e->noutputs(); }
     };
     Emit emitter() { return Emit{this}; }
     RxCore<ModelPolicy> _core;

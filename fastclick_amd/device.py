@@ -162,6 +162,11 @@ def exchange_pack(ctx: N.Context, arena, desc, perm, port_start, world, rank, st
     seg_bytes = host[world + 1:].tolist()
     m = min(ps[world], n)
     seg_n = [min(ps[d + 1], m) - min(ps[d], m) for d in range(world)]
+    if max(seg_bytes, default=0) > 0xFFFFFFFF:
+        # a record's offset within its owner's segment is 32 bits
+        # (fcgpu_xmeta.off): the pack refuses such a segment
+        raise ValueError(f"exchange_pack: an owner's segment of {max(seg_bytes)} B exceeds the 4 GiB "
+                         "a record offset addresses; split the batch")
     total = int(sum(seg_bytes))
     send = torch.empty(total + ARENA_PAD, dtype=torch.uint8, device=dev)
     with torch.cuda.stream(s):

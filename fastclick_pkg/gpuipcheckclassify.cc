@@ -11,10 +11,10 @@
 #include <click/bitvector.hh>
 CLICK_DECLS
 
-enum { h_count, h_drops, h_drop_details, h_port_counts, h_flow_count, h_flow_drops, h_gpu_errors, h_gpu_retries,
-       h_error };
+enum { h_count, h_drops, h_drop_details, h_port_counts, h_flow_count, h_flow_count_fids, h_flow_drops,
+       h_gpu_errors, h_gpu_retries, h_error };
 
-GPUIPCheckClassify::GPUIPCheckClassify() : _timer_us(100)
+GPUIPCheckClassify::GPUIPCheckClassify() : _timer_us(100), _error_output(-1)
 {
     in_batch_mode = BATCH_MODE_NEEDED;
 }
@@ -37,6 +37,7 @@ GPUIPCheckClassify::configure(Vector<String> &conf, ErrorHandler *errh)
     if (probe.configure(_conf, err) < 0)
         return errh->error("%s", err.c_str());
     _timer_us = probe.timer_us();
+    _error_output = probe.error_output();
     return 0;
 }
 
@@ -58,7 +59,7 @@ GPUIPCheckClassify::make_state(int thread, ErrorHandler *errh)
         return -1;
     }
     s.core = c;
-    if (_timer_us >= 0) {
+    if (_timer_us >= 0 || c->flow_timeouts()) {
         s.timer = new Timer(this);
         s.timer->initialize(this);
         s.timer->move_thread(thread);
@@ -69,6 +70,10 @@ GPUIPCheckClassify::make_state(int thread, ErrorHandler *errh)
 int
 GPUIPCheckClassify::initialize(ErrorHandler *errh)
 {
+    // the failed batches' packets need an output that exists
+    // (checked_output_push_batch would kill them uncounted)
+    if (_error_output >= noutputs())
+        return errh->error("ERROR_OUTPUT %d: the element has %d outputs", _error_output, noutputs());
     // a core for every thread that can push into this element
     Bitvector b = get_passing_threads();
     bool any = false;
@@ -98,17 +103,27 @@ GPUIPCheckClassify::cleanup(CleanupStage)
     }
 }
 
-// The timer covers what is staged (due TIMER us after its first packet) and
-// what is on the device.
+// The timer covers what is staged (due TIMER us after its first packet),
+// what is on the device, and (IMP timeouts) the next maintainer run.
 inline void
 GPUIPCheckClassify::arm(State &s)
 {
-    if (!s.timer || s.timer->scheduled() || s.core->idle())
+    if (!s.timer)
         return;
     const uint64_t now = ClickPolicy::now_ns();
-    uint64_t due = s.core->staged() ? s.core->due_ns() : now + (uint64_t)_timer_us * 1000;
+    uint64_t due = ~(uint64_t)0, m;
+    if (_timer_us >= 0 && !s.core->idle())
+        due = s.core->staged() ? s.core->due_ns() : now + (uint64_t)_timer_us * 1000;
+    if (s.core->maint_due_ns(&m) && m < due)
+        due = m;
+    if (due == ~(uint64_t)0)
+        return;
     if (due < now)
         due = now;
+    // an earlier deadline than the one scheduled (a batch staged while the
+    // timer waits for the next maintainer run) moves the timer up
+    if (s.timer->scheduled() && (uint64_t)s.timer->expiry_steady().nsecval() <= due)
+        return;
     s.timer->schedule_after(Timestamp::make_nsec((Timestamp::value_type)(due - now)));
 }
 
@@ -151,8 +166,8 @@ String
 GPUIPCheckClassify::read_handler(Element *e, void *thunk)
 {
     GPUIPCheckClassify *g = static_cast<GPUIPCheckClassify *>(e);
-    static const char *const names[] = {"count", "drops", "drop_details", "port_counts",
-                                        "flow_count", "flow_drops", "gpu_errors", "gpu_retries", "error"};
+    static const char *const names[] = {"count", "drops", "drop_details", "port_counts", "flow_count",
+                                        "flow_count_fids", "flow_drops", "gpu_errors", "gpu_retries", "error"};
     // PER_THREAD_SUM (include/click/sync.hh:384): the per-thread cores'
     // counters are summed on read. Each core's counters and error are read
     // under that core's own lock (RxCore::counters), never racing the thread
@@ -191,6 +206,7 @@ GPUIPCheckClassify::add_handlers()
     add_read_handler("drop_details", read_handler, h_drop_details);
     add_read_handler("port_counts", read_handler, h_port_counts);
     add_read_handler("flow_count", read_handler, h_flow_count);
+    add_read_handler("flow_count_fids", read_handler, h_flow_count_fids);
     add_read_handler("flow_drops", read_handler, h_flow_drops);
     add_read_handler("gpu_errors", read_handler, h_gpu_errors);
     add_read_handler("gpu_retries", read_handler, h_gpu_retries);

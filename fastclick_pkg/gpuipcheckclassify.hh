@@ -102,6 +102,7 @@ class GPUIPCheckClassify : public BatchElement { public:
     struct Emit {
         GPUIPCheckClassify *e;
         void operator()(int port, PacketBatch *b) const { e->checked_output_push_batch(port, b); }
+        int noutputs() const { return e->noutputs(); }
     };
 
     int make_state(int thread, ErrorHandler *errh);
@@ -111,6 +112,7 @@ class GPUIPCheckClassify : public BatchElement { public:
     per_thread<State> _state;
     std::vector<std::string> _conf;
     int64_t _timer_us;
+    int _error_output;
 };
 
 CLICK_ENDDECLS

@@ -650,7 +650,9 @@ int  fcgpu_read_timing(fcgpu_ctx *ctx, double *ms, uint32_t *launches, int nstag
  *       owner d's segment of the send buffer. Each frame takes a 4-B aligned
  *       slot of (length + 3) & ~3 bytes. Segments follow in owner order.
  *   fcgpu_exchange_pack   the frames into d_send (at least the sum of
- *       d_seg_bytes; nothing is written past send_cap): owner d's segment
+ *       d_seg_bytes; nothing is written past send_cap; an owner whose
+ *       d_seg_bytes exceeds 0xffffffff -- its records' 32-bit offsets cannot
+ *       address it -- is not packed, so check the plan's sizes first): owner d's segment
  *       holds its packets in input order; slot bytes past a frame's length
  *       are zero. It reads the frames' arena offsets the plan left in the
  *       context: call it after fcgpu_exchange_plan of the same batch on the

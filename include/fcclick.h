@@ -60,7 +60,8 @@ typedef struct fcclick_result {
     int32_t  *out_nh;       /* [n] network header offset from data() (-1 unset)          */
     uint32_t *out_batches;  /* [1] number of PacketBatches the sinks received             */
     char     *handlers;     /* "name=value\n" for count, drops, drop_details, port_counts,
-                               flow_count, flow_drops, gpu_errors, gpu_retries, error     */
+                               flow_count, flow_count_fids, flow_drops, gpu_errors,
+                               gpu_retries, error                                          */
     size_t    handlers_cap;
     uint8_t  *out_paint;    /* [n] PAINT_ANNO (anno u8 @17) on departure (may be NULL)     */
     uint32_t *out_flow;     /* [n] anno u32 @28 (FLOWID_ANNO default) on departure (may be NULL) */
@@ -101,6 +102,28 @@ int fcclick_run_ex(const char *conf, const uint8_t *arena, const uint32_t *desc,
 int fcclick_run_clocked(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
                         uint32_t burst, uint32_t nsinks, const uint64_t *burst_ns, fcclick_result *res,
                         char *err, size_t errcap);
+
+/* A scripted run on a virtual clock: events in order, each at its own time
+ * t_ns (0 keeps the clock where it is) --
+ *   FCCLICK_EV_BURST: the next `count` packets (in descriptor order) as one
+ *     PacketBatch, as a source whose bursts vary in size (FromIPSummaryDump
+ *     with TIMING and BURST, elements/analysis/fromipsumdump.cc:759-795);
+ *   FCCLICK_EV_READ: the element's Timer fires at t_ns (a partial batch due,
+ *     the flow maintainer's runs due), then every handler is read, as a
+ *     DriverManager `read` at that time would (the texts of all reads go to
+ *     `reads`, each read as "name=value" lines ended by a "--" line).
+ * The bursts must cover the n packets exactly. Ends with flush(); the final
+ * handler values are in res->handlers as for fcclick_run. */
+#define FCCLICK_EV_BURST 0u
+#define FCCLICK_EV_READ  1u
+typedef struct fcclick_event {
+    uint64_t t_ns;
+    uint32_t kind;
+    uint32_t count;
+} fcclick_event;
+int fcclick_run_events(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                       uint32_t nsinks, const fcclick_event *ev, uint32_t nev, fcclick_result *res,
+                       char *reads, size_t reads_cap, char *err, size_t errcap);
 
 /* Host-resident rate: repeat the same run `reps` times (packets recycled
  * LIFO into a mempool sized to what the element can hold, sinks discard), return packets per second through the element

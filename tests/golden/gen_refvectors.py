@@ -32,6 +32,15 @@ Sets (the SURVEY 8(a) rows they pin):
   markipce  ip/MarkIPCE-01.clicktest:19-24,36-43 -- packets FromIPSummaryDump
             (CHECKSUM true) builds that pass CheckIPHeader before and after
             MarkIPCE sets ECN CE with an incremental checksum update.    [A2]
+  flow      flow/flow-no-dynamic.clicktest:9-17,25-31,36-63 and
+            flow/flow-dynamic.clicktest:9-17,25-31,36-61 -- five UDP packets
+            FromIPSummaryDump(CHECKSUM true, TIMING true [, BURST 2]) sends at
+            t = 1, 3, 3, 3.1, 5 s through FlowIPManager_CuckooPP(RESERVE 2,
+            TIMEOUT 5) (the IMP manager, CAPACITY 65536): each packet's first
+            24 bytes as the test's Print lines show them (their IP checksums
+            the reference wrote), the flow ID FlowPrint reports for each run,
+            the PacketBatch runs (BURST 2), and the count / count_fids reads
+            DriverManager makes at t = 0, 2 and 12 s.          [A1 (f)#1 IMP]
 
 Restated here (cited): FromIPSummaryDump's ip_opt text -> option bytes
 (elements/analysis/ipsumdump_ip.cc:628-851, placed and EOL-padded as :173-191),
@@ -406,10 +415,116 @@ def gen_markipce():
     return dict(source=f"test/{rel}:{line} (%file IN), %expect OUT2 at :{eline}", before=before, after=after)
 
 
+def ipv4_udp(src, dst, payload, ttl=100):
+    """FromIPSummaryDump(CHECKSUM true) for a "U" row with a payload: the
+    default IPv4 header (ipsumdumpinfo.cc:422-445: ttl 100, id 0), a UDP
+    header with ports 0 (no sport/dport field) and uh_ulen = ip_len - 20
+    (fromipsumdump.cc:637-642), the payload bytes, then set_checksums
+    (:384-402): the IP header checksum and the UDP checksum over the datagram
+    with its pseudo-header."""
+    total = 20 + 8 + len(payload)
+    iph = bytearray(struct.pack("!BBHHHBBH4s4s", 0x45, 0, total, 0, 0, ttl, 17, 0, ip4(src), ip4(dst)))
+    iph[10:12] = struct.pack("!H", cksum(bytes(iph)))
+    udp = bytearray(struct.pack("!HHHH", 0, 0, 8 + len(payload), 0)) + payload
+    pseudo = ip4(src) + ip4(dst) + struct.pack("!BBH", 0, 17, len(udp))
+    udp[6:8] = struct.pack("!H", cksum(pseudo + bytes(udp)))
+    return bytes(iph + udp)
+
+
+def _flow_section(body, header):
+    """The lines of one flow manager's run in a flow test's %expect stderr
+    (from the line `header` to the next manager's)."""
+    beg = body.index(header)
+    first = next(k for k in range(beg, len(body)) if body[k].startswith("Placing "))
+    end = len(body)
+    for k in range(first + 1, len(body)):
+        if body[k].startswith("Placing ") or body[k] in ("FlowIPManager_DPDK", "FlowIPManagerMP", "FlowIPManager"):
+            end = k
+            break
+    return body[beg:end]
+
+
+def _flow_trace(lines):
+    """Print / FlowPrint / handler lines of one run -> the packets' first
+    bytes (BEFORE order), the source's PacketBatches (Print(BEFORE) prints a
+    whole batch before the manager sees it, so BEFORE lines with no AFTER line
+    between them are one batch), the runs FlowPrint reports (packet indices,
+    flow ID) and the handler reads in order (name, value, packets seen before
+    it)."""
+    before, runs, reads, bursts = [], [], [], []
+    after_seen = 0
+    last = None
+    k = 0
+    while k < len(lines):
+        ln = lines[k]
+        m = re.match(r"BEFORE:\s+(\d+) \| (.*)$", ln)
+        if m:
+            if last == "BEFORE":
+                bursts[-1] += 1
+            else:
+                bursts.append(1)
+            before.append((int(m.group(1)), hexbytes(m.group(2).split())))
+            last = "BEFORE"
+        m = re.match(r"AFTER:\s+\d+ \|", ln)
+        if m:
+            after_seen += 1
+            last = "AFTER"
+        m = re.match(r"fprint :: FlowPrint: (\d+) packets from flow (\d+)\.", ln)
+        if m:
+            cnt = int(m.group(1))
+            runs.append(dict(packets=list(range(after_seen - cnt, after_seen)), flow=int(m.group(2))))
+        m = re.match(r"fm\.(count|count_fids):$", ln)
+        if m:
+            reads.append(dict(handler=m.group(1), value=lines[k + 1], after_packets=len(before)))
+            k += 1
+        k += 1
+    return before, runs, reads, bursts
+
+
+def gen_flow():
+    rel_nd, rel_d = "flow/flow-no-dynamic.clicktest", "flow/flow-dynamic.clicktest"
+    text_nd, text_d = read(rel_nd), read(rel_d)
+    assert "FlowIPManager_CuckooPP" in text_nd and "RESERVE 2, VERBOSE 1, TIMEOUT 5" in text_nd
+    assert "FromIPSummaryDump(IN1, STOP false, CHECKSUM true, TIMING true)" in text_nd
+    assert "FromIPSummaryDump(IN1, STOP false, CHECKSUM true, TIMING true, BURST 2)" in text_d
+    rows, l_in = section(text_nd, "%file IN1")
+    rows_d, _ = section(text_d, "%file IN1")
+    assert rows == rows_d and rows[0].split() == ["!data", "timestamp", "src", "dst", "proto", "payload"]
+    pkts = []
+    for r in rows[1:]:
+        t, src, dst, proto, payload = r.split()
+        assert proto == "U"
+        pkts.append(dict(t=float(t), frame=ipv4_udp(src, dst, payload.encode())))
+    out = dict(source=f"test/{rel_nd}:9-17 (graph), :25-31 (%file IN1 at :{l_in}), %expect stderr; "
+                      f"test/{rel_d}:9-17 (BURST 2), %expect stderr",
+               manager=dict(kind="FlowIPManager_CuckooPP", capacity=65536, timeout_s=5, recycle_ms=1000),
+               packets=[dict(t=p["t"], frame=p["frame"].hex()) for p in pkts])
+    for key, text, header in (("single", text_nd, "Placing  ftest :: TestFlowSpace at [30-33]"),
+                              ("burst2", text_d, "FlowIPManager_CuckooPP")):
+        body, line = section(text, "%expect stderr")
+        sec = _flow_section(body, header)
+        assert "Real capacity for each table will be 65536" in sec
+        before, runs, reads, bursts = _flow_trace(sec)
+        # the Print lines are the packets' first 24 bytes, byte for byte
+        assert len(before) == len(pkts)
+        for (length, head), p in zip(before, pkts):
+            assert length == len(p["frame"]) and head == p["frame"][:24], (key, head.hex(), p["frame"][:24].hex())
+        ids = [None] * len(pkts)
+        for run in runs:
+            for i in run["packets"]:
+                ids[i] = run["flow"]
+        assert None not in ids
+        out[key] = dict(expect_line=line, bursts=bursts, runs=runs, ids=ids, reads=reads)
+    # the reads' times: DriverManager(read.., wait 2s, read.., wait 10s, read..)
+    # on the FromIPSummaryDump TIMING clock (the first packet at t = 0)
+    out["read_times_s"] = [0.0, 2.0, 12.0]
+    return out
+
+
 def main():
     out = dict(generator="tests/golden/gen_refvectors.py", reference_tests_only=True,
                iprouter=gen_iprouter(), ipopt=gen_ipopt(), vlan=gen_vlan(), ipfrag=gen_ipfrag(),
-               tcpfull=gen_tcpfull(), markipce=gen_markipce())
+               tcpfull=gen_tcpfull(), markipce=gen_markipce(), flow=gen_flow())
     with open(OUT, "w") as f:
         json.dump(out, f, indent=1, sort_keys=False)
         f.write("\n")

@@ -50,6 +50,8 @@ API = [
     ("timer.hh", r"Timer\(Element \*element\);", "per-thread Timer"),
     ("timer.hh", r"void schedule_after\(const Timestamp &delta\);", "arm()"),
     ("timer.hh", r"inline bool scheduled\(\) const", "arm()"),
+    ("timer.hh", r"inline const Timestamp &expiry_steady\(\) const", "arm(): an earlier deadline moves the timer up"),
+    ("element.hh", r"inline int noutputs\(\) const", "ERROR_OUTPUT check, Emit::noutputs"),
     ("timer.hh", r"void move_thread\(int tid\);", "per-thread Timer"),
     ("timer.hh", r"void initialize\(Element \*owner, bool quiet = false\);", "per-thread Timer"),
     ("timer.hh", r"inline void clear\(\)", "cleanup"),
@@ -84,6 +86,6 @@ def test_package_uses_only_checked_api():
     own = {"push_list", "push_one", "run_timer", "configure", "initialize", "counters", "nports", "details",
            "error", "timer_us", "idle", "staged", "due_ns", "get", "c_str", "push_back", "clear", "size",
            "first", "get_passing_threads", "error", "name", "checked_output_push_batch", "make_state",
-           "read_handler", "empty"}
+           "read_handler", "empty", "error_output", "flow_timeouts", "maint_due_ns"}
     missing = used - checked - own
     assert not missing, f"unchecked FastClick calls: {sorted(missing)}"

@@ -61,13 +61,15 @@ def all_headers(v):
         out.append((bytes.fromhex(h), v["tcpfull"]["source"]))
     for h in v["markipce"]["before"] + v["markipce"]["after"]:
         out.append((bytes.fromhex(h), v["markipce"]["source"]))
+    for p in v["flow"]["packets"]:      # the flow tests' Print lines (tests/test_flow_reftest.py)
+        out.append((bytes.fromhex(p["frame"])[:20], v["flow"]["source"]))
     return out
 
 
 def test_refvectors_fixture():
     v = vectors()
     assert v["reference_tests_only"] and v["generator"] == "tests/golden/gen_refvectors.py"
-    for k in ("iprouter", "ipopt", "vlan", "ipfrag", "tcpfull", "markipce"):
+    for k in ("iprouter", "ipopt", "vlan", "ipfrag", "tcpfull", "markipce", "flow"):
         assert v[k]["source"].startswith("test/"), k
     assert len(v["ipopt"]["frames"]) == 13 and len(v["vlan"]["cases"]) == 8
     for fr, e in zip(v["ipopt"]["frames"], v["ipopt"]["expect"]):
