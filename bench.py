@@ -94,6 +94,11 @@ def parse(argv=None):
                          "uniform random 5-tuples (configs[3]); c5: 50%% 802.1Q + 30%% IPv6 mix "
                          "through StripEtherVLANHeader + CheckIP6Header/CheckIPHeader (configs[4]). "
                          "Default c2, or c4 with --shard strong")
+    ap.add_argument("--layout", choices=["wire", "split"], default="wire",
+                    help="wire (default): every frame whole in 64-B aligned slots, as received; split: "
+                         "the first 64 B of every frame in a dense ring of 64-B slots (two per 128-B "
+                         "line), as a NIC's header/data buffer split delivers them -- a labelled variant, "
+                         "never the config number")
     ap.add_argument("--frame-bytes", type=int, default=64,
                     help="c2/c4 frame size on the wire (64..1518; captured = size - 4 FCS bytes, "
                          "ip_len = captured - 14, fastudpflows.cc:146-175); the kernel still reads "
@@ -124,6 +129,14 @@ def parse(argv=None):
     ap.add_argument("--rewrite", action="store_true",
                     help="DecIPTTL + SetIPChecksum behind the classifier; the rewritten header bytes go "
                          "to an ip_rw output per batch (not in place: the rotating batches are reused)")
+    ap.add_argument("--flow-reshard", action="store_true",
+                    help="(f)#1 x (e): every step re-shards the rank's batch by flow before the flow table "
+                         "(SURVEY 8(f) #1 on several GPUs): the device owner pass (LB_MODE hash over the "
+                         "world's ranks, whole-batch partition), fcgpu_exchange_plan/_pack, the RCCL "
+                         "all-to-alls of records and frames (dist.exchange_segments), fcgpu_exchange_unpack, "
+                         "then the FlowIPManagerHMP pass over the received batch; C4 (uniform 5-tuples, a "
+                         "different batch per rank). Per-stage times and checked flow counts in "
+                         "config.flow_reshard; a labelled variant, never the headline")
     ap.add_argument("--program-jit", type=int, default=1,
                     help="ipclass16: 1 = the program compiled to code (fcgpu_program_jit, hiprtc, before "
                          "the warmup); 0 = the step interpreter")
@@ -152,6 +165,12 @@ def parse(argv=None):
         a.streams = 1
     if a.partition == "global" and a.streams > 1 and not a.no_perm:
         a.streams = 1    # the whole-batch partition uses context scratch
+    if a.flow_reshard:
+        if a.workload != "c4" or a.shard != "weak" or a.frame_bytes != 64 or a.layout != "wire" or a.errors:
+            ap.error("--flow-reshard runs 64-B C4 batches, weak sharding, wire layout")
+        if a.flow_manager != "hmp":
+            ap.error("--flow-reshard uses the HMP table")
+        a.streams = 1
     return a
 
 
@@ -337,15 +356,37 @@ ERROR_BADSRC = ("192.0.2.255", "255.255.255.255")
 
 def make_host_batch(args):
     """The workload's host batch; with --errors also the number of packets
-    the mix leaves valid."""
+    the mix leaves valid. --layout split: its header-split form."""
     from fastclick_amd import synth
     b = _make_host_batch(args)
-    if not args.errors:
-        return b, b.n
-    kind = synth.inject_errors(b, args.errors, seed=41,
-                               kinds=(synth.ERR_VERSION, synth.ERR_HLEN, synth.ERR_IPLEN, synth.ERR_CKSUM,
-                                      synth.ERR_BADSRC))
-    return b, int((kind < 0).sum())
+    valid = b.n
+    if args.errors:
+        kind = synth.inject_errors(b, args.errors, seed=41,
+                                   kinds=(synth.ERR_VERSION, synth.ERR_HLEN, synth.ERR_IPLEN, synth.ERR_CKSUM,
+                                          synth.ERR_BADSRC))
+        valid = int((kind < 0).sum())
+    if getattr(args, "layout", "wire") == "split":
+        b = synth.header_split(b, 64)
+    return b, valid
+
+
+def traffic_key(args, per_gpu):
+    """The key of a workload's PMC traffic in profiles/pmc_traffic.json: every
+    option that changes what k_rx reads or writes."""
+    parts = [args.workload, f"fb{args.frame_bytes}", getattr(args, "layout", "wire"), f"n{per_gpu}"]
+    if args.flow_capacity:
+        parts.append(f"flow{args.flow_capacity}{args.flow_manager}")
+    if args.classify != "lb":
+        parts.append(args.classify)
+    if args.l4 != "none":
+        parts.append("l4" + args.l4)
+    if args.rewrite:
+        parts.append("rewrite")
+    if args.no_perm or args.partition != "tile":
+        parts.append("nopart" if args.no_perm else args.partition)
+    if args.errors:
+        parts.append(f"err{args.errors:g}")
+    return "/".join(parts)
 
 
 def _make_host_batch(args):
@@ -574,6 +615,170 @@ class DeviceProcessor:
         self.ctx.close()
 
 
+class ReshardProcessor:
+    """--flow-reshard: the flow re-shard inside each step.
+    Rank r's batch is its own C4 batch (seed 4 + r: independent uniform
+    5-tuples, so every rank's flows are new to the others); per step:
+
+      owner pass   k_rx + k_scan + k_part_multi: LB_MODE hash over `world`
+                   outputs (the FlowSwitch formula on the IPFlowID hash), the
+                   whole-batch partition -> each packet's owner rank
+      plan, pack   fcgpu_exchange_plan (3 kernels) + fcgpu_exchange_pack
+      exchange     dist.exchange_segments: RCCL all-to-all of the per-owner
+                   counts, then of the records and the frame bytes (world 1:
+                   the send buffer is the received one, no collective)
+      unpack       fcgpu_exchange_unpack: records -> descriptors
+      flow pass    k_rx with the FlowIPManagerHMP table + the new-flow pass over
+                   the received batch (tile partition, 16 outputs)
+
+    The same --nbuf rotation as the headline keeps the owner pass reading
+    HBM. The flow pass's counters are the step's counters (so the all-reduced
+    valid count checks that every packet arrived exactly once), and after the
+    timed region post_check() all-reduces the tables' flow counts against the
+    distinct 5-tuples of all ranks' batches."""
+
+    def __init__(self, args, lo, hi, gpu):
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+        from fastclick_amd import _native as N, synth
+        from fastclick_amd.device import DeviceOutputs
+        self.N, self.torch, self.args, self.np = N, torch, args, np
+        dev = torch.device("cuda", gpu)
+        self.dev = dev
+        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        self.rank = dist.get_rank() if self.world > 1 else 0
+        n = hi - lo
+        self.n = n
+        seed = 4 + self.rank
+        host = synth.c4(n, seed=seed)
+        fl = synth._rand_flows(np.random.default_rng(seed), n)
+        keys = np.stack([fl["src"].astype(np.uint64) << 32 | fl["dst"].astype(np.uint64),
+                         fl["sport"].astype(np.uint64) << 16 | fl["dport"].astype(np.uint64)], axis=1)
+        self.distinct = int(np.unique(keys, axis=0).shape[0])      # this rank's distinct 5-tuples
+        self.valid_per_batch = n
+        touched = host.arena.nbytes + host.desc.nbytes
+        args.nbuf = rotation_nbuf(touched, args.nbuf)
+        self.rotation_bytes = args.nbuf * touched
+        stride = -(-host.arena.size // 4096) * 4096
+        arena = torch.from_numpy(host.arena).to(dev)
+        desc = torch.from_numpy(host.desc.view(np.int32)).to(dev)
+        self.arena_all = torch.empty((args.nbuf, stride), dtype=torch.uint8, device=dev)
+        self.desc_all = torch.empty((args.nbuf,) + tuple(desc.shape), dtype=torch.int32, device=dev)
+        self.arena_all[:, :arena.numel()].copy_(arena.expand(args.nbuf, -1))
+        self.desc_all.copy_(desc.expand(args.nbuf, *desc.shape))
+        del arena, desc, host
+        self.bufs = [(self.arena_all[k], self.desc_all[k]) for k in range(args.nbuf)]
+        own_cfg = N.make_cfg(offset=14, checksum=True, hash_mode=N.HASH_FLOWID, classify=N.CLS_LB_HASH,
+                             nports=self.world)
+        self.ctx_own = N.Context(gpu, max(n, 1), own_cfg)
+        self.own_out = DeviceOutputs(max(n, 1), self.world, device=dev, verdict=True, hash=False,
+                                     perm=True, port_start=True, partition=N.PART_GLOBAL)
+        # a rank receives ~n packets (uniform owners); room for 2n
+        self.cap = 2 * max(n, 1)
+        flow_cfg = N.make_cfg(offset=14, checksum=True, hash_mode=N.HASH_FLOWID, classify=N.CLS_LB_HASH,
+                              nports=args.nports)
+        self.ctx_flow = N.Context(gpu, self.cap, flow_cfg)
+        self.ctx_flow.flow_enable(args.flow_capacity or self.cap)
+        self.flow_out = DeviceOutputs(self.cap, args.nports, device=dev, verdict=True, hash=True,
+                                      tile_perm=True, partition=N.PART_TILE, flowid=True)
+        self.ctr = torch.zeros(N.CTR_SHARDS, N.NCOUNTERS, dtype=torch.int64, device=dev)
+        self.received = 0
+        self.stage_ms = [0.0] * 5
+        self.ev = None
+        self.timed_steps = 0
+
+    def _step(self, k, timed):
+        import torch
+        from fastclick_amd import device as DV
+        from fastclick_amd.dist import exchange_segments
+        N = self.N
+        a, d = self.bufs[k % len(self.bufs)]
+        s = torch.cuda.current_stream()
+        ev = self.ev if timed else None
+        if ev:
+            ev[0].record(s)
+        o = self.own_out
+        self.ctx_own.process(a.data_ptr(), d.data_ptr(), self.n, stream=s.cuda_stream, **o.ptrs())
+        if ev:
+            ev[1].record(s)
+        send, meta, seg_n, seg_bytes = DV.exchange_pack(self.ctx_own, a, d, o.perm, o.port_start,
+                                                        self.world, self.rank)
+        if ev:
+            ev[2].record(s)
+        buf, rmeta, displ = exchange_segments(send, meta, seg_n, seg_bytes)
+        if ev:
+            ev[3].record(s)
+        rdesc = DV.exchange_unpack(self.ctx_own, rmeta, displ)
+        m = int(rdesc.shape[0])
+        if m > self.cap:
+            raise RuntimeError(f"rank {self.rank} received {m} packets, more than the flow context's {self.cap}")
+        if ev:
+            ev[4].record(s)
+        f = self.flow_out
+        self.ctx_flow.process(buf.data_ptr(), rdesc.data_ptr(), m, stream=s.cuda_stream, **f.ptrs())
+        if ev:
+            ev[5].record(s)
+            torch.cuda.synchronize()
+            for j in range(5):
+                self.stage_ms[j] += ev[j].elapsed_time(ev[j + 1])
+        if timed:
+            self.received += m
+
+    def warmup(self, steps):
+        for k in range(max(steps, 1)):
+            self._step(k, False)
+        self.torch.cuda.synchronize()
+        self.ctx_flow.use_counters(self.ctr.data_ptr())      # timed steps count into the tensor
+        self.ev = [self.torch.cuda.Event(enable_timing=True) for _ in range(6)] \
+            if os.environ.get("FCGPU_RESHARD_STAGES", "1") == "1" else None
+        self.first = max(steps, 1)
+
+    def run_timed(self):
+        for k in range(self.args.steps):
+            self._step(self.first + k, True)
+        self.timed_steps = self.args.steps
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def counters(self):
+        return self.ctr
+
+    def timing(self):
+        return None
+
+    def post_check(self, backend):
+        """After the timed region: every rank's table holds exactly the flows
+        it owns, so the tables' counts add up to the distinct 5-tuples of all
+        ranks' batches (all-reduced; the batches' uniform 96-bit keys do not
+        repeat across ranks), and every packet arrived once."""
+        import torch
+        import torch.distributed as dist
+        dev = self.dev if backend == "nccl" else "cpu"
+        v = torch.tensor([self.ctx_flow.flow_count(), self.distinct, self.received,
+                          self.n * self.timed_steps], dtype=torch.int64, device=dev)
+        if self.world > 1:
+            dist.all_reduce(v, op=dist.ReduceOp.SUM)
+        flows, distinct, received, sent = (int(x) for x in v.cpu().tolist())
+        if flows != distinct:
+            raise AssertionError(f"flow tables hold {flows} flows, the batches have {distinct} distinct 5-tuples")
+        if received != sent:
+            raise AssertionError(f"{received} packets received, {sent} sent")
+        steps = max(self.timed_steps, 1)
+        names = ("owner_pass", "plan_pack", "exchange", "unpack", "flow_pass")
+        return {"flow_table_flows": flows, "distinct_5tuples": distinct, "packets_received": received,
+                "packets_sent": sent, "checked": True,
+                **({"stage_ms_per_step": {k: round(t / steps, 4) for k, t in zip(names, self.stage_ms)},
+                    "stage_basis": "HIP events on the step's stream, synchronised per step (their sum is "
+                                   "below ms_per_step by the host's own work and the syncs)"}
+                   if self.ev else {})}
+
+    def close(self):
+        self.ctx_own.close()
+        self.ctx_flow.close()
+
+
 def _diag_regions(proc, elapsed, enq, timing, repeats=6):
     """FCGPU_BENCH_DIAG=1 (diagnostics, stderr only; the JSON line is the
     first region's): the timed region repeated in the same process on the
@@ -629,6 +834,7 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
         if os.environ.get("FCGPU_BENCH_DIAG"):
             _diag_regions(proc, elapsed, t_enq - t0, timing)
         maintain_ms = getattr(proc, "maintain_ms", None)
+        post = proc.post_check(backend) if hasattr(proc, "post_check") else None
 
         # after the timed region: max time over ranks, counters summed over
         # ranks (RCCL all-reduce of the device vector), per-output offsets
@@ -680,23 +886,25 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
         t_launch = kernel_s if basis == "kernel" else step_s
         achieved = PKT_BYTES_READ * per_gpu / t_launch / 1e9
         traffic, traffic_src = None, None
+        key = traffic_key(args, per_gpu)
         try:
             with open(args.traffic_json) as f:
-                tj = json.load(f)
+                tj = json.load(f).get("entries", {})
             # the stored PMC figure (rocprofv3 cannot run inside the bench) counts
             # only for this workload and only while the kernel sources are the
             # ones it was measured on
-            if tj.get("packets") == per_gpu and tj.get("workload", "c2") == args.workload \
-                    and tj.get("frame_bytes", 64) == args.frame_bytes:
-                if tj.get("source_sha16") == kernel_source_sha():
-                    traffic = tj.get("hbm_bytes_per_launch")
-                    traffic_src = tj.get("source")
+            ent = tj.get(key)
+            if ent is not None:
+                if ent.get("source_sha16") == kernel_source_sha():
+                    traffic = ent.get("hbm_bytes_per_launch")
+                    traffic_src = ent.get("source")
                 else:
                     traffic_src = "stale: profiles/pmc_traffic.json was measured on other kernel sources"
         except Exception:
             pass
         roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=traffic_src,
+                    traffic_key=key,
                     kernel="k_rx", basis=basis,
                     bytes_per_launch=PKT_BYTES_READ * per_gpu,
                     per="batch (a k_rx launch carries up to config.batches_per_launch batches: "
@@ -706,7 +914,8 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                     scan_ms=round(timing["k_scan_ms"], 5), part_ms=round(timing["k_part_ms"], 5),
                     sampled_batches=timing["launches"][0])
     cpu = None
-    if world == 1 and not args.no_cpu and args.workload in ("c2", "c3", "c4") and not args.flow_capacity:
+    if world == 1 and not args.no_cpu and args.workload in ("c2", "c3", "c4") and not args.flow_capacity \
+            and not args.flow_reshard:
         cpu = cpu_baseline(args.cpu_seconds, flows=dict(c2=1, c3=10000).get(args.workload, 4096),
                            program=ipclass16_program() if args.classify == "ipclass16" else None)
     fb = args.frame_bytes
@@ -730,9 +939,15 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
             "workload": (wl
                          + ("; StripEtherVLANHeader + CheckIP6Header/CheckIPHeader(CHECKSUM true)"
                             if auto else "; CheckIPHeader(CHECKSUM true)")
+                         + ("; header-split arena: the first 64 B of every frame in a dense 64-B slot ring "
+                            "(a NIC's header/data buffer split; labelled variant, not the config number)"
+                            if args.layout == "split" else "")
                          + (f" (with-errors mix: {args.errors:g} each of bad version, header length, "
                             f"ip_len, checksum, BADSRC)" if args.errors else "")
                          + (f" + Check{args.l4.upper()}Header" if args.l4 != "none" else "")
+                         + (f" + flow re-shard across the {world} rank(s) (owner pass, fcgpu_exchange_plan/"
+                            f"pack, all-to-all of records and frames, fcgpu_exchange_unpack) + FlowIPManagerHMP "
+                            f"flow table over the received batch" if args.flow_reshard else "")
                          + ((f" + FlowIPManagerHMP flow table ({args.flow_capacity} IDs)"
                              if args.flow_manager == "hmp" else
                              f" + VirtualFlowManagerIMP flow table (CAPACITY {args.flow_capacity}, "
@@ -756,6 +971,7 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
             "batches_per_launch": max(1, min(args.fuse, 8 if args.flow_capacity else 24,
                                              -(-args.steps // max(1, args.streams)))),
             "frame_bytes": fb,
+            "layout": args.layout,
             "packets_per_step_per_gpu": per_gpu,
             "packets_per_step": args.packets if args.shard == "strong" else args.packets * world,
             "hbm_batches": args.nbuf,
@@ -763,6 +979,7 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                if getattr(proc, "rotation_bytes", None) else {}),
             "nports": args.nports,
             **({"flow_maintain_ms": round(maintain_ms, 4)} if maintain_ms is not None else {}),
+            **({"flow_reshard": post} if post is not None else {}),
             "parallelism": ((f"batch-sharded x{world}" if args.shard == "weak" else
                              f"one batch split x{world} (dist.shard_range)")
                             + f", counters all-reduced after the timed region "
@@ -800,7 +1017,8 @@ def main():
             dist.init_process_group("gloo")
     torch.cuda.set_device(gpu)
     try:
-        line = rank_main(args, DeviceProcessor, world=world, rank=rank, gpu=gpu, backend=args.backend,
+        line = rank_main(args, ReshardProcessor if args.flow_reshard else DeviceProcessor, world=world, rank=rank,
+                         gpu=gpu, backend=args.backend,
                          dev_for_collectives=torch.device("cuda", gpu) if args.backend == "nccl" else "cpu")
         if line is not None:
             print(json.dumps(line), flush=True)

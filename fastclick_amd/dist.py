@@ -94,10 +94,19 @@ def exchange_segments(send, meta, seg_n, seg_bytes, group=None):
         raise ValueError(f"{len(seg_n)} segments for a world of {world}")
     if world == 1:
         return send, meta, [0]
+    if send.is_cuda and dist.get_backend(group) == "gloo":
+        # a rehearsal of several ranks on one GPU (bench.py --backend gloo):
+        # gloo's all-to-all takes host tensors
+        buf, rmeta, displ = exchange_segments(send.cpu(), meta.cpu(), seg_n, seg_bytes, group=group)
+        return buf.to(send.device), rmeta.to(send.device), displ
     dev = send.device
     cnt = torch.tensor([[int(a), int(b)] for a, b in zip(seg_n, seg_bytes)], dtype=torch.int64, device=dev)
     rcnt = torch.empty_like(cnt)
     dist.all_to_all_single(rcnt, cnt, group=group)           # [world, 2] from every rank
+    # the one host sync of the exchange: the receive sizes of the next two
+    # all-to-alls are host split lists (RCCL needs them at enqueue). Its cost
+    # is the round trip of this 16*world-byte all-to-all, measured with the
+    # rest of the exchange by bench.py --flow-reshard (config.flow_reshard)
     rc = rcnt.cpu().tolist()
     rn, rb = [r[0] for r in rc], [r[1] for r in rc]
     total = int(sum(rb))

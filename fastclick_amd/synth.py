@@ -242,6 +242,51 @@ def c5(n=1 << 16, seed=5):
     return pack(hdr, flen, meta=dict(config="C5", seed=seed))
 
 
+def header_reach(batch: Batch, ip_off: int = 14) -> np.ndarray:
+    """Per frame, the end of the bytes the receive chain reads: the Ethernet
+    header (an 802.1Q tag when the frame has one and ip_off is 14), the IPv4
+    header (hl words) or the 40-B IPv6 header, and the 4 bytes of ports behind
+    it (IPFlowID, the LB hash). For the synthetic workloads (no IPv6 extension
+    headers); int64[n]."""
+    n = batch.n
+    off = batch.desc[:, 0].astype(np.int64)
+    A = batch.arena
+    o = np.full(n, ip_off, np.int64)
+    if ip_off == 14 and n:
+        tagged = (A[off + 12].astype(np.int64) << 8 | A[off + 13]) == ETH_8021Q
+        o = np.where(tagged, 18, 14)
+    v = A[off + o] >> 4
+    hl = (A[off + o] & 15).astype(np.int64) * 4
+    return o + np.where(v == 6, 40, hl) + 4
+
+
+def header_split(batch: Batch, slot: int = 64, ip_off: int = 14) -> Batch:
+    """The batch as a NIC with header/data buffer split delivers it (DPDK's
+    RTE_ETH_RX_OFFLOAD_BUFFER_SPLIT; the mbuf wrap FromDPDKDevice builds,
+    elements/userlevel/fromdpdkdevice.cc:374-456, points at the first
+    segment): every frame's first `slot` bytes in a dense ring of `slot`-byte
+    slots, two per 128-B line at 64, the descriptor pointing at the slot with
+    the frame's full length. The rest of each frame (its payload segment) is
+    not part of the arena: the chain must not read past `slot` bytes, which is
+    asserted (header_reach)."""
+    n = batch.n
+    reach = header_reach(batch, ip_off)
+    if n and int(reach.max()) > slot:
+        raise ValueError(f"header_split: frames whose chain reads {int(reach.max())} B do not fit {slot}-B slots")
+    arena = np.zeros(n * slot + ARENA_PAD, np.uint8)
+    if n:
+        off = batch.desc[:, 0].astype(np.int64)
+        ln = np.minimum(batch.desc[:, 1].astype(np.int64), slot)
+        idx = off[:, None] + np.arange(slot)[None, :]
+        head = batch.arena[np.minimum(idx, batch.arena.size - 1)]
+        head[np.arange(slot)[None, :] >= ln[:, None]] = 0
+        arena[:n * slot] = head.reshape(-1)
+    desc = np.stack([(np.arange(n, dtype=np.int64) * slot).astype(np.uint32),
+                     batch.desc[:, 1].astype(np.uint32)], axis=1)
+    return Batch(arena=arena, desc=np.ascontiguousarray(desc),
+                 meta=dict(batch.meta, layout=f"header-split {slot}"))
+
+
 def inject_errors(batch: Batch, rate: float, seed: int = 7, kinds=range(6),
                   ip_off: int = 14) -> np.ndarray:
     """Corrupt ~``rate`` of the packets per kind, in place. Returns int8[n] kind

@@ -24,6 +24,17 @@ pmc() {  # name counters... -- bench-args...
   while [ "$1" != "--" ]; do ctrs+=("$1"); shift; done; shift
   step "$name" 120 rocprofv3 --pmc "${ctrs[@]}" --kernel-include-regex k_rx -f csv -d "gpurun_out/prof_$name" -o run -- python3 bench.py "$@"
 }
+pmcv() {  # tag bench-args...: the three PMC passes of one variant, one batch per launch
+  local tag=$1; shift
+  local a="--steps 40 --warmup 4 --no-cpu --no-timing --streams 1 --fuse 1"
+  pmc "pmc_fetch_$tag" FETCH_SIZE -- $a "$@" &&
+  pmc "pmc_write_$tag" WRITE_SIZE -- $a "$@" &&
+  pmc "pmc_ea_$tag" TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum -- $a "$@"
+}
+var() {  # 200-step run of one variant (fused launches, the default layout)
+  local n; n=$(echo "$*" | tr -d ' -' | cut -c1-48)
+  step "var_$n" 300 python bench.py --steps 200 --warmup 20 --no-cpu "$@"
+}
 DRV="--gpus 1 --steps 20 --warmup 5"
 IFS=, read -ra ST <<< "${STEPS:-tests,smoke,bench}"
 for s in "${ST[@]}"; do
@@ -133,6 +144,32 @@ for s in "${ST[@]}"; do
     # the driver's 8-rank command shape, rehearsed on one GPU (gloo: RCCL needs a GPU per rank)
     dist8) step dist8_weak 900 python bench.py --gpus 8 --backend gloo --steps 20 --warmup 5 --no-cpu &&
            step dist8_strong 900 python bench.py --gpus 8 --backend gloo --shard strong --steps 20 --warmup 5 --no-cpu ;;
+    # round 5: every variant on the final kernel sources, 200 steps
+    r5var) var && var --workload c3 && var --workload c3 --layout split && var --workload c4 &&
+           var --workload c5 && var --workload c5 --layout split && var --classify ipclass16 &&
+           var --workload c4 --classify ipclass16 && var --classify ipclass16 --program-jit 0 &&
+           var --classify lbcrc && var --l4 udp && var --rewrite && var --partition global && var --no-perm &&
+           var --errors 0.01 && var --shard strong && var --flow-capacity 1 &&
+           var --workload c3 --flow-capacity 20000 && var --workload c4 --flow-capacity 2000000 &&
+           var --workload c4 --flow-capacity 2000000 --flow-manager imp --flow-timeout 1 ;;
+    r5sweep) for fb in 128 256 512 1024 1500; do var --frame-bytes $fb && var --frame-bytes $fb --layout split || exit $?; done ;;
+    # round 5: PMC traffic of the variants (profiles/pmc_traffic.json, scripts/pmc_traffic.py)
+    r5pmc) pmcv c2 && pmcv c3 --workload c3 && pmcv c3split --workload c3 --layout split &&
+           pmcv c5 --workload c5 && pmcv c5split --workload c5 --layout split ;;
+    r5pmc2) pmcv c4 --workload c4 && pmcv c4flow --workload c4 --flow-capacity 2000000 &&
+            pmcv ipc16 --classify ipclass16 && pmcv l4udp --l4 udp && pmcv rewrite --rewrite &&
+            pmcv fb1500 --frame-bytes 1500 && pmcv fb1500split --frame-bytes 1500 --layout split ;;
+    # round 5: the flow re-shard inside the bench (N = 1 on the GPU, the 8-rank command shape over gloo)
+    reshard) step reshard1 300 python bench.py --flow-reshard --workload c4 --steps 50 --warmup 5 --no-cpu &&
+             step reshard8 900 python bench.py --gpus 8 --backend gloo --flow-reshard --workload c4 --steps 5 --warmup 1 --no-cpu ;;
+    # round 5: the crossover's staging experiment -- zero-copy shared launches (default) against the
+    # same launches with one hipMemcpyAsync of each batch's staged block each way (FCGPU_AGG_STAGE=copy),
+    # beside the CPU port, three interleaved rounds
+    stagexp) for r in 1 2 3; do
+               step "stage_zc_$r" 300 python -u scripts/crossover.py --chains base,udp --threads 8,16 --no-cpu &&
+               FCGPU_AGG_STAGE=copy step "stage_copy_$r" 300 python -u scripts/crossover.py --chains base,udp --threads 8,16 --no-cpu &&
+               step "stage_cpu_$r" 300 python -u scripts/crossover.py --chains base,udp --threads 8,16 --no-gpu || exit $?
+             done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

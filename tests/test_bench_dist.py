@@ -147,6 +147,37 @@ def test_gpu_bench_two_ranks():
         assert line["config"]["packets_per_step"] == (131072 if shard == "weak" else 65536)
 
 
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_gpu_bench_flow_reshard(gpus):
+    """`bench.py --flow-reshard`: every step runs the owner pass, the exchange
+    kernels, the all-to-alls (gloo on one GPU for 2 ranks) and the flow table
+    over the received batch; inside the run the all-reduced valid count is
+    every packet once, and the tables' flow counts add up to the distinct
+    5-tuples of the ranks' batches (config.flow_reshard.checked)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--backend", "gloo",
+                        "--flow-reshard", "--workload", "c4", "--packets", "65536", "--steps", "3", "--warmup", "1",
+                        "--nbuf", "2", "--no-cpu"], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    fr = line["config"]["flow_reshard"]
+    assert fr["checked"] and fr["flow_table_flows"] == fr["distinct_5tuples"] == 65536 * gpus
+    assert fr["packets_received"] == fr["packets_sent"] == 65536 * gpus * 3
+    assert set(fr["stage_ms_per_step"]) == {"owner_pass", "plan_pack", "exchange", "unpack", "flow_pass"}
+
+
+def test_flow_reshard_options():
+    import bench
+    a = bench.parse(["--flow-reshard", "--workload", "c4"])
+    assert a.flow_reshard and a.streams == 1
+    for bad in (["--flow-reshard"], ["--flow-reshard", "--workload", "c4", "--shard", "strong"],
+                ["--flow-reshard", "--workload", "c4", "--flow-manager", "imp"]):
+        with pytest.raises(SystemExit):
+            bench.parse(bad)
+
+
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_strong_shards_rotate_beyond_the_infinity_cache(world):
     """--shard strong (C4, 1M packets): every rank uploads only its own
