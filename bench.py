@@ -674,12 +674,14 @@ class ReshardProcessor:
         self.ctx_own = N.Context(gpu, max(n, 1), own_cfg)
         self.own_out = DeviceOutputs(max(n, 1), self.world, device=dev, verdict=True, hash=False,
                                      perm=True, port_start=True, partition=N.PART_GLOBAL)
-        # a rank receives ~n packets (uniform owners); room for 2n
-        self.cap = 2 * max(n, 1)
+        # a rank receives ~n packets (uniform owners); the flow pass takes them
+        # in batches of at most cap (the flow table's largest batch,
+        # FCGPU_FLOW_MAX_BATCH), in order, so any count fits
+        self.cap = min(N.FLOW_MAX_BATCH, 2 * max(n, 1))
         flow_cfg = N.make_cfg(offset=14, checksum=True, hash_mode=N.HASH_FLOWID, classify=N.CLS_LB_HASH,
                               nports=args.nports)
         self.ctx_flow = N.Context(gpu, self.cap, flow_cfg)
-        self.ctx_flow.flow_enable(args.flow_capacity or self.cap)
+        self.ctx_flow.flow_enable(args.flow_capacity or 2 * max(n, 1))     # room for every flow a rank owns
         self.flow_out = DeviceOutputs(self.cap, args.nports, device=dev, verdict=True, hash=True,
                                       tile_perm=True, partition=N.PART_TILE, flowid=True)
         self.ctr = torch.zeros(N.CTR_SHARDS, N.NCOUNTERS, dtype=torch.int64, device=dev)
@@ -711,12 +713,12 @@ class ReshardProcessor:
             ev[3].record(s)
         rdesc = DV.exchange_unpack(self.ctx_own, rmeta, displ)
         m = int(rdesc.shape[0])
-        if m > self.cap:
-            raise RuntimeError(f"rank {self.rank} received {m} packets, more than the flow context's {self.cap}")
         if ev:
             ev[4].record(s)
         f = self.flow_out
-        self.ctx_flow.process(buf.data_ptr(), rdesc.data_ptr(), m, stream=s.cuda_stream, **f.ptrs())
+        for c0 in range(0, m, self.cap):
+            k = min(self.cap, m - c0)
+            self.ctx_flow.process(buf.data_ptr(), rdesc[c0:].data_ptr(), k, stream=s.cuda_stream, **f.ptrs())
         if ev:
             ev[5].record(s)
             torch.cuda.synchronize()

@@ -1908,15 +1908,6 @@ struct AggItem {
     uint32_t slot;
     fcgpu_job job;            // device (mapped) addresses
     uint32_t layout;          // kLay* bits of job's descriptors and annotations
-    // FCGPU_AGG_STAGE=copy: job reads the slot's device copy of its staged
-    // block (h_in -> d_in before the launch) and writes the device result
-    // block (d_res -> h_out after it); h_in null: zero-copy
-    const void *h_in;
-    uint8_t *d_in;
-    size_t in_bytes;
-    void *h_out;
-    const uint8_t *d_res;
-    size_t out_bytes;
     // the launch inputs, taken on the owner's thread at submit time: the
     // launch may happen on another context's thread, later
     DevCfg dcfg;
@@ -1990,12 +1981,6 @@ struct AggIssue {
     hipFunction_t fn;
     hipStream_t st;
     AggLaunch *al;
-    struct Copy {
-        void *dst;
-        const void *src;
-        size_t bytes;
-    };
-    std::vector<Copy> h2d, d2h;      // FCGPU_AGG_STAGE=copy: the items' blocks, each way
 };
 // Take every pending submission (q.mu held) as launches: the first one with
 // the next ones of its configuration, up to kMaxFuse per launch, until none
@@ -2039,10 +2024,6 @@ static void agg_take_locked(AggQueue &q, std::vector<AggIssue> &out) {
             J.n = j.n;
             J.tile0 = tiles;
             J.layout = it.layout;
-            if (it.h_in) {
-                is.h2d.push_back({it.d_in, it.h_in, it.in_bytes});
-                is.d2h.push_back({it.h_out, it.d_res, it.out_bytes});
-            }
             tiles += (j.n + kTile - 1) / kTile;
         }
         is.tiles = tiles;
@@ -2107,8 +2088,6 @@ static void agg_issue(int device, std::vector<AggIssue> &iss) {
     for (AggIssue &is : iss) {
         hipError_t e = dev_ok && is.st && is.al->ev ? hipSuccess : hipErrorInvalidValue;
         if (e == hipSuccess && fault_take(FCGPU_FAULT_LAUNCH)) e = hipErrorLaunchFailure;
-        for (const AggIssue::Copy &cp : is.h2d)
-            if (e == hipSuccess) e = hipMemcpyAsync(cp.dst, cp.src, cp.bytes, hipMemcpyHostToDevice, is.st);
         if (e == hipSuccess) {
             if (is.fn) {
                 e = launch_rx_fn(is.fn, is.part, is.L, is.tiles, is.st);
@@ -2117,8 +2096,6 @@ static void agg_issue(int device, std::vector<AggIssue> &iss) {
                 if (e == hipSuccess) e = hipGetLastError();
             }
         }
-        for (const AggIssue::Copy &cp : is.d2h)
-            if (e == hipSuccess) e = hipMemcpyAsync(cp.dst, cp.src, cp.bytes, hipMemcpyDeviceToHost, is.st);
         if (e == hipSuccess) e = hipEventRecord(is.al->ev, is.st);
         if (e != hipSuccess) (void)hipGetLastError();
         is.al->state.store(e == hipSuccess ? kAggIssued : kAggFailed, std::memory_order_release);
@@ -2153,9 +2130,8 @@ static void agg_release(int device) {
 // Queue one zero-copy block submission (device addresses in j). Once queued
 // the submission is the owner's to wait for: a failed launch (of its group or
 // another) is reported by that wait (AggLaunch::state), never by this call.
-static int agg_submit(fcgpu_ctx *c, uint32_t slot, const fcgpu_job &j, uint32_t layout, const AggItem *copy) {
+static int agg_submit(fcgpu_ctx *c, uint32_t slot, const fcgpu_job &j, uint32_t layout) {
     AggItem it{};
-    if (copy) it = *copy;          // the staging copies (FCGPU_AGG_STAGE=copy)
     it.c = c;
     it.slot = slot;
     it.job = j;
@@ -2333,17 +2309,6 @@ static hipError_t span_stream(fcgpu_ctx *c, uint32_t slot, hipStream_t *out) {
     return hipSuccess;
 }
 
-// FCGPU_AGG_STAGE=copy (an experiment): the shared
-// queue's launches copy each batch's staged block to the device and its
-// result block back (one hipMemcpyAsync each way per batch, on the launch's
-// stream) instead of the kernel reading and writing them over PCIe.
-// Read at every zero-copy submission (a getenv per batch of thousands of
-// packets), so a test can switch it within one process.
-static bool agg_stage_copy() {
-    const char *e = getenv("FCGPU_AGG_STAGE");
-    return e && !strcmp(e, "copy");
-}
-
 int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_t in_bytes, size_t desc_off,
                             size_t frames_off, uint32_t n, void *h_out, uint32_t outputs, uint32_t partition) {
     if (!c || slot >= FCGPU_SPAN_SLOTS || (n && (!h_in || !h_out))) return FCGPU_EINVAL;
@@ -2377,17 +2342,7 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
     hipStream_t ss = nullptr;
     HIPCHK(c, span_stream(c, slot, &ss));
     const bool zc = !force_copy && span_zerocopy(c);
-    // the shared queue with staging copies: device blocks as in copy mode
-    bool aggc = false;
-    if (zc && n && agg_stage_copy()) {
-        fcgpu_out probe{};
-        probe.partition = partition;
-        if (L.perm != FCGPU_OUT_ABSENT) probe.perm = reinterpret_cast<uint32_t *>(1);
-        if (L.tile_perm != FCGPU_OUT_ABSENT) probe.tile_perm = reinterpret_cast<uint8_t *>(1);
-        if (L.port_start != FCGPU_OUT_ABSENT) probe.port_start = reinterpret_cast<uint32_t *>(1);
-        aggc = agg_eligible(c, probe);
-    }
-    if (zc && n && !aggc) {
+    if (zc && n) {
         // the kernels read h_in and write h_out where they lie (page-locked
         // memory mapped into the device's address space): no copy engine
         if (h_in != sp.zc_hin) {
@@ -2418,7 +2373,7 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
         HIPCHK(c, memset_sync(sp.d_in, 0, cap));
         sp.in_cap = cap;
     }
-    if ((!zc || aggc) && L.bytes > sp.res_cap) {
+    if (!zc && L.bytes > sp.res_cap) {
         HIPCHK(c, hipStreamSynchronize(ss));
         hipFree(sp.d_res);
         sp.d_res = nullptr;
@@ -2433,7 +2388,7 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
     sp.s = c->fl.slots ? c->stream : ss;
     hipStream_t s = sp.s;
     if (n == 0) return FCGPU_OK;
-    uint8_t *din = zc && !aggc ? sp.zc_din : sp.d_in, *dres = zc && !aggc ? sp.zc_dout : sp.d_res;
+    uint8_t *din = zc ? sp.zc_din : sp.d_in, *dres = zc ? sp.zc_dout : sp.d_res;
     if (!zc) HIPCHK(c, hipMemcpyAsync(sp.d_in, h_in, in_bytes, hipMemcpyHostToDevice, s));
     auto at = [&](size_t o) -> void * { return o == FCGPU_OUT_ABSENT ? nullptr : dres + o; };
     fcgpu_out d{};
@@ -2455,17 +2410,7 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
         j.out = d;
         int rc = check_process(c, j.arena, j.desc, n, &j.out);
         if (rc != FCGPU_OK) return rc;
-        if (aggc) {
-            AggItem cp{};
-            cp.h_in = h_in;
-            cp.d_in = sp.d_in;
-            cp.in_bytes = in_bytes;
-            cp.h_out = h_out;
-            cp.d_res = sp.d_res;
-            cp.out_bytes = L.bytes;
-            return agg_submit(c, slot, j, layout, &cp);
-        }
-        return agg_submit(c, slot, j, layout, nullptr);
+        return agg_submit(c, slot, j, layout);
     }
     int rc = check_process(c, din + frames_off, descp(din), n, &d);
     if (rc == FCGPU_OK) rc = process_one(c, din + frames_off, descp(din), n, &d, s, layout);

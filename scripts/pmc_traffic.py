@@ -27,6 +27,8 @@ OUT = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
 def per_dispatch(path, counter):
+    if not os.path.isdir(path):      # scripts/session.sh writes rocprofv3 output under prof_<step>/
+        path = os.path.join(os.path.dirname(path), "prof_" + os.path.basename(path))
     vals = collections.defaultdict(float)
     for r in csv.DictReader(open(os.path.join(path, "run_counter_collection.csv"))):
         if r["Counter_Name"] == counter and "k_rx" in r["Kernel_Name"]:
@@ -57,7 +59,7 @@ def entry(sess, tag, argv):
         "read_over_algorithmic": round(rd / alg, 4),
         "read_bytes_per_packet": round(rd / pk, 2),
         "correction": "read bytes = FETCH_SIZE(KB)*1024*2 (gfx950 half-count, MI355X_MICROARCH.md HBM)",
-        "source": f"{os.path.relpath(sess, ROOT)}/pmc_fetch_{tag}, pmc_write_{tag}, pmc_ea_{tag} "
+        "source": f"{os.path.relpath(sess, ROOT)}/prof_pmc_fetch_{tag}, prof_pmc_write_{tag}, prof_pmc_ea_{tag} "
                   f"(rocprofv3 --pmc, one pass each, {nd} k_rx dispatches of one {pk}-packet batch after "
                   f"4 warmup launches, mean per dispatch)",
     }

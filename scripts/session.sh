@@ -162,14 +162,6 @@ for s in "${ST[@]}"; do
     # round 5: the flow re-shard inside the bench (N = 1 on the GPU, the 8-rank command shape over gloo)
     reshard) step reshard1 300 python bench.py --flow-reshard --workload c4 --steps 50 --warmup 5 --no-cpu &&
              step reshard8 900 python bench.py --gpus 8 --backend gloo --flow-reshard --workload c4 --steps 5 --warmup 1 --no-cpu ;;
-    # round 5: the crossover's staging experiment -- zero-copy shared launches (default) against the
-    # same launches with one hipMemcpyAsync of each batch's staged block each way (FCGPU_AGG_STAGE=copy),
-    # beside the CPU port, three interleaved rounds
-    stagexp) for r in 1 2 3; do
-               step "stage_zc_$r" 300 python -u scripts/crossover.py --chains base,udp --threads 8,16 --no-cpu &&
-               FCGPU_AGG_STAGE=copy step "stage_copy_$r" 300 python -u scripts/crossover.py --chains base,udp --threads 8,16 --no-cpu &&
-               step "stage_cpu_$r" 300 python -u scripts/crossover.py --chains base,udp --threads 8,16 --no-gpu || exit $?
-             done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

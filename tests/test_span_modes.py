@@ -314,16 +314,6 @@ def test_gpu_auto_shared_queue_fuses_contexts(oracle, nsub):
 
 
 @pytest.mark.gpu
-def test_gpu_auto_shared_queue_copy_staging(oracle, monkeypatch):
-    """FCGPU_AGG_STAGE=copy (the staging experiment of DESIGN section 5.4): the
-    shared queue copies every batch's staged block to the device and its
-    result block back around the fused launch instead of reading them over
-    PCIe; the results and per-context counters are the oracle's as before."""
-    monkeypatch.setenv("FCGPU_AGG_STAGE", "copy")
-    test_gpu_auto_shared_queue_fuses_contexts(oracle, 9)
-
-
-@pytest.mark.gpu
 def test_gpu_auto_shared_queue_threads(oracle):
     """Eight threads, each with its own AUTO context and two slots, submitting
     and waiting concurrently through the shared queue (ctypes releases the
