@@ -132,8 +132,8 @@ def parse(argv=None):
     ap.add_argument("--flow-reshard", action="store_true",
                     help="(f)#1 x (e): every step re-shards the rank's batch by flow before the flow table "
                          "(SURVEY 8(f) #1 on several GPUs): the device owner pass (LB_MODE hash over the "
-                         "world's ranks, whole-batch partition), fcgpu_exchange_plan/_pack, the RCCL "
-                         "all-to-alls of records and frames (dist.exchange_segments), fcgpu_exchange_unpack, "
+                         "world's ranks, verdicts), fcgpu_exchange_build, the RCCL all-to-alls of counts, "
+                         "records and frames (dist.exchange_built), fcgpu_exchange_unpack, "
                          "then the FlowIPManagerHMP pass over the received batch; C4 (uniform 5-tuples, a "
                          "different batch per rank). Per-stage times and checked flow counts in "
                          "config.flow_reshard; a labelled variant, never the headline")
@@ -620,13 +620,15 @@ class ReshardProcessor:
     Rank r's batch is its own C4 batch (seed 4 + r: independent uniform
     5-tuples, so every rank's flows are new to the others); per step:
 
-      owner pass   k_rx + k_scan + k_part_multi: LB_MODE hash over `world`
-                   outputs (the FlowSwitch formula on the IPFlowID hash), the
-                   whole-batch partition -> each packet's owner rank
-      plan, pack   fcgpu_exchange_plan (3 kernels) + fcgpu_exchange_pack
-      exchange     dist.exchange_segments: RCCL all-to-all of the per-owner
-                   counts, then of the records and the frame bytes (world 1:
-                   the send buffer is the received one, no collective)
+      owner pass   k_rx: LB_MODE hash over `world` outputs (the FlowSwitch
+                   formula on the IPFlowID hash), verdicts only -> each
+                   packet's owner rank
+      build        fcgpu_exchange_build (3 kernels): records and send buffer
+                   straight from the verdicts, every load in input order
+      exchange     dist.exchange_built: RCCL all-to-all of the per-owner
+                   counts from the device, one host sync for the split sizes,
+                   then the records and the frame bytes (world 1: the send
+                   buffer is the received one, no collective)
       unpack       fcgpu_exchange_unpack: records -> descriptors
       flow pass    k_rx with the FlowIPManagerHMP table + the new-flow pass over
                    the received batch (tile partition, 16 outputs)
@@ -672,8 +674,8 @@ class ReshardProcessor:
         own_cfg = N.make_cfg(offset=14, checksum=True, hash_mode=N.HASH_FLOWID, classify=N.CLS_LB_HASH,
                              nports=self.world)
         self.ctx_own = N.Context(gpu, max(n, 1), own_cfg)
-        self.own_out = DeviceOutputs(max(n, 1), self.world, device=dev, verdict=True, hash=False,
-                                     perm=True, port_start=True, partition=N.PART_GLOBAL)
+        self.own_out = DeviceOutputs(max(n, 1), self.world, device=dev, verdict=True, hash=False)
+        self.send_cap = stride + 4 * max(n, 1)      # every frame's slot (the arena's bytes + 4 per packet)
         # a rank receives ~n packets (uniform owners); the flow pass takes them
         # in batches of at most cap (the flow table's largest batch,
         # FCGPU_FLOW_MAX_BATCH), in order, so any count fits
@@ -693,7 +695,7 @@ class ReshardProcessor:
     def _step(self, k, timed):
         import torch
         from fastclick_amd import device as DV
-        from fastclick_amd.dist import exchange_segments
+        from fastclick_amd.dist import exchange_built
         N = self.N
         a, d = self.bufs[k % len(self.bufs)]
         s = torch.cuda.current_stream()
@@ -704,11 +706,11 @@ class ReshardProcessor:
         self.ctx_own.process(a.data_ptr(), d.data_ptr(), self.n, stream=s.cuda_stream, **o.ptrs())
         if ev:
             ev[1].record(s)
-        send, meta, seg_n, seg_bytes = DV.exchange_pack(self.ctx_own, a, d, o.perm, o.port_start,
-                                                        self.world, self.rank)
+        send, meta, seg_n, seg_bytes = DV.exchange_build(self.ctx_own, a, d, o.verdict, self.world, self.rank,
+                                                         send_cap=self.send_cap)
         if ev:
             ev[2].record(s)
-        buf, rmeta, displ = exchange_segments(send, meta, seg_n, seg_bytes)
+        buf, rmeta, displ = exchange_built(send, meta, seg_n, seg_bytes)
         if ev:
             ev[3].record(s)
         rdesc = DV.exchange_unpack(self.ctx_own, rmeta, displ)
@@ -768,7 +770,7 @@ class ReshardProcessor:
         if received != sent:
             raise AssertionError(f"{received} packets received, {sent} sent")
         steps = max(self.timed_steps, 1)
-        names = ("owner_pass", "plan_pack", "exchange", "unpack", "flow_pass")
+        names = ("owner_pass", "build", "exchange", "unpack", "flow_pass")
         return {"flow_table_flows": flows, "distinct_5tuples": distinct, "packets_received": received,
                 "packets_sent": sent, "checked": True,
                 **({"stage_ms_per_step": {k: round(t / steps, 4) for k, t in zip(names, self.stage_ms)},
@@ -947,8 +949,8 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                          + (f" (with-errors mix: {args.errors:g} each of bad version, header length, "
                             f"ip_len, checksum, BADSRC)" if args.errors else "")
                          + (f" + Check{args.l4.upper()}Header" if args.l4 != "none" else "")
-                         + (f" + flow re-shard across the {world} rank(s) (owner pass, fcgpu_exchange_plan/"
-                            f"pack, all-to-all of records and frames, fcgpu_exchange_unpack) + FlowIPManagerHMP "
+                         + (f" + flow re-shard across the {world} rank(s) (owner pass, fcgpu_exchange_build, "
+                            f"all-to-alls of counts, records and frames, fcgpu_exchange_unpack) + FlowIPManagerHMP "
                             f"flow table over the received batch" if args.flow_reshard else "")
                          + ((f" + FlowIPManagerHMP flow table ({args.flow_capacity} IDs)"
                              if args.flow_manager == "hmp" else

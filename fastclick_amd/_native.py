@@ -15,7 +15,7 @@ LIBFCGPU = os.environ.get("FCGPU_LIB") or os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 21
+ABI_VERSION = 22
 SPAN_SLOTS = 3
 SPAN_COPY = 0
 SPAN_ZEROCOPY = 1
@@ -243,6 +243,9 @@ FCGPU_SYMBOLS = {
                                       C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p]),
     "fcgpu_exchange_unpack": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64), C.c_uint32,
                                         C.c_void_p, C.c_void_p]),
+    "fcgpu_exchange_build": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                       C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                       C.c_void_p]),
     "fcgpu_last_error": (C.c_char_p, [C.c_void_p]),
 }
 
@@ -519,6 +522,13 @@ class Context:
         (after exchange_plan of the same batch on this context)."""
         self._chk(self.lib.fcgpu_exchange_pack(self.h, arena, port_start, meta, seg_bytes, n, world,
                                                send or None, send_cap, stream or None), "fcgpu_exchange_pack")
+
+    def exchange_build(self, arena, desc, verdict, n, world, rank, meta, seg_n, seg_bytes, send, send_cap,
+                       stream=0):
+        """fcgpu_exchange_build on device pointers: records and send buffer from the owner pass's verdicts."""
+        self._chk(self.lib.fcgpu_exchange_build(self.h, arena, desc, verdict, n, world, rank, meta, seg_n,
+                                                seg_bytes, send or None, send_cap, stream or None),
+                  "fcgpu_exchange_build")
 
     def exchange_unpack(self, meta, n, src_displ, desc, stream=0):
         """fcgpu_exchange_unpack: received records -> descriptors (src_displ: per-source segment starts)."""

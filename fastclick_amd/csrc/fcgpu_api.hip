@@ -282,6 +282,8 @@ struct fcgpu_ctx {
     // flow re-shard plan (fcgpu_exchange_plan): block sums and segment starts
     unsigned long long *x_bsum = nullptr, *x_base = nullptr, *x_part = nullptr;
     uint32_t *x_src = nullptr;   // arena offset of each leaving frame (plan -> pack)
+    uint32_t *x_tcnt = nullptr;               // fcgpu_exchange_build: [64][max_tiles] per tile and owner
+    unsigned long long *x_tbyt = nullptr;
     std::string err;
 };
 
@@ -994,6 +996,8 @@ void fcgpu_close(fcgpu_ctx *c) {
         hipFree(c->x_base);
         hipFree(c->x_part);
         hipFree(c->x_src);
+        hipFree(c->x_tcnt);
+        hipFree(c->x_tbyt);
         pool_release(c);
         for (auto e : c->flow_order)
             if (e) hipEventDestroy(e);
@@ -2863,12 +2867,48 @@ int fcgpu_exchange_pack(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_
     // lanes per frame by the mean slot (send_cap / n): 16 B per lane per step
     hipStream_t s = static_cast<hipStream_t>(stream);
     const uint64_t mean = send_cap / n;
-    if (mean <= 64)
+    if (mean <= 96)
         hipLaunchKernelGGL(k_xpack<4>, dim3((n + kXThreads / 4 - 1) / (kXThreads / 4)), dim3(kXThreads), 0, s, X);
     else if (mean <= 512)
         hipLaunchKernelGGL(k_xpack<16>, dim3((n + kXThreads / 16 - 1) / (kXThreads / 16)), dim3(kXThreads), 0, s, X);
     else
         hipLaunchKernelGGL(k_xpack<64>, dim3((n + kXThreads / 64 - 1) / (kXThreads / 64)), dim3(kXThreads), 0, s, X);
+    HIPCHK(c, hipGetLastError());
+    return FCGPU_OK;
+}
+
+int fcgpu_exchange_build(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, const uint16_t *d_verdict,
+                         uint32_t n, uint32_t world, uint32_t rank, fcgpu_xmeta *d_meta, uint32_t *d_seg_n,
+                         uint64_t *d_seg_bytes, uint8_t *d_send, uint64_t send_cap, void *stream) {
+    if (!c) return FCGPU_EINVAL;
+    if (world == 0 || world > FCGPU_MAX_PORTS) return fail(c, FCGPU_EINVAL, "fcgpu_exchange_build: world must be 1..64");
+    if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "fcgpu_exchange_build: batch larger than the context's max_batch");
+    if (!d_seg_n || !d_seg_bytes || (n && (!d_arena || !d_desc || !d_verdict || !d_meta || (send_cap && !d_send))))
+        return fail(c, FCGPU_EINVAL, "fcgpu_exchange_build: null buffer");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (!c->x_tcnt) {
+        HIPCHK(c, hipMalloc(&c->x_tcnt, sizeof(uint32_t) * (size_t)FCGPU_MAX_PORTS * c->max_tiles));
+        HIPCHK(c, hipMalloc(&c->x_tbyt, sizeof(unsigned long long) * (size_t)FCGPU_MAX_PORTS * c->max_tiles));
+    }
+    XBuild B{};
+    B.arena = d_arena;
+    B.desc = d_desc;
+    B.verdict = d_verdict;
+    B.n = n;
+    B.ntiles = (n + kXTile - 1) / kXTile;
+    B.world = world;
+    B.rank = rank;
+    B.tcnt = c->x_tcnt;
+    B.tbyt = c->x_tbyt;
+    B.seg_n = d_seg_n;
+    B.seg_bytes = reinterpret_cast<unsigned long long *>(d_seg_bytes);
+    B.meta = reinterpret_cast<uint4 *>(d_meta);
+    B.send = d_send;
+    B.send_cap = send_cap;
+    if (B.ntiles) hipLaunchKernelGGL(k_xbtile, dim3(B.ntiles), dim3(kXTile), 0, s, B);
+    hipLaunchKernelGGL(k_xbscan, dim3(world), dim3(1024), 0, s, B);    // n = 0: zero counts
+    if (B.ntiles) hipLaunchKernelGGL(k_xbuild, dim3(B.ntiles), dim3(kXTile), 0, s, B);   // lanes per frame: per tile
     HIPCHK(c, hipGetLastError());
     return FCGPU_OK;
 }

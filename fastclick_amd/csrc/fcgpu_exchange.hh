@@ -253,6 +253,50 @@ __global__ __launch_bounds__(kXThreads) void k_xmeta(XPlan P) {
     }
 }
 
+// One frame into its 4-B aligned slot of (len + 3) & ~3 bytes at dstp, lpf
+// lanes (this one is q): 16 B per lane per step, four aligned dwords of the
+// source and the next one funnel-shifted (v_alignbyte) into four dwords of the
+// slot (frames start anywhere in the arena; the ABI's 16 B of readable slack
+// past a frame's end covers the fifth load). Slot bytes past the frame are
+// zero; nothing is stored past the slot. (Stores aligned to the destination
+// instead, the source loads then misaligned, measured slower: k_xpack 38.9 ->
+// 46.3 us for 1M 60-B frames, profiles/r05_exchange/README.md.)
+__device__ __forceinline__ void xcopy_frame(const uint8_t *src, uint32_t len, uint8_t *dstp, uint32_t q,
+                                            uint32_t lpf) {
+    const uintptr_t sa = reinterpret_cast<uintptr_t>(src);
+    const uint32_t sh = (uint32_t)(sa & 3u);
+    const uint32_t *al = reinterpret_cast<const uint32_t *>(sa & ~(uintptr_t)3);
+    uint32_t *out = reinterpret_cast<uint32_t *>(dstp);
+    for (uint32_t w = 16 * q; w < len; w += 16 * lpf) {
+        const xu4 a = *reinterpret_cast<const xu4 *>(al + (w >> 2));
+        // the fifth dword only when the frame reaches into it (so no read
+        // goes further than 16 B past the frame's end)
+        const uint32_t e = sh && w + 16 - sh < len ? al[(w >> 2) + 4] : 0u;
+        uint32_t v0 = __builtin_amdgcn_alignbyte(a.y, a.x, sh);
+        uint32_t v1 = __builtin_amdgcn_alignbyte(a.z, a.y, sh);
+        uint32_t v2 = __builtin_amdgcn_alignbyte(a.w, a.z, sh);
+        uint32_t v3 = __builtin_amdgcn_alignbyte(e, a.w, sh);
+        const uint32_t rem = len - w;
+        if (rem >= 16) {
+            xu4 o;
+            o.x = v0, o.y = v1, o.z = v2, o.w = v3;
+            *reinterpret_cast<xu4 *>(out + (w >> 2)) = o;
+        } else {
+            // the slot's last dwords: bytes past the frame zero, nothing past the slot
+            auto cut = [rem](uint32_t v, uint32_t k) -> uint32_t {
+                if (rem <= 4 * k) return 0u;
+                const uint32_t keep = rem - 4 * k;
+                return keep >= 4 ? v : v & ((1u << (8 * keep)) - 1u);
+            };
+            const uint32_t nd = (rem + 3) >> 2;
+            out[(w >> 2)] = cut(v0, 0);
+            if (nd > 1) out[(w >> 2) + 1] = cut(v1, 1);
+            if (nd > 2) out[(w >> 2) + 2] = cut(v2, 2);
+            if (nd > 3) out[(w >> 2) + 3] = cut(v3, 3);
+        }
+    }
+}
+
 struct XPack {
     const uint8_t *arena;
     const uint32_t *src;            // plan scratch: arena offset of each leaving frame
@@ -264,11 +308,7 @@ struct XPack {
     uint32_t n, world;
 };
 
-// LPF lanes per frame, 16 B each per step: four aligned dwords of the source
-// and the next one funnel-shifted into four aligned destination dwords
-// (frames start anywhere in the arena; the ABI's 16 B of readable slack past
-// a frame's end covers the fifth load). Slot bytes past the frame are zero;
-// nothing is stored past the slot.
+// LPF lanes per frame (xcopy_frame), frames in perm order.
 template <uint32_t LPF>
 __global__ __launch_bounds__(kXThreads) void k_xpack(XPack X) {
     __shared__ uint32_t s_ps[FCGPU_MAX_PORTS + 1];
@@ -308,37 +348,259 @@ __global__ __launch_bounds__(kXThreads) void k_xpack(XPack X) {
     if ((s_big >> own) & 1ull) return;
     const uint64_t dst = s_base[own] + r.x;
     if (dst + slot > X.send_cap) return;           // a send buffer smaller than the plan: nothing past it
-    const uintptr_t sa = reinterpret_cast<uintptr_t>(X.arena + so);
-    const uint32_t sh = (uint32_t)(sa & 3u);
-    const uint32_t *al = reinterpret_cast<const uint32_t *>(sa & ~(uintptr_t)3);
-    uint32_t *out = reinterpret_cast<uint32_t *>(X.send + dst);
-    for (uint32_t w = 16 * q; w < len; w += 16 * LPF) {
-        const xu4 a = *reinterpret_cast<const xu4 *>(al + (w >> 2));
-        // the fifth dword only when the frame reaches into it (so no read
-        // goes further than 16 B past the frame's end)
-        const uint32_t e = sh && w + 16 - sh < len ? al[(w >> 2) + 4] : 0u;
-        uint32_t v0 = __builtin_amdgcn_alignbyte(a.y, a.x, sh);
-        uint32_t v1 = __builtin_amdgcn_alignbyte(a.z, a.y, sh);
-        uint32_t v2 = __builtin_amdgcn_alignbyte(a.w, a.z, sh);
-        uint32_t v3 = __builtin_amdgcn_alignbyte(e, a.w, sh);
-        const uint32_t rem = len - w;
-        if (rem >= 16) {
-            xu4 o;
-            o.x = v0, o.y = v1, o.z = v2, o.w = v3;
-            *reinterpret_cast<xu4 *>(out + (w >> 2)) = o;
-        } else {
-            // the slot's last dwords: bytes past the frame zero, nothing past the slot
-            auto cut = [rem](uint32_t v, uint32_t k) -> uint32_t {
-                if (rem <= 4 * k) return 0u;
-                const uint32_t keep = rem - 4 * k;
-                return keep >= 4 ? v : v & ((1u << (8 * keep)) - 1u);
-            };
-            const uint32_t nd = (rem + 3) >> 2;
-            out[(w >> 2)] = cut(v0, 0);
-            if (nd > 1) out[(w >> 2) + 1] = cut(v1, 1);
-            if (nd > 2) out[(w >> 2) + 2] = cut(v2, 2);
-            if (nd > 3) out[(w >> 2) + 3] = cut(v3, 3);
+    xcopy_frame(X.arena + so, len, X.send + dst, q, LPF);
+}
+
+
+// ---- one pass from the owner pass's verdicts (fcgpu_exchange_build) ---------
+// The same records and send buffer as plan + pack, from a k_rx pass with
+// LB_MODE hash over `world` outputs that wrote only its verdicts (no
+// whole-batch partition, no owner-ordered gather of the descriptors): packet
+// i leaves to owner d = verdict[i] >> 8 when d < world. Each 256-packet tile
+// sorts its packets by owner in LDS (stable: a match-any rank per wave, the
+// waves' counts in order), so tile t's packets of owner d follow the tile's
+// earlier ones of d, and the tiles follow each other:
+//
+//   k_xbtile  per tile: packets and slot bytes of every owner
+//             -> tcnt[d][t], tbyt[d][t]
+//   k_xbscan  one workgroup per owner: exclusive scans of both over the
+//             tiles (the tile's first record / byte within the owner's run),
+//             seg_n[d], seg_bytes[d]
+//   k_xbuild  per tile again: every leaving packet's record at its place in
+//             owner order, then the tile's frames copied into their slots,
+//             owner by owner (consecutive destinations), LPF lanes a frame
+//
+// Every per-packet load (verdict, descriptor) is coalesced in input order;
+// the frames are read once and written once.
+constexpr uint32_t kXTile = 256;
+
+struct XBuild {
+    const uint8_t *arena;
+    const uint32_t *desc;           // [n][2]
+    const uint16_t *verdict;        // [n] reason | port << 8
+    uint32_t n, ntiles, world, rank;
+    uint32_t *tcnt;                 // [world][ntiles] -> exclusive scan over t
+    unsigned long long *tbyt;       // [world][ntiles] -> exclusive scan over t
+    uint32_t *seg_n;                // [world]
+    unsigned long long *seg_bytes;  // [world]
+    uint4 *meta;                    // fcgpu_xmeta [m] (dword-aligned)
+    uint8_t *send;
+    unsigned long long send_cap;
+};
+
+// inclusive scan of x over the 64 lanes of a wave
+__device__ __forceinline__ uint32_t xwave_incl(uint32_t x) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(x, d);
+        if (lane >= (uint32_t)d) x += u;
+    }
+    return x;
+}
+
+// The tile's stable sort by owner (LDS). Outputs per lane: own (world =
+// stays), pos (the lane's place among the tile's leaving packets in owner
+// order; valid when own < world), intra (its slot's byte offset within the
+// tile's run of its owner); in LDS: s_tcnt[d] / s_tstart[d] (the tile's
+// packets of owner d and where they start), s_pre[k] (exclusive byte prefix
+// in sorted order, s_pre[L] = the tile's leaving bytes). 256 threads.
+struct XTileLds {
+    uint32_t wc[4][FCGPU_MAX_PORTS + 1];     // per wave: packets of each owner
+    uint32_t tcnt[FCGPU_MAX_PORTS + 1];
+    uint32_t tstart[FCGPU_MAX_PORTS + 1];
+    uint32_t slot[kXTile];
+    uint32_t pre[kXTile + 1];
+    uint32_t wsum[4];
+};
+__device__ __forceinline__ void xtile_sort(const XBuild &B, uint32_t t, XTileLds &L, uint32_t &own, uint32_t &len,
+                                           uint32_t &src, uint32_t &pos, uint32_t &intra) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t i = t * kXTile + threadIdx.x;
+    own = B.world;
+    len = 0;
+    src = 0;
+    if (i < B.n) {
+        const uint32_t d = (uint32_t)B.verdict[i] >> 8;
+        const xu2 v = *reinterpret_cast<const xu2 *>(B.desc + 2 * (size_t)i);
+        src = v.x;
+        len = v.y;
+        own = d < B.world ? d : B.world;
+    }
+    // rank among the wave's lanes with the same owner (match-any over its bits)
+    const uint32_t nb = B.world + 1, nbits = 32 - __clz((nb - 1) | 1);
+    uint64_t grp = ~0ull;
+    for (uint32_t k = 0; k < nbits; ++k) {
+        const uint64_t bk = __ballot((own >> k) & 1u);
+        grp &= ((own >> k) & 1u) ? bk : ~bk;
+    }
+    const uint32_t rank = (uint32_t)__popcll(grp & ((1ull << lane) - 1ull));
+    for (uint32_t b = lane; b < nb; b += 64) L.wc[wave][b] = 0;
+    __builtin_amdgcn_wave_barrier();
+    if (rank == 0) L.wc[wave][own] = (uint32_t)__popcll(grp);
+    __syncthreads();
+    // per owner: the tile's count; the owners' starts (only leaving owners, in order)
+    if (wave == 0) {
+        uint32_t c = 0;
+        if (lane < B.world) c = L.wc[0][lane] + L.wc[1][lane] + L.wc[2][lane] + L.wc[3][lane];
+        const uint32_t inc = xwave_incl(c);
+        if (lane < B.world) {
+            L.tcnt[lane] = c;
+            L.tstart[lane] = inc - c;
         }
+        if (lane == 63) L.tstart[B.world] = inc;           // = the tile's leaving packets
+    }
+    __syncthreads();
+    pos = 0;
+    if (own < B.world) {
+        uint32_t wpre = 0;
+        for (uint32_t w = 0; w < wave; ++w) wpre += L.wc[w][own];
+        pos = L.tstart[own] + wpre + rank;
+        L.slot[pos] = (uint32_t)xslot(len);
+    }
+    const uint32_t nl = L.tstart[B.world];
+    __syncthreads();
+    // exclusive byte prefix over the sorted slots
+    const uint32_t v = threadIdx.x < nl ? L.slot[threadIdx.x] : 0u;
+    const uint32_t inc = xwave_incl(v);
+    if (lane == 63) L.wsum[wave] = inc;
+    __syncthreads();
+    uint32_t wp = 0;
+    for (uint32_t w = 0; w < wave; ++w) wp += L.wsum[w];
+    L.pre[threadIdx.x] = wp + inc - v;
+    if (threadIdx.x == kXTile - 1) L.pre[kXTile] = wp + inc;
+    __syncthreads();
+    intra = own < B.world ? L.pre[pos] - L.pre[L.tstart[own]] : 0u;
+}
+
+__global__ __launch_bounds__(kXTile) void k_xbtile(XBuild B) {
+    __shared__ XTileLds L;
+    uint32_t own, len, src, pos, intra;
+    const uint32_t t = blockIdx.x;
+    xtile_sort(B, t, L, own, len, src, pos, intra);
+    const uint32_t d = threadIdx.x;
+    if (d < B.world) {
+        const uint32_t a = L.tstart[d], c = L.tcnt[d];
+        B.tcnt[(size_t)d * B.ntiles + t] = c;
+        B.tbyt[(size_t)d * B.ntiles + t] = L.pre[a + c] - L.pre[a];
+    }
+}
+
+// owner d = blockIdx.x: exclusive scans over the tiles, in place; the totals
+__global__ __launch_bounds__(1024) void k_xbscan(XBuild B) {
+    __shared__ unsigned long long s_w[16];
+    __shared__ uint32_t s_c[16];
+    const uint32_t d = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t *cnt = B.tcnt + (size_t)d * B.ntiles;
+    unsigned long long *byt = B.tbyt + (size_t)d * B.ntiles;
+    const uint32_t per = (B.ntiles + 1023) / 1024, beg = threadIdx.x * per;
+    uint32_t cs = 0;
+    uint64_t bs = 0;
+    for (uint32_t k = 0; k < per; ++k)
+        if (beg + k < B.ntiles) {
+            cs += cnt[beg + k];
+            bs += byt[beg + k];
+        }
+    uint32_t ci = cs;
+    uint64_t bi = bs;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(ci, o);
+        const uint64_t ub = __shfl_up(bi, o);
+        if (lane >= (uint32_t)o) {
+            ci += u;
+            bi += ub;
+        }
+    }
+    if (lane == 63) {
+        s_c[wave] = ci;
+        s_w[wave] = bi;
+    }
+    __syncthreads();
+    uint32_t cp = 0, ct = 0;
+    uint64_t bp = 0, bt = 0;
+    for (uint32_t w = 0; w < 16; ++w) {
+        if (w < wave) {
+            cp += s_c[w];
+            bp += s_w[w];
+        }
+        ct += s_c[w];
+        bt += s_w[w];
+    }
+    uint32_t cr = cp + ci - cs;
+    uint64_t br = bp + bi - bs;
+    for (uint32_t k = 0; k < per; ++k)
+        if (beg + k < B.ntiles) {
+            const uint32_t c = cnt[beg + k];
+            const uint64_t b = byt[beg + k];
+            cnt[beg + k] = cr;
+            byt[beg + k] = br;
+            cr += c;
+            br += b;
+        }
+    if (threadIdx.x == 0) {
+        B.seg_n[d] = ct;
+        B.seg_bytes[d] = bt;
+    }
+}
+
+__global__ __launch_bounds__(kXTile) void k_xbuild(XBuild B) {
+    __shared__ XTileLds L;
+    __shared__ uint32_t s_src[kXTile], s_len[kXTile];
+    __shared__ unsigned long long s_dst[kXTile];
+    __shared__ uint32_t s_nbase[FCGPU_MAX_PORTS + 1];
+    __shared__ unsigned long long s_bbase[FCGPU_MAX_PORTS + 1];
+    __shared__ unsigned long long s_big;      // owners whose segment is 4 GiB or more: not packed
+    __shared__ uint32_t s_tc[FCGPU_MAX_PORTS];              // the tile's first record / byte within each owner's run
+    __shared__ unsigned long long s_tb[FCGPU_MAX_PORTS];
+    const uint32_t t = blockIdx.x;
+    // the tile's scanned bases (second wave) and the owners' record and byte
+    // bases (first wave), loaded before the sort so their latency hides under it
+    if (threadIdx.x >= 64 && threadIdx.x < 64 + B.world) {
+        const uint32_t d = threadIdx.x - 64;
+        s_tc[d] = B.tcnt[(size_t)d * B.ntiles + t];
+        s_tb[d] = B.tbyt[(size_t)d * B.ntiles + t];
+    }
+    if (threadIdx.x < 64) {
+        const uint32_t lane = threadIdx.x;
+        const uint32_t c = lane < B.world ? B.seg_n[lane] : 0u;
+        const uint64_t b = lane < B.world ? B.seg_bytes[lane] : 0ull;
+        const uint32_t ci = xwave_incl(c);
+        uint64_t bi = b;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t u = __shfl_up(bi, o);
+            if (lane >= (uint32_t)o) bi += u;
+        }
+        if (lane < B.world) {
+            s_nbase[lane] = ci - c;
+            s_bbase[lane] = bi - b;
+        }
+        const uint64_t big = __ballot(lane < B.world && b > 0xffffffffull);
+        if (lane == 0) s_big = big;
+    }
+    uint32_t own, len, src, pos, intra;
+    xtile_sort(B, t, L, own, len, src, pos, intra);      // its barriers publish the bases too
+    const uint32_t i = t * kXTile + threadIdx.x;
+    if (own < B.world) {
+        const uint32_t j = s_nbase[own] + s_tc[own] + (pos - L.tstart[own]);
+        const uint64_t off = s_tb[own] + intra;
+        *reinterpret_cast<xu4 *>(B.meta + j) = xu4{(uint32_t)off, len, i, B.rank};
+        s_src[pos] = src;
+        s_len[pos] = len;
+        s_dst[pos] = ((s_big >> own) & 1ull) ? ~0ull : s_bbase[own] + off;
+    }
+    __syncthreads();
+    // the tile's frames in owner order, lpf lanes each by the tile's mean
+    // slot (a 60-B frame is ~5 stores: 4 lanes; 1500 B ~95: 64)
+    const uint32_t nl = L.tstart[B.world];
+    const uint32_t mean = nl ? L.pre[kXTile] / nl : 0u;
+    const uint32_t lpf = mean <= 96 ? 4u : mean <= 384 ? 16u : mean <= 768 ? 32u : 64u;
+    for (uint32_t f = threadIdx.x / lpf; f < nl; f += kXTile / lpf) {
+        const uint64_t dst = s_dst[f];
+        const uint32_t fl = s_len[f];
+        if (dst == ~0ull || dst + xslot(fl) > B.send_cap) continue;   // nothing past the buffer
+        xcopy_frame(B.arena + s_src[f], fl, B.send + dst, threadIdx.x % lpf, lpf);
     }
 }
 

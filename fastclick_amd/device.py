@@ -176,6 +176,33 @@ def exchange_pack(ctx: N.Context, arena, desc, perm, port_start, world, rank, st
     return send, meta[:m], seg_n, seg_bytes
 
 
+def exchange_build(ctx: N.Context, arena, desc, verdict, world, rank, send_cap=None, stream=None):
+    """The send side in one call (fcgpu_exchange_build, HIP) from the owner
+    pass's verdicts (LB_MODE hash over `world` outputs, FCGPU_OUT_VERDICT
+    only). Returns (send, meta, seg_n, seg_bytes) as device tensors: the send
+    buffer (send_cap bytes + ARENA_PAD), the int32 [n, 4] record buffer (its
+    first sum(seg_n) rows are the records, in owner order), per owner its
+    packet count (int32) and byte count (int64). No host sync: send_cap
+    defaults to the arena's bytes + 4 per packet, which holds every leaving
+    frame's slot unless descriptors alias; the caller reads seg_bytes (one
+    sync it needs anyway for the all-to-all) and dist.exchange_segments
+    checks the total against the buffer."""
+    torch = _torch()
+    from .dist import ARENA_PAD
+    n = int(desc.shape[0])
+    dev = desc.device
+    s = stream if stream is not None else torch.cuda.current_stream()
+    if send_cap is None:
+        send_cap = int(arena.numel()) + 4 * n
+    meta = torch.empty((max(n, 1), 4), dtype=torch.int32, device=dev)
+    seg_n = torch.empty(world, dtype=torch.int32, device=dev)
+    seg_b = torch.empty(world, dtype=torch.int64, device=dev)
+    send = torch.empty(int(send_cap) + ARENA_PAD, dtype=torch.uint8, device=dev)
+    ctx.exchange_build(arena.data_ptr(), desc.data_ptr(), verdict.data_ptr(), n, world, rank, meta.data_ptr(),
+                       seg_n.data_ptr(), seg_b.data_ptr(), send.data_ptr(), int(send_cap), stream=s.cuda_stream)
+    return send, meta, seg_n, seg_b
+
+
 def exchange_unpack(ctx: N.Context, meta, src_displ, stream=None):
     """The receive side (fcgpu_exchange_unpack, HIP): records -> int32 [k, 2]
     descriptors (uint32 bit patterns) into the received buffer, whose source r

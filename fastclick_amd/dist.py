@@ -125,6 +125,55 @@ def exchange_segments(send, meta, seg_n, seg_bytes, group=None):
     return buf, rmeta, displ
 
 
+def exchange_built(send, meta, seg_n, seg_bytes, group=None):
+    """The all-to-all of a send side built by device.exchange_build (segment
+    sizes still on the device): the per-owner counts go to their owners
+    straight from the device tensors, and one host sync reads this rank's
+    sizes and the sizes it receives together -- the all-to-alls of records
+    and frames need them as host split lists. Returns exchange_segments'
+    (buffer, meta, src_displ)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    if seg_n.numel() != world or seg_bytes.numel() != world:
+        raise ValueError(f"{seg_n.numel()} owner segments for a world of {world}")
+    cnt = torch.stack([seg_n.to(torch.int64), seg_bytes], dim=1)      # [world, 2]
+    if world > 1 and not (send.is_cuda and dist.get_backend(group) == "gloo"):
+        rcnt = torch.empty_like(cnt)
+        dist.all_to_all_single(rcnt, cnt, group=group)
+        both = torch.cat([cnt, rcnt]).cpu().tolist()                  # the one host sync
+        mine, theirs = both[:world], both[world:]
+    else:
+        mine, theirs = cnt.cpu().tolist(), None
+    sn, sb = [int(r[0]) for r in mine], [int(r[1]) for r in mine]
+    total = sum(sb)
+    if total + ARENA_PAD > send.numel() or max(sb, default=0) > 0xFFFFFFFF:
+        raise ValueError(f"exchange_built: {total} B of segments for a {send.numel() - ARENA_PAD}-B send "
+                         "buffer (aliasing descriptors?) or an owner's segment past 4 GiB")
+    m = sum(sn)
+    if world == 1:
+        # the send buffer is the received one: zero its pad after the frames
+        send[total:total + ARENA_PAD].zero_()
+        return send, meta[:m], [0]
+    if theirs is None:                                                # gloo rehearsal: host all-to-alls
+        return exchange_segments(send[:total + ARENA_PAD], meta[:m], sn, sb, group=group)
+    dev = send.device
+    rn, rb = [int(r[0]) for r in theirs], [int(r[1]) for r in theirs]
+    rtotal = sum(rb)
+    if rtotal + ARENA_PAD >= 1 << 32:
+        raise ValueError("received frames exceed the 4 GiB a uint32 descriptor offset addresses")
+    rmeta = torch.empty((sum(rn), 4), dtype=torch.int32, device=dev)
+    dist.all_to_all_single(rmeta, meta[:m].contiguous(), rn, sn, group=group)
+    buf = torch.empty(rtotal + ARENA_PAD, dtype=torch.uint8, device=dev)
+    buf[rtotal:].zero_()
+    dist.all_to_all_single(buf[:rtotal], send[:total], rb, sb, group=group)
+    displ, at = [], 0
+    for b in rb:
+        displ.append(at)
+        at += b
+    return buf, rmeta, displ
+
+
 def exchange_by_flow(ctx, arena, desc, perm, port_start, group=None):
     """Re-shard this rank's device batch by owner rank (one all-to-all).
 

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 21
+#define FCGPU_ABI_VERSION 22
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -685,6 +685,23 @@ int  fcgpu_exchange_pack(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t 
                          uint8_t *d_send, uint64_t send_cap, void *stream);
 int  fcgpu_exchange_unpack(fcgpu_ctx *ctx, const fcgpu_xmeta *d_meta, uint32_t n, const uint64_t *src_displ,
                            uint32_t world, uint32_t *d_desc, void *stream);
+
+/* The send side in one call, from the owner pass's verdicts instead of its
+ * whole-batch partition: packet i leaves to owner d = d_verdict[i] >> 8 when
+ * d < world (a k_rx pass with LB_MODE hash over `world` outputs; the invalid
+ * list, port `world`, stays). Writes exactly what fcgpu_exchange_plan +
+ * fcgpu_exchange_pack write for the stable partition of those owners (records
+ * in owner order, input order within an owner; owner d's segment; slot
+ * padding zero), plus d_seg_n[d], the packets of owner d. send_cap bounds the
+ * send buffer as for fcgpu_exchange_pack (the sum of the leaving frames'
+ * slots fits in send_cap whenever it is at least the arena's frame bytes +
+ * 3 per packet), so no host sync is needed before the call. Every per-packet
+ * load is in input order (three launches: per-tile owner counts and bytes,
+ * their scan per owner, the records and frames per tile). */
+int  fcgpu_exchange_build(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_desc,
+                          const uint16_t *d_verdict, uint32_t n, uint32_t world, uint32_t rank,
+                          fcgpu_xmeta *d_meta, uint32_t *d_seg_n, uint64_t *d_seg_bytes, uint8_t *d_send,
+                          uint64_t send_cap, void *stream);
 
 const char *fcgpu_last_error(fcgpu_ctx *ctx);   /* ctx may be NULL (open errors) */
 

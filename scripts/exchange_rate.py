@@ -9,6 +9,9 @@ times, Mpps and the algorithmic HBM bytes per packet:
           offset 4 written = 40 B
   pack    record 16 + arena offset 4 + frame L read + slot (L+3)&~3 written
   unpack  record 16 read + descriptor 8 written = 24 B
+  build   (fcgpu_exchange_build, from the owner pass's verdicts) verdict 2 +
+          descriptor 8 read twice (per-tile sums, then records and frames),
+          record 16 written, frame L read + slot written
 
 python scripts/exchange_rate.py [--reps 50]
 """
@@ -72,6 +75,34 @@ def main():
                "gbs": {k: round(byt[k] / med[k] / 1e3, 1) for k in med},
                "bytes_per_packet": {k: round(byt[k] / m, 1) for k in byt}}
         print(json.dumps(out), flush=True)
+        # the one-pass send side from the verdicts (fcgpu_exchange_build)
+        vouts = DeviceOutputs(n, world, device="cuda:0", verdict=True, hash=False)
+        run_device(ctx, db, vouts)
+        cap = int(db.arena.numel()) + 4 * n
+        bmeta = torch.empty((n, 4), dtype=torch.int32, device="cuda:0")
+        bsn = torch.empty(world, dtype=torch.int32, device="cuda:0")
+        bsb = torch.empty(world, dtype=torch.int64, device="cuda:0")
+        bsend = torch.empty(cap, dtype=torch.uint8, device="cuda:0")
+        tb, tv = [], []
+        for r in range(a.reps + 3):
+            ev[0].record()
+            run_device(ctx, db, vouts)
+            ev[1].record()
+            ctx.exchange_build(db.arena.data_ptr(), db.desc.data_ptr(), vouts.verdict.data_ptr(), n, world, 0,
+                               bmeta.data_ptr(), bsn.data_ptr(), bsb.data_ptr(), bsend.data_ptr(), cap, stream=s)
+            ev[2].record()
+            torch.cuda.synchronize()
+            if r >= 3:
+                tv.append(ev[0].elapsed_time(ev[1]) * 1e3)
+                tb.append(ev[1].elapsed_time(ev[2]) * 1e3)
+        assert torch.equal(bsb.cpu(), seg.cpu()) and torch.equal(bmeta[:m].cpu(), meta[:m].cpu())
+        assert torch.equal(bsend[:total].cpu(), send[:total].cpu())
+        mb = statistics.median(tb)
+        byt = 10 * n + 10 * n + 16 * m + frame_bytes + total     # verdict+desc twice, records, frames in and out
+        print(json.dumps({"workload": name, "path": "build", "packets": n, "sent": m, "world": world,
+                          "us": {"owner_pass_verdicts": round(statistics.median(tv), 2), "build": round(mb, 2)},
+                          "build_gbs": round(byt / mb / 1e3, 1), "build_bytes_per_packet": round(byt / m, 1),
+                          "mpps_build": round(m / mb, 1)}), flush=True)
         ctx.close()
 
 

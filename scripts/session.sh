@@ -162,6 +162,11 @@ for s in "${ST[@]}"; do
     # round 5: the flow re-shard inside the bench (N = 1 on the GPU, the 8-rank command shape over gloo)
     reshard) step reshard1 300 python bench.py --flow-reshard --workload c4 --steps 50 --warmup 5 --no-cpu &&
              step reshard8 900 python bench.py --gpus 8 --backend gloo --flow-reshard --workload c4 --steps 5 --warmup 1 --no-cpu ;;
+    xbuild) step pytest_xbuild 600 python -u -m pytest tests/test_exchange.py tests/test_bench_dist.py tests/test_dist.py -m gpu -x -v --timeout 120 --timeout-method thread &&
+            step exchange_rate 300 python scripts/exchange_rate.py &&
+            step kt_exchange 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_kt_exchange -o run -- python3 scripts/exchange_rate.py --reps 20 ;;
+    xrate) step exchange_rate 300 python scripts/exchange_rate.py --reps 30 &&
+           step kt_exchange 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_kt_exchange -o run -- python3 scripts/exchange_rate.py --reps 20 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -165,7 +165,7 @@ def test_gpu_bench_flow_reshard(gpus):
     fr = line["config"]["flow_reshard"]
     assert fr["checked"] and fr["flow_table_flows"] == fr["distinct_5tuples"] == 65536 * gpus
     assert fr["packets_received"] == fr["packets_sent"] == 65536 * gpus * 3
-    assert set(fr["stage_ms_per_step"]) == {"owner_pass", "plan_pack", "exchange", "unpack", "flow_pass"}
+    assert set(fr["stage_ms_per_step"]) == {"owner_pass", "build", "exchange", "unpack", "flow_pass"}
 
 
 def test_flow_reshard_options():

@@ -95,7 +95,7 @@ def _owner_cfg(world):
     return N.make_cfg(offset=14, checksum=True, hash_mode=N.HASH_FLOWID, classify=N.CLS_LB_HASH, nports=world)
 
 
-def _flow_worker(rank, world, port, q):
+def _flow_worker(rank, world, port, q, built=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -111,8 +111,13 @@ def _flow_worker(rank, world, port, q):
         send = np.concatenate([X.pack(shard.arena, shard.desc, meta, ps, seg, world),
                                np.zeros(D.ARENA_PAD, np.uint8)])
         seg_n = [int(ps[d + 1]) - int(ps[d]) for d in range(world)]
-        buf, rmeta, displ = D.exchange_segments(torch.from_numpy(send), torch.from_numpy(meta.view(np.int32)),
-                                                seg_n, [int(x) for x in seg], group=None)
+        if built:    # the sizes as fcgpu_exchange_build leaves them: tensors, counts exchanged first
+            buf, rmeta, displ = D.exchange_built(torch.from_numpy(send), torch.from_numpy(meta.view(np.int32)),
+                                                 torch.tensor(seg_n, dtype=torch.int32),
+                                                 torch.tensor([int(x) for x in seg], dtype=torch.int64))
+        else:
+            buf, rmeta, displ = D.exchange_segments(torch.from_numpy(send), torch.from_numpy(meta.view(np.int32)),
+                                                    seg_n, [int(x) for x in seg], group=None)
         rmeta = rmeta.numpy().view(np.uint32)
         desc = X.unpack(rmeta, displ)
         src = rmeta[:, 2:4].copy().view(np.int64).ravel()
@@ -125,11 +130,14 @@ def _flow_worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_exchange_by_flow(oracle):
+@pytest.mark.parametrize("built", [False, True])
+def test_two_rank_exchange_by_flow(oracle, built):
     """Packets of one 6k-packet batch, split over 2 ranks, are re-sharded by
     the flow hash: the records and send buffers the HIP kernels build (their
 numpy restatement, oracle/exchange.py, stands in on the CPU) go through
-fastclick_amd.dist.exchange_segments (gloo all-to-all):
+fastclick_amd.dist.exchange_segments (gloo all-to-all) -- or, built, through
+dist.exchange_built, which takes the segment sizes as tensors the way
+fcgpu_exchange_build leaves them and exchanges the counts first:
     every valid packet lands exactly once, on the rank its flow hash names,
     with its frame bytes intact and in source order; each rank's flow table
     then sees whole flows (IDs from per-rank tables are in order of first
@@ -138,7 +146,7 @@ fastclick_amd.dist.exchange_segments (gloo all-to-all):
     port = 29500 + ((os.getpid() + 500) % 1000)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_flow_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_flow_worker, args=(r, world, port + built, q, built)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])

@@ -1,4 +1,5 @@
-"""Flow re-shard across GPUs (fcgpu_exchange_plan / _pack / _unpack,
+"""Flow re-shard across GPUs (fcgpu_exchange_plan / _pack / _unpack and the
+one-pass fcgpu_exchange_build,
 fastclick_amd/csrc/fcgpu_exchange.hh) against its numpy restatement
 (oracle/exchange.py): records, segment sizes and send buffers bit-exact
 (slot padding included), on ragged frames at unaligned offsets, empty
@@ -168,6 +169,132 @@ def test_gpu_exchange_1m_batch():
     assert np.array_equal(send[:int(eseg.sum())], X.pack(arena, b.desc, emeta, ps, eseg, world))
 
 
+def _build_gpu(ctx, arena, desc, owner, world, rank, send_cap=None):
+    """fcgpu_exchange_build from verdicts whose port is the owner (world = stays)."""
+    from fastclick_amd import device
+    port = np.where((owner >= 0) & (owner < world), owner, world).astype(np.uint16)
+    verdict = (port << 8) | np.where(port < world, N.R_OK, 1).astype(np.uint16)
+    if send_cap is None:
+        # these ragged frames overlap in their arena: the default bound (the
+        # arena's bytes + 4 per packet) assumes they do not
+        send_cap = int(((desc[:, 1].astype(np.int64) + 3) & ~3).sum()) if len(desc) else 0
+    send, meta, seg_n, seg_b = device.exchange_build(ctx, _dev(arena, np.uint8), _dev(desc, np.int32),
+                                                     _dev(verdict, np.int16), world, rank, send_cap=send_cap)
+    torch.cuda.synchronize()
+    sn = seg_n.cpu().numpy().astype(np.int64)
+    m = int(sn.sum())
+    return (send.cpu().numpy(), meta[:m].cpu().numpy().view(np.uint32).reshape(-1, 4), sn,
+            seg_b.cpu().numpy().astype(np.uint64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n,seed", [(1, 5000, 1), (3, 5000, 2), (8, 20000, 3), (64, 20000, 4),
+                                          (5, 1, 5), (2, 255, 6), (2, 257, 7), (7, 2049, 8), (16, 70000, 9)])
+def test_gpu_exchange_build_matches_oracle(world, n, seed):
+    """fcgpu_exchange_build (from verdicts, tile by tile) writes the records,
+    segment sizes and send buffer the restatement gives for the stable
+    partition of the same owners -- what plan + pack write -- on ragged frames
+    at unaligned offsets, tiles cut anywhere, 1 to 64 owners."""
+    arena, desc = _ragged(n, seed)
+    owner = np.random.default_rng(seed + 100).integers(-1, world, n)
+    perm, ps = X.partition(owner, world)
+    ctx = N.Context(0, max(n, 1))
+    try:
+        send, meta, seg_n, seg_b = _build_gpu(ctx, arena, desc, owner, world, rank=5)
+    finally:
+        ctx.close()
+    emeta, eseg = X.plan(desc, perm, ps, world, 5)
+    assert np.array_equal(seg_b, eseg)
+    assert seg_n.tolist() == [int(ps[d + 1] - ps[d]) for d in range(world)]
+    assert np.array_equal(meta, emeta)
+    total = int(eseg.sum())
+    assert np.array_equal(send[:total], X.pack(arena, desc, emeta, ps, eseg, world))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["empty", "all_invalid", "zero_lengths", "one_owner", "short_cap"])
+def test_gpu_exchange_build_edges(case):
+    """No packets, none leaving, zero-length frames, every packet to one owner
+    (one match-any group per wave), and a send buffer smaller than the
+    segments (nothing written past it)."""
+    world = 4
+    n = {"empty": 0}.get(case, 3000)
+    arena, desc = _ragged(n, 12)
+    owner = np.full(n, -1) if case == "all_invalid" else np.full(n, 2) if case == "one_owner" \
+        else np.arange(n) % world
+    if case == "zero_lengths":
+        desc[::2, 1] = 0
+    perm, ps = X.partition(owner, world)
+    emeta, eseg = X.plan(desc, perm, ps, world, 0)
+    cap = int(eseg.sum()) // 2 if case == "short_cap" else None
+    ctx = N.Context(0, max(n, 1))
+    try:
+        send, meta, seg_n, seg_b = _build_gpu(ctx, arena, desc, owner, world, 0, send_cap=cap)
+    finally:
+        ctx.close()
+    assert np.array_equal(seg_b, eseg) and np.array_equal(meta, emeta)
+    esend = X.pack(arena, desc, emeta, ps, eseg, world)
+    if case == "short_cap":
+        # every frame whose slot ends within the buffer is there; nothing past it
+        assert len(send) == cap + D.ARENA_PAD
+        dst = np.concatenate([[0], np.cumsum(eseg)])[:-1]
+        own = np.searchsorted(ps[:world + 1].astype(np.int64), np.arange(len(emeta)), side="right") - 1
+        end = dst[own] + emeta[:, 0].astype(np.int64) + ((emeta[:, 1].astype(np.int64) + 3) & ~3)
+        ok = end <= cap
+        for k in np.nonzero(ok)[0][:200]:
+            o = int(dst[own[k]] + emeta[k, 0])
+            assert np.array_equal(send[o:o + int(emeta[k, 1])], esend[o:o + int(emeta[k, 1])])
+    else:
+        assert np.array_equal(send[:int(eseg.sum())], esend)
+    if case in ("empty", "all_invalid"):
+        assert len(meta) == 0 and int(seg_b.sum()) == 0
+
+
+@pytest.mark.gpu
+def test_gpu_exchange_build_1m_and_owner_pass(oracle):
+    """1M C4 packets with errors: the owner pass (LB_MODE hash over 8 outputs,
+    verdicts only) then fcgpu_exchange_build, against the restatement run on
+    the oracle's owners; then each owner's segment as its receiver gets it
+    from this one source, unpacked on the device: the descriptors point at
+    every packet's bytes."""
+    from fastclick_amd import device
+    from fastclick_amd.device import DeviceBatch, DeviceOutputs
+    world, n = 8, 1 << 20
+    b = synth.c4(n, seed=33)
+    synth.inject_errors(b, 0.01, seed=34)
+    cfg = N.make_cfg(offset=14, checksum=True, hash_mode=N.HASH_FLOWID, classify=N.CLS_LB_HASH, nports=world)
+    exp = oracle.process_batch(cfg, b)
+    owner = np.where(exp["reason"] == N.R_OK, exp["port"].astype(np.int64), -1)
+    perm, ps = X.partition(owner, world)
+    emeta, eseg = X.plan(b.desc, perm, ps, world, 0)
+    ctx = N.Context(0, n, cfg)
+    try:
+        db = DeviceBatch.upload(b, device="cuda:0")
+        outs = DeviceOutputs(n, world, device="cuda:0", verdict=True, hash=False)
+        device.run_device(ctx, db, outs)
+        send, meta, seg_n, seg_b = device.exchange_build(ctx, db.arena, db.desc, outs.verdict, world, 0)
+        torch.cuda.synchronize()
+        assert np.array_equal(seg_b.cpu().numpy().astype(np.uint64), eseg)
+        sn = seg_n.cpu().numpy().astype(np.int64)
+        assert sn.tolist() == [int(ps[d + 1] - ps[d]) for d in range(world)]
+        m = int(sn.sum())
+        assert np.array_equal(meta[:m].cpu().numpy().view(np.uint32), emeta)
+        total = int(eseg.sum())
+        hs = send.cpu().numpy()
+        assert np.array_equal(hs[:total], X.pack(b.arena, b.desc, emeta, ps, eseg, world))
+        sb = np.concatenate([[0], np.cumsum(eseg)]).astype(np.int64)
+        for d in (0, 5):
+            seg = hs[sb[d]:sb[d + 1]]
+            rmeta = meta[int(ps[d]):int(ps[d + 1])]
+            rd = device.exchange_unpack(ctx, rmeta, [0]).cpu().numpy().view(np.uint32)
+            assert np.array_equal(rd, X.unpack(emeta[ps[d]:ps[d + 1]], [0]))
+            for k in range(0, len(rd), 997):
+                o, ln = (int(x) for x in rd[k])
+                assert bytes(seg[o:o + ln]) == b.frame(int(emeta[ps[d] + k, 2]))
+    finally:
+        ctx.close()
+
+
 def test_exchange_rejects_bad_arguments():
     """Argument checks need no device: a null context, world 0 or > 64."""
     lib = N.load()
@@ -175,3 +302,4 @@ def test_exchange_rejects_bad_arguments():
     assert lib.fcgpu_exchange_pack(None, None, None, None, None, 0, 1, None, 0, None) == N.EINVAL
     arr = (N.C.c_uint64 * 1)()
     assert lib.fcgpu_exchange_unpack(None, None, 0, arr, 1, None, None) == N.EINVAL
+    assert lib.fcgpu_exchange_build(None, None, None, None, 0, 1, 0, None, None, None, None, 0, None) == N.EINVAL
