@@ -675,7 +675,7 @@ class ReshardProcessor:
                              nports=self.world)
         self.ctx_own = N.Context(gpu, max(n, 1), own_cfg)
         self.own_out = DeviceOutputs(max(n, 1), self.world, device=dev, verdict=True, hash=False)
-        self.send_cap = stride + 4 * max(n, 1)      # every frame's slot (the arena's bytes + 4 per packet)
+        self.send_cap = stride + 16 * max(n, 1)     # every frame's 16-B slot (the arena's bytes + 16 per packet)
         # a rank receives ~n packets (uniform owners); the flow pass takes them
         # in batches of at most cap (the flow table's largest batch,
         # FCGPU_FLOW_MAX_BATCH), in order, so any count fits

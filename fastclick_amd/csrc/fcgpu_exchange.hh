@@ -46,7 +46,14 @@ constexpr uint32_t kXItems = kXThreads * kXPer;   // packets per plan block
 typedef uint32_t xu4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t xu2 __attribute__((ext_vector_type(2), aligned(4)));
 
-__device__ __forceinline__ uint64_t xslot(uint32_t len) { return ((uint64_t)len + 3u) & ~(uint64_t)3u; }
+// A frame's slot in the send buffer: its length rounded up to 16 B, so every
+// slot starts 16-B aligned and is written in whole aligned 16-B stores
+// (4-B slots, round 4's format, left a segment's lines to be written by two
+// frames' lanes with misaligned stores: k_xbuild 42.8 -> see DESIGN section 6).
+constexpr uint32_t kXSlotAlign = 16;
+__device__ __forceinline__ uint64_t xslot(uint32_t len) {
+    return ((uint64_t)len + (kXSlotAlign - 1)) & ~(uint64_t)(kXSlotAlign - 1);
+}
 
 struct XPlan {
     const uint32_t *desc;
@@ -253,46 +260,56 @@ __global__ __launch_bounds__(kXThreads) void k_xmeta(XPlan P) {
     }
 }
 
-// One frame into its 4-B aligned slot of (len + 3) & ~3 bytes at dstp, lpf
-// lanes (this one is q): 16 B per lane per step, four aligned dwords of the
-// source and the next one funnel-shifted (v_alignbyte) into four dwords of the
-// slot (frames start anywhere in the arena; the ABI's 16 B of readable slack
-// past a frame's end covers the fifth load). Slot bytes past the frame are
-// zero; nothing is stored past the slot. (Stores aligned to the destination
-// instead, the source loads then misaligned, measured slower: k_xpack 38.9 ->
-// 46.3 us for 1M 60-B frames, profiles/r05_exchange/README.md.)
+// One frame into its 16-B aligned slot (xslot) at dstp, lpf lanes (this one
+// is q): 16 B per lane per step, four aligned dwords of the source and the
+// next one funnel-shifted (v_alignbyte) into one aligned 16-B store (frames
+// start anywhere in the arena; the ABI's 16 B of readable slack past a
+// frame's end covers the fifth load). Slot bytes past the frame are zero;
+// nothing is stored past the slot.
 __device__ __forceinline__ void xcopy_frame(const uint8_t *src, uint32_t len, uint8_t *dstp, uint32_t q,
                                             uint32_t lpf) {
     const uintptr_t sa = reinterpret_cast<uintptr_t>(src);
     const uint32_t sh = (uint32_t)(sa & 3u);
     const uint32_t *al = reinterpret_cast<const uint32_t *>(sa & ~(uintptr_t)3);
     uint32_t *out = reinterpret_cast<uint32_t *>(dstp);
-    for (uint32_t w = 16 * q; w < len; w += 16 * lpf) {
-        const xu4 a = *reinterpret_cast<const xu4 *>(al + (w >> 2));
-        // the fifth dword only when the frame reaches into it (so no read
-        // goes further than 16 B past the frame's end)
-        const uint32_t e = sh && w + 16 - sh < len ? al[(w >> 2) + 4] : 0u;
-        uint32_t v0 = __builtin_amdgcn_alignbyte(a.y, a.x, sh);
-        uint32_t v1 = __builtin_amdgcn_alignbyte(a.z, a.y, sh);
-        uint32_t v2 = __builtin_amdgcn_alignbyte(a.w, a.z, sh);
-        uint32_t v3 = __builtin_amdgcn_alignbyte(e, a.w, sh);
-        const uint32_t rem = len - w;
-        if (rem >= 16) {
-            xu4 o;
-            o.x = v0, o.y = v1, o.z = v2, o.w = v3;
-            *reinterpret_cast<xu4 *>(out + (w >> 2)) = o;
-        } else {
-            // the slot's last dwords: bytes past the frame zero, nothing past the slot
-            auto cut = [rem](uint32_t v, uint32_t k) -> uint32_t {
-                if (rem <= 4 * k) return 0u;
-                const uint32_t keep = rem - 4 * k;
-                return keep >= 4 ? v : v & ((1u << (8 * keep)) - 1u);
-            };
-            const uint32_t nd = (rem + 3) >> 2;
-            out[(w >> 2)] = cut(v0, 0);
-            if (nd > 1) out[(w >> 2) + 1] = cut(v1, 1);
-            if (nd > 2) out[(w >> 2) + 2] = cut(v2, 2);
-            if (nd > 3) out[(w >> 2) + 3] = cut(v3, 3);
+    // four of the lane's chunks per round, their loads issued before any
+    // store (a long frame's chunks then wait for memory together)
+    constexpr uint32_t kU = 4;
+    for (uint32_t w0 = 16 * q; w0 < len; w0 += 16 * lpf * kU) {
+        xu4 a[kU];
+        uint32_t e[kU];
+#pragma unroll
+        for (uint32_t k = 0; k < kU; ++k) {
+            const uint32_t w = w0 + 16 * lpf * k;
+            a[k] = xu4{0u, 0u, 0u, 0u};
+            e[k] = 0u;
+            if (w < len) {
+                a[k] = *reinterpret_cast<const xu4 *>(al + (w >> 2));
+                // the fifth dword only when the frame reaches into it (so no
+                // read goes further than 16 B past the frame's end)
+                if (sh && w + 16 - sh < len) e[k] = al[(w >> 2) + 4];
+            }
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kU; ++k) {
+            const uint32_t w = w0 + 16 * lpf * k;
+            if (w >= len) break;
+            uint32_t v0 = __builtin_amdgcn_alignbyte(a[k].y, a[k].x, sh);
+            uint32_t v1 = __builtin_amdgcn_alignbyte(a[k].z, a[k].y, sh);
+            uint32_t v2 = __builtin_amdgcn_alignbyte(a[k].w, a[k].z, sh);
+            uint32_t v3 = __builtin_amdgcn_alignbyte(e[k], a[k].w, sh);
+            const uint32_t rem = len - w;
+            if (rem < 16) {
+                // the slot's last 16 B: bytes past the frame zero
+                auto cut = [rem](uint32_t v, uint32_t j) -> uint32_t {
+                    if (rem <= 4 * j) return 0u;
+                    const uint32_t keep = rem - 4 * j;
+                    return keep >= 4 ? v : v & ((1u << (8 * keep)) - 1u);
+                };
+                v0 = cut(v0, 0), v1 = cut(v1, 1), v2 = cut(v2, 2), v3 = cut(v3, 3);
+            }
+            // the slot is 16-B aligned (xslot): one aligned 16-B store
+            *reinterpret_cast<uint4 *>(out + (w >> 2)) = make_uint4(v0, v1, v2, v3);
         }
     }
 }

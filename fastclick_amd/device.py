@@ -183,7 +183,7 @@ def exchange_build(ctx: N.Context, arena, desc, verdict, world, rank, send_cap=N
     buffer (send_cap bytes + ARENA_PAD), the int32 [n, 4] record buffer (its
     first sum(seg_n) rows are the records, in owner order), per owner its
     packet count (int32) and byte count (int64). No host sync: send_cap
-    defaults to the arena's bytes + 4 per packet, which holds every leaving
+    defaults to the arena's bytes + 16 per packet, which holds every leaving
     frame's slot unless descriptors alias; the caller reads seg_bytes (one
     sync it needs anyway for the all-to-all) and dist.exchange_segments
     checks the total against the buffer."""
@@ -193,7 +193,7 @@ def exchange_build(ctx: N.Context, arena, desc, verdict, world, rank, send_cap=N
     dev = desc.device
     s = stream if stream is not None else torch.cuda.current_stream()
     if send_cap is None:
-        send_cap = int(arena.numel()) + 4 * n
+        send_cap = int(arena.numel()) + 16 * n
     meta = torch.empty((max(n, 1), 4), dtype=torch.int32, device=dev)
     seg_n = torch.empty(world, dtype=torch.int32, device=dev)
     seg_b = torch.empty(world, dtype=torch.int64, device=dev)

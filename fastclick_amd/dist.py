@@ -182,7 +182,7 @@ def exchange_by_flow(ctx, arena, desc, perm, port_start, group=None):
     the whole-batch partition of the device pass that named every packet's
     owner (LB_MODE hash over `world` outputs; the invalid list, output
     `world`, stays here). Returns (arena_recv, desc_recv, src): the frames this
-    rank now owns, in (source rank, source index) order, each at a 4-B aligned
+    rank now owns, in (source rank, source index) order, each at a 16-B aligned
     offset with its bytes and length exact, the buffer followed by ARENA_PAD
     zero bytes; their descriptors; src = source_rank << 32 | source_index.
     Pack and unpack are HIP kernels (fcgpu_exchange_*); there is no CPU path."""

@@ -647,8 +647,10 @@ int  fcgpu_read_timing(fcgpu_ctx *ctx, double *ms, uint32_t *launches, int nstag
  *   fcgpu_exchange_plan   perm[0 .. port_start[world]) -- the packets that
  *       leave (output `world`, the invalid list, stays) -- gets one
  *       fcgpu_xmeta record each, in perm order; d_seg_bytes[d] = the bytes of
- *       owner d's segment of the send buffer. Each frame takes a 4-B aligned
- *       slot of (length + 3) & ~3 bytes. Segments follow in owner order.
+ *       owner d's segment of the send buffer. Each frame takes a 16-B aligned
+ *       slot of (length + 15) & ~15 bytes (ABI 22; 4-B slots before), so every
+ *       slot is written in whole aligned 16-B stores. Segments follow in owner
+ *       order.
  *   fcgpu_exchange_pack   the frames into d_send (at least the sum of
  *       d_seg_bytes; nothing is written past send_cap; an owner whose
  *       d_seg_bytes exceeds 0xffffffff -- its records' 32-bit offsets cannot
@@ -695,7 +697,7 @@ int  fcgpu_exchange_unpack(fcgpu_ctx *ctx, const fcgpu_xmeta *d_meta, uint32_t n
  * padding zero), plus d_seg_n[d], the packets of owner d. send_cap bounds the
  * send buffer as for fcgpu_exchange_pack (the sum of the leaving frames'
  * slots fits in send_cap whenever it is at least the arena's frame bytes +
- * 3 per packet), so no host sync is needed before the call. Every per-packet
+ * 15 per packet), so no host sync is needed before the call. Every per-packet
  * load is in input order (three launches: per-tile owner counts and bytes,
  * their scan per owner, the records and frames per tile). */
 int  fcgpu_exchange_build(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_desc,

@@ -31,8 +31,11 @@ def partition(owner, world):
     return perm, port_start
 
 
+SLOT_ALIGN = 16     # every frame's slot: its length rounded up to 16 B (fcgpu_exchange.hh xslot)
+
+
 def _slot(ln):
-    return (ln.astype(np.uint64) + 3) & ~np.uint64(3)
+    return (ln.astype(np.uint64) + (SLOT_ALIGN - 1)) & ~np.uint64(SLOT_ALIGN - 1)
 
 
 def _owner_of(ps, m):
@@ -63,7 +66,7 @@ def plan(desc, perm, port_start, world, rank):
 
 def pack(arena, desc, meta, port_start, seg_bytes, world):
     """The send buffer: owner d's segment at sum(seg_bytes[:d]), each frame in
-    its 4-B slot, slot bytes past the frame zero."""
+    its 16-B slot, slot bytes past the frame zero."""
     arena = np.asarray(arena, dtype=np.uint8)
     desc = np.asarray(desc, dtype=np.uint32).reshape(-1, 2)
     m = len(meta)

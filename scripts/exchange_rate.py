@@ -78,7 +78,7 @@ def main():
         # the one-pass send side from the verdicts (fcgpu_exchange_build)
         vouts = DeviceOutputs(n, world, device="cuda:0", verdict=True, hash=False)
         run_device(ctx, db, vouts)
-        cap = int(db.arena.numel()) + 4 * n
+        cap = int(db.arena.numel()) + 16 * n
         bmeta = torch.empty((n, 4), dtype=torch.int32, device="cuda:0")
         bsn = torch.empty(world, dtype=torch.int32, device="cuda:0")
         bsb = torch.empty(world, dtype=torch.int64, device="cuda:0")

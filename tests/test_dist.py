@@ -205,7 +205,7 @@ def test_gpu_exchange_pack_and_flow_table(oracle):
     assert np.all(rb.arena[-D.ARENA_PAD:] == 0)
     for k in range(len(g)):
         o, n_ = int(rb.desc[k, 0]), int(rb.desc[k, 1])
-        assert o % 4 == 0 and bytes(rb.arena[o:o + n_]) == b.frame(int(g[k]))
+        assert o % 16 == 0 and bytes(rb.arena[o:o + n_]) == b.frame(int(g[k]))
     fcfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=4)
     res = device.process_batches([rb], fcfg, max_flows=1 << 16, anno=False, perm=False)
     ids = oracle.FlowTable(1 << 16).batch(rb, oracle.process_batch(fcfg, rb))
@@ -216,7 +216,7 @@ def test_exchange_format_round_trip():
     """The re-shard format (oracle/exchange.py, the HIP kernels' checker):
     three ranks' ragged frames at unaligned offsets, packed by owner, moved by
     a simulated all-to-all and unpacked, land on their owners exactly once
-    with their bytes, in (source rank, source index) order, 4-B aligned, the
+    with their bytes, in (source rank, source index) order, 16-B aligned, the
     slot padding zero."""
     from oracle import exchange as X
     rng = np.random.default_rng(5)
@@ -233,7 +233,7 @@ def test_exchange_format_round_trip():
         meta, seg = X.plan(desc, perm, ps, world, rank)
         assert np.all(np.diff(meta[:, 2].astype(np.int64)[ps[0]:ps[1]]) > 0)
         send = X.pack(arena, desc, meta, ps, seg, world)
-        assert len(send) == int(sum(seg)) and len(send) == int(((ln[owner >= 0].astype(np.int64) + 3) // 4 * 4).sum())
+        assert len(send) == int(sum(seg)) and len(send) == int(((ln[owner >= 0].astype(np.int64) + 15) // 16 * 16).sum())
         parts.append((send, meta, ps, seg))
         srcs.append((desc, owner))
     for r, (buf, meta, displ) in enumerate(X.all_to_all(parts, world)):
@@ -242,7 +242,7 @@ def test_exchange_format_round_trip():
         assert [(int(a), int(b)) for a, b in zip(meta[:, 3], meta[:, 2])] == want
         for (o, n_), (s, i) in zip(d.tolist(), want):
             so, sn = srcs[s][0][i].tolist()
-            assert n_ == sn and o % 4 == 0
+            assert n_ == sn and o % 16 == 0
             assert np.array_equal(buf[o:o + n_], arena[so:so + sn])
             assert np.all(buf[o + n_:o + ((n_ + 3) & ~3)] == 0)
 

@@ -177,7 +177,7 @@ def _build_gpu(ctx, arena, desc, owner, world, rank, send_cap=None):
     if send_cap is None:
         # these ragged frames overlap in their arena: the default bound (the
         # arena's bytes + 4 per packet) assumes they do not
-        send_cap = int(((desc[:, 1].astype(np.int64) + 3) & ~3).sum()) if len(desc) else 0
+        send_cap = int(((desc[:, 1].astype(np.int64) + 15) & ~15).sum()) if len(desc) else 0
     send, meta, seg_n, seg_b = device.exchange_build(ctx, _dev(arena, np.uint8), _dev(desc, np.int32),
                                                      _dev(verdict, np.int16), world, rank, send_cap=send_cap)
     torch.cuda.synchronize()
@@ -239,7 +239,7 @@ def test_gpu_exchange_build_edges(case):
         assert len(send) == cap + D.ARENA_PAD
         dst = np.concatenate([[0], np.cumsum(eseg)])[:-1]
         own = np.searchsorted(ps[:world + 1].astype(np.int64), np.arange(len(emeta)), side="right") - 1
-        end = dst[own] + emeta[:, 0].astype(np.int64) + ((emeta[:, 1].astype(np.int64) + 3) & ~3)
+        end = dst[own] + emeta[:, 0].astype(np.int64) + ((emeta[:, 1].astype(np.int64) + 15) & ~15)
         ok = end <= cap
         for k in np.nonzero(ok)[0][:200]:
             o = int(dst[own[k]] + emeta[k, 0])
