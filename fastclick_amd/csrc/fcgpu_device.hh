@@ -620,59 +620,14 @@ __device__ __forceinline__ uint32_t win32(const FrameView &f, uint32_t b) {
     return __builtin_amdgcn_alignbyte(hi, lo, x & 3u);
 }
 
-// Straight-line CheckIP6Header -> IP6FlowID hash -> classify for an IPv6
-// header at o whose 40 bytes + first L4 word lie in the window (no PROCESS_EH:
-// the caller declines that). Same outputs as check_ip6 + process_packet's v6
-// branch (checkip6header.cc:105-150, ip6flowid.hh:220-230).
-template <bool PROG>
-__device__ __forceinline__ bool ip6_fast(const DevCfg &c, const FrameView &f, uint32_t len, uint32_t o, PktResult &r,
-                                         const uint4 *sprog) {
-    const uint32_t x = f.shift + o, a = x & ~3u, sh = x & 3u;
-    if (a + 48 > (uint32_t)kWin) return false;
-    uint32_t w[12];
-#pragma unroll
-    for (int j = 0; j < 12; ++j)
-        w[j] = *reinterpret_cast<const uint32_t *>(f.row + (((((a + 4 * j) >> 4) ^ f.sw) << 4) | ((a + 4 * j) & 15)));
-    uint32_t h[11];
-#pragma unroll
-    for (int j = 0; j < 11; ++j) h[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
-    if (c.classify != FCGPU_CLS_LB_HASH && (!PROG || c.classify != FCGPU_CLS_PROGRAM)) return false;
-    const uint32_t plen = len - o, pl6 = bswap16(h[1] & 0xffff);
-    bool bad = (int)plen < 40 || ((h[0] & 0xff) >> 4) != 6 || pl6 > plen - 40;
-    for (uint32_t j = 0; j < c.nbad6; ++j)   // wave-uniform
-        bad |= h[2] == c.bad6[j][0] && h[3] == c.bad6[j][1] && h[4] == c.bad6[j][2] && h[5] == c.bad6[j][3];
-    fcgpu_anno &an = r.an;
-    an.ipver = 6;
-    uint32_t hv = 0;
-    if (c.hash_mode != FCGPU_HASH_NONE) {
-        const uint32_t s = bswap16(h[10] & 0xffff), d = bswap16(h[10] >> 16);
-        const uint32_t sa = (h[4] << 1) + h[5], da = (h[8] << 1) + h[9];
-        hv = rotl32(sa, s & 15) ^ rotl32(da, 31 - (d & 15)) ^ ((d << 16) | s);
-    }
-    r.reason = bad ? FCGPU_R_BAD_IP6 : FCGPU_R_OK;
-    r.hash = bad ? 0u : hv;
-    an.th = (uint16_t)(bad ? 0u : o + 40);
-    an.ip6_nxt = (uint8_t)(bad ? 0u : (h[1] >> 16) & 0xff);
-    an.length = (uint16_t)(bad ? 0u : (pl6 < plen - 40 ? len - (plen - 40 - pl6) : len));
-    uint32_t port = c.nports;
-    if (!bad) {
-        an.nh = (uint16_t)o;
-        if (c.classify == FCGPU_CLS_LB_HASH) {
-            port = (uint32_t)lb_port(hv, c.nports, c.lb_magic);
-        } else if (PROG) {
-            const uint32_t out = run_program(c, f, an, sprog);
-            if (out >= c.nports) r.reason = FCGPU_R_NO_MATCH;
-            else port = out;
-        }
-    }
-    r.port = port;
-    return true;
-}
-
 // StripEtherVLANHeader / VLANDecap at OFFSET, then the version dispatch of
 // CHECK_AUTO, straight-line for frames whose headers sit in the window;
 // rejected untagged frames (NATIVE_VLAN < 0) and PROCESS_EH take the general
-// path.
+// path. IPv4 and IPv6 lanes share one wave, so both checks run branch-free on
+// one read of the window (12 dwords from the IP header) and each lane keeps
+// its version's result: CheckIPHeader as ip4_fast, CheckIP6Header
+// (checkip6header.cc:105-150) and IP6FlowID::hashcode (ip6flowid.hh:220-230)
+// for the IPv6 header and first L4 word; same outputs as process_packet.
 template <bool CK, bool PROG>
 __device__ __forceinline__ bool auto_fast(const DevCfg &c, const FrameView &f, uint32_t len, PktResult &r,
                                           const uint4 *sprog) {
@@ -683,13 +638,97 @@ __device__ __forceinline__ bool auto_fast(const DevCfg &c, const FrameView &f, u
     const bool tagged = (e & 0xffff) == c.vlan_tpid;
     if (!tagged && c.native_vlan < 0) return false;
     const uint32_t x = o + (tagged ? 18u : 14u);
-    const bool v6 = ((int)(len - x) >= 1) && ((win32(f, x) & 0xf0) == 0x60);
-    const bool done = v6 ? ip6_fast<PROG>(c, f, len, x, r, sprog) : ip4_fast<CK, PROG>(c, f, len, x, r, sprog);
-    if (done) {
-        r.an.vlan_tci = tagged ? (uint16_t)(e >> 16) : (uint16_t)bswap16((uint32_t)c.native_vlan);
-        r.an.nh = (uint16_t)x;                               // the pull() the strip did
+    const uint32_t xa = f.shift + x, a = xa & ~3u, sh = xa & 3u;
+    // dwords past the row wrap into it (their lanes decline below)
+    const uint32_t sw4 = f.sw << 4;
+    uint32_t w[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j)
+        w[j] = *reinterpret_cast<const uint32_t *>(f.row + (((a + 4 * j) & (uint32_t)(kWin - 1)) ^ sw4));
+    uint32_t h[11];
+#pragma unroll
+    for (int j = 0; j < 11; ++j) h[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+    const uint32_t plen = len - x;
+    const bool v6 = (int)plen >= 1 && (h[0] & 0xf0) == 0x60;
+    // classifiers the straight line covers (wave-uniform)
+    const bool prog = PROG && c.classify == FCGPU_CLS_PROGRAM;
+    const bool cls4 = c.classify == FCGPU_CLS_LB_HASH || c.classify == FCGPU_CLS_LB_CRC ||
+                      c.classify == FCGPU_CLS_NONE || prog;
+    const bool cls6 = c.classify == FCGPU_CLS_LB_HASH || prog;
+    // CheckIPHeader::valid's reason chain as predicates (ip4_fast)
+    const uint32_t b0 = h[0] & 0xff, hlen = (b0 & 15) << 2, L = bswap16(h[0] >> 16);
+    const bool tiny = (int)plen < 20, badv = (b0 >> 4) != 4, badhl = hlen < 20;
+    const bool badlen = L > plen || L < hlen;
+    bool ckbad = false;
+    if (CK) {
+        uint64_t sum = (uint64_t)h[0] + h[1] + h[2] + h[3] + h[4];
+        uint32_t t = (uint32_t)sum + (uint32_t)(sum >> 32);
+        t = (t < (uint32_t)sum) ? t + 1 : t;
+        t = (t & 0xffff) + (t >> 16);
+        t = (t & 0xffff) + (t >> 16);
+        ckbad = t != 0xffff;
     }
-    return done;
+    bool srcbad = false;
+    if (c.nbadsrc) {   // wave-uniform
+        bool bad = false, good = false;
+        for (uint32_t j = 0; j < c.nbadsrc; ++j) bad |= (c.badsrc[j] == h[3]);
+        for (uint32_t j = 0; j < c.ngooddst; ++j) good |= (c.gooddst[j] == h[4]);
+        srcbad = bad && !good;
+    }
+    const uint32_t early = tiny ? FCGPU_R_MINISCULE : badv ? FCGPU_R_BAD_VERSION
+                         : badhl ? FCGPU_R_BAD_HLEN : badlen ? FCGPU_R_BAD_IP_LEN : FCGPU_R_OK;
+    // CheckIP6Header: length, payload length, bad source addresses
+    const uint32_t pl6 = bswap16(h[1] & 0xffff);
+    bool bad6 = (int)plen < 40 || pl6 > plen - 40;
+    for (uint32_t j = 0; j < c.nbad6; ++j)   // wave-uniform
+        bad6 |= h[2] == c.bad6[j][0] && h[3] == c.bad6[j][1] && h[4] == c.bad6[j][2] && h[5] == c.bad6[j][3];
+    // decline: header (+ first L4 word) not in the window, IP options, or a
+    // classifier of the general path
+    const bool take = v6 ? (a + 48 <= (uint32_t)kWin && cls6)
+                         : (a + 28 <= (uint32_t)kWin && !(early == FCGPU_R_OK && hlen != 20) && cls4);
+    if (!take) return false;
+    const uint32_t reason = v6 ? (bad6 ? FCGPU_R_BAD_IP6 : FCGPU_R_OK)
+                          : early != FCGPU_R_OK ? early
+                          : ckbad ? FCGPU_R_BAD_CKSUM : srcbad ? FCGPU_R_BAD_SADDR : FCGPU_R_OK;
+    const bool ok = reason == FCGPU_R_OK;
+    uint32_t hv = 0;
+    if (c.hash_mode != FCGPU_HASH_NONE) {   // wave-uniform
+        const uint32_t pw = v6 ? h[10] : h[5];              // sport, dport
+        const uint32_t sp = bswap16(pw & 0xffff), dp = bswap16(pw >> 16);
+        // IPFlowID: non-first fragments hash as the zero flow; IP6Address::hashcode
+        const bool first = (bswap16(h[1] >> 16) & 0x1fff) == 0;
+        const uint32_t sa = v6 ? (h[4] << 1) + h[5] : h[3], da = v6 ? (h[8] << 1) + h[9] : h[4];
+        const uint32_t rs = v6 ? (sp & 15) : (sp & 15) + 1;
+        hv = rotl32(sa, rs) ^ rotl32(da, 31 - (dp & 15)) ^ ((dp << 16) | sp);
+        hv = v6 || first ? hv : 0u;
+        if (c.hash_mode == FCGPU_HASH_FLOW5ID && !v6) hv ^= (h[2] >> 8) & 0xff;
+    }
+    uint32_t port = 0;
+    if (c.classify == FCGPU_CLS_LB_HASH) {
+        port = (uint32_t)lb_port(hv, c.nports, c.lb_magic);
+    } else if (c.classify == FCGPU_CLS_LB_CRC) {   // IPv4 lanes only (cls6)
+        const bool first = (bswap16(h[1] >> 16) & 0x1fff) == 0;
+        const uint32_t crc = flow5_crc(sprog, (h[2] >> 8) & 0xff, first ? h[3] : 0u, first ? h[4] : 0u,
+                                       first ? h[5] : 0u);
+        port = (uint32_t)lb_port(crc, c.nports, c.lb_magic);
+    }
+    r.reason = reason;
+    r.hash = ok ? hv : 0u;
+    fcgpu_anno &an = r.an;
+    an.ipver = v6 ? 6 : early == FCGPU_R_MINISCULE ? 0 : 4;
+    an.nh = (uint16_t)x;                                     // the pull() the strip did
+    an.th = (uint16_t)(ok ? x + (v6 ? 40u : 20u) : 0u);
+    const uint32_t cut = v6 ? (pl6 < plen - 40 ? plen - 40 - pl6 : 0u) : (plen > L ? plen - L : 0u);
+    an.length = (uint16_t)(ok ? len - cut : 0u);
+    an.dst_ip = ok && !v6 ? h[4] : 0u;
+    an.ip6_nxt = (uint8_t)(ok && v6 ? (h[1] >> 16) & 0xff : 0u);
+    an.vlan_tci = tagged ? (uint16_t)(e >> 16) : (uint16_t)bswap16((uint32_t)c.native_vlan);
+    if (prog && ok) {
+        port = run_program(c, f, an, sprog);
+        if (port >= c.nports) r.reason = FCGPU_R_NO_MATCH;
+    }
+    r.port = ok && port < c.nports ? port : c.nports;
+    return true;
 }
 
 // ---- CheckUDPHeader / CheckTCPHeader ----------------------

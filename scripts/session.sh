@@ -167,6 +167,14 @@ for s in "${ST[@]}"; do
             step kt_exchange 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_kt_exchange -o run -- python3 scripts/exchange_rate.py --reps 20 ;;
     xrate) step exchange_rate 300 python scripts/exchange_rate.py --reps 30 &&
            step kt_exchange 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_kt_exchange -o run -- python3 scripts/exchange_rate.py --reps 20 ;;
+    # A/B of the library in fastclick_amd/lib/ab/libfcgpu_old.so against the tree's, interleaved
+    autoab) for k in 1 2; do
+              for w in "--workload c5" "--workload c5 --layout split" "--workload c2"; do
+                n=$(echo "$w" | tr -d ' -' | cut -c1-40)
+                FCGPU_LIB=fastclick_amd/lib/ab/libfcgpu_old.so step "ab_old_${n}_$k" 300 python bench.py --steps 200 --warmup 20 --no-cpu $w &&
+                step "ab_new_${n}_$k" 300 python bench.py --steps 200 --warmup 20 --no-cpu $w || exit $?
+              done
+            done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
