@@ -117,9 +117,10 @@ def parse(argv=None):
                          "run is timed outside the timed region: flow_maintain_ms)")
     ap.add_argument("--flow-timeout", type=int, default=0, help="imp: TIMEOUT in s (0: none)")
     ap.add_argument("--flow-recycle-ms", type=int, default=1000, help="imp: RECYCLE_INTERVAL in ms")
-    ap.add_argument("--classify", choices=["lb", "lbcrc", "ipclass16"], default="lb",
+    ap.add_argument("--classify", choices=["lb", "lbcrc", "lbtable", "ipclass16"], default="lb",
                     help="lb: FlowSwitch LB_MODE hash x16 (headline); lbcrc: LB_MODE hash_crc x16 "
-                         "(CRC32-C of the IPFlow5ID, DPDK builds); ipclass16: the survey's "
+                         "(CRC32-C of the IPFlow5ID, DPDK builds); lbtable: LB_MODE cst_hash_agg x16 "
+                         "(the 1600-bucket consistent-hash ring); ipclass16: the survey's "
                          "IPClassifier with 15 UDP dst-port ranges + '-' (program printed by the "
                          "reference compiler, tests/golden/reftests.json)")
     ap.add_argument("--l4", choices=["none", "udp", "tcp"], default="none",
@@ -498,7 +499,8 @@ class DeviceProcessor:
             args.nports = 16
         self.auto = args.workload == "c5"
         classify = (N.CLS_PROGRAM if program is not None else
-                    N.CLS_LB_CRC if args.classify == "lbcrc" else N.CLS_LB_HASH)
+                    N.CLS_LB_CRC if args.classify == "lbcrc" else
+                    N.CLS_LB_TABLE if args.classify == "lbtable" else N.CLS_LB_HASH)
         cfg = N.make_cfg(check_mode=N.CHECK_AUTO if self.auto else N.CHECK_IP4, offset=0 if self.auto else 14,
                          checksum=True, hash_mode=N.HASH_FLOWID, classify=classify, nports=args.nports,
                          badsrc=[N.raw_addr(a) for a in ERROR_BADSRC] if args.errors else (),
@@ -511,6 +513,8 @@ class DeviceProcessor:
             self.ctx.set_program(*program)
             if args.program_jit:
                 self.ctx.program_jit(True)
+        if classify == N.CLS_LB_TABLE:
+            self.ctx.set_lb_table(N.lb_hash_ring(args.nports))
         self.maintain_ms = None
         if args.flow_capacity:
             if args.flow_manager == "imp":
@@ -959,7 +963,8 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                             if args.flow_capacity else "")
                          + " + AggregateHash + "
                          + ({"lb": "FlowSwitch hash 16 outputs",
-                             "lbcrc": "FlowSwitch LB_MODE hash_crc 16 outputs"}.get(
+                             "lbcrc": "FlowSwitch LB_MODE hash_crc 16 outputs",
+                             "lbtable": "FlowSwitch LB_MODE cst_hash_agg 16 outputs (1600-bucket ring)"}.get(
                                 args.classify, "IPClassifier(15 UDP dst-port ranges, -) 16 outputs"))
                          + ("" if args.no_perm else
                             " + stable per-port partition of every 256-packet PacketBatch"

@@ -15,7 +15,7 @@ LIBFCGPU = os.environ.get("FCGPU_LIB") or os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 22
+ABI_VERSION = 23
 SPAN_SLOTS = 3
 SPAN_COPY = 0
 SPAN_ZEROCOPY = 1
@@ -34,11 +34,12 @@ def reason_slot(r: int) -> int:
     return r if r < 6 else r - 1
 CHECK_IP4, MARK_IP4, CHECK_AUTO, MARK_IP6 = 0, 1, 2, 3
 HASH_NONE, HASH_FLOWID, HASH_FLOW5ID = 0, 1, 2
-CLS_NONE, CLS_LB_HASH, CLS_HASH_IP, CLS_HASHSWITCH, CLS_PROGRAM, CLS_LB_CRC = 0, 1, 2, 3, 4, 5
+CLS_NONE, CLS_LB_HASH, CLS_HASH_IP, CLS_HASHSWITCH, CLS_PROGRAM, CLS_LB_CRC, CLS_LB_TABLE = 0, 1, 2, 3, 4, 5, 6
 PROG_IPFILTER, PROG_CLASSIFIER = 0, 1
 STEP_SHORT_YES = 1
 MAX_STEPS = 8192
 MAX_PORTS = 64
+LB_TABLE_MAX = 1 << 24
 MAX_ADDRS = 16
 CTR_COUNT, CTR_DROPS, CTR_REASON, CTR_PORT = 0, 1, 2, 16
 NCOUNTERS = CTR_PORT + MAX_PORTS + 1
@@ -201,6 +202,8 @@ FCGPU_SYMBOLS = {
                                      C.POINTER(fcgpu_out)]),
     "fcgpu_set_program": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(fcgpu_step), C.c_uint32,
                                     C.c_int32]),
+    "fcgpu_set_lb_table": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    "fcgpu_lb_hash_ring": (C.c_int, [C.c_uint32, C.c_uint32, C.c_void_p]),
     "fcgpu_set_host_threads": (C.c_int, [C.c_void_p, C.c_uint32]),
     "fcgpu_span_submit": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32,
                                     C.POINTER(fcgpu_out)]),
@@ -278,6 +281,19 @@ def load(path: str = LIBFCGPU):
         raise NativeMissing("libfcgpu.so ABI version mismatch")
     _lib = lib
     return lib
+
+
+def lb_hash_ring(nsel: int, size: int | None = None):
+    """The constant_hash_agg ring (fcgpu_lb_hash_ring: LoadBalancer::
+    build_hash_ring over [0, nsel), size CST_BUCKETS or 100 per output) as a
+    uint8 array, the table Context.set_lb_table takes. Host-only."""
+    import numpy as np
+    size = 100 * nsel if size is None else size
+    out = np.zeros(size, np.uint8)
+    rc = load().fcgpu_lb_hash_ring(nsel, size, out.ctypes.data)
+    if rc != OK:
+        raise ValueError(f"fcgpu_lb_hash_ring({nsel}, {size}) failed ({rc})")
+    return out
 
 
 def default_cfg() -> fcgpu_cfg:
@@ -446,6 +462,12 @@ class Context:
             arr[i] = st if isinstance(st, fcgpu_step) else fcgpu_step(*[int(x) for x in st])
         self._chk(self.lib.fcgpu_set_program(self.h, kind, arr, len(steps), output_everything),
                   "fcgpu_set_program")
+
+    def set_lb_table(self, table):
+        """The bucket -> output table of CLS_LB_TABLE (uint8 sequence)."""
+        import numpy as np
+        t = np.ascontiguousarray(table, dtype=np.uint8)
+        self._chk(self.lib.fcgpu_set_lb_table(self.h, t.ctypes.data, len(t)), "fcgpu_set_lb_table")
 
     def program_jit(self, enable=True):
         """Compile the installed (and later) decision programs to code (hiprtc)."""

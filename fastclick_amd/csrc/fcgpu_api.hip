@@ -223,6 +223,9 @@ struct fcgpu_ctx {
     unsigned long long *d_ctr_own = nullptr;  // context-owned vector
     uint4 *d_prog = nullptr;                  // decision program (FCGPU_CLS_PROGRAM)
     uint4 *d_crc = nullptr;                   // LB_CRC slicing tables (crc32c_u32_tab)
+    uint8_t *d_lbtab = nullptr;               // LB_TABLE bucket -> output (fcgpu_set_lb_table)
+    uint32_t lbtab_n = 0, lbtab_max = 0;      // its buckets and largest output
+    uint64_t lbtab_key = 0;                   // hash of its contents (0: none)
     uint32_t prog_n = 0, prog_kind = 0, prog_q = 0, prog_tab = 0;
     int32_t prog_all = -1;
     std::vector<fcgpu_step> prog_host;   // the installed program (capture reach)
@@ -378,7 +381,7 @@ static void launch_rx(const RxLaunch &L, uint32_t grid, hipStream_t s, hipEvent_
             return;
         }
     }
-    const size_t lds = prog_lds_bytes(L.A.cfg);   // program steps (PROG) or CRC tables (LB_CRC), else 0
+    const size_t lds = prog_lds_bytes(L.A.cfg);   // program steps (PROG), CRC tables (LB_CRC), LB table, else 0
     if (ev0)
         hipExtLaunchKernelGGL((k_rx<CM, CK, PART, PROG, L4, FLOW>), dim3(grid), dim3(kTile), lds, s, ev0, ev1,
                               0, L);
@@ -968,6 +971,7 @@ void fcgpu_close(fcgpu_ctx *c) {
         hipFree(c->d_ctr_own);
         hipFree(c->d_prog);
         hipFree(c->d_crc);
+        hipFree(c->d_lbtab);
         hipFree(c->d_verdict);
         hipFree(c->d_arena);
         hipFree(c->d_desc);
@@ -1061,7 +1065,7 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     const bool ip4mode = cfg->check_mode == FCGPU_CHECK_IP4 || cfg->check_mode == FCGPU_MARK_IP4;
     if (cfg->vlan_ethertype > 0xffff) return fail(c, FCGPU_EINVAL, "bad vlan_ethertype");
     if (cfg->hash_mode > FCGPU_HASH_FLOW5ID) return fail(c, FCGPU_EINVAL, "bad hash_mode");
-    if (cfg->classify > FCGPU_CLS_LB_CRC) return fail(c, FCGPU_EINVAL, "bad classify mode");
+    if (cfg->classify > FCGPU_CLS_LB_TABLE) return fail(c, FCGPU_EINVAL, "bad classify mode");
     if (cfg->classify == FCGPU_CLS_LB_CRC && !(cfg->check_mode == FCGPU_CHECK_IP4 || cfg->check_mode == FCGPU_MARK_IP4))
         return fail(c, FCGPU_EINVAL, "LB_MODE hash_crc hashes IPFlow5ID: IPv4 check modes only");
     if (cfg->l4_mode > FCGPU_L4_TCP) return fail(c, FCGPU_EINVAL, "bad l4_mode");
@@ -1119,6 +1123,9 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
         HIPCHK(c, hipMemcpy(c->d_crc, t.data(), sizeof(uint32_t) * 1024, hipMemcpyHostToDevice));
     }
     d.crc_tab = cfg->classify == FCGPU_CLS_LB_CRC ? c->d_crc : nullptr;
+    d.lb_tab = cfg->classify == FCGPU_CLS_LB_TABLE ? c->d_lbtab : nullptr;
+    d.lb_tab_n = c->lbtab_n;
+    d.lb_tab_magic = c->lbtab_n > 1 ? (uint32_t)((((uint64_t)1 << 32) + c->lbtab_n - 1) / c->lbtab_n) : 0u;
     d.prog = c->d_prog;
     d.prog_n = c->prog_n;
     d.prog_q = c->prog_q;
@@ -1141,6 +1148,8 @@ static int check_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d
     if (!c->configured) return fail(c, FCGPU_EINVAL, "not configured");
     if (c->cfg.classify == FCGPU_CLS_PROGRAM && !c->d_prog && c->prog_all < 0)
         return fail(c, FCGPU_EINVAL, "FCGPU_CLS_PROGRAM without fcgpu_set_program");
+    if (c->cfg.classify == FCGPU_CLS_LB_TABLE && (!c->d_lbtab || c->lbtab_max >= c->cfg.nports))
+        return fail(c, FCGPU_EINVAL, "FCGPU_CLS_LB_TABLE without fcgpu_set_lb_table of outputs < nports");
     if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "batch larger than max_batch");
     if (n && (!d_arena || !d_desc)) return fail(c, FCGPU_EINVAL, "null arena/desc");
     if (o->partition > FCGPU_PART_TILE) return fail(c, FCGPU_EINVAL, "bad partition mode");
@@ -1956,6 +1965,7 @@ static bool agg_compatible(const AggItem &a, const AggItem &b) {
     DevCfg x = a.dcfg, y = b.dcfg;
     x.prog = y.prog = nullptr;
     x.crc_tab = y.crc_tab = nullptr;
+    x.lb_tab = y.lb_tab = nullptr;
     return memcmp(&x, &y, sizeof(DevCfg)) == 0 && a.prog_key == b.prog_key &&
            (a.dcfg.crc_tab != nullptr) == (b.dcfg.crc_tab != nullptr) && a.cm == b.cm && a.ck == b.ck &&
            (a.fn != nullptr) == (b.fn != nullptr) && out_part(&a.job.out) == out_part(&b.job.out) &&
@@ -2146,7 +2156,8 @@ static int agg_submit(fcgpu_ctx *c, uint32_t slot, const fcgpu_job &j, uint32_t 
     if (it.cm == FCGPU_MARK_IP4 || it.cm == FCGPU_MARK_IP6) it.ck = false;
     it.ctr = c->d_ctr;
     it.fn = nullptr;
-    it.prog_key = c->cfg.classify == FCGPU_CLS_PROGRAM ? c->prog_key : 0;
+    it.prog_key = c->cfg.classify == FCGPU_CLS_PROGRAM ? c->prog_key
+                : c->cfg.classify == FCGPU_CLS_LB_TABLE ? c->lbtab_key : 0;
     if (c->cfg.classify == FCGPU_CLS_PROGRAM && !c->jit_src.empty()) {
         const bool ip4 = it.cm == FCGPU_CHECK_IP4 || it.cm == FCGPU_MARK_IP4;
         it.fn = jit_function(c, jit_key((int)it.cm, it.ck, out_part(&j.out), ip4 && c->cfg.l4_mode != FCGPU_L4_NONE,
@@ -2747,6 +2758,54 @@ int fcgpu_set_program(fcgpu_ctx *c, uint32_t kind, const fcgpu_step *steps, uint
     for (uint32_t v : {c->prog_n, c->prog_q, c->prog_tab, c->prog_kind, (uint32_t)c->prog_all}) mix(v);
     c->prog_key = key | 1;
     if (c->jit_on && jit_install(c) != FCGPU_OK) c->err.clear();   // a cycle: interpreted
+    return FCGPU_OK;
+}
+
+// Server i at cantor(i, j) % size (include/click/algorithm.hh:136-138,
+// unsigned) for j < ((size - 1) / nsel) + 1, later placements winning; an
+// empty bucket takes the last server placed before it (server 0 before the
+// first).
+int fcgpu_lb_hash_ring(uint32_t nsel, uint32_t size, uint8_t *out) {
+    if (nsel < 1 || nsel > FCGPU_MAX_PORTS || size < 1 || size > FCGPU_LB_TABLE_MAX || !out) return FCGPU_EINVAL;
+    std::vector<uint32_t> ring(size, 0xffffffffu);
+    const uint32_t fac = (size - 1) / nsel + 1;
+    for (uint32_t j = 0; j < fac; ++j)
+        for (uint32_t i = 0; i < nsel; ++i) ring[(((i + j) * (i + j + 1)) / 2 + j) % size] = i;
+    uint32_t cur = 0;
+    for (uint32_t i = 0; i < size; ++i) {
+        if (ring[i] != 0xffffffffu) cur = ring[i];
+        out[i] = (uint8_t)cur;
+    }
+    return FCGPU_OK;
+}
+
+int fcgpu_set_lb_table(fcgpu_ctx *c, const uint8_t *table, uint32_t nbuckets) {
+    if (!c) return FCGPU_EINVAL;
+    if (!table || nbuckets == 0 || nbuckets > FCGPU_LB_TABLE_MAX) return fail(c, FCGPU_EINVAL, "bad LB table size");
+    if (agg_queued(c)) return fail(c, FCGPU_EINVAL, "fcgpu_set_lb_table: a queued span submission is not waited for");
+    // ((h >> 16) ^ (h & 0xffff)) < 65536: entries past 65535 are never read
+    const uint32_t n = std::min(nbuckets, 65536u);
+    uint32_t mx = 0;
+    for (uint32_t k = 0; k < n; ++k) mx = std::max(mx, (uint32_t)table[k]);
+    if (c->configured && mx >= c->cfg.nports) return fail(c, FCGPU_EINVAL, "LB table output >= nports");
+    // k_rx copies kTabLdsBytes into LDS whatever the size: zero-padded
+    std::vector<uint8_t> dev(std::max<size_t>(n, kTabLdsBytes), 0);
+    memcpy(dev.data(), table, n);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());
+    hipFree(c->d_lbtab);
+    c->d_lbtab = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_lbtab, dev.size()));
+    HIPCHK(c, hipMemcpy(c->d_lbtab, dev.data(), dev.size(), hipMemcpyHostToDevice));
+    c->lbtab_n = n;
+    c->lbtab_max = mx;
+    uint64_t key = 1469598103934665603ull;
+    for (uint32_t k = 0; k < n; ++k) key = (key ^ table[k]) * 1099511628211ull;
+    c->lbtab_key = (key ^ n) | 1;
+    DevCfg &d = c->dcfg;
+    d.lb_tab = c->cfg.classify == FCGPU_CLS_LB_TABLE ? c->d_lbtab : nullptr;
+    d.lb_tab_n = n;
+    d.lb_tab_magic = n > 1 ? (uint32_t)((((uint64_t)1 << 32) + n - 1) / n) : 0u;
     return FCGPU_OK;
 }
 

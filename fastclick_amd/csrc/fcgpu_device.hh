@@ -54,6 +54,9 @@ struct DevCfg {
     uint32_t prog_kind;
     int32_t prog_all;         // >= 0: empty program, every packet -> this output
     const uint4 *crc_tab;     // FCGPU_CLS_LB_CRC: 4 x 256 u32 slicing tables (1 KB each)
+    const uint8_t *lb_tab;    // FCGPU_CLS_LB_TABLE: bucket -> output (>= kTabLdsBytes allocated)
+    uint32_t lb_tab_n;        // buckets (<= 65536: the folded hash is < 2^16)
+    uint32_t lb_tab_magic;    // ceil(2^32 / lb_tab_n) for lb_port's fastmod
 };
 
 // Device step: x = (u16)offset | flags << 16, y = value, z = mask,
@@ -215,6 +218,15 @@ __device__ __forceinline__ int lb_port(uint32_t h, uint32_t n, uint32_t m) {
     return n == 1 ? 0 : (int)(x - q * n);
 }
 
+// LoadBalancer constant_hash_agg (loadbalancer.hh:585-589): the ring's entry
+// at ((h >> 16) ^ (h & 0xffff)) % buckets (lb_port's fastmod is exact for any
+// buckets <= 2^16: x * e < 2^16 * 2^16), from the workgroup's LDS copy when the
+// table is there (dyn != nullptr), else from global memory
+__device__ __forceinline__ uint32_t lb_table_port(const DevCfg &c, const uint4 *dyn, uint32_t h) {
+    const uint32_t b = (uint32_t)lb_port(h, c.lb_tab_n, c.lb_tab_magic);
+    return dyn ? reinterpret_cast<const uint8_t *>(dyn)[b] : c.lb_tab[b];
+}
+
 // rte_hash_crc_4byte(data, crc) (DPDK rte_hash_crc.h: _mm_crc32_u32(crc, data)):
 // CRC32-C, reflected polynomial 0x82F63B78, no inversion -- a reflected CRC
 // takes the 32-bit word at once (xor) and shifts it through bit by bit.
@@ -335,11 +347,18 @@ __host__ __device__ inline bool prog_in_lds(const DevCfg &c) {
 #endif
 }
 // dynamic LDS of a k_rx launch: only program mode pays for the step cache,
-// only LB_CRC for its 4-KB slicing tables
+// only LB_CRC for its 4-KB slicing tables, only LB_TABLE for its table when
+// it has at most 4096 buckets (the default ring of 100 per output, up to 40
+// outputs)
 constexpr uint32_t kCrcTabQ = 256;          // 4 x 256 u32 = 256 uint4
+constexpr uint32_t kTabLdsBytes = 4096;     // = kTile x 16 B: one uint4 per thread
 __host__ __device__ inline bool crc_in_lds(const DevCfg &c) { return c.classify == FCGPU_CLS_LB_CRC && c.crc_tab; }
+__host__ __device__ inline bool tab_in_lds(const DevCfg &c) {
+    return c.classify == FCGPU_CLS_LB_TABLE && c.lb_tab && c.lb_tab_n <= kTabLdsBytes;
+}
 inline size_t prog_lds_bytes(const DevCfg &c) {
-    return prog_in_lds(c) ? sizeof(uint4) * c.prog_q : crc_in_lds(c) ? sizeof(uint4) * kCrcTabQ : 0;
+    return prog_in_lds(c) ? sizeof(uint4) * c.prog_q : crc_in_lds(c) ? sizeof(uint4) * kCrcTabQ
+         : tab_in_lds(c) ? kTabLdsBytes : 0;
 }
 #ifdef FCGPU_JIT_PROGRAM
 // The installed program compiled to straight-line code (fcgpu_program_jit,
@@ -510,6 +529,7 @@ __device__ __forceinline__ void process_packet(const DevCfg &c, const FrameView 
         r.port = (uint32_t)lb_port(crc, c.nports, c.lb_magic);
         break;
     }
+    case FCGPU_CLS_LB_TABLE: r.port = lb_table_port(c, sprog, hv); break;
     case FCGPU_CLS_HASH_IP: r.port = (uint32_t)bytesum_port(f, an.length, 26, 8, c.nports); break;
     case FCGPU_CLS_HASHSWITCH:
         r.port = (uint32_t)bytesum_port(f, an.length, c.hs_offset, c.hs_length, c.nports);
@@ -592,6 +612,8 @@ __device__ __forceinline__ bool ip4_fast(const DevCfg &c, const FrameView &f, ui
         const uint32_t crc = flow5_crc(sprog, (h[2] >> 8) & 0xff, first ? h[3] : 0u, first ? h[4] : 0u,
                                        first ? h[5] : 0u);
         port = (uint32_t)lb_port(crc, c.nports, c.lb_magic);
+    } else if (c.classify == FCGPU_CLS_LB_TABLE) {
+        port = lb_table_port(c, sprog, hv);
     } else if (c.classify != FCGPU_CLS_NONE && (!PROG || c.classify != FCGPU_CLS_PROGRAM)) {
         return false;                                  // byte-sum classifiers: general path
     }
@@ -653,8 +675,8 @@ __device__ __forceinline__ bool auto_fast(const DevCfg &c, const FrameView &f, u
     // classifiers the straight line covers (wave-uniform)
     const bool prog = PROG && c.classify == FCGPU_CLS_PROGRAM;
     const bool cls4 = c.classify == FCGPU_CLS_LB_HASH || c.classify == FCGPU_CLS_LB_CRC ||
-                      c.classify == FCGPU_CLS_NONE || prog;
-    const bool cls6 = c.classify == FCGPU_CLS_LB_HASH || prog;
+                      c.classify == FCGPU_CLS_LB_TABLE || c.classify == FCGPU_CLS_NONE || prog;
+    const bool cls6 = c.classify == FCGPU_CLS_LB_HASH || c.classify == FCGPU_CLS_LB_TABLE || prog;
     // CheckIPHeader::valid's reason chain as predicates (ip4_fast)
     const uint32_t b0 = h[0] & 0xff, hlen = (b0 & 15) << 2, L = bswap16(h[0] >> 16);
     const bool tiny = (int)plen < 20, badv = (b0 >> 4) != 4, badhl = hlen < 20;
@@ -711,6 +733,8 @@ __device__ __forceinline__ bool auto_fast(const DevCfg &c, const FrameView &f, u
         const uint32_t crc = flow5_crc(sprog, (h[2] >> 8) & 0xff, first ? h[3] : 0u, first ? h[4] : 0u,
                                        first ? h[5] : 0u);
         port = (uint32_t)lb_port(crc, c.nports, c.lb_magic);
+    } else if (c.classify == FCGPU_CLS_LB_TABLE) {
+        port = lb_table_port(c, sprog, hv);
     }
     r.reason = reason;
     r.hash = ok ? hv : 0u;
@@ -1364,7 +1388,7 @@ template <int CM, bool CK, int PART, bool PROG, bool L4, bool FLOW = false,
 __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4 * kWave * kWin];
     __shared__ uint32_t s_cnt[4][kMaxBins];
-    extern __shared__ uint4 s_prog[];           // prog_lds_bytes(cfg) at launch: program steps or CRC tables
+    extern __shared__ uint4 s_prog[];           // prog_lds_bytes(cfg) at launch: program steps, CRC or LB tables
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const RxArgs &A = L.A;
     RxView V = rx_view(A);
@@ -1415,11 +1439,14 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
     // decision program: the block's LDS copy when it fits (block-uniform)
     const bool prog_lds = PROG && prog_in_lds(A.cfg);
     const bool crc_lds = !PROG && crc_in_lds(A.cfg);          // block-uniform
+    const bool tab_lds = !PROG && tab_in_lds(A.cfg);          // block-uniform
     if (prog_lds && threadIdx.x < A.cfg.prog_q) s_prog[threadIdx.x] = A.cfg.prog[threadIdx.x];
     if (crc_lds) s_prog[threadIdx.x] = A.cfg.crc_tab[threadIdx.x];   // kCrcTabQ == kTile
+    if (tab_lds) s_prog[threadIdx.x] = reinterpret_cast<const uint4 *>(A.cfg.lb_tab)[threadIdx.x];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (prog_lds || crc_lds) __syncthreads();
-    rx_tile<CM, CK, PART, PROG, L4, FAST, FLOW>(A, V, FL, tile, d, wl, s_cnt, prog_lds || crc_lds ? s_prog : nullptr);
+    const bool dyn = prog_lds || crc_lds || tab_lds;
+    if (dyn) __syncthreads();
+    rx_tile<CM, CK, PART, PROG, L4, FAST, FLOW>(A, V, FL, tile, d, wl, s_cnt, dyn ? s_prog : nullptr);
 }
 
 // Exclusive scan of one output's per-tile counts (in place) and its total.

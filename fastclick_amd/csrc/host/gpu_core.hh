@@ -41,8 +41,12 @@
 //   VLAN_ETHERTYPE (default 0x8100)          -- VLANDecap(ETHERTYPE) + Strip(14) (MODE AUTO)
 //   MODE MARK6                               -- MarkIP6Header(OFFSET)
 //   BADADDRS, PROCESS_EH                     -- CheckIP6Header (IPv6, MODE AUTO)
-//   N / LB_MODE hash|hash_agg|hash_ip|hash_crc -- FlowSwitch / LoadBalancer
-//   HASHSWITCH "OFFSET LENGTH"               -- HashSwitch
+//   N / LB_MODE hash|hash_agg|hash_ip|hash_crc|chash|cst_hash_agg, CST_BUCKETS
+//                                            -- FlowSwitch / LoadBalancer (the hash
+//     modes: decided per packet, as the reference's per-flow decision caches it)
+//   HASHSWITCH "OFFSET LENGTH"               -- HashSwitch (hash_ip, chash and
+//     HASHSWITCH count their bytes from the frame start, or with STRIP from the
+//     stripped data, as behind Strip(OFFSET); MODE AUTO needs STRIP false for them)
 //   PROGRAM "<program text>", PROGRAM_KIND IPFILTER|CLASSIFIER, PROGRAM_JIT (default
 //     true: the program compiled to code at initialize, fcgpu_program_jit)
 //                                            -- IPFilter / IPClassifier / Classifier:
@@ -202,10 +206,23 @@ class RxCore {
                 _cfg.nports = (uint32_t)n;
                 if (_cfg.classify == FCGPU_CLS_NONE) _cfg.classify = FCGPU_CLS_LB_HASH;
             } else if (k == "LB_MODE") {
+                // LoadBalancer modetrans (include/click/loadbalancer.hh:23-58)
+                _lb_direct = v == "hash";
                 if (v == "hash" || v == "hash_agg") _cfg.classify = FCGPU_CLS_LB_HASH;
                 else if (v == "hash_ip") _cfg.classify = FCGPU_CLS_HASH_IP;
                 else if (v == "hash_crc") _cfg.classify = FCGPU_CLS_LB_CRC;
-                else return err(errh, "unsupported LB_MODE " + v);
+                else if (v == "cst_hash_agg") _cfg.classify = FCGPU_CLS_LB_TABLE;
+                else if (v == "chash") {
+                    // direct_chash = hash_4tuple (:138-152, :666-668): HashSwitch's
+                    // byte sum over frame bytes [26, 38)
+                    _cfg.classify = FCGPU_CLS_HASHSWITCH;
+                    _cfg.hs_offset = 26;
+                    _cfg.hs_length = 12;
+                } else return err(errh, "unsupported LB_MODE " + v);
+            } else if (k == "CST_BUCKETS") {
+                // the constant_hash_agg ring's size (:264, :273-275)
+                if (!parse_int(v, n) || n < 1 || n > (long)FCGPU_LB_TABLE_MAX) return err(errh, "bad CST_BUCKETS");
+                _cst_buckets = (uint32_t)n;
             } else if (k == "HASHSWITCH") {
                 long o, l;
                 std::istringstream ss(v);
@@ -347,6 +364,21 @@ class RxCore {
             for (size_t j = 0; j < if_good.size(); ++j) _cfg.gooddst[j] = if_good[j];
         }
         if (!strip_set) _strip = (_cfg.check_mode == FCGPU_CHECK_AUTO);
+        // The byte-sum classifiers read from p->data() (hashswitch.cc:52-59,
+        // loadbalancer.hh:138-152,227-243): with STRIP the chain is
+        // Strip(OFFSET) -> CheckIPHeader -> ..., so their bytes count from the
+        // IP header, OFFSET bytes into the frame the device indexes
+        if ((_cfg.classify == FCGPU_CLS_HASH_IP || _cfg.classify == FCGPU_CLS_HASHSWITCH) && _strip) {
+            if (_cfg.check_mode == FCGPU_CHECK_AUTO)
+                return err(errh, "LB_MODE hash_ip / chash / HASHSWITCH behind StripEtherVLANHeader read bytes at a "
+                                 "per-packet offset: use STRIP false (offsets from the frame start)");
+            if (_cfg.classify == FCGPU_CLS_HASH_IP) {   // hash_ip = HashSwitch(26, 8)'s sum
+                _cfg.classify = FCGPU_CLS_HASHSWITCH;
+                _cfg.hs_offset = 26;
+                _cfg.hs_length = 8;
+            }
+            _cfg.hs_offset += _cfg.offset;
+        }
         _eff_batch = _batch;
         const bool ip4 = _cfg.check_mode == FCGPU_CHECK_IP4 || _cfg.check_mode == FCGPU_MARK_IP4;
         if (_cfg.l4_mode != FCGPU_L4_NONE && !ip4) return err(errh, "L4 needs MODE CHECK or MARK");
@@ -354,6 +386,10 @@ class RxCore {
         if (_flow_timeout && _flow_mgr != FCGPU_FLOW_MGR_IMP) return err(errh, "FLOW_TIMEOUT needs FLOW_MANAGER IMP");
         if (_cfg.rewrite && !ip4) return err(errh, "DEC_TTL / SET_CHECKSUM need MODE CHECK or MARK");
         if (_cfg.classify == FCGPU_CLS_LB_CRC && !ip4) return err(errh, "LB_MODE hash_crc needs MODE CHECK or MARK");
+        // direct_hash hashes IPFlowID (loadbalancer.hh:580-584), hash_agg the
+        // AGGREGATE annotation HASH sets
+        if (_lb_direct && _cfg.hash_mode == FCGPU_HASH_FLOW5ID)
+            return err(errh, "LB_MODE hash hashes IPFlowID: with HASH FLOW5ID use LB_MODE hash_agg");
         if (_cfg.classify == FCGPU_CLS_PROGRAM) {
             if (_prog.output_everything >= (int32_t)_cfg.nports && _prog.output_everything != 0x7fff)
                 return err(errh, "PROGRAM sends everything to a missing output");
@@ -390,6 +426,14 @@ class RxCore {
             if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_set_program: ") + fcgpu_last_error(_ctx));
             const uint32_t l3 = (uint32_t)_cfg.offset + (_cfg.check_mode == FCGPU_CHECK_AUTO ? 18u : 0u);
             reach = fcgpu::program_reach(_prog_kind, _prog.steps.data(), (uint32_t)_prog.steps.size(), l3, l3 + 60);
+        }
+        if (_cfg.classify == FCGPU_CLS_LB_TABLE) {
+            // the ring of LoadBalancer::set_mode (loadbalancer.hh:526-530):
+            // CST_BUCKETS, or 100 per output
+            std::vector<uint8_t> ring(_cst_buckets ? _cst_buckets : 100u * _cfg.nports);
+            rc = fcgpu_lb_hash_ring(_cfg.nports, (uint32_t)ring.size(), ring.data());
+            if (rc == FCGPU_OK) rc = fcgpu_set_lb_table(_ctx, ring.data(), (uint32_t)ring.size());
+            if (rc != FCGPU_OK) return err(errh, std::string("fcgpu_set_lb_table: ") + fcgpu_last_error(_ctx));
         }
         if (_flow_cap) {
             fcgpu_flow_config fc{_flow_mgr, _flow_cap, _flow_timeout, _flow_recycle_ms};
@@ -1043,6 +1087,8 @@ class RxCore {
 
     fcgpu_cfg _cfg;
     fcgpu_ctx *_ctx = nullptr;
+    bool _lb_direct = false;          // LB_MODE hash (IPFlowID), not hash_agg
+    uint32_t _cst_buckets = 0;        // CST_BUCKETS (0: 100 per output)
     ParsedProgram _prog;
     uint32_t _prog_kind = FCGPU_PROG_IPFILTER;
     bool _prog_jit = true;

@@ -96,20 +96,22 @@ def run_device(ctx: N.Context, dbatch: DeviceBatch, outs: DeviceOutputs, stream=
 
 
 def process_batch(batch, cfg, *, anno=True, perm=True, device_index=0, partition=N.PART_GLOBAL,
-                  program=None, program_jit=False):
+                  program=None, program_jit=False, lb_table=None):
     """One batch on a fresh context (see process_batches)."""
     return process_batches([batch], cfg, anno=anno, perm=perm, device_index=device_index,
-                           partition=partition, program=program, program_jit=program_jit)[0]
+                           partition=partition, program=program, program_jit=program_jit,
+                           lb_table=lb_table)[0]
 
 
 def process_batches(batches, cfg, *, anno=True, perm=True, device_index=0, partition=N.PART_GLOBAL,
-                    program=None, max_flows=0, program_jit=False):
+                    program=None, max_flows=0, program_jit=False, lb_table=None):
     """Upload host Batches, run the device path over them in order on one
     context, return per-batch numpy results and the running counter vector.
     Convenience for tests and smoke(). program: optional (kind, steps,
     output_everything) for CLS_PROGRAM (fcgpu_set_program), compiled to code
     with program_jit (fcgpu_program_jit); max_flows > 0 enables the flow table
-    (its state carries across the batches)."""
+    (its state carries across the batches); lb_table: the CLS_LB_TABLE table
+    (fcgpu_set_lb_table)."""
     torch = _torch()
     res = []
     with torch.cuda.device(device_index):
@@ -119,6 +121,8 @@ def process_batches(batches, cfg, *, anno=True, perm=True, device_index=0, parti
                 ctx.set_program(*program)
                 if program_jit:
                     ctx.program_jit(True)
+            if lb_table is not None:
+                ctx.set_lb_table(lb_table)
             if max_flows:
                 ctx.flow_enable(max_flows)
             for batch in batches:

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 22
+#define FCGPU_ABI_VERSION 23
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -112,6 +112,11 @@ extern "C" {
                                    (ipv4_hash_crc, include/click/dpdk_glue.hh:13-27, via
                                    rte_hash_crc_4byte = the SSE4.2 crc32 instruction), port =
                                    ((c>>16) ^ (c&0xffff)) % nports. IPv4 check modes only */
+#define FCGPU_CLS_LB_TABLE   6  /* LoadBalancer constant_hash_agg (include/click/
+                                   loadbalancer.hh:585-589): port = table[((H>>16) ^
+                                   (H&0xffff)) % buckets], H the hash_mode hash; the table
+                                   (the reference's consistent-hash ring, :170-189) is set
+                                   by fcgpu_set_lb_table */
 
 /* l4_mode: a CheckUDPHeader / CheckTCPHeader after the IPv4 check (CHECK_IP4 or
  * MARK_IP4 only). The checksum covers the whole L4 segment, so with
@@ -475,6 +480,18 @@ int  fcgpu_set_program(fcgpu_ctx *ctx, uint32_t kind, const fcgpu_step *steps, u
 int  fcgpu_program_jit(fcgpu_ctx *ctx, int enable);
 /* 1 when the installed program runs as compiled code. */
 int  fcgpu_program_jit_active(fcgpu_ctx *ctx);
+
+/* The bucket -> output table of FCGPU_CLS_LB_TABLE: nbuckets entries, each
+ * < the configured nports (checked here and at every submission). The folded
+ * hash is < 65536, so a longer table's entries past 65535 are never read; they
+ * are not kept. Synchronises the device before replacing a table. */
+#define FCGPU_LB_TABLE_MAX (1u << 24)
+int  fcgpu_set_lb_table(fcgpu_ctx *ctx, const uint8_t *table, uint32_t nbuckets);
+/* LoadBalancer::build_hash_ring (include/click/loadbalancer.hh:170-189) over
+ * the selector [0, nsel) (nsel <= FCGPU_MAX_PORTS): out[size] = the
+ * constant_hash_agg ring, the table fcgpu_set_lb_table takes. Host-only (no
+ * device, no context). */
+int  fcgpu_lb_hash_ring(uint32_t nsel, uint32_t size, uint8_t *out);
 
 /* Flow table: the IPFlow5ID flow classification of
  * FlowIPManagerHMP (elements/research/flowipmanagerhmp.cc:96-126; the

@@ -157,6 +157,50 @@ int fco_hashswitch_port(const uint8_t *data, uint32_t len, int o, int l, int n)
     return d % n;
 }
 
+/* LoadBalancer::build_hash_ring (include/click/loadbalancer.hh:170-189) over
+ * the selector [0, nsel) (:519-524), with cantor (include/click/algorithm.hh:
+ * 136-138): every server is placed at cantor(s, j) % size for j < fac, later
+ * placements overwriting earlier ones; the empty buckets then take the last
+ * server placed before them (selector[0] before the first). size = the
+ * CST_BUCKETS keyword, or 100 per destination (:526-530). */
+void fco_lb_hash_ring(uint32_t nsel, uint32_t size, uint32_t *ring)
+{
+    for (uint32_t i = 0; i < size; i++)
+        ring[i] = 0xffffffffu;                 /* resize(size, -1) */
+    const int fac = (int)((size - 1) / nsel) + 1;
+    for (int j = 0; j < fac; j++)
+        for (uint32_t i = 0; i < nsel; i++) {
+            const unsigned a = i, b = (unsigned)j;
+            const unsigned cantor = ((a + b) * (a + b + 1)) / 2 + b;
+            ring[cantor % size] = i;
+        }
+    uint32_t cur = 0;
+    for (uint32_t i = 0; i < size; i++) {
+        if (ring[i] == 0xffffffffu)
+            ring[i] = cur;
+        else
+            cur = ring[i];
+    }
+}
+
+/* constant_hash_agg (include/click/loadbalancer.hh:585-589): the ring's entry
+ * at ((h >> 16) ^ (h & 65535)) % _cst_hash.size(); fco_set_lb_table installs
+ * the ring (global, as the program). */
+static uint8_t *g_lbtab;
+static uint32_t g_lbtab_n;
+void fco_set_lb_table(const uint8_t *t, uint32_t n)
+{
+    free(g_lbtab);
+    g_lbtab = (uint8_t *)malloc(n ? n : 1);
+    if (n) memcpy(g_lbtab, t, n);
+    g_lbtab_n = n;
+}
+int fco_lb_table_port(uint32_t h)
+{
+    if (!g_lbtab_n) return 0;
+    return g_lbtab[((h >> 16) ^ (h & 65535)) % g_lbtab_n];
+}
+
 /* include/click/packetbatch.hh:259-307: stable partition into nbatches lists,
  * out-of-range outputs to the last list. */
 void fco_classify_each_packet(int nbatches, const int *port, uint32_t n,
@@ -500,6 +544,7 @@ void fco_process_packet(const fcgpu_cfg *c, const uint8_t *f, uint32_t len, fco_
                                first ? le32(th) : 0, (int)c->nports);
         break;
     }
+    case FCGPU_CLS_LB_TABLE:   port = fco_lb_table_port(h); break;
     case FCGPU_CLS_HASH_IP:    port = fco_hash_ip_port(f, a->length, (int)c->nports); break;
     case FCGPU_CLS_HASHSWITCH: port = fco_hashswitch_port(f, a->length, c->hs_offset,
                                                            c->hs_length, (int)c->nports); break;

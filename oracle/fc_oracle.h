@@ -90,6 +90,9 @@ uint32_t fco_crc32c_u32(uint32_t data, uint32_t crc);           /* rte_hash_crc_
 int fco_lb_crc_port(uint32_t proto, uint32_t saddr, uint32_t daddr, uint32_t ports, int n); /* A8 direct_hash_crc */
 int fco_hash_ip_port(const uint8_t *data, uint32_t len, int n);  /* A8 hash_ip */
 int fco_hashswitch_port(const uint8_t *data, uint32_t len, int off, int l, int n); /* A9 */
+void fco_lb_hash_ring(uint32_t nsel, uint32_t size, uint32_t *ring);  /* A8 cst_hash_agg ring */
+void fco_set_lb_table(const uint8_t *t, uint32_t n);
+int fco_lb_table_port(uint32_t h);
 void fco_classify_each_packet(int nbatches, const int *port, uint32_t n,
                               uint32_t *perm, uint32_t *start); /* A10 */
 /* A10 applied to consecutive `tile`-packet batches (FCGPU_PART_TILE layout):

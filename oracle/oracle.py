@@ -48,6 +48,10 @@ def load():
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.fco_set_program.restype = None
+    lib.fco_lb_hash_ring.restype = None
+    lib.fco_lb_hash_ring.argtypes = [C.c_uint32, C.c_uint32, C.c_void_p]
+    lib.fco_set_lb_table.restype = None
+    lib.fco_set_lb_table.argtypes = [C.c_void_p, C.c_uint32]
     lib.fco_set_program.argtypes = [C.c_uint32, C.POINTER(N.fcgpu_step), C.c_uint32, C.c_int32]
     lib.fco_process_batch.restype = None
     lib.fco_process_batch.argtypes = [C.POINTER(N.fcgpu_cfg), C.c_void_p, C.c_void_p, C.c_uint32,
@@ -91,13 +95,31 @@ def set_program(kind, steps, output_everything=-1):
     lib.fco_set_program(kind, arr, len(steps), output_everything)
 
 
-def process_batch(cfg, batch, program=None):
+def lb_hash_ring(nsel, size=None):
+    """LoadBalancer::build_hash_ring over the selector [0, nsel): the
+    constant_hash_agg table (CST_BUCKETS size, default 100 per destination)."""
+    size = 100 * nsel if size is None else size
+    ring = np.zeros(size, np.uint32)
+    load().fco_lb_hash_ring(nsel, size, _p(ring))
+    return ring
+
+
+def set_lb_table(table):
+    """Install the CLS_LB_TABLE table the oracle uses (global)."""
+    t = np.ascontiguousarray(table, dtype=np.uint8)
+    load().fco_set_lb_table(_p(t), len(t))
+
+
+def process_batch(cfg, batch, program=None, lb_table=None):
     """Run the oracle over a synth.Batch; returns the same dict as the device path.
-    program: optional (kind, steps, output_everything) for CLS_PROGRAM."""
+    program: optional (kind, steps, output_everything) for CLS_PROGRAM;
+    lb_table: the bucket -> output table for CLS_LB_TABLE."""
     from fastclick_amd import _native as N
     lib = load()
     if program is not None:
         set_program(*program)
+    if lb_table is not None:
+        set_lb_table(lb_table)
     n = batch.n
     arena = np.ascontiguousarray(batch.arena)
     desc = np.ascontiguousarray(batch.desc, dtype=np.uint32)

@@ -167,6 +167,9 @@ for s in "${ST[@]}"; do
             step kt_exchange 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_kt_exchange -o run -- python3 scripts/exchange_rate.py --reps 20 ;;
     xrate) step exchange_rate 300 python scripts/exchange_rate.py --reps 30 &&
            step kt_exchange 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_kt_exchange -o run -- python3 scripts/exchange_rate.py --reps 20 ;;
+    # LB_MODE cst_hash_agg (CLS_LB_TABLE) beside the headline's LB_MODE hash
+    r5lbt) var && var --classify lbtable && var --workload c4 --classify lbtable &&
+           var --workload c5 --layout split --classify lbtable && var --classify lbcrc ;;
     # A/B of the library in fastclick_amd/lib/ab/libfcgpu_old.so against the tree's, interleaved
     autoab) for k in 1 2; do
               for w in "--workload c5" "--workload c5 --layout split" "--workload c2"; do

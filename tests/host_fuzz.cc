@@ -269,9 +269,10 @@ static void fuzz_keywords(Rng &rng) {
                                  "PROGRAM", "PROGRAM_KIND", "PROGRAM_JIT", "L4", "L4_CHECKSUM", "COLOR",
                                  "FLOW_CAPACITY", "FLOWID_ANNO", "FLOW_RUNS", "FLOW_MANAGER", "FLOW_TIMEOUT",
                                  "FLOW_RECYCLE_INTERVAL", "DEC_TTL", "TTL_MULTICAST", "SET_CHECKSUM", "HASH",
-                                 "STRIP", "DEVICE", "BATCH", "TIMER", "PARTITION", "INTERFACES", "BOGUS"};
+                                 "STRIP", "DEVICE", "BATCH", "TIMER", "PARTITION", "INTERFACES", "CST_BUCKETS", "BOGUS"};
     static const char *vals[] = {"", "0", "1", "14", "-1", "65536", "4294967296", "true", "false", "yes", "0x10",
                                  "1.2.3.4", "1.2.3.4 5.6.7.8", "256.1.1.1", "hash", "hash_ip", "hash_crc", "hash_agg",
+                                 "chash", "cst_hash_agg", "rr", "16777217",
                                  "AUTO", "MARK", "MARK6", "CHECK", "UDP", "TCP", "IMP", "HMP", "TILE", "GLOBAL",
                                  "\"14 4\"", "14 4", "IPFILTER", "CLASSIFIER", "0.001", "65.536", "1e9", "x",
                                  "\"0 12/00000000%00000000 yes->[0] no->[1]\"", "99999999999999999999",

@@ -464,12 +464,12 @@ COMPACT_CONFS = [
     ("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 8, LB_MODE hash_crc)", 9),
     ("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 5, LB_MODE hash_ip)", 6),
     ("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, HASHSWITCH 6 8, N 7)", 8),
-    ("GPUIPCheckClassify(OFFSET 14, MODE MARK, N 4, LB_MODE hash, HASH FLOW5ID)", 5),
+    ("GPUIPCheckClassify(OFFSET 14, MODE MARK, N 4, LB_MODE hash_agg, HASH FLOW5ID)", 5),
     ("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4, L4 TCP, L4_CHECKSUM false)", 5),
     ("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 8, DEC_TTL true, SET_CHECKSUM true)", 9),
     ("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4, FLOW_CAPACITY 5000)", 5),
     ("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4, LB_MODE hash, L4 UDP)", 5),
-    ("GPUIPCheckClassify(OFFSET 14, MODE MARK, N 4, LB_MODE hash, HASH FLOW5ID, L4 UDP)", 5),
+    ("GPUIPCheckClassify(OFFSET 14, MODE MARK, N 4, LB_MODE hash_agg, HASH FLOW5ID, L4 UDP)", 5),
 ]
 
 
