@@ -923,7 +923,7 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                     sampled_batches=timing["launches"][0])
     cpu = None
     if world == 1 and not args.no_cpu and args.workload in ("c2", "c3", "c4") and not args.flow_capacity \
-            and not args.flow_reshard:
+            and not args.flow_reshard and args.classify in ("lb", "ipclass16"):   # the chains the port runs
         cpu = cpu_baseline(args.cpu_seconds, flows=dict(c2=1, c3=10000).get(args.workload, 4096),
                            program=ipclass16_program() if args.classify == "ipclass16" else None)
     fb = args.frame_bytes

@@ -55,7 +55,7 @@
 using namespace fcgpu;
 
 static_assert(kTile == FCGPU_TILE, "tile size is part of the ABI");
-static_assert(kCrcTabQ == kTile, "k_rx copies the CRC tables with one uint4 per thread");
+static_assert(kCrcTabQ <= kTile, "k_rx copies the CRC tables with one uint4 per thread");
 static constexpr size_t kCtrWords = (size_t)FCGPU_CTR_SHARDS * FCGPU_NCOUNTERS;
 
 namespace {
@@ -1109,18 +1109,18 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     memcpy(d.gooddst, cfg->gooddst, sizeof(d.gooddst));
     memcpy(d.bad6, cfg->bad6, sizeof(d.bad6));
     if (cfg->classify == FCGPU_CLS_LB_CRC && !c->d_crc) {
-        // T_k[b] = crc32c_u32(b << 8k, 0): rte_hash_crc_4byte's 32 shift steps
-        // are linear, so a word is four lookups (fcgpu_device.hh)
-        std::vector<uint32_t> t(1024);
-        for (uint32_t k = 0; k < 4; ++k)
+        // U_k[b] = 16 shift steps of b << 8k: rte_hash_crc_4byte's 32 steps
+        // are linear, so a word is two rounds of two lookups (fcgpu_device.hh)
+        std::vector<uint32_t> t(512);
+        for (uint32_t k = 0; k < 2; ++k)
             for (uint32_t b = 0; b < 256; ++b) {
                 uint32_t x = b << (8 * k);
-                for (int j = 0; j < 32; ++j) x = (x >> 1) ^ (0x82F63B78u & (0u - (x & 1u)));
+                for (int j = 0; j < 16; ++j) x = (x >> 1) ^ (0x82F63B78u & (0u - (x & 1u)));
                 t[256 * k + b] = x;
             }
         HIPCHK(c, hipSetDevice(c->device));
-        HIPCHK(c, hipMalloc(&c->d_crc, sizeof(uint32_t) * 1024));
-        HIPCHK(c, hipMemcpy(c->d_crc, t.data(), sizeof(uint32_t) * 1024, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMalloc(&c->d_crc, sizeof(uint32_t) * 512));
+        HIPCHK(c, hipMemcpy(c->d_crc, t.data(), sizeof(uint32_t) * 512, hipMemcpyHostToDevice));
     }
     d.crc_tab = cfg->classify == FCGPU_CLS_LB_CRC ? c->d_crc : nullptr;
     d.lb_tab = cfg->classify == FCGPU_CLS_LB_TABLE ? c->d_lbtab : nullptr;
@@ -2788,8 +2788,8 @@ int fcgpu_set_lb_table(fcgpu_ctx *c, const uint8_t *table, uint32_t nbuckets) {
     uint32_t mx = 0;
     for (uint32_t k = 0; k < n; ++k) mx = std::max(mx, (uint32_t)table[k]);
     if (c->configured && mx >= c->cfg.nports) return fail(c, FCGPU_EINVAL, "LB table output >= nports");
-    // k_rx copies kTabLdsBytes into LDS whatever the size: zero-padded
-    std::vector<uint8_t> dev(std::max<size_t>(n, kTabLdsBytes), 0);
+    // k_rx copies whole uint4s of it into LDS: zero-padded to 16 B
+    std::vector<uint8_t> dev((n + 15u) & ~15u, 0);
     memcpy(dev.data(), table, n);
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipDeviceSynchronize());

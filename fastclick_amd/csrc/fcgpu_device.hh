@@ -53,7 +53,7 @@ struct DevCfg {
     uint32_t prog_tab;        // uint4 index where the int16 jump tables start
     uint32_t prog_kind;
     int32_t prog_all;         // >= 0: empty program, every packet -> this output
-    const uint4 *crc_tab;     // FCGPU_CLS_LB_CRC: 4 x 256 u32 slicing tables (1 KB each)
+    const uint4 *crc_tab;     // FCGPU_CLS_LB_CRC: 2 x 256 u32 slicing tables (1 KB each)
     const uint8_t *lb_tab;    // FCGPU_CLS_LB_TABLE: bucket -> output (>= kTabLdsBytes allocated)
     uint32_t lb_tab_n;        // buckets (<= 65536: the folded hash is < 2^16)
     uint32_t lb_tab_magic;    // ceil(2^32 / lb_tab_n) for lb_port's fastmod
@@ -237,13 +237,16 @@ __device__ __forceinline__ uint32_t crc32c_u32(uint32_t data, uint32_t crc) {
     return crc;
 }
 // The same through byte-sliced tables: the 32 shifts are linear over GF(2),
-// so crc32c_u32(d, c) = XOR_k T_k[byte k of (c ^ d)] with T_k[b] =
-// crc32c_u32(b << 8k, 0) -- four LDS reads instead of 32 shift steps. The
-// tables (4 KB) are built on the host (fcgpu_configure) and copied to LDS by
-// the workgroups of an LB_CRC launch.
+// and 16 of them take y to (y >> 16) ^ G(y & 0xffff), with G(v) = U0[v & 0xff]
+// ^ U1[v >> 8] and U_k[b] = 16 shift steps of b << 8k -- so a word is two
+// rounds of two LDS reads. The tables (2 KB) are built on the host
+// (fcgpu_configure) and copied to LDS by the workgroups of an LB_CRC launch:
+// 2 KB keeps 8 workgroups per CU, where four 32-step tables (4 KB) kept 7.
 __device__ __forceinline__ uint32_t crc32c_u32_tab(const uint32_t *t, uint32_t data, uint32_t crc) {
-    const uint32_t x = crc ^ data;
-    return t[x & 0xff] ^ t[256 + ((x >> 8) & 0xff)] ^ t[512 + ((x >> 16) & 0xff)] ^ t[768 + (x >> 24)];
+    uint32_t y = crc ^ data;
+    y = (y >> 16) ^ t[y & 0xff] ^ t[256 + ((y >> 8) & 0xff)];
+    y = (y >> 16) ^ t[y & 0xff] ^ t[256 + ((y >> 8) & 0xff)];
+    return y;
 }
 // ipv4_hash_crc(IPFlow5ID, 0) (include/click/dpdk_glue.hh:13-27): proto, saddr,
 // daddr, then the ports word; a non-first fragment's IPFlow5ID has zero
@@ -347,10 +350,11 @@ __host__ __device__ inline bool prog_in_lds(const DevCfg &c) {
 #endif
 }
 // dynamic LDS of a k_rx launch: only program mode pays for the step cache,
-// only LB_CRC for its 4-KB slicing tables, only LB_TABLE for its table when
-// it has at most 4096 buckets (the default ring of 100 per output, up to 40
-// outputs)
-constexpr uint32_t kCrcTabQ = 256;          // 4 x 256 u32 = 256 uint4
+// only LB_CRC for its 2-KB slicing tables, only LB_TABLE for its table (its
+// buckets rounded up to 16 B) when it has at most 4096 buckets. Up to 2,944
+// bytes keep 8 workgroups per CU (17.5 KB of windows and counts each); the
+// default ring, 100 buckets per output, fits for up to 29 outputs
+constexpr uint32_t kCrcTabQ = 128;          // 2 x 256 u32 = 128 uint4
 constexpr uint32_t kTabLdsBytes = 4096;     // = kTile x 16 B: one uint4 per thread
 __host__ __device__ inline bool crc_in_lds(const DevCfg &c) { return c.classify == FCGPU_CLS_LB_CRC && c.crc_tab; }
 __host__ __device__ inline bool tab_in_lds(const DevCfg &c) {
@@ -358,7 +362,7 @@ __host__ __device__ inline bool tab_in_lds(const DevCfg &c) {
 }
 inline size_t prog_lds_bytes(const DevCfg &c) {
     return prog_in_lds(c) ? sizeof(uint4) * c.prog_q : crc_in_lds(c) ? sizeof(uint4) * kCrcTabQ
-         : tab_in_lds(c) ? kTabLdsBytes : 0;
+         : tab_in_lds(c) ? (c.lb_tab_n + 15u) & ~15u : 0;
 }
 #ifdef FCGPU_JIT_PROGRAM
 // The installed program compiled to straight-line code (fcgpu_program_jit,
@@ -1441,9 +1445,12 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
     const bool crc_lds = !PROG && crc_in_lds(A.cfg);          // block-uniform
     const bool tab_lds = !PROG && tab_in_lds(A.cfg);          // block-uniform
     if (prog_lds && threadIdx.x < A.cfg.prog_q) s_prog[threadIdx.x] = A.cfg.prog[threadIdx.x];
-    if (crc_lds) s_prog[threadIdx.x] = A.cfg.crc_tab[threadIdx.x];   // kCrcTabQ == kTile
-    if (tab_lds) s_prog[threadIdx.x] = reinterpret_cast<const uint4 *>(A.cfg.lb_tab)[threadIdx.x];
+    if (crc_lds && threadIdx.x < kCrcTabQ) s_prog[threadIdx.x] = A.cfg.crc_tab[threadIdx.x];
+    if (tab_lds && threadIdx.x * 16u < A.cfg.lb_tab_n)
+        s_prog[threadIdx.x] = reinterpret_cast<const uint4 *>(A.cfg.lb_tab)[threadIdx.x];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (every wave copying the whole table by LDS-DMA instead, with no block
+    // barrier, measured the same: profiles/r05_lb/nobarrier_*)
     const bool dyn = prog_lds || crc_lds || tab_lds;
     if (dyn) __syncthreads();
     rx_tile<CM, CK, PART, PROG, L4, FAST, FLOW>(A, V, FL, tile, d, wl, s_cnt, dyn ? s_prog : nullptr);

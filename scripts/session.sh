@@ -151,7 +151,8 @@ for s in "${ST[@]}"; do
            var --classify lbcrc && var --l4 udp && var --rewrite && var --partition global && var --no-perm &&
            var --errors 0.01 && var --shard strong && var --flow-capacity 1 &&
            var --workload c3 --flow-capacity 20000 && var --workload c4 --flow-capacity 2000000 &&
-           var --workload c4 --flow-capacity 2000000 --flow-manager imp --flow-timeout 1 ;;
+           var --workload c4 --flow-capacity 2000000 --flow-manager imp --flow-timeout 1 &&
+           var --classify lbtable ;;
     r5sweep) for fb in 128 256 512 1024 1500; do var --frame-bytes $fb && var --frame-bytes $fb --layout split || exit $?; done ;;
     # round 5: PMC traffic of the variants (profiles/pmc_traffic.json, scripts/pmc_traffic.py)
     r5pmc) pmcv c2 && pmcv c3 --workload c3 && pmcv c3split --workload c3 --layout split &&
@@ -178,6 +179,15 @@ for s in "${ST[@]}"; do
                 step "ab_new_${n}_$k" 300 python bench.py --steps 200 --warmup 20 --no-cpu $w || exit $?
               done
             done ;;
+    # the same A/B over the variants in $ABV ("|"-separated bench options)
+    abv) IFS='|' read -ra VV <<< "$ABV"
+         for k in 1 2; do
+           for w in "${VV[@]}"; do
+             n=$(echo "$w" | tr -d ' -' | cut -c1-40)
+             FCGPU_LIB=fastclick_amd/lib/ab/libfcgpu_old.so step "ab_old_${n}_$k" 300 python bench.py --steps 200 --warmup 20 --no-cpu $w &&
+             step "ab_new_${n}_$k" 300 python bench.py --steps 200 --warmup 20 --no-cpu $w || exit $?
+           done
+         done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -196,6 +196,9 @@ def test_element_bytesum_behind_strip(oracle):
     whose byte sum reads the IP packet's bytes 26..33 = frame bytes 40..47."""
     from fastclick_amd import click as K
     b = synth.c4(20_000, seed=97)
+    rng = np.random.default_rng(98)
+    for off in b.desc[:, 0].tolist():                # random UDP payload (bytes 42..59)
+        b.arena[off + 42:off + 60] = rng.integers(0, 256, 18, dtype=np.uint8)
     r = K.run_element("GPUIPCheckClassify(OFFSET 14, CHECKSUM true, STRIP true, N 5, LB_MODE hash_ip)", b,
                       nsinks=6)
     cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_HASHSWITCH, hs_offset=40, hs_length=8, nports=5)
