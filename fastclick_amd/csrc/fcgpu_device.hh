@@ -222,9 +222,16 @@ __device__ __forceinline__ int lb_port(uint32_t h, uint32_t n, uint32_t m) {
 // at ((h >> 16) ^ (h & 0xffff)) % buckets (lb_port's fastmod is exact for any
 // buckets <= 2^16: x * e < 2^16 * 2^16), from the workgroup's LDS copy when the
 // table is there (dyn != nullptr), else from global memory
+// (Two plain branches: a select of the two pointers became one flat load,
+// whose pending count made every later store of the tile wait for all earlier
+// ones -- 4 % on the headline kernel, which never takes this path. The wait
+// after the global load keeps its count from reaching the join.)
 __device__ __forceinline__ uint32_t lb_table_port(const DevCfg &c, const uint4 *dyn, uint32_t h) {
     const uint32_t b = (uint32_t)lb_port(h, c.lb_tab_n, c.lb_tab_magic);
-    return dyn ? reinterpret_cast<const uint8_t *>(dyn)[b] : c.lb_tab[b];
+    if (dyn) return reinterpret_cast<const uint8_t *>(dyn)[b];
+    const uint32_t p = c.lb_tab[b];
+    __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0), expcnt / lgkmcnt left alone
+    return p;
 }
 
 // rte_hash_crc_4byte(data, crc) (DPDK rte_hash_crc.h: _mm_crc32_u32(crc, data)):
