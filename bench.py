@@ -117,10 +117,11 @@ def parse(argv=None):
                          "run is timed outside the timed region: flow_maintain_ms)")
     ap.add_argument("--flow-timeout", type=int, default=0, help="imp: TIMEOUT in s (0: none)")
     ap.add_argument("--flow-recycle-ms", type=int, default=1000, help="imp: RECYCLE_INTERVAL in ms")
-    ap.add_argument("--classify", choices=["lb", "lbcrc", "lbtable", "ipclass16"], default="lb",
+    ap.add_argument("--classify", choices=["lb", "lbcrc", "lbtable", "haship", "ipclass16"], default="lb",
                     help="lb: FlowSwitch LB_MODE hash x16 (headline); lbcrc: LB_MODE hash_crc x16 "
                          "(CRC32-C of the IPFlow5ID, DPDK builds); lbtable: LB_MODE cst_hash_agg x16 "
-                         "(the 1600-bucket consistent-hash ring); ipclass16: the survey's "
+                         "(the 1600-bucket consistent-hash ring); haship: LB_MODE hash_ip x16 (byte sum of "
+                         "frame bytes 26..33); ipclass16: the survey's "
                          "IPClassifier with 15 UDP dst-port ranges + '-' (program printed by the "
                          "reference compiler, tests/golden/reftests.json)")
     ap.add_argument("--l4", choices=["none", "udp", "tcp"], default="none",
@@ -500,7 +501,8 @@ class DeviceProcessor:
         self.auto = args.workload == "c5"
         classify = (N.CLS_PROGRAM if program is not None else
                     N.CLS_LB_CRC if args.classify == "lbcrc" else
-                    N.CLS_LB_TABLE if args.classify == "lbtable" else N.CLS_LB_HASH)
+                    N.CLS_LB_TABLE if args.classify == "lbtable" else
+                    N.CLS_HASH_IP if args.classify == "haship" else N.CLS_LB_HASH)
         cfg = N.make_cfg(check_mode=N.CHECK_AUTO if self.auto else N.CHECK_IP4, offset=0 if self.auto else 14,
                          checksum=True, hash_mode=N.HASH_FLOWID, classify=classify, nports=args.nports,
                          badsrc=[N.raw_addr(a) for a in ERROR_BADSRC] if args.errors else (),
@@ -964,7 +966,8 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
                          + " + AggregateHash + "
                          + ({"lb": "FlowSwitch hash 16 outputs",
                              "lbcrc": "FlowSwitch LB_MODE hash_crc 16 outputs",
-                             "lbtable": "FlowSwitch LB_MODE cst_hash_agg 16 outputs (1600-bucket ring)"}.get(
+                             "lbtable": "FlowSwitch LB_MODE cst_hash_agg 16 outputs (1600-bucket ring)",
+                             "haship": "FlowSwitch LB_MODE hash_ip 16 outputs"}.get(
                                 args.classify, "IPClassifier(15 UDP dst-port ranges, -) 16 outputs"))
                          + ("" if args.no_perm else
                             " + stable per-port partition of every 256-packet PacketBatch"

@@ -180,6 +180,12 @@ struct FrameView {
         const uint32_t x = b + shift;
         return (wdw(x & ~3u) >> (8 * (x & 3u))) & 0xff;
     }
+    // rd8 for a frame byte inside the window: one LDS read
+    __device__ __forceinline__ uint32_t rd8_win(uint32_t b) const {
+        const uint32_t x = b + shift, a = x & ~3u;
+        const uint32_t w = *reinterpret_cast<const uint32_t *>(row + ((((a >> 4) ^ sw) << 4) | (a & 15)));
+        return (w >> (8 * (x & 3u))) & 0xff;
+    }
     // rd32 for a frame byte whose dword pair lies in the window (x + 8 <= kWin):
     // LDS reads only. (wdw's choice between the LDS row and the arena compiles
     // to flat loads, which go through the vector-memory path and wait on it.)
@@ -275,6 +281,26 @@ __device__ __forceinline__ int bytesum_port(const FrameView &f, uint32_t len, in
     for (int i = 0; i < l; ++i) d += (int)f.rd8((uint32_t)(o + i));
     if (n == 2 || n == 4 || n == 8) return (d ^ (d >> 4)) & (int)(n - 1);
     return d % (int)n;
+}
+
+// The same byte sum over frame bytes [o, o + l) inside the lane's LDS window
+// (o + l + shift <= kWin): aligned window dwords, bytes outside the range
+// masked, four bytes summed per v_sad_u8; d < 2^16, so lb_port's fastmod
+// (m = ceil(2^32 / n)) takes d % n exactly.
+__device__ __forceinline__ uint32_t win_bytesum_port(const FrameView &f, uint32_t len, uint32_t o, uint32_t l,
+                                                     uint32_t n, uint32_t m) {
+    if (len < o + l) return 0u;
+    const uint32_t x0 = o + f.shift, x1 = x0 + l;
+    uint32_t d = 0;
+    for (uint32_t a = x0 & ~3u; a < x1; a += 4) {
+        const uint32_t w = *reinterpret_cast<const uint32_t *>(f.row + ((((a >> 4) ^ f.sw) << 4) | (a & 15)));
+        uint32_t k = 0xffffffffu;                          // bytes of [x0, x1) in this dword
+        if (a < x0) k &= 0xffffffffu << (8 * (x0 - a));
+        if (a + 4 > x1) k &= 0xffffffffu >> (8 * (a + 4 - x1));
+        d = __builtin_amdgcn_sad_u8(w & k, 0u, d);
+    }
+    if (n == 2 || n == 4 || n == 8) return (d ^ (d >> 4)) & (n - 1);
+    return n == 1 ? 0u : d - __umulhi(d, m) * n;
 }
 
 // A decision program over one valid packet (IPFilter::match, ipfilter.hh:393-481
@@ -625,8 +651,16 @@ __device__ __forceinline__ bool ip4_fast(const DevCfg &c, const FrameView &f, ui
         port = (uint32_t)lb_port(crc, c.nports, c.lb_magic);
     } else if (c.classify == FCGPU_CLS_LB_TABLE) {
         port = lb_table_port(c, sprog, hv);
+    } else if (c.classify == FCGPU_CLS_HASH_IP || c.classify == FCGPU_CLS_HASHSWITCH) {   // wave-uniform
+        // LoadBalancer::hash_ip (loadbalancer.hh:227-243) = HashSwitch(26, 8),
+        // HashSwitch::process (hashswitch.cc:50-66) over the trimmed packet
+        const uint32_t bo = c.classify == FCGPU_CLS_HASH_IP ? 26u : (uint32_t)c.hs_offset;
+        const uint32_t bl = c.classify == FCGPU_CLS_HASH_IP ? 8u : (uint32_t)c.hs_length;
+        if (f.shift + bo + bl > (uint32_t)kWin) return false;   // bytes past the window: general path
+        const uint32_t tl = plen > L ? len - (plen - L) : len;
+        port = win_bytesum_port(f, tl, bo, bl, c.nports, c.lb_magic);
     } else if (c.classify != FCGPU_CLS_NONE && (!PROG || c.classify != FCGPU_CLS_PROGRAM)) {
-        return false;                                  // byte-sum classifiers: general path
+        return false;
     }
     r.reason = reason;
     r.hash = ok ? hv : 0u;
@@ -685,9 +719,14 @@ __device__ __forceinline__ bool auto_fast(const DevCfg &c, const FrameView &f, u
     const bool v6 = (int)plen >= 1 && (h[0] & 0xf0) == 0x60;
     // classifiers the straight line covers (wave-uniform)
     const bool prog = PROG && c.classify == FCGPU_CLS_PROGRAM;
+    // byte sums (hash_ip = HashSwitch(26, 8)) over frame bytes inside the window
+    const bool bsum = c.classify == FCGPU_CLS_HASH_IP || c.classify == FCGPU_CLS_HASHSWITCH;
+    const uint32_t bo = c.classify == FCGPU_CLS_HASH_IP ? 26u : (uint32_t)c.hs_offset;
+    const uint32_t bl = c.classify == FCGPU_CLS_HASH_IP ? 8u : (uint32_t)c.hs_length;
+    const bool bwin = !bsum || f.shift + bo + bl <= (uint32_t)kWin;
     const bool cls4 = c.classify == FCGPU_CLS_LB_HASH || c.classify == FCGPU_CLS_LB_CRC ||
-                      c.classify == FCGPU_CLS_LB_TABLE || c.classify == FCGPU_CLS_NONE || prog;
-    const bool cls6 = c.classify == FCGPU_CLS_LB_HASH || c.classify == FCGPU_CLS_LB_TABLE || prog;
+                      c.classify == FCGPU_CLS_LB_TABLE || c.classify == FCGPU_CLS_NONE || prog || bsum;
+    const bool cls6 = c.classify == FCGPU_CLS_LB_HASH || c.classify == FCGPU_CLS_LB_TABLE || prog || bsum;
     // CheckIPHeader::valid's reason chain as predicates (ip4_fast)
     const uint32_t b0 = h[0] & 0xff, hlen = (b0 & 15) << 2, L = bswap16(h[0] >> 16);
     const bool tiny = (int)plen < 20, badv = (b0 >> 4) != 4, badhl = hlen < 20;
@@ -717,8 +756,8 @@ __device__ __forceinline__ bool auto_fast(const DevCfg &c, const FrameView &f, u
         bad6 |= h[2] == c.bad6[j][0] && h[3] == c.bad6[j][1] && h[4] == c.bad6[j][2] && h[5] == c.bad6[j][3];
     // decline: header (+ first L4 word) not in the window, IP options, or a
     // classifier of the general path
-    const bool take = v6 ? (a + 48 <= (uint32_t)kWin && cls6)
-                         : (a + 28 <= (uint32_t)kWin && !(early == FCGPU_R_OK && hlen != 20) && cls4);
+    const bool take = bwin && (v6 ? (a + 48 <= (uint32_t)kWin && cls6)
+                                  : (a + 28 <= (uint32_t)kWin && !(early == FCGPU_R_OK && hlen != 20) && cls4));
     if (!take) return false;
     const uint32_t reason = v6 ? (bad6 ? FCGPU_R_BAD_IP6 : FCGPU_R_OK)
                           : early != FCGPU_R_OK ? early
@@ -747,13 +786,14 @@ __device__ __forceinline__ bool auto_fast(const DevCfg &c, const FrameView &f, u
     } else if (c.classify == FCGPU_CLS_LB_TABLE) {
         port = lb_table_port(c, sprog, hv);
     }
+    const uint32_t cut = v6 ? (pl6 < plen - 40 ? plen - 40 - pl6 : 0u) : (plen > L ? plen - L : 0u);
+    if (bsum) port = win_bytesum_port(f, len - cut, bo, bl, c.nports, c.lb_magic);
     r.reason = reason;
     r.hash = ok ? hv : 0u;
     fcgpu_anno &an = r.an;
     an.ipver = v6 ? 6 : early == FCGPU_R_MINISCULE ? 0 : 4;
     an.nh = (uint16_t)x;                                     // the pull() the strip did
     an.th = (uint16_t)(ok ? x + (v6 ? 40u : 20u) : 0u);
-    const uint32_t cut = v6 ? (pl6 < plen - 40 ? plen - 40 - pl6 : 0u) : (plen > L ? plen - L : 0u);
     an.length = (uint16_t)(ok ? len - cut : 0u);
     an.dst_ip = ok && !v6 ? h[4] : 0u;
     an.ip6_nxt = (uint8_t)(ok && v6 ? (h[1] >> 16) & 0xff : 0u);
@@ -770,14 +810,17 @@ __device__ __forceinline__ bool auto_fast(const DevCfg &c, const FrameView &f, u
 
 // Lengths and protocol (checkudpheader.cc:96-111, checktcpheader.cc:96-111).
 // Returns the verdict; l4len = segment length, want_sum = checksum to verify.
+// WIN: every byte it reads is in the LDS window (l4_stage checks it per wave).
+template <bool WIN>
 __device__ __forceinline__ uint32_t l4_check(const DevCfg &c, const FrameView &f, const fcgpu_anno &an,
                                              uint32_t &l4len, bool &want_sum) {
-    const uint32_t w0 = f.rd32(an.nh), w2 = f.rd32(an.nh + 8);
+    auto rd = [&](uint32_t b) { return WIN ? f.rd32_win(b) : f.rd32(b); };
+    const uint32_t w0 = rd(an.nh), w2 = rd(an.nh + 8);
     const uint32_t hl = (w0 & 15) << 2, proto = (w2 >> 8) & 0xff;
     want_sum = false;
     if (c.l4_mode == FCGPU_L4_UDP) {
         if (proto != 17) return FCGPU_R_L4_PROTO;
-        const uint32_t u = f.rd32(an.th + 4);                 // uh_ulen, uh_sum
+        const uint32_t u = rd(an.th + 4);                     // uh_ulen, uh_sum
         const uint32_t len = bswap16(u & 0xffff);
         if (len < 8 || (uint32_t)an.length < len + hl + an.nh) return FCGPU_R_L4_LENGTH;
         l4len = len;
@@ -785,7 +828,7 @@ __device__ __forceinline__ uint32_t l4_check(const DevCfg &c, const FrameView &f
     } else {
         if (proto != 6) return FCGPU_R_L4_PROTO;
         const uint32_t len = bswap16(w0 >> 16) - hl;          // unsigned, as the reference
-        const uint32_t toff = ((f.rd32(an.th + 12) >> 4) & 15) << 2;   // th_off
+        const uint32_t toff = ((rd(an.th + 12) >> 4) & 15) << 2;       // th_off
         if (toff < 20 || len < toff || (uint32_t)an.length < len + hl + an.nh) return FCGPU_R_L4_LENGTH;
         l4len = len;
         want_sum = c.l4_checksum != 0;
@@ -880,24 +923,27 @@ __device__ __forceinline__ uint32_t win_l4_sum(const FrameView &f, uint32_t b, u
 
 // click_in_cksum_pseudohdr (include/clicknet/ip.h:156-163, lib/in_cksum.c:53-111):
 // the final destination of an SSRR/LSRR option replaces ip_dst. True = bad.
+template <bool WIN>
 __device__ __forceinline__ bool l4_cksum_bad(const FrameView &f, const fcgpu_anno &an, uint32_t dsum,
                                              uint32_t len) {
-    const uint32_t w0 = f.rd32(an.nh), hl = (w0 & 15) << 2;
-    const uint32_t proto = (f.rd32(an.nh + 8) >> 8) & 0xff;
-    const uint32_t src = f.rd32(an.nh + 12);
-    uint32_t dst = f.rd32(an.nh + 16);
+    auto rd = [&](uint32_t b) { return WIN ? f.rd32_win(b) : f.rd32(b); };
+    auto rd8 = [&](uint32_t b) { return WIN ? f.rd8_win(b) : f.rd8(b); };
+    const uint32_t w0 = rd(an.nh), hl = (w0 & 15) << 2;
+    const uint32_t proto = (rd(an.nh + 8) >> 8) & 0xff;
+    const uint32_t src = rd(an.nh + 12);
+    uint32_t dst = rd(an.nh + 16);
     if (hl != 20) {
         uint32_t opt = an.nh + 20;
         const uint32_t end = an.nh + hl;
         while (opt < end) {
-            const uint32_t b = f.rd8(opt);
+            const uint32_t b = rd8(opt);
             if (b == 1) { ++opt; continue; }                // IPOPT_NOP
             if (b == 0) break;                              // IPOPT_EOL
             if (opt + 1 >= end) break;
-            const uint32_t l = f.rd8(opt + 1);
+            const uint32_t l = rd8(opt + 1);
             if (l < 2 || opt + l > end) break;
             if ((b == 137 || b == 131) && l >= 7) {         // IPOPT_SSRR, IPOPT_LSRR
-                dst = f.rd32(opt + l - 4);
+                dst = rd(opt + l - 4);
                 break;
             }
             opt += l;
@@ -909,13 +955,15 @@ __device__ __forceinline__ bool l4_cksum_bad(const FrameView &f, const fcgpu_ann
 }
 
 // The L4 stage of k_rx for IPv4-accepted lanes (valid or no program match):
-// length/protocol per lane, then the wave-cooperative checksum.
-__device__ __forceinline__ void l4_stage(const DevCfg &c, const FrameView &f, const uint8_t *frame, bool live,
-                                         PktResult &r) {
+// length/protocol per lane, then the wave-cooperative checksum. WIN: every
+// header byte it reads lies in the LDS window for every such lane of the wave.
+template <bool WIN>
+__device__ __forceinline__ void l4_stage_t(const DevCfg &c, const FrameView &f, const uint8_t *frame, bool live,
+                                           PktResult &r) {
     uint32_t l4len = 0;
     bool want = false;
     if (live && (r.reason == FCGPU_R_OK || r.reason == FCGPU_R_NO_MATCH)) {
-        const uint32_t lr = l4_check(c, f, r.an, l4len, want);
+        const uint32_t lr = l4_check<WIN>(c, f, r.an, l4len, want);
         if (lr != FCGPU_R_OK) {
             r.reason = lr;
             r.port = c.nports;
@@ -928,12 +976,24 @@ __device__ __forceinline__ void l4_stage(const DevCfg &c, const FrameView &f, co
     if (need || __ballot(inwin)) {
         uint32_t dsum = need ? wave_l4_sum(frame + r.an.th, l4len, need) : 0u;
         if (inwin) dsum = win_l4_sum(f, r.an.th, l4len);
-        if (want && l4_cksum_bad(f, r.an, dsum, l4len)) {
+        if (want && l4_cksum_bad<WIN>(f, r.an, dsum, l4len)) {
             r.reason = FCGPU_R_L4_CKSUM;
             r.port = c.nports;
             r.hash = 0;
         }
     }
+}
+// The header reads from the LDS window when, for every lane of the wave that
+// reaches them, the IP header and the first 20 bytes of the L4 header are
+// there (the general reads compile to flat loads, which wait on the
+// vector-memory path): IPv4 puts th right after the options, so th + 20
+// bounds every read of l4_check and l4_cksum_bad.
+__device__ __forceinline__ void l4_stage(const DevCfg &c, const FrameView &f, const uint8_t *frame, bool live,
+                                         PktResult &r) {
+    const bool elig = live && (r.reason == FCGPU_R_OK || r.reason == FCGPU_R_NO_MATCH);
+    const bool inw = (uint32_t)r.an.th + f.shift + 20u <= (uint32_t)kWin;
+    if (!__ballot(elig && !inw)) l4_stage_t<true>(c, f, frame, live, r);
+    else l4_stage_t<false>(c, f, frame, live, r);
 }
 
 // Header windows are read once per launch: non-temporal (cpol nt = 2) keeps

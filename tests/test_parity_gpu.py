@@ -159,6 +159,44 @@ def test_hash_ip_and_hashswitch(dev, oracle, n):
     _check(dev, oracle, b, cfg, f"hashswitch long n={n}")
 
 
+def _shifted(b, seed):
+    """The same frames at offsets 64*i + (0..15): windows at every shift."""
+    rng = np.random.default_rng(seed)
+    sh = rng.integers(0, 16, b.n)
+    slot = int(max(int(b.desc[:, 1].max()) + 16, 64) + 63) & ~63
+    arena = np.zeros(slot * b.n + 4096, np.uint8)
+    desc = np.zeros((b.n, 2), np.uint32)
+    for i, (o, ln) in enumerate(b.desc.tolist()):
+        at = slot * i + int(sh[i])
+        arena[at:at + ln] = b.arena[o:o + ln]
+        desc[i] = (at, ln)
+    return synth.Batch(arena=arena, desc=desc)
+
+
+@pytest.mark.parametrize("n", [4, 8, 11])
+def test_auto_bytesum_classifiers(dev, oracle, n):
+    """hash_ip / HashSwitch on the CHECK_AUTO straight line (VLAN, IPv4 and
+    IPv6 in one wave), their bytes inside the window at every shift, and
+    HashSwitch ranges past it (general path)."""
+    b = _shifted(synth.c5(12_000, seed=90 + n), 91 + n)
+    for cls, o, ln in [(N.CLS_HASH_IP, 0, 1), (N.CLS_HASHSWITCH, 26, 12), (N.CLS_HASHSWITCH, 3, 40),
+                       (N.CLS_HASHSWITCH, 40, 30), (N.CLS_HASHSWITCH, 70, 4)]:
+        cfg = N.make_cfg(check_mode=N.CHECK_AUTO, checksum=True, classify=cls, nports=n, hs_offset=o, hs_length=ln)
+        _check(dev, oracle, b, cfg, f"auto bytesum cls={cls} o={o} l={ln} n={n}")
+
+
+@pytest.mark.parametrize("n", [3, 8, 16])
+def test_ip4_bytesum_classifiers_shifted(dev, oracle, n):
+    """The IPv4 straight line's byte sums at every window shift."""
+    b = synth.c3(12_000, seed=95 + n)
+    synth.inject_errors(b, 0.02, seed=96 + n)
+    b = _shifted(b, 97 + n)
+    for cls, o, ln in [(N.CLS_HASH_IP, 0, 1), (N.CLS_HASHSWITCH, 0, 64), (N.CLS_HASHSWITCH, 13, 35),
+                       (N.CLS_HASHSWITCH, 50, 1)]:
+        cfg = N.make_cfg(offset=14, checksum=True, classify=cls, nports=n, hs_offset=o, hs_length=ln)
+        _check(dev, oracle, b, cfg, f"ip4 bytesum cls={cls} o={o} l={ln} n={n}")
+
+
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 255, 256, 257])
 def test_ragged_sizes(dev, oracle, n):
     b = synth.c4(n, seed=90 + n)
