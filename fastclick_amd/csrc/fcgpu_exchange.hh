@@ -13,7 +13,7 @@
 // buffer of one all-to-all:
 //
 //   k_xsum   per 1024-packet block of perm (4 consecutive packets a
-//            thread): bytes its frames take (4-B slots), and the block's
+//            thread): bytes its frames take (16-B slots), and the block's
 //            partial sum at every segment boundary that falls inside it
 //   k_xscan  one workgroup: exclusive scan of the block sums; each owner's
 //            segment start = its block's scan value + that partial sum
@@ -22,8 +22,8 @@
 //            written coalesced; the frame's arena offset into plan scratch
 //   k_xpack  the frames into their segments, LPF lanes per frame moving 16 B
 //            each (4 / 16 / 64 lanes by the mean frame size): each frame
-//            starts 4-B aligned, the bytes of its last dword past its length
-//            are zero
+//            starts 16-B aligned, the bytes of its slot past its length are
+//            zero
 //   k_xunpack (receiver) records -> descriptors into the received buffer
 // Every per-packet load a thread needs is issued before the first barrier
 // (perm, then the descriptors it names), so a block waits for memory once.
