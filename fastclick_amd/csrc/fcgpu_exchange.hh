@@ -45,6 +45,16 @@ constexpr uint32_t kXItems = kXThreads * kXPer;   // packets per plan block
 // 4-B aligned vectors: the ABI's buffers are only dword-aligned
 typedef uint32_t xu4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t xu2 __attribute__((ext_vector_type(2), aligned(4)));
+// Frame bytes read through global-address-space pointers: a pointer rebuilt
+// from an integer (the dword-aligned base of a frame) is generic, its loads
+// compile to flat loads, which also count on lgkmcnt -- then every LDS wait of
+// the workgroup (the tile sort, the chunk search) waits for them and for the
+// stores too: 199.5 -> see DESIGN section 6.
+typedef const __attribute__((address_space(1))) uint32_t xg32;
+typedef const __attribute__((address_space(1))) xu4 xg4;
+__device__ __forceinline__ xg32 *xgbase(const uint8_t *p, uint32_t sh) {
+    return (xg32 *)(p - sh);        // an address-space cast (no-op for global)
+}
 
 // A frame's slot in the send buffer: its length rounded up to 16 B, so every
 // slot starts 16-B aligned and is written in whole aligned 16-B stores
@@ -268,9 +278,8 @@ __global__ __launch_bounds__(kXThreads) void k_xmeta(XPlan P) {
 // nothing is stored past the slot.
 __device__ __forceinline__ void xcopy_frame(const uint8_t *src, uint32_t len, uint8_t *dstp, uint32_t q,
                                             uint32_t lpf) {
-    const uintptr_t sa = reinterpret_cast<uintptr_t>(src);
-    const uint32_t sh = (uint32_t)(sa & 3u);
-    const uint32_t *al = reinterpret_cast<const uint32_t *>(sa & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3u);
+    xg32 *al = xgbase(src, sh);
     uint32_t *out = reinterpret_cast<uint32_t *>(dstp);
     // four of the lane's chunks per round, their loads issued before any
     // store (a long frame's chunks then wait for memory together)
@@ -284,7 +293,7 @@ __device__ __forceinline__ void xcopy_frame(const uint8_t *src, uint32_t len, ui
             a[k] = xu4{0u, 0u, 0u, 0u};
             e[k] = 0u;
             if (w < len) {
-                a[k] = *reinterpret_cast<const xu4 *>(al + (w >> 2));
+                a[k] = *(xg4 *)(al + (w >> 2));
                 // the fifth dword only when the frame reaches into it (so no
                 // read goes further than 16 B past the frame's end)
                 if (sh && w + 16 - sh < len) e[k] = al[(w >> 2) + 4];
@@ -608,16 +617,68 @@ __global__ __launch_bounds__(kXTile) void k_xbuild(XBuild B) {
         s_dst[pos] = ((s_big >> own) & 1ull) ? ~0ull : s_bbase[own] + off;
     }
     __syncthreads();
-    // the tile's frames in owner order, lpf lanes each by the tile's mean
-    // slot (a 60-B frame is ~5 stores: 4 lanes; 1500 B ~95: 64)
+    // The tile's leaving slots, in owner order, as one run of 16-B chunks
+    // (L.pre: their byte prefix): lane k takes chunks k, k + 256, ..., four
+    // at a time (loads before stores), each found by a binary search of
+    // L.pre. Every lane moves data whatever the frame sizes, and a wave's
+    // stores are 1 KB contiguous but at owner boundaries.
     const uint32_t nl = L.tstart[B.world];
-    const uint32_t mean = nl ? L.pre[kXTile] / nl : 0u;
-    const uint32_t lpf = mean <= 96 ? 4u : mean <= 384 ? 16u : mean <= 768 ? 32u : 64u;
-    for (uint32_t f = threadIdx.x / lpf; f < nl; f += kXTile / lpf) {
-        const uint64_t dst = s_dst[f];
-        const uint32_t fl = s_len[f];
-        if (dst == ~0ull || dst + xslot(fl) > B.send_cap) continue;   // nothing past the buffer
-        xcopy_frame(B.arena + s_src[f], fl, B.send + dst, threadIdx.x % lpf, lpf);
+    const uint32_t nch = L.pre[nl] >> 4;
+    constexpr uint32_t kU = 4;
+    for (uint32_t c0 = threadIdx.x; c0 < nch; c0 += kXTile * kU) {
+        xu4 a[kU];
+        uint32_t e[kU], fr[kU], off[kU];
+#pragma unroll
+        for (uint32_t k = 0; k < kU; ++k) {
+            const uint32_t c = c0 + kXTile * k;
+            a[k] = xu4{0u, 0u, 0u, 0u};
+            e[k] = 0u;
+            fr[k] = 0u;
+            off[k] = 0u;
+            if (c < nch) {
+                // the last frame whose slot starts at or before byte 16c
+                // (empty slots share their start with the next one)
+                const uint32_t x = c << 4;
+                uint32_t lo = 0;
+#pragma unroll
+                for (uint32_t step = kXTile / 2; step; step >>= 1)
+                    if (lo + step < nl && L.pre[lo + step] <= x) lo += step;
+                fr[k] = lo;
+                off[k] = x - L.pre[lo];
+                const uint32_t fl = s_len[lo];
+                const uint8_t *p = B.arena + s_src[lo] + off[k];
+                const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3u);
+                xg32 *al = xgbase(p, sh);
+                a[k] = *(xg4 *)al;
+                // the fifth dword only when the frame reaches into it (so no
+                // read goes further than 16 B past the frame's end)
+                if (sh && off[k] + 16 - sh < fl) e[k] = al[4];
+            }
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kU; ++k) {
+            const uint32_t c = c0 + kXTile * k;
+            if (c >= nch) break;
+            const uint32_t f = fr[k], fl = s_len[f];
+            const uint64_t fd = s_dst[f];
+            if (fd == ~0ull || fd + xslot(fl) > B.send_cap) continue;   // nothing past the buffer
+            const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(B.arena) + s_src[f]) & 3u);
+            uint32_t v0 = __builtin_amdgcn_alignbyte(a[k].y, a[k].x, sh);
+            uint32_t v1 = __builtin_amdgcn_alignbyte(a[k].z, a[k].y, sh);
+            uint32_t v2 = __builtin_amdgcn_alignbyte(a[k].w, a[k].z, sh);
+            uint32_t v3 = __builtin_amdgcn_alignbyte(e[k], a[k].w, sh);
+            const uint32_t rem = fl - off[k];
+            if (rem < 16) {
+                // the slot's last 16 B: bytes past the frame zero
+                auto cut = [rem](uint32_t v, uint32_t j) -> uint32_t {
+                    if (rem <= 4 * j) return 0u;
+                    const uint32_t keep = rem - 4 * j;
+                    return keep >= 4 ? v : v & ((1u << (8 * keep)) - 1u);
+                };
+                v0 = cut(v0, 0), v1 = cut(v1, 1), v2 = cut(v2, 2), v3 = cut(v3, 3);
+            }
+            *reinterpret_cast<uint4 *>(B.send + fd + off[k]) = make_uint4(v0, v1, v2, v3);
+        }
     }
 }
 
