@@ -1530,8 +1530,18 @@ __device__ __forceinline__ void scan_column(uint32_t *tilecnt, uint32_t ntiles, 
     uint32_t *col = tilecnt + (size_t)b * ntiles;
     const uint32_t per = (ntiles + 1023) / 1024;
     const uint32_t beg = threadIdx.x * per;
+    // a thread's first kScanRegs counts stay in registers for the second
+    // pass (a 1M-packet batch has 4 per thread): one round trip to memory
+    constexpr uint32_t kScanRegs = 8;
+    uint32_t keep[kScanRegs];
     uint32_t sum = 0;
-    for (uint32_t j = 0; j < per; ++j) {
+#pragma unroll
+    for (uint32_t j = 0; j < kScanRegs; ++j) {
+        const uint32_t t = beg + j;
+        keep[j] = j < per && t < ntiles ? col[t] : 0u;
+        sum += keep[j];
+    }
+    for (uint32_t j = kScanRegs; j < per; ++j) {
         const uint32_t t = beg + j;
         if (t < ntiles) sum += col[t];
     }
@@ -1551,7 +1561,15 @@ __device__ __forceinline__ void scan_column(uint32_t *tilecnt, uint32_t ntiles, 
         total += v;
     }
     uint32_t run = wpre + incl - sum;
-    for (uint32_t j = 0; j < per; ++j) {
+#pragma unroll
+    for (uint32_t j = 0; j < kScanRegs; ++j) {
+        const uint32_t t = beg + j;
+        if (j < per && t < ntiles) {
+            col[t] = run;
+            run += keep[j];
+        }
+    }
+    for (uint32_t j = kScanRegs; j < per; ++j) {
         const uint32_t t = beg + j;
         if (t < ntiles) {
             const uint32_t v = col[t];

@@ -489,18 +489,24 @@ def test_process_jobs_fused(dev, oracle, partition):
         ctx.close()
 
 
-@pytest.mark.parametrize("mode", ["c5_auto", "mark_crc", "ipclass"])
+@pytest.mark.parametrize("mode", ["c5_auto", "mark_crc", "ipclass", "lbtable_lds", "lbtable_global"])
 def test_process_jobs_fused_equal_batches(dev, oracle, mode):
     """One fused k_rx launch over 24 equal batches (the equal-tile division of
     the grid) plus a ragged tail batch in another launch: C5's
     StripEtherVLANHeader + IPv4/IPv6 dispatch, MarkIPHeader + LB_MODE
-    hash_crc (LDS tables), an IPClassifier program -- every batch's results
-    are the oracle's."""
+    hash_crc (LDS tables), an IPClassifier program, LB_MODE cst_hash_agg with
+    its ring in LDS (1,600 buckets) or read from global memory (70,000) --
+    every batch's results are the oracle's."""
     import torch
     from fastclick_amd import click
     from fastclick_amd.device import DeviceBatch, DeviceOutputs
     program = None
-    if mode == "c5_auto":
+    ring = None
+    if mode.startswith("lbtable"):
+        cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_TABLE, nports=16)
+        ring = N.lb_hash_ring(16, 1600 if mode == "lbtable_lds" else 70_000)
+        mk = lambda k, n: synth.c4(n, seed=650 + k)  # noqa: E731
+    elif mode == "c5_auto":
         cfg = N.make_cfg(check_mode=N.CHECK_AUTO, offset=0, checksum=True, classify=N.CLS_LB_HASH, nports=16)
         mk = lambda k, n: synth.c5(n, seed=500 + k)  # noqa: E731
     elif mode == "mark_crc":
@@ -518,6 +524,8 @@ def test_process_jobs_fused_equal_batches(dev, oracle, mode):
     try:
         if program is not None:
             ctx.set_program(*program)
+        if ring is not None:
+            ctx.set_lb_table(ring)
         dbs = [DeviceBatch.upload(b, device="cuda:0") for b in batches]
         outs = [DeviceOutputs(b.n, 16, device="cuda:0", perm=True, anno=False, partition=N.PART_TILE)
                 for b in dbs]
@@ -526,7 +534,7 @@ def test_process_jobs_fused_equal_batches(dev, oracle, mode):
         torch.cuda.synchronize()
         for k, (b, o) in enumerate(zip(batches, outs)):
             got = o.numpy()
-            exp = oracle.process_batch(cfg, b, program=program)
+            exp = oracle.process_batch(cfg, b, program=program, lb_table=ring)
             for key in ("reason", "port", "perm_tile"):
                 assert np.array_equal(got[key][:b.n], exp[key]), (mode, k, key)
             ok = exp["reason"] == N.R_OK

@@ -430,6 +430,51 @@ def test_gpu_auto_shared_queue_programs_and_flows(oracle):
 
 
 @pytest.mark.gpu
+def test_gpu_auto_shared_queue_lb_tables(oracle):
+    """The shared queue with LB_MODE cst_hash_agg contexts whose rings differ
+    (two with the 1,200-bucket ring of 12 outputs, one with a 333-bucket ring,
+    one with a 5,000-bucket ring read from global memory): a launch fuses only
+    contexts with the same table, and every context's ports are the oracle's
+    with its own ring."""
+    lib = N.load()
+    b = synth.c4(6000 + 13, seed=652)
+    synth.inject_errors(b, 0.02, seed=653)
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_TABLE, nports=12)
+    rings = [N.lb_hash_ring(12, 1200), N.lb_hash_ring(12, 1200), N.lb_hash_ring(12, 333),
+             N.lb_hash_ring(12, 5000)]
+    ctxs, blks = [], []
+    try:
+        for r in rings:
+            c = N.Context(0, 8192, cfg)
+            c.set_lb_table(r)
+            assert lib.fcgpu_span_mode(c.h, N.SPAN_AUTO) == N.OK
+            ctxs.append(c)
+            blks.append([Block(lib, c.h, b, 8192), Block(lib, c.h, b, 8192)])
+        for s in range(2):
+            for c, bl in zip(ctxs, blks):
+                bl[s].res[:] = 0xEE
+                rc = lib.fcgpu_span_submit_block(c.h, s, bl[s].pin, bl[s].in_bytes, 0, bl[s].frames_off, bl[s].n,
+                                                 bl[s].out, OUTS, N.PART_TILE)
+                assert rc == N.OK, lib.fcgpu_last_error(c.h)
+        for s in range(2):
+            for c in ctxs:
+                assert lib.fcgpu_span_wait(c.h, s) == N.OK, lib.fcgpu_last_error(c.h)
+        for k, (r, bl) in enumerate(zip(rings, blks)):
+            exp = oracle.process_batch(cfg, b, lb_table=r)
+            for s in range(2):
+                L, n = bl[s].L, bl[s].n
+                v = bl[s].res[L.verdict:L.verdict + 2 * n].view(np.uint16)
+                assert np.array_equal(v & 0xff, exp["reason"].astype(np.uint16)), (k, s)
+                assert np.array_equal(v >> 8, exp["port"].astype(np.uint16)), (k, s)
+    finally:
+        for bl in blks:
+            for x in bl:
+                x.free()
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", [N.SPAN_COPY, N.SPAN_ZEROCOPY])
 def test_gpu_block_anno8_matches_anno(oracle, mode):
     """FCGPU_OUT_ANNO8 (IPv4 check modes): the 8-B annotations decode to the
