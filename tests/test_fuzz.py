@@ -78,6 +78,19 @@ CONFIGS = {
     "auto-qinq": dict(check_mode=N.CHECK_AUTO, offset=0, checksum=True, classify=N.CLS_LB_HASH, nports=5,
                       vlan_ethertype=0x88A8),
     "mark6": dict(check_mode=N.MARK_IP6, offset=14, classify=N.CLS_LB_HASH, nports=8),
+    # round 5's per-packet classifiers on the fuzzed frames (the straight-line
+    # paths and their declines): hash_crc, the cst_hash_agg ring (LDS and
+    # global), hash_ip / chash byte sums; the ring and hash_ip behind CHECK_AUTO
+    # (hash_crc hashes IPFlow5ID: IPv4 check modes only)
+    "check-lbcrc": dict(offset=14, checksum=True, classify=N.CLS_LB_CRC, nports=16),
+    "check-lbtable": dict(offset=14, checksum=True, classify=N.CLS_LB_TABLE, nports=16, lb_ring=1600),
+    "check-lbtable-global": dict(offset=14, checksum=True, classify=N.CLS_LB_TABLE, nports=9, lb_ring=70_000),
+    "check-haship": dict(offset=14, checksum=True, classify=N.CLS_HASH_IP, nports=8),
+    "check-chash": dict(offset=14, checksum=True, classify=N.CLS_HASHSWITCH, nports=11, hs_offset=26, hs_length=12),
+    "mark-lbcrc": dict(check_mode=N.MARK_IP4, offset=14, classify=N.CLS_LB_CRC, nports=6),
+    "auto-lbtable": dict(check_mode=N.CHECK_AUTO, offset=0, checksum=True, classify=N.CLS_LB_TABLE, nports=12,
+                         lb_ring=333),
+    "auto-haship": dict(check_mode=N.CHECK_AUTO, offset=0, checksum=True, classify=N.CLS_HASH_IP, nports=4),
 }
 
 
@@ -87,10 +100,13 @@ CONFIGS = {
 def test_gpu_fuzz_vs_oracle(oracle, name, seed):
     from fastclick_amd import device
     b = fuzz_batch(20_000, seed)
-    cfg = N.make_cfg(**CONFIGS[name])
-    exp = oracle.process_batch(cfg, b)
+    conf = dict(CONFIGS[name])
+    ring = conf.pop("lb_ring", None)
+    cfg = N.make_cfg(**conf)
+    ring = None if ring is None else N.lb_hash_ring(cfg.nports, ring)
+    exp = oracle.process_batch(cfg, b, lb_table=ring)
     for part in (N.PART_GLOBAL, N.PART_TILE):
-        got = device.process_batch(b, cfg, anno=True, perm=True, partition=part)
+        got = device.process_batch(b, cfg, anno=True, perm=True, partition=part, lb_table=ring)
         compare(got, exp, ctx=f"fuzz {name} seed={seed} part={part}")
         assert np.array_equal(got["counters"], exp["counters"]), f"fuzz {name}: counters"
         if cfg.rewrite:
