@@ -134,6 +134,8 @@ ELEMENT_CONFS = [
     "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BADSRC 192.0.2.255)",
     "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 4, LB_MODE hash_ip, L4 UDP)",
     "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 8, DEC_TTL true, SET_CHECKSUM true, HASH FLOW5ID)",
+    "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 12, LB_MODE cst_hash_agg, CST_BUCKETS 777)",
+    "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE chash)",
 ]
 
 
@@ -151,7 +153,10 @@ def test_gpu_fuzz_element_compact_vs_full(oracle, conf):
     for k in ("port", "seq", "agg", "dst", "len", "nh", "ip8", "batch"):
         assert np.array_equal(full[k], comp[k]), k
     assert full["handlers"] == comp["handlers"]
-    e = oracle.process_batch(K.element_cfg(conf), b)
+    cfg = K.element_cfg(conf)
+    ring = oracle.lb_hash_ring(cfg.nports, 777).astype(np.uint8) if cfg.classify == N.CLS_LB_TABLE else None
+    e = oracle.process_batch(cfg, b, lb_table=ring)
     ok = e["reason"] == N.R_OK
     assert int(comp["handlers"]["drops"]) == int((e["reason"] < N.R_OK).sum())
     assert np.array_equal(comp["agg"][ok], e["hash"][ok])
+    assert np.array_equal(comp["port"], e["port"].astype(np.uint32))
