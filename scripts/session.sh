@@ -153,6 +153,9 @@ for s in "${ST[@]}"; do
            var --workload c3 --flow-capacity 20000 && var --workload c4 --flow-capacity 2000000 &&
            var --workload c4 --flow-capacity 2000000 --flow-manager imp --flow-timeout 1 &&
            var --classify lbtable && var --classify haship ;;
+    r5flowvar) var --flow-capacity 1 && var --workload c3 --flow-capacity 20000 &&
+               var --workload c4 --flow-capacity 2000000 &&
+               var --workload c4 --flow-capacity 2000000 --flow-manager imp --flow-timeout 1 && var ;;
     r5sweep) for fb in 128 256 512 1024 1500; do var --frame-bytes $fb && var --frame-bytes $fb --layout split || exit $?; done ;;
     # round 5: PMC traffic of the variants (profiles/pmc_traffic.json, scripts/pmc_traffic.py)
     r5pmc) pmcv c2 && pmcv c3 --workload c3 && pmcv c3split --workload c3 --layout split &&
