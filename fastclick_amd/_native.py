@@ -302,7 +302,7 @@ def default_cfg() -> fcgpu_cfg:
     if lib is not None:
         lib.fcgpu_default_cfg(C.byref(cfg))
     else:
-        # same values as fcgpu_default_cfg (fcgpu_api.hip)
+        # same values as fcgpu_default_cfg (fcgpu_context.hip)
         cfg.size = C.sizeof(fcgpu_cfg)
         cfg.check_mode = CHECK_IP4
         cfg.hash_mode = HASH_FLOWID

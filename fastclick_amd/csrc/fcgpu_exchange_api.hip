@@ -1,0 +1,140 @@
+// fcgpu_exchange_api.hip -- the flow re-shard across GPUs (SURVEY 8(f) #1 x
+// (e), fcgpu_exchange.hh): plan / pack (the counted exchange of a
+// partitioned batch), build (owner pass + send records in one sequence of
+// launches) and unpack (descriptors over the received arena).
+#include "fcgpu_internal.hh"
+#include "fcgpu_exchange.hh"
+
+using namespace fcgpu;
+using namespace fcgpu_rt;
+
+extern "C" {
+
+int fcgpu_exchange_plan(fcgpu_ctx *c, const uint32_t *d_desc, const uint32_t *d_perm, const uint32_t *d_port_start,
+                        uint32_t n, uint32_t world, uint32_t rank, fcgpu_xmeta *d_meta, uint64_t *d_seg_bytes,
+                        void *stream) {
+    if (!c) return FCGPU_EINVAL;
+    if (world == 0 || world > FCGPU_MAX_PORTS) return fail(c, FCGPU_EINVAL, "fcgpu_exchange_plan: world must be 1..64");
+    if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "fcgpu_exchange_plan: batch larger than the context's max_batch");
+    if (!d_port_start || !d_seg_bytes || (n && (!d_desc || !d_perm || !d_meta)))
+        return fail(c, FCGPU_EINVAL, "fcgpu_exchange_plan: null buffer");
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint32_t nblk_max = (c->max_batch + kXItems - 1) / kXItems;
+    if (!c->x_bsum) {
+        HIPCHK(c, hipMalloc(&c->x_bsum, sizeof(unsigned long long) * (nblk_max + 1)));
+        HIPCHK(c, hipMalloc(&c->x_base, sizeof(unsigned long long) * (FCGPU_MAX_PORTS + 1)));
+        HIPCHK(c, hipMalloc(&c->x_part, sizeof(unsigned long long) * (FCGPU_MAX_PORTS + 1)));
+        HIPCHK(c, hipMalloc(&c->x_src, sizeof(uint32_t) * ((size_t)c->max_batch + 1)));
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    XPlan P{};
+    P.desc = d_desc;
+    P.perm = d_perm;
+    P.port_start = d_port_start;
+    P.n = n;
+    P.world = world;
+    P.rank = rank;
+    P.nblk = (n + kXItems - 1) / kXItems;
+    P.meta = reinterpret_cast<uint4 *>(d_meta);
+    P.bsum = c->x_bsum;
+    P.base = c->x_base;
+    P.part = c->x_part;
+    P.src = c->x_src;
+    P.seg_bytes = reinterpret_cast<unsigned long long *>(d_seg_bytes);
+    if (P.nblk) hipLaunchKernelGGL(k_xsum, dim3(P.nblk), dim3(kXThreads), 0, s, P);
+    hipLaunchKernelGGL(k_xscan, dim3(1), dim3(1024), 0, s, P);
+    if (P.nblk) hipLaunchKernelGGL(k_xmeta, dim3(P.nblk), dim3(kXThreads), 0, s, P);
+    HIPCHK(c, hipGetLastError());
+    return FCGPU_OK;
+}
+
+int fcgpu_exchange_pack(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_port_start,
+                        const fcgpu_xmeta *d_meta, const uint64_t *d_seg_bytes, uint32_t n, uint32_t world,
+                        uint8_t *d_send, uint64_t send_cap, void *stream) {
+    if (!c) return FCGPU_EINVAL;
+    if (world == 0 || world > FCGPU_MAX_PORTS) return fail(c, FCGPU_EINVAL, "fcgpu_exchange_pack: world must be 1..64");
+    if (!d_port_start || !d_seg_bytes || (n && (!d_arena || !d_meta || (send_cap && !d_send))))
+        return fail(c, FCGPU_EINVAL, "fcgpu_exchange_pack: null buffer");
+    if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "fcgpu_exchange_pack: batch larger than the context's max_batch");
+    if (n == 0) return FCGPU_OK;
+    if (!c->x_src) return fail(c, FCGPU_EINVAL, "fcgpu_exchange_pack: no fcgpu_exchange_plan on this context");
+    HIPCHK(c, hipSetDevice(c->device));
+    XPack X{};
+    X.arena = d_arena;
+    X.src = c->x_src;
+    X.port_start = d_port_start;
+    X.meta = reinterpret_cast<const uint4 *>(d_meta);
+    X.seg_bytes = reinterpret_cast<const unsigned long long *>(d_seg_bytes);
+    X.send = d_send;
+    X.send_cap = send_cap;
+    X.n = n;
+    X.world = world;
+    // lanes per frame by the mean slot (send_cap / n): 16 B per lane per step
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint64_t mean = send_cap / n;
+    if (mean <= 96)
+        hipLaunchKernelGGL(k_xpack<4>, dim3((n + kXThreads / 4 - 1) / (kXThreads / 4)), dim3(kXThreads), 0, s, X);
+    else if (mean <= 512)
+        hipLaunchKernelGGL(k_xpack<16>, dim3((n + kXThreads / 16 - 1) / (kXThreads / 16)), dim3(kXThreads), 0, s, X);
+    else
+        hipLaunchKernelGGL(k_xpack<64>, dim3((n + kXThreads / 64 - 1) / (kXThreads / 64)), dim3(kXThreads), 0, s, X);
+    HIPCHK(c, hipGetLastError());
+    return FCGPU_OK;
+}
+
+int fcgpu_exchange_build(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, const uint16_t *d_verdict,
+                         uint32_t n, uint32_t world, uint32_t rank, fcgpu_xmeta *d_meta, uint32_t *d_seg_n,
+                         uint64_t *d_seg_bytes, uint8_t *d_send, uint64_t send_cap, void *stream) {
+    if (!c) return FCGPU_EINVAL;
+    if (world == 0 || world > FCGPU_MAX_PORTS) return fail(c, FCGPU_EINVAL, "fcgpu_exchange_build: world must be 1..64");
+    if (n > c->max_batch) return fail(c, FCGPU_ENOMEM, "fcgpu_exchange_build: batch larger than the context's max_batch");
+    if (!d_seg_n || !d_seg_bytes || (n && (!d_arena || !d_desc || !d_verdict || !d_meta || (send_cap && !d_send))))
+        return fail(c, FCGPU_EINVAL, "fcgpu_exchange_build: null buffer");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (!c->x_tcnt) {
+        HIPCHK(c, hipMalloc(&c->x_tcnt, sizeof(uint32_t) * (size_t)FCGPU_MAX_PORTS * c->max_tiles));
+        HIPCHK(c, hipMalloc(&c->x_tbyt, sizeof(unsigned long long) * (size_t)FCGPU_MAX_PORTS * c->max_tiles));
+    }
+    XBuild B{};
+    B.arena = d_arena;
+    B.desc = d_desc;
+    B.verdict = d_verdict;
+    B.n = n;
+    B.ntiles = (n + kXTile - 1) / kXTile;
+    B.world = world;
+    B.rank = rank;
+    B.tcnt = c->x_tcnt;
+    B.tbyt = c->x_tbyt;
+    B.seg_n = d_seg_n;
+    B.seg_bytes = reinterpret_cast<unsigned long long *>(d_seg_bytes);
+    B.meta = reinterpret_cast<uint4 *>(d_meta);
+    B.send = d_send;
+    B.send_cap = send_cap;
+    if (B.ntiles) hipLaunchKernelGGL(k_xbtile, dim3(B.ntiles), dim3(kXTile), 0, s, B);
+    hipLaunchKernelGGL(k_xbscan, dim3(world), dim3(1024), 0, s, B);    // n = 0: zero counts
+    if (B.ntiles) hipLaunchKernelGGL(k_xbuild, dim3(B.ntiles), dim3(kXTile), 0, s, B);   // lanes per frame: per tile
+    HIPCHK(c, hipGetLastError());
+    return FCGPU_OK;
+}
+
+int fcgpu_exchange_unpack(fcgpu_ctx *c, const fcgpu_xmeta *d_meta, uint32_t n, const uint64_t *src_displ,
+                          uint32_t world, uint32_t *d_desc, void *stream) {
+    if (!c) return FCGPU_EINVAL;
+    if (world == 0 || world > FCGPU_MAX_PORTS) return fail(c, FCGPU_EINVAL, "fcgpu_exchange_unpack: world must be 1..64");
+    if (!src_displ || (n && (!d_meta || !d_desc))) return fail(c, FCGPU_EINVAL, "fcgpu_exchange_unpack: null buffer");
+    if (n == 0) return FCGPU_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    XUnpack U{};
+    U.meta = reinterpret_cast<const uint4 *>(d_meta);
+    U.desc = d_desc;
+    U.n = n;
+    U.world = world;
+    for (uint32_t r = 0; r < world; ++r) U.displ[r] = src_displ[r];
+    hipLaunchKernelGGL(k_xunpack, dim3((n + kXThreads - 1) / kXThreads), dim3(kXThreads), 0,
+                       static_cast<hipStream_t>(stream), U);
+    HIPCHK(c, hipGetLastError());
+    return FCGPU_OK;
+}
+
+}  // extern "C"

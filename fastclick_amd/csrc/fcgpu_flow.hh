@@ -542,13 +542,7 @@ __global__ __launch_bounds__(kFlowGridBlock) void k_flow_assign(FlowArgs F, uint
 // memory latency per 1024 entries.)
 constexpr uint32_t kMaxWheel = 1u << 14;     // wheel buckets (LDS counters)
 constexpr uint32_t kMaintChunk = 1024;       // walk entries per chunk (= block)
-struct MaintArgs {
-    uint32_t *qbsr;          // [wstride] IDs released by the last run, in release order
-    uint32_t *dead;          // [wstride] run number that released the ID
-    uint32_t *counts;        // [chunks][te + 1] per-chunk counts, then offsets
-    uint16_t *rbuf;          // [wstride] each walk entry's destination
-    uint32_t now, to_ms, ri_ms, eps, seq;
-};
+// (the maintainer runs' arguments, MaintArgs, are in fcgpu_device.hh)
 
 // lastseen -> destination: 0 = release, else reschedule r epochs ahead
 __device__ __forceinline__ uint32_t maint_dest(const FlowArgs &F, const MaintArgs &M, uint32_t ls) {

@@ -226,7 +226,7 @@ def main():
     out["mbuf_ingress_mpps_256k_shuffled_2streams"] = round(mbuf_mpps(streams=2), 2)
     out["mbuf_ingress_mpps_256k_shuffled_4streams"] = round(mbuf_mpps(streams=4), 2)
     out["process_host_mpps_1M_global"] = round(raw_host(1 << 20), 2)
-    # fcgpu_process_host's pipeline chunk (kChunk in fcgpu_api.hip, overridable)
+    # fcgpu_process_host's pipeline chunk (kChunk in fcgpu_internal.hh, overridable)
     out["chunk"] = int(os.environ.get("FCGPU_HOST_CHUNK", "131072"))
     for threads in (1, 4, 8):
         out[f"process_host_mpps_1M_tile_t{threads}"] = round(raw_host(1 << 20, threads, tile=True), 2)
