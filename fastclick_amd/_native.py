@@ -15,7 +15,7 @@ LIBFCGPU = os.environ.get("FCGPU_LIB") or os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 23
+ABI_VERSION = 24
 SPAN_SLOTS = 3
 SPAN_COPY = 0
 SPAN_ZEROCOPY = 1
@@ -210,6 +210,7 @@ FCGPU_SYMBOLS = {
     "fcgpu_span_wait": (C.c_int, [C.c_void_p, C.c_uint32]),
     "fcgpu_span_poll": (C.c_int, [C.c_void_p, C.c_uint32]),
     "fcgpu_span_mode": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "fcgpu_span_reserve": (C.c_int, [C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32]),
     "fcgpu_span_zerocopy_active": (C.c_int, [C.c_void_p]),
     "fcgpu_inject_fault": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32]),
     "fcgpu_launch_guard_selftest": (C.c_int, []),

@@ -81,6 +81,11 @@ def load():
         lib.fcclick_bench_timed.restype = C.c_int
         lib.fcclick_bench_timed.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
                                             C.c_double, C.c_uint32, C.POINTER(C.c_double), C.c_char_p, C.c_size_t]
+    if hasattr(lib, "fcclick_run_threads"):        # absent from older A/B builds of the harness
+        lib.fcclick_run_threads.restype = C.c_int
+        lib.fcclick_run_threads.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                            C.c_uint32, C.c_uint32, C.c_void_p, C.c_char_p, C.c_size_t, C.c_char_p,
+                                            C.c_size_t]
     _lib = lib
     return lib
 
@@ -270,3 +275,22 @@ def bench_element(conf: str, batch, *, burst: int = 32, reps: int = 5, threads: 
     if rc != 0:
         raise RuntimeError(err.value.decode())
     return pps.value
+
+
+def run_element_threads(conf: str, batch, *, threads: int, reps: int = 1, burst: int = 32, nsinks: int = 1):
+    """`threads` element instances (one GPU context each) set up, then each
+    pushing `batch` `reps` times and flushing, all at once
+    (fcclick_run_threads). Returns (port_pkts [threads, nsinks]: the packets
+    each thread's outputs received, [one handler dict per thread])."""
+    lib = load()
+    arena = np.ascontiguousarray(batch.arena)
+    desc = np.ascontiguousarray(batch.desc, dtype=np.uint32)
+    pk = np.zeros((threads, nsinks), np.uint64)
+    cap = 4096 * threads
+    hbuf = C.create_string_buffer(cap)
+    err = C.create_string_buffer(512)
+    rc = lib.fcclick_run_threads(conf.encode(), arena.ctypes.data, desc.ctypes.data, batch.n, burst, reps, threads,
+                                 nsinks, pk.ctypes.data, hbuf, cap, err, 512)
+    if rc != 0:
+        raise RuntimeError(err.value.decode())
+    return pk, [parse_handlers(b) for b in hbuf.value.decode().split("--\n")[:-1]]

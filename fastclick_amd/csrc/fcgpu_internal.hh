@@ -23,6 +23,7 @@
 #include <stdlib.h>
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <map>
@@ -145,9 +146,13 @@ struct AggLaunch {
     hipEvent_t ev = nullptr;
     uint32_t refs = 0;        // submissions it carries that have not been waited for
     // kAggIssuing until the thread that took the group from the queue has
-    // issued it (outside the queue's lock), then kAggIssued or kAggFailed
+    // issued it (outside the queue's lock), then kAggIssued or kAggFailed;
+    // owners waiting for that sleep on the queue's condition variable
     std::atomic<int> state{0};
+    // where the issuing thread is (kAggPhase*), for the wait's watchdog report
+    std::atomic<int> phase{0};
 };
+constexpr int kAggPhaseTaken = 0, kAggPhaseLaunch = 1, kAggPhaseRecord = 2;
 constexpr int kAggIssuing = 0, kAggIssued = 1, kAggFailed = 2;
 
 struct SpanSlot {
@@ -173,6 +178,7 @@ struct SpanSlot {
     bool agg = false;
     AggLaunch *al = nullptr;
     bool busy = false;
+    bool reserved = false;       // fcgpu_span_reserve sized d_in / d_res: never regrown on submission
     bool doomed = false;         // fcgpu_inject_fault(FCGPU_FAULT_WAIT): accepted, nothing ran, the wait fails
     hipEvent_t done = nullptr;   // shared streams: the slot's last operation (else the stream is waited)
     bool evt = false;            // the last submission recorded `done`

@@ -68,6 +68,9 @@ struct AggQueue {
     hipStream_t st[4] = {};
     uint32_t rr = 0;
     std::vector<AggLaunch *> spare;
+    // owners whose launch is still being issued by another thread sleep
+    // here (agg_finish); agg_issue wakes them
+    std::condition_variable cv;
 };
 constexpr uint32_t kAggLaunch = 4;
 static std::mutex g_agg_mu;
@@ -204,6 +207,7 @@ static void agg_take_locked(AggQueue &q, std::vector<AggIssue> &out) {
             }
         }
         al->state.store(kAggIssuing, std::memory_order_relaxed);
+        al->phase.store(kAggPhaseTaken, std::memory_order_relaxed);
         al->refs = (uint32_t)grp.size();
         is.al = al;
         for (size_t k : grp) {
@@ -222,12 +226,14 @@ static void agg_take_locked(AggQueue &q, std::vector<AggIssue> &out) {
     }
 }
 // Issue taken launches (no lock held); their owners' waits see the outcome.
-static void agg_issue(int device, std::vector<AggIssue> &iss) {
+// Nothing here waits for anything: a launch, one event record per group.
+static void agg_issue(AggQueue &q, std::vector<AggIssue> &iss) {
     if (iss.empty()) return;
-    const bool dev_ok = hipSetDevice(device) == hipSuccess;
+    const bool dev_ok = hipSetDevice(q.device) == hipSuccess;
     for (AggIssue &is : iss) {
         hipError_t e = dev_ok && is.st && is.al->ev ? hipSuccess : hipErrorInvalidValue;
         if (e == hipSuccess && fault_take(FCGPU_FAULT_LAUNCH)) e = hipErrorLaunchFailure;
+        is.al->phase.store(kAggPhaseLaunch, std::memory_order_relaxed);
         if (e == hipSuccess) {
             if (is.fn) {
                 e = launch_rx_fn(is.fn, is.part, is.L, is.tiles, is.st);
@@ -236,11 +242,17 @@ static void agg_issue(int device, std::vector<AggIssue> &iss) {
                 if (e == hipSuccess) e = hipGetLastError();
             }
         }
+        is.al->phase.store(kAggPhaseRecord, std::memory_order_relaxed);
         if (e == hipSuccess) e = hipEventRecord(is.al->ev, is.st);
         if (e != hipSuccess) (void)hipGetLastError();
         is.al->state.store(e == hipSuccess ? kAggIssued : kAggFailed, std::memory_order_release);
     }
     iss.clear();
+    {   // an owner that found its launch still being issued is asleep in
+        // agg_finish: taking the lock orders this wake-up after its check
+        std::lock_guard<std::mutex> g(q.mu);
+    }
+    q.cv.notify_all();
 }
 // The last AUTO context of a device is gone: every submission it queued was
 // waited for (fcgpu_close / fcgpu_span_mode wait or refuse busy slots), so
@@ -300,7 +312,7 @@ static int agg_submit(fcgpu_ctx *c, uint32_t slot, const fcgpu_job &j, uint32_t 
         sp.busy = true;
         if (q.pending.size() >= kAggLaunch) agg_take_locked(q, iss);
     }
-    agg_issue(q.device, iss);
+    agg_issue(q, iss);
     return FCGPU_OK;
 }
 // Wait for (block = true) or poll a queued submission: launched first if
@@ -315,12 +327,27 @@ static int agg_finish(fcgpu_ctx *c, uint32_t slot, bool block) {
         if (!sp.al) agg_take_locked(q, iss);     // still pending: it (and every other) goes now
         al = sp.al;
     }
-    agg_issue(q.device, iss);
-    // the thread that took its group issues it outside the lock
-    int st;
-    while ((st = al->state.load(std::memory_order_acquire)) == kAggIssuing) {
+    agg_issue(q, iss);
+    // the thread that took its group issues it outside the lock: sleep until
+    // it has (a yield loop here kept up to 15 owner threads spinning on the
+    // CPUs the issuing thread needed). Issuing never waits for anything, so
+    // a launch still not issued after seconds means a stall inside the HIP
+    // runtime on that thread: reported (stderr) every 5 s, with where it is
+    int st = al->state.load(std::memory_order_acquire);
+    if (st == kAggIssuing) {
         if (!block) return 0;
-        std::this_thread::yield();
+        std::unique_lock<std::mutex> lk(q.mu);
+        uint32_t waited_s = 0;
+        while ((st = al->state.load(std::memory_order_acquire)) == kAggIssuing) {
+            if (q.cv.wait_for(lk, std::chrono::seconds(5)) == std::cv_status::timeout &&
+                al->state.load(std::memory_order_acquire) == kAggIssuing) {
+                waited_s += 5;
+                static const char *const where[] = {"taken, not yet launched", "in its k_rx launch",
+                                                    "recording its completion event"};
+                fprintf(stderr, "fcgpu: shared-queue launch not issued after %u s: the issuing thread is %s\n",
+                        waited_s, where[al->phase.load(std::memory_order_relaxed) % 3]);
+            }
+        }
     }
     hipError_t e = hipSuccess;
     if (st == kAggIssued) {
@@ -570,6 +597,56 @@ static hipError_t span_stream(fcgpu_ctx *c, uint32_t slot, hipStream_t *out) {
     return hipSuccess;
 }
 
+// Slot `slot`'s device blocks for block submissions through copies: an
+// input block of in_bytes (padded for the header-window over-read, zeroed)
+// and a result block for a full batch with these outputs. Replacing smaller
+// ones waits for the slot's stream first. Setup work: fcgpu_span_reserve runs
+// it for every slot; a submission only when no reservation was made.
+static int span_blocks(fcgpu_ctx *c, uint32_t slot, hipStream_t ss, size_t in_bytes, uint32_t outputs,
+                       uint32_t partition) {
+    SpanSlot &sp = c->span[slot];
+    fcgpu_block_layout M;    // room for a full batch with these outputs
+    if (fcgpu_block_layout_for(c, c->max_batch, outputs, partition, &M) != FCGPU_OK)
+        return fail(c, FCGPU_EINVAL, "bad block layout");
+    if (in_bytes + kArenaPad > sp.in_cap) {
+        HIPCHK(c, hipStreamSynchronize(ss));
+        hipFree(sp.d_in);
+        sp.d_in = nullptr;
+        sp.in_cap = 0;
+        const size_t cap = (in_bytes + kArenaPad + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+        HIPCHK(c, hipMalloc(&sp.d_in, cap));
+        HIPCHK(c, memset_sync(sp.d_in, 0, cap));
+        sp.in_cap = cap;
+    }
+    if (M.bytes > sp.res_cap) {
+        HIPCHK(c, hipStreamSynchronize(ss));
+        hipFree(sp.d_res);
+        sp.d_res = nullptr;
+        sp.res_cap = 0;
+        HIPCHK(c, hipMalloc(&sp.d_res, M.bytes));
+        sp.res_cap = M.bytes;
+    }
+    return FCGPU_OK;
+}
+
+int fcgpu_span_reserve(fcgpu_ctx *c, size_t in_bytes, uint32_t outputs, uint32_t partition) {
+    if (!c || partition > FCGPU_PART_TILE) return FCGPU_EINVAL;
+    outputs &= ~(FCGPU_SUBMIT_COPY | FCGPU_SUBMIT_DESC32);
+    if (in_bytes > 0xffffffffull - kArenaPad) return fail(c, FCGPU_EINVAL, "reservation larger than 4 GiB");
+    for (const SpanSlot &sp : c->span)
+        if (sp.busy) return fail(c, FCGPU_EINVAL, "fcgpu_span_reserve: a span slot is in flight");
+    HIPCHK(c, hipSetDevice(c->device));
+    for (uint32_t k = 0; k < FCGPU_SPAN_SLOTS; ++k) {
+        hipStream_t ss = nullptr;
+        HIPCHK(c, span_stream(c, k, &ss));
+        int rc = span_blocks(c, k, ss, in_bytes, outputs, partition);
+        if (rc != FCGPU_OK) return rc;
+        c->span[k].reserved = true;
+    }
+    if (c->fl.slots && !c->stream) HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    return FCGPU_OK;
+}
+
 int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_t in_bytes, size_t desc_off,
                             size_t frames_off, uint32_t n, void *h_out, uint32_t outputs, uint32_t partition) {
     if (!c || slot >= FCGPU_SPAN_SLOTS || (n && (!h_in || !h_out))) return FCGPU_EINVAL;
@@ -624,26 +701,13 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t slot, const void *h_in, size_
             sp.zc_hout = h_out;
             sp.zc_dout = static_cast<uint8_t *>(d);
         }
-    } else if (in_bytes + kArenaPad > sp.in_cap) {
-        HIPCHK(c, hipStreamSynchronize(ss));
-        hipFree(sp.d_in);
-        sp.d_in = nullptr;
-        sp.in_cap = 0;
-        const size_t cap = (in_bytes + kArenaPad + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
-        HIPCHK(c, hipMalloc(&sp.d_in, cap));
-        HIPCHK(c, memset_sync(sp.d_in, 0, cap));
-        sp.in_cap = cap;
-    }
-    if (!zc && L.bytes > sp.res_cap) {
-        HIPCHK(c, hipStreamSynchronize(ss));
-        hipFree(sp.d_res);
-        sp.d_res = nullptr;
-        sp.res_cap = 0;
-        fcgpu_block_layout M;    // room for a full batch with these outputs
-        fcgpu_block_layout_for(c, c->max_batch, outputs, partition, &M);
-        const size_t cap = std::max(M.bytes, L.bytes);
-        HIPCHK(c, hipMalloc(&sp.d_res, cap));
-        sp.res_cap = cap;
+    } else if (in_bytes + kArenaPad > sp.in_cap || L.bytes > sp.res_cap) {
+        // a reservation is never grown here: growing means freeing device
+        // memory (a device-wide wait) on a submitting thread
+        if (sp.reserved)
+            return fail(c, FCGPU_ENOMEM, "block larger than the fcgpu_span_reserve reservation");
+        int rc = span_blocks(c, slot, ss, in_bytes, outputs, partition);
+        if (rc != FCGPU_OK) return rc;
     }
     if (c->fl.slots && !c->stream) HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     sp.s = c->fl.slots ? c->stream : ss;

@@ -19,8 +19,8 @@ namespace {
 // Records every packet that leaves the element on one output, then frees it.
 class Sink : public Element {
   public:
-    Sink(int port, fcclick_result *r, uint32_t *seq, uint32_t *nbatch)
-        : _port(port), _r(r), _seq(seq), _nbatch(nbatch) {}
+    Sink(int port, fcclick_result *r, uint32_t *seq, uint32_t *nbatch, uint64_t *count = nullptr)
+        : _port(port), _r(r), _seq(seq), _nbatch(nbatch), _count(count) {}
     const char *class_name() const override { return "Sink"; }
     int configure(const std::vector<std::string> &, std::string &) override { return 0; }
     void push_batch(int, PacketBatch *b) override {
@@ -52,12 +52,14 @@ class Sink : public Element {
             p = nx;
         }
         if (cnt != b->count()) fprintf(stderr, "Sink: batch count %u != linked %u\n", b->count(), cnt);
+        if (_count) *_count += cnt;
     }
 
   private:
     int _port;
     fcclick_result *_r;
     uint32_t *_seq, *_nbatch;
+    uint64_t *_count;
 };
 
 // The harness floor: a BatchElement that forwards every PacketBatch to output
@@ -550,5 +552,68 @@ extern "C" int fcclick_bench_threads(const char *conf, const uint8_t *arena, con
     }
     const double s = std::chrono::duration<double>(e - b).count();
     if (pps) *pps = s > 0 ? (double)n * reps * threads / s : 0.0;
+    return 0;
+}
+
+extern "C" int fcclick_run_threads(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                                   uint32_t burst, uint32_t reps, uint32_t threads, uint32_t nsinks,
+                                   uint64_t *port_pkts, char *handlers, size_t handlers_cap, char *err,
+                                   size_t errcap) {
+    if (threads == 0 || !port_pkts || nsinks == 0) {
+        copy_err("threads, nsinks and port_pkts are required", err, errcap);
+        return -1;
+    }
+    if (burst == 0) burst = 32;
+    std::vector<std::string> es(threads), hs(threads);
+    std::vector<int> rc(threads, 0);
+    std::vector<std::thread> th;
+    StartLine line;
+    line.parties = threads;
+    for (uint32_t t = 0; t < threads; ++t)
+        th.emplace_back([&, t]() {
+            auto el = make_element(conf, es[t]);
+            if (!el || el->initialize(es[t]) < 0) {
+                rc[t] = -1;
+                line.arrive();
+                return;
+            }
+            uint32_t seq = 0, nbatch = 0;
+            uint64_t *cnt = port_pkts + (size_t)t * nsinks;
+            std::vector<std::unique_ptr<Sink>> sinks;
+            for (uint32_t k = 0; k < nsinks; ++k) {
+                cnt[k] = 0;
+                sinks.emplace_back(new Sink((int)k, nullptr, &seq, &nbatch, cnt + k));
+                el->connect_output((int)k, sinks.back().get(), 0);
+            }
+            const uint32_t headroom = 128;
+            PacketPool pool(std::max<uint32_t>(4096, el->max_held() + 4 * burst + 4096),
+                            headroom + max_len(desc, n) + 64, headroom);
+            line.arrive();                    // every thread's context exists: the run starts together
+            for (uint32_t r = 0; r < reps; ++r)
+                for (uint32_t i = 0; i < n; i += burst) {
+                    const uint32_t m = n - i < burst ? n - i : burst;
+                    if (pool.available() < m) el->flush();
+                    Packet *head = nullptr, *prev = nullptr;
+                    for (uint32_t j = 0; j < m; ++j) {
+                        Packet *p = pool.make(arena + desc[2 * (i + j)], desc[2 * (i + j) + 1]);
+                        if (prev) prev->set_next(p);
+                        else head = p;
+                        prev = p;
+                    }
+                    el->push_batch(0, PacketBatch::make_from_list(head, prev, m));
+                }
+            el->flush();
+            hs[t] = read_all(el.get());
+            el.reset();                       // before the pool its packets belong to
+        });
+    for (auto &x : th) x.join();
+    for (uint32_t t = 0; t < threads; ++t)
+        if (rc[t] < 0) {
+            copy_err(es[t], err, errcap);
+            return -1;
+        }
+    std::string all;
+    for (uint32_t t = 0; t < threads; ++t) all += hs[t] + "--\n";
+    if (handlers && handlers_cap) snprintf(handlers, handlers_cap, "%s", all.c_str());
     return 0;
 }

@@ -463,6 +463,12 @@ class RxCore {
         for (uint32_t k = 0; k < _nslots; ++k)
             if (!_slot[k].alloc(_cap, (size_t)_cap * per + 65536 + _lead, L.bytes))
                 return err(errh, "cannot allocate pinned staging (fcgpu_host_alloc)");
+        // the device blocks of every slot now, at the staging blocks' size: a
+        // submission through copies -- and a failed batch's re-submission
+        // while other threads' batches run on the shared queue -- then never
+        // allocates, frees or synchronises the device
+        if (fcgpu_span_reserve(_ctx, _slot[0].in_cap, _outputs, _partition) != FCGPU_OK)
+            return err(errh, std::string("fcgpu_span_reserve: ") + fcgpu_last_error(_ctx));
         return 0;
     }
 

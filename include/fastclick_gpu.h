@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 23
+#define FCGPU_ABI_VERSION 24
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -365,6 +365,18 @@ int  fcgpu_block_layout_for(const fcgpu_ctx *ctx, uint32_t n, uint32_t outputs, 
 int  fcgpu_span_submit_block(fcgpu_ctx *ctx, uint32_t slot, const void *h_in, size_t in_bytes,
                              size_t desc_off, size_t frames_off, uint32_t n, void *h_out, uint32_t outputs,
                              uint32_t partition);
+/* Reserve every slot's device blocks (an in_bytes input block, a result block
+ * for max_batch packets with these outputs) and streams now, on the calling
+ * thread, instead of on the first submissions that need them. After it,
+ * fcgpu_span_submit_block never allocates, frees or synchronises the device
+ * -- not on its copy path, not for an FCGPU_SUBMIT_COPY re-submission while
+ * other contexts' batches run on the device's shared queue -- and a block
+ * larger than in_bytes is refused (FCGPU_ENOMEM). Without it the first
+ * submission through copies sizes the blocks. Call it with no slot in flight
+ * (FCGPU_EINVAL otherwise); again to grow the reservation. (Round 6: an
+ * element's many threads must not grow device blocks while the shared queue
+ * runs) */
+int  fcgpu_span_reserve(fcgpu_ctx *ctx, size_t in_bytes, uint32_t outputs, uint32_t partition);
 
 /* How span and block submissions reach the device (per context, default COPY):
  *   FCGPU_SPAN_COPY     -- one H2D copy of h_in and one D2H copy of the

@@ -139,6 +139,17 @@ int fcclick_bench_threads(const char *conf, const uint8_t *arena, const uint32_t
                           uint32_t burst, uint32_t reps, uint32_t threads, double *pps, char *err,
                           size_t errcap);
 
+/* `threads` element instances (one GPU context each, as Click threads),
+ * set up first, then each pushing the trace `reps` times in BURST-packet
+ * PacketBatches and flushing, all at once. port_pkts[t * nsinks + k]: the
+ * packets thread t's output k received; handlers: every thread's handler
+ * dump (the fcclick_run format), each followed by a "--" line. What a
+ * multi-threaded run of the element must account for exactly (packets in =
+ * packets out + killed), e.g. with GPU faults injected mid-run. */
+int fcclick_run_threads(const char *conf, const uint8_t *arena, const uint32_t *desc, uint32_t n,
+                        uint32_t burst, uint32_t reps, uint32_t threads, uint32_t nsinks, uint64_t *port_pkts,
+                        char *handlers, size_t handlers_cap, char *err, size_t errcap);
+
 /* `threads` element instances pushing whole passes over the trace for
  * `seconds` (a source that keeps pushing, as the CPU baseline's threads do:
  * no thread's tail of a fixed packet count stretches the window): *pps = all

@@ -87,6 +87,7 @@ int fcgpu_block_layout_for(const fcgpu_ctx *c, uint32_t n, uint32_t outputs, uin
     L->bytes = (off + 255) & ~(size_t)255;
     return FCGPU_OK;
 }
+int fcgpu_span_reserve(fcgpu_ctx *, size_t, uint32_t, uint32_t) { return FCGPU_OK; }
 // every packet valid, on output 0, the tile partition the identity
 int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t, const void *h_in, size_t, size_t desc_off, size_t,
                             uint32_t n, void *h_out, uint32_t outputs, uint32_t partition) {

@@ -282,3 +282,36 @@ def test_gpu_malformed_jobs_refused(oracle):
         assert np.array_equal(got["reason"], exp["reason"]) and np.array_equal(got["port"], exp["port"])
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_element_retries_under_busy_shared_queue(oracle, no_faults):
+    """Sixteen element threads on the UDP chain share the GPU's zero-copy
+    queue (ZEROCOPY auto: FCGPU_SPAN_AUTO with >= 4 contexts). Six of that
+    queue's launches fail mid-run (fcgpu_inject_fault LAUNCH, after 40 good
+    ones), so their batches' owners re-submit them through copies
+    (FCGPU_SUBMIT_COPY) while the other threads keep the queue busy -- the
+    interleaving of round 5's hung staging experiment.
+    The device blocks those re-submissions use were reserved at initialize
+    (fcgpu_span_reserve), so none allocates or synchronises the device.
+    Every packet is accounted for: each thread's outputs received exactly the
+    oracle's per-output counts, every failed batch went through once more and
+    succeeded, and the run ends (the test's timeout)."""
+    from fastclick_amd import click as K
+    lib = no_faults
+    conf = "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, L4 UDP)"
+    b = synth.c3(65536, nflows=2000, seed=1541)
+    synth.set_udp_checksums(b)
+    synth.inject_errors(b, 0.03, seed=1542)
+    e = oracle.process_batch(K.element_cfg(conf), b)
+    per_port = np.bincount(e["port"].astype(np.int64), minlength=17)
+    assert per_port.sum() == b.n and per_port[16] > 0
+    threads, reps = 16, 4
+    lib.fcgpu_inject_fault(N.FAULT_LAUNCH, 40, 6)
+    pk, hs = K.run_element_threads(conf, b, threads=threads, reps=reps, nsinks=17)
+    retries = sum(int(h["gpu_retries"]) for h in hs)
+    assert retries >= 6, retries                          # each failed launch carried >= 1 batch
+    for t, h in enumerate(hs):
+        assert h["gpu_errors"] == "0" and h["error"] == "", (t, h)
+        assert np.array_equal(pk[t], per_port * reps), t
+        assert int(h["count"]) == int((e["reason"] == N.R_OK).sum()) * reps, t
