@@ -101,6 +101,7 @@ struct FlowArgs {
     uint32_t wmask;          // wheel buckets - 1
     uint32_t te;             // timeout in maintainer epochs
     uint32_t now;            // this batch's time (ms, fcgpu_flow_set_time)
+    uint32_t ls_mode;        // lastseen stamps (kLs*): per run, per run if the stored time differs, per packet
 };
 constexpr uint32_t kFsNext = 0;   // HMP: next flow ID; IMP: IDs out of the stack (max_flows - stack size)
 constexpr uint32_t kFsBase = 1;   // the ID base of the batch being finished (grid-wide finish)
@@ -117,6 +118,7 @@ struct MaintArgs {
     uint16_t *rbuf;          // [wstride] each walk entry's destination
     uint32_t now, to_ms, ri_ms, eps, seq;
 };
+constexpr uint32_t kLsRun = 0, kLsCheck = 1, kLsPacket = 2;   // FlowArgs::ls_mode
 constexpr uint32_t kFlowMiss = 0xfffffffdu;
 constexpr uint32_t kSlotNone = 0xffffffffu;
 
@@ -1177,10 +1179,22 @@ __device__ __forceinline__ void flow_resolve(const FlowArgs &F, FlowProbe &q, bo
             q.pos = (q.pos + 1) & F.mask;
             q.sl = F.slots[q.pos];
         }
-        // IMP with timeouts: a flow with a packet in the batch is stamped with
-        // the batch's time (virtualflowmanager.hh:236-239,311-313); new flows
-        // are stamped by their first packet in the new-flow pass
-        if (F.lastseen && id < kTagFull) F.lastseen[id] = F.now;
+    }
+    // IMP with timeouts: a flow with a packet in the batch is stamped with the
+    // batch's time once per run of its packets (kLsRun), as the reference's
+    // BatchBuilder stamps each run it pushes (update_lastseen at every run
+    // boundary, virtualflowmanager.hh:236-239,304-313): the first packet of
+    // a run of one flow in the wave stores (lane 0 always: a run crossing a
+    // wave boundary is stamped twice with the same time). With kLsCheck the
+    // stored time is read first and only a different one is written: one
+    // store per flow and batch instead of per run (tables small enough to
+    // stay in the caches). New flows are stamped by their first packet in
+    // the new-flow pass. (kLsPacket, every packet stamping, is round 5's way,
+    // kept for same-box A/B runs: FCGPU_LASTSEEN=packet.)
+    if (F.lastseen) {
+        const uint32_t prev = __shfl_up(id, 1);
+        const bool head = (threadIdx.x & 63) == 0 || prev != id || F.ls_mode == kLsPacket;
+        if (head && id < kTagFull && (F.ls_mode != kLsCheck || F.lastseen[id] != F.now)) F.lastseen[id] = F.now;
     }
     // The lookup only reads the table: a miss keeps its record (key, and the
     // empty slot its probe stopped at) at its packet index for the new-flow

@@ -175,6 +175,16 @@ int fcgpu_flow_configure(fcgpu_ctx *c, const fcgpu_flow_config *fc) {
         F.wstride = cap;
         F.wmask = nb - 1;
         F.te = te;
+        // lastseen stamps once per run of a flow's packets; read before they
+        // write while the array stays in the caches (<= 1 MiB: up to 256k
+        // flows). FCGPU_LASTSEEN=run|check|packet forces one way (same-box
+        // A/B runs)
+        F.ls_mode = (uint64_t)cap * 4u <= (1u << 20) ? kLsCheck : kLsRun;
+        if (const char *e = getenv("FCGPU_LASTSEEN")) {
+            if (!strcmp(e, "run")) F.ls_mode = kLsRun;
+            else if (!strcmp(e, "check")) F.ls_mode = kLsCheck;
+            else if (!strcmp(e, "packet")) F.ls_mode = kLsPacket;
+        }
         HIPCHK(c, hipMalloc(&F.lastseen, sizeof(uint32_t) * cap));
         HIPCHK(c, hipMalloc(&F.wheel, sizeof(uint32_t) * (size_t)nb * cap));
         HIPCHK(c, hipMalloc(&F.wheel_len, sizeof(uint32_t) * nb));
