@@ -54,7 +54,7 @@ struct DevCfg {
     uint32_t prog_kind;
     int32_t prog_all;         // >= 0: empty program, every packet -> this output
     const uint4 *crc_tab;     // FCGPU_CLS_LB_CRC: 2 x 256 u32 slicing tables (1 KB each)
-    const uint8_t *lb_tab;    // FCGPU_CLS_LB_TABLE: bucket -> output (>= kTabLdsBytes allocated)
+    const uint8_t *lb_tab;    // FCGPU_CLS_LB_TABLE: bucket -> output ((lb_tab_n + 15) & ~15 bytes, zero-padded)
     uint32_t lb_tab_n;        // buckets (<= 65536: the folded hash is < 2^16)
     uint32_t lb_tab_magic;    // ceil(2^32 / lb_tab_n) for lb_port's fastmod
 };

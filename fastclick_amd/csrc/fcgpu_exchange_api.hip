@@ -92,9 +92,20 @@ int fcgpu_exchange_build(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d
         return fail(c, FCGPU_EINVAL, "fcgpu_exchange_build: null buffer");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (!c->x_tcnt) {
-        HIPCHK(c, hipMalloc(&c->x_tcnt, sizeof(uint32_t) * (size_t)FCGPU_MAX_PORTS * c->max_tiles));
-        HIPCHK(c, hipMalloc(&c->x_tbyt, sizeof(unsigned long long) * (size_t)FCGPU_MAX_PORTS * c->max_tiles));
+    if (!c->x_tcnt || !c->x_tbyt) {
+        // both or neither: a failed allocation leaves none, so the next call
+        // allocates again instead of launching with a null one
+        hipError_t e = hipMalloc(&c->x_tcnt, sizeof(uint32_t) * (size_t)FCGPU_MAX_PORTS * c->max_tiles);
+        if (e == hipSuccess)
+            e = hipMalloc(&c->x_tbyt, sizeof(unsigned long long) * (size_t)FCGPU_MAX_PORTS * c->max_tiles);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            hipFree(c->x_tcnt);
+            hipFree(c->x_tbyt);
+            c->x_tcnt = nullptr;
+            c->x_tbyt = nullptr;
+            return fail(c, FCGPU_ENOMEM, std::string("fcgpu_exchange_build scratch: ") + hipGetErrorString(e));
+        }
     }
     XBuild B{};
     B.arena = d_arena;

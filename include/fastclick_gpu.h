@@ -728,7 +728,9 @@ int  fcgpu_exchange_unpack(fcgpu_ctx *ctx, const fcgpu_xmeta *d_meta, uint32_t n
  * slots fits in send_cap whenever it is at least the arena's frame bytes +
  * 15 per packet), so no host sync is needed before the call. Every per-packet
  * load is in input order (three launches: per-tile owner counts and bytes,
- * their scan per owner, the records and frames per tile). */
+ * their scan per owner, the records and frames per tile). The per-tile
+ * counts are one scratch per context: builds on one context must be
+ * serialised on one stream (as plan -> pack are). */
 int  fcgpu_exchange_build(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_desc,
                           const uint16_t *d_verdict, uint32_t n, uint32_t world, uint32_t rank,
                           fcgpu_xmeta *d_meta, uint32_t *d_seg_n, uint64_t *d_seg_bytes, uint8_t *d_send,
