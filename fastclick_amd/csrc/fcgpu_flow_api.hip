@@ -175,11 +175,11 @@ int fcgpu_flow_configure(fcgpu_ctx *c, const fcgpu_flow_config *fc) {
         F.wstride = cap;
         F.wmask = nb - 1;
         F.te = te;
-        // lastseen stamps once per run of a flow's packets; read before they
-        // write while the array stays in the caches (<= 1 MiB: up to 256k
-        // flows). FCGPU_LASTSEEN=run|check|packet forces one way (same-box
-        // A/B runs)
-        F.ls_mode = (uint64_t)cap * 4u <= (1u << 20) ? kLsCheck : kLsRun;
+        // lastseen stamps once per run of a flow's packets, read before they
+        // write (at 1 / 10k / 1M flows no slower than storing, 2.7 % faster at
+        // 10k, 2 % at 1M: profiles/r06_imp/summary.txt). FCGPU_LASTSEEN=
+        // run|check|packet forces one way (same-box A/B runs)
+        F.ls_mode = kLsCheck;
         if (const char *e = getenv("FCGPU_LASTSEEN")) {
             if (!strcmp(e, "run")) F.ls_mode = kLsRun;
             else if (!strcmp(e, "check")) F.ls_mode = kLsCheck;

@@ -65,7 +65,8 @@ struct AggQueue {
     std::mutex mu;
     int device = -1;
     std::vector<AggItem> pending;
-    hipStream_t st[4] = {};
+    hipStream_t st[4] = {};   // created by agg_issue (st_mu), never under mu
+    std::mutex st_mu;
     uint32_t rr = 0;
     std::vector<AggLaunch *> spare;
     // owners whose launch is still being issued by another thread sleep
@@ -122,7 +123,7 @@ struct AggIssue {
     uint32_t cm, tiles;
     bool ck;
     hipFunction_t fn;
-    hipStream_t st;
+    uint32_t si;              // the queue stream it goes on
     AggLaunch *al;
 };
 // Take every pending submission (q.mu held) as launches: the first one with
@@ -189,22 +190,15 @@ static void agg_take_locked(AggQueue &q, std::vector<AggIssue> &out) {
         a.ip_rw = J0.ip_rw;
         a.ctr = J0.ctr;
         a.layout = J0.layout;
-        const uint32_t si = q.rr++ % 4;
-        if (!q.st[si] && hipStreamCreateWithFlags(&q.st[si], hipStreamNonBlocking) != hipSuccess) {
-            (void)hipGetLastError();
-            q.st[si] = nullptr;
-        }
-        is.st = q.st[si];
+        // no HIP call under the queue's lock: the stream and a new launch's
+        // event are created by the issuing thread (agg_issue)
+        is.si = q.rr++ % 4;
         AggLaunch *al = nullptr;
         if (!q.spare.empty()) {
             al = q.spare.back();
             q.spare.pop_back();
         } else {
             al = new AggLaunch();
-            if (hipEventCreateWithFlags(&al->ev, hipEventDisableTiming) != hipSuccess) {
-                (void)hipGetLastError();
-                al->ev = nullptr;
-            }
         }
         al->state.store(kAggIssuing, std::memory_order_relaxed);
         al->phase.store(kAggPhaseTaken, std::memory_order_relaxed);
@@ -231,19 +225,32 @@ static void agg_issue(AggQueue &q, std::vector<AggIssue> &iss) {
     if (iss.empty()) return;
     const bool dev_ok = hipSetDevice(q.device) == hipSuccess;
     for (AggIssue &is : iss) {
-        hipError_t e = dev_ok && is.st && is.al->ev ? hipSuccess : hipErrorInvalidValue;
+        hipStream_t st = nullptr;
+        if (dev_ok) {
+            std::lock_guard<std::mutex> g(q.st_mu);
+            if (!q.st[is.si] && hipStreamCreateWithFlags(&q.st[is.si], hipStreamNonBlocking) != hipSuccess) {
+                (void)hipGetLastError();
+                q.st[is.si] = nullptr;
+            }
+            st = q.st[is.si];
+        }
+        if (dev_ok && !is.al->ev && hipEventCreateWithFlags(&is.al->ev, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            is.al->ev = nullptr;
+        }
+        hipError_t e = dev_ok && st && is.al->ev ? hipSuccess : hipErrorInvalidValue;
         if (e == hipSuccess && fault_take(FCGPU_FAULT_LAUNCH)) e = hipErrorLaunchFailure;
         is.al->phase.store(kAggPhaseLaunch, std::memory_order_relaxed);
         if (e == hipSuccess) {
             if (is.fn) {
-                e = launch_rx_fn(is.fn, is.part, is.L, is.tiles, is.st);
+                e = launch_rx_fn(is.fn, is.part, is.L, is.tiles, st);
             } else {
-                e = launch_rx_any(is.part, is.cm, is.ck, is.L, is.tiles, is.st, nullptr, nullptr, nullptr);
+                e = launch_rx_any(is.part, is.cm, is.ck, is.L, is.tiles, st, nullptr, nullptr, nullptr);
                 if (e == hipSuccess) e = hipGetLastError();
             }
         }
         is.al->phase.store(kAggPhaseRecord, std::memory_order_relaxed);
-        if (e == hipSuccess) e = hipEventRecord(is.al->ev, is.st);
+        if (e == hipSuccess) e = hipEventRecord(is.al->ev, st);
         if (e != hipSuccess) (void)hipGetLastError();
         is.al->state.store(e == hipSuccess ? kAggIssued : kAggFailed, std::memory_order_release);
     }
@@ -266,6 +273,7 @@ static void agg_release(int device) {
         q = it->second;
     }
     std::lock_guard<std::mutex> g(q->mu);
+    std::lock_guard<std::mutex> g2(q->st_mu);
     if (!q->pending.empty()) return;
     for (AggLaunch *al : q->spare) {
         if (al->ev) hipEventDestroy(al->ev);
