@@ -139,6 +139,15 @@ def parse(argv=None):
                          "then the FlowIPManagerHMP pass over the received batch; C4 (uniform 5-tuples, a "
                          "different batch per rank). Per-stage times and checked flow counts in "
                          "config.flow_reshard; a labelled variant, never the headline")
+    ap.add_argument("--reshard-exchange", choices=["fixed", "counted"], default="fixed",
+                    help="--flow-reshard: fixed = equal-split all-to-alls of fixed-capacity owner segments "
+                         "(fcgpu_exchange_build_fixed / _unpack_fixed, fcgpu_process_counted: no host sync "
+                         "per step; a step whose segments overflow stalls and is replayed through the counted "
+                         "exchange, config.flow_reshard.fallback_steps); counted = dist.exchange_built "
+                         "(one host sync per step for the split sizes)")
+    ap.add_argument("--reshard-slack", type=float, default=1.25,
+                    help="--flow-reshard fixed: an owner segment holds a uniform share of the batch x this "
+                         "(below 1, also at one rank: forces overflows, to exercise the replay)")
     ap.add_argument("--program-jit", type=int, default=1,
                     help="ipclass16: 1 = the program compiled to code (fcgpu_program_jit, hiprtc, before "
                          "the warmup); 0 = the step interpreter")
@@ -697,15 +706,103 @@ class ReshardProcessor:
         self.stage_ms = [0.0] * 5
         self.ev = None
         self.timed_steps = 0
+        # the fixed-capacity exchange: every buffer sized once, the step's
+        # counts stay on the device (received packets summed there too)
+        self.fixed = args.reshard_exchange == "fixed"
+        self.recv_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.fallback_steps = 0
+        self.step_id = 0
+        self.step_k = {}
+        if self.fixed:
+            from fastclick_amd import device as DV
+            from fastclick_amd.dist import ARENA_PAD
+            if args.reshard_slack < 1:      # forced overflows (also at one rank)
+                recs = max(1, int(n * args.reshard_slack))
+                segb = (max(16, int(self.send_cap * args.reshard_slack)) + 15) // 16 * 16
+            else:
+                recs, segb = DV.fixed_capacity(n, self.send_cap, self.world, args.reshard_slack)
+            self.recs, self.segb = recs, segb
+            W = self.world
+            self.fmeta = torch.empty((W * (recs + 1), 4), dtype=torch.int32, device=dev)
+            self.fsend = torch.zeros(W * segb + ARENA_PAD, dtype=torch.uint8, device=dev)
+            self.frmeta = torch.empty_like(self.fmeta) if W > 1 else None
+            self.frbuf = torch.zeros(W * segb + ARENA_PAD, dtype=torch.uint8, device=dev) if W > 1 else None
+            self.fdesc = torch.empty((W * recs, 2), dtype=torch.int32, device=dev)
+            self.fcount = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.fstall = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def _step(self, k, timed):
+        if self.fixed:
+            return self._step_fixed(k, timed)
+        return self._step_counted(k, timed)
+
+    def _step_fixed(self, k, timed):
+        """One step, no host sync: owner pass, fixed-capacity build, equal-split
+        all-to-alls, unpack (the received count stays on the device), the flow
+        pass over the bound with that count (fcgpu_process_counted)."""
+        import torch
+        from fastclick_amd import device as DV
+        from fastclick_amd.dist import exchange_fixed
+        a, d = self.bufs[k % len(self.bufs)]
+        s = torch.cuda.current_stream()
+        ev = self.ev[k - self.first] if timed and self.ev else None
+        if ev:
+            ev[0].record(s)
+        o = self.own_out
+        self.ctx_own.process(a.data_ptr(), d.data_ptr(), self.n, stream=s.cuda_stream, **o.ptrs())
+        if ev:
+            ev[1].record(s)
+        DV.exchange_build_fixed(self.ctx_own, a, d, o.verdict, self.world, self.rank, self.recs, self.segb,
+                                self.fmeta, self.fsend, stream=s)
+        if ev:
+            ev[2].record(s)
+        out = (self.frmeta, self.frbuf) if self.world > 1 else None
+        rmeta, rbuf = exchange_fixed(self.fmeta, self.fsend, self.recs, self.segb, out=out)
+        if ev:
+            ev[3].record(s)
+        self.step_id += 1
+        self.step_k[self.step_id] = (k, timed)
+        DV.exchange_unpack_fixed(self.ctx_own, rmeta, self.world, self.recs, self.segb, self.fdesc, self.fcount,
+                                 self.fstall, self.step_id, stream=s)
+        if ev:
+            ev[4].record(s)
+        f = self.flow_out
+        bound = self.world * self.recs
+        for c0 in range(0, bound, self.cap):
+            self.ctx_flow.process_counted(rbuf.data_ptr(), self.fdesc[c0:].data_ptr(), min(self.cap, bound - c0),
+                                          self.fcount.data_ptr(), c0, stream=s.cuda_stream, **f.ptrs())
+        if ev:
+            ev[5].record(s)
+        if timed:
+            self.recv_dev += self.fcount       # device-side: no sync
+
+    def _repair(self):
+        """The fixed exchange's stalled steps (a segment overflowed; every later
+        step stalled too): replayed in order through the counted exchange --
+        collective, so every rank replays from the earliest stalled step of any
+        rank, and processes a step's packets only from its own stalled step on.
+        One host read of the stall word (where the caller synchronises anyway)."""
+        if not self.fixed:
+            return
+        from fastclick_amd.dist import first_stalled
+        mine = int(self.fstall.item())
+        first = first_stalled(mine)
+        if first:
+            for sid in range(first, self.step_id + 1):
+                k, timed = self.step_k[sid]
+                self._step_counted(k, timed, process=bool(mine) and sid >= mine, replay=True)
+            self.fallback_steps += self.step_id + 1 - first
+            self.fstall.zero_()
+        self.step_k.clear()
+
+    def _step_counted(self, k, timed, process=True, replay=False):
         import torch
         from fastclick_amd import device as DV
         from fastclick_amd.dist import exchange_built
         N = self.N
         a, d = self.bufs[k % len(self.bufs)]
         s = torch.cuda.current_stream()
-        ev = self.ev[k - self.first] if timed and self.ev else None
+        ev = self.ev[k - self.first] if timed and self.ev and not replay else None
         if ev:
             ev[0].record(s)
         o = self.own_out
@@ -724,6 +821,8 @@ class ReshardProcessor:
         if ev:
             ev[4].record(s)
         f = self.flow_out
+        if not process:          # a replayed step this rank's table already took
+            m = 0
         for c0 in range(0, m, self.cap):
             k = min(self.cap, m - c0)
             self.ctx_flow.process(buf.data_ptr(), rdesc[c0:].data_ptr(), k, stream=s.cuda_stream, **f.ptrs())
@@ -735,6 +834,7 @@ class ReshardProcessor:
     def warmup(self, steps):
         for k in range(max(steps, 1)):
             self._step(k, False)
+        self._repair()
         self.torch.cuda.synchronize()
         self.ctx_flow.use_counters(self.ctr.data_ptr())      # timed steps count into the tensor
         # six markers per timed step, created here and read after the timed
@@ -746,6 +846,7 @@ class ReshardProcessor:
     def run_timed(self):
         for k in range(self.args.steps):
             self._step(self.first + k, True)
+        self._repair()           # inside the timed region: replays are work done
         self.timed_steps = self.args.steps
 
     def sync(self):
@@ -765,7 +866,8 @@ class ReshardProcessor:
         import torch
         import torch.distributed as dist
         dev = self.dev if backend == "nccl" else "cpu"
-        v = torch.tensor([self.ctx_flow.flow_count(), self.distinct, self.received,
+        received = self.received + int(self.recv_dev.item())
+        v = torch.tensor([self.ctx_flow.flow_count(), self.distinct, received,
                           self.n * self.timed_steps], dtype=torch.int64, device=dev)
         if self.world > 1:
             dist.all_reduce(v, op=dist.ReduceOp.SUM)
@@ -781,12 +883,16 @@ class ReshardProcessor:
                 for j in range(5):
                     self.stage_ms[j] += ev[j].elapsed_time(ev[j + 1])
         names = ("owner_pass", "build", "exchange", "unpack", "flow_pass")
+        fx = ({"exchange": "fixed", "seg_recs": self.recs, "seg_bytes": self.segb,
+               "slack": self.args.reshard_slack, "fallback_steps": self.fallback_steps}
+              if self.fixed else {"exchange": "counted"})
         return {"flow_table_flows": flows, "distinct_5tuples": distinct, "packets_received": received,
-                "packets_sent": sent, "checked": True,
+                "packets_sent": sent, "checked": True, **fx,
                 **({"stage_ms_per_step": {k: round(t / steps, 4) for k, t in zip(names, self.stage_ms)},
                     "stage_basis": "HIP events on the step's stream, read after the timed region (their "
-                                   "sum is below ms_per_step by the host's own work and the "
-                                   "exchange's host sync for the split sizes)"}
+                                   "sum is below ms_per_step by the host's own work"
+                                   + (")" if self.fixed else " and the exchange's host sync for the "
+                                      "split sizes)")}
                    if self.ev else {})}
 
     def close(self):

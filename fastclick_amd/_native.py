@@ -250,6 +250,13 @@ FCGPU_SYMBOLS = {
     "fcgpu_exchange_build": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
                                        C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                        C.c_void_p]),
+    "fcgpu_exchange_build_fixed": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                             C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, C.c_void_p,
+                                             C.c_void_p, C.c_void_p]),
+    "fcgpu_exchange_unpack_fixed": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64,
+                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "fcgpu_process_counted": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
+                                        C.POINTER(fcgpu_out), C.c_void_p]),
     "fcgpu_last_error": (C.c_char_p, [C.c_void_p]),
 }
 
@@ -403,6 +410,17 @@ class Context:
         self._chk(self.lib.fcgpu_process(self.h, arena_ptr, desc_ptr, n, C.byref(out),
                                          stream or None), "fcgpu_process")
 
+    def process_counted(self, arena_ptr, desc_ptr, n_max, count_ptr, base=0, *, verdict=0, hash=0, anno=0,
+                        perm=0, port_start=0, tile_count=0, partition=PART_TILE, tile_perm=0, flowid=0, ip_rw=0,
+                        stream=0):
+        """fcgpu_process_counted: the first *count_ptr - base packets (a device word) of
+        at most n_max; the launch covers n_max, nothing is read back to the host."""
+        out = fcgpu_out(verdict or None, hash or None, anno or None, perm or None, port_start or None,
+                        tile_count or None,
+                        partition, 0, tile_perm or None, flowid or None, ip_rw or None)
+        self._chk(self.lib.fcgpu_process_counted(self.h, arena_ptr, desc_ptr, n_max, count_ptr, base,
+                                                 C.byref(out), stream or None), "fcgpu_process_counted")
+
     def jobs(self, specs):
         """Prepare an fcgpu_job array from (arena_ptr, desc_ptr, n, stream, outputs-dict)
         tuples; run it with run_jobs (no per-job Python work on the launch path)."""
@@ -552,6 +570,19 @@ class Context:
         self._chk(self.lib.fcgpu_exchange_build(self.h, arena, desc, verdict, n, world, rank, meta, seg_n,
                                                 seg_bytes, send or None, send_cap, stream or None),
                   "fcgpu_exchange_build")
+
+    def exchange_build_fixed(self, arena, desc, verdict, n, world, rank, seg_recs, seg_bytes, meta, send,
+                             stream=0):
+        """fcgpu_exchange_build_fixed on device pointers: every owner's segment at its
+        fixed place (header + seg_recs records; seg_bytes frame bytes)."""
+        self._chk(self.lib.fcgpu_exchange_build_fixed(self.h, arena, desc, verdict, n, world, rank, seg_recs,
+                                                      seg_bytes, meta, send, stream or None),
+                  "fcgpu_exchange_build_fixed")
+
+    def exchange_unpack_fixed(self, rmeta, world, seg_recs, seg_bytes, desc, count, stall, step, stream=0):
+        """fcgpu_exchange_unpack_fixed: received fixed segments -> descriptors, *count, *stall."""
+        self._chk(self.lib.fcgpu_exchange_unpack_fixed(self.h, rmeta, world, seg_recs, seg_bytes, desc, count,
+                                                       stall, step, stream or None), "fcgpu_exchange_unpack_fixed")
 
     def exchange_unpack(self, meta, n, src_displ, desc, stream=0):
         """fcgpu_exchange_unpack: received records -> descriptors (src_displ: per-source segment starts)."""

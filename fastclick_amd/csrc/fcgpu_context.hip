@@ -164,6 +164,8 @@ void fcgpu_close(fcgpu_ctx *c) {
         hipFree(c->x_src);
         hipFree(c->x_tcnt);
         hipFree(c->x_tbyt);
+        hipFree(c->x_segn);
+        hipFree(c->x_segb);
         pool_release(c);
         for (auto e : c->flow_order)
             if (e) hipEventDestroy(e);

@@ -147,6 +147,11 @@ struct RxArgs {
     FlowArgs fl;               // FLOW instances only
     uint32_t *ip_rw;           // [n] rewritten IP header bytes 8..11 (cfg.rewrite)
     uint32_t layout;           // kLay* bits: how desc and anno are laid out
+    // a count on the device (fcgpu_process_counted, one batch per launch):
+    // packets i >= *n_dev - n_base are not processed (n is then the bound the
+    // grid covers); null: all n are
+    const uint32_t *n_dev;
+    uint32_t n_base;
     DevCfg cfg;
 };
 
@@ -1169,7 +1174,7 @@ __device__ __forceinline__ FlowProbe flow_issue(const FlowArgs &F, const FrameVi
     }
     return q;
 }
-__device__ __forceinline__ void flow_resolve(const FlowArgs &F, FlowProbe &q, bool live, uint32_t i) {
+__device__ __forceinline__ void flow_resolve(const FlowArgs &F, FlowProbe &q, bool live, uint32_t i, bool word) {
     uint32_t id = FCGPU_FLOW_NONE;
     if (q.want) {
         id = kFlowMiss;
@@ -1199,12 +1204,14 @@ __device__ __forceinline__ void flow_resolve(const FlowArgs &F, FlowProbe &q, bo
     // The lookup only reads the table: a miss keeps its record (key, and the
     // empty slot its probe stopped at) at its packet index for the new-flow
     // pass, which looks it up again and places it in batch order
-    // (fcgpu_flow.hh). The wave writes its 64-bit miss word, and a wave with
-    // misses stamps the batch's epoch -- plain stores: only the next launch
+    // (fcgpu_flow.hh). The wave writes its 64-bit miss word (also a wave with
+    // no live lane inside a counted launch's bound: `word`, so the new-flow
+    // pass over the bound reads no stale word), and a wave with misses stamps
+    // the batch's epoch -- plain stores: only the next launch
     // reads them. (An atomic on one miss counter per wave with misses
     // serialised at ~30 ns each at the memory: 10k misses cost 300 us.)
     const uint64_t mm = __ballot(id == kFlowMiss), lv = __ballot(live);
-    if ((threadIdx.x & 63) == 0 && lv) {
+    if ((threadIdx.x & 63) == 0 && (lv || word)) {
         F.missmask[i >> 6] = mm;
         if (mm) *F.missed = F.epoch;
     }
@@ -1430,7 +1437,7 @@ __device__ __forceinline__ void rx_tile(const RxArgs &A, const RxView &V, const 
             if (V.tile_perm) st_nt(V.tile_perm + pos, (uint8_t)threadIdx.x);
         }
     }
-    if (FLOW) flow_resolve(FL, fq, live, i);
+    if (FLOW) flow_resolve(FL, fq, live, i, A.n_dev != nullptr && (i & ~63u) < A.n);
     // counters: one atomic per non-zero bin per tile, sharded by tile. "count"
     // and "drops" are not kept here: both follow from these bins on read
     // (fcgpu_counters_derive), which saves an atomic per tile (-0.4 us / 1M).
@@ -1530,6 +1537,10 @@ __global__ __launch_bounds__(kTile, 8) void k_rx(RxLaunch L) {
             FL.flowid = J.flowid;
             FL.epoch += j;
         }
+    }
+    if (A.n_dev) {   // counted launch (one batch): the live packets are the first *n_dev - n_base
+        const uint32_t c = *A.n_dev;
+        V.n = c > A.n_base ? (c - A.n_base < V.n ? c - A.n_base : V.n) : 0u;
     }
     const uint32_t i = tile * kTile + threadIdx.x;
     uint2 d = make_uint2(0, 0);

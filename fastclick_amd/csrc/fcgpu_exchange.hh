@@ -412,6 +412,12 @@ struct XBuild {
     uint4 *meta;                    // fcgpu_xmeta [m] (dword-aligned)
     uint8_t *send;
     unsigned long long send_cap;
+    // fixed-capacity layout (fcgpu_exchange_build_fixed; 0: the counted one):
+    // owner d's segment holds a header record and fix_recs records at meta
+    // + d (fix_recs + 1), fix_bytes frame bytes at send + d fix_bytes; an
+    // owner whose packets do not fit gets its header alone (overflow flag)
+    uint32_t fix_recs;
+    unsigned long long fix_bytes;
 };
 
 // inclusive scan of x over the 64 lanes of a wave
@@ -567,6 +573,9 @@ __global__ __launch_bounds__(1024) void k_xbscan(XBuild B) {
     if (threadIdx.x == 0) {
         B.seg_n[d] = ct;
         B.seg_bytes[d] = bt;
+        if (B.fix_recs)      // the segment's header (fcgpu_xseg): packets, bytes, overflow
+            *reinterpret_cast<xu4 *>(B.meta + (size_t)d * (B.fix_recs + 1)) =
+                xu4{ct, (uint32_t)bt, (uint32_t)(bt >> 32), (ct > B.fix_recs || bt > B.fix_bytes) ? 1u : 0u};
     }
 }
 
@@ -599,19 +608,22 @@ __global__ __launch_bounds__(kXTile) void k_xbuild(XBuild B) {
             if (lane >= (uint32_t)o) bi += u;
         }
         if (lane < B.world) {
-            s_nbase[lane] = ci - c;
-            s_bbase[lane] = bi - b;
+            s_nbase[lane] = B.fix_recs ? lane * (B.fix_recs + 1) + 1 : ci - c;
+            s_bbase[lane] = B.fix_recs ? lane * B.fix_bytes : bi - b;
         }
-        const uint64_t big = __ballot(lane < B.world && b > 0xffffffffull);
+        // owners not packed: a segment of 4 GiB or more, or (fixed layout)
+        // one that does not fit its capacity -- header only
+        const bool over = B.fix_recs && (c > B.fix_recs || b > B.fix_bytes);
+        const uint64_t big = __ballot(lane < B.world && (b > 0xffffffffull || over));
         if (lane == 0) s_big = big;
     }
     uint32_t own, len, src, pos, intra;
     xtile_sort(B, t, L, own, len, src, pos, intra);      // its barriers publish the bases too
     const uint32_t i = t * kXTile + threadIdx.x;
     if (own < B.world) {
-        const uint32_t j = s_nbase[own] + s_tc[own] + (pos - L.tstart[own]);
+        const uint32_t j = ((s_big >> own) & 1ull) ? ~0u : s_nbase[own] + s_tc[own] + (pos - L.tstart[own]);
         const uint64_t off = s_tb[own] + intra;
-        *reinterpret_cast<xu4 *>(B.meta + j) = xu4{(uint32_t)off, len, i, B.rank};
+        if (j != ~0u) *reinterpret_cast<xu4 *>(B.meta + j) = xu4{(uint32_t)off, len, i, B.rank};
         s_src[pos] = src;
         s_len[pos] = len;
         s_dst[pos] = ((s_big >> own) & 1ull) ? ~0ull : s_bbase[own] + off;
@@ -697,6 +709,62 @@ __global__ __launch_bounds__(kXThreads) void k_xunpack(XUnpack U) {
     const unsigned long long off = ok ? U.displ[r.w] + r.x : 0ull;
     U.desc[2 * (size_t)j] = (uint32_t)off;
     U.desc[2 * (size_t)j + 1] = ok ? r.y : 0u;
+}
+
+// The receive side of the fixed-capacity layout (fcgpu_exchange_unpack_fixed):
+// source s's segment (header + records, frames at s x bytes) in place after
+// the equal-split all-to-all. Block (c, s): records c*256 .. of source s ->
+// descriptors at the exclusive prefix of the sources' packet counts, so the
+// list is in (source rank, source order) as the counted exchange's. *count =
+// the packets received; 0, with *stall = step (if it was 0), when any
+// segment overflowed or an earlier step already stalled -- the flow pass
+// that follows then processes nothing and the host replays the stalled steps
+// through the counted exchange, in order (fastclick_amd.dist).
+struct XUnpackFixed {
+    const uint4 *meta;
+    uint32_t *desc;
+    uint32_t world, recs;
+    unsigned long long bytes;
+    uint32_t *count;
+    uint32_t *stall;
+    uint32_t step;
+};
+__global__ __launch_bounds__(kXThreads) void k_xunpack_fixed(XUnpackFixed U) {
+    __shared__ uint32_t s_pre[FCGPU_MAX_PORTS + 1];
+    __shared__ uint32_t s_bad;
+    const uint32_t lane = threadIdx.x & 63;
+    if (threadIdx.x < 64) {
+        uint32_t c = 0;
+        bool bad = false;
+        if (lane < U.world) {
+            const xu4 h = *reinterpret_cast<const xu4 *>(U.meta + (size_t)lane * (U.recs + 1));
+            const uint64_t b = (uint64_t)h.z << 32 | h.y;
+            bad = (h.w & 1u) || h.x > U.recs || b > U.bytes;
+            c = bad ? 0u : h.x;
+        }
+        const uint32_t inc = xwave_incl(c);
+        if (lane < U.world) s_pre[lane] = inc - c;
+        if (lane == 63) s_pre[U.world] = inc;
+        const bool any = __ballot(bad) != 0ull;
+        if (lane == 0) s_bad = (any || *U.stall != 0u) ? 1u : 0u;
+    }
+    __syncthreads();
+    const uint32_t s = blockIdx.y;
+    if (s_bad) {
+        if (blockIdx.x == 0 && s == 0 && threadIdx.x == 0) {
+            *U.count = 0u;
+            if (*U.stall == 0u) *U.stall = U.step;
+        }
+        return;
+    }
+    if (blockIdx.x == 0 && s == 0 && threadIdx.x == 0) *U.count = s_pre[U.world];
+    const uint32_t k = blockIdx.x * kXThreads + threadIdx.x;
+    const uint32_t ns = s_pre[s + 1] - s_pre[s];
+    if (k >= ns) return;
+    const xu4 r = *reinterpret_cast<const xu4 *>(U.meta + (size_t)s * (U.recs + 1) + 1 + k);
+    const size_t j = (size_t)s_pre[s] + k;
+    U.desc[2 * j] = (uint32_t)(s * U.bytes + r.x);
+    U.desc[2 * j + 1] = r.y;
 }
 
 }  // namespace fcgpu

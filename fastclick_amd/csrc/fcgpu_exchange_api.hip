@@ -82,6 +82,41 @@ int fcgpu_exchange_pack(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_
     return FCGPU_OK;
 }
 
+// The build's per-tile scratch ([64][max_tiles] counts and bytes) and the
+// per-owner totals: allocated together on first use, or not at all (a failed
+// allocation leaves none, so the next call allocates again instead of
+// launching with a null one).
+static int xbuild_scratch(fcgpu_ctx *c) {
+    if (c->x_tcnt && c->x_tbyt && c->x_segn && c->x_segb) return FCGPU_OK;
+    hipError_t e = hipMalloc(&c->x_tcnt, sizeof(uint32_t) * (size_t)FCGPU_MAX_PORTS * c->max_tiles);
+    if (e == hipSuccess)
+        e = hipMalloc(&c->x_tbyt, sizeof(unsigned long long) * (size_t)FCGPU_MAX_PORTS * c->max_tiles);
+    if (e == hipSuccess) e = hipMalloc(&c->x_segn, sizeof(uint32_t) * FCGPU_MAX_PORTS);
+    if (e == hipSuccess) e = hipMalloc(&c->x_segb, sizeof(unsigned long long) * FCGPU_MAX_PORTS);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        for (void *p : {(void *)c->x_tcnt, (void *)c->x_tbyt, (void *)c->x_segn, (void *)c->x_segb}) hipFree(p);
+        c->x_tcnt = nullptr;
+        c->x_tbyt = nullptr;
+        c->x_segn = nullptr;
+        c->x_segb = nullptr;
+        return fail(c, FCGPU_ENOMEM, std::string("fcgpu_exchange_build scratch: ") + hipGetErrorString(e));
+    }
+    return FCGPU_OK;
+}
+
+// k_xbtile -> k_xbscan -> k_xbuild over B (counted or fixed layout).
+static int xbuild_launch(fcgpu_ctx *c, XBuild &B, hipStream_t s) {
+    B.ntiles = (B.n + kXTile - 1) / kXTile;
+    B.tcnt = c->x_tcnt;
+    B.tbyt = c->x_tbyt;
+    if (B.ntiles) hipLaunchKernelGGL(k_xbtile, dim3(B.ntiles), dim3(kXTile), 0, s, B);
+    hipLaunchKernelGGL(k_xbscan, dim3(B.world), dim3(1024), 0, s, B);    // n = 0: zero counts
+    if (B.ntiles) hipLaunchKernelGGL(k_xbuild, dim3(B.ntiles), dim3(kXTile), 0, s, B);   // lanes per frame: per tile
+    HIPCHK(c, hipGetLastError());
+    return FCGPU_OK;
+}
+
 int fcgpu_exchange_build(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, const uint16_t *d_verdict,
                          uint32_t n, uint32_t world, uint32_t rank, fcgpu_xmeta *d_meta, uint32_t *d_seg_n,
                          uint64_t *d_seg_bytes, uint8_t *d_send, uint64_t send_cap, void *stream) {
@@ -91,40 +126,80 @@ int fcgpu_exchange_build(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d
     if (!d_seg_n || !d_seg_bytes || (n && (!d_arena || !d_desc || !d_verdict || !d_meta || (send_cap && !d_send))))
         return fail(c, FCGPU_EINVAL, "fcgpu_exchange_build: null buffer");
     HIPCHK(c, hipSetDevice(c->device));
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    if (!c->x_tcnt || !c->x_tbyt) {
-        // both or neither: a failed allocation leaves none, so the next call
-        // allocates again instead of launching with a null one
-        hipError_t e = hipMalloc(&c->x_tcnt, sizeof(uint32_t) * (size_t)FCGPU_MAX_PORTS * c->max_tiles);
-        if (e == hipSuccess)
-            e = hipMalloc(&c->x_tbyt, sizeof(unsigned long long) * (size_t)FCGPU_MAX_PORTS * c->max_tiles);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            hipFree(c->x_tcnt);
-            hipFree(c->x_tbyt);
-            c->x_tcnt = nullptr;
-            c->x_tbyt = nullptr;
-            return fail(c, FCGPU_ENOMEM, std::string("fcgpu_exchange_build scratch: ") + hipGetErrorString(e));
-        }
-    }
+    int rc = xbuild_scratch(c);
+    if (rc != FCGPU_OK) return rc;
     XBuild B{};
     B.arena = d_arena;
     B.desc = d_desc;
     B.verdict = d_verdict;
     B.n = n;
-    B.ntiles = (n + kXTile - 1) / kXTile;
     B.world = world;
     B.rank = rank;
-    B.tcnt = c->x_tcnt;
-    B.tbyt = c->x_tbyt;
     B.seg_n = d_seg_n;
     B.seg_bytes = reinterpret_cast<unsigned long long *>(d_seg_bytes);
     B.meta = reinterpret_cast<uint4 *>(d_meta);
     B.send = d_send;
     B.send_cap = send_cap;
-    if (B.ntiles) hipLaunchKernelGGL(k_xbtile, dim3(B.ntiles), dim3(kXTile), 0, s, B);
-    hipLaunchKernelGGL(k_xbscan, dim3(world), dim3(1024), 0, s, B);    // n = 0: zero counts
-    if (B.ntiles) hipLaunchKernelGGL(k_xbuild, dim3(B.ntiles), dim3(kXTile), 0, s, B);   // lanes per frame: per tile
+    return xbuild_launch(c, B, static_cast<hipStream_t>(stream));
+}
+
+int fcgpu_exchange_build_fixed(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc,
+                               const uint16_t *d_verdict, uint32_t n, uint32_t world, uint32_t rank,
+                               uint32_t seg_recs, uint64_t seg_bytes, fcgpu_xmeta *d_meta, uint8_t *d_send,
+                               void *stream) {
+    if (!c) return FCGPU_EINVAL;
+    if (world == 0 || world > FCGPU_MAX_PORTS)
+        return fail(c, FCGPU_EINVAL, "fcgpu_exchange_build_fixed: world must be 1..64");
+    if (n > c->max_batch)
+        return fail(c, FCGPU_ENOMEM, "fcgpu_exchange_build_fixed: batch larger than the context's max_batch");
+    if (seg_recs == 0 || seg_recs > 0x7fffffffu / world || seg_bytes == 0 || (seg_bytes & 15) ||
+        (uint64_t)world * seg_bytes > 0xffffffffull - 256)
+        return fail(c, FCGPU_EINVAL, "fcgpu_exchange_build_fixed: capacities (seg_bytes a multiple of 16, "
+                                     "world x seg_bytes below 4 GiB)");
+    if (!d_meta || !d_send || (n && (!d_arena || !d_desc || !d_verdict)))
+        return fail(c, FCGPU_EINVAL, "fcgpu_exchange_build_fixed: null buffer");
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = xbuild_scratch(c);
+    if (rc != FCGPU_OK) return rc;
+    XBuild B{};
+    B.arena = d_arena;
+    B.desc = d_desc;
+    B.verdict = d_verdict;
+    B.n = n;
+    B.world = world;
+    B.rank = rank;
+    B.seg_n = c->x_segn;
+    B.seg_bytes = c->x_segb;
+    B.meta = reinterpret_cast<uint4 *>(d_meta);
+    B.send = d_send;
+    B.send_cap = (uint64_t)world * seg_bytes;
+    B.fix_recs = seg_recs;
+    B.fix_bytes = seg_bytes;
+    return xbuild_launch(c, B, static_cast<hipStream_t>(stream));
+}
+
+int fcgpu_exchange_unpack_fixed(fcgpu_ctx *c, const fcgpu_xmeta *d_rmeta, uint32_t world, uint32_t seg_recs,
+                                uint64_t seg_bytes, uint32_t *d_desc, uint32_t *d_count, uint32_t *d_stall,
+                                uint32_t step, void *stream) {
+    if (!c) return FCGPU_EINVAL;
+    if (world == 0 || world > FCGPU_MAX_PORTS)
+        return fail(c, FCGPU_EINVAL, "fcgpu_exchange_unpack_fixed: world must be 1..64");
+    if (seg_recs == 0 || seg_recs > 0x7fffffffu / world || (uint64_t)world * seg_bytes > 0xffffffffull - 256)
+        return fail(c, FCGPU_EINVAL, "fcgpu_exchange_unpack_fixed: capacities");
+    if (!d_rmeta || !d_desc || !d_count || !d_stall || step == 0)
+        return fail(c, FCGPU_EINVAL, "fcgpu_exchange_unpack_fixed: null buffer or step 0");
+    HIPCHK(c, hipSetDevice(c->device));
+    XUnpackFixed U{};
+    U.meta = reinterpret_cast<const uint4 *>(d_rmeta);
+    U.desc = d_desc;
+    U.world = world;
+    U.recs = seg_recs;
+    U.bytes = seg_bytes;
+    U.count = d_count;
+    U.stall = d_stall;
+    U.step = step;
+    hipLaunchKernelGGL(k_xunpack_fixed, dim3((seg_recs + kXThreads - 1) / kXThreads, world), dim3(kXThreads), 0,
+                       static_cast<hipStream_t>(stream), U);
     HIPCHK(c, hipGetLastError());
     return FCGPU_OK;
 }

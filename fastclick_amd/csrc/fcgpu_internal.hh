@@ -280,6 +280,8 @@ struct fcgpu_ctx {
     uint32_t *x_src = nullptr;   // arena offset of each leaving frame (plan -> pack)
     uint32_t *x_tcnt = nullptr;               // fcgpu_exchange_build: [64][max_tiles] per tile and owner
     unsigned long long *x_tbyt = nullptr;
+    uint32_t *x_segn = nullptr;               // fcgpu_exchange_build_fixed: per-owner totals (scratch)
+    unsigned long long *x_segb = nullptr;
     std::string err;
 };
 
@@ -314,8 +316,10 @@ hipError_t launch_rx_fn(hipFunction_t fn, int part, const RxLaunch &L, uint32_t 
 
 // ---- fcgpu_process.hip ------------------------------------------------------
 int check_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, uint32_t n, const fcgpu_out *o);
+// n_dev: a counted batch (fcgpu_process_counted): n is the bound, the packets
+// processed the first *n_dev - n_base
 int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, uint32_t n, const fcgpu_out *o,
-                hipStream_t s, uint32_t layout = 0);
+                hipStream_t s, uint32_t layout = 0, const uint32_t *n_dev = nullptr, uint32_t n_base = 0);
 int out_part(const fcgpu_out *o);
 void pool_release(fcgpu_ctx *c);
 

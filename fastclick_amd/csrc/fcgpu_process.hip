@@ -40,7 +40,7 @@ int check_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
 // layout: kLay* bits of the batch's descriptors and annotations (0 through
 // the public entry points: {off, len} descriptors, fcgpu_anno).
 int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, uint32_t n,
-                       const fcgpu_out *o, hipStream_t s, uint32_t layout) {
+                       const fcgpu_out *o, hipStream_t s, uint32_t layout, const uint32_t *n_dev, uint32_t n_base) {
     if (n == 0) return FCGPU_OK;
     const uint32_t ntiles = (n + kTile - 1) / kTile;
     const uint32_t nports = c->cfg.nports;
@@ -77,6 +77,8 @@ int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, ui
     }
     a.ip_rw = o->ip_rw;
     a.layout = layout;
+    a.n_dev = n_dev;
+    a.n_base = n_base;
 
     // sampled timing: the timing_every-th, 2*timing_every-th, ... launch since
     // fcgpu_set_timing (not the first: a start event ahead of an idle queue's
@@ -627,6 +629,19 @@ int fcgpu_process(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, 
     if (rc != FCGPU_OK || n == 0) return rc;
     HIPCHK(c, hipSetDevice(c->device));
     return process_one(c, d_arena, d_desc, n, o, (hipStream_t)stream);   // NULL = the null stream
+}
+
+int fcgpu_process_counted(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, uint32_t n_max,
+                          const uint32_t *d_count, uint32_t base, const fcgpu_out *o, void *stream) {
+    if (!c || !o) return FCGPU_EINVAL;
+    if (!d_count) return fail(c, FCGPU_EINVAL, "fcgpu_process_counted: null count");
+    // the whole-batch partition's scan and scatter take the host's n
+    if (o->partition == FCGPU_PART_GLOBAL && (o->perm || o->port_start))
+        return fail(c, FCGPU_EINVAL, "fcgpu_process_counted: no whole-batch partition (FCGPU_PART_GLOBAL)");
+    int rc = check_process(c, d_arena, d_desc, n_max, o);
+    if (rc != FCGPU_OK || n_max == 0) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    return process_one(c, d_arena, d_desc, n_max, o, (hipStream_t)stream, 0, d_count, base);
 }
 
 int fcgpu_process_jobs(fcgpu_ctx *c, const fcgpu_job *jobs, uint32_t njobs, void *stream) {

@@ -217,3 +217,40 @@ def exchange_unpack(ctx: N.Context, meta, src_displ, stream=None):
     desc = torch.empty((max(k, 1), 2), dtype=torch.int32, device=meta.device)
     ctx.exchange_unpack(meta.data_ptr() if k else 0, k, src_displ, desc.data_ptr(), stream=s.cuda_stream)
     return desc[:k]
+
+
+# ---- the fixed-capacity re-shard (no host sync per step) -------------------
+
+def fixed_capacity(n: int, send_cap: int, world: int, slack: float = 1.25):
+    """Per-owner capacities of the fixed-capacity exchange (fcgpu_exchange_build_fixed):
+    a uniform owner's share of the batch's n packets and send_cap slot bytes
+    (the arena's bytes + 16 per packet bound them) times `slack`, plus a floor
+    (256 packets, 64 KiB), never more than the whole batch. World 1: the
+    whole batch, so a segment cannot overflow. Returns (seg_recs, seg_bytes)."""
+    if world <= 1:
+        return max(n, 1), (max(send_cap, 16) + 15) // 16 * 16
+    recs = min(max(n, 1), int(n / world * slack) + 256)
+    nbytes = min(max(send_cap, 16), int(send_cap / world * slack) + (64 << 10))
+    return recs, (nbytes + 15) // 16 * 16
+
+
+def exchange_build_fixed(ctx: N.Context, arena, desc, verdict, world, rank, seg_recs, seg_bytes, meta, send,
+                         stream=None):
+    """fcgpu_exchange_build_fixed into preallocated device buffers: meta int32
+    [world * (seg_recs + 1), 4] (each owner's header + records), send uint8
+    [world * seg_bytes + ARENA_PAD]. No host sync."""
+    torch = _torch()
+    n = int(desc.shape[0])
+    s = stream if stream is not None else torch.cuda.current_stream()
+    ctx.exchange_build_fixed(arena.data_ptr(), desc.data_ptr(), verdict.data_ptr(), n, world, rank, seg_recs,
+                             seg_bytes, meta.data_ptr(), send.data_ptr(), stream=s.cuda_stream)
+
+
+def exchange_unpack_fixed(ctx: N.Context, rmeta, world, seg_recs, seg_bytes, desc, count, stall, step,
+                          stream=None):
+    """fcgpu_exchange_unpack_fixed: the received segments -> desc int32 [world *
+    seg_recs, 2] (the first *count rows), count / stall int32 [1] device words."""
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    ctx.exchange_unpack_fixed(rmeta.data_ptr(), world, seg_recs, seg_bytes, desc.data_ptr(), count.data_ptr(),
+                              stall.data_ptr(), step, stream=s.cuda_stream)

@@ -174,6 +174,57 @@ def exchange_built(send, meta, seg_n, seg_bytes, group=None):
     return buf, rmeta, displ
 
 
+def exchange_fixed(meta, send, seg_recs, seg_bytes, group=None, out=None):
+    """The all-to-alls of the fixed-capacity re-shard (fcgpu_exchange_build_fixed):
+    meta int32 [world * (seg_recs + 1), 4] and send uint8 [world * seg_bytes
+    (+ pad)] go out with equal splits -- owner d's segment to rank d -- so no
+    split size is read on the host and the step never waits for the device.
+    Returns (rmeta, rbuf): source s's segment at s, rbuf followed by ARENA_PAD
+    zero bytes (out: preallocated (rmeta, rbuf) to receive into). World 1: the
+    send side is the received one (no collective; send's pad must be zero)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    rows, nb = world * (seg_recs + 1), world * seg_bytes
+    if meta.shape[0] < rows or send.numel() < nb:
+        raise ValueError(f"exchange_fixed: {meta.shape[0]} rows / {send.numel()} B for a world of {world}")
+    if world == 1:
+        return meta, send
+    if send.is_cuda and dist.get_backend(group) == "gloo":
+        # a rehearsal of several ranks on one GPU: gloo's all-to-all takes host tensors
+        rm, rb = exchange_fixed(meta[:rows].cpu(), send[:nb].cpu(), seg_recs, seg_bytes, group=group)
+        return rm.to(meta.device), rb.to(send.device)
+    if out is None:
+        rmeta = torch.empty((rows, 4), dtype=meta.dtype, device=meta.device)
+        rbuf = torch.empty(nb + ARENA_PAD, dtype=torch.uint8, device=send.device)
+        rbuf[nb:].zero_()
+    else:
+        rmeta, rbuf = out
+    dist.all_to_all_single(rmeta[:rows], meta[:rows].contiguous(), group=group)
+    dist.all_to_all_single(rbuf[:nb], send[:nb], group=group)
+    return rmeta, rbuf
+
+
+def first_stalled(step, group=None):
+    """The fixed-capacity re-shard's replay point: `step` is this rank's stall
+    word (the first step whose received segments overflowed, 0: none). Returns
+    the earliest stalled step over all ranks (0: none) -- every rank replays
+    the steps from there through the counted exchange (its all-to-alls are
+    collective), and a rank processes a replayed step's packets only from its
+    own stalled step on (the ones before it already went through its flow
+    table)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return int(step)
+    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    big = 1 << 62
+    v = torch.tensor([int(step) if step else big], dtype=torch.int64, device=dev)
+    dist.all_reduce(v, op=dist.ReduceOp.MIN, group=group)
+    r = int(v.item())
+    return 0 if r == big else r
+
+
 def exchange_by_flow(ctx, arena, desc, perm, port_start, group=None):
     """Re-shard this rank's device batch by owner rank (one all-to-all).
 

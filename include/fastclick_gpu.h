@@ -255,6 +255,17 @@ void fcgpu_close(fcgpu_ctx *ctx);
 int  fcgpu_process(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_desc,
                    uint32_t n, const fcgpu_out *d_out, void *stream);
 
+/* fcgpu_process for a batch whose size is known only on the device: the
+ * first *d_count - base packets (at most n_max) of d_desc are processed, the
+ * launch covers n_max. No host sync: what a received re-shard batch goes
+ * through (fcgpu_exchange_unpack_fixed writes *d_count), in chunks of
+ * max_batch (base = the chunk's first packet). Outputs are those of
+ * fcgpu_process for the processed packets (per-tile counts of the tiles past
+ * them are 0); a whole-batch partition (FCGPU_PART_GLOBAL with perm or
+ * port_start) is refused. */
+int  fcgpu_process_counted(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_desc, uint32_t n_max,
+                           const uint32_t *d_count, uint32_t base, const fcgpu_out *d_out, void *stream);
+
 /* Several independent device-resident batches in one call -- e.g. the
  * batches of several rx queues, or a ring of batches a NIC filled: job k is
  * processed exactly as fcgpu_process(ctx, jobs[k].arena, jobs[k].desc,
@@ -735,6 +746,40 @@ int  fcgpu_exchange_build(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t
                           const uint16_t *d_verdict, uint32_t n, uint32_t world, uint32_t rank,
                           fcgpu_xmeta *d_meta, uint32_t *d_seg_n, uint64_t *d_seg_bytes, uint8_t *d_send,
                           uint64_t send_cap, void *stream);
+
+/* The fixed-capacity exchange: no host sync anywhere in a re-shard step.
+ * Owner d's segment has room for seg_recs packets and seg_bytes frame bytes
+ * (16-B slots): d_meta holds world x (seg_recs + 1) records -- segment d at
+ * d (seg_recs + 1): a header (fcgpu_xseg) then its records, as
+ * fcgpu_exchange_build writes them -- and d_send world x seg_bytes bytes,
+ * segment d at d x seg_bytes (record offsets relative to it). Both go through
+ * all-to-alls with equal splits (the split sizes never leave the device). An
+ * owner whose packets do not fit gets its header alone, flags bit 0 set:
+ * the receivers then process nothing for that step and the caller falls
+ * back to the counted exchange (fcgpu_exchange_build) for it
+ * (fastclick_amd.dist). world x seg_bytes must stay below 4 GiB. */
+typedef struct fcgpu_xseg {
+    uint32_t packets;         /* the owner's packets this step                          */
+    uint32_t bytes_lo;        /* their slot bytes                                         */
+    uint32_t bytes_hi;
+    uint32_t flags;           /* bit 0: overflow -- more than the capacity, none sent     */
+} fcgpu_xseg;
+int  fcgpu_exchange_build_fixed(fcgpu_ctx *ctx, const uint8_t *d_arena, const uint32_t *d_desc,
+                                const uint16_t *d_verdict, uint32_t n, uint32_t world, uint32_t rank,
+                                uint32_t seg_recs, uint64_t seg_bytes, fcgpu_xmeta *d_meta, uint8_t *d_send,
+                                void *stream);
+/* The receive side after the equal-split all-to-alls: d_rmeta / the received
+ * frames in the layout above, source s's segment at s. Writes the received
+ * packets' descriptors (in source-rank order, then source order, as
+ * fcgpu_exchange_unpack) into d_desc (room for world x seg_recs) and their
+ * number into *d_count. If any segment overflowed, or *d_stall is already
+ * non-zero (an earlier step stalled and is not repaired yet), *d_count = 0
+ * and *d_stall = step when it was 0: the flow pass of this step and of every
+ * later one processes nothing until the caller has replayed them, in order,
+ * through the counted exchange and cleared *d_stall. step must be non-zero. */
+int  fcgpu_exchange_unpack_fixed(fcgpu_ctx *ctx, const fcgpu_xmeta *d_rmeta, uint32_t world, uint32_t seg_recs,
+                                 uint64_t seg_bytes, uint32_t *d_desc, uint32_t *d_count, uint32_t *d_stall,
+                                 uint32_t step, void *stream);
 
 const char *fcgpu_last_error(fcgpu_ctx *ctx);   /* ctx may be NULL (open errors) */
 

@@ -114,3 +114,82 @@ def all_to_all(parts, world):
         out.append((np.concatenate(bufs) if bufs else np.zeros(0, np.uint8),
                     np.concatenate(metas) if metas else np.zeros((0, 4), np.uint32), displ))
     return out
+
+
+# ---- the fixed-capacity layout (fcgpu_exchange_build_fixed / _unpack_fixed) ----
+
+def build_fixed(arena, desc, owner, world, rank, seg_recs, seg_bytes):
+    """The fixed-capacity send side from each packet's owner (owner[i] >= world:
+    stays): (meta uint32 [world * (seg_recs + 1), 4], send uint8 [world *
+    seg_bytes], defined uint8 mask of send's written bytes, defined_meta bool
+    [world * (seg_recs + 1)]). Owner d's segment: its header (packets, bytes
+    low, bytes high, overflow) at row d (seg_recs + 1), then its records in
+    input order (offset within the segment, length, source index, source
+    rank), its frames from byte d seg_bytes in 16-B slots (slot bytes past the
+    frame zero). An owner with more than seg_recs packets or seg_bytes slot
+    bytes gets its header alone, overflow 1. Unwritten rows and bytes are not
+    part of the format (the mask)."""
+    arena = np.asarray(arena, dtype=np.uint8)
+    desc = np.asarray(desc, dtype=np.uint32).reshape(-1, 2)
+    owner = np.asarray(owner, dtype=np.int64)
+    rows = seg_recs + 1
+    meta = np.zeros((world * rows, 4), dtype=np.uint32)
+    dm = np.zeros(world * rows, dtype=bool)
+    send = np.zeros(world * seg_bytes, dtype=np.uint8)
+    defined = np.zeros(world * seg_bytes, dtype=bool)
+    for d in range(world):
+        idx = np.nonzero(owner == d)[0]
+        ln = desc[idx, 1].astype(np.uint64)
+        slot = _slot(ln)
+        total = int(slot.sum(dtype=np.uint64))
+        over = len(idx) > seg_recs or total > seg_bytes
+        meta[d * rows] = (len(idx), total & 0xFFFFFFFF, total >> 32, 1 if over else 0)
+        dm[d * rows] = True
+        if over or not len(idx):
+            continue
+        at = (np.cumsum(slot) - slot).astype(np.int64)
+        r0 = d * rows + 1
+        meta[r0:r0 + len(idx), 0] = at.astype(np.uint32)
+        meta[r0:r0 + len(idx), 1] = ln.astype(np.uint32)
+        meta[r0:r0 + len(idx), 2] = idx.astype(np.uint32)
+        meta[r0:r0 + len(idx), 3] = rank
+        dm[r0:r0 + len(idx)] = True
+        for k, i in enumerate(idx):
+            o, L, s = d * seg_bytes + int(at[k]), int(ln[k]), int(slot[k])
+            send[o:o + L] = arena[int(desc[i, 0]):int(desc[i, 0]) + L]
+            defined[o:o + s] = True
+    return meta, send, defined, dm
+
+
+def all_to_all_fixed(parts, world, seg_recs, seg_bytes):
+    """Equal-split all-to-all of the ranks' (meta, send): receiver r gets every
+    source s's segment r at position s."""
+    rows = seg_recs + 1
+    out = []
+    for r in range(world):
+        out.append((np.concatenate([m[r * rows:(r + 1) * rows] for m, _ in parts]),
+                    np.concatenate([b[r * seg_bytes:(r + 1) * seg_bytes] for _, b in parts])))
+    return out
+
+
+def unpack_fixed(rmeta, world, seg_recs, seg_bytes, stall, step):
+    """The receive side: (desc uint32 [count, 2], count, stall) -- descriptors
+    in (source rank, source order) into the received frames (source s at s
+    seg_bytes); count 0 and stall = step (if it was 0) when a segment
+    overflowed or stall was already set."""
+    rmeta = np.asarray(rmeta, dtype=np.uint32).reshape(-1, 4)
+    rows = seg_recs + 1
+    hdr = rmeta[::rows][:world]
+    nbytes = hdr[:, 1].astype(np.uint64) | (hdr[:, 2].astype(np.uint64) << np.uint64(32))
+    bad = (hdr[:, 3] & 1).astype(bool) | (hdr[:, 0] > seg_recs) | (nbytes > seg_bytes)
+    if bad.any() or stall:
+        return np.zeros((0, 2), np.uint32), 0, (stall or step)
+    out = []
+    for s in range(world):
+        recs = rmeta[s * rows + 1:s * rows + 1 + int(hdr[s, 0])]
+        d = np.zeros((len(recs), 2), np.uint32)
+        d[:, 0] = (s * seg_bytes + recs[:, 0].astype(np.int64)).astype(np.uint32)
+        d[:, 1] = recs[:, 1]
+        out.append(d)
+    desc = np.concatenate(out) if out else np.zeros((0, 2), np.uint32)
+    return desc, len(desc), stall

@@ -191,6 +191,14 @@ for s in "${ST[@]}"; do
              step "ab_new_${n}_$k" 300 python bench.py --steps 200 --warmup 20 --no-cpu $w || exit $?
            done
          done ;;
+    # round 6: the fixed-capacity re-shard (no host sync per step) against the counted one, interleaved;
+    # a forced-overflow run (every step replayed); the 8-rank command shape over gloo
+    r6reshard) for k in 1 2; do
+                 step "reshard1_fixed_$k" 300 python bench.py --flow-reshard --workload c4 --steps 50 --warmup 5 --no-cpu &&
+                 step "reshard1_counted_$k" 300 python bench.py --flow-reshard --workload c4 --steps 50 --warmup 5 --no-cpu --reshard-exchange counted || exit $?
+               done &&
+               step reshard1_overflow 300 python bench.py --flow-reshard --workload c4 --steps 20 --warmup 2 --no-cpu --reshard-slack 0.5 &&
+               step reshard8_fixed 900 python bench.py --gpus 8 --backend gloo --flow-reshard --workload c4 --steps 5 --warmup 1 --no-cpu ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

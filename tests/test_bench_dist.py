@@ -149,23 +149,31 @@ def test_gpu_bench_two_ranks():
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("gpus", [1, 2])
-def test_gpu_bench_flow_reshard(gpus):
+@pytest.mark.parametrize("gpus,exchange,slack", [(1, "fixed", 1.25), (2, "fixed", 1.25), (1, "counted", 1.25),
+                                                 (2, "counted", 1.25), (1, "fixed", 0.5), (2, "fixed", 0.4)])
+def test_gpu_bench_flow_reshard(gpus, exchange, slack):
     """`bench.py --flow-reshard`: every step runs the owner pass, the exchange
     kernels, the all-to-alls (gloo on one GPU for 2 ranks) and the flow table
     over the received batch; inside the run the all-reduced valid count is
     every packet once, and the tables' flow counts add up to the distinct
-    5-tuples of the ranks' batches (config.flow_reshard.checked)."""
+    5-tuples of the ranks' batches (config.flow_reshard.checked). The fixed
+    exchange (no host sync per step) with too small a capacity (slack < 1)
+    stalls at its first step and replays every step through the counted
+    exchange, with the same checked result."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--backend", "gloo",
                         "--flow-reshard", "--workload", "c4", "--packets", "65536", "--steps", "3", "--warmup", "1",
-                        "--nbuf", "2", "--no-cpu"], env=env, capture_output=True, text=True, timeout=240)
+                        "--nbuf", "2", "--no-cpu", "--reshard-exchange", exchange, "--reshard-slack", str(slack)],
+                       env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     fr = line["config"]["flow_reshard"]
     assert fr["checked"] and fr["flow_table_flows"] == fr["distinct_5tuples"] == 65536 * gpus
     assert fr["packets_received"] == fr["packets_sent"] == 65536 * gpus * 3
     assert set(fr["stage_ms_per_step"]) == {"owner_pass", "build", "exchange", "unpack", "flow_pass"}
+    assert fr["exchange"] == exchange
+    if exchange == "fixed":
+        assert fr["fallback_steps"] == (3 if slack < 1 else 0)
 
 
 def test_flow_reshard_options():

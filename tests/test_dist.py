@@ -299,3 +299,100 @@ def test_three_rank_exchange_segments_with_empty_segments():
         for (o, n_), (s, i) in zip(d.tolist(), want):
             so, sn = res[s][1][i].tolist()
             assert n_ == sn and np.array_equal(buf[o:o + n_], res[s][0][so:so + sn])
+
+
+def _fixed_owner(src, n):
+    # source 0 sends 90 % of its packets to rank 1, source 1 half to each
+    i = np.arange(n)
+    return np.where(i % 10 != 0, 1, 0) if src == 0 else i % 2
+
+
+def _fixed_worker(rank, world, port, q):
+    """Two steps of the fixed-capacity re-shard (the HIP build and unpack
+    restated by oracle/exchange.py, the all-to-alls through
+    dist.exchange_fixed over gloo): step 1 with room for everything, step 2
+    with segments of 60 % of a batch -- source 0's 90 % for rank 1 does not
+    fit, so rank 1 stalls and rank 0 does not. dist.first_stalled names step
+    2 on both ranks, both replay it through the counted exchange
+    (dist.exchange_segments), and only rank 1 takes the replayed packets."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import exchange as X
+        b = _flow_batch()
+        lo, hi = D.shard_range(b.n, world, rank)
+        shard = synth.Batch(arena=b.arena, desc=np.ascontiguousarray(b.desc[lo:hi]))
+        n = hi - lo
+        owner = _fixed_owner(rank, n)
+        cap = int(((shard.desc[:, 1].astype(np.int64) + 15) & ~15).sum())
+        got, stall, replayed = [], 0, 0
+        for step, frac in ((1, 1.0), (2, 0.6)):
+            c = torch.tensor([int(n * frac), (int(cap * frac) + 15) // 16 * 16], dtype=torch.int64)
+            dist.all_reduce(c, op=dist.ReduceOp.MIN)      # the ranks agree on one capacity
+            recs, segb = int(c[0]), int(c[1])
+            meta, send, _, _ = X.build_fixed(shard.arena, shard.desc, owner, world, rank, recs, segb)
+            rmeta, rbuf = D.exchange_fixed(torch.from_numpy(meta.view(np.int32)),
+                                           torch.from_numpy(np.concatenate([send, np.zeros(D.ARENA_PAD, np.uint8)])),
+                                           recs, segb)
+            rmeta = rmeta.numpy().view(np.uint32)
+            rbuf = rbuf.numpy()
+            assert len(rbuf) == world * segb + D.ARENA_PAD and not rbuf[world * segb:].any()
+            desc, count, stall = X.unpack_fixed(rmeta, world, recs, segb, stall, step)
+            if count:
+                rows = recs + 1
+                src = np.concatenate([rmeta[s * rows + 1:s * rows + 1 + int(rmeta[s * rows, 0])]
+                                      for s in range(world)])
+                got.append([(int(x[3]), int(x[2]), bytes(rbuf[d[0]:d[0] + d[1]])) for x, d in zip(src, desc)])
+        first = D.first_stalled(stall)
+        if first:       # the replay: every step from `first`, counted, collectively
+            perm, ps = X.partition(owner, world)
+            meta, seg = X.plan(shard.desc, perm, ps, world, rank)
+            send = np.concatenate([X.pack(shard.arena, shard.desc, meta, ps, seg, world),
+                                   np.zeros(D.ARENA_PAD, np.uint8)])
+            seg_n = [int(ps[d + 1]) - int(ps[d]) for d in range(world)]
+            buf, rm, displ = D.exchange_segments(torch.from_numpy(send), torch.from_numpy(meta.view(np.int32)),
+                                                 seg_n, [int(x) for x in seg])
+            rm = rm.numpy().view(np.uint32)
+            desc = X.unpack(rm, displ)
+            buf = buf.numpy()
+            if stall and 2 >= stall:      # this rank's own stalled step on: its table takes them
+                got.append([(int(x[3]), int(x[2]), bytes(buf[d[0]:d[0] + d[1]])) for x, d in zip(rm, desc)])
+                replayed += 1
+        q.put((rank, stall, first, replayed, got))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_fixed_exchange_and_overflow_replay():
+    """The fixed-capacity re-shard over gloo, two ranks: with room, each rank
+    receives exactly its packets (source rank, source order, frame bytes);
+    when a step's segment overflows, its receiver stalls (count 0), every rank
+    learns the first stalled step (dist.first_stalled), the step is replayed
+    through the counted exchange, and only the stalled rank takes the
+    replayed packets (the other already has them) -- the fallback the bench
+    counts (config.flow_reshard.fallback_steps)."""
+    world = 2
+    port = 29500 + ((os.getpid() + 700) % 1000)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_fixed_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    b = _flow_batch()
+    for rank, stall, first, replayed, got in res:
+        assert first == 2
+        assert stall == (2 if rank == 1 else 0) and replayed == (1 if rank == 1 else 0)
+        exp = []
+        for src in range(world):
+            lo, hi = D.shard_range(b.n, world, src)
+            own = _fixed_owner(src, hi - lo)
+            exp += [(src, i, b.frame(lo + i)) for i in range(hi - lo) if own[i] == rank]
+        assert len(got) == 2
+        for batch in got:
+            assert batch == exp

@@ -295,6 +295,130 @@ def test_gpu_exchange_build_1m_and_owner_pass(oracle):
         ctx.close()
 
 
+def _build_fixed_gpu(ctx, arena, desc, owner, world, rank, recs, segb):
+    from fastclick_amd import device
+    port = np.where((owner >= 0) & (owner < world), owner, world).astype(np.uint16)
+    verdict = (port << 8) | np.where(port < world, N.R_OK, 1).astype(np.uint16)
+    meta = torch.full((world * (recs + 1), 4), -1, dtype=torch.int32, device="cuda:0")
+    send = torch.zeros(world * segb + D.ARENA_PAD, dtype=torch.uint8, device="cuda:0")
+    device.exchange_build_fixed(ctx, _dev(arena, np.uint8), _dev(desc, np.int32), _dev(verdict, np.int16), world,
+                                rank, recs, segb, meta, send)
+    torch.cuda.synchronize()
+    return meta, send
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n,seed,slack", [(1, 5000, 41, 1.0), (3, 5000, 42, 1.25), (8, 20000, 43, 1.25),
+                                                (64, 20000, 44, 2.0), (2, 257, 45, 1.25), (16, 70000, 46, 1.1),
+                                                (4, 3000, 47, 0.5), (8, 9000, 48, 0.9)])
+def test_gpu_exchange_fixed_matches_oracle(world, n, seed, slack):
+    """fcgpu_exchange_build_fixed writes every owner's header, records and
+    frames at its fixed place as the restatement does (overflowing owners:
+    the header alone, flag set), and after an equal-split all-to-all
+    (simulated over copies of this one source's buffers, as every rank sent
+    the same) fcgpu_exchange_unpack_fixed gives the restatement's descriptors
+    and count -- or count 0 and the stall word set to the step when a segment
+    overflowed. fcgpu_process_counted then checks exactly the first *count
+    packets of the bound."""
+    from fastclick_amd import device
+    arena, desc = _ragged(n, seed)
+    owner = np.random.default_rng(seed + 100).integers(-1, world, n)
+    cap_bytes = int(((desc[:, 1].astype(np.int64) + 15) & ~15).sum())
+    if slack >= 1:
+        recs, segb = device.fixed_capacity(n, cap_bytes, world, slack)
+    else:
+        recs, segb = max(1, int(n / world * slack)), (int(cap_bytes / world * slack) + 15) // 16 * 16
+    ctx = N.Context(0, max(n, 1))
+    try:
+        meta, send = _build_fixed_gpu(ctx, arena, desc, owner, world, 3, recs, segb)
+        em, es, defined, dm = X.build_fixed(arena, desc, owner, world, 3, recs, segb)
+        hm = meta.cpu().numpy().view(np.uint32)
+        assert np.array_equal(hm[dm], em[dm])
+        hs = send.cpu().numpy()
+        assert np.array_equal(hs[:world * segb][defined], es[defined])
+        over = em[::recs + 1][:world, 3].astype(bool)
+        # receiver 0 of `world` sources that all sent these buffers
+        parts = [(em, es)] * world
+        rmeta_np, rbuf_np = X.all_to_all_fixed(parts, world, recs, segb)[0]
+        rmeta = torch.from_numpy(rmeta_np.view(np.int32)).to("cuda:0")
+        rbuf = torch.from_numpy(np.concatenate([rbuf_np, np.zeros(D.ARENA_PAD, np.uint8)])).to("cuda:0")
+        rdesc = torch.zeros((world * recs, 2), dtype=torch.int32, device="cuda:0")
+        count = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+        stall = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+        device.exchange_unpack_fixed(ctx, rmeta, world, recs, segb, rdesc, count, stall, 7)
+        torch.cuda.synchronize()
+        edesc, ecount, estall = X.unpack_fixed(rmeta_np, world, recs, segb, 0, 7)
+        assert int(count.item()) == ecount and int(stall.item()) == estall
+        assert bool(over[0]) == (estall == 7)
+        if ecount:
+            assert np.array_equal(rdesc[:ecount].cpu().numpy().view(np.uint32), edesc)
+            # the received frames are this source's owner-0 frames, in order
+            idx = np.nonzero(owner == 0)[0]
+            for k in range(0, min(len(idx), ecount), 97):
+                o, ln = (int(x) for x in edesc[k])
+                assert bytes(rbuf_np[o:o + ln]) == bytes(arena[desc[idx[k], 0]:desc[idx[k], 0] + ln])
+        # a later step while stalled stays stalled (count 0, the first step kept)
+        device.exchange_unpack_fixed(ctx, rmeta, world, recs, segb, rdesc, count, stall, 8)
+        torch.cuda.synchronize()
+        assert int(stall.item()) == estall and (int(count.item()) == 0) == bool(estall)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flow", [False, True])
+def test_gpu_process_counted_matches_prefix(oracle, flow):
+    """fcgpu_process_counted over a bound of 9000 packets with the count on the
+    device: its outputs and counters are fcgpu_process's over the first
+    *count - base packets (2 chunks of a context whose max_batch is 5000),
+    per-tile counts past them 0; with a flow table, the same flow IDs and
+    table as fcgpu_process over exactly those packets."""
+    from fastclick_amd.device import DeviceBatch, DeviceOutputs
+    b = synth.c3(9000, nflows=800, seed=51)
+    synth.inject_errors(b, 0.03, seed=52)
+    cfg = N.make_cfg(offset=14, checksum=True, classify=N.CLS_LB_HASH, nports=8)
+    live = 6203
+    db = DeviceBatch.upload(b, device="cuda:0")
+    res = []
+    for counted in (False, True):
+        ctx = N.Context(0, 5000, cfg)
+        try:
+            if flow:
+                ctx.flow_enable(20000)
+            ctr = torch.zeros(N.CTR_SHARDS, N.NCOUNTERS, dtype=torch.int64, device="cuda:0")
+            ctx.use_counters(ctr.data_ptr())
+            outs = [DeviceOutputs(5000, 8, device="cuda:0", verdict=True, hash=True, tile_perm=True,
+                                  partition=N.PART_TILE, flowid=flow) for _ in range(2)]
+            for o in outs:
+                o.tile_count.fill_(-1)
+            cnt = torch.tensor([live], dtype=torch.int32, device="cuda:0")
+            for k, (c0, m) in enumerate(((0, 5000), (5000, 4000 if counted else live - 5000))):
+                dptr = db.desc[c0:].data_ptr()
+                if counted:
+                    ctx.process_counted(db.arena.data_ptr(), dptr, m, cnt.data_ptr(), c0, **outs[k].ptrs())
+                else:
+                    ctx.process(db.arena.data_ptr(), dptr, m, **outs[k].ptrs())
+            torch.cuda.synchronize()
+            res.append(dict(ctr=N.derive_counters(ctr.sum(0).cpu().numpy()), outs=outs,
+                            flows=ctx.flow_count() if flow else 0))
+        finally:
+            ctx.close()
+    a, c = res
+    assert np.array_equal(a["ctr"], c["ctr"])
+    assert a["flows"] == c["flows"]
+    m2 = live - 5000
+    for k, m in ((0, 5000), (1, m2)):
+        for key in ("verdict", "hash") + (("flowid",) if flow else ()):
+            x = getattr(a["outs"][k], key)[:m].cpu().numpy()
+            y = getattr(c["outs"][k], key)[:m].cpu().numpy()
+            assert np.array_equal(x, y), (k, key)
+    nb = 9
+    t_live = -(-m2 // 256)
+    tc = c["outs"][1].tile_count.cpu().numpy().reshape(-1, nb)
+    assert np.array_equal(tc[:t_live], a["outs"][1].tile_count.cpu().numpy().reshape(-1, nb)[:t_live])
+    assert (tc[t_live:-(-4000 // 256)] == 0).all()
+
+
 def test_exchange_rejects_bad_arguments():
     """Argument checks need no device: a null context, world 0 or > 64."""
     lib = N.load()
