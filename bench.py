@@ -709,6 +709,9 @@ class ReshardProcessor:
         # the fixed-capacity exchange: every buffer sized once, the step's
         # counts stay on the device (received packets summed there too)
         self.fixed = args.reshard_exchange == "fixed"
+        # FCGPU_RESHARD_HOST=1: the host's own time per stage of the fixed
+        # step (enqueue work), reported in config.flow_reshard
+        self.host_t = [0.0] * 6 if os.environ.get("FCGPU_RESHARD_HOST") == "1" else None
         self.recv_dev = torch.zeros(1, dtype=torch.int64, device=dev)
         self.fallback_steps = 0
         self.step_id = 0
@@ -746,26 +749,37 @@ class ReshardProcessor:
         a, d = self.bufs[k % len(self.bufs)]
         s = torch.cuda.current_stream()
         ev = self.ev[k - self.first] if timed and self.ev else None
+        ht = self.host_t
+        if ht is not None:
+            h0 = time.perf_counter()
         if ev:
             ev[0].record(s)
         o = self.own_out
         self.ctx_own.process(a.data_ptr(), d.data_ptr(), self.n, stream=s.cuda_stream, **o.ptrs())
         if ev:
             ev[1].record(s)
+        if ht is not None:
+            h1 = time.perf_counter()
         DV.exchange_build_fixed(self.ctx_own, a, d, o.verdict, self.world, self.rank, self.recs, self.segb,
                                 self.fmeta, self.fsend, stream=s)
         if ev:
             ev[2].record(s)
+        if ht is not None:
+            h2 = time.perf_counter()
         out = (self.frmeta, self.frbuf) if self.world > 1 else None
         rmeta, rbuf = exchange_fixed(self.fmeta, self.fsend, self.recs, self.segb, out=out)
         if ev:
             ev[3].record(s)
+        if ht is not None:
+            h3 = time.perf_counter()
         self.step_id += 1
         self.step_k[self.step_id] = (k, timed)
         DV.exchange_unpack_fixed(self.ctx_own, rmeta, self.world, self.recs, self.segb, self.fdesc, self.fcount,
                                  self.fstall, self.step_id, stream=s)
         if ev:
             ev[4].record(s)
+        if ht is not None:
+            h4 = time.perf_counter()
         f = self.flow_out
         bound = self.world * self.recs
         for c0 in range(0, bound, self.cap):
@@ -775,6 +789,11 @@ class ReshardProcessor:
             ev[5].record(s)
         if timed:
             self.recv_dev += self.fcount       # device-side: no sync
+        if ht is not None:
+            h5 = time.perf_counter()
+            for j, (x, y) in enumerate(((h0, h1), (h1, h2), (h2, h3), (h3, h4), (h4, h5))):
+                ht[j] += y - x
+            ht[5] += 1
 
     def _repair(self):
         """The fixed exchange's stalled steps (a segment overflowed; every later
@@ -791,7 +810,7 @@ class ReshardProcessor:
             for sid in range(first, self.step_id + 1):
                 k, timed = self.step_k[sid]
                 self._step_counted(k, timed, process=bool(mine) and sid >= mine, replay=True)
-            self.fallback_steps += self.step_id + 1 - first
+                self.fallback_steps += 1 if timed else 0      # timed steps replayed
             self.fstall.zero_()
         self.step_k.clear()
 
@@ -886,6 +905,9 @@ class ReshardProcessor:
         fx = ({"exchange": "fixed", "seg_recs": self.recs, "seg_bytes": self.segb,
                "slack": self.args.reshard_slack, "fallback_steps": self.fallback_steps}
               if self.fixed else {"exchange": "counted"})
+        if self.host_t is not None and self.host_t[5]:
+            fx["host_us_per_step"] = {k: round(1e6 * t / self.host_t[5], 1) for k, t in
+                                      zip(("owner_pass", "build", "exchange", "unpack", "flow_pass"), self.host_t)}
         return {"flow_table_flows": flows, "distinct_5tuples": distinct, "packets_received": received,
                 "packets_sent": sent, "checked": True, **fx,
                 **({"stage_ms_per_step": {k: round(t / steps, 4) for k, t in zip(names, self.stage_ms)},

@@ -199,6 +199,14 @@ for s in "${ST[@]}"; do
                done &&
                step reshard1_overflow 300 python bench.py --flow-reshard --workload c4 --steps 20 --warmup 2 --no-cpu --reshard-slack 0.5 &&
                step reshard8_fixed 900 python bench.py --gpus 8 --backend gloo --flow-reshard --workload c4 --steps 5 --warmup 1 --no-cpu ;;
+    # round 6: the build's scan inside k_xbtile (lib/ab/libfcgpu_old.so: the three-launch build), interleaved
+    r6xbuild) for k in 1 2; do
+                FCGPU_LIB=fastclick_amd/lib/ab/libfcgpu_old.so step "xrate_old_$k" 300 python scripts/exchange_rate.py --reps 30 &&
+                step "xrate_new_$k" 300 python scripts/exchange_rate.py --reps 30 || exit $?
+              done ;;
+    # round 6: the fixed re-shard's host time per stage and its kernel trace
+    r6reshost) FCGPU_RESHARD_HOST=1 step reshard1_fixed_host 300 python bench.py --flow-reshard --workload c4 --steps 50 --warmup 5 --no-cpu &&
+               kt kt_reshard_fixed 300 --flow-reshard --workload c4 --steps 10 --warmup 2 --no-cpu ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
