@@ -1,0 +1,131 @@
+// kgather.hip -- the bare header-window gather of a real batch layout
+// (microbenchmark, not product code).
+//
+// Question: on the wire-layout BASELINE configs (C3 IMIX, C5 VLAN/IPv6 mix)
+// k_rx reaches 0.52 / 0.59 of the HBM roofline with 1.38x / 1.27x read
+// traffic. Is all of that the layout (windows alone in their 128-B lines),
+// or is part of it the kernel? This kernel does exactly k_rx's loads for the
+// batch -- the descriptors (one per lane, as load_desc) and each packet's
+// 64-B header window through LDS-DMA (fcgpu::win_src / glds16, the same
+// addresses, order and cache policy) -- and nothing else: one dword of each
+// window is folded into a per-workgroup word so the loads are not dead.
+// Variant "+outputs" also stores what the bench's k_rx stores per packet
+// (verdict 2 B, hash 4 B, tile_perm 1 B, non-temporal; per-tile counts).
+// The batch comes from scripts/gather_bound.py: its descriptors (uint32
+// pairs) in a file, the arena's size; the arena's contents do not matter for
+// the line pattern. As many arena + descriptor copies as keep 1.2 GB in
+// play (bench.py's rotation); each launch carries 16 batches (workgroup w:
+// batch w / tiles, as k_rx's fused launches), so the time per batch is
+// comparable to the bench's roofline.kernel_ms.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Ifastclick_amd/csrc -Iinclude scripts/kgather.hip -o scripts/kgather
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+
+#include "fcgpu_device.hh"
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+using namespace fcgpu;
+
+constexpr uint32_t kFuse = 16;
+struct Batches {
+    const uint8_t *arena[kFuse];
+    const uint2 *desc[kFuse];
+};
+template <bool OUT>
+__global__ __launch_bounds__(kTile, 8) void k_gather(Batches B, uint32_t tiles, uint32_t n, uint32_t *fold,
+                                                    uint16_t *verdict, uint32_t *hash, uint8_t *tperm,
+                                                    uint16_t *tcount) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[4 * kWave * kWin];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t j = blockIdx.x / tiles, tile = blockIdx.x - j * tiles;
+    const uint8_t *arena = B.arena[j];
+    const uint2 *desc = B.desc[j];
+    const uint32_t i = tile * kTile + threadIdx.x;
+    uint2 d = make_uint2(0, 0);
+    if (i < n) d = load_desc(desc, i, 0);
+    uint8_t *wl = s_win + wave * (kWave * kWin);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) glds16(win_src(arena, d.x, lane, k), wl + k * 1024);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t w = *reinterpret_cast<const uint32_t *>(wl + (lane >> 4) * 1024 + (lane & 15) * 64);
+    const uint32_t x = w ^ d.y;
+    if (OUT && i < n) {
+        st_nt(verdict + i, (uint16_t)(x & 0xff));
+        st_nt(hash + i, x);
+        st_nt(tperm + i, (uint8_t)threadIdx.x);
+    }
+    const uint64_t m = __ballot(x == 0x9e3779b9u);      // never true: keeps the loads live
+    if (OUT && threadIdx.x < 17) tcount[(size_t)tile * 17 + threadIdx.x] = (uint16_t)m;
+    if (m && lane == 0) fold[tile] = x;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 4) {
+        printf("usage: kgather <desc.bin> <n> <arena_bytes> [reps]\n");
+        return 2;
+    }
+    const uint32_t n = (uint32_t)atoi(argv[2]);
+    const size_t arena_bytes = (size_t)atoll(argv[3]) + 256;
+    const int reps = argc > 4 ? atoi(argv[4]) : 20;
+    std::vector<uint32_t> h(2ull * n);
+    FILE *f = fopen(argv[1], "rb");
+    if (!f || fread(h.data(), 8, n, f) != n) {
+        printf("cannot read %u descriptors from %s\n", n, argv[1]);
+        return 1;
+    }
+    fclose(f);
+    const size_t per = arena_bytes + 8ull * n;
+    const uint32_t nbuf = (uint32_t)std::max<size_t>(2, ((size_t)1200 << 20) / per + 1);
+    std::vector<uint8_t *> ar(nbuf);
+    std::vector<uint2 *> de(nbuf);
+    for (uint32_t b = 0; b < nbuf; ++b) {
+        CK(hipMalloc(&ar[b], arena_bytes));
+        CK(hipMemset(ar[b], 0x45, arena_bytes));
+        CK(hipMalloc(&de[b], 8ull * n));
+        CK(hipMemcpy(de[b], h.data(), 8ull * n, hipMemcpyHostToDevice));
+    }
+    const uint32_t tiles = (n + kTile - 1) / kTile;
+    uint32_t *fold;
+    uint16_t *verdict, *tcount;
+    uint32_t *hash;
+    uint8_t *tperm;
+    CK(hipMalloc(&fold, 4ull * tiles));
+    CK(hipMalloc(&verdict, 2ull * n));
+    CK(hipMalloc(&hash, 4ull * n));
+    CK(hipMalloc(&tperm, (size_t)n + kTile));
+    CK(hipMalloc(&tcount, 2ull * 17 * tiles));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int out = 0; out < 2; ++out) {
+        auto launch = [&](int r) {
+            Batches B;
+            for (uint32_t k = 0; k < kFuse; ++k) {
+                B.arena[k] = ar[(r * kFuse + k) % nbuf];
+                B.desc[k] = de[(r * kFuse + k) % nbuf];
+            }
+            if (out)
+                hipLaunchKernelGGL(k_gather<true>, dim3(tiles * kFuse), dim3(kTile), 0, 0, B, tiles, n, fold, verdict,
+                                   hash, tperm, tcount);
+            else
+                hipLaunchKernelGGL(k_gather<false>, dim3(tiles * kFuse), dim3(kTile), 0, 0, B, tiles, n, fold,
+                                   verdict, hash, tperm, tcount);
+        };
+        for (int r = 0; r < 8; ++r) launch(r);
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a, 0));
+        for (int r = 0; r < reps; ++r) launch(r);
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        printf("{\"variant\": \"%s\", \"us_per_batch\": %.3f, \"nbuf\": %u, \"launches\": %d, "
+               "\"batches_per_launch\": %u}\n",
+               out ? "gather+outputs" : "gather", ms * 1e3 / (reps * kFuse), nbuf, reps, kFuse);
+    }
+    return 0;
+}

@@ -207,6 +207,8 @@ for s in "${ST[@]}"; do
     # round 6: the fixed re-shard's host time per stage and its kernel trace
     r6reshost) FCGPU_RESHARD_HOST=1 step reshard1_fixed_host 300 python bench.py --flow-reshard --workload c4 --steps 50 --warmup 5 --no-cpu &&
                kt kt_reshard_fixed 300 --flow-reshard --workload c4 --steps 10 --warmup 2 --no-cpu ;;
+    # round 6: the wire layouts' own ceiling (bare window gather vs k_rx, same box)
+    r6gather) step gather_bound 600 python scripts/gather_bound.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
