@@ -712,7 +712,7 @@ class ReshardProcessor:
         # FCGPU_RESHARD_HOST=1: the host's own time per stage of the fixed
         # step (enqueue work), reported in config.flow_reshard
         self.host_t = [0.0] * 6 if os.environ.get("FCGPU_RESHARD_HOST") == "1" else None
-        self.recv_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.recv_dev = torch.zeros(1, dtype=torch.int64, device=dev)   # the unpack adds each timed step's count
         self.fallback_steps = 0
         self.step_id = 0
         self.step_k = {}
@@ -775,7 +775,7 @@ class ReshardProcessor:
         self.step_id += 1
         self.step_k[self.step_id] = (k, timed)
         DV.exchange_unpack_fixed(self.ctx_own, rmeta, self.world, self.recs, self.segb, self.fdesc, self.fcount,
-                                 self.fstall, self.step_id, stream=s)
+                                 self.fstall, self.step_id, total=self.recv_dev if timed else None, stream=s)
         if ev:
             ev[4].record(s)
         if ht is not None:
@@ -787,8 +787,6 @@ class ReshardProcessor:
                                           self.fcount.data_ptr(), c0, stream=s.cuda_stream, **f.ptrs())
         if ev:
             ev[5].record(s)
-        if timed:
-            self.recv_dev += self.fcount       # device-side: no sync
         if ht is not None:
             h5 = time.perf_counter()
             for j, (x, y) in enumerate(((h0, h1), (h1, h2), (h2, h3), (h3, h4), (h4, h5))):

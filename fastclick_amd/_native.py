@@ -254,7 +254,8 @@ FCGPU_SYMBOLS = {
                                              C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, C.c_void_p,
                                              C.c_void_p, C.c_void_p]),
     "fcgpu_exchange_unpack_fixed": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64,
-                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
+                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                              C.c_void_p]),
     "fcgpu_process_counted": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
                                         C.POINTER(fcgpu_out), C.c_void_p]),
     "fcgpu_last_error": (C.c_char_p, [C.c_void_p]),
@@ -579,10 +580,13 @@ class Context:
                                                       seg_bytes, meta, send, stream or None),
                   "fcgpu_exchange_build_fixed")
 
-    def exchange_unpack_fixed(self, rmeta, world, seg_recs, seg_bytes, desc, count, stall, step, stream=0):
-        """fcgpu_exchange_unpack_fixed: received fixed segments -> descriptors, *count, *stall."""
+    def exchange_unpack_fixed(self, rmeta, world, seg_recs, seg_bytes, desc, count, stall, step, total=0,
+                              stream=0):
+        """fcgpu_exchange_unpack_fixed: received fixed segments -> descriptors, *count, *stall
+        (and *total += count when total is given)."""
         self._chk(self.lib.fcgpu_exchange_unpack_fixed(self.h, rmeta, world, seg_recs, seg_bytes, desc, count,
-                                                       stall, step, stream or None), "fcgpu_exchange_unpack_fixed")
+                                                       stall, total or None, step, stream or None),
+                  "fcgpu_exchange_unpack_fixed")
 
     def exchange_unpack(self, meta, n, src_displ, desc, stream=0):
         """fcgpu_exchange_unpack: received records -> descriptors (src_displ: per-source segment starts)."""

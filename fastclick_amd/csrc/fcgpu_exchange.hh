@@ -517,12 +517,22 @@ __device__ __forceinline__ void xtile_sort(const XBuild &B, uint32_t t, XTileLds
     intra = own < B.world ? L.pre[pos] - L.pre[L.tstart[own]] : 0u;
 }
 
-// loads of other workgroups' results (after the ticket's acquire): agent scope, past this CU's L1
+// What one workgroup writes for another (the tickets' last blocks) goes
+// through agent-scope relaxed atomic stores and loads: coherent across the
+// XCDs' L2s without a release/acquire fence -- an agent-scope fence writes
+// back the whole L2 of the XCD (buffer_wbl2), which per workgroup made
+// k_xbtile 45x slower (7.5 -> 340 us, profiles/r06_exchange/).
 __device__ __forceinline__ uint32_t xld32(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint64_t xld64(const unsigned long long *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void xst32(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void xst64(unsigned long long *p, uint64_t v) {
+    __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // inclusive scan over the 64 lanes of a wave (64-bit)
 __device__ __forceinline__ uint64_t xwave_incl64(uint64_t x) {
@@ -534,17 +544,17 @@ __device__ __forceinline__ uint64_t xwave_incl64(uint64_t x) {
     }
     return x;
 }
-// this workgroup's turn at a ticket: true for the last of `parties` (all of
-// the block's prior global writes released first, the others' acquired after)
+// this workgroup's turn at a ticket: true for the last of `parties`. The
+// block's atomic stores have completed (vmcnt 0: acknowledged at the agent's
+// coherence point) before its ticket is taken, so the last block's atomic
+// loads after its ticket see every other block's.
 __device__ __forceinline__ bool xlast(uint32_t *ticket, uint32_t parties, uint32_t *s_flag) {
-    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
-        *s_flag = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == parties - 1;
+        *s_flag = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == parties - 1;
     __syncthreads();
-    const bool last = *s_flag != 0;
-    if (last) __threadfence();
-    return last;
+    return *s_flag != 0;
 }
 
 __global__ __launch_bounds__(kXTile) void k_xbtile(XBuild B) {
@@ -558,8 +568,8 @@ __global__ __launch_bounds__(kXTile) void k_xbtile(XBuild B) {
         const uint32_t d = threadIdx.x;
         if (d < B.world) {
             const uint32_t a = L.tstart[d], c = L.tcnt[d];
-            B.tcnt[(size_t)d * B.ntiles + t] = c;
-            B.tbyt[(size_t)d * B.ntiles + t] = L.pre[a + c] - L.pre[a];
+            xst32(B.tcnt + (size_t)d * B.ntiles + t, c);
+            xst64(B.tbyt + (size_t)d * B.ntiles + t, L.pre[a + c] - L.pre[a]);
         }
     }
     // the last tile of group g to finish: in-group exclusive prefixes, the group's totals
@@ -577,8 +587,8 @@ __global__ __launch_bounds__(kXTile) void k_xbtile(XBuild B) {
             B.tbyt[at] = bi - b;
         }
         if (lane == 63) {
-            B.gcnt[(size_t)d * B.ngroups + g] = ci;
-            B.gbyt[(size_t)d * B.ngroups + g] = bi;
+            xst32(B.gcnt + (size_t)d * B.ngroups + g, ci);
+            xst64(B.gbyt + (size_t)d * B.ngroups + g, bi);
         }
     }
     if (threadIdx.x == 0) B.ticket[g] = 0u;      // every tile of the group has taken its turn
@@ -771,6 +781,7 @@ struct XUnpackFixed {
     unsigned long long bytes;
     uint32_t *count;
     uint32_t *stall;
+    unsigned long long *total;   // optional: += the count (a running total, no host read per step)
     uint32_t step;
 };
 __global__ __launch_bounds__(kXThreads) void k_xunpack_fixed(XUnpackFixed U) {
@@ -801,7 +812,10 @@ __global__ __launch_bounds__(kXThreads) void k_xunpack_fixed(XUnpackFixed U) {
         }
         return;
     }
-    if (blockIdx.x == 0 && s == 0 && threadIdx.x == 0) *U.count = s_pre[U.world];
+    if (blockIdx.x == 0 && s == 0 && threadIdx.x == 0) {
+        *U.count = s_pre[U.world];
+        if (U.total) *U.total += s_pre[U.world];
+    }
     const uint32_t k = blockIdx.x * kXThreads + threadIdx.x;
     const uint32_t ns = s_pre[s + 1] - s_pre[s];
     if (k >= ns) return;

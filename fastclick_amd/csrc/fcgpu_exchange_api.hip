@@ -200,7 +200,7 @@ int fcgpu_exchange_build_fixed(fcgpu_ctx *c, const uint8_t *d_arena, const uint3
 
 int fcgpu_exchange_unpack_fixed(fcgpu_ctx *c, const fcgpu_xmeta *d_rmeta, uint32_t world, uint32_t seg_recs,
                                 uint64_t seg_bytes, uint32_t *d_desc, uint32_t *d_count, uint32_t *d_stall,
-                                uint32_t step, void *stream) {
+                                uint64_t *d_total, uint32_t step, void *stream) {
     if (!c) return FCGPU_EINVAL;
     if (world == 0 || world > FCGPU_MAX_PORTS)
         return fail(c, FCGPU_EINVAL, "fcgpu_exchange_unpack_fixed: world must be 1..64");
@@ -217,6 +217,7 @@ int fcgpu_exchange_unpack_fixed(fcgpu_ctx *c, const fcgpu_xmeta *d_rmeta, uint32
     U.bytes = seg_bytes;
     U.count = d_count;
     U.stall = d_stall;
+    U.total = reinterpret_cast<unsigned long long *>(d_total);
     U.step = step;
     hipLaunchKernelGGL(k_xunpack_fixed, dim3((seg_recs + kXThreads - 1) / kXThreads, world), dim3(kXThreads), 0,
                        static_cast<hipStream_t>(stream), U);

@@ -247,10 +247,12 @@ def exchange_build_fixed(ctx: N.Context, arena, desc, verdict, world, rank, seg_
 
 
 def exchange_unpack_fixed(ctx: N.Context, rmeta, world, seg_recs, seg_bytes, desc, count, stall, step,
-                          stream=None):
+                          total=None, stream=None):
     """fcgpu_exchange_unpack_fixed: the received segments -> desc int32 [world *
-    seg_recs, 2] (the first *count rows), count / stall int32 [1] device words."""
+    seg_recs, 2] (the first *count rows), count / stall int32 [1] device words;
+    total (int64 [1], optional) += count."""
     torch = _torch()
     s = stream if stream is not None else torch.cuda.current_stream()
     ctx.exchange_unpack_fixed(rmeta.data_ptr(), world, seg_recs, seg_bytes, desc.data_ptr(), count.data_ptr(),
-                              stall.data_ptr(), step, stream=s.cuda_stream)
+                              stall.data_ptr(), step, total=total.data_ptr() if total is not None else 0,
+                              stream=s.cuda_stream)

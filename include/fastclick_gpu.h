@@ -776,10 +776,12 @@ int  fcgpu_exchange_build_fixed(fcgpu_ctx *ctx, const uint8_t *d_arena, const ui
  * non-zero (an earlier step stalled and is not repaired yet), *d_count = 0
  * and *d_stall = step when it was 0: the flow pass of this step and of every
  * later one processes nothing until the caller has replayed them, in order,
- * through the counted exchange and cleared *d_stall. step must be non-zero. */
+ * through the counted exchange and cleared *d_stall. step must be non-zero.
+ * d_total (may be NULL): *d_total += the count, a running total of the
+ * packets received that needs no host read per step. */
 int  fcgpu_exchange_unpack_fixed(fcgpu_ctx *ctx, const fcgpu_xmeta *d_rmeta, uint32_t world, uint32_t seg_recs,
                                  uint64_t seg_bytes, uint32_t *d_desc, uint32_t *d_count, uint32_t *d_stall,
-                                 uint32_t step, void *stream);
+                                 uint64_t *d_total, uint32_t step, void *stream);
 
 const char *fcgpu_last_error(fcgpu_ctx *ctx);   /* ctx may be NULL (open errors) */
 
