@@ -407,6 +407,8 @@ __global__ __launch_bounds__(kXThreads) void k_xpack(XPack X) {
 // the frames are read once and written once.
 constexpr uint32_t kXTile = 256;
 constexpr uint32_t kXGroup = 64;    // tiles per group of the two-level scan (one per lane of a wave)
+constexpr uint32_t kXTicketStride = 32;   // uint32s between tickets: one 128-B line each (atomics on
+                                          // one line serialise; 64 tickets in two lines cost k_xbtile 30 us)
 
 struct XBuild {
     const uint8_t *arena;
@@ -417,7 +419,7 @@ struct XBuild {
     unsigned long long *tbyt;       // [world][ntiles] -> exclusive scan over t within its group
     uint32_t *gcnt;                 // [world][ngroups] -> exclusive scan over the groups
     unsigned long long *gbyt;       // [world][ngroups]
-    uint32_t *ticket;               // [ngroups + 1], zero between builds
+    uint32_t *ticket;               // [(ngroups + 1) x kXTicketStride], zero between builds
     uint32_t ngroups;
     uint32_t *seg_n;                // [world]
     unsigned long long *seg_bytes;  // [world]
@@ -575,7 +577,7 @@ __global__ __launch_bounds__(kXTile) void k_xbtile(XBuild B) {
     // the last tile of group g to finish: in-group exclusive prefixes, the group's totals
     const uint32_t g = t / kXGroup, g0 = g * kXGroup;
     const uint32_t gt = B.ntiles - g0 < kXGroup ? B.ntiles - g0 : kXGroup;
-    if (!xlast(B.ticket + g, gt, &s_flag)) return;
+    if (!xlast(B.ticket + (size_t)g * kXTicketStride, gt, &s_flag)) return;
     for (uint32_t d = wave; d < B.world; d += kXTile / 64) {
         const size_t at = (size_t)d * B.ntiles + g0 + lane;
         const uint32_t c = lane < gt ? xld32(B.tcnt + at) : 0u;
@@ -591,9 +593,9 @@ __global__ __launch_bounds__(kXTile) void k_xbtile(XBuild B) {
             xst64(B.gbyt + (size_t)d * B.ngroups + g, bi);
         }
     }
-    if (threadIdx.x == 0) B.ticket[g] = 0u;      // every tile of the group has taken its turn
+    if (threadIdx.x == 0) B.ticket[(size_t)g * kXTicketStride] = 0u;   // every tile of the group has taken its turn
     // the last group to finish: exclusive prefixes over the groups, the totals
-    if (!xlast(B.ticket + B.ngroups, B.ngroups, &s_flag)) return;
+    if (!xlast(B.ticket + (size_t)B.ngroups * kXTicketStride, B.ngroups, &s_flag)) return;
     for (uint32_t d = wave; d < B.world; d += kXTile / 64) {
         uint32_t run = 0;
         uint64_t runb = 0;
@@ -620,7 +622,7 @@ __global__ __launch_bounds__(kXTile) void k_xbtile(XBuild B) {
                         (run > B.fix_recs || runb > B.fix_bytes) ? 1u : 0u};
         }
     }
-    if (threadIdx.x == 0) B.ticket[B.ngroups] = 0u;
+    if (threadIdx.x == 0) B.ticket[(size_t)B.ngroups * kXTicketStride] = 0u;
 }
 
 // An empty batch (no tile): every owner's totals 0 (and the fixed layout's headers).

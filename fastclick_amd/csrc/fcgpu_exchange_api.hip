@@ -98,8 +98,8 @@ static int xbuild_scratch(fcgpu_ctx *c) {
     if (e == hipSuccess) e = hipMalloc(&c->x_segb, sizeof(unsigned long long) * FCGPU_MAX_PORTS);
     if (e == hipSuccess) e = hipMalloc(&c->x_gcnt, sizeof(uint32_t) * FCGPU_MAX_PORTS * ng);
     if (e == hipSuccess) e = hipMalloc(&c->x_gbyt, sizeof(unsigned long long) * FCGPU_MAX_PORTS * ng);
-    if (e == hipSuccess) e = hipMalloc(&c->x_ticket, sizeof(uint32_t) * ng);
-    if (e == hipSuccess) e = memset_sync(c->x_ticket, 0, sizeof(uint32_t) * ng);
+    if (e == hipSuccess) e = hipMalloc(&c->x_ticket, sizeof(uint32_t) * kXTicketStride * ng);
+    if (e == hipSuccess) e = memset_sync(c->x_ticket, 0, sizeof(uint32_t) * kXTicketStride * ng);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         for (void *p : {(void *)c->x_tcnt, (void *)c->x_tbyt, (void *)c->x_segn, (void *)c->x_segb,
