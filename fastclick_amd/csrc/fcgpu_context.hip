@@ -166,9 +166,6 @@ void fcgpu_close(fcgpu_ctx *c) {
         hipFree(c->x_tbyt);
         hipFree(c->x_segn);
         hipFree(c->x_segb);
-        hipFree(c->x_gcnt);
-        hipFree(c->x_gbyt);
-        hipFree(c->x_ticket);
         pool_release(c);
         for (auto e : c->flow_order)
             if (e) hipEventDestroy(e);

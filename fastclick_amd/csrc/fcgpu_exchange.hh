@@ -388,39 +388,28 @@ __global__ __launch_bounds__(kXThreads) void k_xpack(XPack X) {
 // earlier ones of d, and the tiles follow each other:
 //
 //   k_xbtile  per tile: packets and slot bytes of every owner
-//             -> tcnt[d][t], tbyt[d][t]; then the scan over the tiles in two
-//             levels inside the same launch (round 6; a third launch,
-//             k_xbscan, did it before): the last block to finish a group of
-//             kXGroup tiles (a ticket per group) turns its group's counts
-//             into exclusive prefixes within the group and writes the group's
-//             totals; the last group to finish (a ticket over the groups)
-//             scans the groups -> gcnt[d][g], gbyt[d][g], seg_n[d],
-//             seg_bytes[d] (and the fixed layout's headers). Tickets only:
-//             no block waits for another, so nothing assumes forward progress
-//             of other workgroups; each last block resets its ticket.
+//             -> tcnt[d][t], tbyt[d][t]
+//   k_xbscan  one workgroup per owner: exclusive scans of both over the
+//             tiles (the tile's first record / byte within the owner's run),
+//             seg_n[d], seg_bytes[d] (round 6 measured the scan folded into
+//             k_xbtile's last blocks instead -- ticketed, two levels, no
+//             third launch: 53.5 against 52.8 us for C4, 191.5 against 191.0
+//             for C3, so the launch stays; profiles/r06_exchange/)
 //   k_xbuild  per tile again: every leaving packet's record at its place in
-//             owner order (tile prefix = group prefix + in-group prefix),
-//             then the tile's frames copied into their slots, owner by owner
-//             (consecutive destinations), LPF lanes a frame
+//             owner order, then the tile's frames copied into their slots,
+//             owner by owner (consecutive destinations), LPF lanes a frame
 //
 // Every per-packet load (verdict, descriptor) is coalesced in input order;
 // the frames are read once and written once.
 constexpr uint32_t kXTile = 256;
-constexpr uint32_t kXGroup = 64;    // tiles per group of the two-level scan (one per lane of a wave)
-constexpr uint32_t kXTicketStride = 32;   // uint32s between tickets: one 128-B line each (atomics on
-                                          // one line serialise; 64 tickets in two lines cost k_xbtile 30 us)
 
 struct XBuild {
     const uint8_t *arena;
     const uint32_t *desc;           // [n][2]
     const uint16_t *verdict;        // [n] reason | port << 8
     uint32_t n, ntiles, world, rank;
-    uint32_t *tcnt;                 // [world][ntiles] -> exclusive scan over t within its group
-    unsigned long long *tbyt;       // [world][ntiles] -> exclusive scan over t within its group
-    uint32_t *gcnt;                 // [world][ngroups] -> exclusive scan over the groups
-    unsigned long long *gbyt;       // [world][ngroups]
-    uint32_t *ticket;               // [(ngroups + 1) x kXTicketStride], zero between builds
-    uint32_t ngroups;
+    uint32_t *tcnt;                 // [world][ntiles] -> exclusive scan over t
+    unsigned long long *tbyt;       // [world][ntiles] -> exclusive scan over t
     uint32_t *seg_n;                // [world]
     unsigned long long *seg_bytes;  // [world]
     uint4 *meta;                    // fcgpu_xmeta [m] (dword-aligned)
@@ -519,119 +508,78 @@ __device__ __forceinline__ void xtile_sort(const XBuild &B, uint32_t t, XTileLds
     intra = own < B.world ? L.pre[pos] - L.pre[L.tstart[own]] : 0u;
 }
 
-// What one workgroup writes for another (the tickets' last blocks) goes
-// through agent-scope relaxed atomic stores and loads: coherent across the
-// XCDs' L2s without a release/acquire fence -- an agent-scope fence writes
-// back the whole L2 of the XCD (buffer_wbl2), which per workgroup made
-// k_xbtile 45x slower (7.5 -> 340 us, profiles/r06_exchange/).
-__device__ __forceinline__ uint32_t xld32(const uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t xld64(const unsigned long long *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void xst32(uint32_t *p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void xst64(unsigned long long *p, uint64_t v) {
-    __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// inclusive scan over the 64 lanes of a wave (64-bit)
-__device__ __forceinline__ uint64_t xwave_incl64(uint64_t x) {
-    const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t u = __shfl_up(x, o);
-        if (lane >= (uint32_t)o) x += u;
-    }
-    return x;
-}
-// this workgroup's turn at a ticket: true for the last of `parties`. The
-// block's atomic stores have completed (vmcnt 0: acknowledged at the agent's
-// coherence point) before its ticket is taken, so the last block's atomic
-// loads after its ticket see every other block's.
-__device__ __forceinline__ bool xlast(uint32_t *ticket, uint32_t parties, uint32_t *s_flag) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-        *s_flag = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == parties - 1;
-    __syncthreads();
-    return *s_flag != 0;
-}
-
 __global__ __launch_bounds__(kXTile) void k_xbtile(XBuild B) {
     __shared__ XTileLds L;
-    __shared__ uint32_t s_flag;
     uint32_t own, len, src, pos, intra;
     const uint32_t t = blockIdx.x;
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     xtile_sort(B, t, L, own, len, src, pos, intra);
-    {
-        const uint32_t d = threadIdx.x;
-        if (d < B.world) {
-            const uint32_t a = L.tstart[d], c = L.tcnt[d];
-            xst32(B.tcnt + (size_t)d * B.ntiles + t, c);
-            xst64(B.tbyt + (size_t)d * B.ntiles + t, L.pre[a + c] - L.pre[a]);
-        }
+    const uint32_t d = threadIdx.x;
+    if (d < B.world) {
+        const uint32_t a = L.tstart[d], c = L.tcnt[d];
+        B.tcnt[(size_t)d * B.ntiles + t] = c;
+        B.tbyt[(size_t)d * B.ntiles + t] = L.pre[a + c] - L.pre[a];
     }
-    // the last tile of group g to finish: in-group exclusive prefixes, the group's totals
-    const uint32_t g = t / kXGroup, g0 = g * kXGroup;
-    const uint32_t gt = B.ntiles - g0 < kXGroup ? B.ntiles - g0 : kXGroup;
-    if (!xlast(B.ticket + (size_t)g * kXTicketStride, gt, &s_flag)) return;
-    for (uint32_t d = wave; d < B.world; d += kXTile / 64) {
-        const size_t at = (size_t)d * B.ntiles + g0 + lane;
-        const uint32_t c = lane < gt ? xld32(B.tcnt + at) : 0u;
-        const uint64_t b = lane < gt ? xld64(B.tbyt + at) : 0ull;
-        const uint32_t ci = xwave_incl(c);
-        const uint64_t bi = xwave_incl64(b);
-        if (lane < gt) {
-            B.tcnt[at] = ci - c;
-            B.tbyt[at] = bi - b;
-        }
-        if (lane == 63) {
-            xst32(B.gcnt + (size_t)d * B.ngroups + g, ci);
-            xst64(B.gbyt + (size_t)d * B.ngroups + g, bi);
-        }
-    }
-    if (threadIdx.x == 0) B.ticket[(size_t)g * kXTicketStride] = 0u;   // every tile of the group has taken its turn
-    // the last group to finish: exclusive prefixes over the groups, the totals
-    if (!xlast(B.ticket + (size_t)B.ngroups * kXTicketStride, B.ngroups, &s_flag)) return;
-    for (uint32_t d = wave; d < B.world; d += kXTile / 64) {
-        uint32_t run = 0;
-        uint64_t runb = 0;
-        for (uint32_t h0 = 0; h0 < B.ngroups; h0 += 64) {
-            const uint32_t h = h0 + lane;
-            const size_t at = (size_t)d * B.ngroups + h;
-            const uint32_t c = h < B.ngroups ? xld32(B.gcnt + at) : 0u;
-            const uint64_t b = h < B.ngroups ? xld64(B.gbyt + at) : 0ull;
-            const uint32_t ci = xwave_incl(c);
-            const uint64_t bi = xwave_incl64(b);
-            if (h < B.ngroups) {
-                B.gcnt[at] = run + ci - c;
-                B.gbyt[at] = runb + bi - b;
-            }
-            run += __shfl(ci, 63);
-            runb += __shfl(bi, 63);
-        }
-        if (lane == 0) {
-            B.seg_n[d] = run;
-            B.seg_bytes[d] = runb;
-            if (B.fix_recs)      // the segment's header (fcgpu_xseg): packets, bytes, overflow
-                *reinterpret_cast<xu4 *>(B.meta + (size_t)d * (B.fix_recs + 1)) =
-                    xu4{run, (uint32_t)runb, (uint32_t)(runb >> 32),
-                        (run > B.fix_recs || runb > B.fix_bytes) ? 1u : 0u};
-        }
-    }
-    if (threadIdx.x == 0) B.ticket[(size_t)B.ngroups * kXTicketStride] = 0u;
 }
 
-// An empty batch (no tile): every owner's totals 0 (and the fixed layout's headers).
-__global__ void k_xbempty(XBuild B) {
-    const uint32_t d = threadIdx.x;
-    if (d >= B.world) return;
-    B.seg_n[d] = 0;
-    B.seg_bytes[d] = 0;
-    if (B.fix_recs) *reinterpret_cast<xu4 *>(B.meta + (size_t)d * (B.fix_recs + 1)) = xu4{0u, 0u, 0u, 0u};
+// owner d = blockIdx.x: exclusive scans over the tiles, in place; the totals
+__global__ __launch_bounds__(1024) void k_xbscan(XBuild B) {
+    __shared__ unsigned long long s_w[16];
+    __shared__ uint32_t s_c[16];
+    const uint32_t d = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t *cnt = B.tcnt + (size_t)d * B.ntiles;
+    unsigned long long *byt = B.tbyt + (size_t)d * B.ntiles;
+    const uint32_t per = (B.ntiles + 1023) / 1024, beg = threadIdx.x * per;
+    uint32_t cs = 0;
+    uint64_t bs = 0;
+    for (uint32_t k = 0; k < per; ++k)
+        if (beg + k < B.ntiles) {
+            cs += cnt[beg + k];
+            bs += byt[beg + k];
+        }
+    uint32_t ci = cs;
+    uint64_t bi = bs;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(ci, o);
+        const uint64_t ub = __shfl_up(bi, o);
+        if (lane >= (uint32_t)o) {
+            ci += u;
+            bi += ub;
+        }
+    }
+    if (lane == 63) {
+        s_c[wave] = ci;
+        s_w[wave] = bi;
+    }
+    __syncthreads();
+    uint32_t cp = 0, ct = 0;
+    uint64_t bp = 0, bt = 0;
+    for (uint32_t w = 0; w < 16; ++w) {
+        if (w < wave) {
+            cp += s_c[w];
+            bp += s_w[w];
+        }
+        ct += s_c[w];
+        bt += s_w[w];
+    }
+    uint32_t cr = cp + ci - cs;
+    uint64_t br = bp + bi - bs;
+    for (uint32_t k = 0; k < per; ++k)
+        if (beg + k < B.ntiles) {
+            const uint32_t c = cnt[beg + k];
+            const uint64_t b = byt[beg + k];
+            cnt[beg + k] = cr;
+            byt[beg + k] = br;
+            cr += c;
+            br += b;
+        }
+    if (threadIdx.x == 0) {
+        B.seg_n[d] = ct;
+        B.seg_bytes[d] = bt;
+        if (B.fix_recs)      // the segment's header (fcgpu_xseg): packets, bytes, overflow
+            *reinterpret_cast<xu4 *>(B.meta + (size_t)d * (B.fix_recs + 1)) =
+                xu4{ct, (uint32_t)bt, (uint32_t)(bt >> 32), (ct > B.fix_recs || bt > B.fix_bytes) ? 1u : 0u};
+    }
 }
 
 __global__ __launch_bounds__(kXTile) void k_xbuild(XBuild B) {
@@ -644,13 +592,12 @@ __global__ __launch_bounds__(kXTile) void k_xbuild(XBuild B) {
     __shared__ uint32_t s_tc[FCGPU_MAX_PORTS];              // the tile's first record / byte within each owner's run
     __shared__ unsigned long long s_tb[FCGPU_MAX_PORTS];
     const uint32_t t = blockIdx.x;
-    // the tile's bases within each owner's run (second wave: the group's
-    // prefix + the tile's within its group) and the owners' record and byte
+    // the tile's scanned bases (second wave) and the owners' record and byte
     // bases (first wave), loaded before the sort so their latency hides under it
     if (threadIdx.x >= 64 && threadIdx.x < 64 + B.world) {
-        const uint32_t d = threadIdx.x - 64, g = t / kXGroup;
-        s_tc[d] = B.gcnt[(size_t)d * B.ngroups + g] + B.tcnt[(size_t)d * B.ntiles + t];
-        s_tb[d] = B.gbyt[(size_t)d * B.ngroups + g] + B.tbyt[(size_t)d * B.ntiles + t];
+        const uint32_t d = threadIdx.x - 64;
+        s_tc[d] = B.tcnt[(size_t)d * B.ntiles + t];
+        s_tb[d] = B.tbyt[(size_t)d * B.ntiles + t];
     }
     if (threadIdx.x < 64) {
         const uint32_t lane = threadIdx.x;

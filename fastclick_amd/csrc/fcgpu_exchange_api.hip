@@ -82,57 +82,37 @@ int fcgpu_exchange_pack(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_
     return FCGPU_OK;
 }
 
-// The build's scratch: per-tile counts and bytes ([64][max_tiles]), per-group
-// sums ([64][max_groups]), the group tickets (zeroed here once; every build
-// leaves them zero) and the per-owner totals -- allocated together on first
-// use, or not at all (a failed allocation leaves none, so the next call
-// allocates again instead of launching with a null one).
-static uint32_t xgroups(uint32_t tiles) { return (tiles + kXGroup - 1) / kXGroup; }
+// The build's per-tile scratch ([64][max_tiles] counts and bytes) and the
+// per-owner totals: allocated together on first use, or not at all (a failed
+// allocation leaves none, so the next call allocates again instead of
+// launching with a null one).
 static int xbuild_scratch(fcgpu_ctx *c) {
-    if (c->x_tcnt && c->x_tbyt && c->x_segn && c->x_segb && c->x_gcnt && c->x_gbyt && c->x_ticket) return FCGPU_OK;
-    const size_t ng = xgroups(c->max_tiles) + 1;
+    if (c->x_tcnt && c->x_tbyt && c->x_segn && c->x_segb) return FCGPU_OK;
     hipError_t e = hipMalloc(&c->x_tcnt, sizeof(uint32_t) * (size_t)FCGPU_MAX_PORTS * c->max_tiles);
     if (e == hipSuccess)
         e = hipMalloc(&c->x_tbyt, sizeof(unsigned long long) * (size_t)FCGPU_MAX_PORTS * c->max_tiles);
     if (e == hipSuccess) e = hipMalloc(&c->x_segn, sizeof(uint32_t) * FCGPU_MAX_PORTS);
     if (e == hipSuccess) e = hipMalloc(&c->x_segb, sizeof(unsigned long long) * FCGPU_MAX_PORTS);
-    if (e == hipSuccess) e = hipMalloc(&c->x_gcnt, sizeof(uint32_t) * FCGPU_MAX_PORTS * ng);
-    if (e == hipSuccess) e = hipMalloc(&c->x_gbyt, sizeof(unsigned long long) * FCGPU_MAX_PORTS * ng);
-    if (e == hipSuccess) e = hipMalloc(&c->x_ticket, sizeof(uint32_t) * kXTicketStride * ng);
-    if (e == hipSuccess) e = memset_sync(c->x_ticket, 0, sizeof(uint32_t) * kXTicketStride * ng);
     if (e != hipSuccess) {
         (void)hipGetLastError();
-        for (void *p : {(void *)c->x_tcnt, (void *)c->x_tbyt, (void *)c->x_segn, (void *)c->x_segb,
-                        (void *)c->x_gcnt, (void *)c->x_gbyt, (void *)c->x_ticket})
-            hipFree(p);
+        for (void *p : {(void *)c->x_tcnt, (void *)c->x_tbyt, (void *)c->x_segn, (void *)c->x_segb}) hipFree(p);
         c->x_tcnt = nullptr;
         c->x_tbyt = nullptr;
         c->x_segn = nullptr;
         c->x_segb = nullptr;
-        c->x_gcnt = nullptr;
-        c->x_gbyt = nullptr;
-        c->x_ticket = nullptr;
         return fail(c, FCGPU_ENOMEM, std::string("fcgpu_exchange_build scratch: ") + hipGetErrorString(e));
     }
     return FCGPU_OK;
 }
 
-// k_xbtile (counts, then the two-level scan in its last blocks) -> k_xbuild,
-// over B (counted or fixed layout); an empty batch only writes zero totals.
+// k_xbtile -> k_xbscan -> k_xbuild over B (counted or fixed layout).
 static int xbuild_launch(fcgpu_ctx *c, XBuild &B, hipStream_t s) {
     B.ntiles = (B.n + kXTile - 1) / kXTile;
-    B.ngroups = xgroups(B.ntiles);
     B.tcnt = c->x_tcnt;
     B.tbyt = c->x_tbyt;
-    B.gcnt = c->x_gcnt;
-    B.gbyt = c->x_gbyt;
-    B.ticket = c->x_ticket;
-    if (B.ntiles) {
-        hipLaunchKernelGGL(k_xbtile, dim3(B.ntiles), dim3(kXTile), 0, s, B);
-        hipLaunchKernelGGL(k_xbuild, dim3(B.ntiles), dim3(kXTile), 0, s, B);   // lanes per frame: per tile
-    } else {
-        hipLaunchKernelGGL(k_xbempty, dim3(1), dim3(64), 0, s, B);
-    }
+    if (B.ntiles) hipLaunchKernelGGL(k_xbtile, dim3(B.ntiles), dim3(kXTile), 0, s, B);
+    hipLaunchKernelGGL(k_xbscan, dim3(B.world), dim3(1024), 0, s, B);    // n = 0: zero counts
+    if (B.ntiles) hipLaunchKernelGGL(k_xbuild, dim3(B.ntiles), dim3(kXTile), 0, s, B);   // lanes per frame: per tile
     HIPCHK(c, hipGetLastError());
     return FCGPU_OK;
 }

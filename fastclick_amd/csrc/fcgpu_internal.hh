@@ -282,9 +282,6 @@ struct fcgpu_ctx {
     unsigned long long *x_tbyt = nullptr;
     uint32_t *x_segn = nullptr;               // fcgpu_exchange_build_fixed: per-owner totals (scratch)
     unsigned long long *x_segb = nullptr;
-    uint32_t *x_gcnt = nullptr;               // [64][max groups] the build's group sums, then prefixes
-    unsigned long long *x_gbyt = nullptr;
-    uint32_t *x_ticket = nullptr;             // [max groups + 1] zero between builds
     std::string err;
 };
 
