@@ -207,6 +207,13 @@ for s in "${ST[@]}"; do
     # round 6: the fixed re-shard's host time per stage and its kernel trace
     r6reshost) FCGPU_RESHARD_HOST=1 step reshard1_fixed_host 300 python bench.py --flow-reshard --workload c4 --steps 50 --warmup 5 --no-cpu &&
                kt kt_reshard_fixed 300 --flow-reshard --workload c4 --steps 10 --warmup 2 --no-cpu ;;
+    # round 6: the final re-shard rates (fixed and counted interleaved, host times, overflow, 8-rank shape)
+    r6reshard2) for k in 1 2 3; do
+                  FCGPU_RESHARD_HOST=1 step "reshard1_fixed_f$k" 300 python bench.py --flow-reshard --workload c4 --steps 50 --warmup 5 --no-cpu &&
+                  step "reshard1_counted_f$k" 300 python bench.py --flow-reshard --workload c4 --steps 50 --warmup 5 --no-cpu --reshard-exchange counted || exit $?
+                done &&
+                step reshard1_overflow_f 300 python bench.py --flow-reshard --workload c4 --steps 20 --warmup 2 --no-cpu --reshard-slack 0.5 &&
+                step reshard8_fixed_f 900 python bench.py --gpus 8 --backend gloo --flow-reshard --workload c4 --steps 5 --warmup 1 --no-cpu ;;
     # round 6: the wire layouts' own ceiling (bare window gather vs k_rx, same box)
     r6gather) step gather_bound 600 python scripts/gather_bound.py ;;
     *) echo "unknown step $s"; exit 2 ;;
