@@ -214,6 +214,12 @@ for s in "${ST[@]}"; do
                 done &&
                 step reshard1_overflow_f 300 python bench.py --flow-reshard --workload c4 --steps 20 --warmup 2 --no-cpu --reshard-slack 0.5 &&
                 step reshard8_fixed_f 900 python bench.py --gpus 8 --backend gloo --flow-reshard --workload c4 --steps 5 --warmup 1 --no-cpu ;;
+    # round 6: k_xbuild's copy loop, 4 / 8 chunks in flight per lane, plain / non-temporal source loads
+    r6xcopy) for k in 1 2; do
+               for v in 4 8 4nt 8nt; do
+                 FCGPU_XBUILD=$v step "xcopy_${v}_$k" 300 python scripts/exchange_rate.py --reps 30 || exit $?
+               done
+             done ;;
     # round 6: the wire layouts' own ceiling (bare window gather vs k_rx, same box)
     r6gather) step gather_bound 600 python scripts/gather_bound.py ;;
     *) echo "unknown step $s"; exit 2 ;;
