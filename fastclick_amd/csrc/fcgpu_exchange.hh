@@ -582,7 +582,6 @@ __global__ __launch_bounds__(1024) void k_xbscan(XBuild B) {
     }
 }
 
-template <uint32_t KU = 4, bool NTL = false>
 __global__ __launch_bounds__(kXTile) void k_xbuild(XBuild B) {
     __shared__ XTileLds L;
     __shared__ uint32_t s_src[kXTile], s_len[kXTile];
@@ -640,7 +639,9 @@ __global__ __launch_bounds__(kXTile) void k_xbuild(XBuild B) {
     // stores are 1 KB contiguous but at owner boundaries.
     const uint32_t nl = L.tstart[B.world];
     const uint32_t nch = L.pre[nl] >> 4;
-    constexpr uint32_t kU = KU;
+    // (8 chunks in flight per lane, and non-temporal source loads, measured
+    // slower: C4 55.7 / 55.3 / 59.6 against 52.4 us, profiles/r06_exchange/xcopy/)
+    constexpr uint32_t kU = 4;
     for (uint32_t c0 = threadIdx.x; c0 < nch; c0 += kXTile * kU) {
         xu4 a[kU];
         uint32_t e[kU], fr[kU], off[kU];
@@ -665,7 +666,7 @@ __global__ __launch_bounds__(kXTile) void k_xbuild(XBuild B) {
                 const uint8_t *p = B.arena + s_src[lo] + off[k];
                 const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3u);
                 xg32 *al = xgbase(p, sh);
-                a[k] = NTL ? __builtin_nontemporal_load((xg4 *)al) : *(xg4 *)al;
+                a[k] = *(xg4 *)al;
                 // the fifth dword only when the frame reaches into it (so no
                 // read goes further than 16 B past the frame's end)
                 if (sh && off[k] + 16 - sh < fl) e[k] = al[4];

@@ -112,19 +112,7 @@ static int xbuild_launch(fcgpu_ctx *c, XBuild &B, hipStream_t s) {
     B.tbyt = c->x_tbyt;
     if (B.ntiles) hipLaunchKernelGGL(k_xbtile, dim3(B.ntiles), dim3(kXTile), 0, s, B);
     hipLaunchKernelGGL(k_xbscan, dim3(B.world), dim3(1024), 0, s, B);    // n = 0: zero counts
-    // FCGPU_XBUILD=4|8|4nt|8nt: chunks in flight per lane, non-temporal
-    // source loads (a same-box A/B, round 6)
-    static const int v = [] {
-        const char *e = getenv("FCGPU_XBUILD");
-        if (!e) return 0;
-        return (!strcmp(e, "8") ? 1 : 0) + (!strcmp(e, "4nt") ? 2 : 0) + (!strcmp(e, "8nt") ? 3 : 0);
-    }();
-    if (B.ntiles) {
-        if (v == 1) hipLaunchKernelGGL((k_xbuild<8, false>), dim3(B.ntiles), dim3(kXTile), 0, s, B);
-        else if (v == 2) hipLaunchKernelGGL((k_xbuild<4, true>), dim3(B.ntiles), dim3(kXTile), 0, s, B);
-        else if (v == 3) hipLaunchKernelGGL((k_xbuild<8, true>), dim3(B.ntiles), dim3(kXTile), 0, s, B);
-        else hipLaunchKernelGGL((k_xbuild<4, false>), dim3(B.ntiles), dim3(kXTile), 0, s, B);
-    }
+    if (B.ntiles) hipLaunchKernelGGL(k_xbuild, dim3(B.ntiles), dim3(kXTile), 0, s, B);   // lanes per frame: per tile
     HIPCHK(c, hipGetLastError());
     return FCGPU_OK;
 }
