@@ -44,11 +44,13 @@ def main():
         line = json.loads([x for x in rb.stdout.splitlines() if x.startswith("{")][-1])
         k = line["roofline"]["kernel_ms"] * 1e3
         bare, bare_out = g["gather"]["us_per_batch"], g["gather+outputs"]["us_per_batch"]
+        more = {k: g[k]["us_per_batch"] for k in ("gather+packed", "gather+vh", "gather+tperm") if k in g}
         print(json.dumps({"workload": w, "packets": b.n, "arena_bytes": int(b.arena.nbytes),
                           "k_rx_us": round(k, 2), "bare_gather_us": bare, "gather_plus_outputs_us": bare_out,
                           "k_rx_over_bare_gather": round(k / bare, 3),
                           "k_rx_over_gather_plus_outputs": round(k / bare_out, 3),
                           "k_rx_roofline_frac": line["roofline"]["frac"], "nbuf_gather": g["gather"]["nbuf"],
+                          "store_variants_us": more,
                           "bench_hbm_batches": line["config"].get("hbm_batches")}), flush=True)
 
 

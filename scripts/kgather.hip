@@ -10,7 +10,10 @@
 // addresses, order and cache policy) -- and nothing else: one dword of each
 // window is folded into a per-workgroup word so the loads are not dead.
 // Variant "+outputs" also stores what the bench's k_rx stores per packet
-// (verdict 2 B, hash 4 B, tile_perm 1 B, non-temporal; per-tile counts).
+// (verdict 2 B, hash 4 B, tile_perm 1 B, non-temporal; per-tile counts);
+// "+packed" stores verdict and hash as one 8-B word per packet instead (the
+// question whether one fuller store per lane costs less than two); "+vh"
+// the verdict and hash alone, "+tperm" the tile permutation and counts alone.
 // The batch comes from scripts/gather_bound.py: its descriptors (uint32
 // pairs) in a file, the arena's size; the arena's contents do not matter for
 // the line pattern. As many arena + descriptor copies as keep 1.2 GB in
@@ -34,7 +37,7 @@ struct Batches {
     const uint8_t *arena[kFuse];
     const uint2 *desc[kFuse];
 };
-template <bool OUT>
+template <int OUT>
 __global__ __launch_bounds__(kTile, 8) void k_gather(Batches B, uint32_t tiles, uint32_t n, uint32_t *fold,
                                                     uint16_t *verdict, uint32_t *hash, uint8_t *tperm,
                                                     uint16_t *tcount) {
@@ -53,13 +56,16 @@ __global__ __launch_bounds__(kTile, 8) void k_gather(Batches B, uint32_t tiles, 
     __builtin_amdgcn_wave_barrier();
     const uint32_t w = *reinterpret_cast<const uint32_t *>(wl + (lane >> 4) * 1024 + (lane & 15) * 64);
     const uint32_t x = w ^ d.y;
-    if (OUT && i < n) {
-        st_nt(verdict + i, (uint16_t)(x & 0xff));
-        st_nt(hash + i, x);
-        st_nt(tperm + i, (uint8_t)threadIdx.x);
+    if (i < n) {
+        if (OUT == 1 || OUT == 3) {
+            st_nt(verdict + i, (uint16_t)(x & 0xff));
+            st_nt(hash + i, x);
+        }
+        if (OUT == 2) st_nt(reinterpret_cast<uint64_t *>(hash) + i, (uint64_t)x << 32 | (x & 0xff));
+        if (OUT == 1 || OUT == 2 || OUT == 4) st_nt(tperm + i, (uint8_t)threadIdx.x);
     }
     const uint64_t m = __ballot(x == 0x9e3779b9u);      // never true: keeps the loads live
-    if (OUT && threadIdx.x < 17) tcount[(size_t)tile * 17 + threadIdx.x] = (uint16_t)m;
+    if ((OUT == 1 || OUT == 2 || OUT == 4) && threadIdx.x < 17) tcount[(size_t)tile * 17 + threadIdx.x] = (uint16_t)m;
     if (m && lane == 0) fold[tile] = x;
 }
 
@@ -95,25 +101,26 @@ int main(int argc, char **argv) {
     uint8_t *tperm;
     CK(hipMalloc(&fold, 4ull * tiles));
     CK(hipMalloc(&verdict, 2ull * n));
-    CK(hipMalloc(&hash, 4ull * n));
+    CK(hipMalloc(&hash, 8ull * n));
     CK(hipMalloc(&tperm, (size_t)n + kTile));
     CK(hipMalloc(&tcount, 2ull * 17 * tiles));
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    for (int out = 0; out < 2; ++out) {
+    typedef void (*Kern)(Batches, uint32_t, uint32_t, uint32_t *, uint16_t *, uint32_t *, uint8_t *, uint16_t *);
+    struct V { const char *name; Kern k; } vs[] = {
+        {"gather", k_gather<0>}, {"gather+outputs", k_gather<1>}, {"gather+packed", k_gather<2>},
+        {"gather+vh", k_gather<3>}, {"gather+tperm", k_gather<4>},
+    };
+    for (auto &v : vs) {
         auto launch = [&](int r) {
             Batches B;
             for (uint32_t k = 0; k < kFuse; ++k) {
                 B.arena[k] = ar[(r * kFuse + k) % nbuf];
                 B.desc[k] = de[(r * kFuse + k) % nbuf];
             }
-            if (out)
-                hipLaunchKernelGGL(k_gather<true>, dim3(tiles * kFuse), dim3(kTile), 0, 0, B, tiles, n, fold, verdict,
-                                   hash, tperm, tcount);
-            else
-                hipLaunchKernelGGL(k_gather<false>, dim3(tiles * kFuse), dim3(kTile), 0, 0, B, tiles, n, fold,
-                                   verdict, hash, tperm, tcount);
+            hipLaunchKernelGGL(v.k, dim3(tiles * kFuse), dim3(kTile), 0, 0, B, tiles, n, fold, verdict, hash, tperm,
+                               tcount);
         };
         for (int r = 0; r < 8; ++r) launch(r);
         CK(hipDeviceSynchronize());
@@ -125,7 +132,7 @@ int main(int argc, char **argv) {
         CK(hipEventElapsedTime(&ms, a, b));
         printf("{\"variant\": \"%s\", \"us_per_batch\": %.3f, \"nbuf\": %u, \"launches\": %d, "
                "\"batches_per_launch\": %u}\n",
-               out ? "gather+outputs" : "gather", ms * 1e3 / (reps * kFuse), nbuf, reps, kFuse);
+               v.name, ms * 1e3 / (reps * kFuse), nbuf, reps, kFuse);
     }
     return 0;
 }
