@@ -15,7 +15,7 @@ LIBFCGPU = os.environ.get("FCGPU_LIB") or os.path.join(LIB_DIR, "libfcgpu.so")
 LIBFCCLICK = os.path.join(LIB_DIR, "libfcclick.so")
 
 # ---- constants mirrored from include/fastclick_gpu.h -----------------------
-ABI_VERSION = 24
+ABI_VERSION = 25
 SPAN_SLOTS = 3
 SPAN_COPY = 0
 SPAN_ZEROCOPY = 1
@@ -49,7 +49,7 @@ OUT_VERDICT, OUT_HASH, OUT_ANNO, OUT_PERM, OUT_PORT_START, OUT_TILE_COUNT, OUT_T
     OUT_IP_RW, OUT_ANNO8 = (1 << k for k in range(10))
 SUBMIT_COPY = 1 << 31
 SUBMIT_DESC32 = 1 << 30
-FAULT_SUBMIT, FAULT_WAIT, FAULT_LAUNCH = 0, 1, 2
+FAULT_SUBMIT, FAULT_WAIT, FAULT_LAUNCH, FAULT_ALLOC = 0, 1, 2, 3
 OUT_ABSENT = (1 << 64) - 1
 TILE = 256
 

@@ -69,7 +69,7 @@ hipEvent_t take_event(fcgpu_ctx *c) {
 
 static std::atomic<uint32_t> g_fault_armed{0};     // bit k: kind k has events to skip or fail
 static std::mutex g_fault_mu;
-static uint32_t g_fault_skip[3], g_fault_count[3];
+static uint32_t g_fault_skip[4], g_fault_count[4];
 bool fault_take(uint32_t where) {
     if (!(g_fault_armed.load(std::memory_order_relaxed) & (1u << where))) return false;
     std::lock_guard<std::mutex> g(g_fault_mu);
@@ -81,6 +81,37 @@ bool fault_take(uint32_t where) {
     }
     if (!g_fault_count[where]) g_fault_armed.fetch_and(~(1u << where), std::memory_order_relaxed);
     return hit;
+}
+
+hipError_t dev_malloc(void **p, size_t bytes) {
+    if (fault_take(FCGPU_FAULT_ALLOC)) return hipErrorOutOfMemory;
+    return hipMalloc(p, bytes);
+}
+
+hipError_t alloc_group(std::initializer_list<Scratch> g) {
+    hipError_t e = hipSuccess;
+    for (const Scratch &b : g) {
+        if (b.kind == 2) e = fault_take(FCGPU_FAULT_ALLOC) ? hipErrorOutOfMemory
+                                                           : hipHostMalloc(b.p, b.bytes, hipHostMallocDefault);
+        else e = dev_malloc(b.p, b.bytes);
+        if (e == hipSuccess && b.kind == 1) e = memset_sync(*b.p, 0, b.bytes);
+        if (e != hipSuccess) break;
+    }
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        for (const Scratch &b : g) {
+            if (*b.p) (void)(b.kind == 2 ? hipHostFree(*b.p) : hipFree(*b.p));
+            *b.p = nullptr;
+        }
+    }
+    return e;
+}
+
+int alloc_or_fail(fcgpu_ctx *c, const char *what, std::initializer_list<Scratch> g) {
+    const hipError_t e = alloc_group(g);
+    if (e == hipSuccess) return FCGPU_OK;
+    return fail(c, e == hipErrorOutOfMemory ? FCGPU_ENOMEM : FCGPU_ERUNTIME,
+                std::string(what) + ": " + hipGetErrorString(e));
 }
 
 }  // namespace fcgpu_rt
@@ -282,8 +313,13 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
                 t[256 * k + b] = x;
             }
         HIPCHK(c, hipSetDevice(c->device));
-        HIPCHK(c, hipMalloc(&c->d_crc, sizeof(uint32_t) * 512));
-        HIPCHK(c, hipMemcpy(c->d_crc, t.data(), sizeof(uint32_t) * 512, hipMemcpyHostToDevice));
+        uint4 *tab = nullptr;
+        if (int rc = alloc_or_fail(c, "CRC table", {dev_buf(tab, sizeof(uint32_t) * 512)})) return rc;
+        if (hipError_t e = hipMemcpy(tab, t.data(), sizeof(uint32_t) * 512, hipMemcpyHostToDevice)) {
+            (void)hipFree(tab);
+            return fail(c, FCGPU_ERUNTIME, std::string("CRC table upload: ") + hipGetErrorString(e));
+        }
+        c->d_crc = tab;
     }
     d.crc_tab = cfg->classify == FCGPU_CLS_LB_CRC ? c->d_crc : nullptr;
     d.lb_tab = cfg->classify == FCGPU_CLS_LB_TABLE ? c->d_lbtab : nullptr;
@@ -300,7 +336,7 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
 }
 
 int fcgpu_inject_fault(uint32_t where, uint32_t skip, uint32_t count) {
-    if (where > FCGPU_FAULT_LAUNCH) return FCGPU_EINVAL;
+    if (where > FCGPU_FAULT_ALLOC) return FCGPU_EINVAL;
     std::lock_guard<std::mutex> g(g_fault_mu);
     g_fault_skip[where] = count ? skip : 0;
     g_fault_count[where] = count;

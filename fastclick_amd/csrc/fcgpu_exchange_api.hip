@@ -21,10 +21,12 @@ int fcgpu_exchange_plan(fcgpu_ctx *c, const uint32_t *d_desc, const uint32_t *d_
     HIPCHK(c, hipSetDevice(c->device));
     const uint32_t nblk_max = (c->max_batch + kXItems - 1) / kXItems;
     if (!c->x_bsum) {
-        HIPCHK(c, hipMalloc(&c->x_bsum, sizeof(unsigned long long) * (nblk_max + 1)));
-        HIPCHK(c, hipMalloc(&c->x_base, sizeof(unsigned long long) * (FCGPU_MAX_PORTS + 1)));
-        HIPCHK(c, hipMalloc(&c->x_part, sizeof(unsigned long long) * (FCGPU_MAX_PORTS + 1)));
-        HIPCHK(c, hipMalloc(&c->x_src, sizeof(uint32_t) * ((size_t)c->max_batch + 1)));
+        const int rc = alloc_or_fail(c, "fcgpu_exchange_plan scratch",
+                                     {dev_buf(c->x_bsum, sizeof(unsigned long long) * (nblk_max + 1)),
+                                      dev_buf(c->x_base, sizeof(unsigned long long) * (FCGPU_MAX_PORTS + 1)),
+                                      dev_buf(c->x_part, sizeof(unsigned long long) * (FCGPU_MAX_PORTS + 1)),
+                                      dev_buf(c->x_src, sizeof(uint32_t) * ((size_t)c->max_batch + 1))});
+        if (rc != FCGPU_OK) return rc;
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
     XPlan P{};
@@ -87,22 +89,12 @@ int fcgpu_exchange_pack(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_
 // allocation leaves none, so the next call allocates again instead of
 // launching with a null one).
 static int xbuild_scratch(fcgpu_ctx *c) {
-    if (c->x_tcnt && c->x_tbyt && c->x_segn && c->x_segb) return FCGPU_OK;
-    hipError_t e = hipMalloc(&c->x_tcnt, sizeof(uint32_t) * (size_t)FCGPU_MAX_PORTS * c->max_tiles);
-    if (e == hipSuccess)
-        e = hipMalloc(&c->x_tbyt, sizeof(unsigned long long) * (size_t)FCGPU_MAX_PORTS * c->max_tiles);
-    if (e == hipSuccess) e = hipMalloc(&c->x_segn, sizeof(uint32_t) * FCGPU_MAX_PORTS);
-    if (e == hipSuccess) e = hipMalloc(&c->x_segb, sizeof(unsigned long long) * FCGPU_MAX_PORTS);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        for (void *p : {(void *)c->x_tcnt, (void *)c->x_tbyt, (void *)c->x_segn, (void *)c->x_segb}) hipFree(p);
-        c->x_tcnt = nullptr;
-        c->x_tbyt = nullptr;
-        c->x_segn = nullptr;
-        c->x_segb = nullptr;
-        return fail(c, FCGPU_ENOMEM, std::string("fcgpu_exchange_build scratch: ") + hipGetErrorString(e));
-    }
-    return FCGPU_OK;
+    if (c->x_tcnt) return FCGPU_OK;         // the group is all or nothing
+    return alloc_or_fail(c, "fcgpu_exchange_build scratch",
+                         {dev_buf(c->x_tcnt, sizeof(uint32_t) * (size_t)FCGPU_MAX_PORTS * c->max_tiles),
+                          dev_buf(c->x_tbyt, sizeof(unsigned long long) * (size_t)FCGPU_MAX_PORTS * c->max_tiles),
+                          dev_buf(c->x_segn, sizeof(uint32_t) * FCGPU_MAX_PORTS),
+                          dev_buf(c->x_segb, sizeof(unsigned long long) * FCGPU_MAX_PORTS)});
 }
 
 // k_xbtile -> k_xbscan -> k_xbuild over B (counted or fixed layout).

@@ -153,63 +153,72 @@ int fcgpu_flow_configure(fcgpu_ctx *c, const fcgpu_flow_config *fc) {
     HIPCHK(c, hipDeviceSynchronize());
     flow_free(c);
     if (cap == 0) return FCGPU_OK;
-    // at most max_flows IDs plus one batch of FULL markers (the batch that
-    // fills the table): keep the load at or under 1/2
-    uint32_t slots = 1024;
-    while (slots < 2 * (max_flows + c->max_batch)) slots <<= 1;
-    const uint32_t words = (c->max_batch + 63) / 64 + 1;
-    FlowArgs &F = c->fl;
-    HIPCHK(c, hipMalloc(&F.slots, sizeof(uint4) * slots));
-    HIPCHK(c, hipMalloc(&F.claim, sizeof(uint32_t) * slots));
-    HIPCHK(c, hipMalloc(&F.first, sizeof(uint32_t) * slots));
-    HIPCHK(c, hipMalloc(&F.miss_key, sizeof(uint4) * c->max_batch));
-    HIPCHK(c, hipMalloc(&F.miss_slot, sizeof(uint32_t) * c->max_batch));
-    HIPCHK(c, hipMalloc(&F.miss_first, sizeof(uint32_t) * c->max_batch));
-    HIPCHK(c, hipMalloc(&F.missmask, sizeof(uint64_t) * words));
-    HIPCHK(c, hipMalloc(&F.firstmask, sizeof(uint64_t) * words));
-    HIPCHK(c, hipMalloc(&F.wordpre, sizeof(uint32_t) * words));
-    HIPCHK(c, hipMalloc(&F.state, sizeof(uint32_t) * 16));
-    F.missed = F.state + kFsMissed;
-    if (imp) HIPCHK(c, hipMalloc(&F.stack, sizeof(uint32_t) * max_flows));
-    if (te) {
-        F.wstride = cap;
-        F.wmask = nb - 1;
-        F.te = te;
-        // lastseen stamps once per run of a flow's packets, read before they
-        // write (at 1 / 10k / 1M flows no slower than storing, 2.7 % faster at
-        // 10k, 2 % at 1M: profiles/r06_imp/summary.txt). FCGPU_LASTSEEN=
-        // run|check|packet forces one way (same-box A/B runs)
-        F.ls_mode = kLsCheck;
-        if (const char *e = getenv("FCGPU_LASTSEEN")) {
-            if (!strcmp(e, "run")) F.ls_mode = kLsRun;
-            else if (!strcmp(e, "check")) F.ls_mode = kLsCheck;
-            else if (!strcmp(e, "packet")) F.ls_mode = kLsPacket;
+    // a failure part way leaves no table: never a partial one that the next
+    // launch would use (the pointers k_rx reads are all set or all null)
+    const int rc = [&]() -> int {
+        // at most max_flows IDs plus one batch of FULL markers (the batch that
+        // fills the table): keep the load at or under 1/2
+        uint32_t slots = 1024;
+        while (slots < 2 * (max_flows + c->max_batch)) slots <<= 1;
+        const uint32_t words = (c->max_batch + 63) / 64 + 1;
+        FlowArgs &F = c->fl;
+        HIPCHK(c, dev_malloc(&F.slots, sizeof(uint4) * slots));
+        HIPCHK(c, dev_malloc(&F.claim, sizeof(uint32_t) * slots));
+        HIPCHK(c, dev_malloc(&F.first, sizeof(uint32_t) * slots));
+        HIPCHK(c, dev_malloc(&F.miss_key, sizeof(uint4) * c->max_batch));
+        HIPCHK(c, dev_malloc(&F.miss_slot, sizeof(uint32_t) * c->max_batch));
+        HIPCHK(c, dev_malloc(&F.miss_first, sizeof(uint32_t) * c->max_batch));
+        HIPCHK(c, dev_malloc(&F.missmask, sizeof(uint64_t) * words));
+        HIPCHK(c, dev_malloc(&F.firstmask, sizeof(uint64_t) * words));
+        HIPCHK(c, dev_malloc(&F.wordpre, sizeof(uint32_t) * words));
+        HIPCHK(c, dev_malloc(&F.state, sizeof(uint32_t) * 16));
+        F.missed = F.state + kFsMissed;
+        if (imp) HIPCHK(c, dev_malloc(&F.stack, sizeof(uint32_t) * max_flows));
+        if (te) {
+            F.wstride = cap;
+            F.wmask = nb - 1;
+            F.te = te;
+            // lastseen stamps once per run of a flow's packets, read before they
+            // write (at 1 / 10k / 1M flows no slower than storing, 2.7 % faster at
+            // 10k, 2 % at 1M: profiles/r06_imp/summary.txt). FCGPU_LASTSEEN=
+            // run|check|packet forces one way (same-box A/B runs)
+            F.ls_mode = kLsCheck;
+            if (const char *e = getenv("FCGPU_LASTSEEN")) {
+                if (!strcmp(e, "run")) F.ls_mode = kLsRun;
+                else if (!strcmp(e, "check")) F.ls_mode = kLsCheck;
+                else if (!strcmp(e, "packet")) F.ls_mode = kLsPacket;
+            }
+            HIPCHK(c, dev_malloc(&F.lastseen, sizeof(uint32_t) * cap));
+            HIPCHK(c, dev_malloc(&F.wheel, sizeof(uint32_t) * (size_t)nb * cap));
+            HIPCHK(c, dev_malloc(&F.wheel_len, sizeof(uint32_t) * nb));
+            HIPCHK(c, dev_malloc(&c->flow_spare, sizeof(uint4) * slots));
+            HIPCHK(c, dev_malloc(&c->maint.qbsr, sizeof(uint32_t) * cap));
+            HIPCHK(c, dev_malloc(&c->maint.dead, sizeof(uint32_t) * cap));
+            HIPCHK(c, dev_malloc(&c->maint.rbuf, sizeof(uint16_t) * cap));
+            HIPCHK(c, dev_malloc(&c->maint.counts, sizeof(uint32_t) * (size_t)((cap + kMaintChunk - 1) / kMaintChunk) *
+                                                      (te + 1)));
+            c->maint.to_ms = fc->timeout_s * 1000u;
+            c->maint.ri_ms = fc->recycle_ms;
+            c->maint.eps = eps;
         }
-        HIPCHK(c, hipMalloc(&F.lastseen, sizeof(uint32_t) * cap));
-        HIPCHK(c, hipMalloc(&F.wheel, sizeof(uint32_t) * (size_t)nb * cap));
-        HIPCHK(c, hipMalloc(&F.wheel_len, sizeof(uint32_t) * nb));
-        HIPCHK(c, hipMalloc(&c->flow_spare, sizeof(uint4) * slots));
-        HIPCHK(c, hipMalloc(&c->maint.qbsr, sizeof(uint32_t) * cap));
-        HIPCHK(c, hipMalloc(&c->maint.dead, sizeof(uint32_t) * cap));
-        HIPCHK(c, hipMalloc(&c->maint.rbuf, sizeof(uint16_t) * cap));
-        HIPCHK(c, hipMalloc(&c->maint.counts, sizeof(uint32_t) * (size_t)((cap + kMaintChunk - 1) / kMaintChunk) *
-                                                  (te + 1)));
-        c->maint.to_ms = fc->timeout_s * 1000u;
-        c->maint.ri_ms = fc->recycle_ms;
-        c->maint.eps = eps;
+        HIPCHK(c, hipHostMalloc((void **)&c->flow_hint, sizeof(uint32_t), hipHostMallocMapped));
+        for (auto &e : c->flow_order)
+            if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHK(c, hipHostGetDevicePointer((void **)&F.host_hint, c->flow_hint, 0));
+        F.mask = slots - 1;
+        F.max_flows = max_flows;
+        c->max_flows = max_flows;
+        c->flow_slots = slots;
+        c->flow_words = words;
+        c->flow_conf = *fc;
+        c->flow_conf.capacity = cap;
+        return flow_clear(c);
+    }();
+    if (rc != FCGPU_OK) {
+        (void)hipGetLastError();
+        flow_free(c);
     }
-    HIPCHK(c, hipHostMalloc((void **)&c->flow_hint, sizeof(uint32_t), hipHostMallocMapped));
-    for (auto &e : c->flow_order)
-        if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIPCHK(c, hipHostGetDevicePointer((void **)&F.host_hint, c->flow_hint, 0));
-    F.mask = slots - 1;
-    F.max_flows = max_flows;
-    c->max_flows = max_flows;
-    c->flow_slots = slots;
-    c->flow_words = words;
-    c->flow_conf = *fc;
-    c->flow_conf.capacity = cap;
-    return flow_clear(c);
+    return rc;
 }
 
 int fcgpu_flow_enable(fcgpu_ctx *c, uint32_t max_flows) {

@@ -28,6 +28,7 @@
 #include <functional>
 #include <map>
 #include <mutex>
+#include <initializer_list>
 #include <string>
 #include <thread>
 #include <vector>
@@ -294,6 +295,33 @@ hipError_t memset_sync(void *p, int v, size_t bytes);
 hipEvent_t take_event(fcgpu_ctx *c);
 uint32_t host_capture(const fcgpu_ctx *c);
 bool fault_take(uint32_t where);
+
+// Device and pinned scratch made after fcgpu_open (lazily, or at a
+// reconfiguration), all or nothing: a group's buffers are allocated in order
+// and, at the first failure, the ones made are freed and every pointer of the
+// group is null again -- the guard that skips a group next time never sees a
+// partial set, so a failed call returns its error and the next one retries
+// instead of launching on a null or stale pointer. Every allocation is one
+// FCGPU_FAULT_ALLOC event. The group's pointers must be null on entry.
+struct Scratch {
+    void **p;
+    size_t bytes;
+    uint8_t kind;        // 0 device, 1 device zero-filled, 2 pinned host
+};
+template <class T> inline Scratch dev_buf(T *&p, size_t bytes, bool zero = false) {
+    return Scratch{reinterpret_cast<void **>(&p), bytes, static_cast<uint8_t>(zero ? 1 : 0)};
+}
+template <class T> inline Scratch pinned_buf(T *&p, size_t bytes) {
+    return Scratch{reinterpret_cast<void **>(&p), bytes, 2};
+}
+hipError_t alloc_group(std::initializer_list<Scratch> g);
+// alloc_group, and on failure fail(c, FCGPU_ENOMEM / FCGPU_ERUNTIME, what: ...)
+int alloc_or_fail(fcgpu_ctx *c, const char *what, std::initializer_list<Scratch> g);
+// one device allocation that counts as a FCGPU_FAULT_ALLOC event
+hipError_t dev_malloc(void **p, size_t bytes);
+template <class T> inline hipError_t dev_malloc(T **p, size_t bytes) {
+    return dev_malloc(reinterpret_cast<void **>(p), bytes);
+}
 
 #define HIPCHK(ctx, expr)                                                                   \
     do {                                                                                    \

@@ -46,7 +46,10 @@ int process_one(fcgpu_ctx *c, const uint8_t *d_arena, const uint32_t *d_desc, ui
     const uint32_t nports = c->cfg.nports;
     uint16_t *verdict = o->verdict;
     if (!verdict && o->partition == FCGPU_PART_GLOBAL && o->perm) {
-        if (!c->d_verdict) HIPCHK(c, hipMalloc(&c->d_verdict, sizeof(uint16_t) * c->max_batch));
+        if (!c->d_verdict) {
+            const int rc = alloc_or_fail(c, "verdict scratch", {dev_buf(c->d_verdict, sizeof(uint16_t) * c->max_batch)});
+            if (rc != FCGPU_OK) return rc;
+        }
         verdict = c->d_verdict;
     }
     const bool tile = o->partition == FCGPU_PART_TILE;
@@ -196,12 +199,12 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
         // each batch's miss records apart; one epoch per batch, none 0
         const size_t words = c->flow_words;
         if (!c->fuse_key) {
-            HIPCHK(c, hipMalloc(&c->fuse_key, sizeof(uint4) * (size_t)kMaxFuseFlow * c->max_batch));
-            HIPCHK(c, hipMalloc(&c->fuse_slot, sizeof(uint32_t) * (size_t)kMaxFuseFlow * c->max_batch));
-            HIPCHK(c, hipMalloc(&c->fuse_mask, sizeof(uint64_t) * kMaxFuseFlow * words));
-            HIPCHK(c, hipMalloc(&c->fuse_missed, sizeof(uint32_t) * kMaxFuseFlow));
-            HIPCHK(c, memset_sync(c->fuse_mask, 0, sizeof(uint64_t) * kMaxFuseFlow * words));
-            HIPCHK(c, memset_sync(c->fuse_missed, 0, sizeof(uint32_t) * kMaxFuseFlow));
+            const int rc = alloc_or_fail(c, "fused flow scratch",
+                                         {dev_buf(c->fuse_key, sizeof(uint4) * (size_t)kMaxFuseFlow * c->max_batch),
+                                          dev_buf(c->fuse_slot, sizeof(uint32_t) * (size_t)kMaxFuseFlow * c->max_batch),
+                                          dev_buf(c->fuse_mask, sizeof(uint64_t) * kMaxFuseFlow * words, true),
+                                          dev_buf(c->fuse_missed, sizeof(uint32_t) * kMaxFuseFlow, true)});
+            if (rc != FCGPU_OK) return rc;
         }
         if (c->flow_epoch > 0xffffffffu - 2 * kMaxFuse) c->flow_epoch = 0;
         epoch0 = c->flow_epoch + 1;
@@ -216,8 +219,11 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
         L.flow_words = (uint32_t)words;
     }
     if (part == kPartGlobal && !c->fuse_tilecnt) {
-        HIPCHK(c, hipMalloc(&c->fuse_tilecnt, sizeof(uint32_t) * (size_t)kMaxFuse * kFuseCntStride * c->max_tiles));
-        HIPCHK(c, hipMalloc(&c->fuse_totals, sizeof(uint32_t) * (size_t)kMaxFuse * kFuseCntStride));
+        const int rc = alloc_or_fail(
+            c, "fused partition scratch",
+            {dev_buf(c->fuse_tilecnt, sizeof(uint32_t) * (size_t)kMaxFuse * kFuseCntStride * c->max_tiles),
+             dev_buf(c->fuse_totals, sizeof(uint32_t) * (size_t)kMaxFuse * kFuseCntStride)});
+        if (rc != FCGPU_OK) return rc;
     }
     uint32_t tiles = 0;
     for (uint32_t k = 0; k < g; ++k) {
@@ -346,23 +352,22 @@ static int process_fused(fcgpu_ctx *c, const fcgpu_job *const *grp, uint32_t g, 
 static int process_host_whole(fcgpu_ctx *c, const uint8_t *const *frames, const uint32_t *lens, uint32_t n,
                               const fcgpu_out *h) {
     const size_t arena_cap = (size_t)c->max_batch * kHostCap + kArenaPad;
-    if (!c->h_arena) {
-        // the context's own stream exists only for the host-resident path (a
-        // stream per context maps onto one of the few hardware queues)
-        HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        HIPCHK(c, hipHostMalloc((void **)&c->h_arena, arena_cap, hipHostMallocDefault));
-        HIPCHK(c, hipHostMalloc((void **)&c->h_desc, sizeof(uint32_t) * 2 * c->max_batch, hipHostMallocDefault));
-        HIPCHK(c, hipMalloc(&c->d_arena, arena_cap));
-        HIPCHK(c, memset_sync(c->d_arena, 0, arena_cap));
-        c->h_arena_cap = arena_cap;
-        HIPCHK(c, hipMalloc(&c->d_desc, sizeof(uint32_t) * 2 * c->max_batch));
-        HIPCHK(c, hipMalloc(&c->d_hv, sizeof(uint16_t) * c->max_batch));
-        HIPCHK(c, hipMalloc(&c->d_hh, sizeof(uint32_t) * c->max_batch));
-        HIPCHK(c, hipMalloc(&c->d_hperm, sizeof(uint32_t) * c->max_batch));
-        HIPCHK(c, hipMalloc(&c->d_hstart, sizeof(uint32_t) * (FCGPU_MAX_PORTS + 2)));
-        HIPCHK(c, hipMalloc(&c->d_hanno, sizeof(fcgpu_anno) * c->max_batch));
-        HIPCHK(c, hipMalloc(&c->d_htc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * c->max_tiles));
-        HIPCHK(c, hipMalloc(&c->d_htp, (size_t)c->max_batch + kTile));
+    // the context's own stream exists only for the host-resident path and a
+    // flow table's span slots (a stream per context maps onto one of the few
+    // hardware queues)
+    if (!c->stream) HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (!c->d_desc) {
+        const int rc = alloc_or_fail(c, "host-resident staging",
+                                     {pinned_buf(c->h_desc, sizeof(uint32_t) * 2 * c->max_batch),
+                                      dev_buf(c->d_desc, sizeof(uint32_t) * 2 * c->max_batch),
+                                      dev_buf(c->d_hv, sizeof(uint16_t) * c->max_batch),
+                                      dev_buf(c->d_hh, sizeof(uint32_t) * c->max_batch),
+                                      dev_buf(c->d_hperm, sizeof(uint32_t) * c->max_batch),
+                                      dev_buf(c->d_hstart, sizeof(uint32_t) * (FCGPU_MAX_PORTS + 2)),
+                                      dev_buf(c->d_hanno, sizeof(fcgpu_anno) * c->max_batch),
+                                      dev_buf(c->d_htc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * c->max_tiles),
+                                      dev_buf(c->d_htp, (size_t)c->max_batch + kTile)});
+        if (rc != FCGPU_OK) return rc;
     }
     // gather: first min(len, 128) bytes of each frame (whole frames for the L4
     // checksum) at 64-B aligned offsets. The device sees the real frame
@@ -373,16 +378,19 @@ static int process_host_whole(fcgpu_ctx *c, const uint8_t *const *frames, const 
         const uint32_t cap = lens[i] < hcap ? lens[i] : hcap;
         need += cap ? (cap + 63) & ~(size_t)63 : 64;
     }
-    if (need > c->h_arena_cap) {
-        hipHostFree(c->h_arena);
-        hipFree(c->d_arena);
+    if (need > c->h_arena_cap) {          // first use (max_batch * kHostCap), or whole frames past it
+        if (c->h_arena) {
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            hipHostFree(c->h_arena);
+            hipFree(c->d_arena);
+        }
         c->h_arena = nullptr;
         c->d_arena = nullptr;
         c->h_arena_cap = 0;
-        HIPCHK(c, hipHostMalloc((void **)&c->h_arena, need, hipHostMallocDefault));
-        HIPCHK(c, hipMalloc(&c->d_arena, need));
-        HIPCHK(c, memset_sync(c->d_arena, 0, need));
-        c->h_arena_cap = need;
+        const size_t want = std::max(need, arena_cap);
+        const int rc = alloc_or_fail(c, "host-resident arena", {pinned_buf(c->h_arena, want), dev_buf(c->d_arena, want, true)});
+        if (rc != FCGPU_OK) return rc;
+        c->h_arena_cap = want;
     }
     size_t off = 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -432,28 +440,23 @@ static int process_host_whole(fcgpu_ctx *c, const uint8_t *const *frames, const 
 
 static int slot_alloc(fcgpu_ctx *c, HostSlot &sl, uint32_t cap) {
     const size_t tiles = (cap + kTile - 1) / kTile;
-    HIPCHK(c, hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
-    HIPCHK(c, hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    if (!sl.s) HIPCHK(c, hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
+    if (!sl.done) HIPCHK(c, hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    if (sl.d_desc) return FCGPU_OK;       // made by an earlier call (the group is all or nothing)
     const size_t arena = (size_t)cap * kHostCap + kArenaPad;
+    const int rc = alloc_or_fail(c, "host-resident slot",
+                                 {pinned_buf(sl.h_arena, arena), pinned_buf(sl.h_desc, sizeof(uint32_t) * 2 * cap),
+                                  dev_buf(sl.d_arena, arena, true), dev_buf(sl.d_desc, sizeof(uint32_t) * 2 * cap),
+                                  dev_buf(sl.d_v, sizeof(uint16_t) * cap), dev_buf(sl.d_h, sizeof(uint32_t) * cap),
+                                  dev_buf(sl.d_an, sizeof(fcgpu_anno) * cap), dev_buf(sl.d_perm, sizeof(uint32_t) * cap),
+                                  dev_buf(sl.d_tp, (size_t)cap + kTile),
+                                  dev_buf(sl.d_tc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * tiles),
+                                  pinned_buf(sl.h_v, sizeof(uint16_t) * cap), pinned_buf(sl.h_h, sizeof(uint32_t) * cap),
+                                  pinned_buf(sl.h_an, sizeof(fcgpu_anno) * cap),
+                                  pinned_buf(sl.h_perm, sizeof(uint32_t) * cap), pinned_buf(sl.h_tp, (size_t)cap + kTile),
+                                  pinned_buf(sl.h_tc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * tiles)});
+    if (rc != FCGPU_OK) return rc;
     sl.arena_cap = arena;
-    HIPCHK(c, hipHostMalloc((void **)&sl.h_arena, arena, hipHostMallocDefault));
-    HIPCHK(c, hipHostMalloc((void **)&sl.h_desc, sizeof(uint32_t) * 2 * cap, hipHostMallocDefault));
-    HIPCHK(c, hipMalloc(&sl.d_arena, arena));
-    HIPCHK(c, memset_sync(sl.d_arena, 0, arena));
-    HIPCHK(c, hipMalloc(&sl.d_desc, sizeof(uint32_t) * 2 * cap));
-    HIPCHK(c, hipMalloc(&sl.d_v, sizeof(uint16_t) * cap));
-    HIPCHK(c, hipMalloc(&sl.d_h, sizeof(uint32_t) * cap));
-    HIPCHK(c, hipMalloc(&sl.d_an, sizeof(fcgpu_anno) * cap));
-    HIPCHK(c, hipMalloc(&sl.d_perm, sizeof(uint32_t) * cap));
-    HIPCHK(c, hipMalloc(&sl.d_tp, (size_t)cap + kTile));
-    HIPCHK(c, hipMalloc(&sl.d_tc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * tiles));
-    HIPCHK(c, hipHostMalloc((void **)&sl.h_v, sizeof(uint16_t) * cap, hipHostMallocDefault));
-    HIPCHK(c, hipHostMalloc((void **)&sl.h_h, sizeof(uint32_t) * cap, hipHostMallocDefault));
-    HIPCHK(c, hipHostMalloc((void **)&sl.h_an, sizeof(fcgpu_anno) * cap, hipHostMallocDefault));
-    HIPCHK(c, hipHostMalloc((void **)&sl.h_perm, sizeof(uint32_t) * cap, hipHostMallocDefault));
-    HIPCHK(c, hipHostMalloc((void **)&sl.h_tp, (size_t)cap + kTile, hipHostMallocDefault));
-    HIPCHK(c, hipHostMalloc((void **)&sl.h_tc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * tiles,
-                            hipHostMallocDefault));
     return FCGPU_OK;
 }
 
@@ -538,9 +541,9 @@ static int process_host_pipelined(fcgpu_ctx *c, const uint8_t *const *frames, co
             sl.h_arena = nullptr;
             sl.d_arena = nullptr;
             sl.arena_cap = 0;
-            HIPCHK(c, hipHostMalloc((void **)&sl.h_arena, want, hipHostMallocDefault));
-            HIPCHK(c, hipMalloc(&sl.d_arena, want));
-            HIPCHK(c, memset_sync(sl.d_arena, 0, want));
+            const int rc = alloc_or_fail(c, "host-resident slot arena",
+                                         {pinned_buf(sl.h_arena, want), dev_buf(sl.d_arena, want, true)});
+            if (rc != FCGPU_OK) return rc;
             sl.arena_cap = want;
         }
         c->pool.run([&](uint32_t part, uint32_t nparts) {

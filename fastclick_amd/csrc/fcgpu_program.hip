@@ -182,10 +182,16 @@ int fcgpu_set_program(fcgpu_ctx *c, uint32_t kind, const fcgpu_step *steps, uint
     const uint32_t total_n = nsteps ? build_tables(dev, nsteps, tab_q) : 0;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipDeviceSynchronize());
+    // the new program is uploaded before the old one is freed: a failure
+    // leaves the context's program (and the device config naming it) intact
+    uint4 *np = nullptr;
+    if (int rc = alloc_or_fail(c, "fcgpu_set_program", {dev_buf(np, sizeof(uint4) * dev.size())})) return rc;
+    if (hipError_t e = hipMemcpy(np, dev.data(), sizeof(uint4) * dev.size(), hipMemcpyHostToDevice)) {
+        (void)hipFree(np);
+        return fail(c, FCGPU_ERUNTIME, std::string("fcgpu_set_program upload: ") + hipGetErrorString(e));
+    }
     hipFree(c->d_prog);
-    c->d_prog = nullptr;
-    HIPCHK(c, hipMalloc(&c->d_prog, sizeof(uint4) * dev.size()));
-    HIPCHK(c, hipMemcpy(c->d_prog, dev.data(), sizeof(uint4) * dev.size(), hipMemcpyHostToDevice));
+    c->d_prog = np;
     c->prog_host.assign(steps, steps + nsteps);
     c->prog_n = total_n;
     c->prog_q = (uint32_t)dev.size();
@@ -248,10 +254,15 @@ int fcgpu_set_lb_table(fcgpu_ctx *c, const uint8_t *table, uint32_t nbuckets) {
     memcpy(dev.data(), table, n);
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipDeviceSynchronize());
+    // uploaded before the old table is freed: a failure leaves it intact
+    uint8_t *nt = nullptr;
+    if (int rc = alloc_or_fail(c, "fcgpu_set_lb_table", {dev_buf(nt, dev.size())})) return rc;
+    if (hipError_t e = hipMemcpy(nt, dev.data(), dev.size(), hipMemcpyHostToDevice)) {
+        (void)hipFree(nt);
+        return fail(c, FCGPU_ERUNTIME, std::string("fcgpu_set_lb_table upload: ") + hipGetErrorString(e));
+    }
     hipFree(c->d_lbtab);
-    c->d_lbtab = nullptr;
-    HIPCHK(c, hipMalloc(&c->d_lbtab, dev.size()));
-    HIPCHK(c, hipMemcpy(c->d_lbtab, dev.data(), dev.size(), hipMemcpyHostToDevice));
+    c->d_lbtab = nt;
     c->lbtab_n = n;
     c->lbtab_max = mx;
     uint64_t key = 1469598103934665603ull;

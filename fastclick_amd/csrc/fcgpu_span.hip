@@ -394,20 +394,19 @@ int fcgpu_span_submit(fcgpu_ctx *c, uint32_t slot, const uint8_t *h_span, size_t
         return FCGPU_OK;
     }
     HIPCHK(c, hipSetDevice(c->device));
-    if (!sp.own) {
+    if (!sp.d_desc) {                     // all or nothing
         const size_t m = c->max_batch, tiles = (m + kTile - 1) / kTile;
-        HIPCHK(c, hipStreamCreateWithFlags(&sp.own, hipStreamNonBlocking));
-        HIPCHK(c, hipMalloc(&sp.d_desc, sizeof(uint32_t) * 2 * m));
-        HIPCHK(c, hipMalloc(&sp.d_v, sizeof(uint16_t) * m));
-        HIPCHK(c, hipMalloc(&sp.d_h, sizeof(uint32_t) * m));
-        HIPCHK(c, hipMalloc(&sp.d_an, sizeof(fcgpu_anno) * m));
-        HIPCHK(c, hipMalloc(&sp.d_perm, sizeof(uint32_t) * m));
-        HIPCHK(c, hipMalloc(&sp.d_start, sizeof(uint32_t) * (FCGPU_MAX_PORTS + 2)));
-        HIPCHK(c, hipMalloc(&sp.d_tp, m + kTile));
-        HIPCHK(c, hipMalloc(&sp.d_tc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * tiles));
-        HIPCHK(c, hipMalloc(&sp.d_fl, sizeof(uint32_t) * m));
-        HIPCHK(c, hipMalloc(&sp.d_rw, sizeof(uint32_t) * m));
+        const int rc = alloc_or_fail(c, "span slot outputs",
+                                     {dev_buf(sp.d_desc, sizeof(uint32_t) * 2 * m), dev_buf(sp.d_v, sizeof(uint16_t) * m),
+                                      dev_buf(sp.d_h, sizeof(uint32_t) * m), dev_buf(sp.d_an, sizeof(fcgpu_anno) * m),
+                                      dev_buf(sp.d_perm, sizeof(uint32_t) * m),
+                                      dev_buf(sp.d_start, sizeof(uint32_t) * (FCGPU_MAX_PORTS + 2)),
+                                      dev_buf(sp.d_tp, m + kTile),
+                                      dev_buf(sp.d_tc, sizeof(uint16_t) * (FCGPU_MAX_PORTS + 1) * tiles),
+                                      dev_buf(sp.d_fl, sizeof(uint32_t) * m), dev_buf(sp.d_rw, sizeof(uint32_t) * m)});
+        if (rc != FCGPU_OK) return rc;
     }
+    if (!sp.own) HIPCHK(c, hipStreamCreateWithFlags(&sp.own, hipStreamNonBlocking));
     const bool zc = span_zerocopy(c);
     if (!zc && bytes + kArenaPad > sp.span_cap) {
         HIPCHK(c, hipStreamSynchronize(sp.own));
@@ -415,8 +414,8 @@ int fcgpu_span_submit(fcgpu_ctx *c, uint32_t slot, const uint8_t *h_span, size_t
         sp.d_span = nullptr;
         sp.span_cap = 0;
         const size_t cap = (bytes + kArenaPad + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
-        HIPCHK(c, hipMalloc(&sp.d_span, cap));
-        HIPCHK(c, memset_sync(sp.d_span, 0, cap));
+        const int rc = alloc_or_fail(c, "span block", {dev_buf(sp.d_span, cap, true)});
+        if (rc != FCGPU_OK) return rc;
         sp.span_cap = cap;
     }
     // a flow table assigns IDs in batch order: every slot then runs on the
@@ -622,8 +621,8 @@ static int span_blocks(fcgpu_ctx *c, uint32_t slot, hipStream_t ss, size_t in_by
         sp.d_in = nullptr;
         sp.in_cap = 0;
         const size_t cap = (in_bytes + kArenaPad + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
-        HIPCHK(c, hipMalloc(&sp.d_in, cap));
-        HIPCHK(c, memset_sync(sp.d_in, 0, cap));
+        const int rc = alloc_or_fail(c, "span input block", {dev_buf(sp.d_in, cap, true)});
+        if (rc != FCGPU_OK) return rc;
         sp.in_cap = cap;
     }
     if (M.bytes > sp.res_cap) {
@@ -631,7 +630,8 @@ static int span_blocks(fcgpu_ctx *c, uint32_t slot, hipStream_t ss, size_t in_by
         hipFree(sp.d_res);
         sp.d_res = nullptr;
         sp.res_cap = 0;
-        HIPCHK(c, hipMalloc(&sp.d_res, M.bytes));
+        const int rc = alloc_or_fail(c, "span result block", {dev_buf(sp.d_res, M.bytes)});
+        if (rc != FCGPU_OK) return rc;
         sp.res_cap = M.bytes;
     }
     return FCGPU_OK;

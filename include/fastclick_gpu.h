@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define FCGPU_ABI_VERSION 24
+#define FCGPU_ABI_VERSION 25
 
 #define FCGPU_OK          0
 #define FCGPU_EINVAL     -1   /* bad argument / configuration            */
@@ -437,13 +437,22 @@ int  fcgpu_span_mode(fcgpu_ctx *ctx, uint32_t mode);
  *                         returns the error and frees the slot;
  *   FCGPU_FAULT_LAUNCH -- the next shared-queue launch (FCGPU_SPAN_AUTO) fails:
  *                         every batch it carried reports the error through its
- *                         owner's wait or poll.
+ *                         owner's wait or poll;
+ *   FCGPU_FAULT_ALLOC  -- a device or pinned allocation made after fcgpu_open
+ *                         (scratch made on first use, span and staging blocks,
+ *                         flow tables, programs) fails as out of memory: the
+ *                         call returns FCGPU_ENOMEM or FCGPU_ERUNTIME and
+ *                         leaves no partial state -- a group of buffers is made
+ *                         whole or not at all, a flow table or program being
+ *                         replaced is absent / the previous one -- so the next
+ *                         call retries.
  * Events: submissions for SUBMIT and WAIT (an element's re-submission is
- * one), shared launches for LAUNCH. count 0 clears the kind. Returns
- * FCGPU_EINVAL for another kind. */
+ * one), shared launches for LAUNCH, allocations for ALLOC. count 0 clears
+ * the kind. Returns FCGPU_EINVAL for another kind. */
 #define FCGPU_FAULT_SUBMIT 0u
 #define FCGPU_FAULT_WAIT   1u
 #define FCGPU_FAULT_LAUNCH 2u
+#define FCGPU_FAULT_ALLOC  3u
 int  fcgpu_inject_fault(uint32_t where, uint32_t skip, uint32_t count);
 
 /* Host-only self-test of the launch guard every kernel launch passes (no

@@ -155,5 +155,11 @@ int fcgpu_flow_configure(fcgpu_ctx *, const fcgpu_flow_config *) { return FCGPU_
 int fcgpu_flow_count(fcgpu_ctx *, uint32_t *n) { *n = 0; return FCGPU_OK; }
 int fcgpu_flow_maintain(fcgpu_ctx *, uint32_t, void *) { return FCGPU_OK; }
 int fcgpu_flow_set_time(fcgpu_ctx *, uint32_t) { return FCGPU_OK; }
+int fcgpu_flow_stats(fcgpu_ctx *, fcgpu_flow_stat *st) { memset(st, 0, sizeof *st); return FCGPU_OK; }
+int fcgpu_set_lb_table(fcgpu_ctx *, const uint8_t *, uint32_t) { return FCGPU_OK; }
+int fcgpu_lb_hash_ring(uint32_t nsel, uint32_t size, uint8_t *out) {
+    for (uint32_t i = 0; i < size; ++i) out[i] = (uint8_t)(nsel ? i % nsel : 0);
+    return FCGPU_OK;
+}
 
 }  // extern "C"

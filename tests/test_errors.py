@@ -36,8 +36,8 @@ def test_launch_guard_selftest():
 
 def test_inject_fault_arguments():
     lib = N.load()
-    assert lib.fcgpu_inject_fault(3, 0, 1) == N.EINVAL
-    for k in (N.FAULT_SUBMIT, N.FAULT_WAIT, N.FAULT_LAUNCH):
+    assert lib.fcgpu_inject_fault(4, 0, 1) == N.EINVAL
+    for k in (N.FAULT_SUBMIT, N.FAULT_WAIT, N.FAULT_LAUNCH, N.FAULT_ALLOC):
         assert lib.fcgpu_inject_fault(k, 0, 0) == N.OK
 
 
@@ -64,7 +64,7 @@ def _exp(oracle, b):
 def no_faults():
     lib = N.load()
     yield lib
-    for k in (N.FAULT_SUBMIT, N.FAULT_WAIT, N.FAULT_LAUNCH):
+    for k in (N.FAULT_SUBMIT, N.FAULT_WAIT, N.FAULT_LAUNCH, N.FAULT_ALLOC):
         lib.fcgpu_inject_fault(k, 0, 0)
 
 
