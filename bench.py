@@ -417,6 +417,19 @@ def _make_host_batch(args):
 
 
 ROTATION_BYTES = 1_150_000_000   # > 4 x the 256 MB Infinity Cache of one MI355X
+MALL_BYTES = 256 << 20           # the Infinity Cache (MALL) of one MI355X
+
+
+def residency(rotation_bytes) -> str:
+    """Where the timed steps' input comes from, by the rotation's size (SURVEY
+    8(d): a cache-resident number is reported apart and labelled)."""
+    if not rotation_bytes:
+        return "n/a"
+    if rotation_bytes >= ROTATION_BYTES:
+        return "hbm"
+    if rotation_bytes <= MALL_BYTES:
+        return "cache-resident: the rotation fits the 256 MB Infinity Cache (not an HBM figure)"
+    return "mixed: the rotation is under 4x the Infinity Cache (not an HBM figure)"
 
 
 def shard_arrays(host, lo, hi, pad=256):
@@ -1118,7 +1131,8 @@ def rank_main(args, processor_factory, *, world, rank, gpu, backend, dev_for_col
             "packets_per_step_per_gpu": per_gpu,
             "packets_per_step": args.packets if args.shard == "strong" else args.packets * world,
             "hbm_batches": args.nbuf,
-            **({"rotation_bytes_per_gpu": int(proc.rotation_bytes)}
+            **({"rotation_bytes_per_gpu": int(proc.rotation_bytes),
+                "residency": residency(proc.rotation_bytes)}
                if getattr(proc, "rotation_bytes", None) else {}),
             "nports": args.nports,
             **({"flow_maintain_ms": round(maintain_ms, 4)} if maintain_ms is not None else {}),

@@ -222,6 +222,10 @@ for s in "${ST[@]}"; do
              done ;;
     # round 6: the wire layouts' own ceiling (bare window gather vs k_rx, same box)
     r6gather) step gather_bound 600 python scripts/gather_bound.py ;;
+    r6cache) for r in 1 2; do for nb in 1 2 3 16; do
+               step cache_nb${nb}_$r 300 python bench.py --nbuf $nb --steps 200 --warmup 20 --no-cpu || exit 1
+               step cache20_nb${nb}_$r 300 python bench.py --nbuf $nb --no-cpu || exit 1
+             done; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -214,6 +214,12 @@ def test_strong_shards_rotate_beyond_the_infinity_cache(world):
         shard = synth.Batch(arena=arena, desc=desc)
         assert shard.frame(hi - lo - 1) == host.frame(hi - 1)
     assert bench.rotation_nbuf(131072 * 64 + 256 + 131072 * 8) == 122   # 122 x 9.4 MB at N = 8
+    # the default rotation reads HBM; --nbuf 1..3 of the C2 batch is labelled cache-resident
+    touched = (1 << 20) * 72
+    assert bench.residency(bench.rotation_nbuf(touched) * touched) == "hbm"
+    for nbuf in (1, 2, 3):
+        assert bench.residency(nbuf * touched).startswith("cache-resident")
+    assert bench.residency(8 * touched).startswith("mixed")
 
 
 def test_nccl_world_larger_than_devices_fails_at_startup():
