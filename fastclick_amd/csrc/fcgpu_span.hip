@@ -61,11 +61,16 @@ struct AggItem {
     hipFunction_t fn;         // the compiled program's k_rx (nullptr: the built-in kernel)
     uint64_t prog_key;        // the program's contents (dcfg.prog is this context's copy of it)
 };
+// the queue's launch streams: HIP maps a process's streams onto
+// GPU_MAX_HW_QUEUES hardware queues (4 by default). FCGPU_AGG_STREAMS=1..8
+// changes the count (same-box A/B with GPU_MAX_HW_QUEUES)
+constexpr uint32_t kAggStreams = 4, kAggStreamsMax = 8;
 struct AggQueue {
     std::mutex mu;
     int device = -1;
     std::vector<AggItem> pending;
-    hipStream_t st[4] = {};   // created by agg_issue (st_mu), never under mu
+    hipStream_t st[kAggStreamsMax] = {};   // created by agg_issue (st_mu), never under mu
+    uint32_t nst = kAggStreams;
     std::mutex st_mu;
     uint32_t rr = 0;
     std::vector<AggLaunch *> spare;
@@ -83,6 +88,10 @@ static AggQueue &agg_queue(fcgpu_ctx *c) {
     if (!q) {
         q = new AggQueue();
         q->device = c->device;
+        if (const char *e = getenv("FCGPU_AGG_STREAMS")) {
+            const int v = atoi(e);
+            if (v >= 1 && v <= (int)kAggStreamsMax) q->nst = (uint32_t)v;
+        }
     }
     c->aq = q;
     return *q;
@@ -192,7 +201,7 @@ static void agg_take_locked(AggQueue &q, std::vector<AggIssue> &out) {
         a.layout = J0.layout;
         // no HIP call under the queue's lock: the stream and a new launch's
         // event are created by the issuing thread (agg_issue)
-        is.si = q.rr++ % 4;
+        is.si = q.rr++ % q.nst;
         AggLaunch *al = nullptr;
         if (!q.spare.empty()) {
             al = q.spare.back();

@@ -222,6 +222,10 @@ for s in "${ST[@]}"; do
              done ;;
     # round 6: the wire layouts' own ceiling (bare window gather vs k_rx, same box)
     r6gather) step gather_bound 600 python scripts/gather_bound.py ;;
+    r6hwq) for r in 1 2; do for c in 4:4 8:8 16:16 4:8; do
+             ns=${c%%:*}; hq=${c##*:}
+             FCGPU_AGG_STREAMS=$ns GPU_MAX_HW_QUEUES=$hq step hwq_s${ns}_q${hq}_$r 120 python scripts/element_threads.py 16 || exit 1
+           done; done ;;
     r6cache) for r in 1 2; do for nb in 1 2 3 16; do
                step cache_nb${nb}_$r 300 python bench.py --nbuf $nb --steps 200 --warmup 20 --no-cpu || exit 1
                step cache20_nb${nb}_$r 300 python bench.py --nbuf $nb --no-cpu || exit 1
