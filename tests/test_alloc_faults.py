@@ -318,3 +318,30 @@ def test_gpu_alloc_fault_span_submit(oracle, alloc_fault, skip):
         ctx.close()
     _span_check(dict(verdict=verdict, hash=hsh), exp, f"span submit, skip {skip}")
     assert np.array_equal(tp, (exp["perm_tile"] % 256).astype(np.uint8))
+
+
+@pytest.mark.gpu
+def test_gpu_span_slot_block_then_span_submit(oracle):
+    """One slot used first by the element's block path and then by
+    fcgpu_span_submit: the slot's stream exists from the first, its device
+    output buffers only from the second -- the second makes them (the guard
+    is the buffers, not the stream) and both results equal the oracle."""
+    from tests.test_span_modes import Block, _cfg as span_cfg
+    b = _batch(2000, seed=53)
+    cfg = span_cfg()
+    exp = oracle.process_batch(cfg, b)
+    lib = N.load()
+    ctx = N.Context(0, 4096, cfg)
+    blk = Block(lib, ctx.h, b, 4096)
+    verdict = np.zeros(b.n, np.uint16)
+    hsh = np.zeros(b.n, np.uint32)
+    try:
+        assert lib.fcgpu_span_mode(ctx.h, N.SPAN_COPY) == N.OK
+        _span_check(blk.run(ctx.h), exp, "block path")
+        ctx.span_submit(0, blk.pin + blk.frames_off, b.n * 64, blk.pin, b.n, verdict=verdict.ctypes.data,
+                        hash=hsh.ctypes.data)
+        ctx.span_wait(0)
+    finally:
+        blk.free()
+        ctx.close()
+    _span_check(dict(verdict=verdict, hash=hsh), exp, "span submit after the block path")
