@@ -316,9 +316,11 @@ int  fcgpu_process_host(fcgpu_ctx *ctx, const uint8_t *const *frames,
  * FCGPU_SPAN_SLOTS submissions are in flight, each on its own stream (one
  * stream for all when a flow table is enabled, which needs batch order);
  * h_span, h_desc and h_out must stay valid until fcgpu_span_wait(slot).
- * Pinned buffers (fcgpu_host_alloc) make the copies true DMA. The span must be
- * readable 128 bytes past every frame start (the context pads its device
- * copy; bytes past the span are never part of a verdict). */
+ * Pinned buffers (fcgpu_host_alloc) make the copies true DMA. Every frame
+ * starts inside the span (desc offsets < span_bytes: the descriptors are the
+ * caller's and not checked per packet, as for fcgpu_process's arena) and the
+ * span must be readable 128 bytes past every frame start (the context pads
+ * its device copy; bytes past the span are never part of a verdict). */
 #define FCGPU_SPAN_SLOTS 3
 int  fcgpu_span_submit(fcgpu_ctx *ctx, uint32_t slot, const uint8_t *h_span, size_t span_bytes,
                        const uint32_t *h_desc, uint32_t n, const fcgpu_out *h_out);
