@@ -414,9 +414,15 @@ static int process_host_whole(fcgpu_ctx *c, const uint8_t *const *frames, const 
     d.partition = h->partition;
     d.reserved = 0;
     d.tile_perm = h->tile_perm ? c->d_htp : nullptr;
-    if (h->flowid && !c->d_hflow) HIPCHK(c, hipMalloc(&c->d_hflow, sizeof(uint32_t) * c->max_batch));
+    if (h->flowid && !c->d_hflow) {
+        const int rc = alloc_or_fail(c, "host-resident flow IDs", {dev_buf(c->d_hflow, sizeof(uint32_t) * c->max_batch)});
+        if (rc != FCGPU_OK) return rc;
+    }
     d.flowid = h->flowid ? c->d_hflow : nullptr;
-    if (h->ip_rw && !c->d_hrw) HIPCHK(c, hipMalloc(&c->d_hrw, sizeof(uint32_t) * c->max_batch));
+    if (h->ip_rw && !c->d_hrw) {
+        const int rc = alloc_or_fail(c, "host-resident ip_rw", {dev_buf(c->d_hrw, sizeof(uint32_t) * c->max_batch)});
+        if (rc != FCGPU_OK) return rc;
+    }
     d.ip_rw = h->ip_rw ? c->d_hrw : nullptr;
     int rc = fcgpu_process(c, c->d_arena, c->d_desc, n, &d, s);
     if (rc != FCGPU_OK) return rc;
@@ -725,6 +731,13 @@ int fcgpu_pool_register(fcgpu_ctx *c, void *base, size_t bytes) {
         c->pool_host = c->pool_bytes = 0;
         c->pool_dev = nullptr;
     }
+    // the descriptor scratch first: a failure leaves no pool registered
+    if (!c->d_mptr) {
+        const int rc = alloc_or_fail(c, "fcgpu_pool_register scratch",
+                                     {dev_buf(c->d_mptr, sizeof(uint64_t) * c->max_batch),
+                                      dev_buf(c->d_mdesc, sizeof(uint2) * c->max_batch)});
+        if (rc != FCGPU_OK) return rc;
+    }
     // several contexts (one per rx queue / thread) may share one pool: the
     // library pins it once and unpins it when the last of them lets go
     {
@@ -742,15 +755,16 @@ int fcgpu_pool_register(fcgpu_ctx *c, void *base, size_t bytes) {
         }
     }
     c->pool_owned = true;
-    void *dev = nullptr;
-    HIPCHK(c, hipHostGetDevicePointer(&dev, base, 0));
     c->pool_host = (uint64_t)base;
     c->pool_bytes = bytes;
-    c->pool_dev = static_cast<uint8_t *>(dev);
-    if (!c->d_mptr) {
-        HIPCHK(c, hipMalloc(&c->d_mptr, sizeof(uint64_t) * c->max_batch));
-        HIPCHK(c, hipMalloc(&c->d_mdesc, sizeof(uint2) * c->max_batch));
+    void *dev = nullptr;
+    if (hipError_t e = hipHostGetDevicePointer(&dev, base, 0)) {
+        (void)hipGetLastError();
+        pool_release(c);                  // the registration's reference goes back
+        c->pool_host = c->pool_bytes = 0;
+        return fail(c, FCGPU_ERUNTIME, std::string("hipHostGetDevicePointer(pool): ") + hipGetErrorString(e));
     }
+    c->pool_dev = static_cast<uint8_t *>(dev);
     return FCGPU_OK;
 }
 

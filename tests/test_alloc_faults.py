@@ -345,3 +345,34 @@ def test_gpu_span_slot_block_then_span_submit(oracle):
         blk.free()
         ctx.close()
     _span_check(dict(verdict=verdict, hash=hsh), exp, "span submit after the block path")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("skip", [0, 1])
+def test_gpu_alloc_fault_pool_register(oracle, alloc_fault, skip):
+    """fcgpu_pool_register's descriptor scratch (2 buffers) is made before the
+    pool is pinned: a failure registers nothing (fcgpu_process_mbufs then
+    refuses, no launch), the next registration works and the mbuf batch
+    equals the oracle."""
+    from fastclick_amd.device import DeviceOutputs
+    from tests.test_mbuf import make_pool
+    b = _batch(3000, seed=61)
+    buf, arr, base, size, ptrs = make_pool(b.frames(), np.random.default_rng(62))
+    cfg = _cfg()
+    exp = oracle.process_batch(cfg, b)
+    ctx = N.Context(0, b.n, cfg)
+    try:
+        alloc_fault(skip)
+        with pytest.raises(RuntimeError, match="out of memory"):
+            ctx.pool_register(base, size)
+        _clear()
+        outs = DeviceOutputs(b.n, 16, device="cuda:0", perm=True, partition=N.PART_TILE)
+        with pytest.raises(RuntimeError, match="no pool registered"):
+            ctx.process_mbufs(ptrs.ctypes.data, b.n, **outs.ptrs())
+        ctx.pool_register(base, size)
+        ctx.process_mbufs(ptrs.ctypes.data, b.n, **outs.ptrs())
+        torch.cuda.synchronize()
+        got = outs.numpy()
+    finally:
+        ctx.close()
+    _check(got, exp, f"mbufs, skip {skip}")
