@@ -276,6 +276,27 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
         return fail(c, FCGPU_EINVAL, "bad rewrite flags");
     if ((cfg->rewrite & (FCGPU_RW_DECTTL | FCGPU_RW_SETCKSUM)) && !ip4mode)
         return fail(c, FCGPU_EINVAL, "rewrite needs an IPv4 check mode (CHECK_IP4 or MARK_IP4)");
+    // the one allocation comes first: a failed reconfiguration leaves the
+    // previous configuration (c->cfg and the device config) as it was
+    if (cfg->classify == FCGPU_CLS_LB_CRC && !c->d_crc) {
+        // U_k[b] = 16 shift steps of b << 8k: rte_hash_crc_4byte's 32 steps
+        // are linear, so a word is two rounds of two lookups (fcgpu_device.hh)
+        std::vector<uint32_t> t(512);
+        for (uint32_t k = 0; k < 2; ++k)
+            for (uint32_t b = 0; b < 256; ++b) {
+                uint32_t x = b << (8 * k);
+                for (int j = 0; j < 16; ++j) x = (x >> 1) ^ (0x82F63B78u & (0u - (x & 1u)));
+                t[256 * k + b] = x;
+            }
+        HIPCHK(c, hipSetDevice(c->device));
+        uint4 *tab = nullptr;
+        if (int rc = alloc_or_fail(c, "CRC table", {dev_buf(tab, sizeof(uint32_t) * 512)})) return rc;
+        if (hipError_t e = hipMemcpy(tab, t.data(), sizeof(uint32_t) * 512, hipMemcpyHostToDevice)) {
+            (void)hipFree(tab);
+            return fail(c, FCGPU_ERUNTIME, std::string("CRC table upload: ") + hipGetErrorString(e));
+        }
+        c->d_crc = tab;
+    }
     c->cfg = *cfg;
     DevCfg &d = c->dcfg;
     memset(&d, 0, sizeof(d));
@@ -302,25 +323,6 @@ int fcgpu_configure(fcgpu_ctx *c, const fcgpu_cfg *cfg) {
     memcpy(d.badsrc, cfg->badsrc, sizeof(d.badsrc));
     memcpy(d.gooddst, cfg->gooddst, sizeof(d.gooddst));
     memcpy(d.bad6, cfg->bad6, sizeof(d.bad6));
-    if (cfg->classify == FCGPU_CLS_LB_CRC && !c->d_crc) {
-        // U_k[b] = 16 shift steps of b << 8k: rte_hash_crc_4byte's 32 steps
-        // are linear, so a word is two rounds of two lookups (fcgpu_device.hh)
-        std::vector<uint32_t> t(512);
-        for (uint32_t k = 0; k < 2; ++k)
-            for (uint32_t b = 0; b < 256; ++b) {
-                uint32_t x = b << (8 * k);
-                for (int j = 0; j < 16; ++j) x = (x >> 1) ^ (0x82F63B78u & (0u - (x & 1u)));
-                t[256 * k + b] = x;
-            }
-        HIPCHK(c, hipSetDevice(c->device));
-        uint4 *tab = nullptr;
-        if (int rc = alloc_or_fail(c, "CRC table", {dev_buf(tab, sizeof(uint32_t) * 512)})) return rc;
-        if (hipError_t e = hipMemcpy(tab, t.data(), sizeof(uint32_t) * 512, hipMemcpyHostToDevice)) {
-            (void)hipFree(tab);
-            return fail(c, FCGPU_ERUNTIME, std::string("CRC table upload: ") + hipGetErrorString(e));
-        }
-        c->d_crc = tab;
-    }
     d.crc_tab = cfg->classify == FCGPU_CLS_LB_CRC ? c->d_crc : nullptr;
     d.lb_tab = cfg->classify == FCGPU_CLS_LB_TABLE ? c->d_lbtab : nullptr;
     d.lb_tab_n = c->lbtab_n;

@@ -376,3 +376,24 @@ def test_gpu_alloc_fault_pool_register(oracle, alloc_fault, skip):
     finally:
         ctx.close()
     _check(got, exp, f"mbufs, skip {skip}")
+
+
+@pytest.mark.gpu
+def test_gpu_alloc_fault_reconfigure_keeps_config(oracle, alloc_fault):
+    """fcgpu_configure to LB_MODE hash_crc makes the CRC tables before it
+    touches the context's configuration: a failed allocation leaves the
+    previous configuration in force (no launch with a null table), the next
+    configure switches."""
+    b = _batch(4000, seed=71)
+    cfg_a, cfg_b = _cfg(), _cfg(classify=N.CLS_LB_CRC)
+    ctx = N.Context(0, b.n, cfg_a)
+    try:
+        alloc_fault(0)
+        with pytest.raises(RuntimeError, match="CRC table"):
+            ctx.configure(cfg_b)
+        _clear()
+        _check(_run(ctx, b, cfg_a), oracle.process_batch(cfg_a, b), "previous configuration kept")
+        ctx.configure(cfg_b)
+        _check(_run(ctx, b, cfg_b), oracle.process_batch(cfg_b, b), "hash_crc after the retry")
+    finally:
+        ctx.close()
