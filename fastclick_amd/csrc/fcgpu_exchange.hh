@@ -508,16 +508,34 @@ __device__ __forceinline__ void xtile_sort(const XBuild &B, uint32_t t, XTileLds
     intra = own < B.world ? L.pre[pos] - L.pre[L.tstart[own]] : 0u;
 }
 
+// Per owner the tile's packets and slot bytes are sums, which the order the
+// build sorts in does not change: LDS atomics and one barrier, no sort
+// (the sort's five barriers per tile made this pass latency-bound).
 __global__ __launch_bounds__(kXTile) void k_xbtile(XBuild B) {
-    __shared__ XTileLds L;
-    uint32_t own, len, src, pos, intra;
-    const uint32_t t = blockIdx.x;
-    xtile_sort(B, t, L, own, len, src, pos, intra);
+    __shared__ uint32_t s_c[FCGPU_MAX_PORTS], s_b[FCGPU_MAX_PORTS];
+    const uint32_t t = blockIdx.x, i = t * kXTile + threadIdx.x;
+    if (threadIdx.x < B.world) {
+        s_c[threadIdx.x] = 0;
+        s_b[threadIdx.x] = 0;
+    }
+    uint32_t own = B.world, slot = 0;
+    if (i < B.n) {
+        const uint32_t d = (uint32_t)B.verdict[i] >> 8;
+        if (d < B.world) {
+            own = d;
+            slot = (uint32_t)xslot(B.desc[2 * (size_t)i + 1]);
+        }
+    }
+    __syncthreads();
+    if (own < B.world) {
+        atomicAdd(&s_c[own], 1u);
+        atomicAdd(&s_b[own], slot);
+    }
+    __syncthreads();
     const uint32_t d = threadIdx.x;
     if (d < B.world) {
-        const uint32_t a = L.tstart[d], c = L.tcnt[d];
-        B.tcnt[(size_t)d * B.ntiles + t] = c;
-        B.tbyt[(size_t)d * B.ntiles + t] = L.pre[a + c] - L.pre[a];
+        B.tcnt[(size_t)d * B.ntiles + t] = s_c[d];
+        B.tbyt[(size_t)d * B.ntiles + t] = s_b[d];
     }
 }
 

@@ -226,6 +226,9 @@ for s in "${ST[@]}"; do
              ns=${c%%:*}; hq=${c##*:}
              FCGPU_AGG_STREAMS=$ns GPU_MAX_HW_QUEUES=$hq step hwq_s${ns}_q${hq}_$r 120 python scripts/element_threads.py 16 || exit 1
            done; done ;;
+    r6stages) for r in 1 2; do for st in 1 0; do
+                FCGPU_RESHARD_STAGES=$st step reshard_st${st}_$r 300 python bench.py --flow-reshard --workload c4 --steps 50 --warmup 5 --no-cpu || exit 1
+              done; done ;;
     r6cache) for r in 1 2; do for nb in 1 2 3 16; do
                step cache_nb${nb}_$r 300 python bench.py --nbuf $nb --steps 200 --warmup 20 --no-cpu || exit 1
                step cache20_nb${nb}_$r 300 python bench.py --nbuf $nb --no-cpu || exit 1
