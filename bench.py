@@ -867,10 +867,15 @@ class ReshardProcessor:
         self._repair()
         self.torch.cuda.synchronize()
         self.ctx_flow.use_counters(self.ctr.data_ptr())      # timed steps count into the tensor
-        # six markers per timed step, created here and read after the timed
-        # region, so the steps are not synchronised one by one
-        self.ev = [[self.torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(self.args.steps)] \
-            if os.environ.get("FCGPU_RESHARD_STAGES", "1") == "1" else None
+        # six markers on every STAGE_EVERY-th timed step (FCGPU_RESHARD_STAGES,
+        # default 5; 0: none), created here and read after the timed region,
+        # so the steps are not synchronised one by one. Markers cost the step
+        # ~20 us when every step has them (113 -> 133 us at N = 1,
+        # profiles/r06_reshard/stages), hence the sample
+        every = int(os.environ.get("FCGPU_RESHARD_STAGES", "5") or 0)
+        self.stage_every = every
+        self.ev = [[self.torch.cuda.Event(enable_timing=True) for _ in range(6)] if k % every == every - 1 else None
+                   for k in range(self.args.steps)] if every > 0 else None
         self.first = max(steps, 1)
 
     def run_timed(self):
@@ -906,10 +911,10 @@ class ReshardProcessor:
             raise AssertionError(f"flow tables hold {flows} flows, the batches have {distinct} distinct 5-tuples")
         if received != sent:
             raise AssertionError(f"{received} packets received, {sent} sent")
-        steps = max(self.timed_steps, 1)
-        if self.ev:
+        sampled = [ev for ev in self.ev[:self.timed_steps] if ev] if self.ev else []
+        if sampled:
             torch.cuda.synchronize()
-            for ev in self.ev[:self.timed_steps]:
+            for ev in sampled:
                 for j in range(5):
                     self.stage_ms[j] += ev[j].elapsed_time(ev[j + 1])
         names = ("owner_pass", "build", "exchange", "unpack", "flow_pass")
@@ -921,12 +926,14 @@ class ReshardProcessor:
                                       zip(("owner_pass", "build", "exchange", "unpack", "flow_pass"), self.host_t)}
         return {"flow_table_flows": flows, "distinct_5tuples": distinct, "packets_received": received,
                 "packets_sent": sent, "checked": True, **fx,
-                **({"stage_ms_per_step": {k: round(t / steps, 4) for k, t in zip(names, self.stage_ms)},
-                    "stage_basis": "HIP events on the step's stream, read after the timed region (their "
+                **({"stage_ms_per_step": {k: round(t / len(sampled), 4) for k, t in zip(names, self.stage_ms)},
+                    "stage_sampled_steps": len(sampled),
+                    "stage_basis": f"HIP events on the step's stream, every {self.stage_every}th timed step, "
+                                   "read after the timed region (their "
                                    "sum is below ms_per_step by the host's own work"
                                    + (")" if self.fixed else " and the exchange's host sync for the "
                                       "split sizes)")}
-                   if self.ev else {})}
+                   if sampled else {})}
 
     def close(self):
         self.ctx_own.close()

@@ -228,7 +228,8 @@ for s in "${ST[@]}"; do
            done; done ;;
     r6stages) for r in 1 2; do for st in 1 0; do
                 FCGPU_RESHARD_STAGES=$st step reshard_st${st}_$r 300 python bench.py --flow-reshard --workload c4 --steps 50 --warmup 5 --no-cpu || exit 1
-              done; done ;;
+              done; done &&
+              FCGPU_RESHARD_STAGES=0 FCGPU_RESHARD_HOST=1 step reshard_host 300 python bench.py --flow-reshard --workload c4 --steps 50 --warmup 5 --no-cpu ;;
     r6cache) for r in 1 2; do for nb in 1 2 3 16; do
                step cache_nb${nb}_$r 300 python bench.py --nbuf $nb --steps 200 --warmup 20 --no-cpu || exit 1
                step cache20_nb${nb}_$r 300 python bench.py --nbuf $nb --no-cpu || exit 1

@@ -161,6 +161,7 @@ def test_gpu_bench_flow_reshard(gpus, exchange, slack):
     stalls at its first step and replays every step through the counted
     exchange, with the same checked result."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["FCGPU_RESHARD_STAGES"] = "2"       # stage markers on every 2nd timed step: step 1 of 0..2
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--backend", "gloo",
                         "--flow-reshard", "--workload", "c4", "--packets", "65536", "--steps", "3", "--warmup", "1",
                         "--nbuf", "2", "--no-cpu", "--reshard-exchange", exchange, "--reshard-slack", str(slack)],
@@ -171,6 +172,7 @@ def test_gpu_bench_flow_reshard(gpus, exchange, slack):
     assert fr["checked"] and fr["flow_table_flows"] == fr["distinct_5tuples"] == 65536 * gpus
     assert fr["packets_received"] == fr["packets_sent"] == 65536 * gpus * 3
     assert set(fr["stage_ms_per_step"]) == {"owner_pass", "build", "exchange", "unpack", "flow_pass"}
+    assert fr["stage_sampled_steps"] == 1
     assert fr["exchange"] == exchange
     if exchange == "fixed":
         assert fr["fallback_steps"] == (3 if slack < 1 else 0)
