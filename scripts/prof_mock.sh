@@ -4,6 +4,7 @@
 set -e
 cd "$(dirname "$0")/.."
 T=${1:-1}
+export MOCK_ZEROCOPY=${MOCK_ZEROCOPY:-1}     # the batch size the element runs at on the shared queue (BATCH auto)
 D=${TMPDIR:-/tmp}/prof_mock
 mkdir -p $D gpurun_out
 sed 's/    run("Pass", &floor, err);/    if (getenv("FLOOR")) run("Pass", \&floor, err);/' scripts/mock_element_bench.cc > $D/eb.cc
