@@ -226,6 +226,9 @@ for s in "${ST[@]}"; do
              ns=${c%%:*}; hq=${c##*:}
              FCGPU_AGG_STREAMS=$ns GPU_MAX_HW_QUEUES=$hq step hwq_s${ns}_q${hq}_$r 120 python scripts/element_threads.py 16 || exit 1
            done; done ;;
+    r6cbatch) for r in 1 2; do for t in 1 2 3; do for b in 16384 8192 4096; do
+                step cb_t${t}_b${b}_$r 120 python scripts/element_threads.py $t $b false || exit 1
+              done; done; done ;;
     r6stages) for r in 1 2; do for st in 1 0; do
                 FCGPU_RESHARD_STAGES=$st step reshard_st${st}_$r 300 python bench.py --flow-reshard --workload c4 --steps 50 --warmup 5 --no-cpu || exit 1
               done; done &&
