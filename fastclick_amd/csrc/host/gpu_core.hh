@@ -493,6 +493,7 @@ class RxCore {
     template <class Emit>
     void push_list(Packet *p, Emit &&emit) {
         while (p) {
+            if (_plan.compact && (p = stage_compact_run(p)) == nullptr) break;
             Packet *nx = P::next(p);
             stage(p, emit);
             p = nx;
@@ -793,6 +794,44 @@ class RxCore {
         if (s->n == _cap || (_batch && s->n >= _eff_batch)) submit(emit);
     }
 
+    // stage()'s compact-record case over a run of a list, with the plan and
+    // the slot's state in locals (stage() reloads them per packet: its
+    // descriptor stores may alias them). Stages packets while the open slot
+    // takes them as they are -- DESC32 words, room in the block, below the
+    // batch size -- and returns the first packet it leaves to stage() (a slot
+    // to open or submit, a descriptor DESC32 cannot carry), nullptr at the
+    // list's end. Same records and descriptors as stage().
+    Packet *stage_compact_run(Packet *p) {
+        Slot &s = _slot[_cur];
+        if (!s.n || !s.desc32) return p;
+        const fcgpu::StagePlan plan = _plan;
+        const uint32_t off = (uint32_t)_cfg.offset;
+        const size_t lead = _lead, room = s.in_cap - s.frames_off - lead;
+        // stage() submits once n reaches _cap, or _eff_batch under BATCH: the
+        // packet that reaches it goes through stage()
+        const uint32_t limit = _batch && _eff_batch < _cap ? _eff_batch : _cap;
+        uint8_t *const span = s.span + lead;
+        uint32_t *const desc = s.desc;
+        Packet **const pkts = s.pkts.data();
+        uint32_t n = s.n;
+        size_t used = s.used;
+        while (p && n + 1 < limit) {
+            const uint32_t len = P::length(p);
+            const uint8_t *src = P::data(p);
+            uint32_t so, cp;
+            const size_t rec = fcgpu::stage_record_size(plan, off, src, len, so, cp);
+            if (used + rec > room || len > 0xffffu || lead + used + rec > kDesc32Reach) break;
+            copy_head(span + used, src + so, cp);
+            desc[n] = (uint32_t)((lead + used - plan.start) >> 3) | (len << 16);
+            pkts[n++] = p;
+            used += rec;
+            p = P::next(p);
+        }
+        s.n = n;
+        s.used = used;
+        return p;
+    }
+
     // The current slot goes to the device (asynchronous); the next slot is
     // made free, completing the batch in it first if it is still in flight.
     template <class Emit>
@@ -923,46 +962,57 @@ class RxCore {
         constexpr uint32_t kAhead = 16;
         const bool hashing = _cfg.hash_mode != FCGPU_HASH_NONE;
         const bool autom = _cfg.check_mode == FCGPU_CHECK_AUTO;
-        for (uint32_t i = b; i < e && i < b + kAhead; ++i) prefetch_packet(s.pkts[i]);
+        // loop invariants in locals: the annotation stores below may alias
+        // any member of a matching type, so the compiler reloads members
+        const int color = _color;
+        const bool strip = _strip;
+        const int flow_anno = _flow_anno;
+        const uint32_t offset = (uint32_t)_cfg.offset, n = s.n;
+        const fcgpu_anno8 *const anno8 = s.anno8;
+        const fcgpu_anno *const anno = s.anno;
+        const uint16_t *const verdict = s.verdict;
+        const uint32_t *const hash = s.hash, *const flowid = s.flowid, *const iprw = s.iprw;
+        Packet **const pkts = s.pkts.data();
+        for (uint32_t i = b; i < e && i < b + kAhead; ++i) prefetch_packet(pkts[i]);
         for (uint32_t i = b; i < e; ++i) {
-            Packet *p = s.pkts[i];
-            if (i + kAhead < s.n) prefetch_packet(s.pkts[i + kAhead]);
+            Packet *p = pkts[i];
+            if (i + kAhead < n) prefetch_packet(pkts[i + kAhead]);
             fcgpu_anno a8v;
-            if (s.anno8) {                                // IPv4 chain: the 8-B form
-                const fcgpu_anno8 &q = s.anno8[i];
+            if (anno8) {                                  // IPv4 chain: the 8-B form
+                const fcgpu_anno8 &q = anno8[i];
                 a8v = fcgpu_anno{q.dst_ip, q.length, 0, q.nh, (uint16_t)(q.nh + q.thl), 0, 4, 0};
             }
-            const fcgpu_anno &a = s.anno8 ? a8v : s.anno[i];
-            const uint32_t reason = s.verdict[i] & 0xff;
-            if (_color >= 0) P::set_anno_u8(p, P::kPaint, (uint8_t)_color);     // SET_PAINT_ANNO
+            const fcgpu_anno &a = anno8 ? a8v : anno[i];
+            const uint32_t reason = verdict[i] & 0xff;
+            if (color >= 0) P::set_anno_u8(p, P::kPaint, (uint8_t)color);       // SET_PAINT_ANNO
             if (autom && reason != FCGPU_R_VLAN_REJECT)
                 P::set_anno_u16(p, P::kVlanTci, a.vlan_tci);                     // StripEtherVLANHeader
             if (reason == FCGPU_R_OK || reason >= FCGPU_R_NO_MATCH) {
                 // DecIPTTL / SetIPChecksum: ip_rw holds every R_OK packet's bytes
                 // 8..11 as they leave; only a changed word is written back
-                if (s.iprw && reason == FCGPU_R_OK && memcmp(P::data(p) + a.nh + 8u, &s.iprw[i], 4) != 0) {
-                    Packet *q = P::write_bytes(p, a.nh + 8u, &s.iprw[i], 4);
+                if (iprw && reason == FCGPU_R_OK && memcmp(P::data(p) + a.nh + 8u, &iprw[i], 4) != 0) {
+                    Packet *q = P::write_bytes(p, a.nh + 8u, &iprw[i], 4);
                     if (!q) {                                                    // uniqueify failed: freed
-                        s.pkts[i] = nullptr;
+                        pkts[i] = nullptr;
                         s.holes = true;
                         continue;
                     }
-                    s.pkts[i] = p = q;
+                    pkts[i] = p = q;
                 }
                 P::set_headers(p, a.nh, a.th);                                   // set_ip_header / set_ip6_header
                 if (a.length < P::length(p)) P::take(p, P::length(p) - a.length);
                 if (a.ipver == 6) P::set_anno_u8(p, P::kIp6Nxt, a.ip6_nxt);
                 else P::set_anno_u32(p, P::kDstIp, a.dst_ip);
                 if (hashing && reason <= FCGPU_R_NO_MATCH)                       // AggregateHash (not after an L4 drop)
-                    P::set_anno_u32(p, P::kAggregate, s.hash[i]);
-                if (s.flowid && s.flowid[i] != FCGPU_FLOW_NONE && s.flowid[i] != FCGPU_FLOW_FULL)
-                    P::set_anno_u32(p, _flow_anno, s.flowid[i]);
-                if (_strip) P::pull(p, a.nh);
+                    P::set_anno_u32(p, P::kAggregate, hash[i]);
+                if (flowid && flowid[i] != FCGPU_FLOW_NONE && flowid[i] != FCGPU_FLOW_FULL)
+                    P::set_anno_u32(p, flow_anno, flowid[i]);
+                if (strip) P::pull(p, a.nh);
                 if (reason > FCGPU_R_NO_MATCH) drop_chatter(reason);
             } else {
                 drop_chatter(reason);
                 // the replaced Strip / StripEtherVLANHeader ran before the checker
-                if (_strip && reason != FCGPU_R_VLAN_REJECT) P::pull(p, autom ? a.nh : (uint32_t)_cfg.offset);
+                if (strip && reason != FCGPU_R_VLAN_REJECT) P::pull(p, autom ? a.nh : offset);
             }
         }
     }

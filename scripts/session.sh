@@ -226,6 +226,11 @@ for s in "${ST[@]}"; do
              ns=${c%%:*}; hq=${c##*:}
              FCGPU_AGG_STREAMS=$ns GPU_MAX_HW_QUEUES=$hq step hwq_s${ns}_q${hq}_$r 120 python scripts/element_threads.py 16 || exit 1
            done; done ;;
+    r6elab) for r in 1 2 3; do
+              FCCLICK_LIB=fastclick_amd/lib/ab/libfcclick_old.so step el_old_$r 300 python scripts/crossover.py --chains base,udp --threads 8,16 --no-cpu || exit 1
+              step el_new_$r 300 python scripts/crossover.py --chains base,udp --threads 8,16 --no-cpu || exit 1
+            done &&
+            for r in 1 2; do step el_cpu_$r 300 python scripts/crossover.py --chains base,udp --threads 16 --no-gpu || exit 1; done ;;
     r6cbatch) for r in 1 2; do for t in 1 2 3; do for b in 16384 8192 4096; do
                 step cb_t${t}_b${b}_$r 120 python scripts/element_threads.py $t $b false || exit 1
               done; done; done ;;
