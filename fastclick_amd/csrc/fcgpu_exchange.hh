@@ -510,32 +510,45 @@ __device__ __forceinline__ void xtile_sort(const XBuild &B, uint32_t t, XTileLds
 
 // Per owner the tile's packets and slot bytes are sums, which the order the
 // build sorts in does not change: LDS atomics and one barrier, no sort
-// (the sort's five barriers per tile made this pass latency-bound).
+// (the sort's five barriers per tile made this pass latency-bound), and
+// kXbTiles tiles per workgroup, their loads issued together (one tile per
+// workgroup was bound by the workgroup dispatch rate, as k_part_multi was).
+constexpr uint32_t kXbTiles = 4;
 __global__ __launch_bounds__(kXTile) void k_xbtile(XBuild B) {
-    __shared__ uint32_t s_c[FCGPU_MAX_PORTS], s_b[FCGPU_MAX_PORTS];
-    const uint32_t t = blockIdx.x, i = t * kXTile + threadIdx.x;
-    if (threadIdx.x < B.world) {
-        s_c[threadIdx.x] = 0;
-        s_b[threadIdx.x] = 0;
+    __shared__ uint32_t s_c[kXbTiles][FCGPU_MAX_PORTS], s_b[kXbTiles][FCGPU_MAX_PORTS];
+    const uint32_t t0 = blockIdx.x * kXbTiles;
+    for (uint32_t k = threadIdx.x; k < kXbTiles * FCGPU_MAX_PORTS; k += kXTile) {
+        (&s_c[0][0])[k] = 0;
+        (&s_b[0][0])[k] = 0;
     }
-    uint32_t own = B.world, slot = 0;
-    if (i < B.n) {
-        const uint32_t d = (uint32_t)B.verdict[i] >> 8;
-        if (d < B.world) {
-            own = d;
-            slot = (uint32_t)xslot(B.desc[2 * (size_t)i + 1]);
+    uint32_t own[kXbTiles], slot[kXbTiles];
+#pragma unroll
+    for (uint32_t k = 0; k < kXbTiles; ++k) {
+        const uint32_t i = (t0 + k) * kXTile + threadIdx.x;
+        own[k] = B.world;
+        slot[k] = 0;
+        if (i < B.n) {
+            const uint32_t d = (uint32_t)B.verdict[i] >> 8;
+            if (d < B.world) {
+                own[k] = d;
+                slot[k] = (uint32_t)xslot(B.desc[2 * (size_t)i + 1]);
+            }
         }
     }
     __syncthreads();
-    if (own < B.world) {
-        atomicAdd(&s_c[own], 1u);
-        atomicAdd(&s_b[own], slot);
-    }
+#pragma unroll
+    for (uint32_t k = 0; k < kXbTiles; ++k)
+        if (own[k] < B.world) {
+            atomicAdd(&s_c[k][own[k]], 1u);
+            atomicAdd(&s_b[k][own[k]], slot[k]);
+        }
     __syncthreads();
-    const uint32_t d = threadIdx.x;
-    if (d < B.world) {
-        B.tcnt[(size_t)d * B.ntiles + t] = s_c[d];
-        B.tbyt[(size_t)d * B.ntiles + t] = s_b[d];
+    for (uint32_t q = threadIdx.x; q < kXbTiles * B.world; q += kXTile) {
+        const uint32_t k = q / B.world, d = q - k * B.world, t = t0 + k;
+        if (t < B.ntiles) {
+            B.tcnt[(size_t)d * B.ntiles + t] = s_c[k][d];
+            B.tbyt[(size_t)d * B.ntiles + t] = s_b[k][d];
+        }
     }
 }
 
@@ -547,13 +560,29 @@ __global__ __launch_bounds__(1024) void k_xbscan(XBuild B) {
     uint32_t *cnt = B.tcnt + (size_t)d * B.ntiles;
     unsigned long long *byt = B.tbyt + (size_t)d * B.ntiles;
     const uint32_t per = (B.ntiles + 1023) / 1024, beg = threadIdx.x * per;
+    // up to kScanRegs tiles a thread (a 1M batch: 4) stay in registers between
+    // the sum and the offsets: one round trip to memory, not two
+    constexpr uint32_t kScanRegs = 8;
+    uint32_t rc[kScanRegs];
+    uint64_t rb[kScanRegs];
     uint32_t cs = 0;
     uint64_t bs = 0;
-    for (uint32_t k = 0; k < per; ++k)
-        if (beg + k < B.ntiles) {
-            cs += cnt[beg + k];
-            bs += byt[beg + k];
+    if (per <= kScanRegs) {
+#pragma unroll
+        for (uint32_t k = 0; k < kScanRegs; ++k) {
+            const bool in = k < per && beg + k < B.ntiles;
+            rc[k] = in ? cnt[beg + k] : 0u;
+            rb[k] = in ? byt[beg + k] : 0ull;
+            cs += rc[k];
+            bs += rb[k];
         }
+    } else {
+        for (uint32_t k = 0; k < per; ++k)
+            if (beg + k < B.ntiles) {
+                cs += cnt[beg + k];
+                bs += byt[beg + k];
+            }
+    }
     uint32_t ci = cs;
     uint64_t bi = bs;
 #pragma unroll
@@ -582,15 +611,26 @@ __global__ __launch_bounds__(1024) void k_xbscan(XBuild B) {
     }
     uint32_t cr = cp + ci - cs;
     uint64_t br = bp + bi - bs;
-    for (uint32_t k = 0; k < per; ++k)
-        if (beg + k < B.ntiles) {
-            const uint32_t c = cnt[beg + k];
-            const uint64_t b = byt[beg + k];
-            cnt[beg + k] = cr;
-            byt[beg + k] = br;
-            cr += c;
-            br += b;
-        }
+    if (per <= kScanRegs) {
+#pragma unroll
+        for (uint32_t k = 0; k < kScanRegs; ++k)
+            if (k < per && beg + k < B.ntiles) {
+                cnt[beg + k] = cr;
+                byt[beg + k] = br;
+                cr += rc[k];
+                br += rb[k];
+            }
+    } else {
+        for (uint32_t k = 0; k < per; ++k)
+            if (beg + k < B.ntiles) {
+                const uint32_t c = cnt[beg + k];
+                const uint64_t b = byt[beg + k];
+                cnt[beg + k] = cr;
+                byt[beg + k] = br;
+                cr += c;
+                br += b;
+            }
+    }
     if (threadIdx.x == 0) {
         B.seg_n[d] = ct;
         B.seg_bytes[d] = bt;

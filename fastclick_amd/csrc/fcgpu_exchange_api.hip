@@ -102,7 +102,7 @@ static int xbuild_launch(fcgpu_ctx *c, XBuild &B, hipStream_t s) {
     B.ntiles = (B.n + kXTile - 1) / kXTile;
     B.tcnt = c->x_tcnt;
     B.tbyt = c->x_tbyt;
-    if (B.ntiles) hipLaunchKernelGGL(k_xbtile, dim3(B.ntiles), dim3(kXTile), 0, s, B);
+    if (B.ntiles) hipLaunchKernelGGL(k_xbtile, dim3((B.ntiles + kXbTiles - 1) / kXbTiles), dim3(kXTile), 0, s, B);
     hipLaunchKernelGGL(k_xbscan, dim3(B.world), dim3(1024), 0, s, B);    // n = 0: zero counts
     if (B.ntiles) hipLaunchKernelGGL(k_xbuild, dim3(B.ntiles), dim3(kXTile), 0, s, B);   // lanes per frame: per tile
     HIPCHK(c, hipGetLastError());

@@ -493,7 +493,7 @@ class RxCore {
     template <class Emit>
     void push_list(Packet *p, Emit &&emit) {
         while (p) {
-            if (_plan.compact && (p = stage_compact_run(p)) == nullptr) break;
+            if ((p = stage_run(p)) == nullptr) break;
             Packet *nx = P::next(p);
             stage(p, emit);
             p = nx;
@@ -794,14 +794,15 @@ class RxCore {
         if (s->n == _cap || (_batch && s->n >= _eff_batch)) submit(emit);
     }
 
-    // stage()'s compact-record case over a run of a list, with the plan and
-    // the slot's state in locals (stage() reloads them per packet: its
-    // descriptor stores may alias them). Stages packets while the open slot
-    // takes them as they are -- DESC32 words, room in the block, below the
-    // batch size -- and returns the first packet it leaves to stage() (a slot
-    // to open or submit, a descriptor DESC32 cannot carry), nullptr at the
-    // list's end. Same records and descriptors as stage().
-    Packet *stage_compact_run(Packet *p) {
+    // stage() over a run of a list, with the plan and the slot's state in
+    // locals (stage() reloads them per packet: its descriptor stores may alias
+    // them). Stages packets while the open slot takes them as they are --
+    // room in the block, below the batch size, and with compact records
+    // DESC32 words -- and returns the first packet it leaves to stage() (a
+    // slot to open or submit, a descriptor DESC32 cannot carry), nullptr at
+    // the list's end. Same records and descriptors as stage().
+    Packet *stage_run(Packet *p) {
+        if (!_plan.compact) return stage_capture_run(p);
         Slot &s = _slot[_cur];
         if (!s.n || !s.desc32) return p;
         const fcgpu::StagePlan plan = _plan;
@@ -823,6 +824,35 @@ class RxCore {
             if (used + rec > room || len > 0xffffu || lead + used + rec > kDesc32Reach) break;
             copy_head(span + used, src + so, cp);
             desc[n] = (uint32_t)((lead + used - plan.start) >> 3) | (len << 16);
+            pkts[n++] = p;
+            used += rec;
+            p = P::next(p);
+        }
+        s.n = n;
+        s.used = used;
+        return p;
+    }
+    // The same for whole captures (the first min(len, capture) bytes of every
+    // frame in 64-B aligned records, (offset, length) descriptors).
+    Packet *stage_capture_run(Packet *p) {
+        Slot &s = _slot[_cur];
+        if (!s.n || s.desc32) return p;
+        const uint32_t capture = _capture;
+        const size_t lead = _lead, room = s.in_cap - s.frames_off - lead;
+        const uint32_t limit = _batch && _eff_batch < _cap ? _eff_batch : _cap;
+        uint8_t *const span = s.span + lead;
+        uint32_t *const desc = s.desc;
+        Packet **const pkts = s.pkts.data();
+        uint32_t n = s.n;
+        size_t used = s.used;
+        while (p && n + 1 < limit) {
+            const uint32_t len = P::length(p);
+            const uint32_t cp = len < capture ? len : capture;
+            const size_t rec = cp ? ((size_t)cp + 63) & ~(size_t)63 : 64;
+            if (used + rec > room) break;
+            copy_head(span + used, P::data(p), cp);
+            desc[2 * n] = (uint32_t)(lead + used);
+            desc[2 * n + 1] = len;
             pkts[n++] = p;
             used += rec;
             p = P::next(p);

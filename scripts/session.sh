@@ -226,6 +226,10 @@ for s in "${ST[@]}"; do
              ns=${c%%:*}; hq=${c##*:}
              FCGPU_AGG_STREAMS=$ns GPU_MAX_HW_QUEUES=$hq step hwq_s${ns}_q${hq}_$r 120 python scripts/element_threads.py 16 || exit 1
            done; done ;;
+    r6prog) for r in 1 2 3; do
+              FCCLICK_LIB=fastclick_amd/lib/ab/libfcclick_prev.so step pg_prev_$r 300 python scripts/crossover.py --chains prog16 --threads 8,16 --no-cpu || exit 1
+              step pg_new_$r 300 python scripts/crossover.py --chains prog16 --threads 8,16 --no-cpu || exit 1
+            done ;;
     r6fbatch) for r in 1 2; do
                 step fb_flow_$r 300 python scripts/element_batch_sweep.py flow20k 16 auto,4096,16384,32768,65536 || exit 1
                 step fb_base_$r 300 python scripts/element_batch_sweep.py base 16 auto,4096,16384 || exit 1
