@@ -510,10 +510,11 @@ __device__ __forceinline__ void xtile_sort(const XBuild &B, uint32_t t, XTileLds
 
 // Per owner the tile's packets and slot bytes are sums, which the order the
 // build sorts in does not change: LDS atomics and one barrier, no sort
-// (the sort's five barriers per tile made this pass latency-bound), and
-// kXbTiles tiles per workgroup, their loads issued together (one tile per
-// workgroup was bound by the workgroup dispatch rate, as k_part_multi was).
-constexpr uint32_t kXbTiles = 4;
+// (the sort's five barriers per tile made this pass latency-bound). kXbTiles
+// tiles per workgroup: four, their loads issued together, measured slower
+// than one (6.4 against 5.3 us for 1M packets, profiles/r06_exchange/
+// xbscan_regs: a quarter of the workgroups hides less latency).
+constexpr uint32_t kXbTiles = 1;
 __global__ __launch_bounds__(kXTile) void k_xbtile(XBuild B) {
     __shared__ uint32_t s_c[kXbTiles][FCGPU_MAX_PORTS], s_b[kXbTiles][FCGPU_MAX_PORTS];
     const uint32_t t0 = blockIdx.x * kXbTiles;
