@@ -2,7 +2,9 @@
 // host-side ceiling with scripts/mock_fcgpu.cc standing in for the GPU.
 // A 64K-packet C2-shaped trace (60-B frames in 64-B slots) through
 // GPUIPCheckClassify behind a BURST-32 source, as scripts/element_threads.py
-// does on the GPU box.  Usage: element_bench THREADS [BATCH] [REPS]
+// does on the GPU box.  Usage: element_bench THREADS [BATCH] [REPS] [CONF]
+// (CONF: another GPUIPCheckClassify configuration; tests/test_host_sanitizers.py
+// runs the element's data path under ASan/UBSan this way).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -29,7 +31,8 @@ int main(int argc, char **argv) {
         desc[2 * i] = i * 64;
         desc[2 * i + 1] = 60;
     }
-    std::string conf = "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BATCH " + batch + ")";
+    std::string conf = argc > 4 ? std::string(argv[4])
+                                : "GPUIPCheckClassify(OFFSET 14, CHECKSUM true, N 16, LB_MODE hash, BATCH " + batch + ")";
     auto run = [&](const char *c, double *pps, char *err) {
         return reps ? fcclick_bench_threads(c, arena.data(), desc.data(), n, 32, reps, threads, pps, err, 512)
                     : fcclick_bench_timed(c, arena.data(), desc.data(), n, 32, 2.0, threads, pps, err, 512);

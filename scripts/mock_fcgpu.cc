@@ -95,14 +95,17 @@ int fcgpu_span_submit_block(fcgpu_ctx *c, uint32_t, const void *h_in, size_t, si
     // the element never writes its result blocks: a block that already holds
     // the fixed result for n packets is left as is, so the mock costs the
     // calling thread nothing per packet in steady state
-    for (int k = 0; k < 4; ++k)
-        if (c->filled[k] == h_out && c->filled_n[k] == n) return FCGPU_OK;
-    for (int k = 0; k < 4; ++k)
-        if (!c->filled[k] || k == 3) {
-            c->filled[k] = h_out;
-            c->filled_n[k] = n;
-            break;
-        }
+    // one entry per block: a block refilled for another n is re-keyed (a
+    // stale entry for the old n would skip a later refill)
+    int slot = -1;
+    for (int k = 0; k < 4 && slot < 0; ++k)
+        if (c->filled[k] == h_out) slot = k;
+    if (slot >= 0 && c->filled_n[slot] == n) return FCGPU_OK;
+    for (int k = 0; k < 4 && slot < 0; ++k)
+        if (!c->filled[k]) slot = k;
+    if (slot < 0) slot = 3;
+    c->filled[slot] = h_out;
+    c->filled_n[slot] = n;
     fcgpu_block_layout L;
     fcgpu_block_layout_for(c, n, outputs, partition, &L);
     uint8_t *o = static_cast<uint8_t *>(h_out);
