@@ -71,6 +71,7 @@ struct AggQueue {
     std::vector<AggItem> pending;
     hipStream_t st[kAggStreamsMax] = {};   // created by agg_issue (st_mu), never under mu
     uint32_t nst = kAggStreams;
+    uint32_t take_at = 4;     // pending submissions that trigger a launch (kAggLaunch, FCGPU_AGG_LAUNCH)
     std::mutex st_mu;
     uint32_t rr = 0;
     std::vector<AggLaunch *> spare;
@@ -78,7 +79,7 @@ struct AggQueue {
     // here (agg_finish); agg_issue wakes them
     std::condition_variable cv;
 };
-constexpr uint32_t kAggLaunch = 4;
+constexpr uint32_t kAggLaunch = 4;    // default of AggQueue::take_at
 static std::mutex g_agg_mu;
 static std::map<int, AggQueue *> g_agg;
 static AggQueue &agg_queue(fcgpu_ctx *c) {
@@ -91,6 +92,11 @@ static AggQueue &agg_queue(fcgpu_ctx *c) {
         if (const char *e = getenv("FCGPU_AGG_STREAMS")) {
             const int v = atoi(e);
             if (v >= 1 && v <= (int)kAggStreamsMax) q->nst = (uint32_t)v;
+        }
+        q->take_at = kAggLaunch;
+        if (const char *e = getenv("FCGPU_AGG_LAUNCH")) {     // same-box A/B
+            const int v = atoi(e);
+            if (v >= 1 && v <= (int)kMaxFuse) q->take_at = (uint32_t)v;
         }
     }
     c->aq = q;
@@ -327,7 +333,7 @@ static int agg_submit(fcgpu_ctx *c, uint32_t slot, const fcgpu_job &j, uint32_t 
         sp.agg = true;
         sp.al = nullptr;
         sp.busy = true;
-        if (q.pending.size() >= kAggLaunch) agg_take_locked(q, iss);
+        if (q.pending.size() >= q.take_at) agg_take_locked(q, iss);
     }
     agg_issue(q, iss);
     return FCGPU_OK;

@@ -226,6 +226,9 @@ for s in "${ST[@]}"; do
              ns=${c%%:*}; hq=${c##*:}
              FCGPU_AGG_STREAMS=$ns GPU_MAX_HW_QUEUES=$hq step hwq_s${ns}_q${hq}_$r 120 python scripts/element_threads.py 16 || exit 1
            done; done ;;
+    r6agg) for r in 1 2 3; do for a in 4 8 2; do
+             FCGPU_AGG_LAUNCH=$a step agg${a}_$r 300 python scripts/crossover.py --chains base,udp --threads 16 --no-cpu || exit 1
+           done; done ;;
     r6prog) for r in 1 2 3; do
               FCCLICK_LIB=fastclick_amd/lib/ab/libfcclick_prev.so step pg_prev_$r 300 python scripts/crossover.py --chains prog16 --threads 8,16 --no-cpu || exit 1
               step pg_new_$r 300 python scripts/crossover.py --chains prog16 --threads 8,16 --no-cpu || exit 1
