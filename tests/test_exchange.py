@@ -427,3 +427,26 @@ def test_exchange_rejects_bad_arguments():
     arr = (N.C.c_uint64 * 1)()
     assert lib.fcgpu_exchange_unpack(None, None, 0, arr, 1, None, None) == N.EINVAL
     assert lib.fcgpu_exchange_build(None, None, None, None, 0, 1, 0, None, None, None, None, 0, None) == N.EINVAL
+
+
+@pytest.mark.gpu
+def test_gpu_exchange_build_sequence_one_context():
+    """Builds one after another on one context, worlds of 1 to 64 owners,
+    empty to 1M-packet batches: every build equals the restatement -- no
+    per-tile counts or scans carried over from the build before."""
+    ctx = N.Context(0, 1 << 20)
+    try:
+        for k, (world, n) in enumerate([(4, 3000), (4, 3000), (32, 5000), (8, 70000), (4, 0), (16, 20000),
+                                        (1, 257), (2, 1 << 20), (64, 4000), (3, 9999)]):
+            arena, desc = _ragged(n, 300 + k, max_len=64 if n > 100_000 else 1600)
+            owner = np.random.default_rng(400 + k).integers(-1, world, n)
+            perm, ps = X.partition(owner, world)
+            send, meta, seg_n, seg_b = _build_gpu(ctx, arena, desc, owner, world, rank=k % max(world, 1))
+            emeta, eseg = X.plan(desc, perm, ps, world, k % max(world, 1))
+            assert np.array_equal(seg_b, eseg), (k, world, n)
+            assert seg_n.tolist() == [int(ps[d + 1] - ps[d]) for d in range(world)], (k, world, n)
+            assert np.array_equal(meta, emeta), (k, world, n)
+            total = int(eseg.sum())
+            assert np.array_equal(send[:total], X.pack(arena, desc, emeta, ps, eseg, world)), (k, world, n)
+    finally:
+        ctx.close()
